@@ -1,0 +1,164 @@
+/*
+ * sehip — MI355X-native complex-spectral enhancement ops (C ABI).
+ *
+ * This is the drop-in boundary for the hot path of shs2783/Speech-Enhancement
+ * (SURVEY.md §8a/§8b). The reference has no FFI of its own: its "plugin API"
+ * is the nn.Module surface of models/conv_stft.py and
+ * models/modules/complex_nn.py. Each entry point below replaces the ATen
+ * calls made at the cited reference line(s); the Python host package
+ * (speech-enhancement_amd/sehip) mirrors the reference modules on top of it.
+ *
+ * Conventions
+ *   - Plain pointers to device memory (fp32, contiguous NCHW / [B, F, T]).
+ *   - Complex tensors are channel-stacked: channels [0, C/2) are the real
+ *     parts, [C/2, C) the imaginary parts (complex_nn.py:18-42).
+ *   - `stream` is a hipStream_t (the caller's current stream). Nothing here
+ *     synchronises the device; all launches are asynchronous on `stream`.
+ *   - The library allocates nothing. Scratch is passed in (`ws`, `ws_bytes`);
+ *     query the size with the matching *_workspace_size function.
+ *   - Return value: SE_OK (0) or a negative SE_E_* code; se_strerror() names it.
+ */
+#ifndef SEHIP_H
+#define SEHIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SEHIP_ABI_VERSION 1
+
+enum {
+  SE_OK = 0,
+  SE_E_ARG = -1,          /* null pointer / negative size / bad flag          */
+  SE_E_SHAPE = -2,        /* inconsistent shapes (e.g. reflect pad > length)  */
+  SE_E_UNSUPPORTED = -3,  /* valid but not implemented (e.g. nfft radix)      */
+  SE_E_LAUNCH = -4,       /* hipGetLastError() after a launch                 */
+  SE_E_WORKSPACE = -5     /* ws_bytes smaller than *_workspace_size()         */
+};
+
+int se_abi_version(void);
+const char* se_strerror(int code);
+
+/* Loader self-test: out[i] = 3*i + 1 for i < n (one tiny kernel). */
+int se_probe(int* out, int n, void* stream);
+
+/* ------------------------------------------------------------------------
+ * ConvSTFT / ConviSTFT (models/conv_stft.py:7-116)
+ *
+ * Both are computed as packed real FFTs in LDS (two frames per complex FFT
+ * of length nfft), NOT as the reference's DFT-basis conv1d; the results are
+ * the same linear maps (conv_stft.py:7-26 builds the basis from rfft(eye(N))
+ * and its pinv). nfft must factor into 2,3,4,5 and be <= 1024; win <= nfft.
+ *
+ * window : fp32 [win]  periodic Hann (scipy get_window(win_type, win)).
+ * twiddle: fp32 [2*nfft] interleaved (cos(2*pi*k/nfft), -sin(2*pi*k/nfft)).
+ * ------------------------------------------------------------------------ */
+
+/* Number of frames produced for a length-L signal (conv_stft.py:54-56). */
+int se_stft_num_frames(int L, int win, int hop, int nfft, int center);
+
+/* ConvSTFT.forward (conv_stft.py:48-66).
+ * x: [B, L]. center=1 reflect-pads nfft/2 on both sides (requires L > nfft/2).
+ * mag_phase=0: out0 = spec [B, nfft+2, T] (rows 0..nfft/2 real, rest imag).
+ * mag_phase=1: out0 = mags [B, nfft/2+1, T], out1 = phase (atan2(im, re)). */
+int se_stft_fwd(const float* x, float* out0, float* out1, int B, int L, int win,
+                int hop, int nfft, int center, int mag_phase,
+                const float* window, const float* twiddle, void* stream);
+
+/* ConviSTFT.forward (conv_stft.py:89-116) for a complex spec [B, nfft+2, T]:
+ * overlap-add of the pinv-basis frames divided by (OLA(window^2) + 1e-8),
+ * out[b, s] = full[b, s + offset] for 0 <= s < out_len. */
+int se_istft_fwd(const float* spec, float* out, int B, int T, int win, int hop,
+                 int nfft, int offset, int out_len, const float* window,
+                 const float* twiddle, void* stream);
+
+/* Adjoint of se_istft_fwd: gspec = d(out)/d(spec)^T gout. */
+int se_istft_bwd(const float* gout, float* gspec, int B, int T, int win,
+                 int hop, int nfft, int offset, int out_len,
+                 const float* window, const float* twiddle, void* stream);
+
+/* ------------------------------------------------------------------------
+ * Complex (transposed) 2-D convolution as ONE fused implicit GEMM
+ * (complex_nn.py:52-91). The four real convs of the reference
+ *   re = Wr*xr - Wi*xi ,  im = Wi*xr + Wr*xi
+ * become a single contraction against the block weight
+ *   conv : [[Wr, -Wi], [Wi, Wr]]  in (Cout, Cin) layout
+ *   convT: [[Wr,  Wi], [-Wi, Wr]] in (Cin, Cout) layout
+ * assembled in the workspace from the two nn.Conv2d / nn.ConvTranspose2d
+ * weight tensors (real_conv.weight, imag_conv.weight). Transposed convs are
+ * split into stride-phase classes so no MFMA work is spent on inserted zeros.
+ * Arithmetic: fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32.
+ * ------------------------------------------------------------------------ */
+typedef struct se_conv2d_desc {
+  int batch;
+  int in_channels;    /* real channel count (2 x complex channels)          */
+  int in_h, in_w;
+  int out_channels;   /* real channel count (2 x complex channels)          */
+  int kernel_h, kernel_w;
+  int stride_h, stride_w;
+  int pad_h, pad_w;
+  int dil_h, dil_w;
+  int out_pad_h, out_pad_w; /* ConvTranspose2d output_padding              */
+  int transposed;     /* 0: ComplexConv2d, 1: ComplexConvTranspose2d         */
+  int complex_weights;/* 1: (wr, wi) pair; 0: plain real conv, weight in wr  */
+} se_conv2d_desc;
+
+/* Output spatial size (nn.Conv2d / nn.ConvTranspose2d formulas). */
+int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w);
+
+/* Workspace bytes needed by each of the calls below for this descriptor. */
+size_t se_conv2d_workspace_size(const se_conv2d_desc* d);
+
+/* y = conv(x) (+ bias). x: [B, Cin, Hi, Wi]; y: [B, Cout, Ho, Wo].
+ * wr, wi: [Cout/2, Cin/2, kh, kw] (conv) or [Cin/2, Cout/2, kh, kw] (convT);
+ * br, bi: [Cout/2] or NULL. Real mode: wr = full weight, br = full bias.   */
+int se_conv2d_fwd(const se_conv2d_desc* d, const float* x, const float* wr,
+                  const float* wi, const float* br, const float* bi, float* y,
+                  void* ws, size_t ws_bytes, void* stream);
+
+/* dx = d(y)/d(x)^T dy. */
+int se_conv2d_bwd_data(const se_conv2d_desc* d, const float* dy,
+                       const float* wr, const float* wi, float* dx, void* ws,
+                       size_t ws_bytes, void* stream);
+
+/* dwr, dwi (same shapes as wr, wi; OVERWRITTEN) and, if non-NULL, dbr, dbi. */
+int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x,
+                         const float* dy, float* dwr, float* dwi, float* dbr,
+                         float* dbi, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
+ * ComplexBatchNorm2d (complex_nn.py:148-329) with optional fused
+ * LeakyReLU / ReLU (frcrn.py:22,34; ccbam.py:12,15).
+ * x, y: [B, C, H, W], C = 2*Cc. Per complex channel: mean (Mr, Mi), biased
+ * covariance (Vrr, Vri, Vii) + eps, U = V^-1/2 by the closed 2x2 form
+ * (complex_nn.py:288-297), Z = W U with symmetric W, y = Z (x - M) + B.
+ *
+ * params: device fp32 [5*Cc] = Wrr | Wri | Wii | Br | Bi   (NULL if !affine)
+ * running: device fp32 [5*Cc] = RMr | RMi | RVrr | RVri | RVii (NULL if !track)
+ * nbt: device int64 [1] num_batches_tracked (NULL if !track)
+ * save: device fp32 [16*Cc] per-channel state for the backward pass.
+ * act: 0 none, 1 LeakyReLU(slope), 2 ReLU.
+ * training: 1 = batch statistics (+ running-stat update when running!=NULL).
+ * momentum < 0 means "None" (cumulative average, complex_nn.py:223-224).
+ * ------------------------------------------------------------------------ */
+size_t se_cbn_workspace_size(int B, int C, int HW);
+
+int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
+               const float* params, float* running, int64_t* nbt,
+               float* save, int training, float eps, float momentum, int act,
+               float slope, void* ws, size_t ws_bytes, void* stream);
+
+/* Backward. gy = dL/dy (post-activation), y = forward output, x = input.
+ * dx overwritten; dparams (fp32 [5*Cc], NULL if !affine) overwritten. */
+int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
+               int B, int C, int HW, const float* params, const float* save,
+               float* dparams, int training, int act, float slope, void* ws,
+               size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SEHIP_H */

@@ -1,0 +1,117 @@
+"""ctypes binding of libsehip.so (the C ABI declared in include/sehip.h).
+
+The product path has no fallback: if the HIP library is missing or a call
+returns an error, a RuntimeError is raised. torch is imported first so that
+the process-wide HIP runtime (torch's bundled libamdhip64.so.7) is the one
+libsehip.so binds to — device pointers and hipStream_t handles taken from
+torch are then valid inside the library.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import re
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsehip.so")
+HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "sehip.h"))
+
+c_int = ctypes.c_int
+c_float = ctypes.c_float
+c_size_t = ctypes.c_size_t
+c_void_p = ctypes.c_void_p
+c_char_p = ctypes.c_char_p
+
+
+class ConvDesc(ctypes.Structure):
+    """Mirror of se_conv2d_desc (include/sehip.h)."""
+
+    _fields_ = [(n, c_int) for n in (
+        "batch", "in_channels", "in_h", "in_w", "out_channels",
+        "kernel_h", "kernel_w", "stride_h", "stride_w", "pad_h", "pad_w",
+        "dil_h", "dil_w", "out_pad_h", "out_pad_w", "transposed",
+        "complex_weights")]
+
+
+_P = c_void_p
+_SIGNATURES = {
+    "se_abi_version": (c_int, []),
+    "se_strerror": (c_char_p, [c_int]),
+    "se_probe": (c_int, [_P, c_int, _P]),
+    "se_stft_num_frames": (c_int, [c_int] * 5),
+    "se_stft_fwd": (c_int, [_P, _P, _P] + [c_int] * 7 + [_P, _P, _P]),
+    "se_istft_fwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
+    "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
+    "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
+    "se_conv2d_workspace_size": (c_size_t, [_P]),
+    "se_conv2d_fwd": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
+    "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),
+    "se_conv2d_bwd_weight": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
+    "se_cbn_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, _P,
+                           c_int, c_float, c_float, c_int, c_float, _P,
+                           c_size_t, _P]),
+    "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _P, _P, _P,
+                           c_int, c_int, c_float, _P, c_size_t, _P]),
+}
+
+
+def header_symbols(path: str = HEADER_PATH) -> list[str]:
+    """Every function name declared in include/sehip.h."""
+    with open(path) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"\b(se_[a-z0-9_]+)\s*\(", text)))
+
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    """Load libsehip.so once; raise loudly if it is missing."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"sehip: native library not built ({LIB_PATH}); run "
+                "`python -c 'import __graft_entry__ as g; g.build()'`")
+        handle = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (res, args) in _SIGNATURES.items():
+            f = getattr(handle, name)  # AttributeError = symbol not exported
+            f.restype = res
+            f.argtypes = args
+        _lib = handle
+    return _lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != 0:
+        msg = lib().se_strerror(rc).decode()
+        raise RuntimeError(f"sehip: {what} failed: {msg} (code {rc})")
+
+
+def stream_of(t: torch.Tensor) -> int:
+    """The caller's current HIP stream for tensor t's device."""
+    return torch.cuda.current_stream(t.device).cuda_stream
+
+
+def ptr(t) -> int | None:
+    return None if t is None else t.data_ptr()
+
+
+def require_device(*ts: torch.Tensor) -> None:
+    for t in ts:
+        if t is None:
+            continue
+        if not t.is_cuda:
+            raise RuntimeError("sehip ops run on the GPU only (got a CPU tensor); "
+                               "there is no CPU fallback in the product path")
+        if t.dtype != torch.float32:
+            raise RuntimeError(f"sehip ops take float32 tensors (got {t.dtype})")
+
+
+def probe(n: int = 1000, device: str = "cuda") -> torch.Tensor:
+    out = torch.empty(n, dtype=torch.int32, device=device)
+    check(lib().se_probe(out.data_ptr(), n, stream_of(out)), "se_probe")
+    return out
