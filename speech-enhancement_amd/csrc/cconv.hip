@@ -1,0 +1,816 @@
+// Complex (transposed) 2-D convolution as one fused implicit GEMM on MFMA.
+//
+// Replaces ComplexConv.forward (complex_nn.py:52-65) — four real
+// nn.Conv2d / nn.ConvTranspose2d calls plus sub/add/cat — and their autograd
+// backward, for ComplexConv2d (complex_nn.py:67-78) and
+// ComplexConvTranspose2d (complex_nn.py:80-91); also plain real convs
+// (frcrn.py:115 final_conv) when complex_weights == 0.
+//
+// Every pass (forward, data-grad) is an OUTPUT-STATIONARY GATHER GEMM
+//   Y[b, n, p_h + S_h*q_h, p_w + S_w*q_w] = sum_k G[m, k] * Wp[k, n]
+//   m = (b, q_h, q_w),  k = tap * Cg + c,
+//   G[m, k] = X[b, c, q_h*s_h + off_h[tap], q_w*s_w + off_w[tap]]   (0 outside)
+// A strided conv is one class (S = 1, s = stride). A transposed conv (and a
+// conv's data-grad) is split into stride-phase classes p (S = stride, s = 1)
+// whose tap lists keep only the kernel rows that hit that phase, so no MFMA
+// work is spent on the zeros a naive "dilate then convolve" would insert.
+// The weight-grad pass is a reduction GEMM over m:
+//   dWp[k, n] = sum_m G[m, k] * D[m, n]
+//
+// Tiles: fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32 (exact fp32,
+// no TF32 on gfx950). A workgroup of 4 waves computes BN x BM outputs; the
+// MFMA A operand is the weight tile (rows = n), the B operand the gathered
+// activations (cols = m) so the accumulator's lane index runs along m = the
+// contiguous time axis and epilogue stores are 128-B coalesced.
+#include "common.hpp"
+
+#include <algorithm>
+#include <vector>
+
+namespace {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+constexpr int kThreads = 256;
+constexpr int kBK = 32;      // reduction depth per K-step (16 MFMA k-pairs)
+constexpr int kMaxTaps = 64; // per-class taps (kh*kw <= 64)
+constexpr int kInvalidOff = -(1 << 29);
+
+// ---------------------------------------------------------------------------
+// Gather-GEMM (forward and data-grad)
+// ---------------------------------------------------------------------------
+struct GatherArgs {
+  const float* X;      // gathered tensor [B, Cg, Hi, Wi]
+  const int4* ktab;    // [Kp] {c*Hi*Wi + offh*Wi + offw, offh, offw, 0}
+  const float* Wp;     // [Kp, ldw]
+  const float* bias;   // [N] or nullptr
+  float* Y;            // [B, N, Ho, Wo]
+  int Cg, Hi, Wi;
+  int N, Ho, Wo;
+  int ph, pw, Sh, Sw, Qh, Qw, sh, sw;
+  int Kp, ldw, M;
+};
+
+template <int BN, int BM, int WN, int WM>
+__global__ void __launch_bounds__(kThreads)
+gather_gemm_kernel(const GatherArgs a) {
+  static_assert(WN * WM == 4, "4 waves");
+  constexpr int TN = BN / WN, TM = BM / WM;       // wave tile
+  constexpr int RN = TN / 32, RM = TM / 32;       // 32x32 MFMA repeats
+  constexpr int KR = kThreads / BM;               // threads per m column
+  constexpr int AJ = kBK / KR;                    // A rows per thread per step
+  constexpr int WV = (kBK * BN) / (4 * kThreads); // float4 weight loads/thread
+  static_assert(RN >= 1 && RM >= 1 && KR >= 1 && WV >= 1, "tile shape");
+
+  __shared__ __attribute__((aligned(16))) float sA[2][kBK][BM];
+  __shared__ __attribute__((aligned(16))) float sW[2][kBK][BN];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM;
+  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  const long long HiWi = (long long)a.Hi * a.Wi;
+
+  // --- this thread's gather column (fixed for the whole K loop) ---
+  const int am = tid % BM, akr = tid / BM;        // akr is wave-uniform
+  const int m = m0 + am;
+  const bool mval = m < a.M;
+  int hb = 0, wb = 0;
+  long long xbase = 0;
+  if (mval) {
+    const int qhw = a.Qh * a.Qw;
+    const int b = m / qhw, r = m - b * qhw;
+    const int qh = r / a.Qw, qw = r - qh * a.Qw;
+    hb = qh * a.sh;
+    wb = qw * a.sw;
+    xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+  }
+
+  float ra[AJ];
+  float4 rw[WV];
+  auto load_tile = [&](int k0) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) {
+      const int k = __builtin_amdgcn_readfirstlane(k0 + akr + KR * j);
+      const int4 e = a.ktab[k];
+      const int hi = hb + e.y, wi = wb + e.z;
+      const bool ok = mval && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+      ra[j] = ok ? a.X[xbase + e.x] : 0.f;
+    }
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int idx = tid + kThreads * j;           // float4 index in [BK][BN/4]
+      const int kr = idx / (BN / 4), c4 = idx % (BN / 4);
+      rw[j] = *reinterpret_cast<const float4*>(a.Wp + (long long)(k0 + kr) * a.ldw + n0 + 4 * c4);
+    }
+  };
+  auto store_tile = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < AJ; ++j) sA[buf][akr + KR * j][am] = ra[j];
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int idx = tid + kThreads * j;
+      const int kr = idx / (BN / 4), c4 = idx % (BN / 4);
+      *reinterpret_cast<float4*>(&sW[buf][kr][4 * c4]) = rw[j];
+    }
+  };
+
+  f32x16 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int j = 0; j < RM; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nk = a.Kp / kBK;
+  if (nk > 0) {
+    load_tile(0);
+    store_tile(0);
+  }
+  __syncthreads();
+  const int lk = lane >> 5, lc = lane & 31;
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) load_tile((kt + 1) * kBK);
+#pragma unroll
+    for (int kk = 0; kk < kBK / 2; ++kk) {
+      float fa[RN], fb[RM];
+#pragma unroll
+      for (int i = 0; i < RN; ++i) fa[i] = sW[cur][2 * kk + lk][wn * TN + 32 * i + lc];
+#pragma unroll
+      for (int j = 0; j < RM; ++j) fb[j] = sA[cur][2 * kk + lk][wm * TM + 32 * j + lc];
+#pragma unroll
+      for (int i = 0; i < RN; ++i)
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (kt + 1 < nk) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // --- epilogue: lane -> m (coalesced along time), registers -> n ---
+  const long long HoWo = (long long)a.Ho * a.Wo;
+#pragma unroll
+  for (int j = 0; j < RM; ++j) {
+    const int mm = m0 + wm * TM + 32 * j + lc;
+    if (mm >= a.M) continue;
+    const int qhw = a.Qh * a.Qw;
+    const int b = mm / qhw, r = mm - b * qhw;
+    const int qh = r / a.Qw, qw = r - qh * a.Qw;
+    const long long ybase = (long long)b * a.N * HoWo +
+                            (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int r2 = 0; r2 < 16; ++r2) {
+        const int n = n0 + wn * TN + 32 * i + (r2 & 3) + 8 * (r2 >> 2) + 4 * lk;
+        if (n < a.N) {
+          float v = acc[i][j][r2];
+          if (a.bias) v += a.bias[n];
+          a.Y[ybase + n * HoWo] = v;
+        }
+      }
+  }
+}
+
+// Small-N variant (N <= 16: final_conv 128->2, the CCBAM k7 conv 4->2 and its
+// data-grad): HBM-bound, one output position per thread, weights in LDS.
+template <int NOUT>
+__global__ void __launch_bounds__(kThreads)
+gather_smalln_kernel(const GatherArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float sWs[];  // [Kp][NOUT]
+  for (int i = threadIdx.x; i < a.Kp * NOUT; i += kThreads) {
+    const int k = i / NOUT, n = i % NOUT;
+    sWs[i] = a.Wp[(long long)k * a.ldw + n];
+  }
+  __syncthreads();
+  const int m = blockIdx.x * kThreads + threadIdx.x;
+  if (m >= a.M) return;
+  const int qhw = a.Qh * a.Qw;
+  const int b = m / qhw, r = m - b * qhw;
+  const int qh = r / a.Qw, qw = r - qh * a.Qw;
+  const int hb = qh * a.sh, wb = qw * a.sw;
+  const long long HiWi = (long long)a.Hi * a.Wi;
+  const long long xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+  float acc[NOUT];
+#pragma unroll
+  for (int n = 0; n < NOUT; ++n) acc[n] = 0.f;
+  for (int k = 0; k < a.Kp; ++k) {
+    const int4 e = a.ktab[k];
+    const int hi = hb + e.y, wi = wb + e.z;
+    if ((unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi) {
+      const float x = a.X[xbase + e.x];
+#pragma unroll
+      for (int n = 0; n < NOUT; ++n) acc[n] = fmaf(x, sWs[k * NOUT + n], acc[n]);
+    }
+  }
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  const long long ybase = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
+                          (a.pw + a.Sw * qw);
+#pragma unroll
+  for (int n = 0; n < NOUT; ++n)
+    if (n < a.N) a.Y[ybase + n * HoWo] = acc[n] + (a.bias ? a.bias[n] : 0.f);
+}
+
+// ---------------------------------------------------------------------------
+// Weight-grad reduction GEMM: dWp[k, n] = sum_m G[m, k] * D[m, n]
+// Each workgroup reduces one m-range (split) for one BKO x BNO tile and
+// writes a partial slab; wgrad_finish_kernel sums the slabs (deterministic).
+// ---------------------------------------------------------------------------
+struct WgradArgs {
+  const float* X;      // gathered tensor [B, Cg, Hi, Wi]
+  const int4* ktab;    // [Kp]
+  const float* D;      // direct tensor [B, N, Qh, Qw]
+  float* slab;         // [splits, Kp, Np]
+  int Cg, Hi, Wi;
+  int N, Qh, Qw, sh, sw;
+  int Kp, Np, M;
+  int m_per_split;     // multiple of BMR
+};
+
+constexpr int kBMR = 64;   // m per reduction step (one wave-width of positions)
+
+template <int BKO, int BNO, int WK, int WNn>
+__global__ void __launch_bounds__(kThreads)
+wgrad_gemm_kernel(const WgradArgs a) {
+  static_assert(WK * WNn == 4, "4 waves");
+  constexpr int TK = BKO / WK, TN = BNO / WNn;
+  constexpr int RK = TK / 32, RN = TN / 32;
+  constexpr int GJ = BKO / 4;      // G rows per wave per step (row = wave + 4j)
+  constexpr int DJ = BNO / 4;      // D rows per wave per step
+  constexpr int L = kBMR + 1;      // padded [row][m] images: conflict-free both ways
+  __shared__ float sG[2][BKO * L];
+  __shared__ float sD[2][BNO * L];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wk = wave / WNn, wnn = wave % WNn;
+  const int k0 = blockIdx.x * BKO, n0 = blockIdx.y * BNO;
+  const int split = blockIdx.z;
+  const int mbeg = split * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  const long long HiWi = (long long)a.Hi * a.Wi;
+  const long long QQ = (long long)a.Qh * a.Qw;
+
+  // incremental decode of this lane's m = mbeg + lane + step*64
+  int cb, cqh, cqw;
+  {
+    const long long mm = mbeg + lane;
+    cb = (int)(mm / QQ);
+    const int r = (int)(mm - cb * QQ);
+    cqh = r / a.Qw;
+    cqw = r - cqh * a.Qw;
+  }
+  float rg[GJ], rd[DJ];
+  auto load_step = [&](int mstep) {
+    const bool mv = mstep + lane < mend;
+    const int hb = cqh * a.sh, wb = cqw * a.sw;
+    const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) {
+      const int4 e = a.ktab[k0 + wave + 4 * j];          // wave-uniform -> scalar load
+      const int hi = hb + e.y, wi = wb + e.z;
+      const bool ok = mv && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+      rg[j] = ok ? a.X[xb + e.x] : 0.f;
+    }
+    const long long db = (long long)cb * a.N * QQ + (long long)cqh * a.Qw + cqw;
+#pragma unroll
+    for (int j = 0; j < DJ; ++j) {
+      const int n = n0 + wave + 4 * j;
+      rd[j] = (mv && n < a.N) ? a.D[db + (long long)n * QQ] : 0.f;
+    }
+    cqw += kBMR;
+    while (cqw >= a.Qw) {
+      cqw -= a.Qw;
+      if (++cqh >= a.Qh) { cqh = 0; ++cb; }
+    }
+  };
+  auto store_step = [&](int buf) {
+#pragma unroll
+    for (int j = 0; j < GJ; ++j) sG[buf][(wave + 4 * j) * L + lane] = rg[j];
+#pragma unroll
+    for (int j = 0; j < DJ; ++j) sD[buf][(wave + 4 * j) * L + lane] = rd[j];
+  };
+
+  f32x16 acc[RK][RN];
+#pragma unroll
+  for (int i = 0; i < RK; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nsteps = (mend > mbeg) ? (mend - mbeg + kBMR - 1) / kBMR : 0;
+  if (nsteps > 0) {
+    load_step(mbeg);
+    store_step(0);
+  }
+  __syncthreads();
+  const int lk = lane >> 5, lc = lane & 31;
+  for (int s = 0; s < nsteps; ++s) {
+    const int cur = s & 1;
+    if (s + 1 < nsteps) load_step(mbeg + (s + 1) * kBMR);
+#pragma unroll 8
+    for (int kk = 0; kk < kBMR / 2; ++kk) {
+      float fa[RK], fb[RN];
+#pragma unroll
+      for (int i = 0; i < RK; ++i) fa[i] = sG[cur][(wk * TK + 32 * i + lc) * L + 2 * kk + lk];
+#pragma unroll
+      for (int j = 0; j < RN; ++j) fb[j] = sD[cur][(wnn * TN + 32 * j + lc) * L + 2 * kk + lk];
+#pragma unroll
+      for (int i = 0; i < RK; ++i)
+#pragma unroll
+        for (int j = 0; j < RN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+    }
+    if (s + 1 < nsteps) store_step(cur ^ 1);
+    __syncthreads();
+  }
+  // acc[i][j][r]: row k = 32i + (r&3) + 8(r>>2) + 4*lk, col n = 32j + lc
+  float* out = a.slab + (long long)split * a.Kp * a.Np;
+#pragma unroll
+  for (int i = 0; i < RK; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = k0 + wk * TK + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int n = n0 + wnn * TN + 32 * j + lc;
+        out[(long long)k * a.Np + n] = acc[i][j][r];
+      }
+}
+
+// ---------------------------------------------------------------------------
+// Weight packing / unpacking (the complex block weight, complex_nn.py:52-65)
+// ---------------------------------------------------------------------------
+// The real-equivalent kernel K(ci, co, i, j) of a complex layer, in terms of
+// the (input block, output block) of the channel-stacked tensors:
+//   (re, re) -> Wr, (re, im) -> Wi, (im, re) -> -Wi, (im, im) -> Wr.
+// Wr/Wi memory layout: conv [Co/2, Ci/2, kh, kw]; convT [Ci/2, Co/2, kh, kw].
+struct WeightView {
+  const float* wr;
+  const float* wi;
+  int Ci, Co, kh, kw;
+  int transposed, complex_w;
+};
+
+__device__ __forceinline__ float kernel_value(const WeightView& w, int ci, int co, int i, int j) {
+  if (!w.complex_w) {
+    const long long idx = w.transposed ? (((long long)ci * w.Co + co) * w.kh + i) * w.kw + j
+                                       : (((long long)co * w.Ci + ci) * w.kh + i) * w.kw + j;
+    return w.wr[idx];
+  }
+  const int hci = w.Ci / 2, hco = w.Co / 2;
+  const bool ci_im = ci >= hci, co_im = co >= hco;
+  const int a = ci_im ? ci - hci : ci, b = co_im ? co - hco : co;
+  const long long idx = w.transposed ? (((long long)a * hco + b) * w.kh + i) * w.kw + j
+                                     : (((long long)b * hci + a) * w.kh + i) * w.kw + j;
+  if (ci_im == co_im) return w.wr[idx];
+  return co_im ? w.wi[idx] : -w.wi[idx];
+}
+
+struct TapList {
+  int n;
+  int ti[kMaxTaps], tj[kMaxTaps];     // kernel (i, j) of each tap
+  int offh[kMaxTaps], offw[kMaxTaps]; // input offsets
+};
+
+// Builds Wp[k = t*Cg + c][n] (zero rows/cols up to Kp x ldw) and ktab[k].
+// data_grad = 0: gather channel c is ci, output n is co; 1: c is co, n is ci.
+__global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int Kp, int ldw,
+                                  int Hi, int Wi, int data_grad, float* Wp, int4* ktab) {
+  const int K = taps.n * Cg;
+  const long long total = (long long)Kp * ldw;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(idx / ldw), n = (int)(idx % ldw);
+    float v = 0.f;
+    if (k < K && n < N) {
+      const int t = k / Cg, c = k % Cg;
+      const int ci = data_grad ? n : c, co = data_grad ? c : n;
+      v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
+    }
+    Wp[idx] = v;
+    if (n == 0) {
+      int4 e;
+      if (k < K) {
+        const int t = k / Cg, c = k % Cg;
+        e.x = (int)((long long)c * Hi * Wi + (long long)taps.offh[t] * Wi + taps.offw[t]);
+        e.y = taps.offh[t];
+        e.z = taps.offw[t];
+      } else {
+        e.x = 0; e.y = kInvalidOff; e.z = 0;
+      }
+      e.w = 0;
+      ktab[k] = e;
+    }
+  }
+}
+
+// bias_full[n] for the fused complex conv: re = br - bi, im = bi + br.
+__global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out) {
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  if (!complex_w) { out[n] = br[n]; return; }
+  const int h = N / 2;
+  out[n] = n < h ? br[n] - bi[n] : bi[n - h] + br[n - h];
+}
+
+// Sums the wgrad slabs and scatters the real-equivalent gradient dK back onto
+// dWr / dWi: dWr = dK(re,re) + dK(im,im); dWi = dK(re,im) - dK(im,re).
+// dWp layout: [k = t*Cg + c][n]; conv: c = ci, n = co; convT: c = co, n = ci.
+struct UnpackArgs {
+  const float* slab;
+  int splits, Kp, Np;
+  float* dwr; float* dwi;
+  int Ci, Co, kh, kw, transposed, complex_w;
+  int Cg;                                  // gather channels of the wgrad pass
+  int tap_of[kMaxTaps];                    // (i*kw + j) -> tap index t
+};
+
+__device__ __forceinline__ float dk_sum(const UnpackArgs& u, int ci, int co, int t) {
+  const int c = u.transposed ? co : ci;
+  const int n = u.transposed ? ci : co;
+  const long long off = (long long)(t * u.Cg + c) * u.Np + n;
+  float s = 0.f;
+  for (int sp = 0; sp < u.splits; ++sp) s += u.slab[(long long)sp * u.Kp * u.Np + off];
+  return s;
+}
+
+__global__ void wgrad_finish_kernel(const UnpackArgs u) {
+  const int hci = u.complex_w ? u.Ci / 2 : u.Ci, hco = u.complex_w ? u.Co / 2 : u.Co;
+  const long long total = (long long)hci * hco * u.kh * u.kw;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    // idx enumerates the weight tensor in memory order
+    const int j = (int)(idx % u.kw);
+    const int i = (int)((idx / u.kw) % u.kh);
+    const long long ab = idx / ((long long)u.kw * u.kh);
+    int a0, b0;   // a0 = first dim, b0 = second dim of the weight tensor
+    if (u.transposed) { a0 = (int)(ab / hco); b0 = (int)(ab % hco); }
+    else { a0 = (int)(ab / hci); b0 = (int)(ab % hci); }
+    const int ci = u.transposed ? a0 : b0, co = u.transposed ? b0 : a0;
+    const int t = u.tap_of[i * u.kw + j];
+    if (!u.complex_w) {
+      u.dwr[idx] = dk_sum(u, ci, co, t);
+      continue;
+    }
+    const float rr = dk_sum(u, ci, co, t), ii = dk_sum(u, ci + hci, co + hco, t);
+    const float ri = dk_sum(u, ci, co + hco, t), ir = dk_sum(u, ci + hci, co, t);
+    u.dwr[idx] = rr + ii;
+    u.dwi[idx] = ri - ir;
+  }
+}
+
+// Bias grad: db_full[n] = sum over (b, h, w) of dy[b, n, h, w]; then fold.
+__global__ void bias_grad_kernel(const float* dy, int B, int N, long long HW, int complex_w,
+                                 float* dbr, float* dbi) {
+  const int n = blockIdx.x;  // one block per real output channel (re and im folded below)
+  __shared__ float red[kThreads / 64];
+  float s = 0.f;
+  for (int b = 0; b < B; ++b) {
+    const float* p = dy + ((long long)b * N + n) * HW;
+    for (long long i = threadIdx.x; i < HW; i += kThreads) s += p[i];
+  }
+  s = se::wave_sum(s);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int i = 0; i < kThreads / 64; ++i) t += red[i];
+    if (!complex_w) { dbr[n] = t; return; }
+    const int h = N / 2;
+    // d(br) = sum(dy_re) + sum(dy_im); d(bi) = -sum(dy_re) + sum(dy_im)
+    if (n < h) { atomicAdd(&dbr[n], t); atomicAdd(&dbi[n], -t); }
+    else { atomicAdd(&dbr[n - h], t); atomicAdd(&dbi[n - h], t); }
+  }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side planning
+// ---------------------------------------------------------------------------
+struct Dim1 {   // one spatial dim of one class
+  int p, S, Q, s;
+  int ntaps;
+  int tap[16], off[16];
+};
+
+// strided gather: out q in [0, Lout), in = q*stride + i*dil - pad
+static Dim1 strided_dim(int Lout, int k, int stride, int pad, int dil) {
+  Dim1 d{};
+  d.p = 0; d.S = 1; d.Q = Lout; d.s = stride;
+  d.ntaps = k;
+  for (int i = 0; i < k; ++i) { d.tap[i] = i; d.off[i] = i * dil - pad; }
+  return d;
+}
+
+// phase-class gather for class p of a stride-`stride` scatter:
+// out o = p + stride*q ; in = q + (p + pad - i*dil)/stride for matching taps
+static Dim1 phase_dim(int Lout, int k, int stride, int pad, int dil, int p) {
+  Dim1 d{};
+  d.p = p; d.S = stride; d.s = 1;
+  d.Q = Lout > p ? (Lout - p + stride - 1) / stride : 0;
+  d.ntaps = 0;
+  for (int i = 0; i < k; ++i) {
+    const int num = p + pad - i * dil;
+    const int r = ((num % stride) + stride) % stride;
+    if (r == 0) { d.tap[d.ntaps] = i; d.off[d.ntaps] = num / stride; ++d.ntaps; }
+  }
+  return d;
+}
+
+struct ClassPlan {
+  Dim1 h, w;
+  TapList taps;
+  int K, Kp;
+};
+
+static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
+
+static void finish_plan(ClassPlan& c, int Cg) {
+  c.taps.n = c.h.ntaps * c.w.ntaps;
+  int t = 0;
+  for (int a = 0; a < c.h.ntaps; ++a)
+    for (int b = 0; b < c.w.ntaps; ++b, ++t) {
+      c.taps.ti[t] = c.h.tap[a]; c.taps.tj[t] = c.w.tap[b];
+      c.taps.offh[t] = c.h.off[a]; c.taps.offw[t] = c.w.off[b];
+    }
+  c.K = c.taps.n * Cg;
+  c.Kp = round_up(std::max(c.K, 1), kBK);
+}
+
+enum Pass { kFwd = 0, kData = 1 };
+
+struct ConvGeom {
+  int B, Ci, Hi, Wi, Co, Ho, Wo;
+  int kh, kw, sh, sw, ph, pw, dh, dw, oph, opw, transposed, complex_w;
+};
+
+static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
+  if (!d) return SE_E_ARG;
+  g.B = d->batch; g.Ci = d->in_channels; g.Hi = d->in_h; g.Wi = d->in_w; g.Co = d->out_channels;
+  g.kh = d->kernel_h; g.kw = d->kernel_w; g.sh = d->stride_h; g.sw = d->stride_w;
+  g.ph = d->pad_h; g.pw = d->pad_w; g.dh = d->dil_h; g.dw = d->dil_w;
+  g.oph = d->out_pad_h; g.opw = d->out_pad_w; g.transposed = d->transposed; g.complex_w = d->complex_weights;
+  if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
+      g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
+    return SE_E_ARG;
+  if (g.kh > 16 || g.kw > 16 || g.kh * g.kw > kMaxTaps) return SE_E_UNSUPPORTED;
+  if (g.complex_w && ((g.Ci & 1) || (g.Co & 1))) return SE_E_SHAPE;
+  if (g.transposed) {
+    g.Ho = (g.Hi - 1) * g.sh - 2 * g.ph + g.dh * (g.kh - 1) + g.oph + 1;
+    g.Wo = (g.Wi - 1) * g.sw - 2 * g.pw + g.dw * (g.kw - 1) + g.opw + 1;
+  } else {
+    g.Ho = (g.Hi + 2 * g.ph - g.dh * (g.kh - 1) - 1) / g.sh + 1;
+    g.Wo = (g.Wi + 2 * g.pw - g.dw * (g.kw - 1) - 1) / g.sw + 1;
+  }
+  if (g.Ho <= 0 || g.Wo <= 0) return SE_E_SHAPE;
+  return SE_OK;
+}
+
+// Classes of a gather pass. kFwd: conv -> strided, convT -> phase.
+// kData: conv -> phase (scatter back), convT -> strided.
+static std::vector<ClassPlan> plan_pass(const ConvGeom& g, Pass pass) {
+  std::vector<ClassPlan> out;
+  const bool phase = (pass == kFwd) ? g.transposed : !g.transposed;
+  const int Lh = (pass == kFwd) ? g.Ho : g.Hi, Lw = (pass == kFwd) ? g.Wo : g.Wi;
+  const int Cg = (pass == kFwd) ? g.Ci : g.Co;
+  if (!phase) {
+    ClassPlan c{};
+    c.h = strided_dim(Lh, g.kh, g.sh, g.ph, g.dh);
+    c.w = strided_dim(Lw, g.kw, g.sw, g.pw, g.dw);
+    finish_plan(c, Cg);
+    out.push_back(c);
+    return out;
+  }
+  for (int p = 0; p < g.sh; ++p)
+    for (int q = 0; q < g.sw; ++q) {
+      ClassPlan c{};
+      c.h = phase_dim(Lh, g.kh, g.sh, g.ph, g.dh, p);
+      c.w = phase_dim(Lw, g.kw, g.sw, g.pw, g.dw, q);
+      if (c.h.Q == 0 || c.w.Q == 0) continue;
+      finish_plan(c, Cg);
+      out.push_back(c);
+    }
+  return out;
+}
+
+static inline int ldw_for(int N) {
+  if (N <= 16) return N <= 4 ? 4 : (N <= 8 ? 8 : 16);  // = the small-N kernel's NOUT
+  return round_up(N, N <= 64 ? 64 : 128);
+}
+
+static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N) {
+  size_t bytes = 0;
+  const int ldw = ldw_for(N);
+  for (const auto& c : cls) {
+    bytes += (size_t)c.Kp * ldw * sizeof(float);
+    bytes += (size_t)c.Kp * sizeof(int4);
+  }
+  bytes += (size_t)round_up(N, 128) * sizeof(float);  // bias_full
+  return bytes + 256;
+}
+
+// wgrad plan: G is gathered (strided) over the grid of D.
+struct WgradPlan {
+  ClassPlan c;        // strided class over D's grid
+  int Cg, N, Qh, Qw;  // gather channels, D channels, D grid
+  int Hi, Wi;         // G spatial dims
+  int M, splits, m_per_split, Np;
+};
+
+static WgradPlan plan_wgrad(const ConvGeom& g) {
+  WgradPlan w{};
+  if (!g.transposed) {   // G = x strided over y's grid, D = dy
+    w.c.h = strided_dim(g.Ho, g.kh, g.sh, g.ph, g.dh);
+    w.c.w = strided_dim(g.Wo, g.kw, g.sw, g.pw, g.dw);
+    w.Cg = g.Ci; w.N = g.Co; w.Qh = g.Ho; w.Qw = g.Wo; w.Hi = g.Hi; w.Wi = g.Wi;
+  } else {               // G = dy strided over x's grid, D = x
+    w.c.h = strided_dim(g.Hi, g.kh, g.sh, g.ph, g.dh);
+    w.c.w = strided_dim(g.Wi, g.kw, g.sw, g.pw, g.dw);
+    w.Cg = g.Co; w.N = g.Ci; w.Qh = g.Hi; w.Qw = g.Wi; w.Hi = g.Ho; w.Wi = g.Wo;
+  }
+  finish_plan(w.c, w.Cg);
+  w.c.Kp = round_up(std::max(w.c.K, 1), 128);
+  w.Np = round_up(w.N, w.N <= 32 ? 32 : 128);
+  w.M = g.B * w.Qh * w.Qw;
+  const int tiles = (w.c.Kp / 128) * (w.Np / (w.N <= 32 ? 32 : 128));
+  int splits = std::max(1, 1024 / std::max(tiles, 1));
+  const int max_by_m = std::max(1, w.M / (kBMR * 8));
+  splits = std::min(splits, max_by_m);
+  // keep the slab <= 256 MB
+  const size_t per = (size_t)w.c.Kp * w.Np * sizeof(float);
+  splits = (int)std::min<size_t>(splits, std::max<size_t>(1, (256u << 20) / per));
+  w.m_per_split = round_up((w.M + splits - 1) / splits, kBMR);
+  w.splits = (w.M + w.m_per_split - 1) / w.m_per_split;
+  return w;
+}
+
+static size_t wgrad_ws_bytes(const WgradPlan& w) {
+  return (size_t)w.splits * w.c.Kp * w.Np * sizeof(float) + (size_t)w.c.Kp * sizeof(int4) + 256;
+}
+
+static inline char* align256(char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); }
+
+static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const float* wr,
+                         const float* wi, const float* bias_br, const float* bias_bi, float* Y,
+                         void* ws, size_t ws_bytes, hipStream_t st) {
+  auto cls = plan_pass(g, pass);
+  const int N = (pass == kFwd) ? g.Co : g.Ci;
+  const int Cg = (pass == kFwd) ? g.Ci : g.Co;
+  const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
+  const int Ho = (pass == kFwd) ? g.Ho : g.Hi, Wo = (pass == kFwd) ? g.Wo : g.Wi;
+  if (ws_bytes < gather_ws_bytes(cls, N)) return SE_E_WORKSPACE;
+  const int ldw = ldw_for(N);
+  WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w};
+
+  char* p = align256((char*)ws);
+  float* bias_full = nullptr;
+  if (pass == kFwd && bias_br) {
+    bias_full = (float*)p;
+    p = align256(p + round_up(N, 128) * sizeof(float));
+    hipLaunchKernelGGL(prep_bias_kernel, dim3(se::ceil_div(N, 256)), dim3(256), 0, st,
+                       bias_br, bias_bi, N, g.complex_w, bias_full);
+  }
+  for (const auto& c : cls) {
+    float* Wp = (float*)p;
+    p = align256(p + (size_t)c.Kp * ldw * sizeof(float));
+    int4* ktab = (int4*)p;
+    p = align256(p + (size_t)c.Kp * sizeof(int4));
+    const long long tot = (long long)c.Kp * ldw;
+    hipLaunchKernelGGL(prep_class_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
+                       dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, pass == kData ? 1 : 0,
+                       Wp, ktab);
+    GatherArgs a{};
+    a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.Y = Y;
+    a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
+    a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
+    a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
+    const long long M = (long long)g.B * c.h.Q * c.w.Q;
+    if (M > INT32_MAX) return SE_E_UNSUPPORTED;
+    a.M = (int)M;
+    if (N <= 16) {
+      const size_t sh = (size_t)c.Kp * ldw * sizeof(float);
+      if (sh > 64 * 1024) return SE_E_UNSUPPORTED;
+      dim3 grid(se::ceil_div(M, kThreads));
+      if (ldw <= 4) hipLaunchKernelGGL(gather_smalln_kernel<4>, grid, dim3(kThreads), sh, st, a);
+      else if (ldw <= 8) hipLaunchKernelGGL(gather_smalln_kernel<8>, grid, dim3(kThreads), sh, st, a);
+      else hipLaunchKernelGGL(gather_smalln_kernel<16>, grid, dim3(kThreads), sh, st, a);
+    } else if (ldw == 64) {
+      dim3 grid(se::ceil_div(M, 256), 1);
+      hipLaunchKernelGGL((gather_gemm_kernel<64, 256, 1, 4>), grid, dim3(kThreads), 0, st, a);
+    } else {
+      dim3 grid(se::ceil_div(M, 128), ldw / 128);
+      hipLaunchKernelGGL((gather_gemm_kernel<128, 128, 2, 2>), grid, dim3(kThreads), 0, st, a);
+    }
+    SE_LAUNCH_CHECK();
+  }
+  return SE_OK;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// C ABI
+// ---------------------------------------------------------------------------
+extern "C" int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w) {
+  ConvGeom g;
+  const int rc = geom_of(d, g);
+  if (rc) return rc;
+  if (out_h) *out_h = g.Ho;
+  if (out_w) *out_w = g.Wo;
+  return SE_OK;
+}
+
+extern "C" size_t se_conv2d_workspace_size(const se_conv2d_desc* d) {
+  ConvGeom g;
+  if (geom_of(d, g)) return 0;
+  size_t a = gather_ws_bytes(plan_pass(g, kFwd), g.Co);
+  size_t b = gather_ws_bytes(plan_pass(g, kData), g.Ci);
+  size_t c = wgrad_ws_bytes(plan_wgrad(g));
+  return std::max(a, std::max(b, c));
+}
+
+extern "C" int se_conv2d_fwd(const se_conv2d_desc* d, const float* x, const float* wr,
+                             const float* wi, const float* br, const float* bi, float* y,
+                             void* ws, size_t ws_bytes, void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if (!x || !wr || !y || !ws || (g.complex_w && !wi) || (g.complex_w && br && !bi)) return SE_E_ARG;
+  return launch_gather(g, kFwd, x, wr, wi, br, bi, y, ws, ws_bytes, se::as_stream(stream));
+}
+
+extern "C" int se_conv2d_bwd_data(const se_conv2d_desc* d, const float* dy, const float* wr,
+                                  const float* wi, float* dx, void* ws, size_t ws_bytes,
+                                  void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if (!dy || !wr || !dx || !ws || (g.complex_w && !wi)) return SE_E_ARG;
+  // the phase classes tile dx completely; positions hit by no tap get 0
+  return launch_gather(g, kData, dy, wr, wi, nullptr, nullptr, dx, ws, ws_bytes,
+                       se::as_stream(stream));
+}
+
+extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, const float* dy,
+                                    float* dwr, float* dwi, float* dbr, float* dbi, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if (!x || !dy || !dwr || !ws || (g.complex_w && !dwi) || (g.complex_w && dbr && !dbi))
+    return SE_E_ARG;
+  hipStream_t st = se::as_stream(stream);
+  WgradPlan w = plan_wgrad(g);
+  if (ws_bytes < wgrad_ws_bytes(w)) return SE_E_WORKSPACE;
+  char* p = align256((char*)ws);
+  float* slab = (float*)p;
+  p = align256(p + (size_t)w.splits * w.c.Kp * w.Np * sizeof(float));
+  int4* ktab = (int4*)p;
+
+  // ktab only (no weights): reuse prep_class_kernel with ldw = 1 writing into slab[0]
+  // would clobber; build it with a one-column pass into a scratch row instead.
+  {
+    WeightView wv{nullptr, nullptr, g.Ci, g.Co, g.kh, g.kw, g.transposed, 0};
+    // N = 0 -> every Wp entry is 0 and only ktab matters; Wp scratch = slab start
+    hipLaunchKernelGGL(prep_class_kernel, dim3(se::ceil_div(w.c.Kp, 256)), dim3(256), 0, st, wv,
+                       w.c.taps, w.Cg, 0, w.c.Kp, 1, w.Hi, w.Wi, 0, slab, ktab);
+  }
+  WgradArgs a{};
+  a.X = g.transposed ? dy : x;
+  a.D = g.transposed ? x : dy;
+  a.ktab = ktab; a.slab = slab;
+  a.Cg = w.Cg; a.Hi = w.Hi; a.Wi = w.Wi;
+  a.N = w.N; a.Qh = w.Qh; a.Qw = w.Qw; a.sh = w.c.h.s; a.sw = w.c.w.s;
+  a.Kp = w.c.Kp; a.Np = w.Np; a.M = w.M; a.m_per_split = w.m_per_split;
+  if (w.Np == 32) {
+    dim3 grid(w.c.Kp / 128, 1, w.splits);
+    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1>), grid, dim3(kThreads), 0, st, a);
+  } else {
+    dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
+    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2>), grid, dim3(kThreads), 0, st, a);
+  }
+  SE_LAUNCH_CHECK();
+
+  UnpackArgs u{};
+  u.slab = slab; u.splits = w.splits; u.Kp = w.c.Kp; u.Np = w.Np;
+  u.dwr = dwr; u.dwi = dwi; u.Ci = g.Ci; u.Co = g.Co; u.kh = g.kh; u.kw = g.kw;
+  u.transposed = g.transposed; u.complex_w = g.complex_w; u.Cg = w.Cg;
+  for (int t = 0; t < w.c.taps.n; ++t) u.tap_of[w.c.taps.ti[t] * g.kw + w.c.taps.tj[t]] = t;
+  const long long nw = (long long)(g.complex_w ? g.Ci / 2 : g.Ci) * (g.complex_w ? g.Co / 2 : g.Co) * g.kh * g.kw;
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)std::min<long long>((nw + 255) / 256, 4096)),
+                     dim3(256), 0, st, u);
+  SE_LAUNCH_CHECK();
+
+  if (dbr) {
+    const int hco = g.complex_w ? g.Co / 2 : g.Co;
+    if (g.complex_w) {
+      (void)hipMemsetAsync(dbr, 0, sizeof(float) * hco, st);
+      (void)hipMemsetAsync(dbi, 0, sizeof(float) * hco, st);
+    }
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(g.Co), dim3(kThreads), 0, st, dy, g.B, g.Co,
+                       (long long)g.Ho * g.Wo, g.complex_w, dbr, dbi);
+    SE_LAUNCH_CHECK();
+  }
+  return SE_OK;
+}

@@ -1,0 +1,95 @@
+"""GPU parity: fused complex conv / convT implicit GEMM vs reference goldens
+and vs the oracle's four-real-conv form at FRCRN layer shapes (fp32, 1e-5)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, rel_l2
+import paramfill
+from oracle import complex_nn as O_cnn
+
+pytestmark = pytest.mark.gpu
+
+CONV_CASES = [
+    ("enc", False, 16, 12, (5, 2), dict(stride=(2, 1), bias=False)),
+    ("padbias", False, 8, 6, (5, 3), dict(stride=(2, 2), padding=(2, 1), bias=True)),
+    ("k7", False, 4, 2, 7, dict(padding=3, bias=False)),
+    ("dec", True, 16, 12, (5, 2), dict(stride=(2, 1), bias=False)),
+    ("dccrn_dec", True, 8, 6, (5, 2), dict(stride=(2, 1), padding=(2, 0), output_padding=(1, 0), bias=True)),
+    ("dcunet_dec", True, 8, 6, (5, 3), dict(stride=(2, 2), padding=(2, 1), bias=False)),
+]
+
+
+def _run(F, m, x, gy, transposed, kw):
+    wr = m.real_conv.weight.detach().cuda().requires_grad_(True)
+    wi = m.imag_conv.weight.detach().cuda().requires_grad_(True)
+    br = bi = None
+    if m.real_conv.bias is not None:
+        br = m.real_conv.bias.detach().cuda().requires_grad_(True)
+        bi = m.imag_conv.bias.detach().cuda().requires_grad_(True)
+    xg = x.cuda().requires_grad_(True)
+    y = F.conv2d(xg, wr, wi, br, bi, out_channels=2 * m.real_conv.out_channels,
+                 kernel=m.real_conv.kernel_size, stride=kw.get("stride", 1),
+                 padding=kw.get("padding", 0), output_padding=kw.get("output_padding", 0),
+                 transposed=transposed)
+    y.backward(gy.cuda())
+    torch.cuda.synchronize()
+    out = dict(y=y.detach().cpu(), dx=xg.grad.cpu(), dwr=wr.grad.cpu(), dwi=wi.grad.cpu())
+    if br is not None:
+        out.update(dbr=br.grad.cpu(), dbi=bi.grad.cpu())
+    return out
+
+
+@pytest.mark.parametrize("i,case", list(enumerate(CONV_CASES)))
+def test_conv_golden(i, case, gpu_device):
+    from sehip import functional as F
+    g = golden("cconv")
+    name, tr, cin, cout, k, kw = case
+    cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
+    m = paramfill.fill_(cls(cin, cout, k, **kw), seed=i)
+    r = _run(F, m, torch.from_numpy(g[f"{name}_x"]), torch.from_numpy(g[f"{name}_gy"]), tr, kw)
+    for key in ("y", "dx", "dwr", "dwi") + (("dbr", "dbi") if f"{name}_dbr" in g else ()):
+        assert rel_l2(r[key].numpy(), g[f"{name}_{key}"]) < 1e-5, (name, key)
+
+
+def test_real_conv_golden(gpu_device):
+    from sehip import functional as F
+    g = golden("cconv")
+    m = paramfill.fill_(torch.nn.Conv2d(16, 2, (1, 2), bias=False), seed=9)
+    w = m.weight.detach().cuda().requires_grad_(True)
+    x = torch.from_numpy(g["real_x"]).cuda().requires_grad_(True)
+    y = F.conv2d(x, w, out_channels=2, kernel=(1, 2))
+    y.backward(torch.from_numpy(g["real_gy"]).cuda())
+    assert rel_l2(y.detach().cpu().numpy(), g["real_y"]) < 1e-5
+    assert rel_l2(x.grad.cpu().numpy(), g["real_dx"]) < 1e-5
+    assert rel_l2(w.grad.cpu().numpy(), g["real_dw"]) < 1e-5
+
+
+# FRCRN layer geometries at reduced batch/time (frcrn.py:62-102)
+FRCRN_LAYERS = [
+    ("enc0", False, 2, 128, (2, 2, 320, 41)),
+    ("enc1", False, 128, 128, (2, 128, 158, 41)),
+    ("enc5", False, 128, 128, (2, 128, 7, 41)),
+    ("dec0", True, 256, 128, (2, 256, 2, 40)),
+    ("dec4", True, 256, 128, (2, 256, 77, 40)),
+    ("dec5", True, 256, 128, (2, 256, 158, 40)),
+]
+
+
+@pytest.mark.parametrize("name,tr,cin,cout,shape", FRCRN_LAYERS)
+def test_frcrn_layer_vs_oracle(name, tr, cin, cout, shape, gpu_device):
+    from sehip import functional as F
+    cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
+    m = paramfill.fill_(cls(cin, cout, (5, 2), stride=(2, 1), bias=False), seed=7)
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(*shape, generator=gen)
+    xo = x.clone().requires_grad_(True)
+    yo = m(xo)
+    gy = torch.randn(yo.shape, generator=gen)
+    yo.backward(gy)
+    r = _run(F, m, x, gy, tr, dict(stride=(2, 1)))
+    assert rel_l2(r["y"].numpy(), yo.detach().numpy()) < 1e-5
+    assert rel_l2(r["dwr"].numpy(), m.real_conv.weight.grad.numpy()) < 1e-5
+    assert rel_l2(r["dwi"].numpy(), m.imag_conv.weight.grad.numpy()) < 1e-5
+    if name != "enc0":
+        assert rel_l2(r["dx"].numpy(), xo.grad.numpy()) < 1e-5
