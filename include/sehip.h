@@ -135,28 +135,35 @@ int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x,
  * x, y: [B, C, H, W], C = 2*Cc. Per complex channel: mean (Mr, Mi), biased
  * covariance (Vrr, Vri, Vii) + eps, U = V^-1/2 by the closed 2x2 form
  * (complex_nn.py:288-297), Z = W U with symmetric W, y = Z (x - M) + B.
+ * Moments are accumulated in fp64 (one pass over x).
  *
- * params: device fp32 [5*Cc] = Wrr | Wri | Wii | Br | Bi   (NULL if !affine)
- * running: device fp32 [5*Cc] = RMr | RMi | RVrr | RVri | RVii (NULL if !track)
- * nbt: device int64 [1] num_batches_tracked (NULL if !track)
- * save: device fp32 [16*Cc] per-channel state for the backward pass.
- * act: 0 none, 1 LeakyReLU(slope), 2 ReLU.
- * training: 1 = batch statistics (+ running-stat update when running!=NULL).
+ * params : host array of 5 device pointers Wrr, Wri, Wii, Br, Bi, each fp32
+ *          [Cc] (the module's nn.Parameters), or NULL when affine=False.
+ * running: host array of 5 device pointers RMr, RMi, RVrr, RVri, RVii, or
+ *          NULL when track_running_stats=False; updated in place in training.
+ * nbt    : device int64 num_batches_tracked (NULL if not tracking).
+ * save   : device fp32 [16*Cc] per-channel state for se_cbn_bwd.
+ * act    : 0 none, 1 LeakyReLU(slope), 2 ReLU (applied after the affine).
+ * training: 1 = batch statistics (+ running update when running != NULL),
+ *          0 = running statistics.
  * momentum < 0 means "None" (cumulative average, complex_nn.py:223-224).
  * ------------------------------------------------------------------------ */
 size_t se_cbn_workspace_size(int B, int C, int HW);
 
 int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
-               const float* params, float* running, int64_t* nbt,
-               float* save, int training, float eps, float momentum, int act,
-               float slope, void* ws, size_t ws_bytes, void* stream);
-
-/* Backward. gy = dL/dy (post-activation), y = forward output, x = input.
- * dx overwritten; dparams (fp32 [5*Cc], NULL if !affine) overwritten. */
-int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
-               int B, int C, int HW, const float* params, const float* save,
-               float* dparams, int training, int act, float slope, void* ws,
+               const float* const* params, float* const* running,
+               int64_t* nbt, float* save, int training, float eps,
+               float momentum, int act, float slope, void* ws,
                size_t ws_bytes, void* stream);
+
+/* Backward. gy = dL/dy (after the activation), y = forward output,
+ * x = forward input. dx is overwritten. dparams: host array of 5 device
+ * pointers dWrr, dWri, dWii, dBr, dBi (overwritten), or NULL. */
+int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
+               int B, int C, int HW, const float* const* params,
+               const float* save, float* const* dparams, int training,
+               int act, float slope, void* ws, size_t ws_bytes,
+               void* stream);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,327 @@
+// ComplexBatchNorm2d (complex_nn.py:148-329) + fused activation.
+//
+// Reference cost: ~40 ATen launches per call and >= 4 reads of x
+// (SURVEY.md §3.4). Here a training forward is 3 launches and 2 reads of x:
+//   cbn_moments_kernel  : one pass, 5 fp64 moments per complex channel
+//   cbn_finalize_kernel : mean, covariance, running-stat lerp, the closed
+//                         2x2 inverse square root (:288-297), Z = W U
+//   cbn_apply_kernel    : y = act(Z (x - M) + B)
+// and a training backward is 3 launches reading (gy, y, x) twice.
+// All kernels stream the channel planes contiguously (HBM-bound).
+#include "common.hpp"
+
+#include <algorithm>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kSeg = 8192;   // elements of one (b, c) plane per reduction row
+constexpr int kSave = 16;    // floats of per-channel state
+// save layout
+enum { S_MR = 0, S_MI, S_VRR, S_VRI, S_VII, S_URR, S_URI, S_UII,
+       S_ZRR, S_ZRI, S_ZIR, S_ZII, S_BR, S_BI, S_S, S_T };
+
+struct Ptr5 { const float* p[5]; };
+struct MPtr5 { float* p[5]; };
+
+template <int NS>
+__device__ __forceinline__ void block_reduce_store(double (&v)[NS], double* out) {
+  __shared__ double red[kThreads / 64][NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) v[k] = se::wave_sum(v[k]);
+  if ((threadIdx.x & 63) == 0)
+#pragma unroll
+    for (int k = 0; k < NS; ++k) red[threadIdx.x >> 6][k] = v[k];
+  __syncthreads();
+  if (threadIdx.x < NS) {
+    double s = 0;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) s += red[w][threadIdx.x];
+    out[threadIdx.x] = s;
+  }
+}
+
+__device__ __forceinline__ float act_grad(float y, int act, float slope) {
+  if (act == 1) return y > 0.f ? 1.f : slope;
+  if (act == 2) return y > 0.f ? 1.f : 0.f;
+  return 1.f;
+}
+
+// grid (Cc, P). Row r = (b, segment) of channel c; rows strided over P.
+__global__ void __launch_bounds__(kThreads)
+cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, double* part) {
+  const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
+  const int nseg = (HW + kSeg - 1) / kSeg;
+  double v[5] = {0, 0, 0, 0, 0};
+  for (int row = p; row < B * nseg; row += P) {
+    const int b = row / nseg, sg = row - b * nseg;
+    const float* xr = x + ((long long)b * C + c) * HW;
+    const float* xi = x + ((long long)b * C + Cc + c) * HW;
+    const int i1 = min(HW, (sg + 1) * kSeg);
+    for (int i = sg * kSeg + threadIdx.x; i < i1; i += kThreads) {
+      const double r = xr[i], m = xi[i];
+      v[0] += r; v[1] += m; v[2] += r * r; v[3] += r * m; v[4] += m * m;
+    }
+  }
+  block_reduce_store<5>(v, part + ((long long)c * P + p) * 5);
+}
+
+// One block; channel c per thread (strided).
+__global__ void cbn_finalize_kernel(const double* part, int P, double count, int Cc,
+                                    Ptr5 params, int affine, MPtr5 running, int has_running,
+                                    int64_t* nbt, float* save, int training, float eps,
+                                    float momentum) {
+  float factor = 0.f;
+  if (training && has_running) {
+    factor = momentum >= 0.f ? momentum : (float)(1.0 / (double)(nbt ? (*nbt + 1) : 1));
+  }
+  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
+    double mr, mi, vrr, vri, vii;
+    if (training) {
+      double s[5] = {0, 0, 0, 0, 0};
+      for (int p = 0; p < P; ++p)
+        for (int k = 0; k < 5; ++k) s[k] += part[((long long)c * P + p) * 5 + k];
+      mr = s[0] / count; mi = s[1] / count;
+      vrr = s[2] / count - mr * mr;
+      vri = s[3] / count - mr * mi;
+      vii = s[4] / count - mi * mi;
+      if (has_running) {  // lerp_ in fp32 like the reference (:250-251, :272-274)
+        float* rm[5] = {running.p[0], running.p[1], running.p[2], running.p[3], running.p[4]};
+        const float nv[5] = {(float)mr, (float)mi, (float)vrr, (float)vri, (float)vii};
+        for (int k = 0; k < 5; ++k) rm[k][c] = rm[k][c] + factor * (nv[k] - rm[k][c]);
+      }
+    } else {
+      mr = running.p[0][c]; mi = running.p[1][c];
+      vrr = running.p[2][c]; vri = running.p[3][c]; vii = running.p[4][c];
+    }
+    vrr += eps; vii += eps;
+    const double s = sqrt(vrr * vii - vri * vri);
+    const double t = sqrt(vrr + vii + 2.0 * s);
+    const double r = 1.0 / (s * t);
+    const double urr = (s + vii) * r, uii = (s + vrr) * r, uri = -vri * r;
+    double zrr = urr, zri = uri, zir = uri, zii = uii, br = 0, bi = 0;
+    if (affine) {
+      const double wrr = params.p[0][c], wri = params.p[1][c], wii = params.p[2][c];
+      zrr = wrr * urr + wri * uri;
+      zri = wrr * uri + wri * uii;
+      zir = wri * urr + wii * uri;
+      zii = wri * uri + wii * uii;
+      br = params.p[3][c]; bi = params.p[4][c];
+    }
+    float* o = save + (long long)c * kSave;
+    o[S_MR] = (float)mr; o[S_MI] = (float)mi;
+    o[S_VRR] = (float)vrr; o[S_VRI] = (float)vri; o[S_VII] = (float)vii;
+    o[S_URR] = (float)urr; o[S_URI] = (float)uri; o[S_UII] = (float)uii;
+    o[S_ZRR] = (float)zrr; o[S_ZRI] = (float)zri; o[S_ZIR] = (float)zir; o[S_ZII] = (float)zii;
+    o[S_BR] = (float)br; o[S_BI] = (float)bi; o[S_S] = (float)s; o[S_T] = (float)t;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0 && training && has_running && nbt) *nbt += 1;
+}
+
+// grid (ceil(HW / (kThreads*4)), Cc, B)
+__global__ void __launch_bounds__(kThreads)
+cbn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
+                 const float* __restrict__ save, int act, float slope) {
+  const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  const float* s = save + c * kSave;
+  const float mr = s[S_MR], mi = s[S_MI], zrr = s[S_ZRR], zri = s[S_ZRI];
+  const float zir = s[S_ZIR], zii = s[S_ZII], br = s[S_BR], bi = s[S_BI];
+  const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+  const int base = blockIdx.x * kThreads * 4 + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = base + u * kThreads;
+    if (i < HW) {
+      const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+      float yr = zrr * xr + zri * xi + br;
+      float yi = zir * xr + zii * xi + bi;
+      if (act == 1) { yr = yr > 0.f ? yr : yr * slope; yi = yi > 0.f ? yi : yi * slope; }
+      else if (act == 2) { yr = fmaxf(yr, 0.f); yi = fmaxf(yi, 0.f); }
+      y[offr + i] = yr;
+      y[offi + i] = yi;
+    }
+  }
+}
+
+// Backward moments: g = gy * act'(y), xt = x - M.
+// sums: gr, gi, gr*xtr, gr*xti, gi*xtr, gi*xti
+__global__ void __launch_bounds__(kThreads)
+cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                       const float* __restrict__ x, int B, int C, int HW, int P,
+                       const float* __restrict__ save, int act, float slope, double* part) {
+  const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
+  const int nseg = (HW + kSeg - 1) / kSeg;
+  const float mr = save[c * kSave + S_MR], mi = save[c * kSave + S_MI];
+  double v[6] = {0, 0, 0, 0, 0, 0};
+  for (int row = p; row < B * nseg; row += P) {
+    const int b = row / nseg, sg = row - b * nseg;
+    const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+    const int i1 = min(HW, (sg + 1) * kSeg);
+    for (int i = sg * kSeg + threadIdx.x; i < i1; i += kThreads) {
+      const float gr = gy[offr + i] * act_grad(y[offr + i], act, slope);
+      const float gi = gy[offi + i] * act_grad(y[offi + i], act, slope);
+      const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+      v[0] += gr; v[1] += gi;
+      v[2] += (double)gr * xr; v[3] += (double)gr * xi;
+      v[4] += (double)gi * xr; v[5] += (double)gi * xi;
+    }
+  }
+  block_reduce_store<6>(v, part + ((long long)c * P + p) * 6);
+}
+
+// coef layout per channel (12 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi pad
+constexpr int kCoef = 12;
+
+__global__ void cbn_bwd_finalize_kernel(const double* part, int P, double count, int Cc,
+                                        const float* save, Ptr5 params, int affine,
+                                        MPtr5 dparams, int has_dparams, int training,
+                                        float* coef) {
+  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
+    double sm[6] = {0, 0, 0, 0, 0, 0};
+    for (int p = 0; p < P; ++p)
+      for (int k = 0; k < 6; ++k) sm[k] += part[((long long)c * P + p) * 6 + k];
+    const float* s = save + (long long)c * kSave;
+    const double urr = s[S_URR], uri = s[S_URI], uii = s[S_UII];
+    const double vrr = s[S_VRR], vri = s[S_VRI], vii = s[S_VII];
+    const double ss = s[S_S], tt = s[S_T];
+    // dZ = sum g xt^T
+    const double dz00 = sm[2], dz01 = sm[3], dz10 = sm[4], dz11 = sm[5];
+    double wrr = 1, wri = 0, wii = 1;
+    if (affine) { wrr = params.p[0][c]; wri = params.p[1][c]; wii = params.p[2][c]; }
+    double gurr, guri, guii;
+    if (affine) {
+      // dW = dZ U (U symmetric); W symmetric -> Wri collects both off-diagonals
+      const double dw00 = dz00 * urr + dz01 * uri, dw01 = dz00 * uri + dz01 * uii;
+      const double dw10 = dz10 * urr + dz11 * uri, dw11 = dz10 * uri + dz11 * uii;
+      if (has_dparams) {
+        dparams.p[0][c] = (float)dw00;
+        dparams.p[1][c] = (float)(dw01 + dw10);
+        dparams.p[2][c] = (float)dw11;
+        dparams.p[3][c] = (float)sm[0];
+        dparams.p[4][c] = (float)sm[1];
+      }
+      // dU = W^T dZ = W dZ
+      gurr = wrr * dz00 + wri * dz10;
+      guii = wri * dz01 + wii * dz11;
+      guri = (wrr * dz01 + wri * dz11) + (wri * dz00 + wii * dz10);
+    } else {
+      gurr = dz00; guii = dz11; guri = dz01 + dz10;
+    }
+    const double zrr = s[S_ZRR], zri = s[S_ZRI], zir = s[S_ZIR], zii = s[S_ZII];
+    double gbr = 0, gbi = 0, grr = 0, gri = 0, gii = 0;
+    if (training) {
+      // back through U(Vrr, Vri, Vii) = closed form with s = sqrt(det), t = sqrt(tr + 2s)
+      const double r = 1.0 / (ss * tt);
+      const double g_r = gurr * (ss + vii) + guii * (ss + vrr) - guri * vri;
+      const double g_t = -g_r * r / tt;
+      const double g_s = (gurr + guii) * r - g_r * r / ss + g_t / tt;
+      const double g_tau = g_t / (2.0 * tt);
+      const double g_del = g_s / (2.0 * ss);
+      const double gvrr = guii * r + g_tau + g_del * vii;
+      const double gvii = gurr * r + g_tau + g_del * vrr;
+      const double gvri = -guri * r - 2.0 * vri * g_del;
+      grr = 2.0 * gvrr / count; gri = gvri / count; gii = 2.0 * gvii / count;
+      gbr = sm[0] / count; gbi = sm[1] / count;
+    }
+    float* o = coef + (long long)c * kCoef;
+    o[0] = (float)zrr; o[1] = (float)zir;   // dxr = Zrr g_r + Zir g_i
+    o[2] = (float)zri; o[3] = (float)zii;   // dxi = Zri g_r + Zii g_i
+    o[4] = (float)gbr; o[5] = (float)gbi;
+    o[6] = (float)grr; o[7] = (float)gri; o[8] = (float)gii;
+    o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = 0.f;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+                     const float* __restrict__ x, float* __restrict__ dx, int C, int HW,
+                     const float* __restrict__ coef, int act, float slope) {
+  const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  const float* k = coef + c * kCoef;
+  const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
+  const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
+  const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+  const int base = blockIdx.x * kThreads * 4 + threadIdx.x;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int i = base + u * kThreads;
+    if (i < HW) {
+      const float gr = gy[offr + i] * act_grad(y[offr + i], act, slope) - gbr;
+      const float gi = gy[offi + i] * act_grad(y[offi + i], act, slope) - gbi;
+      const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+      dx[offr + i] = a00 * gr + a01 * gi + grr * xr + gri * xi;
+      dx[offi + i] = a10 * gr + a11 * gi + gri * xr + gii * xi;
+    }
+  }
+}
+
+int pick_P(int B, int Cc, int HW) {
+  const int rows = B * ((HW + kSeg - 1) / kSeg);
+  return std::max(1, std::min(rows, std::max(1, 2048 / std::max(Cc, 1))));
+}
+
+}  // namespace
+
+extern "C" size_t se_cbn_workspace_size(int B, int C, int HW) {
+  if (B <= 0 || C <= 0 || HW <= 0) return 0;
+  const int Cc = C / 2;
+  const int P = pick_P(B, Cc, HW);
+  return (size_t)Cc * P * 6 * sizeof(double) + (size_t)Cc * kCoef * sizeof(float) + 512;
+}
+
+extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
+                          const float* const* params, float* const* running, int64_t* nbt,
+                          float* save, int training, float eps, float momentum, int act,
+                          float slope, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || act < 0 || act > 2)
+    return SE_E_ARG;
+  if (!training && !running) return SE_E_ARG;  // eval needs running statistics
+  if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
+  hipStream_t st = se::as_stream(stream);
+  const int Cc = C / 2;
+  const int P = pick_P(B, Cc, HW);
+  double* part = (double*)ws;
+  Ptr5 pp{};
+  MPtr5 rp{};
+  if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
+  if (running) for (int k = 0; k < 5; ++k) rp.p[k] = running[k];
+  if (training) {
+    hipLaunchKernelGGL(cbn_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part);
+    SE_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(cbn_finalize_kernel, dim3(1), dim3(256), 0, st, part, P, (double)B * HW, Cc,
+                     pp, params ? 1 : 0, rp, running ? 1 : 0, nbt, save, training, eps, momentum);
+  SE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), Cc, B), dim3(kThreads),
+                     0, st, x, y, C, HW, save, act, slope);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx, int B,
+                          int C, int HW, const float* const* params, const float* save,
+                          float* const* dparams, int training, int act, float slope, void* ws,
+                          size_t ws_bytes, void* stream) {
+  if (!gy || !y || !x || !dx || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0) return SE_E_ARG;
+  if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
+  hipStream_t st = se::as_stream(stream);
+  const int Cc = C / 2;
+  const int P = pick_P(B, Cc, HW);
+  double* part = (double*)ws;
+  float* coef = (float*)((char*)ws + (size_t)Cc * P * 6 * sizeof(double));
+  Ptr5 pp{};
+  MPtr5 dp{};
+  if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
+  if (dparams) for (int k = 0; k < 5; ++k) dp.p[k] = dparams[k];
+  hipLaunchKernelGGL(cbn_bwd_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, gy, y, x, B, C,
+                     HW, P, save, act, slope, part);
+  SE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cbn_bwd_finalize_kernel, dim3(1), dim3(256), 0, st, part, P, (double)B * HW,
+                     Cc, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, coef);
+  SE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cbn_bwd_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), Cc, B),
+                     dim3(kThreads), 0, st, gy, y, x, dx, C, HW, coef, act, slope);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}

@@ -1,0 +1,430 @@
+// ConvSTFT / ConviSTFT (models/conv_stft.py) as packed real FFTs in LDS.
+//
+// The reference implements the STFT as conv1d against a [N+2, 1, win] basis
+// (conv_stft.py:56) and the inverse as conv_transpose1d against the pinv of
+// that basis followed by a window^2 overlap-add normaliser (:101-106). Both
+// are linear maps we evaluate with FFTs instead (O(N log N) per frame, HBM-
+// bound), two real frames packed into one complex FFT of length N = nfft:
+//
+//   analysis  X[k]  = sum_{n<win} w[n] x[t*hop + n - pad] e^{-2 pi i k n / N}
+//   synthesis the pinv basis is M (M^T M)^{-1} with M^T M = (N/2) I + ee^T + oo^T
+//             (e, o = even / odd index indicators over n < win), so a frame is
+//             w[n] * (z[n] - e/o correction)/(N/2) where
+//             z[n] = Re sum_{k<=N/2} X[k] e^{+2 pi i k n / N}.
+//
+// Frames are gathered with the reflect pad folded into the load; the inverse
+// is tiled over OUTPUT samples (halo frames recomputed) so every output sample
+// is written exactly once, coalesced, with no atomics and no frame buffer.
+#include "common.hpp"
+
+#include <algorithm>
+#include <cmath>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kMaxPasses = 12;
+constexpr int kLdsBudget = 80 * 1024;
+
+struct FftPlan {
+  int N, npass;
+  int radix[kMaxPasses];
+};
+
+__device__ __forceinline__ float2 cmul(float2 a, float2 b) {
+  return make_float2(a.x * b.x - a.y * b.y, a.x * b.y + a.y * b.x);
+}
+__device__ __forceinline__ float2 cadd(float2 a, float2 b) { return make_float2(a.x + b.x, a.y + b.y); }
+__device__ __forceinline__ float2 csub(float2 a, float2 b) { return make_float2(a.x - b.x, a.y - b.y); }
+__device__ __forceinline__ float2 cscale(float2 a, float s) { return make_float2(a.x * s, a.y * s); }
+// -i * a
+__device__ __forceinline__ float2 mul_mi(float2 a) { return make_float2(a.y, -a.x); }
+
+// Stockham autosort FFT (forward sign) of P length-N sequences held in LDS.
+// Returns the buffer that holds the result.
+__device__ float2* fft_forward(float2* a, float2* b, int P, const FftPlan& pl, const float2* __restrict__ tw) {
+  const int N = pl.N;
+  int Ns = 1;
+  for (int ps = 0; ps < pl.npass; ++ps) {
+    const int R = pl.radix[ps];
+    const int nbf = N / R;
+    const int tstep = N / (Ns * R);
+    for (int idx = threadIdx.x; idx < P * nbf; idx += blockDim.x) {
+      const int pr = idx / nbf, j = idx - pr * nbf;
+      const float2* src = a + pr * N;
+      float2* dst = b + pr * N;
+      const int k = j % Ns;
+      float2 v[5];
+      for (int q = 0; q < R; ++q) v[q] = src[j + q * nbf];
+      if (Ns > 1)
+        for (int q = 1; q < R; ++q) v[q] = cmul(v[q], tw[q * k * tstep]);  // < N
+      const int d = (j / Ns) * Ns * R + k;
+      if (R == 2) {
+        dst[d] = cadd(v[0], v[1]);
+        dst[d + Ns] = csub(v[0], v[1]);
+      } else if (R == 4) {
+        const float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+        const float2 t2 = cadd(v[1], v[3]), t3 = mul_mi(csub(v[1], v[3]));
+        dst[d] = cadd(t0, t2);
+        dst[d + Ns] = cadd(t1, t3);
+        dst[d + 2 * Ns] = csub(t0, t2);
+        dst[d + 3 * Ns] = csub(t1, t3);
+      } else if (R == 3) {
+        const float h = 0.86602540378443864676f;
+        const float2 s = cadd(v[1], v[2]), df = csub(v[1], v[2]);
+        const float2 m = csub(v[0], cscale(s, 0.5f));
+        const float2 r = cscale(mul_mi(df), h);
+        dst[d] = cadd(v[0], s);
+        dst[d + Ns] = cadd(m, r);
+        dst[d + 2 * Ns] = csub(m, r);
+      } else {  // R == 5
+        const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+        const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+        const float2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
+        const float2 t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
+        const float2 a1 = cadd(v[0], cadd(cscale(t1, c1), cscale(t2, c2)));
+        const float2 a2 = cadd(v[0], cadd(cscale(t1, c2), cscale(t2, c1)));
+        const float2 b1 = mul_mi(cadd(cscale(t3, s1), cscale(t4, s2)));
+        const float2 b2 = mul_mi(csub(cscale(t3, s2), cscale(t4, s1)));
+        dst[d] = cadd(v[0], cadd(t1, t2));
+        dst[d + Ns] = cadd(a1, b1);
+        dst[d + 4 * Ns] = csub(a1, b1);
+        dst[d + 2 * Ns] = cadd(a2, b2);
+        dst[d + 3 * Ns] = csub(a2, b2);
+      }
+    }
+    __syncthreads();
+    float2* t = a; a = b; b = t;
+    Ns *= R;
+  }
+  return a;
+}
+
+__device__ __forceinline__ int reflect_index(int i, int L) {
+  if (i < 0) i = -i;
+  if (i >= L) i = 2 * (L - 1) - i;
+  return i;
+}
+
+__device__ __forceinline__ int floor_div(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+__device__ __forceinline__ int ceil_div_i(int a, int b) { return -floor_div(-a, b); }
+
+// Unpack two packed real-FFT results (pair j) and store rows k = 0..N/2 of frames
+// t0 + 2j, t0 + 2j + 1. out layout [B, N+2, T] or mags/phase [B, N/2+1, T].
+__device__ void unpack_store(const float2* Z, int P, int N, int t0, int T, int b,
+                             float* out0, float* out1, int mag_phase) {
+  const int half = N / 2 + 1;
+  const int FT = 2 * P;
+  for (int idx = threadIdx.x; idx < half * FT; idx += blockDim.x) {
+    const int k = idx / FT, f = idx - k * FT;
+    const int t = t0 + f;
+    if (t >= T) continue;
+    const int j = f >> 1;
+    const float2 zk = Z[j * N + k];
+    const float2 zc = Z[j * N + ((N - k) % N)];
+    float re, im;
+    if ((f & 1) == 0) {  // (Z[k] + conj Z[N-k]) / 2
+      re = 0.5f * (zk.x + zc.x);
+      im = 0.5f * (zk.y - zc.y);
+    } else {             // (Z[k] - conj Z[N-k]) / (2i)
+      re = 0.5f * (zk.y + zc.y);
+      im = -0.5f * (zk.x - zc.x);
+    }
+    im += 0.f;   // -0 -> +0: DC / Nyquist imag parts are exact zeros (atan2 branch cut)
+    if (!mag_phase) {
+      out0[((long long)b * (2 * half) + k) * T + t] = re;
+      out0[((long long)b * (2 * half) + half + k) * T + t] = im;
+    } else {
+      out0[((long long)b * half + k) * T + t] = sqrtf(re * re + im * im);
+      out1[((long long)b * half + k) * T + t] = atan2f(im, re);
+    }
+  }
+}
+
+struct StftArgs {
+  const float* x;      // [B, L]
+  float* out0;
+  float* out1;
+  const float* window; // [win]
+  const float2* tw;    // [N]
+  int L, win, hop, T, pad, mag_phase, P;
+  FftPlan pl;
+};
+
+// grid (ceil(T / 2P), B)
+__global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  const int N = a.pl.N, P = a.P;
+  float2* A = lds;
+  float2* Bf = lds + P * N;
+  const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
+  const float* x = a.x + (long long)b * a.L;
+  for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) {
+    const int j = idx / N, n = idx - j * N;
+    const int ta = t0 + 2 * j, tb = ta + 1;
+    float ya = 0.f, yb = 0.f;
+    if (n < a.win) {
+      const float w = a.window[n];
+      if (ta < a.T) ya = w * x[reflect_index(ta * a.hop + n - a.pad, a.L)];
+      if (tb < a.T) yb = w * x[reflect_index(tb * a.hop + n - a.pad, a.L)];
+    }
+    A[idx] = make_float2(ya, yb);
+  }
+  __syncthreads();
+  const float2* Z = fft_forward(A, Bf, P, a.pl, a.tw);
+  unpack_store(Z, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase);
+}
+
+struct IstftArgs {
+  const float* in;     // fwd: spec [B, N+2, T]; bwd: gout [B, out_len]
+  float* out;          // fwd: out [B, out_len]; bwd: gspec [B, N+2, T]
+  const float* window;
+  const float2* tw;
+  int T, win, hop, offset, out_len, P, FT;
+  FftPlan pl;
+};
+
+// Sums of v[f][n] over even / odd n < win for every frame f (one wave per frame).
+__device__ void parity_sums(const float2* V, int P, int N, int win, float* sums /*[2P][2]*/) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  for (int f = wave; f < 2 * P; f += nw) {
+    const float2* v = V + (f >> 1) * N;
+    float se = 0.f, so = 0.f;
+    for (int n = lane; n < win; n += 64) {
+      const float val = (f & 1) ? v[n].y : v[n].x;
+      if (n & 1) so += val; else se += val;
+    }
+    se = se::wave_sum(se);
+    so = se::wave_sum(so);
+    if (lane == 0) { sums[2 * f] = se; sums[2 * f + 1] = so; }
+  }
+  __syncthreads();
+}
+
+// G = (M^T M)^{-1} applied to a frame: (v - e*Se/(a+ne) - o*So/(a+no)) / a
+__device__ __forceinline__ float apply_g(float v, int n, float se_, float so_, float inv_a,
+                                         float ce, float co) {
+  return (v - ((n & 1) ? so_ * co : se_ * ce)) * inv_a;
+}
+
+// ConviSTFT forward. grid (ceil(out_len / (FT*hop)), B)
+__global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  __shared__ float sums[64];
+  const int N = a.pl.N, P = a.P, half = N / 2 + 1;
+  float2* A = lds;
+  float2* Bf = lds + P * N;
+  const int b = blockIdx.y;
+  const int s0 = a.offset + blockIdx.x * a.FT * a.hop;
+  const int s1 = min(s0 + a.FT * a.hop, a.offset + a.out_len);
+  const int t_lo = max(0, ceil_div_i(s0 - a.win + 1, a.hop));
+  const int t_hi = min(a.T - 1, floor_div(s1 - 1, a.hop));
+  const float* spec = a.in + (long long)b * 2 * half * a.T;
+
+  // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
+  for (int idx = threadIdx.x; idx < half * P; idx += blockDim.x) {
+    const int k = idx / P, j = idx - k * P;
+    const int ta = t_lo + 2 * j, tb = ta + 1;
+    float2 xa = make_float2(0.f, 0.f), xb = xa;
+    if (ta <= t_hi) xa = make_float2(spec[(long long)k * a.T + ta], spec[(long long)(half + k) * a.T + ta]);
+    if (tb <= t_hi) xb = make_float2(spec[(long long)k * a.T + tb], spec[(long long)(half + k) * a.T + tb]);
+    float2* c = A + j * N;
+    if (k == 0 || k == N / 2) {
+      // E[k] = Re X[k]; C = Re Xa + i Re Xb; store conj
+      c[k] = make_float2(xa.x, -xb.x);
+    } else {
+      // C[k] = Xa/2 + i Xb/2 ; C[N-k] = conj(Xa)/2 + i conj(Xb)/2
+      const float2 ck = make_float2(0.5f * (xa.x - xb.y), 0.5f * (xa.y + xb.x));
+      const float2 cn = make_float2(0.5f * (xa.x + xb.y), 0.5f * (-xa.y + xb.x));
+      c[k] = make_float2(ck.x, -ck.y);
+      c[N - k] = make_float2(cn.x, -cn.y);
+    }
+  }
+  __syncthreads();
+  float2* R = fft_forward(A, Bf, P, a.pl, a.tw);
+  // z = conj(R): z_a = R.x, z_b = -R.y. Fold the sign into the sums/application.
+  for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) R[idx].y = -R[idx].y;
+  __syncthreads();
+  parity_sums(R, P, N, a.win, sums);
+  const float ah = 0.5f * N, inv_a = 1.f / ah;
+  const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
+  float* fr = reinterpret_cast<float*>(R == A ? Bf : A);   // [2P][win] frames
+  for (int idx = threadIdx.x; idx < 2 * P * a.win; idx += blockDim.x) {
+    const int f = idx / a.win, n = idx - f * a.win;
+    const float2 z = R[(f >> 1) * N + n];
+    const float v = (f & 1) ? z.y : z.x;
+    fr[idx] = a.window[n] * apply_g(v, n, sums[2 * f], sums[2 * f + 1], inv_a, ce, co);
+  }
+  __syncthreads();
+  float* out = a.out + (long long)b * a.out_len;
+  for (int s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
+    const int tb0 = max(t_lo, ceil_div_i(s - a.win + 1, a.hop));
+    const int tb1 = min(t_hi, floor_div(s, a.hop));
+    float acc = 0.f, cf = 0.f;
+    for (int t = tb0; t <= tb1; ++t) {
+      const int n = s - t * a.hop;
+      const float w = a.window[n];
+      acc += fr[(t - t_lo) * a.win + n];
+      cf += w * w;
+    }
+    out[s - a.offset] = acc / (cf + 1e-8f);
+  }
+}
+
+// Adjoint of istft_fwd. grid (ceil(T / 2P), B)
+__global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) {
+  extern __shared__ __attribute__((aligned(16))) float2 lds[];
+  __shared__ float sums[64];
+  const int N = a.pl.N, P = a.P;
+  float2* A = lds;
+  float2* Bf = lds + P * N;
+  const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
+  const float* g = a.in + (long long)b * a.out_len;
+  for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) {
+    const int j = idx / N, n = idx - j * N;
+    float va = 0.f, vb = 0.f;
+    if (n < a.win) {
+      const float w = a.window[n];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int t = t0 + 2 * j + h;
+        if (t >= a.T) continue;
+        const int u = t * a.hop + n;
+        if (u < a.offset || u >= a.offset + a.out_len) continue;
+        // OLA normaliser at u (window^2 summed over covering frames)
+        const int tb0 = max(0, ceil_div_i(u - a.win + 1, a.hop));
+        const int tb1 = min(a.T - 1, floor_div(u, a.hop));
+        float cf = 0.f;
+        for (int tt = tb0; tt <= tb1; ++tt) {
+          const float ww = a.window[u - tt * a.hop];
+          cf += ww * ww;
+        }
+        const float v = w * g[u - a.offset] / (cf + 1e-8f);
+        if (h == 0) va = v; else vb = v;
+      }
+    }
+    A[idx] = make_float2(va, vb);
+  }
+  __syncthreads();
+  parity_sums(A, P, N, a.win, sums);
+  const float ah = 0.5f * N, inv_a = 1.f / ah;
+  const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
+  for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) {
+    const int j = idx / N, n = idx - j * N;
+    if (n < a.win) {
+      const float2 v = A[idx];
+      A[idx] = make_float2(apply_g(v.x, n, sums[4 * j], sums[4 * j + 1], inv_a, ce, co),
+                           apply_g(v.y, n, sums[4 * j + 2], sums[4 * j + 3], inv_a, ce, co));
+    }
+  }
+  __syncthreads();
+  const float2* Z = fft_forward(A, Bf, P, a.pl, a.tw);
+  unpack_store(Z, P, N, t0, a.T, b, a.out, nullptr, 0);
+}
+
+// ---------------------------------------------------------------------------
+static bool make_plan(int N, FftPlan& pl) {
+  if (N < 2 || N > 1024) return false;
+  pl.N = N;
+  pl.npass = 0;
+  int n = N;
+  const int order[4] = {4, 2, 3, 5};
+  for (int r : order) {
+    while (n % r == 0) {
+      if (pl.npass >= kMaxPasses) return false;
+      pl.radix[pl.npass++] = r;
+      n /= r;
+    }
+  }
+  return n == 1;
+}
+
+static int pick_pairs(int N) {
+  const int p = kLdsBudget / (2 * N * (int)sizeof(float2));
+  return std::max(1, std::min(16, p));   // sums[] holds 2 floats for 32 frames
+}
+
+static int check_common(int win, int hop, int nfft, FftPlan& pl) {
+  if (win <= 0 || hop <= 0 || nfft <= 0 || win > nfft) return SE_E_ARG;
+  if (nfft & 1) return SE_E_UNSUPPORTED;   // the pinv closed form assumes a Nyquist bin
+  if (!make_plan(nfft, pl)) return SE_E_UNSUPPORTED;
+  return SE_OK;
+}
+
+}  // namespace
+
+extern "C" int se_stft_num_frames(int L, int win, int hop, int nfft, int center) {
+  if (L <= 0 || win <= 0 || hop <= 0 || nfft <= 0) return -1;
+  const int pad = center ? nfft / 2 : 0;
+  const int Lp = L + 2 * pad;
+  if (Lp < win) return 0;
+  return (Lp - win) / hop + 1;
+}
+
+extern "C" int se_stft_fwd(const float* x, float* out0, float* out1, int B, int L, int win,
+                           int hop, int nfft, int center, int mag_phase, const float* window,
+                           const float* twiddle, void* stream) {
+  FftPlan pl;
+  int rc = check_common(win, hop, nfft, pl);
+  if (rc) return rc;
+  if (!x || !out0 || !window || !twiddle || B <= 0 || L <= 0 || (mag_phase && !out1)) return SE_E_ARG;
+  const int pad = center ? nfft / 2 : 0;
+  if (center && L <= pad) return SE_E_SHAPE;   // reflect pad needs L > pad (F.pad reflect)
+  const int T = se_stft_num_frames(L, win, hop, nfft, center);
+  if (T <= 0) return SE_E_SHAPE;
+  StftArgs a{};
+  a.x = x; a.out0 = out0; a.out1 = out1; a.window = window; a.tw = (const float2*)twiddle;
+  a.L = L; a.win = win; a.hop = hop; a.T = T; a.pad = pad; a.mag_phase = mag_phase;
+  a.P = pick_pairs(nfft); a.pl = pl;
+  const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
+  hipLaunchKernelGGL(stft_fwd_kernel, dim3(se::ceil_div(T, 2 * a.P), B), dim3(kThreads), shm,
+                     se::as_stream(stream), a);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+static int istft_setup(int B, int T, int win, int hop, int nfft, int offset, int out_len,
+                       IstftArgs& a) {
+  FftPlan pl;
+  int rc = check_common(win, hop, nfft, pl);
+  if (rc) return rc;
+  if (B <= 0 || T <= 0 || offset < 0 || out_len < 0) return SE_E_ARG;
+  if (offset + out_len > (T - 1) * hop + win) return SE_E_SHAPE;
+  a.T = T; a.win = win; a.hop = hop; a.offset = offset; a.out_len = out_len;
+  a.P = pick_pairs(nfft); a.pl = pl;
+  // output tile: the covering frames of FT*hop samples must fit in 2P
+  a.FT = 2 * a.P - 1 - (win - 1) / hop;
+  if (a.FT < 1) return SE_E_UNSUPPORTED;
+  return SE_OK;
+}
+
+extern "C" int se_istft_fwd(const float* spec, float* out, int B, int T, int win, int hop,
+                            int nfft, int offset, int out_len, const float* window,
+                            const float* twiddle, void* stream) {
+  IstftArgs a{};
+  int rc = istft_setup(B, T, win, hop, nfft, offset, out_len, a);
+  if (rc) return rc;
+  if (!spec || !out || !window || !twiddle) return SE_E_ARG;
+  if (out_len == 0) return SE_OK;
+  a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle;
+  const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
+  hipLaunchKernelGGL(istft_fwd_kernel, dim3(se::ceil_div(out_len, a.FT * hop), B), dim3(kThreads),
+                     shm, se::as_stream(stream), a);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_istft_bwd(const float* gout, float* gspec, int B, int T, int win, int hop,
+                            int nfft, int offset, int out_len, const float* window,
+                            const float* twiddle, void* stream) {
+  IstftArgs a{};
+  int rc = istft_setup(B, T, win, hop, nfft, offset, out_len, a);
+  if (rc) return rc;
+  if (!gout || !gspec || !window || !twiddle) return SE_E_ARG;
+  a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle;
+  const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
+  hipLaunchKernelGGL(istft_bwd_kernel, dim3(se::ceil_div(T, 2 * a.P), B), dim3(kThreads), shm,
+                     se::as_stream(stream), a);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}

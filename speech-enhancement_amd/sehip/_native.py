@@ -36,6 +36,7 @@ class ConvDesc(ctypes.Structure):
 
 
 _P = c_void_p
+_PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
     "se_abi_version": (c_int, []),
     "se_strerror": (c_char_p, [c_int]),
@@ -50,10 +51,10 @@ _SIGNATURES = {
     "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_weight": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
     "se_cbn_workspace_size": (c_size_t, [c_int, c_int, c_int]),
-    "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, _P,
+    "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P,
                            c_int, c_float, c_float, c_int, c_float, _P,
                            c_size_t, _P]),
-    "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _P, _P, _P,
+    "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP,
                            c_int, c_int, c_float, _P, c_size_t, _P]),
 }
 
@@ -114,6 +115,13 @@ def require_device(*ts: torch.Tensor) -> None:
                                "there is no CPU fallback in the product path")
         if t.dtype != torch.float32:
             raise RuntimeError(f"sehip ops take float32 tensors (got {t.dtype})")
+
+
+def ptr_array(ts):
+    """Host array of device pointers (for the se_cbn_* pointer-array args)."""
+    if ts is None:
+        return None
+    return (c_void_p * len(ts))(*[t.data_ptr() for t in ts])
 
 
 def probe(n: int = 1000, device: str = "cuda") -> torch.Tensor:

@@ -1,0 +1,259 @@
+"""Complex layers on channel-stacked [re; im] tensors, HIP path.
+
+Drop-in for /root/reference/models/modules/complex_nn.py: same class names,
+constructor signatures and state_dict keys (``real_conv``/``imag_conv`` stay
+real nn.Conv2d / nn.ConvTranspose2d parameter holders so utils.py:47-84
+``initialize_params`` still finds them). Forward passes run the fused
+kernels of csrc/cconv.hip and csrc/cbn.hip; the holders' own forward is never
+called.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import functional as F
+
+
+# ----------------------------------------------------------- layout helpers
+def split_complex(x, dim=1):
+    """complex_nn.py:18-30."""
+    if isinstance(x, (tuple, list)):
+        real, imag = x
+        return real, imag
+    if torch.is_complex(x):
+        return x.real, x.imag
+    if isinstance(x, torch.Tensor):
+        return torch.chunk(x, 2, dim=dim)
+    raise ValueError("Input must be a complex tensor or a tuple of real and imaginary tensors")
+
+
+def merge_real_imag(x, real, imag, dim=1):
+    """complex_nn.py:32-42: output in the container kind of x."""
+    if isinstance(x, (tuple, list)):
+        return [real, imag]
+    if torch.is_complex(x):
+        return torch.complex(real, imag)
+    return torch.cat([real, imag], dim=dim)
+
+
+def complex_concat(inputs, dim=1):
+    """complex_nn.py:4-16: concat real halves, then imag halves."""
+    halves = [torch.chunk(t, 2, dim=dim) for t in inputs]
+    return torch.cat([h[0] for h in halves] + [h[1] for h in halves], dim=dim)
+
+
+def _stacked(x):
+    """(stacked tensor, rebuild fn) for any of the reference's complex containers."""
+    if isinstance(x, (tuple, list)):
+        return torch.cat([x[0], x[1]], dim=1), lambda y: list(torch.chunk(y, 2, dim=1))
+    if torch.is_complex(x):
+        return torch.cat([x.real, x.imag], dim=1), lambda y: torch.complex(*torch.chunk(y, 2, dim=1))
+    return x, lambda y: y
+
+
+def _check_even(n, what):
+    assert n % 2 == 0, f"{what} must be a factor of 2, current channels: {n}"
+    return n // 2
+
+
+# ---------------------------------------------------------------- conv ops
+class _FusedComplexConv(nn.Module):
+    """Shared forward of ComplexConv2d / ComplexConvTranspose2d
+    (complex_nn.py:44-65): one GEMM against the block weight instead of four
+    real convs + sub/add/cat."""
+
+    transposed = False
+
+    def _geometry(self):
+        c = self.real_conv
+        if c.groups != 1:
+            raise NotImplementedError("sehip complex conv: groups != 1")
+        if getattr(c, "padding_mode", "zeros") != "zeros":
+            raise NotImplementedError("sehip complex conv: padding_mode must be 'zeros'")
+        if isinstance(c.padding, str):
+            raise NotImplementedError("sehip complex conv: string padding")
+        return c
+
+    def forward(self, x):
+        xs, rebuild = _stacked(x)
+        c = self._geometry()
+        y = F.conv2d(xs, c.weight, self.imag_conv.weight, c.bias, self.imag_conv.bias,
+                     out_channels=2 * c.out_channels, kernel=c.kernel_size, stride=c.stride,
+                     padding=c.padding, dilation=c.dilation,
+                     output_padding=getattr(c, "output_padding", (0, 0)),
+                     transposed=self.transposed)
+        return rebuild(y)
+
+
+class ComplexConv2d(_FusedComplexConv):
+    """complex_nn.py:67-78."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, **kwargs):
+        super().__init__()
+        cin = _check_even(in_channels, "in_channels")
+        cout = _check_even(out_channels, "out_channels")
+        self.real_conv = nn.Conv2d(cin, cout, kernel_size, **kwargs)
+        self.imag_conv = nn.Conv2d(cin, cout, kernel_size, **kwargs)
+
+
+class ComplexConvTranspose2d(_FusedComplexConv):
+    """complex_nn.py:80-91."""
+
+    transposed = True
+
+    def __init__(self, in_channels, out_channels, kernel_size, **kwargs):
+        super().__init__()
+        cin = _check_even(in_channels, "in_channels")
+        cout = _check_even(out_channels, "out_channels")
+        self.real_conv = nn.ConvTranspose2d(cin, cout, kernel_size, **kwargs)
+        self.imag_conv = nn.ConvTranspose2d(cin, cout, kernel_size, **kwargs)
+
+
+def real_conv2d(conv: nn.Module, x):
+    """A plain nn.Conv2d / nn.ConvTranspose2d evaluated by the same HIP GEMM
+    (e.g. FRCRN's real final_conv, frcrn.py:115)."""
+    tr = isinstance(conv, nn.ConvTranspose2d)
+    if conv.groups != 1 or isinstance(conv.padding, str):
+        raise NotImplementedError("sehip real conv: groups / string padding")
+    return F.conv2d(x, conv.weight, None, conv.bias, None, out_channels=conv.out_channels,
+                    kernel=conv.kernel_size, stride=conv.stride, padding=conv.padding,
+                    dilation=conv.dilation, output_padding=getattr(conv, "output_padding", (0, 0)),
+                    transposed=tr)
+
+
+# ------------------------------------------------------------- linear / LSTM
+class ComplexLinear(nn.Module):
+    """complex_nn.py:93-113 (separate real / imag linears, no cross terms)."""
+
+    def __init__(self, in_channels, out_channels, **kwargs):
+        super().__init__()
+        cin = _check_even(in_channels, "in_channels")
+        cout = _check_even(out_channels, "out_channels")
+        self.real_linear = nn.Linear(cin, cout, **kwargs)
+        self.imag_linear = nn.Linear(cin, cout, **kwargs)
+
+    def forward(self, x):
+        re, im = split_complex(x, dim=-1)
+        return merge_real_imag(x, self.real_linear(re), self.imag_linear(im), dim=-1)
+
+
+class ComplexLSTM(nn.Module):
+    """complex_nn.py:115-145. The reference makes four LSTM calls; the real
+    and imaginary inputs are independent sequences through the SAME weights,
+    so each nn.LSTM runs once over both stacked on the batch axis (2 calls,
+    identical math, half the sequential launches)."""
+
+    def __init__(self, in_channels, hidden_channels, **kwargs):
+        super().__init__()
+        cin = _check_even(in_channels, "in_channels")
+        hid = _check_even(hidden_channels, "hidden_channels")
+        self.real_lstm = nn.LSTM(cin, hid, **kwargs)
+        self.imag_lstm = nn.LSTM(cin, hid, **kwargs)
+        self._bdim = 0 if kwargs.get("batch_first", False) else 1
+
+    def forward(self, x):
+        re, im = split_complex(x, dim=-1)
+        both = torch.cat([re, im], dim=self._bdim)
+        r_out = self.real_lstm(both)[0]
+        i_out = self.imag_lstm(both)[0]
+        rr, ir = torch.chunk(r_out, 2, dim=self._bdim)     # real_lstm(re), real_lstm(im)
+        ri, ii = torch.chunk(i_out, 2, dim=self._bdim)     # imag_lstm(re), imag_lstm(im)
+        return merge_real_imag(x, rr - ii, ri + ir, dim=-1)
+
+    def flatten_parameters(self):
+        self.real_lstm.flatten_parameters()
+        self.imag_lstm.flatten_parameters()
+
+
+# ------------------------------------------------------------- batch norm
+class ComplexBatchNorm2d(nn.Module):
+    """complex_nn.py:148-329 — whitening complex BN on the HIP kernels."""
+
+    def __init__(self, num_features, eps=1e-5, momentum=0.1, affine=True,
+                 track_running_stats=True, complex_axis=1):
+        super().__init__()
+        if complex_axis != 1:
+            raise NotImplementedError("sehip ComplexBatchNorm2d: complex_axis must be 1")
+        self.num_features = num_features // 2
+        self.eps, self.momentum, self.affine = eps, momentum, affine
+        self.track_running_stats, self.complex_axis = track_running_stats, complex_axis
+        c = self.num_features
+        for name in ("Wrr", "Wri", "Wii", "Br", "Bi"):
+            if affine:
+                setattr(self, name, nn.Parameter(torch.empty(c)))
+            else:
+                self.register_parameter(name, None)
+        if track_running_stats:
+            self.register_buffer("RMr", torch.zeros(c))
+            self.register_buffer("RMi", torch.zeros(c))
+            self.register_buffer("RVrr", torch.ones(c))
+            self.register_buffer("RVri", torch.zeros(c))
+            self.register_buffer("RVii", torch.ones(c))
+            self.register_buffer("num_batches_tracked", torch.tensor(0, dtype=torch.long))
+        else:
+            for name in ("RMr", "RMi", "RVrr", "RVri", "RVii", "num_batches_tracked"):
+                self.register_parameter(name, None)
+        self.reset_parameters()
+
+    def reset_running_stats(self):
+        if self.track_running_stats:
+            self.RMr.zero_(); self.RMi.zero_(); self.RVri.zero_()
+            self.RVrr.fill_(1); self.RVii.fill_(1)
+            self.num_batches_tracked.zero_()
+
+    def reset_parameters(self):                               # complex_nn.py:202-209
+        self.reset_running_stats()
+        if self.affine:
+            with torch.no_grad():
+                self.Br.zero_(); self.Bi.zero_()
+                self.Wrr.fill_(1); self.Wii.fill_(1)
+                self.Wri.uniform_(-.9, +.9)
+
+    def forward_act(self, x, act=F.ACT_NONE, slope=0.0):
+        """BN followed by a fused activation (LeakyReLU / ReLU)."""
+        running = (self.RMr, self.RMi, self.RVrr, self.RVri, self.RVii) if self.track_running_stats else None
+        training = self.training or not self.track_running_stats    # complex_nn.py:234
+        return F.complex_batch_norm(
+            x, self.Wrr, self.Wri, self.Wii, self.Br, self.Bi, running,
+            self.num_batches_tracked if self.track_running_stats else None,
+            training, self.eps, self.momentum, act, slope)
+
+    def forward(self, inputs):
+        return self.forward_act(inputs)
+
+    def extra_repr(self):
+        return ("{num_features}, eps={eps}, momentum={momentum}, affine={affine}, "
+                "track_running_stats={track_running_stats}".format(**self.__dict__))
+
+
+def norm_act(norm: nn.Module, act: nn.Module, x):
+    """act(norm(x)) with the activation fused into the CBN kernel when both are
+    the kinds the kernel knows; otherwise the two modules are applied in turn."""
+    if isinstance(norm, ComplexBatchNorm2d):
+        if isinstance(act, nn.LeakyReLU):
+            return norm.forward_act(x, F.ACT_LEAKY, act.negative_slope)
+        if isinstance(act, nn.ReLU):
+            return norm.forward_act(x, F.ACT_RELU, 0.0)
+        if isinstance(act, nn.Identity):
+            return norm.forward_act(x)
+    return act(norm(x))
+
+
+class ComplexPReLU(nn.Module):
+    """complex_nn.py:337-357."""
+
+    def __init__(self, **kwargs):
+        super().__init__()
+        self.real_prelu = nn.PReLU(**kwargs)
+        self.imag_prelu = nn.PReLU(**kwargs)
+
+    def forward(self, x):
+        re, im = split_complex(x, dim=1)
+        out_re = self.real_prelu(re) - self.imag_prelu(im)
+        out_im = self.imag_prelu(re) + self.real_prelu(im)
+        return merge_real_imag(x, out_re, out_im, dim=1)
+
+
+ComplexReLU = nn.ReLU            # complex_nn.py:359
+ComplexLeakyReLU = nn.LeakyReLU  # complex_nn.py:360

@@ -91,3 +91,127 @@ def conv2d(x, wr, wi=None, br=None, bi=None, *, out_channels, kernel, stride=1, 
     geom = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
             _pair(output_padding), bool(transposed), wi is not None)
     return _Conv2d.apply(x, wr, wi, br, bi, geom)
+
+
+# --------------------------------------------------------------------------
+# ComplexBatchNorm2d (+ fused activation) — se_cbn_* (cbn.hip)
+# --------------------------------------------------------------------------
+ACT_NONE, ACT_LEAKY, ACT_RELU = 0, 1, 2
+
+
+class _ComplexBN(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum, act, slope):
+        N.require_device(x, wrr)
+        x = x.contiguous()
+        b, c = x.shape[:2]
+        hw = x[0, 0].numel()
+        y = torch.empty_like(x)
+        save = torch.empty(16 * (c // 2), device=x.device, dtype=torch.float32)
+        params = (wrr, wri, wii, br, bi) if wrr is not None else None
+        lib = N.lib()
+        ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
+        mom = -1.0 if momentum is None else float(momentum)
+        N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
+                               N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
+                               save.data_ptr(), int(training), float(eps), mom, int(act),
+                               float(slope), ws.data_ptr(), ws.numel(), N.stream_of(x)),
+                "se_cbn_fwd")
+        ctx.save_for_backward(x, y, save, *(params or ()))
+        ctx.cfg = (int(training), int(act), float(slope), params is not None)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, y, save, *params = ctx.saved_tensors
+        training, act, slope, affine = ctx.cfg
+        gy = gy.contiguous()
+        b, c = x.shape[:2]
+        hw = x[0, 0].numel()
+        dx = torch.empty_like(x)
+        dparams = [torch.empty_like(p) for p in params] if affine else None
+        lib = N.lib()
+        ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
+        N.check(lib.se_cbn_bwd(gy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(), b, c, hw,
+                               N.ptr_array(params if affine else None), save.data_ptr(),
+                               N.ptr_array(dparams), training, act, slope, ws.data_ptr(),
+                               ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
+        g = dparams or [None] * 5
+        return (dx, *g, None, None, None, None, None, None, None)
+
+
+def complex_batch_norm(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
+                       act=ACT_NONE, slope=0.0):
+    """ComplexBatchNorm2d forward (+ optional fused activation) on the HIP path.
+    running: (RMr, RMi, RVrr, RVri, RVii) or None; nbt: int64 tensor or None."""
+    return _ComplexBN.apply(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
+                            act, slope)
+
+
+# --------------------------------------------------------------------------
+# ConvSTFT / ConviSTFT — se_stft_* / se_istft_* (stft.hip)
+# --------------------------------------------------------------------------
+class _Stft(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, window, twiddle, win, hop, nfft, center, mag_phase):
+        N.require_device(x, window, twiddle)
+        x = x.contiguous()
+        b, length = x.shape
+        lib = N.lib()
+        t = lib.se_stft_num_frames(length, win, hop, nfft, int(center))
+        if t <= 0:
+            raise RuntimeError(f"sehip ConvSTFT: input of length {length} too short for window {win}")
+        half = nfft // 2 + 1
+        if mag_phase:
+            out0 = torch.empty((b, half, t), device=x.device, dtype=x.dtype)
+            out1 = torch.empty_like(out0)
+        else:
+            out0 = torch.empty((b, 2 * half, t), device=x.device, dtype=x.dtype)
+            out1 = None
+        N.check(lib.se_stft_fwd(x.data_ptr(), out0.data_ptr(), N.ptr(out1), b, length, win, hop, nfft,
+                                int(center), int(mag_phase), window.data_ptr(), twiddle.data_ptr(),
+                                N.stream_of(x)), "se_stft_fwd")
+        return (out0, out1) if mag_phase else out0
+
+    @staticmethod
+    def backward(ctx, *grads):
+        raise NotImplementedError("sehip ConvSTFT has no input gradient (the reference's basis "
+                                  "is a fixed buffer and the training input carries no grad)")
+
+
+def stft(x, window, twiddle, win, hop, nfft, center=True, mag_phase=False):
+    """x: [B, L] -> spec [B, nfft+2, T] (or (mags, phase) [B, nfft/2+1, T])."""
+    return _Stft.apply(x, window, twiddle, win, hop, nfft, center, mag_phase)
+
+
+class _Istft(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, spec, window, twiddle, win, hop, nfft, offset, out_len):
+        N.require_device(spec, window, twiddle)
+        spec = spec.contiguous()
+        b, rows, t = spec.shape
+        if rows != nfft + 2:
+            raise RuntimeError(f"sehip ConviSTFT: expected {nfft + 2} spectrum rows, got {rows}")
+        out = torch.empty((b, out_len), device=spec.device, dtype=spec.dtype)
+        N.check(N.lib().se_istft_fwd(spec.data_ptr(), out.data_ptr(), b, t, win, hop, nfft, offset,
+                                     out_len, window.data_ptr(), twiddle.data_ptr(),
+                                     N.stream_of(spec)), "se_istft_fwd")
+        ctx.save_for_backward(window, twiddle)
+        ctx.cfg = (b, t, win, hop, nfft, offset, out_len)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        window, twiddle = ctx.saved_tensors
+        b, t, win, hop, nfft, offset, out_len = ctx.cfg
+        gout = gout.contiguous()
+        gspec = torch.empty((b, nfft + 2, t), device=gout.device, dtype=gout.dtype)
+        N.check(N.lib().se_istft_bwd(gout.data_ptr(), gspec.data_ptr(), b, t, win, hop, nfft,
+                                     offset, out_len, window.data_ptr(), twiddle.data_ptr(),
+                                     N.stream_of(gout)), "se_istft_bwd")
+        return gspec, None, None, None, None, None, None, None
+
+
+def istft(spec, window, twiddle, win, hop, nfft, offset, out_len):
+    """spec [B, nfft+2, T] -> wav [B, out_len] = full OLA signal[offset:offset+out_len]."""
+    return _Istft.apply(spec, window, twiddle, win, hop, nfft, offset, out_len)

@@ -1,0 +1,148 @@
+"""FRCRN on the HIP path (drop-in for models/_2206_07293_frcrn.py).
+
+Constructor signature, module tree and state_dict keys (279 entries) match
+the reference. The spectral front/back end (ConvSTFT/ConviSTFT), every
+complex conv / transposed conv, every ComplexBatchNorm2d (+ fused
+LeakyReLU) and the real final_conv run on csrc/*.hip kernels; LSTM, CCBAM
+pooling, pads/concats and the tanh mask are PyTorch device ops.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as TF
+
+from ..ccbam import CCBAM
+from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLSTM,
+                          complex_concat, norm_act, real_conv2d)
+from ..conv_stft import ConvSTFT, ConviSTFT
+
+
+class _CausalConvBase(nn.Module):
+    """frcrn.py:11-59: left-pad time by padding[1] ('causal') or both sides,
+    then (transposed) conv -> norm -> act."""
+
+    conv_attr = "conv"
+
+    def _conv(self):
+        return getattr(self, self.conv_attr)
+
+    def forward(self, x):
+        lp = self.padding[1]
+        x = TF.pad(x, (lp, 0 if self.causal else lp, 0, 0))
+        conv = self._conv()
+        y = conv(x) if not isinstance(conv, (nn.Conv2d, nn.ConvTranspose2d)) else real_conv2d(conv, x)
+        return norm_act(self.norm, self.act, y)
+
+
+def _make_block(block, transposed, in_channels, out_channels, kernel_size, padding, norm, act,
+                causal, is_complex, kwargs):
+    block.causal, block.padding = causal, padding
+    slope = kwargs.pop("negative_slope", 0.2)
+    if is_complex:
+        conv_cls = ComplexConvTranspose2d if transposed else ComplexConv2d
+        norm_m = ComplexBatchNorm2d(out_channels) if norm else nn.Identity()
+    else:
+        conv_cls = nn.ConvTranspose2d if transposed else nn.Conv2d
+        norm_m = nn.BatchNorm2d(out_channels) if norm else nn.Identity()
+    setattr(block, block.conv_attr, conv_cls(in_channels, out_channels, kernel_size,
+                                             padding=(padding[0], 0), bias=not norm, **kwargs))
+    block.norm = norm_m
+    block.act = nn.LeakyReLU(slope) if act else nn.Identity()
+
+
+class ConvBlock(_CausalConvBase):
+    """frcrn.py:11-34."""
+
+    def __init__(self, in_channels, out_channels, kernel_size, padding=(0, 0), norm=True, act=True,
+                 causal=True, is_complex=True, **kwargs):
+        super().__init__()
+        _make_block(self, False, in_channels, out_channels, kernel_size, padding, norm, act, causal,
+                    is_complex, kwargs)
+
+
+class ConvTransposeBlock(_CausalConvBase):
+    """frcrn.py:36-59."""
+
+    conv_attr = "conv_transposed"
+
+    def __init__(self, in_channels, out_channels, kernel_size, padding=(0, 0), norm=True, act=True,
+                 causal=True, is_complex=True, **kwargs):
+        super().__init__()
+        _make_block(self, True, in_channels, out_channels, kernel_size, padding, norm, act, causal,
+                    is_complex, kwargs)
+
+
+class Encoder(nn.Module):
+    """frcrn.py:62-76: six (5,2)/(2,1) causal complex conv blocks."""
+
+    def __init__(self, in_channels=1, out_channels=128, num_repeats=6, is_complex=True):
+        super().__init__()
+        chans = [in_channels] + [out_channels] * num_repeats
+        self.layers = nn.ModuleList(
+            ConvBlock(chans[i], chans[i + 1], kernel_size=(5, 2), stride=(2, 1), padding=(0, 1),
+                      causal=True, is_complex=is_complex) for i in range(num_repeats))
+
+    def forward(self, x):
+        skips = []
+        for layer in self.layers:
+            x = layer(x)
+            skips.append(x)
+        return x, skips
+
+
+class Decoder(nn.Module):
+    """frcrn.py:78-102: CCBAM on each skip, align, complex concat, convT block."""
+
+    def __init__(self, in_channels=128, out_channels=128, num_repeats=6, reduction_ratio=16,
+                 is_complex=True):
+        super().__init__()
+        self.skip_connection_attention_layers = nn.ModuleList()
+        self.layers = nn.ModuleList()
+        c = in_channels
+        for _ in range(num_repeats):
+            self.skip_connection_attention_layers.append(CCBAM(c, reduction_ratio))
+            self.layers.append(ConvTransposeBlock(2 * c, out_channels, kernel_size=(5, 2), stride=(2, 1),
+                                                  padding=(0, 0), causal=True, is_complex=is_complex))
+            c = out_channels
+
+    def forward(self, x, encoder_outputs):
+        for attention, layer in zip(self.skip_connection_attention_layers, self.layers):
+            skip = attention(encoder_outputs.pop())
+            if x.shape[-1] > skip.shape[-1]:          # frcrn.py:95-96
+                x = x[..., :-1]
+            if x.shape[-2] < skip.shape[-2]:          # frcrn.py:97-98
+                x = TF.pad(x, (0, 0, 0, 1))
+            x = layer(complex_concat([x, skip], dim=1))
+        return x
+
+
+class FRCRN(nn.Module):
+    """frcrn.py:104-155."""
+
+    def __init__(self, window_size=320, hop_size=160, fft_size=640, lstm_channels=256,
+                 reduction_ratio=16, is_complex=True):
+        super().__init__()
+        self.stft = ConvSTFT(window_size, hop_size, fft_size)
+        self.istft = ConviSTFT(window_size, hop_size, fft_size)
+        self.encoder = Encoder(in_channels=2, out_channels=128, is_complex=is_complex)
+        self.decoder = Decoder(in_channels=128, out_channels=128, is_complex=is_complex,
+                               reduction_ratio=reduction_ratio)
+        self.lstm = ComplexLSTM(256, lstm_channels, num_layers=2, bidirectional=False, batch_first=True)
+        self.final_conv = nn.Conv2d(128, 2, kernel_size=(1, 2), bias=False)
+        self.fft_size = fft_size
+
+    def forward(self, x):
+        half = self.fft_size // 2 + 1
+        spec = self.stft(x)                                            # [B, N+2, T]
+        noisy = spec.view(spec.shape[0], 2, half, spec.shape[-1])[:, :, 1:]   # drop DC (:123-127)
+        h, skips = self.encoder(noisy.contiguous())
+        b, c, f, t = h.shape                                           # :133-137
+        h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2))
+        h = h.transpose(1, 2).reshape(b, c, f, t)
+        h = self.decoder(h, skips)
+        mask = torch.tanh(TF.pad(real_conv2d(self.final_conv, h), (0, 0, 1, 0)))   # :140-144
+        est = TF.pad(mask * noisy, (0, 0, 1, 0))                       # :145-146 (DC back as 0)
+        est = est.reshape(b, 2 * half, est.shape[-1])                  # cat(re, im) on dim 1 (:149-152)
+        wav = self.istft(est)
+        return est, torch.clamp_(wav, -1, 1)                           # :153-155
