@@ -1,0 +1,174 @@
+#!/usr/bin/env python3
+"""FRCRN training throughput on MI355X — BASELINE.json's metric.
+
+One step = one FRCRN training iteration (trainer.py:99-124 + 210-221:
+forward, SI-SNR, backward, clip_grad_norm_(0.5), AdamW) on 64 synthetic
+4 s @ 16 kHz noisy/clean pairs per GPU, inputs resident in HBM.
+fp32 throughout (the reference's precision; parity is judged at 1e-4 fp32).
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Rank 0 prints ONE JSON line. `value` = utterances processed by all ranks
+during the K timed steps / max-over-ranks wall time. `roofline` is measured
+live with HIP events around the complex-conv GEMM entry points during the
+timed region; `cpu_baseline` times the oracle (the pure-PyTorch CPU port)
+on a bounded sample of the same workload.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "speech-enhancement_amd"))
+
+import torch  # noqa: E402
+
+METRIC = "utterances/sec (4s@16kHz) FRCRN train at 1/2/4/8 MI355X"
+FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-in MFMA dense peak
+HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
+SR, SECONDS = 16000, 4
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--batch", type=int, default=64, help="utterances per GPU")
+    ap.add_argument("--cpu-steps", type=int, default=2)
+    ap.add_argument("--cpu-batch", type=int, default=4)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-op-timing", action="store_true")
+    return ap.parse_args()
+
+
+def cpu_baseline(batch, steps):
+    """Oracle (pure-PyTorch CPU restatement of the reference, pinned by the
+    golden fixtures) timed on this box's host cores: a bounded sample."""
+    sys.path.insert(0, ROOT)
+    from oracle import models as O, train as OT
+    from sehip.data import synthetic_pairs
+    threads = torch.get_num_threads()
+    noisy, clean = synthetic_pairs(batch, SR * SECONDS, seed=99, device="cpu")
+    m = O.FRCRN().train()
+    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-2)
+    OT.train_step(m, opt, noisy, clean)                     # warm-up
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        OT.train_step(m, opt, noisy, clean)
+    dt = time.perf_counter() - t0
+    return {"value": batch * steps / dt, "unit": "utterances/sec", "cores": threads, "kind": "port",
+            "sample": f"{steps} oracle FRCRN train steps (fwd+SI-SNR+bwd+clip+AdamW, fp32, "
+                      f"B={batch} x 4 s @ 16 kHz) after 1 warm-up step, torch CPU, {threads} threads",
+            "seconds": dt}
+
+
+def main():
+    args = parse()
+    from sehip import functional as SF
+    from sehip.data import synthetic_pairs
+    from sehip.models import FRCRN
+    from sehip.train import make_optimizer, setup_distributed, train_step, wrap_ddp
+
+    rank, world, local, device = setup_distributed()
+    if device.type != "cuda":
+        raise SystemExit("bench.py needs a GPU")
+    torch.manual_seed(2023 + rank)
+    model = FRCRN().to(device).train()
+    model = wrap_ddp(model, device)
+    opt = make_optimizer(model)
+    B, L = args.batch, SR * SECONDS
+    batches = [synthetic_pairs(B, L, seed=2023 + rank * 1_000_003 + i, device=device) for i in range(2)]
+
+    for i in range(args.warmup):
+        noisy, clean = batches[i % 2]
+        train_step(model, opt, noisy, clean)
+    torch.cuda.synchronize()
+
+    timer = None if args.no_op_timing else SF.OpTimer()
+    dist = torch.distributed if (world > 1 and torch.distributed.is_initialized()) else None
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    SF.set_op_timer(timer)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        noisy, clean = batches[i % 2]
+        loss = train_step(model, opt, noisy, clean)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    SF.set_op_timer(None)
+    if dist:
+        t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    loss_v = float(loss)
+    kern = timer.summary() if timer else {}
+
+    if rank != 0:
+        return
+    value = world * B * args.steps / elapsed
+    out = {
+        "metric": METRIC, "value": round(value, 3), "unit": "utterances/sec", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "data": "synthetic: on-device 4 s @ 16 kHz harmonic+AM clean / Gaussian-noise pairs at "
+                "SNR U{-5..20} dB, random-init FRCRN (no datasets/checkpoints offline)",
+        "config": {"workload": "FRCRN train step: fwd + SI-SNR + bwd + clip_grad_norm 0.5 + AdamW "
+                               "(320/160/640 STFT, 4 s @ 16 kHz)",
+                   "per_gpu_batch": B, "global_batch": B * world, "seq_len": L,
+                   "parallelism": f"dp{world}"},
+        "final_loss": round(loss_v, 4),
+    }
+    if kern:
+        g = kern.get("conv_gather_gemm")
+        if g:
+            ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
+            out["roofline"] = {
+                "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
+                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
+                "traffic": _pmc_traffic("gather_gemm_kernel"),
+                "kernel": "gather_gemm_kernel (se_conv2d_fwd + se_conv2d_bwd_data, fp32 MFMA 32x32x2)",
+                "launch_calls": g["calls"], "avg_ms_per_call": round(g["ms"] / g["calls"], 4),
+                "algorithmic_flops_per_call": g["flops"] / g["calls"]}
+        st = kern.get("stft_fwd")
+        if st:
+            gbs = st["bytes"] / (st["ms"] * 1e-3) / 1e9
+            out["stft_roofline"] = {
+                "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("stft_fwd_kernel"),
+                "kernel": "stft_fwd_kernel (se_stft_fwd)",
+                "avg_ms_per_call": round(st["ms"] / st["calls"], 4),
+                "algorithmic_bytes_per_call": st["bytes"] / st["calls"]}
+        out["op_breakdown"] = {
+            k: {"calls": v["calls"], "ms_per_step": round(v["ms"] / args.steps, 3),
+                **({"tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {}),
+                **({"gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} if v["bytes"] else {})}
+            for k, v in kern.items()}
+        total_conv = sum(v["flops"] for k, v in kern.items() if k.startswith("conv"))
+        out["conv_flops_per_utt"] = total_conv / (B * args.steps)
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_steps)
+    print(json.dumps(out), flush=True)
+
+
+def _pmc_traffic(kernel):
+    """HBM bytes per launch from the committed PMC summary (tools/pmc_summary.py
+    -> profiles/pmc_traffic.json), or None when not collected."""
+    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    try:
+        with open(path) as f:
+            return json.load(f).get(kernel, {}).get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        return None
+
+
+if __name__ == "__main__":
+    main()

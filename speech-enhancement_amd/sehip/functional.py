@@ -19,6 +19,56 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
 
 
+class OpTimer:
+    """Live per-entry-point timing with HIP events on the launching stream
+    (used by bench.py for the roofline numbers). Disabled unless installed
+    with set_op_timer(); then every C-ABI call in this module is bracketed by
+    two events and tagged with its algorithmic FLOPs and bytes."""
+
+    def __init__(self):
+        self.records = []   # (tag, start_event, end_event, flops, bytes)
+
+    def begin(self):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        return ev
+
+    def end(self, tag, start, flops=0.0, nbytes=0.0):
+        ev = torch.cuda.Event(enable_timing=True)
+        ev.record()
+        self.records.append((tag, start, ev, float(flops), float(nbytes)))
+
+    def summary(self):
+        torch.cuda.synchronize()
+        out = {}
+        for tag, a, b, fl, nb in self.records:
+            d = out.setdefault(tag, dict(calls=0, ms=0.0, flops=0.0, bytes=0.0))
+            d["calls"] += 1
+            d["ms"] += a.elapsed_time(b)
+            d["flops"] += fl
+            d["bytes"] += nb
+        return out
+
+
+_TIMER: OpTimer | None = None
+
+
+def set_op_timer(t: OpTimer | None):
+    global _TIMER
+    _TIMER = t
+
+
+def _conv_flops(d) -> float:
+    """Algorithmic FLOPs of one pass (= torch FlopCounterMode's conv formula:
+    2 * positions * Cin * Cout * kh * kw over the conv's (input for convT,
+    output for conv) grid). The fused complex conv does the work of the
+    reference's four real convs of Cin/2 x Cout/2 channels exactly."""
+    ho, wo = N.c_int(), N.c_int()
+    N.lib().se_conv2d_out_shape(N.ctypes.byref(d), N.ctypes.byref(ho), N.ctypes.byref(wo))
+    grid = (d.in_h * d.in_w) if d.transposed else (ho.value * wo.value)
+    return 2.0 * d.batch * grid * d.in_channels * d.out_channels * d.kernel_h * d.kernel_w
+
+
 # --------------------------------------------------------------------------
 # Complex / real (transposed) conv2d — se_conv2d_* (cconv.hip)
 # --------------------------------------------------------------------------
@@ -52,9 +102,12 @@ class _Conv2d(torch.autograd.Function):
         y = torch.empty((x.shape[0], out_channels, ho.value, wo.value), device=x.device, dtype=x.dtype)
         nbytes = lib.se_conv2d_workspace_size(N.ctypes.byref(d))
         ws = _workspace(nbytes, x.device)
+        t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_conv2d_fwd(N.ctypes.byref(d), x.data_ptr(), wr.data_ptr(), N.ptr(wi),
                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(),
                                   N.stream_of(x)), "se_conv2d_fwd")
+        if t0 is not None:
+            _TIMER.end("conv_gather_gemm", t0, _conv_flops(d))
         ctx.save_for_backward(x, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias = d, nbytes, br is not None
         return y
@@ -68,9 +121,12 @@ class _Conv2d(torch.autograd.Function):
         dx = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
+            t0 = _TIMER.begin() if _TIMER else None
             N.check(lib.se_conv2d_bwd_data(N.ctypes.byref(d), gy.data_ptr(), wr.data_ptr(), N.ptr(wi),
                                            dx.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(gy)),
                     "se_conv2d_bwd_data")
+            if t0 is not None:
+                _TIMER.end("conv_gather_gemm", t0, _conv_flops(d))
         if any(ctx.needs_input_grad[1:5]):
             dwr = torch.empty_like(wr)
             dwi = torch.empty_like(wi) if wi is not None else None
@@ -78,10 +134,13 @@ class _Conv2d(torch.autograd.Function):
                 nb = d.out_channels // 2 if d.complex_weights else d.out_channels
                 dbr = torch.empty(nb, device=gy.device, dtype=gy.dtype)
                 dbi = torch.empty(nb, device=gy.device, dtype=gy.dtype) if d.complex_weights else None
+            t0 = _TIMER.begin() if _TIMER else None
             N.check(lib.se_conv2d_bwd_weight(N.ctypes.byref(d), x.data_ptr(), gy.data_ptr(),
                                              dwr.data_ptr(), N.ptr(dwi), N.ptr(dbr), N.ptr(dbi),
                                              ws.data_ptr(), ws.numel(), N.stream_of(gy)),
                     "se_conv2d_bwd_weight")
+            if t0 is not None:
+                _TIMER.end("conv_wgrad_gemm", t0, _conv_flops(d))
         return dx, dwr, dwi, dbr, dbi, None
 
 
@@ -112,11 +171,14 @@ class _ComplexBN(torch.autograd.Function):
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
         mom = -1.0 if momentum is None else float(momentum)
+        t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
                                N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
                                save.data_ptr(), int(training), float(eps), mom, int(act),
                                float(slope), ws.data_ptr(), ws.numel(), N.stream_of(x)),
                 "se_cbn_fwd")
+        if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write
+            _TIMER.end("cbn_fwd", t0, 0.0, 4.0 * x.numel() * (3 if training else 2))
         ctx.save_for_backward(x, y, save, *(params or ()))
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         return y
@@ -132,10 +194,13 @@ class _ComplexBN(torch.autograd.Function):
         dparams = [torch.empty_like(p) for p in params] if affine else None
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
+        t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_cbn_bwd(gy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(), b, c, hw,
                                N.ptr_array(params if affine else None), save.data_ptr(),
                                N.ptr_array(dparams), training, act, slope, ws.data_ptr(),
                                ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
+        if t0 is not None:   # (gy, y, x) read twice + dx written
+            _TIMER.end("cbn_bwd", t0, 0.0, 4.0 * x.numel() * 7)
         g = dparams or [None] * 5
         return (dx, *g, None, None, None, None, None, None, None)
 
@@ -168,9 +233,12 @@ class _Stft(torch.autograd.Function):
         else:
             out0 = torch.empty((b, 2 * half, t), device=x.device, dtype=x.dtype)
             out1 = None
+        t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_stft_fwd(x.data_ptr(), out0.data_ptr(), N.ptr(out1), b, length, win, hop, nfft,
                                 int(center), int(mag_phase), window.data_ptr(), twiddle.data_ptr(),
                                 N.stream_of(x)), "se_stft_fwd")
+        if t0 is not None:   # algorithmic bytes: read the wav once, write the spectrum once
+            _TIMER.end("stft_fwd", t0, 0.0, 4.0 * (x.numel() + out0.numel() + (out1.numel() if mag_phase else 0)))
         return (out0, out1) if mag_phase else out0
 
     @staticmethod
@@ -193,9 +261,12 @@ class _Istft(torch.autograd.Function):
         if rows != nfft + 2:
             raise RuntimeError(f"sehip ConviSTFT: expected {nfft + 2} spectrum rows, got {rows}")
         out = torch.empty((b, out_len), device=spec.device, dtype=spec.dtype)
+        t0 = _TIMER.begin() if _TIMER else None
         N.check(N.lib().se_istft_fwd(spec.data_ptr(), out.data_ptr(), b, t, win, hop, nfft, offset,
                                      out_len, window.data_ptr(), twiddle.data_ptr(),
                                      N.stream_of(spec)), "se_istft_fwd")
+        if t0 is not None:
+            _TIMER.end("istft_fwd", t0, 0.0, 4.0 * (spec.numel() + out.numel()))
         ctx.save_for_backward(window, twiddle)
         ctx.cfg = (b, t, win, hop, nfft, offset, out_len)
         return out
@@ -206,9 +277,12 @@ class _Istft(torch.autograd.Function):
         b, t, win, hop, nfft, offset, out_len = ctx.cfg
         gout = gout.contiguous()
         gspec = torch.empty((b, nfft + 2, t), device=gout.device, dtype=gout.dtype)
+        t0 = _TIMER.begin() if _TIMER else None
         N.check(N.lib().se_istft_bwd(gout.data_ptr(), gspec.data_ptr(), b, t, win, hop, nfft,
                                      offset, out_len, window.data_ptr(), twiddle.data_ptr(),
                                      N.stream_of(gout)), "se_istft_bwd")
+        if t0 is not None:
+            _TIMER.end("istft_bwd", t0, 0.0, 4.0 * (gout.numel() + gspec.numel()))
         return gspec, None, None, None, None, None, None, None
 
 
