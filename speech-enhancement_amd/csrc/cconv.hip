@@ -70,7 +70,8 @@ gather_gemm_kernel(const GatherArgs a) {
   const long long HiWi = (long long)a.Hi * a.Wi;
 
   // --- this thread's gather column (fixed for the whole K loop) ---
-  const int am = tid % BM, akr = tid / BM;        // akr is wave-uniform
+  const int am = tid % BM;
+  const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // wave-uniform k row
   const int m = m0 + am;
   const bool mval = m < a.M;
   int hb = 0, wb = 0;
@@ -89,11 +90,13 @@ gather_gemm_kernel(const GatherArgs a) {
   auto load_tile = [&](int k0) {
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
-      const int k = __builtin_amdgcn_readfirstlane(k0 + akr + KR * j);
-      const int4 e = a.ktab[k];
+      const int4 e = a.ktab[k0 + akr + KR * j];        // uniform index -> s_load
       const int hi = hb + e.y, wi = wb + e.z;
-      const bool ok = mval && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
-      ra[j] = ok ? a.X[xbase + e.x] : 0.f;
+      const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      // unconditional load from a clamped address, then select: a predicated
+      // load makes hipcc branch around it and drain vmcnt(0) per element
+      const float v = a.X[ok ? xbase + e.x : 0];
+      ra[j] = ok ? v : 0.f;
     }
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
@@ -149,7 +152,14 @@ gather_gemm_kernel(const GatherArgs a) {
   }
 
   // --- epilogue: lane -> m (coalesced along time), registers -> n ---
+  float* sBias = &sW[0][0][0];                     // reuse the drained weight tile
+  for (int i = tid; i < BN; i += kThreads) {
+    const int n = n0 + i;
+    sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+  }
+  __syncthreads();
   const long long HoWo = (long long)a.Ho * a.Wo;
+  const bool full_n = n0 + BN <= a.N;
 #pragma unroll
   for (int j = 0; j < RM; ++j) {
     const int mm = m0 + wm * TM + 32 * j + lc;
@@ -157,18 +167,15 @@ gather_gemm_kernel(const GatherArgs a) {
     const int qhw = a.Qh * a.Qw;
     const int b = mm / qhw, r = mm - b * qhw;
     const int qh = r / a.Qw, qw = r - qh * a.Qw;
-    const long long ybase = (long long)b * a.N * HoWo +
-                            (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
+    const int nl0 = wn * TN + 4 * lk;               // this lane's first local row
+    float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
+                (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
 #pragma unroll
     for (int i = 0; i < RN; ++i)
 #pragma unroll
       for (int r2 = 0; r2 < 16; ++r2) {
-        const int n = n0 + wn * TN + 32 * i + (r2 & 3) + 8 * (r2 >> 2) + 4 * lk;
-        if (n < a.N) {
-          float v = acc[i][j][r2];
-          if (a.bias) v += a.bias[n];
-          a.Y[ybase + n * HoWo] = v;
-        }
+        const int nl = 32 * i + (r2 & 3) + 8 * (r2 >> 2);   // compile-time
+        if (full_n || n0 + nl0 + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
       }
   }
 }
@@ -198,11 +205,11 @@ gather_smalln_kernel(const GatherArgs a) {
   for (int k = 0; k < a.Kp; ++k) {
     const int4 e = a.ktab[k];
     const int hi = hb + e.y, wi = wb + e.z;
-    if ((unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi) {
-      const float x = a.X[xbase + e.x];
+    const bool ok = (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+    const float xv = a.X[ok ? xbase + e.x : 0];
+    const float x = ok ? xv : 0.f;
 #pragma unroll
-      for (int n = 0; n < NOUT; ++n) acc[n] = fmaf(x, sWs[k * NOUT + n], acc[n]);
-    }
+    for (int n = 0; n < NOUT; ++n) acc[n] = fmaf(x, sWs[k * NOUT + n], acc[n]);
   }
   const long long HoWo = (long long)a.Ho * a.Wo;
   const long long ybase = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
@@ -225,24 +232,28 @@ struct WgradArgs {
   int Cg, Hi, Wi;
   int N, Qh, Qw, sh, sw;
   int Kp, Np, M;
-  int m_per_split;     // multiple of BMR
+  int m_per_split;     // multiple of the kernel's BMR (64)
 };
 
-constexpr int kBMR = 64;   // m per reduction step (one wave-width of positions)
-
-template <int BKO, int BNO, int WK, int WNn>
+// One reduction step covers BMR consecutive positions m; a wave-instruction
+// loads LPW = 64 / BMR rows (k or n) x BMR positions, lanes along m so every
+// load is coalesced along the time axis.
+template <int BKO, int BNO, int WK, int WNn, int BMR>
 __global__ void __launch_bounds__(kThreads)
 wgrad_gemm_kernel(const WgradArgs a) {
   static_assert(WK * WNn == 4, "4 waves");
   constexpr int TK = BKO / WK, TN = BNO / WNn;
   constexpr int RK = TK / 32, RN = TN / 32;
-  constexpr int GJ = BKO / 4;      // G rows per wave per step (row = wave + 4j)
-  constexpr int DJ = BNO / 4;      // D rows per wave per step
-  constexpr int L = kBMR + 1;      // padded [row][m] images: conflict-free both ways
+  constexpr int LPW = 64 / BMR;            // rows per wave-instruction
+  constexpr int RS = 4 * LPW;              // rows covered by the workgroup per j
+  constexpr int GJ = BKO / RS, DJ = BNO / RS;
+  constexpr int L = BMR + 1;               // padded [row][m] images: conflict-free both ways
   __shared__ float sG[2][BKO * L];
   __shared__ float sD[2][BNO * L];
+  __shared__ int4 sK[BKO];
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = wave / WNn, wnn = wave % WNn;
   const int k0 = blockIdx.x * BKO, n0 = blockIdx.y * BNO;
   const int split = blockIdx.z;
@@ -250,11 +261,16 @@ wgrad_gemm_kernel(const WgradArgs a) {
   const int mend = min(a.M, mbeg + a.m_per_split);
   const long long HiWi = (long long)a.Hi * a.Wi;
   const long long QQ = (long long)a.Qh * a.Qw;
+  const int ml = lane % BMR, lr = lane / BMR;
+  const int row0 = wave * LPW + lr;        // + RS * j
 
-  // incremental decode of this lane's m = mbeg + lane + step*64
+  for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab[k0 + i];
+  __syncthreads();
+
+  // incremental decode of this lane's m = mbeg + ml + step*BMR
   int cb, cqh, cqw;
   {
-    const long long mm = mbeg + lane;
+    const long long mm = mbeg + ml;
     cb = (int)(mm / QQ);
     const int r = (int)(mm - cb * QQ);
     cqh = r / a.Qw;
@@ -262,23 +278,26 @@ wgrad_gemm_kernel(const WgradArgs a) {
   }
   float rg[GJ], rd[DJ];
   auto load_step = [&](int mstep) {
-    const bool mv = mstep + lane < mend;
+    const bool mv = mstep + ml < mend;
     const int hb = cqh * a.sh, wb = cqw * a.sw;
     const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
 #pragma unroll
     for (int j = 0; j < GJ; ++j) {
-      const int4 e = a.ktab[k0 + wave + 4 * j];          // wave-uniform -> scalar load
+      const int4 e = sK[row0 + RS * j];
       const int hi = hb + e.y, wi = wb + e.z;
-      const bool ok = mv && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
-      rg[j] = ok ? a.X[xb + e.x] : 0.f;
+      const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      const float v = a.X[ok ? xb + e.x : 0];
+      rg[j] = ok ? v : 0.f;
     }
     const long long db = (long long)cb * a.N * QQ + (long long)cqh * a.Qw + cqw;
 #pragma unroll
     for (int j = 0; j < DJ; ++j) {
-      const int n = n0 + wave + 4 * j;
-      rd[j] = (mv && n < a.N) ? a.D[db + (long long)n * QQ] : 0.f;
+      const int n = n0 + row0 + RS * j;
+      const bool ok = mv & (n < a.N);
+      const float v = a.D[ok ? db + (long long)n * QQ : 0];
+      rd[j] = ok ? v : 0.f;
     }
-    cqw += kBMR;
+    cqw += BMR;
     while (cqw >= a.Qw) {
       cqw -= a.Qw;
       if (++cqh >= a.Qh) { cqh = 0; ++cb; }
@@ -286,9 +305,9 @@ wgrad_gemm_kernel(const WgradArgs a) {
   };
   auto store_step = [&](int buf) {
 #pragma unroll
-    for (int j = 0; j < GJ; ++j) sG[buf][(wave + 4 * j) * L + lane] = rg[j];
+    for (int j = 0; j < GJ; ++j) sG[buf][(row0 + RS * j) * L + ml] = rg[j];
 #pragma unroll
-    for (int j = 0; j < DJ; ++j) sD[buf][(wave + 4 * j) * L + lane] = rd[j];
+    for (int j = 0; j < DJ; ++j) sD[buf][(row0 + RS * j) * L + ml] = rd[j];
   };
 
   f32x16 acc[RK][RN];
@@ -299,7 +318,7 @@ wgrad_gemm_kernel(const WgradArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nsteps = (mend > mbeg) ? (mend - mbeg + kBMR - 1) / kBMR : 0;
+  const int nsteps = (mend > mbeg) ? (mend - mbeg + BMR - 1) / BMR : 0;
   if (nsteps > 0) {
     load_step(mbeg);
     store_step(0);
@@ -308,9 +327,9 @@ wgrad_gemm_kernel(const WgradArgs a) {
   const int lk = lane >> 5, lc = lane & 31;
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
-    if (s + 1 < nsteps) load_step(mbeg + (s + 1) * kBMR);
-#pragma unroll 8
-    for (int kk = 0; kk < kBMR / 2; ++kk) {
+    if (s + 1 < nsteps) load_step(mbeg + (s + 1) * BMR);
+#pragma unroll
+    for (int kk = 0; kk < BMR / 2; ++kk) {
       float fa[RK], fb[RN];
 #pragma unroll
       for (int i = 0; i < RK; ++i) fa[i] = sG[cur][(wk * TK + 32 * i + lc) * L + 2 * kk + lk];
@@ -337,6 +356,16 @@ wgrad_gemm_kernel(const WgradArgs a) {
         const int n = n0 + wnn * TN + 32 * j + lc;
         out[(long long)k * a.Np + n] = acc[i][j][r];
       }
+}
+
+// Deterministic split reduction: slab[0][k][n] = sum_s slab[s][k][n] (coalesced).
+__global__ void slab_reduce_kernel(float* slab, int splits, long long per) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < per;
+       i += (long long)gridDim.x * blockDim.x) {
+    float s = slab[i];
+    for (int sp = 1; sp < splits; ++sp) s += slab[(long long)sp * per + i];
+    slab[i] = s;
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -635,12 +664,12 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
   w.M = g.B * w.Qh * w.Qw;
   const int tiles = (w.c.Kp / 128) * (w.Np / (w.N <= 32 ? 32 : 128));
   int splits = std::max(1, 1024 / std::max(tiles, 1));
-  const int max_by_m = std::max(1, w.M / (kBMR * 8));
+  const int max_by_m = std::max(1, w.M / 512);
   splits = std::min(splits, max_by_m);
   // keep the slab <= 256 MB
   const size_t per = (size_t)w.c.Kp * w.Np * sizeof(float);
   splits = (int)std::min<size_t>(splits, std::max<size_t>(1, (256u << 20) / per));
-  w.m_per_split = round_up((w.M + splits - 1) / splits, kBMR);
+  w.m_per_split = round_up((w.M + splits - 1) / splits, 64);
   w.splits = (w.M + w.m_per_split - 1) / w.m_per_split;
   return w;
 }
@@ -785,15 +814,21 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
   a.Kp = w.c.Kp; a.Np = w.Np; a.M = w.M; a.m_per_split = w.m_per_split;
   if (w.Np == 32) {
     dim3 grid(w.c.Kp / 128, 1, w.splits);
-    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1>), grid, dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64>), grid, dim3(kThreads), 0, st, a);
   } else {
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
-    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2>), grid, dim3(kThreads), 0, st, a);
+    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2, 32>), grid, dim3(kThreads), 0, st, a);
   }
   SE_LAUNCH_CHECK();
 
+  const long long per = (long long)w.c.Kp * w.Np;
+  if (w.splits > 1) {
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<long long>((per + 255) / 256, 2048)),
+                       dim3(256), 0, st, slab, w.splits, per);
+    SE_LAUNCH_CHECK();
+  }
   UnpackArgs u{};
-  u.slab = slab; u.splits = w.splits; u.Kp = w.c.Kp; u.Np = w.Np;
+  u.slab = slab; u.splits = 1; u.Kp = w.c.Kp; u.Np = w.Np;
   u.dwr = dwr; u.dwi = dwi; u.Ci = g.Ci; u.Co = g.Co; u.kh = g.kh; u.kw = g.kw;
   u.transposed = g.transposed; u.complex_w = g.complex_w; u.Cg = w.Cg;
   for (int t = 0; t < w.c.taps.n; ++t) u.tap_of[w.c.taps.ti[t] * g.kw + w.c.taps.tj[t]] = t;

@@ -88,17 +88,18 @@ def test_frcrn_train_step_golden(gpu_device):
     assert np.median(rel) < 1e-4, np.median(rel)
     # Per-tensor gate against the fp64 oracle: a few CCBAM
     # gradients are ill-conditioned (ReLU/max routing), where the reference's
-    # own fp32 result is ~1e-2 off fp64. The HIP error must stay within 3x the
-    # fp32 oracle's error on every tensor.
+    # own fp32 result is ~1e-2 off fp64. Every HIP gradient must be within
+    # max(3x the fp32 oracle's error, 1e-3) of fp64 (rel-L2 per tensor), and
+    # the median over tensors within 3x the fp32 oracle's median.
     g64, g32 = _oracle_grads(torch.float64), _oracle_grads(torch.float32)
     errs = []
     for n, p in m.named_parameters():
         d = g64[n].norm().item() + 1e-30
         errs.append(((p.grad.double().cpu() - g64[n]).norm().item() / d,
                      (g32[n] - g64[n]).norm().item() / d, n))
-    floor = 3 * float(np.median([e[1] for e in errs]))
-    bad = [e for e in errs if e[0] > max(3 * e[1], floor)]
+    bad = [e for e in errs if e[0] > max(3 * e[1], 1e-3)]
     assert not bad, bad[:5]
+    assert np.median([e[0] for e in errs]) < 3 * np.median([e[1] for e in errs])
     total = torch.nn.utils.clip_grad_norm_(m.parameters(), 0.5)
     assert abs(float(total) - float(g["grad_total_norm"])) < 1e-3 * float(g["grad_total_norm"])
     opt.step()
