@@ -35,6 +35,14 @@ constexpr int kBK = 32;      // reduction depth per K-step (16 MFMA k-pairs)
 constexpr int kMaxTaps = 64; // per-class taps (kh*kw <= 64)
 constexpr int kInvalidOff = -(1 << 29);
 
+typedef float f32x4 __attribute__((ext_vector_type(4)));   // native vector (SROA-friendly)
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+// Out-of-range gather lanes read a zeroed page of the workspace (global
+// memory, like the tensors, so the select stays a global_load) instead of
+// selecting after the load: the loaded register then feeds the LDS write
+// directly and the load stays in flight across the MFMA loop.
+constexpr size_t kZeroBytes = 256;
+
 // ---------------------------------------------------------------------------
 // Gather-GEMM (forward and data-grad)
 // ---------------------------------------------------------------------------
@@ -43,6 +51,7 @@ struct GatherArgs {
   const int4* ktab;    // [Kp] {c*Hi*Wi + offh*Wi + offw, offh, offw, 0}
   const float* Wp;     // [Kp, ldw]
   const float* bias;   // [N] or nullptr
+  const float* zero;   // zeroed workspace page
   float* Y;            // [B, N, Ho, Wo]
   int Cg, Hi, Wi;
   int N, Ho, Wo;
@@ -50,16 +59,23 @@ struct GatherArgs {
   int Kp, ldw, M;
 };
 
+// LDS images of both operands are column-interleaved inside every 64-wide
+// wave block: column 32*i + l is stored at 2*l + i, so each lane fetches its
+// two MFMA operands (i = 0, 1) with one conflict-free ds_read_b64. The weight
+// columns are pre-interleaved by prep_class_kernel (ldw >= 64).
+__device__ __forceinline__ int ilv64(int c) { return (c & ~63) | ((c & 31) << 1) | ((c >> 5) & 1); }
+
 template <int BN, int BM, int WN, int WM>
 __global__ void __launch_bounds__(kThreads)
 gather_gemm_kernel(const GatherArgs a) {
   static_assert(WN * WM == 4, "4 waves");
   constexpr int TN = BN / WN, TM = BM / WM;       // wave tile
   constexpr int RN = TN / 32, RM = TM / 32;       // 32x32 MFMA repeats
+  static_assert(RN == 2 && RM == 2, "interleaved LDS images assume 64-wide wave tiles");
   constexpr int KR = kThreads / BM;               // threads per m column
   constexpr int AJ = kBK / KR;                    // A rows per thread per step
   constexpr int WV = (kBK * BN) / (4 * kThreads); // float4 weight loads/thread
-  static_assert(RN >= 1 && RM >= 1 && KR >= 1 && WV >= 1, "tile shape");
+  static_assert(KR >= 1 && WV >= 1, "tile shape");
 
   __shared__ __attribute__((aligned(16))) float sA[2][kBK][BM];
   __shared__ __attribute__((aligned(16))) float sW[2][kBK][BN];
@@ -71,6 +87,7 @@ gather_gemm_kernel(const GatherArgs a) {
 
   // --- this thread's gather column (fixed for the whole K loop) ---
   const int am = tid % BM;
+  const int am_pos = ilv64(am);
   const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // wave-uniform k row
   const int m = m0 + am;
   const bool mval = m < a.M;
@@ -86,33 +103,32 @@ gather_gemm_kernel(const GatherArgs a) {
   }
 
   float ra[AJ];
-  float4 rw[WV];
-  auto load_tile = [&](int k0) {
+  f32x4 rw[WV];
+  auto load_tile = [&](int k0) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
       const int4 e = a.ktab[k0 + akr + KR * j];        // uniform index -> s_load
       const int hi = hb + e.y, wi = wb + e.z;
       const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      // unconditional load from a clamped address, then select: a predicated
-      // load makes hipcc branch around it and drain vmcnt(0) per element
-      const float v = a.X[ok ? xbase + e.x : 0];
-      ra[j] = ok ? v : 0.f;
+      // unconditional load (a predicated one makes hipcc branch around it and
+      // drain vmcnt(0) per element); invalid lanes read the zero page
+      ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
     }
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
       const int idx = tid + kThreads * j;           // float4 index in [BK][BN/4]
       const int kr = idx / (BN / 4), c4 = idx % (BN / 4);
-      rw[j] = *reinterpret_cast<const float4*>(a.Wp + (long long)(k0 + kr) * a.ldw + n0 + 4 * c4);
+      rw[j] = *reinterpret_cast<const f32x4*>(a.Wp + (long long)(k0 + kr) * a.ldw + n0 + 4 * c4);
     }
   };
-  auto store_tile = [&](int buf) {
+  auto store_tile = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) sA[buf][akr + KR * j][am] = ra[j];
+    for (int j = 0; j < AJ; ++j) sA[buf][akr + KR * j][am_pos] = ra[j];
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
       const int idx = tid + kThreads * j;
       const int kr = idx / (BN / 4), c4 = idx % (BN / 4);
-      *reinterpret_cast<float4*>(&sW[buf][kr][4 * c4]) = rw[j];
+      *reinterpret_cast<f32x4*>(&sW[buf][kr][4 * c4]) = rw[j];
     }
   };
 
@@ -131,22 +147,29 @@ gather_gemm_kernel(const GatherArgs a) {
   }
   __syncthreads();
   const int lk = lane >> 5, lc = lane & 31;
+  const int wcol = wn * TN + 2 * lc, mcol = wm * TM + 2 * lc;
   for (int kt = 0; kt < nk; ++kt) {
     const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile((kt + 1) * kBK);
+    if (kt + 1 < nk) load_tile((kt + 1) * kBK);     // in flight during the MFMAs below
+    // fragments software-pipelined one k-pair ahead
+    f32x2 fa = *reinterpret_cast<const f32x2*>(&sW[cur][lk][wcol]);
+    f32x2 fb = *reinterpret_cast<const f32x2*>(&sA[cur][lk][mcol]);
 #pragma unroll
     for (int kk = 0; kk < kBK / 2; ++kk) {
-      float fa[RN], fb[RM];
-#pragma unroll
-      for (int i = 0; i < RN; ++i) fa[i] = sW[cur][2 * kk + lk][wn * TN + 32 * i + lc];
-#pragma unroll
-      for (int j = 0; j < RM; ++j) fb[j] = sA[cur][2 * kk + lk][wm * TM + 32 * j + lc];
-#pragma unroll
-      for (int i = 0; i < RN; ++i)
-#pragma unroll
-        for (int j = 0; j < RM; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      f32x2 na = fa, nb = fb;
+      if (kk + 1 < kBK / 2) {
+        na = *reinterpret_cast<const f32x2*>(&sW[cur][2 * kk + 2 + lk][wcol]);
+        nb = *reinterpret_cast<const f32x2*>(&sA[cur][2 * kk + 2 + lk][mcol]);
+      }
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, fb.x, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, fb.y, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, fb.x, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, fb.y, acc[1][1], 0, 0, 0);
+      fa = na; fb = nb;
     }
+    // keep the next tile's LDS writes (and so their vmcnt waits) AFTER the
+    // MFMA loop: the buffers are disjoint, so hipcc would otherwise hoist them
+    __builtin_amdgcn_sched_barrier(0);
     if (kt + 1 < nk) store_tile(cur ^ 1);
     __syncthreads();
   }
@@ -228,6 +251,7 @@ struct WgradArgs {
   const float* X;      // gathered tensor [B, Cg, Hi, Wi]
   const int4* ktab;    // [Kp]
   const float* D;      // direct tensor [B, N, Qh, Qw]
+  const float* zero;   // zeroed workspace page
   float* slab;         // [splits, Kp, Np]
   int Cg, Hi, Wi;
   int N, Qh, Qw, sh, sw;
@@ -277,7 +301,7 @@ wgrad_gemm_kernel(const WgradArgs a) {
     cqw = r - cqh * a.Qw;
   }
   float rg[GJ], rd[DJ];
-  auto load_step = [&](int mstep) {
+  auto load_step = [&](int mstep) __attribute__((always_inline)) {
     const bool mv = mstep + ml < mend;
     const int hb = cqh * a.sh, wb = cqw * a.sw;
     const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
@@ -286,16 +310,14 @@ wgrad_gemm_kernel(const WgradArgs a) {
       const int4 e = sK[row0 + RS * j];
       const int hi = hb + e.y, wi = wb + e.z;
       const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      const float v = a.X[ok ? xb + e.x : 0];
-      rg[j] = ok ? v : 0.f;
+      rg[j] = *(ok ? a.X + xb + e.x : a.zero);
     }
     const long long db = (long long)cb * a.N * QQ + (long long)cqh * a.Qw + cqw;
 #pragma unroll
     for (int j = 0; j < DJ; ++j) {
       const int n = n0 + row0 + RS * j;
       const bool ok = mv & (n < a.N);
-      const float v = a.D[ok ? db + (long long)n * QQ : 0];
-      rd[j] = ok ? v : 0.f;
+      rd[j] = *(ok ? a.D + db + (long long)n * QQ : a.zero);
     }
     cqw += BMR;
     while (cqw >= a.Qw) {
@@ -303,7 +325,7 @@ wgrad_gemm_kernel(const WgradArgs a) {
       if (++cqh >= a.Qh) { cqh = 0; ++cb; }
     }
   };
-  auto store_step = [&](int buf) {
+  auto store_step = [&](int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < GJ; ++j) sG[buf][(row0 + RS * j) * L + ml] = rg[j];
 #pragma unroll
@@ -341,6 +363,7 @@ wgrad_gemm_kernel(const WgradArgs a) {
         for (int j = 0; j < RN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
     }
+    __builtin_amdgcn_sched_barrier(0);   // keep the LDS writes (and their vmcnt) after the MFMAs
     if (s + 1 < nsteps) store_step(cur ^ 1);
     __syncthreads();
   }
@@ -397,6 +420,8 @@ __device__ __forceinline__ float kernel_value(const WeightView& w, int ci, int c
   return co_im ? w.wi[idx] : -w.wi[idx];
 }
 
+__device__ __forceinline__ int ilv64_host_dev(int c) { return (c & ~63) | ((c & 31) << 1) | ((c >> 5) & 1); }
+
 struct TapList {
   int n;
   int ti[kMaxTaps], tj[kMaxTaps];     // kernel (i, j) of each tap
@@ -418,7 +443,7 @@ __global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int
       const int ci = data_grad ? n : c, co = data_grad ? c : n;
       v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
     }
-    Wp[idx] = v;
+    Wp[ldw >= 64 ? (long long)k * ldw + ilv64_host_dev(n) : idx] = v;
     if (n == 0) {
       int4 e;
       if (k < K) {
@@ -636,7 +661,7 @@ static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N) {
     bytes += (size_t)c.Kp * sizeof(int4);
   }
   bytes += (size_t)round_up(N, 128) * sizeof(float);  // bias_full
-  return bytes + 256;
+  return bytes + kZeroBytes + 512;
 }
 
 // wgrad plan: G is gathered (strided) over the grid of D.
@@ -675,7 +700,8 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
 }
 
 static size_t wgrad_ws_bytes(const WgradPlan& w) {
-  return (size_t)w.splits * w.c.Kp * w.Np * sizeof(float) + (size_t)w.c.Kp * sizeof(int4) + 256;
+  return (size_t)w.splits * w.c.Kp * w.Np * sizeof(float) + (size_t)w.c.Kp * sizeof(int4) +
+         kZeroBytes + 512;
 }
 
 static inline char* align256(char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); }
@@ -693,6 +719,9 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w};
 
   char* p = align256((char*)ws);
+  const float* zero = (const float*)p;
+  (void)hipMemsetAsync(p, 0, kZeroBytes, st);
+  p = align256(p + kZeroBytes);
   float* bias_full = nullptr;
   if (pass == kFwd && bias_br) {
     bias_full = (float*)p;
@@ -710,7 +739,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
                        dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, pass == kData ? 1 : 0,
                        Wp, ktab);
     GatherArgs a{};
-    a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.Y = Y;
+    a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.zero = zero; a.Y = Y;
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
@@ -793,6 +822,9 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
   WgradPlan w = plan_wgrad(g);
   if (ws_bytes < wgrad_ws_bytes(w)) return SE_E_WORKSPACE;
   char* p = align256((char*)ws);
+  const float* zero = (const float*)p;
+  (void)hipMemsetAsync(p, 0, kZeroBytes, st);
+  p = align256(p + kZeroBytes);
   float* slab = (float*)p;
   p = align256(p + (size_t)w.splits * w.c.Kp * w.Np * sizeof(float));
   int4* ktab = (int4*)p;
@@ -808,7 +840,7 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
   WgradArgs a{};
   a.X = g.transposed ? dy : x;
   a.D = g.transposed ? x : dy;
-  a.ktab = ktab; a.slab = slab;
+  a.ktab = ktab; a.slab = slab; a.zero = zero;
   a.Cg = w.Cg; a.Hi = w.Hi; a.Wi = w.Wi;
   a.N = w.N; a.Qh = w.Qh; a.Qw = w.Qw; a.sh = w.c.h.s; a.sw = w.c.w.s;
   a.Kp = w.c.Kp; a.Np = w.Np; a.M = w.M; a.m_per_split = w.m_per_split;
