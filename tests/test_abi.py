@@ -1,0 +1,100 @@
+"""CPU-only checks of the C-ABI library: it loads, exports every symbol
+include/sehip.h declares, and its host-side planning/validation entry points
+(no kernel launches) behave like the reference's shape rules."""
+import ctypes
+
+import pytest
+import torch
+
+from sehip import _native as N
+from sehip import functional as F
+
+
+def test_library_exports_header_symbols():
+    lib = N.lib()
+    syms = N.header_symbols()
+    assert len(syms) >= 15
+    for s in syms:
+        assert hasattr(lib, s), f"libsehip.so does not export {s}"
+    assert N.MISSING == []
+    assert lib.se_abi_version() == 1
+
+
+def test_strerror():
+    lib = N.lib()
+    assert lib.se_strerror(0) == b"ok"
+    for code in (-1, -2, -3, -4, -5):
+        assert lib.se_strerror(code) not in (b"ok", b"unknown sehip error")
+    assert lib.se_strerror(-99) == b"unknown sehip error"
+
+
+CONV_GEOMS = [
+    # (transposed, x shape, cout, kernel, stride, padding, dilation, output_padding)
+    (False, (2, 2, 320, 404), 128, (5, 2), (2, 1), (0, 0), (1, 1), (0, 0)),     # FRCRN enc0
+    (False, (3, 8, 17, 11), 6, (5, 3), (2, 2), (2, 1), (1, 1), (0, 0)),
+    (False, (1, 4, 9, 10), 2, (7, 7), (1, 1), (3, 3), (1, 1), (0, 0)),         # CCBAM k7
+    (False, (1, 6, 20, 30), 4, (3, 3), (1, 2), (1, 1), (2, 1), (0, 0)),        # dilation
+    (True, (2, 256, 77, 403), 128, (5, 2), (2, 1), (0, 0), (1, 1), (0, 0)),    # FRCRN dec
+    (True, (2, 8, 6, 7), 6, (5, 2), (2, 1), (2, 0), (1, 1), (1, 0)),           # DCCRN dec
+    (True, (2, 8, 6, 5), 6, (5, 3), (2, 2), (2, 1), (1, 1), (0, 0)),           # DCUNet dec
+    (True, (1, 4, 5, 7), 2, (1, 3), (2, 1), (0, 1), (1, 1), (1, 0)),           # CARN-like k1 s2
+]
+
+
+@pytest.mark.parametrize("g", CONV_GEOMS)
+def test_conv_out_shape_matches_torch(g):
+    tr, xs, cout, k, s, p, d, op = g
+    desc = F.conv_desc(xs, cout, k, s, p, d, op, tr, True)
+    ho, wo = ctypes.c_int(), ctypes.c_int()
+    assert N.lib().se_conv2d_out_shape(ctypes.byref(desc), ctypes.byref(ho), ctypes.byref(wo)) == 0
+    cls = torch.nn.ConvTranspose2d if tr else torch.nn.Conv2d
+    kw = dict(stride=s, padding=p, dilation=d)
+    if tr:
+        kw["output_padding"] = op
+    ref = cls(xs[1], cout, k, bias=False, **kw)(torch.zeros(xs)).shape
+    assert (ho.value, wo.value) == tuple(ref[2:])
+    assert N.lib().se_conv2d_workspace_size(ctypes.byref(desc)) > 0
+
+
+def test_conv_argument_errors_need_no_gpu():
+    lib = N.lib()
+    d = F.conv_desc((1, 3, 8, 8), 4, (3, 3), (1, 1), (1, 1), (1, 1), (0, 0), False, True)
+    # odd channel count with complex weights
+    assert lib.se_conv2d_out_shape(ctypes.byref(d), None, None) == -2
+    d = F.conv_desc((1, 4, 8, 8), 4, (3, 3), (0, 1), (1, 1), (1, 1), (0, 0), False, True)
+    assert lib.se_conv2d_out_shape(ctypes.byref(d), None, None) == -1   # stride 0
+    d = F.conv_desc((1, 4, 8, 8), 4, (3, 3), (1, 1), (1, 1), (1, 1), (0, 0), False, True)
+    assert lib.se_conv2d_fwd(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
+    d = F.conv_desc((1, 4, 8, 8), 4, (9, 9), (1, 1), (1, 1), (1, 1), (0, 0), False, True)
+    assert lib.se_conv2d_out_shape(ctypes.byref(d), None, None) == -3   # 81 taps > 64
+
+
+@pytest.mark.parametrize("L,win,hop,nfft,center", [
+    (64000, 320, 160, 640, 1), (64000, 400, 100, 512, 1), (32000, 512, 128, 512, 1),
+    (16000, 320, 160, 320, 1), (1440000, 320, 160, 512, 1), (4000, 320, 160, 640, 0)])
+def test_stft_num_frames_matches_conv1d(L, win, hop, nfft, center):
+    pad = nfft // 2 if center else 0
+    expect = (L + 2 * pad - win) // hop + 1
+    assert N.lib().se_stft_num_frames(L, win, hop, nfft, center) == expect
+
+
+def test_stft_validation_needs_no_gpu():
+    lib = N.lib()
+    # nfft with a factor 7 is not supported by the radix-2/3/4/5 FFT
+    assert lib.se_stft_fwd(None, None, None, 1, 4000, 320, 160, 7 * 64, 1, 0, None, None, None) == -3
+    assert lib.se_stft_fwd(None, None, None, 1, 4000, 320, 160, 642, 1, 0, None, None, None) == -3
+    assert lib.se_stft_fwd(None, None, None, 1, 4000, 700, 160, 640, 1, 0, None, None, None) == -1
+    assert lib.se_istft_fwd(None, None, 1, 10, 320, 160, 640, 0, 10 ** 6, None, None, None) == -2
+
+
+def test_cbn_workspace():
+    assert N.lib().se_cbn_workspace_size(64, 128, 77 * 403) > 0
+    assert N.lib().se_cbn_workspace_size(0, 128, 10) == 0
+
+
+def test_cpu_tensors_are_rejected():
+    """The product path must fail loudly instead of falling back to the CPU."""
+    from sehip.complex_nn import ComplexConv2d
+    m = ComplexConv2d(4, 4, 3, padding=1)
+    with pytest.raises(RuntimeError, match="GPU only"):
+        m(torch.zeros(1, 4, 8, 8))

@@ -1,0 +1,45 @@
+"""Turn rocprofv3 PMC passes into per-launch HBM traffic for bench.py.
+
+Usage: python tools/pmc_summary.py <fetch_dir> <write_dir> [out.json]
+Each dir holds a rocprofv3 --pmc csv run (run_counter_collection.csv) of the
+same bench command, one with FETCH_SIZE, one with WRITE_SIZE (TCC slots do not
+fit both in one pass). gfx950 correction (MI355X_MICROARCH.md §HBM):
+FETCH_SIZE counts 64 B per 128-B request of wide streaming reads, i.e. half the
+bytes -> doubled; both counters are in KiB.
+"""
+import collections, csv, json, os, re, sys
+
+
+def load(d, counter):
+    path = os.path.join(d, "run_counter_collection.csv")
+    per = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        if r["Counter_Name"] != counter:
+            continue
+        name = re.sub(r"^.*::", "", r["Kernel_Name"].split("(")[0]).split("<")[0].strip()
+        per[name].append(float(r["Counter_Value"]) * 1024.0)
+    return per
+
+
+def main():
+    fd, wd = sys.argv[1], sys.argv[2]
+    out = sys.argv[3] if len(sys.argv) > 3 else "profiles/pmc_traffic.json"
+    fetch, write = load(fd, "FETCH_SIZE"), load(wd, "WRITE_SIZE")
+    res = {}
+    for k in sorted(set(fetch) | set(write)):
+        f, w = fetch.get(k, []), write.get(k, [])
+        if not f or not w:
+            continue
+        fb = 2.0 * sum(f) / len(f)          # gfx950: FETCH_SIZE reads half the streamed bytes
+        wb = sum(w) / len(w)
+        res[k] = {"launches": len(f), "fetch_bytes_per_launch_corrected": fb,
+                  "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb}
+    json.dump(res, open(out, "w"), indent=1, sort_keys=True)
+    for k in ("gather_gemm_kernel", "wgrad_gemm_kernel", "stft_fwd_kernel", "istft_fwd_kernel",
+              "cbn_apply_kernel"):
+        if k in res:
+            print(k, {a: f"{b:.4g}" for a, b in res[k].items()})
+
+
+if __name__ == "__main__":
+    main()
