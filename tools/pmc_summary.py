@@ -16,7 +16,9 @@ def load(d, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = re.sub(r"^.*::", "", r["Kernel_Name"].split("(")[0]).split("<")[0].strip()
+        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
+        name = re.sub(r"^void\s+", "", name)
+        name = re.split(r"[<(]", name)[0].split("::")[-1].strip()
         per[name].append(float(r["Counter_Value"]) * 1024.0)
     return per
 
