@@ -25,6 +25,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 namespace {
@@ -57,6 +58,7 @@ struct GatherArgs {
   int N, Ho, Wo;
   int ph, pw, Sh, Sw, Qh, Qw, sh, sw;
   int Kp, ldw, M;
+  int ablate;          // debug only (SEHIP_ABLATE): bit0 no loads in the loop, bit1 no MFMA
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -65,8 +67,12 @@ struct GatherArgs {
 // columns are pre-interleaved by prep_class_kernel (ldw >= 64).
 __device__ __forceinline__ int ilv64(int c) { return (c & ~63) | ((c & 31) << 1) | ((c >> 5) & 1); }
 
-template <int BN, int BM, int WN, int WM>
-__global__ void __launch_bounds__(kThreads)
+// TU ("tap-uniform"): every K-step lies inside one tap (Cg % kBK == 0), so a
+// lane's bounds check and 32-bit voffset are computed once per step and the
+// 16 channel loads are raw buffer loads with a scalar soffset = c*Hi*Wi*4;
+// out-of-range lanes get an out-of-bounds voffset and the hardware returns 0.
+template <int BN, int BM, int WN, int WM, bool TU>
+__global__ void __launch_bounds__(kThreads, 2)   // 2 waves/SIMD: <= 256 VGPR+AGPR
 gather_gemm_kernel(const GatherArgs a) {
   static_assert(WN * WM == 4, "4 waves");
   constexpr int TN = BN / WN, TM = BM / WM;       // wave tile
@@ -102,9 +108,55 @@ gather_gemm_kernel(const GatherArgs a) {
     xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
   }
 
-  float ra[AJ];
-  f32x4 rw[WV];
-  auto load_tile = [&](int k0) __attribute__((always_inline)) {
+  // two register staging sets: tile t+2 is loading while tile t+1 waits to be
+  // written to LDS and tile t is consumed by the MFMAs (prefetch distance 2)
+  struct Stage { float ra[AJ]; f32x4 rw[WV]; };
+  Stage s0, s1;
+  // TU path: buffer descriptors built from wave-uniform values only
+  const int b0 = m0 / (a.Qh * a.Qw);               // first batch item of the tile
+  // descriptor inputs made PROVABLY uniform (readfirstlane on both pointer
+  // halves), else hipcc wraps every buffer op in a waterfall loop (guide T20)
+  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.X + (long long)b0 * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  __amdgpu_buffer_rsrc_t rwp = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.Wp), (short)0, 0x7FFFFFFF, 0x00020000);
+  int xoff = 0, woff[WV];
+  if constexpr (TU) {
+    const int qhw = a.Qh * a.Qw;
+    if (mval) {
+      const int b = m / qhw;
+      xoff = (int)(((long long)(b - b0) * a.Cg * HiWi + (long long)hb * a.Wi + wb) * 4);
+    }
+#pragma unroll
+    for (int j = 0; j < WV; ++j) {
+      const int idx = tid + kThreads * j;
+      const int kr = idx / (BN / 4), c4 = idx % (BN / 4);
+      woff[j] = (kr * a.ldw + n0 + 4 * c4) * 4;
+    }
+  }
+  auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
+    if constexpr (TU) {
+      const int4 e0 = a.ktab[k0];                     // tap of this step (uniform)
+      const int tap = k0 / a.Cg;
+      const int c0 = k0 - tap * a.Cg + akr;
+      const int hi = hb + e0.y, wi = wb + e0.z;
+      const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      const int vo = ok ? xoff + (e0.y * a.Wi + e0.z) * 4 : (int)0x80000000;
+      const int cs = (int)(HiWi * 4);
+#pragma unroll
+      for (int j = 0; j < AJ; ++j)
+        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (c0 + KR * j) * cs, 0));
+      const int so = k0 * a.ldw * 4;
+#pragma unroll
+      for (int j = 0; j < WV; ++j)
+        st.rw[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(rwp, woff[j], so, 0));
+      return;
+    }
 #pragma unroll
     for (int j = 0; j < AJ; ++j) {
       const int4 e = a.ktab[k0 + akr + KR * j];        // uniform index -> s_load
@@ -112,23 +164,23 @@ gather_gemm_kernel(const GatherArgs a) {
       const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
       // unconditional load (a predicated one makes hipcc branch around it and
       // drain vmcnt(0) per element); invalid lanes read the zero page
-      ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
+      st.ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
     }
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
       const int idx = tid + kThreads * j;           // float4 index in [BK][BN/4]
       const int kr = idx / (BN / 4), c4 = idx % (BN / 4);
-      rw[j] = *reinterpret_cast<const f32x4*>(a.Wp + (long long)(k0 + kr) * a.ldw + n0 + 4 * c4);
+      st.rw[j] = *reinterpret_cast<const f32x4*>(a.Wp + (long long)(k0 + kr) * a.ldw + n0 + 4 * c4);
     }
   };
-  auto store_tile = [&](int buf) __attribute__((always_inline)) {
+  auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < AJ; ++j) sA[buf][akr + KR * j][am_pos] = ra[j];
+    for (int j = 0; j < AJ; ++j) sA[buf][akr + KR * j][am_pos] = st.ra[j];
 #pragma unroll
     for (int j = 0; j < WV; ++j) {
       const int idx = tid + kThreads * j;
       const int kr = idx / (BN / 4), c4 = idx % (BN / 4);
-      *reinterpret_cast<f32x4*>(&sW[buf][kr][4 * c4]) = rw[j];
+      *reinterpret_cast<f32x4*>(&sW[buf][kr][4 * c4]) = st.rw[j];
     }
   };
 
@@ -140,39 +192,67 @@ gather_gemm_kernel(const GatherArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nk = a.Kp / kBK;
-  if (nk > 0) {
-    load_tile(0);
-    store_tile(0);
-  }
-  __syncthreads();
   const int lk = lane >> 5, lc = lane & 31;
   const int wcol = wn * TN + 2 * lc, mcol = wm * TM + 2 * lc;
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) load_tile((kt + 1) * kBK);     // in flight during the MFMAs below
-    // fragments software-pipelined one k-pair ahead
-    f32x2 fa = *reinterpret_cast<const f32x2*>(&sW[cur][lk][wcol]);
-    f32x2 fb = *reinterpret_cast<const f32x2*>(&sA[cur][lk][mcol]);
+  // one K-step of MFMAs on LDS buffer `cur`
+  auto compute = [&](int cur) __attribute__((always_inline)) {
+    // Fragments of the whole step in registers, fetched in two halves: the
+    // second half's ds_reads are issued (and fenced) before the first half's
+    // MFMAs, so the LDS latency hides under 32 MFMAs instead of stalling each.
+    constexpr int KP = kBK / 2, H = KP / 2;
+    f32x2 fa[KP], fb[KP];
 #pragma unroll
-    for (int kk = 0; kk < kBK / 2; ++kk) {
-      f32x2 na = fa, nb = fb;
-      if (kk + 1 < kBK / 2) {
-        na = *reinterpret_cast<const f32x2*>(&sW[cur][2 * kk + 2 + lk][wcol]);
-        nb = *reinterpret_cast<const f32x2*>(&sA[cur][2 * kk + 2 + lk][mcol]);
-      }
-      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, fb.x, acc[0][0], 0, 0, 0);
-      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.x, fb.y, acc[0][1], 0, 0, 0);
-      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, fb.x, acc[1][0], 0, 0, 0);
-      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa.y, fb.y, acc[1][1], 0, 0, 0);
-      fa = na; fb = nb;
+    for (int kk = 0; kk < H; ++kk) {
+      fa[kk] = *reinterpret_cast<const f32x2*>(&sW[cur][2 * kk + lk][wcol]);
+      fb[kk] = *reinterpret_cast<const f32x2*>(&sA[cur][2 * kk + lk][mcol]);
     }
-    // keep the next tile's LDS writes (and so their vmcnt waits) AFTER the
-    // MFMA loop: the buffers are disjoint, so hipcc would otherwise hoist them
     __builtin_amdgcn_sched_barrier(0);
-    if (kt + 1 < nk) store_tile(cur ^ 1);
+#pragma unroll
+    for (int kk = H; kk < KP; ++kk) {
+      fa[kk] = *reinterpret_cast<const f32x2*>(&sW[cur][2 * kk + lk][wcol]);
+      fb[kk] = *reinterpret_cast<const f32x2*>(&sA[cur][2 * kk + lk][mcol]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    if (!(a.ablate & 2)) {
+#pragma unroll
+      for (int kk = 0; kk < KP; ++kk) {
+        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].x, acc[0][0], 0, 0, 0);
+        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].y, acc[0][1], 0, 0, 0);
+        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].x, acc[1][0], 0, 0, 0);
+        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].y, acc[1][1], 0, 0, 0);
+        if (kk == H - 1) __builtin_amdgcn_sched_barrier(0);
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < KP; ++kk) acc[0][0][0] += fa[kk].x * fb[kk].x + fa[kk].y * fb[kk].y;
+    }
+    // keep the following LDS writes (and so their vmcnt waits) AFTER the
+    // MFMAs: the buffers are disjoint, so hipcc would otherwise hoist them
+    __builtin_amdgcn_sched_barrier(0);
+  };
+
+  const int nk = a.Kp / kBK;
+  const bool noload = a.ablate & 1;
+  // prologue: tile 0 -> LDS[0]; tile 1 in flight in s1
+  load_tile(s0, 0);
+  store_tile(s0, 0);
+  if (nk > 1) load_tile(s1, kBK);
+  __syncthreads();
+  // main loop, unrolled by two so the staging sets alternate by name
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    // even step: consume LDS[0]; s1 holds tile kt+1; load kt+2 into s0
+    if (kt + 2 < nk && !noload) load_tile(s0, (kt + 2) * kBK);
+    compute(0);
+    if (!noload) store_tile(s1, 1);
+    __syncthreads();
+    // odd step: consume LDS[1]; s0 holds tile kt+2; load kt+3 into s1
+    if (kt + 3 < nk && !noload) load_tile(s1, (kt + 3) * kBK);
+    compute(1);
+    if (kt + 2 < nk && !noload) store_tile(s0, 0);
     __syncthreads();
   }
+  if (kt < nk) compute(0);   // odd tile count: the last tile sits in LDS[0]
 
   // --- epilogue: lane -> m (coalesced along time), registers -> n ---
   float* sBias = &sW[0][0][0];                     // reuse the drained weight tile
@@ -262,7 +342,9 @@ struct WgradArgs {
 // One reduction step covers BMR consecutive positions m; a wave-instruction
 // loads LPW = 64 / BMR rows (k or n) x BMR positions, lanes along m so every
 // load is coalesced along the time axis.
-template <int BKO, int BNO, int WK, int WNn, int BMR>
+// TU: the K-tile lies inside one tap (Cg % BKO == 0): per step a lane's bounds
+// check and 32-bit voffsets are computed once, rows are scalar soffsets.
+template <int BKO, int BNO, int WK, int WNn, int BMR, bool TU>
 __global__ void __launch_bounds__(kThreads)
 wgrad_gemm_kernel(const WgradArgs a) {
   static_assert(WK * WNn == 4, "4 waves");
@@ -271,9 +353,9 @@ wgrad_gemm_kernel(const WgradArgs a) {
   constexpr int LPW = 64 / BMR;            // rows per wave-instruction
   constexpr int RS = 4 * LPW;              // rows covered by the workgroup per j
   constexpr int GJ = BKO / RS, DJ = BNO / RS;
-  constexpr int L = BMR + 1;               // padded [row][m] images: conflict-free both ways
-  __shared__ float sG[2][BKO * L];
-  __shared__ float sD[2][BNO * L];
+  constexpr int L = BMR + 2;               // padded [row][m] images (even: 8-B aligned rows)
+  __shared__ __attribute__((aligned(16))) float sG[2][BKO * L];
+  __shared__ __attribute__((aligned(16))) float sD[2][BNO * L];
   __shared__ int4 sK[BKO];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -301,7 +383,48 @@ wgrad_gemm_kernel(const WgradArgs a) {
     cqw = r - cqh * a.Qw;
   }
   float rg[GJ], rd[DJ];
+  // TU buffer descriptors over the split's first batch item (uniform inputs)
+  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  const int bfirst = (int)(mbeg / QQ);
+  __amdgpu_buffer_rsrc_t rg_src = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.X + (long long)bfirst * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  __amdgpu_buffer_rsrc_t rd_src = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.D + (long long)bfirst * a.N * QQ), (short)0, 0x7FFFFFFF, 0x00020000);
+  const int4 tap_e = a.ktab[k0];              // TU: the tile's single tap
+  const int cbase = k0 % a.Cg;
   auto load_step = [&](int mstep) __attribute__((always_inline)) {
+    if constexpr (TU) {
+      const bool mv = mstep + ml < mend;
+      const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
+      const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      const int rb = cb - bfirst;
+      const int vg = ok ? (int)(((long long)rb * a.Cg * HiWi + (long long)(cbase + lr) * HiWi +
+                                 (long long)hi * a.Wi + wi) * 4) : (int)0x80000000;
+      const int vd = mv ? (int)(((long long)rb * a.N * QQ + (long long)(n0 + lr) * QQ +
+                                 (long long)cqh * a.Qw + cqw) * 4) : (int)0x80000000;
+      const int gs = (int)(HiWi * 4), ds = (int)(QQ * 4);
+#pragma unroll
+      for (int j = 0; j < GJ; ++j)
+        rg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            rg_src, vg, (wave * LPW + RS * j) * gs, 0));
+#pragma unroll
+      for (int j = 0; j < DJ; ++j) {
+        const bool nok = n0 + wave * LPW + RS * j + lr < a.N;   // only the Np-padded tail fails
+        rd[j] = nok ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                          rd_src, vd, (wave * LPW + RS * j) * ds, 0)) : 0.f;
+      }
+      cqw += BMR;
+      while (cqw >= a.Qw) {
+        cqw -= a.Qw;
+        if (++cqh >= a.Qh) { cqh = 0; ++cb; }
+      }
+      return;
+    }
     const bool mv = mstep + ml < mend;
     const int hb = cqh * a.sh, wb = cqw * a.sw;
     const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
@@ -350,18 +473,44 @@ wgrad_gemm_kernel(const WgradArgs a) {
   for (int s = 0; s < nsteps; ++s) {
     const int cur = s & 1;
     if (s + 1 < nsteps) load_step(mbeg + (s + 1) * BMR);
+    // Reduction index of MFMA kk (0..BMR/2-1) for lane half lk is m = kk + (BMR/2)*lk,
+    // so k-pairs 2q and 2q+1 of one operand row come from ONE ds_read_b64. The
+    // step's fragments are fetched in two fenced halves (second half's reads
+    // overlap the first half's MFMAs).
+    constexpr int Q = BMR / 4, HQ = Q / 2;
+    f32x2 ga[RK][Q], gb[RN][Q];
+    const int col = (BMR / 2) * lk;
 #pragma unroll
-    for (int kk = 0; kk < BMR / 2; ++kk) {
-      float fa[RK], fb[RN];
-#pragma unroll
-      for (int i = 0; i < RK; ++i) fa[i] = sG[cur][(wk * TK + 32 * i + lc) * L + 2 * kk + lk];
-#pragma unroll
-      for (int j = 0; j < RN; ++j) fb[j] = sD[cur][(wnn * TN + 32 * j + lc) * L + 2 * kk + lk];
+    for (int q = 0; q < HQ; ++q) {
 #pragma unroll
       for (int i = 0; i < RK; ++i)
+        ga[i][q] = *reinterpret_cast<const f32x2*>(&sG[cur][(wk * TK + 32 * i + lc) * L + col + 2 * q]);
 #pragma unroll
-        for (int j = 0; j < RN; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i], fb[j], acc[i][j], 0, 0, 0);
+      for (int j = 0; j < RN; ++j)
+        gb[j][q] = *reinterpret_cast<const f32x2*>(&sD[cur][(wnn * TN + 32 * j + lc) * L + col + 2 * q]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = HQ; q < Q; ++q) {
+#pragma unroll
+      for (int i = 0; i < RK; ++i)
+        ga[i][q] = *reinterpret_cast<const f32x2*>(&sG[cur][(wk * TK + 32 * i + lc) * L + col + 2 * q]);
+#pragma unroll
+      for (int j = 0; j < RN; ++j)
+        gb[j][q] = *reinterpret_cast<const f32x2*>(&sD[cur][(wnn * TN + 32 * j + lc) * L + col + 2 * q]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int i = 0; i < RK; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(e ? ga[i][q].y : ga[i][q].x,
+                                                             e ? gb[j][q].y : gb[j][q].x, acc[i][j], 0, 0, 0);
+      if (q == HQ - 1) __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the LDS writes (and their vmcnt) after the MFMAs
     if (s + 1 < nsteps) store_step(cur ^ 1);
@@ -743,6 +892,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
+    static const int ablate = getenv("SEHIP_ABLATE") ? atoi(getenv("SEHIP_ABLATE")) : 0;
+    a.ablate = ablate;
     const long long M = (long long)g.B * c.h.Q * c.w.Q;
     if (M > INT32_MAX) return SE_E_UNSUPPORTED;
     a.M = (int)M;
@@ -753,12 +904,23 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       if (ldw <= 4) hipLaunchKernelGGL(gather_smalln_kernel<4>, grid, dim3(kThreads), sh, st, a);
       else if (ldw <= 8) hipLaunchKernelGGL(gather_smalln_kernel<8>, grid, dim3(kThreads), sh, st, a);
       else hipLaunchKernelGGL(gather_smalln_kernel<16>, grid, dim3(kThreads), sh, st, a);
-    } else if (ldw == 64) {
-      dim3 grid(se::ceil_div(M, 256), 1);
-      hipLaunchKernelGGL((gather_gemm_kernel<64, 256, 1, 4>), grid, dim3(kThreads), 0, st, a);
     } else {
-      dim3 grid(se::ceil_div(M, 128), ldw / 128);
-      hipLaunchKernelGGL((gather_gemm_kernel<128, 128, 2, 2>), grid, dim3(kThreads), 0, st, a);
+      // TU needs whole K-steps inside one tap and 32-bit buffer offsets over the
+      // batch items one M-tile can span
+      const long long qhw = (long long)c.h.Q * c.w.Q;
+      const int bm = ldw == 64 ? 256 : 128;
+      const long long span = (bm + qhw - 1) / qhw + 1;
+      const bool tu = (Cg % kBK == 0) && span * Cg * (long long)Hi * Wi * 4 < (1ll << 31) &&
+                      (long long)c.Kp * ldw * 4 < (1ll << 31);
+      if (ldw == 64) {
+        dim3 grid(se::ceil_div(M, 256), 1);
+        if (tu) hipLaunchKernelGGL((gather_gemm_kernel<64, 256, 1, 4, true>), grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((gather_gemm_kernel<64, 256, 1, 4, false>), grid, dim3(kThreads), 0, st, a);
+      } else {
+        dim3 grid(se::ceil_div(M, 128), ldw / 128);
+        if (tu) hipLaunchKernelGGL((gather_gemm_kernel<128, 128, 2, 2, true>), grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((gather_gemm_kernel<128, 128, 2, 2, false>), grid, dim3(kThreads), 0, st, a);
+      }
     }
     SE_LAUNCH_CHECK();
   }
@@ -844,12 +1006,18 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
   a.Cg = w.Cg; a.Hi = w.Hi; a.Wi = w.Wi;
   a.N = w.N; a.Qh = w.Qh; a.Qw = w.Qw; a.sh = w.c.h.s; a.sw = w.c.w.s;
   a.Kp = w.c.Kp; a.Np = w.Np; a.M = w.M; a.m_per_split = w.m_per_split;
+  const long long QQ = (long long)w.Qh * w.Qw;
+  const long long span = (w.m_per_split + QQ - 1) / QQ + 1;
+  const bool tu = (w.Cg % 128 == 0) && span * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
+                  span * (long long)w.Np * QQ * 4 < (1ll << 31);
   if (w.Np == 32) {
     dim3 grid(w.c.Kp / 128, 1, w.splits);
-    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64>), grid, dim3(kThreads), 0, st, a);
+    if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
   } else {
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
-    hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2, 32>), grid, dim3(kThreads), 0, st, a);
+    if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2, 32, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2, 32, false>), grid, dim3(kThreads), 0, st, a);
   }
   SE_LAUNCH_CHECK();
 
