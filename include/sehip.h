@@ -165,6 +165,32 @@ int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
                int act, float slope, void* ws, size_t ws_bytes,
                void* stream);
 
+/* ------------------------------------------------------------------------
+ * LSTM recurrence (torch.nn.LSTM as used by ComplexLSTM, complex_nn.py:115-145)
+ *
+ * L independent single-layer LSTMs with hidden size H in {64, 128}, batch B
+ * (even), T steps, h0 = c0 = 0, gate order i, f, g, o. The input projection
+ * xproj = X W_ih^T + b_ih + b_hh (row (l, b*T + t) at
+ * xproj + l*x_lstm_stride + (b*T + t)*x_row_stride, 4H wide) and every
+ * weight gradient are plain GEMMs left to the caller. Bit l of rev_mask runs
+ * LSTM l right-to-left (the reverse half of a bidirectional layer).
+ *
+ * zero  : device fp32 [H] of zeros (h_{-1}; read with scalar loads)
+ * h, c  : fp32 [L][B][T][H]   outputs (h) and cell states (saved for bwd)
+ * gates : fp32 [L][B][T][4H]  post-activation gates (saved for bwd)
+ * dy    : fp32 [L][B][T][H]   dLoss/dh
+ * dgates: fp32 [L][B][T][4H]  dLoss/d(pre-activation gates); then
+ *         dW_ih = dgates^T X, dW_hh = dgates^T h_prev, db = sum dgates,
+ *         dX = dgates W_ih.
+ * ------------------------------------------------------------------------ */
+int se_lstm_supported(int hidden);
+int se_lstm_fwd(const float* xproj, long long x_lstm_stride, int x_row_stride,
+                const float* w_hh, const float* zero, float* h, float* c, float* gates, int L,
+                int B, int T, int H, unsigned rev_mask, void* stream);
+int se_lstm_bwd(const float* dy, const float* w_hh, const float* gates,
+                const float* c, float* dgates, int L, int B, int T, int H,
+                unsigned rev_mask, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -58,7 +58,6 @@ struct GatherArgs {
   int N, Ho, Wo;
   int ph, pw, Sh, Sw, Qh, Qw, sh, sw;
   int Kp, ldw, M;
-  int ablate;          // debug only (SEHIP_ABLATE): bit0 no loads in the loop, bit1 no MFMA
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -213,18 +212,13 @@ gather_gemm_kernel(const GatherArgs a) {
       fb[kk] = *reinterpret_cast<const f32x2*>(&sA[cur][2 * kk + lk][mcol]);
     }
     __builtin_amdgcn_sched_barrier(0);
-    if (!(a.ablate & 2)) {
 #pragma unroll
-      for (int kk = 0; kk < KP; ++kk) {
-        acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].x, acc[0][0], 0, 0, 0);
-        acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].y, acc[0][1], 0, 0, 0);
-        acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].x, acc[1][0], 0, 0, 0);
-        acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].y, acc[1][1], 0, 0, 0);
-        if (kk == H - 1) __builtin_amdgcn_sched_barrier(0);
-      }
-    } else {
-#pragma unroll
-      for (int kk = 0; kk < KP; ++kk) acc[0][0][0] += fa[kk].x * fb[kk].x + fa[kk].y * fb[kk].y;
+    for (int kk = 0; kk < KP; ++kk) {
+      acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].x, acc[0][0], 0, 0, 0);
+      acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].y, acc[0][1], 0, 0, 0);
+      acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].x, acc[1][0], 0, 0, 0);
+      acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].y, acc[1][1], 0, 0, 0);
+      if (kk == H - 1) __builtin_amdgcn_sched_barrier(0);
     }
     // keep the following LDS writes (and so their vmcnt waits) AFTER the
     // MFMAs: the buffers are disjoint, so hipcc would otherwise hoist them
@@ -232,7 +226,6 @@ gather_gemm_kernel(const GatherArgs a) {
   };
 
   const int nk = a.Kp / kBK;
-  const bool noload = a.ablate & 1;
   // prologue: tile 0 -> LDS[0]; tile 1 in flight in s1
   load_tile(s0, 0);
   store_tile(s0, 0);
@@ -242,14 +235,14 @@ gather_gemm_kernel(const GatherArgs a) {
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
     // even step: consume LDS[0]; s1 holds tile kt+1; load kt+2 into s0
-    if (kt + 2 < nk && !noload) load_tile(s0, (kt + 2) * kBK);
+    if (kt + 2 < nk) load_tile(s0, (kt + 2) * kBK);
     compute(0);
-    if (!noload) store_tile(s1, 1);
+    store_tile(s1, 1);
     __syncthreads();
     // odd step: consume LDS[1]; s0 holds tile kt+2; load kt+3 into s1
-    if (kt + 3 < nk && !noload) load_tile(s1, (kt + 3) * kBK);
+    if (kt + 3 < nk) load_tile(s1, (kt + 3) * kBK);
     compute(1);
-    if (kt + 2 < nk && !noload) store_tile(s0, 0);
+    if (kt + 2 < nk) store_tile(s0, 0);
     __syncthreads();
   }
   if (kt < nk) compute(0);   // odd tile count: the last tile sits in LDS[0]
@@ -892,8 +885,6 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
-    static const int ablate = getenv("SEHIP_ABLATE") ? atoi(getenv("SEHIP_ABLATE")) : 0;
-    a.ablate = ablate;
     const long long M = (long long)g.B * c.h.Q * c.w.Q;
     if (M > INT32_MAX) return SE_E_UNSUPPORTED;
     a.M = (int)M;

@@ -56,6 +56,10 @@ _SIGNATURES = {
                            c_size_t, _P]),
     "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP,
                            c_int, c_int, c_float, _P, c_size_t, _P]),
+    "se_lstm_supported": (c_int, [c_int]),
+    "se_lstm_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P, _P] + [c_int] * 4
+                    + [ctypes.c_uint, _P]),
+    "se_lstm_bwd": (c_int, [_P] * 5 + [c_int] * 4 + [ctypes.c_uint, _P]),
 }
 
 

@@ -138,11 +138,54 @@ class ComplexLinear(nn.Module):
         return merge_real_imag(x, self.real_linear(re), self.imag_linear(im), dim=-1)
 
 
+def _hip_lstm_ok(m: nn.LSTM) -> bool:
+    return (m.proj_size == 0 and m.hidden_size in (64, 128)
+            and (m.dropout == 0 or not m.training) and m.mode == "LSTM")
+
+
+def stacked_lstms(x, lstms, batch_first=True):
+    """Run several nn.LSTMs (same shape) over the same input x on the HIP
+    recurrence, all of them in the same launches: per layer one projection
+    GEMM, one se_lstm_fwd over every (LSTM, direction), and in backward one
+    se_lstm_bwd. Returns one output per LSTM, shaped like nn.LSTM's output[0].
+    The modules keep their own parameters (state_dict keys unchanged)."""
+    m0 = lstms[0]
+    nd = 2 if m0.bidirectional else 1
+    H = m0.hidden_size
+    xb = x if batch_first else x.transpose(0, 1)
+    inp = xb.contiguous()                         # layer 0: [B, T, I] shared by every LSTM
+    rev_mask = sum(1 << (i * nd + 1) for i in range(len(lstms))) if nd == 2 else 0
+    out = None
+    for k in range(m0.num_layers):
+        sfx = [f"_l{k}", f"_l{k}_reverse"][:nd]
+        w_ih = torch.stack([getattr(m, "weight_ih" + s) for m in lstms for s in sfx])
+        w_hh = torch.stack([getattr(m, "weight_hh" + s) for m in lstms for s in sfx])
+        b_ih = b_hh = None
+        if m0.bias:
+            b_ih = torch.stack([getattr(m, "bias_ih" + s) for m in lstms for s in sfx])
+            b_hh = torch.stack([getattr(m, "bias_hh" + s) for m in lstms for s in sfx])
+        h = F.lstm_layer(inp, w_ih, w_hh, b_ih, b_hh, rev_mask)      # [len*nd, B, T, H]
+        Bn, T = h.shape[1], h.shape[2]
+        if nd == 2:   # per LSTM: cat(forward, reverse) on features, fed to both directions
+            out = h.view(len(lstms), 2, Bn, T, H).permute(0, 2, 3, 1, 4).reshape(len(lstms), Bn, T, 2 * H)
+        else:
+            out = h
+        if k + 1 < m0.num_layers:
+            if m0.dropout > 0 and m0.training:
+                out = torch.nn.functional.dropout(out, m0.dropout, True)
+            inp = out.repeat_interleave(nd, dim=0) if nd == 2 else out
+    outs = list(out.unbind(0))
+    return outs if batch_first else [o.transpose(0, 1) for o in outs]
+
+
 class ComplexLSTM(nn.Module):
     """complex_nn.py:115-145. The reference makes four LSTM calls; the real
     and imaginary inputs are independent sequences through the SAME weights,
-    so each nn.LSTM runs once over both stacked on the batch axis (2 calls,
-    identical math, half the sequential launches)."""
+    so re and im are stacked on the batch axis, and real_lstm / imag_lstm run
+    together in the stacked HIP recurrence (stacked_lstms): per layer one
+    launch forward and one backward instead of MIOpen's per-time-step kernels.
+    Configurations the HIP recurrence does not cover (hidden size other than
+    64 / 128, proj_size) run each nn.LSTM once over the stacked batch."""
 
     def __init__(self, in_channels, hidden_channels, **kwargs):
         super().__init__()
@@ -155,8 +198,12 @@ class ComplexLSTM(nn.Module):
     def forward(self, x):
         re, im = split_complex(x, dim=-1)
         both = torch.cat([re, im], dim=self._bdim)
-        r_out = self.real_lstm(both)[0]
-        i_out = self.imag_lstm(both)[0]
+        if _hip_lstm_ok(self.real_lstm):
+            r_out, i_out = stacked_lstms(both, [self.real_lstm, self.imag_lstm],
+                                         batch_first=self._bdim == 0)
+        else:
+            r_out = self.real_lstm(both)[0]
+            i_out = self.imag_lstm(both)[0]
         rr, ir = torch.chunk(r_out, 2, dim=self._bdim)     # real_lstm(re), real_lstm(im)
         ri, ii = torch.chunk(i_out, 2, dim=self._bdim)     # imag_lstm(re), imag_lstm(im)
         return merge_real_imag(x, rr - ii, ri + ir, dim=-1)

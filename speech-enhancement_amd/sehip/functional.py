@@ -289,3 +289,117 @@ class _Istft(torch.autograd.Function):
 def istft(spec, window, twiddle, win, hop, nfft, offset, out_len):
     """spec [B, nfft+2, T] -> wav [B, out_len] = full OLA signal[offset:offset+out_len]."""
     return _Istft.apply(spec, window, twiddle, win, hop, nfft, offset, out_len)
+
+
+# --------------------------------------------------------------------------
+# LSTM layer of L stacked independent LSTMs — se_lstm_* (lstm.hip)
+# --------------------------------------------------------------------------
+_ZEROS: dict = {}
+
+
+def _zero_row(n: int, device) -> torch.Tensor:
+    key = (str(device), n)
+    z = _ZEROS.get(key)
+    if z is None:
+        z = _ZEROS[key] = torch.zeros(n, device=device, dtype=torch.float32)
+    return z
+
+
+def lstm_supported(hidden: int) -> bool:
+    return bool(N.lib().se_lstm_supported(int(hidden)))
+
+
+class _LstmLayer(torch.autograd.Function):
+    """One layer of L independent LSTMs run together (torch.nn.LSTM math,
+    gate order i, f, g, o, zero initial state).
+
+    x: [B, T, I] fed to all L LSTMs, or [L, B, T, I]; w_ih [L, 4H, I];
+    w_hh [L, 4H, H]; b_ih, b_hh [L, 4H] or None; bit l of rev_mask runs LSTM l
+    right-to-left. Returns h [L, B, T, H].
+
+    The input projection and all weight/input gradients are plain GEMMs
+    (rocBLAS through torch); the time recurrence is one persistent HIP
+    launch per direction (fwd: se_lstm_fwd, bwd: se_lstm_bwd)."""
+
+    @staticmethod
+    def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, rev_mask):
+        N.require_device(x, w_ih, w_hh, b_ih, b_hh)
+        L, G, I = w_ih.shape
+        H = G // 4
+        shared = x.dim() == 3
+        B, T = x.shape[-3], x.shape[-2]
+        if x.shape[-1] != I or tuple(w_hh.shape) != (L, G, H):
+            raise ValueError("sehip lstm: inconsistent shapes")
+        bias = None
+        if b_ih is not None or b_hh is not None:
+            bias = (b_ih if b_ih is not None else 0) + (b_hh if b_hh is not None else 0)
+        if shared:
+            x2 = x.reshape(B * T, I)
+            wt = w_ih.reshape(L * G, I).t()
+            xproj = torch.addmm(bias.reshape(L * G), x2, wt) if bias is not None else x2 @ wt
+            x_lstm, x_row = G, L * G
+        else:
+            x3 = x.reshape(L, B * T, I)
+            wt = w_ih.transpose(1, 2)
+            xproj = (torch.baddbmm(bias.unsqueeze(1), x3, wt) if bias is not None
+                     else torch.bmm(x3, wt))
+            x_lstm, x_row = B * T * G, G
+        w_hh = w_hh.contiguous()
+        h = torch.empty((L, B, T, H), device=x.device, dtype=x.dtype)
+        c = torch.empty_like(h)
+        gates = torch.empty((L, B, T, G), device=x.device, dtype=x.dtype)
+        t0 = _TIMER.begin() if _TIMER else None
+        N.check(N.lib().se_lstm_fwd(xproj.data_ptr(), x_lstm, x_row, w_hh.data_ptr(),
+                                    _zero_row(H, x.device).data_ptr(), h.data_ptr(), c.data_ptr(),
+                                    gates.data_ptr(), L, B, T, H, int(rev_mask), N.stream_of(x)),
+                "se_lstm_fwd")
+        if t0 is not None:
+            _TIMER.end("lstm_fwd", t0, 2.0 * L * B * T * G * H, 4.0 * L * B * T * (G + 2 * G + 2 * H))
+        ctx.save_for_backward(x, w_ih, w_hh, h, c, gates)
+        ctx.rev_mask, ctx.has_b = int(rev_mask), (b_ih is not None, b_hh is not None)
+        return h
+
+    @staticmethod
+    def backward(ctx, dh):
+        x, w_ih, w_hh, h, c, gates = ctx.saved_tensors
+        L, B, T, H = h.shape
+        G, I = 4 * H, w_ih.shape[2]
+        dh = dh.contiguous()
+        dgates = torch.empty_like(gates)
+        t0 = _TIMER.begin() if _TIMER else None
+        N.check(N.lib().se_lstm_bwd(dh.data_ptr(), w_hh.data_ptr(), gates.data_ptr(), c.data_ptr(),
+                                    dgates.data_ptr(), L, B, T, H, ctx.rev_mask, N.stream_of(dh)),
+                "se_lstm_bwd")
+        if t0 is not None:
+            _TIMER.end("lstm_bwd", t0, 2.0 * L * B * T * G * H, 4.0 * L * B * T * (H + 2 * G + 2 * H))
+        dg = dgates.reshape(L, B * T, G)
+        dgt = dg.transpose(1, 2)
+        shared = x.dim() == 3
+        dx = dw_ih = dw_hh = db_ih = db_hh = None
+        if ctx.needs_input_grad[0]:
+            if shared:
+                dx = torch.bmm(dg, w_ih).sum(0).reshape(B, T, I)
+            else:
+                dx = torch.bmm(dg, w_ih).reshape(L, B, T, I)
+        if ctx.needs_input_grad[1]:
+            xs = x.reshape(B * T, I) if shared else x.reshape(L, B * T, I)
+            dw_ih = torch.matmul(dgt, xs)
+        if ctx.needs_input_grad[2]:
+            # h_{t-1} in processing order (zero at the first step of each direction)
+            hp = torch.zeros_like(h)
+            for l in range(L):
+                if (ctx.rev_mask >> l) & 1:
+                    hp[l, :, :-1] = h[l, :, 1:]
+                else:
+                    hp[l, :, 1:] = h[l, :, :-1]
+            dw_hh = torch.bmm(dgt, hp.reshape(L, B * T, H))
+        if ctx.has_b[0] and ctx.needs_input_grad[3] or ctx.has_b[1] and ctx.needs_input_grad[4]:
+            db = dg.sum(1)
+            db_ih = db if ctx.has_b[0] else None
+            db_hh = db if ctx.has_b[1] else None
+        return dx, dw_ih, dw_hh, db_ih, db_hh, None
+
+
+def lstm_layer(x, w_ih, w_hh, b_ih=None, b_hh=None, rev_mask: int = 0):
+    """h [L, B, T, H] of L stacked LSTMs over x ([B, T, I] shared or [L, B, T, I])."""
+    return _LstmLayer.apply(x, w_ih, w_hh, b_ih, b_hh, rev_mask)

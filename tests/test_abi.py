@@ -98,3 +98,27 @@ def test_cpu_tensors_are_rejected():
     m = ComplexConv2d(4, 4, 3, padding=1)
     with pytest.raises(RuntimeError, match="GPU only"):
         m(torch.zeros(1, 4, 8, 8))
+
+
+def test_lstm_validation_needs_no_gpu():
+    lib = N.lib()
+    assert lib.se_lstm_supported(128) == 1 and lib.se_lstm_supported(64) == 1
+    assert lib.se_lstm_supported(96) == 0 and lib.se_lstm_supported(1024) == 0
+    # (xproj, x_lstm, x_row, w_hh, zero, h, c, gates, L, B, T, H, rev_mask, stream)
+    assert lib.se_lstm_fwd(None, 0, 512, None, None, None, None, None, 2, 128, 403, 96, 0, None) == -3
+    assert lib.se_lstm_fwd(None, 0, 512, None, None, None, None, None, 0, 128, 403, 128, 0, None) == -1
+    assert lib.se_lstm_fwd(None, 0, 512, None, None, None, None, None, 2, 128, 403, 128, 0, None) == -1
+    assert lib.se_lstm_fwd(None, 0, 100, None, None, None, None, None, 2, 128, 403, 128, 0, None) == -1
+    assert lib.se_lstm_bwd(None, None, None, None, None, 2, 128, 403, 64, 0, None) == -1
+    assert lib.se_lstm_bwd(None, None, None, None, None, 2, 0, 403, 64, 0, None) == -1
+
+
+def test_complex_lstm_state_dict_matches_reference_layout():
+    """ComplexLSTM keeps the reference's parameter names (real_lstm / imag_lstm
+    nn.LSTM modules) although the HIP path does not call them."""
+    from sehip.complex_nn import ComplexLSTM
+    from oracle.complex_nn import ComplexLSTM as O
+    a = ComplexLSTM(256, 256, num_layers=2, batch_first=True).state_dict()
+    b = O(256, 256, num_layers=2, batch_first=True).state_dict()
+    assert list(a) == list(b)
+    assert all(a[k].shape == b[k].shape for k in a)
