@@ -191,6 +191,41 @@ int se_lstm_bwd(const float* dy, const float* w_hh, const float* gates,
                 const float* c, float* dgates, int L, int B, int T, int H,
                 unsigned rev_mask, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Complex CBAM skip attention (models/modules/ccbam.py:28-106), the passes
+ * over the full skip tensor x [B, C, HW] (C even, <= 512; channels [0, C/2)
+ * real, [C/2, C) imag). The shared MLP (ccbam.py:38-41) and the 4->2 k7
+ * ComplexConv2d + CBN + ReLU (ccbam.py:65-71) run as their own modules on
+ * the small pooled maps. Max-pool gradients go to the first maximal index
+ * (AdaptiveMaxPool2d / torch.max(dim) semantics).
+ *
+ * channel_pool : mean, max, first argmax over HW per (b, c)   [B, C]
+ * spatial_pool : pooled [B, 4, HW] = (mean_re, max_re, mean_im, max_im) of
+ *                x*ca over each half's channels; idx int16 [B, 2, HW] = the
+ *                argmax channel within the half (ccbam.py:73-83)
+ * apply        : out = x*ca + sa[b, half(c)]                   (ccbam.py:98-105)
+ * bwd_sa       : dsa [B, 2, HW] = per-half channel sums of gout
+ * bwd_dca      : dca [B, C] = sum_hw gx1*x, gx1 = gout + dpooled_mean/(C/2)
+ *                + [argmax] dpooled_max; needs se_ccbam_workspace_size bytes
+ * bwd_dx       : dx = gx1*ca + dmean/HW + [hw == argmax_hw(b,c)] dmax
+ * ------------------------------------------------------------------------ */
+size_t se_ccbam_workspace_size(int B, int C, int HW);
+int se_ccbam_channel_pool(const float* x, float* mean, float* mx, int* amax,
+                          int B, int C, int HW, void* stream);
+int se_ccbam_spatial_pool(const float* x, const float* ca, float* pooled,
+                          short* idx, int B, int C, int HW, void* stream);
+int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out,
+                   int B, int C, int HW, void* stream);
+int se_ccbam_bwd_sa(const float* gout, float* dsa, int B, int C, int HW,
+                    void* stream);
+int se_ccbam_bwd_dca(const float* gout, const float* x, const float* dpooled,
+                     const short* idx, float* dca, int B, int C, int HW,
+                     void* ws, size_t ws_bytes, void* stream);
+int se_ccbam_bwd_dx(const float* gout, const float* dpooled, const short* idx,
+                    const float* ca, const float* dmean, const float* dmax,
+                    const int* amax, float* dx, int B, int C, int HW,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

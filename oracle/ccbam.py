@@ -67,7 +67,8 @@ class SpatialAttention(nn.Module):
     def forward(self, x):
         xr, xi = split_complex(x)
         avg = torch.cat([xr.mean(1, keepdim=True), xi.mean(1, keepdim=True)], 1)
-        mx = torch.cat([xr.amax(1, keepdim=True), xi.amax(1, keepdim=True)], 1)
+        # torch.max(dim)[0] as at ccbam.py:79-80: the gradient goes to ONE index
+        mx = torch.cat([torch.max(xr, 1, keepdim=True)[0], torch.max(xi, 1, keepdim=True)[0]], 1)
         return torch.sigmoid(self.conv(complex_concat([avg, mx], dim=1)))
 
 

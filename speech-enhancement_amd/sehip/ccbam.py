@@ -1,15 +1,20 @@
 """Complex CBAM skip attention (FRCRN decoder), HIP path.
 
-Drop-in for /root/reference/models/modules/ccbam.py (same module tree and
-state_dict keys). The spatial branch's ComplexConv2d(4->2, k7) + CBN + ReLU
-run on the fused HIP kernels; the pooling / sigmoid glue is plain PyTorch
-on the device for now (SURVEY.md §8f rank 2 fuses it).
+Drop-in for models/modules/ccbam.py (same module tree and state_dict keys).
+CCBAM.forward runs the fused path (_CCBAMFn): the five passes over the full
+skip tensor are csrc/ccbam.hip kernels (se_ccbam_*), the shared MLP and the
+spatial ComplexConv2d(4->2, k7) + CBN + ReLU run as their own modules on the
+small pooled maps (the conv/CBN on the HIP conv and CBN kernels). The
+sub-modules' own forward methods (ChannelAttention, SpatialAttention) keep
+the unfused reference formulation for anyone calling them directly.
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 
+from . import _native as N
+from . import functional as F
 from .complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexLinear, complex_concat,
                          merge_real_imag, norm_act, split_complex)
 
@@ -73,9 +78,88 @@ class SpatialAttention(nn.Module):
         return torch.sigmoid(self.conv(complex_concat([avg, mx], dim=1)))
 
 
+def _call(fn, name, *args):
+    N.check(fn(*args), name)
+
+
+class _CCBAMFn(torch.autograd.Function):
+    """out = CCBAM(x) with the full-tensor passes on se_ccbam_* kernels.
+
+    The MLP (channel branch) and conv/CBN/ReLU (spatial branch) are built as
+    small autograd graphs inside forward (on detached pooled inputs) and
+    differentiated with torch.autograd.grad in backward, so their parameters
+    (and CBN's HIP kernels) are used unchanged."""
+
+    @staticmethod
+    def forward(ctx, x, mod, *params):
+        N.require_device(x)
+        x = x.contiguous()
+        B, C, H, W = x.shape
+        HW = H * W
+        lib, st, dev = N.lib(), N.stream_of(x), x.device
+        need_grad = any(ctx.needs_input_grad)
+        cab, sab = mod.channel_attention_branch, mod.spatial_attention_branch
+        mean = torch.empty(B, C, device=dev)
+        mx = torch.empty(B, C, device=dev)
+        amax = torch.empty(B, C, device=dev, dtype=torch.int32)
+        _call(lib.se_ccbam_channel_pool, "se_ccbam_channel_pool", x.data_ptr(), mean.data_ptr(),
+              mx.data_ptr(), amax.data_ptr(), B, C, HW, st)
+        with torch.set_grad_enabled(need_grad):
+            pooled = torch.cat([mean, mx], 0)
+            if need_grad:
+                pooled.requires_grad_(True)
+            a, m = torch.chunk(cab.shared_fc_layer(pooled), 2, dim=0)
+            ca = torch.sigmoid(a + m).contiguous()                   # [B, C]
+        P = torch.empty(B, 4, H, W, device=dev)
+        idx = torch.empty(B, 2, H, W, device=dev, dtype=torch.int16)
+        _call(lib.se_ccbam_spatial_pool, "se_ccbam_spatial_pool", x.data_ptr(), ca.data_ptr(),
+              P.data_ptr(), idx.data_ptr(), B, C, HW, st)
+        with torch.set_grad_enabled(need_grad):
+            Pl = P.requires_grad_(True) if need_grad else P
+            sa = torch.sigmoid(sab.conv(Pl)).contiguous()             # [B, 2, H, W]
+        out = torch.empty_like(x)
+        _call(lib.se_ccbam_apply, "se_ccbam_apply", x.data_ptr(), ca.data_ptr(), sa.data_ptr(),
+              out.data_ptr(), B, C, HW, st)
+        if need_grad:
+            ctx.save_for_backward(x, idx, amax)
+            ctx.graphs = (pooled, ca, Pl, sa)
+            ctx.mod = mod
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, idx, amax = ctx.saved_tensors
+        pooled, ca, Pl, sa = ctx.graphs
+        mod = ctx.mod
+        B, C, H, W = x.shape
+        HW = H * W
+        lib, st, dev = N.lib(), N.stream_of(gout), gout.device
+        gout = gout.contiguous()
+        dsa = torch.empty(B, 2, H, W, device=dev)
+        _call(lib.se_ccbam_bwd_sa, "se_ccbam_bwd_sa", gout.data_ptr(), dsa.data_ptr(), B, C, HW, st)
+        sp = list(mod.spatial_attention_branch.parameters())
+        ch = list(mod.channel_attention_branch.parameters())
+        gs = torch.autograd.grad(sa, [Pl] + sp, dsa, allow_unused=True)
+        dP = gs[0].contiguous()
+        dca = torch.empty(B, C, device=dev)
+        ws = F._workspace(lib.se_ccbam_workspace_size(B, C, HW), dev)
+        _call(lib.se_ccbam_bwd_dca, "se_ccbam_bwd_dca", gout.data_ptr(), x.data_ptr(), dP.data_ptr(),
+              idx.data_ptr(), dca.data_ptr(), B, C, HW, ws.data_ptr(), ws.numel(), st)
+        gc = torch.autograd.grad(ca, [pooled] + ch, dca, allow_unused=True)
+        dmean, dmax = (t.contiguous() for t in torch.chunk(gc[0], 2, dim=0))
+        dx = torch.empty_like(x)
+        _call(lib.se_ccbam_bwd_dx, "se_ccbam_bwd_dx", gout.data_ptr(), dP.data_ptr(), idx.data_ptr(),
+              ca.data_ptr(), dmean.data_ptr(), dmax.data_ptr(), amax.data_ptr(), dx.data_ptr(),
+              B, C, HW, st)
+        grads = {id(p): g for p, g in zip(sp, gs[1:])}
+        grads.update({id(p): g for p, g in zip(ch, gc[1:])})
+        del ctx.graphs
+        return (dx, None) + tuple(grads.get(id(p)) for p in mod.parameters())
+
+
 class CCBAM(nn.Module):
     """ccbam.py:88-106: channel gate (multiplicative), then the 2-channel
-    spatial map ADDED to the real and the imaginary halves."""
+    spatial map ADDED to the real and the imaginary halves (fused: _CCBAMFn)."""
 
     def __init__(self, feature_map_channels, reduction=16):
         super().__init__()
@@ -83,6 +167,10 @@ class CCBAM(nn.Module):
         self.spatial_attention_branch = SpatialAttention()
 
     def forward(self, x):
+        return _CCBAMFn.apply(x, self, *self.parameters())
+
+    def forward_unfused(self, x):
+        """The reference's op-by-op formulation (PyTorch device ops)."""
         x = x * self.channel_attention_branch(x)
         sa = self.spatial_attention_branch(x)
         re, im = split_complex(x)
