@@ -104,6 +104,11 @@ typedef struct se_conv2d_desc {
   int out_pad_h, out_pad_w; /* ConvTranspose2d output_padding              */
   int transposed;     /* 0: ComplexConv2d, 1: ComplexConvTranspose2d         */
   int complex_weights;/* 1: (wr, wi) pair; 0: plain real conv, weight in wr  */
+  int pad_h_end, pad_w_end; /* bottom / right padding; -1 = same as pad_h /
+                       * pad_w (symmetric, nn.Conv2d). Asymmetric padding
+                       * folds a zero pad of the input (e.g. FRCRN's causal
+                       * F.pad(x, (1, 0)) before each encoder conv,
+                       * frcrn.py:28-30) into the gather at no cost.          */
 } se_conv2d_desc;
 
 /* Output spatial size (nn.Conv2d / nn.ConvTranspose2d formulas). */

@@ -739,6 +739,7 @@ enum Pass { kFwd = 0, kData = 1 };
 struct ConvGeom {
   int B, Ci, Hi, Wi, Co, Ho, Wo;
   int kh, kw, sh, sw, ph, pw, dh, dw, oph, opw, transposed, complex_w;
+  int phe, pwe;   // end (bottom / right) padding; ph / pw are the begin offsets
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -747,17 +748,19 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.kh = d->kernel_h; g.kw = d->kernel_w; g.sh = d->stride_h; g.sw = d->stride_w;
   g.ph = d->pad_h; g.pw = d->pad_w; g.dh = d->dil_h; g.dw = d->dil_w;
   g.oph = d->out_pad_h; g.opw = d->out_pad_w; g.transposed = d->transposed; g.complex_w = d->complex_weights;
+  g.phe = d->pad_h_end < 0 ? g.ph : d->pad_h_end;
+  g.pwe = d->pad_w_end < 0 ? g.pw : d->pad_w_end;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
     return SE_E_ARG;
   if (g.kh > 16 || g.kw > 16 || g.kh * g.kw > kMaxTaps) return SE_E_UNSUPPORTED;
   if (g.complex_w && ((g.Ci & 1) || (g.Co & 1))) return SE_E_SHAPE;
   if (g.transposed) {
-    g.Ho = (g.Hi - 1) * g.sh - 2 * g.ph + g.dh * (g.kh - 1) + g.oph + 1;
-    g.Wo = (g.Wi - 1) * g.sw - 2 * g.pw + g.dw * (g.kw - 1) + g.opw + 1;
+    g.Ho = (g.Hi - 1) * g.sh - (g.ph + g.phe) + g.dh * (g.kh - 1) + g.oph + 1;
+    g.Wo = (g.Wi - 1) * g.sw - (g.pw + g.pwe) + g.dw * (g.kw - 1) + g.opw + 1;
   } else {
-    g.Ho = (g.Hi + 2 * g.ph - g.dh * (g.kh - 1) - 1) / g.sh + 1;
-    g.Wo = (g.Wi + 2 * g.pw - g.dw * (g.kw - 1) - 1) / g.sw + 1;
+    g.Ho = (g.Hi + g.ph + g.phe - g.dh * (g.kh - 1) - 1) / g.sh + 1;
+    g.Wo = (g.Wi + g.pw + g.pwe - g.dw * (g.kw - 1) - 1) / g.sw + 1;
   }
   if (g.Ho <= 0 || g.Wo <= 0) return SE_E_SHAPE;
   return SE_OK;

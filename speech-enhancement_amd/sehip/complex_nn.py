@@ -58,6 +58,18 @@ def _check_even(n, what):
 
 
 # ---------------------------------------------------------------- conv ops
+def _fold_pad(padding, input_pad, transposed):
+    """(begin, end) conv padding equivalent to zero-padding the input by
+    input_pad = (left, right, top, bottom) and then applying `padding`."""
+    ph, pw = padding
+    if not input_pad or not any(input_pad):
+        return (ph, pw), None
+    if transposed:
+        raise NotImplementedError("sehip: input padding folds into plain convs only")
+    left, right, top, bottom = input_pad
+    return (ph + top, pw + left), (ph + bottom, pw + right)
+
+
 class _FusedComplexConv(nn.Module):
     """Shared forward of ComplexConv2d / ComplexConvTranspose2d
     (complex_nn.py:44-65): one GEMM against the block weight instead of four
@@ -75,12 +87,16 @@ class _FusedComplexConv(nn.Module):
             raise NotImplementedError("sehip complex conv: string padding")
         return c
 
-    def forward(self, x):
+    def forward(self, x, input_pad=None):
+        """input_pad = (left, right, top, bottom) zeros around x (TF.pad order),
+        folded into the conv's own padding instead of materialised (plain
+        convs only)."""
         xs, rebuild = _stacked(x)
         c = self._geometry()
+        begin, end = _fold_pad(c.padding, input_pad, self.transposed)
         y = F.conv2d(xs, c.weight, self.imag_conv.weight, c.bias, self.imag_conv.bias,
                      out_channels=2 * c.out_channels, kernel=c.kernel_size, stride=c.stride,
-                     padding=c.padding, dilation=c.dilation,
+                     padding=begin, padding_end=end, dilation=c.dilation,
                      output_padding=getattr(c, "output_padding", (0, 0)),
                      transposed=self.transposed)
         return rebuild(y)
@@ -110,14 +126,16 @@ class ComplexConvTranspose2d(_FusedComplexConv):
         self.imag_conv = nn.ConvTranspose2d(cin, cout, kernel_size, **kwargs)
 
 
-def real_conv2d(conv: nn.Module, x):
+def real_conv2d(conv: nn.Module, x, input_pad=None):
     """A plain nn.Conv2d / nn.ConvTranspose2d evaluated by the same HIP GEMM
-    (e.g. FRCRN's real final_conv, frcrn.py:115)."""
+    (e.g. FRCRN's real final_conv, frcrn.py:115); input_pad as in
+    _FusedComplexConv.forward."""
     tr = isinstance(conv, nn.ConvTranspose2d)
     if conv.groups != 1 or isinstance(conv.padding, str):
         raise NotImplementedError("sehip real conv: groups / string padding")
+    begin, end = _fold_pad(conv.padding, input_pad, tr)
     return F.conv2d(x, conv.weight, None, conv.bias, None, out_channels=conv.out_channels,
-                    kernel=conv.kernel_size, stride=conv.stride, padding=conv.padding,
+                    kernel=conv.kernel_size, stride=conv.stride, padding=begin, padding_end=end,
                     dilation=conv.dilation, output_padding=getattr(conv, "output_padding", (0, 0)),
                     transposed=tr)
 

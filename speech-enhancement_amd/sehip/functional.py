@@ -73,7 +73,9 @@ def _conv_flops(d) -> float:
 # Complex / real (transposed) conv2d — se_conv2d_* (cconv.hip)
 # --------------------------------------------------------------------------
 def conv_desc(x_shape, out_channels, kernel, stride, padding, dilation, output_padding,
-              transposed, complex_w) -> N.ConvDesc:
+              transposed, complex_w, padding_end=None) -> N.ConvDesc:
+    """padding = (top, left) begin padding; padding_end = (bottom, right), or
+    None for symmetric padding (nn.Conv2d)."""
     b, cin, h, w = x_shape
     d = N.ConvDesc()
     d.batch, d.in_channels, d.in_h, d.in_w = b, cin, h, w
@@ -84,17 +86,19 @@ def conv_desc(x_shape, out_channels, kernel, stride, padding, dilation, output_p
     d.dil_h, d.dil_w = dilation
     d.out_pad_h, d.out_pad_w = output_padding
     d.transposed, d.complex_weights = int(transposed), int(complex_w)
+    d.pad_h_end, d.pad_w_end = (-1, -1) if padding_end is None else padding_end
     return d
 
 
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wr, wi, br, bi, geom):
-        out_channels, kernel, stride, padding, dilation, output_padding, transposed, complex_w = geom
+        (out_channels, kernel, stride, padding, dilation, output_padding, transposed, complex_w,
+         padding_end) = geom
         N.require_device(x, wr, wi, br, bi)
         x = x.contiguous()
         d = conv_desc(tuple(x.shape), out_channels, kernel, stride, padding, dilation,
-                      output_padding, transposed, complex_w)
+                      output_padding, transposed, complex_w, padding_end)
         lib = N.lib()
         ho, wo = N.c_int(), N.c_int()
         N.check(lib.se_conv2d_out_shape(N.ctypes.byref(d), N.ctypes.byref(ho), N.ctypes.byref(wo)),
@@ -145,10 +149,13 @@ class _Conv2d(torch.autograd.Function):
 
 
 def conv2d(x, wr, wi=None, br=None, bi=None, *, out_channels, kernel, stride=1, padding=0,
-           dilation=1, output_padding=0, transposed=False):
-    """Fused complex conv (wi given) or real conv (wi None) on the HIP path."""
+           dilation=1, output_padding=0, transposed=False, padding_end=None):
+    """Fused complex conv (wi given) or real conv (wi None) on the HIP path.
+    padding is the (top, left) begin padding; padding_end (bottom, right)
+    defaults to the same (symmetric, as nn.Conv2d)."""
     geom = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
-            _pair(output_padding), bool(transposed), wi is not None)
+            _pair(output_padding), bool(transposed), wi is not None,
+            None if padding_end is None else _pair(padding_end))
     return _Conv2d.apply(x, wr, wi, br, bi, geom)
 
 

@@ -29,9 +29,16 @@ class _CausalConvBase(nn.Module):
 
     def forward(self, x):
         lp = self.padding[1]
-        x = TF.pad(x, (lp, 0 if self.causal else lp, 0, 0))
+        pad = (lp, 0 if self.causal else lp, 0, 0)
         conv = self._conv()
-        y = conv(x) if not isinstance(conv, (nn.Conv2d, nn.ConvTranspose2d)) else real_conv2d(conv, x)
+        plain = isinstance(conv, (nn.Conv2d, nn.ConvTranspose2d))
+        transposed = isinstance(conv, (nn.ConvTranspose2d, ComplexConvTranspose2d))
+        if lp and transposed:                      # zero input columns of a convT: materialise
+            x, pad = TF.pad(x, pad), None
+        elif not lp:
+            pad = None
+        # the time pad of a plain conv is folded into its (asymmetric) padding
+        y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
         return norm_act(self.norm, self.act, y)
 
 

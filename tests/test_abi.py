@@ -122,3 +122,22 @@ def test_complex_lstm_state_dict_matches_reference_layout():
     b = O(256, 256, num_layers=2, batch_first=True).state_dict()
     assert list(a) == list(b)
     assert all(a[k].shape == b[k].shape for k in a)
+
+
+@pytest.mark.parametrize("tr,xs,pb,pe", [
+    (False, (2, 8, 20, 31), (0, 1), (0, 0)),      # FRCRN causal time pad folded into the conv
+    (False, (1, 4, 9, 10), (2, 0), (1, 3)),
+    (True, (2, 8, 6, 7), (1, 0), (0, 1)),
+])
+def test_asymmetric_padding_out_shape(tr, xs, pb, pe):
+    k, s = (5, 2), (2, 1)
+    desc = F.conv_desc(xs, 6, k, s, pb, (1, 1), (0, 0), tr, True, padding_end=pe)
+    ho, wo = ctypes.c_int(), ctypes.c_int()
+    assert N.lib().se_conv2d_out_shape(ctypes.byref(desc), ctypes.byref(ho), ctypes.byref(wo)) == 0
+    if tr:   # convT with crop (pb, pe): full output cropped at begin/end
+        full = torch.nn.ConvTranspose2d(xs[1], 6, k, stride=s, bias=False)(torch.zeros(xs)).shape
+        ref = (full[2] - pb[0] - pe[0], full[3] - pb[1] - pe[1])
+    else:    # conv of the zero-padded input
+        xp = torch.nn.functional.pad(torch.zeros(xs), (pb[1], pe[1], pb[0], pe[0]))
+        ref = tuple(torch.nn.Conv2d(xs[1], 6, k, stride=s, bias=False)(xp).shape[2:])
+    assert (ho.value, wo.value) == tuple(ref)

@@ -93,3 +93,30 @@ def test_frcrn_layer_vs_oracle(name, tr, cin, cout, shape, gpu_device):
     assert rel_l2(r["dwi"].numpy(), m.imag_conv.weight.grad.numpy()) < 1e-5
     if name != "enc0":
         assert rel_l2(r["dx"].numpy(), xo.grad.numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("input_pad", [(1, 0, 0, 0), (2, 1, 1, 3), (0, 3, 2, 0)])
+def test_input_pad_folded_into_conv(input_pad, gpu_device):
+    """ComplexConv2d(x, input_pad) == oracle conv of F.pad(x, input_pad): the
+    causal pad of FRCRN's encoder blocks (frcrn.py:28-30) as asymmetric conv
+    padding, forward and all three backward passes."""
+    from sehip.complex_nn import ComplexConv2d
+    torch.manual_seed(11)
+    ref = paramfill.fill_(O_cnn.ComplexConv2d(16, 12, (5, 2), stride=(2, 1), padding=(1, 0), bias=True), seed=3)
+    mod = ComplexConv2d(16, 12, (5, 2), stride=(2, 1), padding=(1, 0), bias=True)
+    mod.load_state_dict(ref.state_dict())
+    x = torch.randn(2, 16, 21, 13)
+    xr = x.clone().requires_grad_(True)
+    yr = ref(torch.nn.functional.pad(xr, input_pad))
+    gy = torch.randn_like(yr)
+    (yr * gy).sum().backward()
+    mod = mod.to(gpu_device)
+    xd = x.to(gpu_device).requires_grad_(True)
+    yd = mod(xd, input_pad)
+    assert yd.shape == yr.shape
+    assert rel_l2(yd.detach().cpu().numpy(), yr.detach().numpy()) < 1e-5
+    (yd * gy.to(gpu_device)).sum().backward()
+    assert rel_l2(xd.grad.cpu().numpy(), xr.grad.numpy()) < 1e-5
+    rp = dict(ref.named_parameters())
+    for n, p in mod.named_parameters():
+        assert rel_l2(p.grad.cpu().numpy(), rp[n].grad.numpy()) < 1e-5, n
