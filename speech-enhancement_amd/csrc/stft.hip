@@ -100,6 +100,92 @@ __device__ float2* fft_forward(float2* a, float2* b, int P, const FftPlan& pl, c
   return a;
 }
 
+// Compile-time plan for the common nfft values: every pass's radix, stride and
+// butterfly count are constants, so the index divisions become multiply-shifts
+// and the pass loop unrolls (the runtime plan above serves any other nfft).
+struct CPlan {
+  int npass;
+  int radix[kMaxPasses];
+};
+constexpr CPlan make_cplan(int N) {
+  CPlan p{};
+  int n = N;
+  const int order[4] = {4, 2, 3, 5};
+  for (int oi = 0; oi < 4; ++oi)
+    while (n > 1 && n % order[oi] == 0 && p.npass < kMaxPasses) { p.radix[p.npass++] = order[oi]; n /= order[oi]; }
+  return p;
+}
+
+template <int R>
+__device__ __forceinline__ void butterfly(float2 (&v)[5], float2* dst, int d, int Ns) {
+  if constexpr (R == 2) {
+    dst[d] = cadd(v[0], v[1]);
+    dst[d + Ns] = csub(v[0], v[1]);
+  } else if constexpr (R == 4) {
+    const float2 t0 = cadd(v[0], v[2]), t1 = csub(v[0], v[2]);
+    const float2 t2 = cadd(v[1], v[3]), t3 = mul_mi(csub(v[1], v[3]));
+    dst[d] = cadd(t0, t2);
+    dst[d + Ns] = cadd(t1, t3);
+    dst[d + 2 * Ns] = csub(t0, t2);
+    dst[d + 3 * Ns] = csub(t1, t3);
+  } else if constexpr (R == 3) {
+    const float h = 0.86602540378443864676f;
+    const float2 s = cadd(v[1], v[2]), df = csub(v[1], v[2]);
+    const float2 m = csub(v[0], cscale(s, 0.5f));
+    const float2 r = cscale(mul_mi(df), h);
+    dst[d] = cadd(v[0], s);
+    dst[d + Ns] = cadd(m, r);
+    dst[d + 2 * Ns] = csub(m, r);
+  } else {
+    const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+    const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+    const float2 t1 = cadd(v[1], v[4]), t2 = cadd(v[2], v[3]);
+    const float2 t3 = csub(v[1], v[4]), t4 = csub(v[2], v[3]);
+    const float2 a1 = cadd(v[0], cadd(cscale(t1, c1), cscale(t2, c2)));
+    const float2 a2 = cadd(v[0], cadd(cscale(t1, c2), cscale(t2, c1)));
+    const float2 b1 = mul_mi(cadd(cscale(t3, s1), cscale(t4, s2)));
+    const float2 b2 = mul_mi(csub(cscale(t3, s2), cscale(t4, s1)));
+    dst[d] = cadd(v[0], cadd(t1, t2));
+    dst[d + Ns] = cadd(a1, b1);
+    dst[d + 4 * Ns] = csub(a1, b1);
+    dst[d + 2 * Ns] = cadd(a2, b2);
+    dst[d + 3 * Ns] = csub(a2, b2);
+  }
+}
+
+template <int N, int P, int PS, int NS>
+__device__ float2* fft_pass(float2* a, float2* b, const float2* __restrict__ tw) {
+  constexpr CPlan pl = make_cplan(N);
+  if constexpr (PS == pl.npass) {
+    return a;
+  } else {
+    constexpr int R = pl.radix[PS], nbf = N / R, tstep = N / (NS * R);
+    for (int idx = threadIdx.x; idx < P * nbf; idx += kThreads) {
+      const int pr = idx / nbf, j = idx - pr * nbf;
+      const float2* src = a + pr * N;
+      float2* dst = b + pr * N;
+      const int k = j % NS;
+      float2 v[5];
+#pragma unroll
+      for (int q = 0; q < R; ++q) v[q] = src[j + q * nbf];
+      if constexpr (NS > 1) {
+#pragma unroll
+        for (int q = 1; q < R; ++q) v[q] = cmul(v[q], tw[q * k * tstep]);
+      }
+      butterfly<R>(v, dst, (j / NS) * NS * R + k, NS);
+    }
+    __syncthreads();
+    return fft_pass<N, P, PS + 1, NS * R>(b, a, tw);
+  }
+}
+
+// FFT of P sequences: compile-time plan when CN != 0, else the runtime plan.
+template <int CN, int CP>
+__device__ __forceinline__ float2* fft_any(float2* a, float2* b, int P, const FftPlan& pl, const float2* tw) {
+  if constexpr (CN != 0) return fft_pass<CN, CP, 0, 1>(a, b, tw);
+  else return fft_forward(a, b, P, pl, tw);
+}
+
 __device__ __forceinline__ int reflect_index(int i, int L) {
   if (i < 0) i = -i;
   if (i >= L) i = 2 * (L - 1) - i;
@@ -111,8 +197,10 @@ __device__ __forceinline__ int ceil_div_i(int a, int b) { return -floor_div(-a, 
 
 // Unpack two packed real-FFT results (pair j) and store rows k = 0..N/2 of frames
 // t0 + 2j, t0 + 2j + 1. out layout [B, N+2, T] or mags/phase [B, N/2+1, T].
-__device__ void unpack_store(const float2* Z, int P, int N, int t0, int T, int b,
+template <int CN, int CP>
+__device__ void unpack_store(const float2* Z, int Pr, int Nr, int t0, int T, int b,
                              float* out0, float* out1, int mag_phase) {
+  const int N = CN ? CN : Nr, P = CP ? CP : Pr;
   const int half = N / 2 + 1;
   const int FT = 2 * P;
   for (int idx = threadIdx.x; idx < half * FT; idx += blockDim.x) {
@@ -152,9 +240,10 @@ struct StftArgs {
 };
 
 // grid (ceil(T / 2P), B)
+template <int CN, int CP>
 __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
-  const int N = a.pl.N, P = a.P;
+  const int N = CN ? CN : a.pl.N, P = CP ? CP : a.P;
   float2* A = lds;
   float2* Bf = lds + P * N;
   const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
@@ -171,8 +260,8 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
     A[idx] = make_float2(ya, yb);
   }
   __syncthreads();
-  const float2* Z = fft_forward(A, Bf, P, a.pl, a.tw);
-  unpack_store(Z, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase);
+  const float2* Z = fft_any<CN, CP>(A, Bf, P, a.pl, a.tw);
+  unpack_store<CN, CP>(Z, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase);
 }
 
 struct IstftArgs {
@@ -208,10 +297,11 @@ __device__ __forceinline__ float apply_g(float v, int n, float se_, float so_, f
 }
 
 // ConviSTFT forward. grid (ceil(out_len / (FT*hop)), B)
+template <int CN, int CP>
 __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   __shared__ float sums[64];
-  const int N = a.pl.N, P = a.P, half = N / 2 + 1;
+  const int N = CN ? CN : a.pl.N, P = CP ? CP : a.P, half = N / 2 + 1;
   float2* A = lds;
   float2* Bf = lds + P * N;
   const int b = blockIdx.y;
@@ -241,7 +331,7 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
     }
   }
   __syncthreads();
-  float2* R = fft_forward(A, Bf, P, a.pl, a.tw);
+  float2* R = fft_any<CN, CP>(A, Bf, P, a.pl, a.tw);
   // z = conj(R): z_a = R.x, z_b = -R.y. Fold the sign into the sums/application.
   for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) R[idx].y = -R[idx].y;
   __syncthreads();
@@ -272,10 +362,11 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
 }
 
 // Adjoint of istft_fwd. grid (ceil(T / 2P), B)
+template <int CN, int CP>
 __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   __shared__ float sums[64];
-  const int N = a.pl.N, P = a.P;
+  const int N = CN ? CN : a.pl.N, P = CP ? CP : a.P;
   float2* A = lds;
   float2* Bf = lds + P * N;
   const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
@@ -318,8 +409,8 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) 
     }
   }
   __syncthreads();
-  const float2* Z = fft_forward(A, Bf, P, a.pl, a.tw);
-  unpack_store(Z, P, N, t0, a.T, b, a.out, nullptr, 0);
+  const float2* Z = fft_any<CN, CP>(A, Bf, P, a.pl, a.tw);
+  unpack_store<CN, CP>(Z, P, N, t0, a.T, b, a.out, nullptr, 0);
 }
 
 // ---------------------------------------------------------------------------
@@ -339,10 +430,28 @@ static bool make_plan(int N, FftPlan& pl) {
   return n == 1;
 }
 
+// Frame pairs per block. kPairs (4) keeps a block's LDS at <= 40 KB for
+// nfft <= 640 so four blocks (16 waves) share a CU; larger nfft fall back to
+// what the LDS budget allows.
+constexpr int kPairs = 4;
 static int pick_pairs(int N) {
   const int p = kLdsBudget / (2 * N * (int)sizeof(float2));
-  return std::max(1, std::min(16, p));   // sums[] holds 2 floats for 32 frames
+  return std::max(1, std::min(kPairs, p));   // sums[] holds 2 floats for 32 frames
 }
+
+// Launch K<CN, CP> for the compiled plans (CP = kPairs), else K<0, 0>.
+#define SE_STFT_DISPATCH(K, nfft, P, grid, shm, st, a)                                              \
+  do {                                                                                             \
+    const bool cp_ = (P) == kPairs;                                                                \
+    switch (cp_ ? (nfft) : 0) {                                                                    \
+      case 640: hipLaunchKernelGGL((K<640, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
+      case 512: hipLaunchKernelGGL((K<512, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
+      case 400: hipLaunchKernelGGL((K<400, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
+      case 320: hipLaunchKernelGGL((K<320, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
+      case 256: hipLaunchKernelGGL((K<256, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
+      default: hipLaunchKernelGGL((K<0, 0>), grid, dim3(kThreads), shm, st, a); break;             \
+    }                                                                                              \
+  } while (0)
 
 static int check_common(int win, int hop, int nfft, FftPlan& pl) {
   if (win <= 0 || hop <= 0 || nfft <= 0 || win > nfft) return SE_E_ARG;
@@ -377,8 +486,7 @@ extern "C" int se_stft_fwd(const float* x, float* out0, float* out1, int B, int 
   a.L = L; a.win = win; a.hop = hop; a.T = T; a.pad = pad; a.mag_phase = mag_phase;
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
-  hipLaunchKernelGGL(stft_fwd_kernel, dim3(se::ceil_div(T, 2 * a.P), B), dim3(kThreads), shm,
-                     se::as_stream(stream), a);
+  SE_STFT_DISPATCH(stft_fwd_kernel, nfft, a.P, dim3(se::ceil_div(T, 2 * a.P), B), shm, se::as_stream(stream), a);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
@@ -408,8 +516,8 @@ extern "C" int se_istft_fwd(const float* spec, float* out, int B, int T, int win
   if (out_len == 0) return SE_OK;
   a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
-  hipLaunchKernelGGL(istft_fwd_kernel, dim3(se::ceil_div(out_len, a.FT * hop), B), dim3(kThreads),
-                     shm, se::as_stream(stream), a);
+  SE_STFT_DISPATCH(istft_fwd_kernel, nfft, a.P, dim3(se::ceil_div(out_len, a.FT * hop), B), shm,
+                   se::as_stream(stream), a);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
@@ -423,8 +531,7 @@ extern "C" int se_istft_bwd(const float* gout, float* gspec, int B, int T, int w
   if (!gout || !gspec || !window || !twiddle) return SE_E_ARG;
   a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
-  hipLaunchKernelGGL(istft_bwd_kernel, dim3(se::ceil_div(T, 2 * a.P), B), dim3(kThreads), shm,
-                     se::as_stream(stream), a);
+  SE_STFT_DISPATCH(istft_bwd_kernel, nfft, a.P, dim3(se::ceil_div(T, 2 * a.P), B), shm, se::as_stream(stream), a);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

@@ -66,3 +66,19 @@ def test_stft_vs_oracle_4s(gpu_device):
     s = torch.randn(2, 642, 403)
     assert rel_l2(ConviSTFT(320, 160, 640).cuda()(s.cuda()).cpu().numpy(),
                   O.ConviSTFT(320, 160, 640)(s).numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("win,hop,nfft", [(256, 128, 256), (300, 150, 480), (400, 100, 400)])
+def test_stft_istft_vs_oracle_more_plans(win, hop, nfft, gpu_device):
+    """Compiled FFT plans (256, 400) and the runtime-plan path (480 = 4*4*2*3*5)
+    against the oracle's DFT-basis conv1d restatement (conv_stft.py:48-116)."""
+    from oracle import stft as O
+    from sehip.conv_stft import ConvSTFT, ConviSTFT
+    torch.manual_seed(nfft)
+    x = torch.randn(3, 8000) * 0.3
+    ref = O.ConvSTFT(win, hop, nfft)(x)
+    out = ConvSTFT(win, hop, nfft).cuda()(x.cuda()).cpu()
+    assert rel_l2(out.numpy(), ref.numpy()) < 1e-5
+    s = torch.randn_like(ref)
+    assert rel_l2(ConviSTFT(win, hop, nfft).cuda()(s.cuda()).cpu().numpy(),
+                  O.ConviSTFT(win, hop, nfft)(s).numpy()) < 1e-5
