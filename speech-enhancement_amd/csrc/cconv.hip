@@ -298,7 +298,8 @@ gather_smalln_kernel(const GatherArgs a) {
   float acc[NOUT];
 #pragma unroll
   for (int n = 0; n < NOUT; ++n) acc[n] = 0.f;
-  for (int k = 0; k < a.Kp; ++k) {
+#pragma unroll 8
+  for (int k = 0; k < a.Kp; ++k) {     // Kp % 32 == 0: eight gathered loads in flight
     const int4 e = a.ktab[k];
     const int hi = hb + e.y, wi = wb + e.z;
     const bool ok = (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
@@ -331,6 +332,70 @@ struct WgradArgs {
   int Kp, Np, M;
   int m_per_split;     // multiple of the kernel's BMR (64)
 };
+
+// Small-N weight grad (N <= 8: FRCRN's final_conv 128->2 and the CCBAM spatial
+// ComplexConv2d 4->2): an MFMA tile would be >= 75% padding, and the pass is
+// bound by reading the gathered tensor once. One workgroup = KG rows of K x
+// one m-split; a thread walks positions m (coalesced along time), keeps its
+// N values of D in registers and accumulates KG*N products; the block then
+// reduces and writes one slab row block (same slab / finish path as the GEMM).
+template <int NOUT>
+__global__ void __launch_bounds__(kThreads)
+wgrad_smalln_kernel(const WgradArgs a) {
+  constexpr int KG = 16;
+  const int k0 = blockIdx.x * KG, split = blockIdx.y;
+  const int mbeg = split * a.m_per_split, mend = min(a.M, mbeg + a.m_per_split);
+  const int QQ = a.Qh * a.Qw;
+  const long long HiWi = (long long)a.Hi * a.Wi;
+  int4 e[KG];
+#pragma unroll
+  for (int k = 0; k < KG; ++k) e[k] = a.ktab[k0 + k];
+  float acc[KG][NOUT];
+#pragma unroll
+  for (int k = 0; k < KG; ++k)
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n) acc[k][n] = 0.f;
+  // position m -> (b, qh, qw), advanced incrementally by kThreads per step
+  int m = mbeg + threadIdx.x;
+  int b = m / QQ, r = m - b * QQ;
+  int qh = r / a.Qw, qw = r - qh * a.Qw;
+  for (; m < mend; m += kThreads) {
+    const int hb = qh * a.sh, wb = qw * a.sw;
+    float dv[NOUT];
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n)
+      dv[n] = n < a.N ? a.D[(((long long)b * a.N + n) * a.Qh + qh) * a.Qw + qw] : 0.f;
+    const long long xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+#pragma unroll
+    for (int k = 0; k < KG; ++k) {
+      const int hi = hb + e[k].y, wi = wb + e[k].z;
+      const bool ok = (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+      const float xv = a.X[ok ? xbase + e[k].x : 0];
+      const float x = ok ? xv : 0.f;
+#pragma unroll
+      for (int n = 0; n < NOUT; ++n) acc[k][n] = fmaf(x, dv[n], acc[k][n]);
+    }
+    qw += kThreads;
+    while (qw >= a.Qw) {
+      qw -= a.Qw;
+      if (++qh == a.Qh) { qh = 0; ++b; }
+    }
+  }
+  __shared__ float red[kThreads / 64][KG * NOUT];
+  const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+#pragma unroll
+  for (int k = 0; k < KG; ++k)
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n) {
+      const float v = se::wave_sum(acc[k][n]);
+      if (lane == 0) red[w][k * NOUT + n] = v;
+    }
+  __syncthreads();
+  for (int i = threadIdx.x; i < KG * NOUT; i += kThreads) {
+    const float v = (red[0][i] + red[1][i]) + (red[2][i] + red[3][i]);
+    a.slab[((long long)split * a.Kp + k0 + i / NOUT) * a.Np + (i % NOUT)] = v;
+  }
+}
 
 // One reduction step covers BMR consecutive positions m; a wave-instruction
 // loads LPW = 64 / BMR rows (k or n) x BMR positions, lanes along m so every
@@ -809,6 +874,8 @@ static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N) {
   return bytes + kZeroBytes + 512;
 }
 
+constexpr int kSmallWgradN = 8;   // N at or below: wgrad_smalln_kernel
+
 // wgrad plan: G is gathered (strided) over the grid of D.
 struct WgradPlan {
   ClassPlan c;        // strided class over D's grid
@@ -830,8 +897,17 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
   }
   finish_plan(w.c, w.Cg);
   w.c.Kp = round_up(std::max(w.c.K, 1), 128);
-  w.Np = round_up(w.N, w.N <= 32 ? 32 : 128);
   w.M = g.B * w.Qh * w.Qw;
+  if (w.N <= kSmallWgradN) {      // direct kernel: Kp/16 row groups x splits
+    w.Np = w.N <= 4 ? 4 : 8;
+    const int groups = w.c.Kp / 16;
+    int splits = std::max(1, 4096 / groups);
+    splits = std::min(splits, std::max(1, w.M / 1024));
+    w.m_per_split = (w.M + splits - 1) / splits;
+    w.splits = (w.M + w.m_per_split - 1) / w.m_per_split;
+    return w;
+  }
+  w.Np = round_up(w.N, w.N <= 32 ? 32 : 128);
   const int tiles = (w.c.Kp / 128) * (w.Np / (w.N <= 32 ? 32 : 128));
   int splits = std::max(1, 1024 / std::max(tiles, 1));
   const int max_by_m = std::max(1, w.M / 512);
@@ -1004,7 +1080,11 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
   const long long span = (w.m_per_split + QQ - 1) / QQ + 1;
   const bool tu = (w.Cg % 128 == 0) && span * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
                   span * (long long)w.Np * QQ * 4 < (1ll << 31);
-  if (w.Np == 32) {
+  if (w.N <= kSmallWgradN) {
+    dim3 grid(w.c.Kp / 16, w.splits);
+    if (w.Np == 4) hipLaunchKernelGGL(wgrad_smalln_kernel<4>, grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL(wgrad_smalln_kernel<8>, grid, dim3(kThreads), 0, st, a);
+  } else if (w.Np == 32) {
     dim3 grid(w.c.Kp / 128, 1, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
