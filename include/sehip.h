@@ -161,9 +161,11 @@ int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
                float momentum, int act, float slope, void* ws,
                size_t ws_bytes, void* stream);
 
-/* Backward. gy = dL/dy (after the activation), y = forward output,
- * x = forward input. dx is overwritten. dparams: host array of 5 device
- * pointers dWrr, dWri, dWii, dBr, dBi (overwritten), or NULL. */
+/* Backward. gy = dL/dy (after the activation), x = forward input. y (the
+ * forward output) is NOT read and may be NULL: the activation derivative is
+ * taken from the pre-activation Z(x - M) + B recomputed from x and `save`.
+ * dx is overwritten. dparams: host array of 5 device pointers dWrr, dWri,
+ * dWii, dBr, dBi (overwritten), or NULL. */
 int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
                int B, int C, int HW, const float* const* params,
                const float* save, float* const* dparams, int training,

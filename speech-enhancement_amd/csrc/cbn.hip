@@ -6,7 +6,10 @@
 //   cbn_finalize_kernel : mean, covariance, running-stat lerp, the closed
 //                         2x2 inverse square root (:288-297), Z = W U
 //   cbn_apply_kernel    : y = act(Z (x - M) + B)
-// and a training backward is 3 launches reading (gy, y, x) twice.
+// and a training backward is 3 launches reading (gy, x) twice: the activation
+// derivative comes from the sign of the pre-activation z = Z (x - M) + B,
+// recomputed from x with the forward's own expression, so y is never read
+// (2 of the 7 backward passes over the activation of the old design).
 // All kernels stream the channel planes contiguously (HBM-bound).
 #include "common.hpp"
 
@@ -152,16 +155,19 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ y
                        const float* __restrict__ save, int act, float slope, double* part) {
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
   const int nseg = (HW + kSeg - 1) / kSeg;
-  const float mr = save[c * kSave + S_MR], mi = save[c * kSave + S_MI];
+  const float* sv = save + c * kSave;
+  const float mr = sv[S_MR], mi = sv[S_MI];
+  const float zrr = sv[S_ZRR], zri = sv[S_ZRI], zir = sv[S_ZIR], zii = sv[S_ZII], br = sv[S_BR], bi = sv[S_BI];
   double v[6] = {0, 0, 0, 0, 0, 0};
   for (int row = p; row < B * nseg; row += P) {
     const int b = row / nseg, sg = row - b * nseg;
     const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
     const int i1 = min(HW, (sg + 1) * kSeg);
     for (int i = sg * kSeg + threadIdx.x; i < i1; i += kThreads) {
-      const float gr = gy[offr + i] * act_grad(y[offr + i], act, slope);
-      const float gi = gy[offi + i] * act_grad(y[offi + i], act, slope);
       const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+      const float zr = zrr * xr + zri * xi + br, zi = zir * xr + zii * xi + bi;   // = forward pre-activation
+      const float gr = gy[offr + i] * act_grad(zr, act, slope);
+      const float gi = gy[offi + i] * act_grad(zi, act, slope);
       v[0] += gr; v[1] += gi;
       v[2] += (double)gr * xr; v[3] += (double)gr * xi;
       v[4] += (double)gi * xr; v[5] += (double)gi * xi;
@@ -170,8 +176,8 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ y
   block_reduce_store<6>(v, part + ((long long)c * P + p) * 6);
 }
 
-// coef layout per channel (12 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi pad
-constexpr int kCoef = 12;
+// coef layout per channel (16 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi Br Bi pad
+constexpr int kCoef = 16;
 
 __global__ void cbn_bwd_finalize_kernel(const double* part, int P, double count, int Cc,
                                         const float* save, Ptr5 params, int affine,
@@ -229,7 +235,8 @@ __global__ void cbn_bwd_finalize_kernel(const double* part, int P, double count,
     o[2] = (float)zri; o[3] = (float)zii;   // dxi = Zri g_r + Zii g_i
     o[4] = (float)gbr; o[5] = (float)gbi;
     o[6] = (float)grr; o[7] = (float)gri; o[8] = (float)gii;
-    o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = 0.f;
+    o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = s[S_BR]; o[12] = s[S_BI];
+    o[13] = o[14] = o[15] = 0.f;
   }
 }
 
@@ -241,15 +248,18 @@ cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ y,
   const float* k = coef + c * kCoef;
   const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
   const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
+  const float br = k[11], bi = k[12];
+  // forward Z = [[a00, a10], [a01, a11]] (coef holds Z^T)
   const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
   const int base = blockIdx.x * kThreads * 4 + threadIdx.x;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = base + u * kThreads;
     if (i < HW) {
-      const float gr = gy[offr + i] * act_grad(y[offr + i], act, slope) - gbr;
-      const float gi = gy[offi + i] * act_grad(y[offi + i], act, slope) - gbi;
       const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+      const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
+      const float gr = gy[offr + i] * act_grad(zr, act, slope) - gbr;
+      const float gi = gy[offi + i] * act_grad(zi, act, slope) - gbi;
       dx[offr + i] = a00 * gr + a01 * gi + grr * xr + gri * xi;
       dx[offi + i] = a10 * gr + a11 * gi + gri * xr + gii * xi;
     }
@@ -303,7 +313,8 @@ extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float
                           int C, int HW, const float* const* params, const float* save,
                           float* const* dparams, int training, int act, float slope, void* ws,
                           size_t ws_bytes, void* stream) {
-  if (!gy || !y || !x || !dx || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0) return SE_E_ARG;
+  (void)y;   // not read: act' is recomputed from x (see the file comment); may be NULL
+  if (!gy || !x || !dx || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0) return SE_E_ARG;
   if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
   const int Cc = C / 2;

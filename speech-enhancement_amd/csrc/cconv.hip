@@ -440,7 +440,8 @@ wgrad_gemm_kernel(const WgradArgs a) {
     cqh = r / a.Qw;
     cqw = r - cqh * a.Qw;
   }
-  float rg[GJ], rd[DJ];
+  struct Stage { float rg[GJ], rd[DJ]; };
+  Stage st0, st1;   // two register staging sets: prefetch distance 2
   // TU buffer descriptors over the split's first batch item (uniform inputs)
   auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
     const unsigned long long v = (unsigned long long)p;
@@ -455,7 +456,7 @@ wgrad_gemm_kernel(const WgradArgs a) {
       uniform_ptr(a.D + (long long)bfirst * a.N * QQ), (short)0, 0x7FFFFFFF, 0x00020000);
   const int4 tap_e = a.ktab[k0];              // TU: the tile's single tap
   const int cbase = k0 % a.Cg;
-  auto load_step = [&](int mstep) __attribute__((always_inline)) {
+  auto load_step = [&](Stage& S, int mstep) __attribute__((always_inline)) {
     if constexpr (TU) {
       const bool mv = mstep + ml < mend;
       const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
@@ -468,12 +469,12 @@ wgrad_gemm_kernel(const WgradArgs a) {
       const int gs = (int)(HiWi * 4), ds = (int)(QQ * 4);
 #pragma unroll
       for (int j = 0; j < GJ; ++j)
-        rg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        S.rg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
             rg_src, vg, (wave * LPW + RS * j) * gs, 0));
 #pragma unroll
       for (int j = 0; j < DJ; ++j) {
         const bool nok = n0 + wave * LPW + RS * j + lr < a.N;   // only the Np-padded tail fails
-        rd[j] = nok ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+        S.rd[j] = nok ? __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
                           rd_src, vd, (wave * LPW + RS * j) * ds, 0)) : 0.f;
       }
       cqw += BMR;
@@ -491,14 +492,14 @@ wgrad_gemm_kernel(const WgradArgs a) {
       const int4 e = sK[row0 + RS * j];
       const int hi = hb + e.y, wi = wb + e.z;
       const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      rg[j] = *(ok ? a.X + xb + e.x : a.zero);
+      S.rg[j] = *(ok ? a.X + xb + e.x : a.zero);
     }
     const long long db = (long long)cb * a.N * QQ + (long long)cqh * a.Qw + cqw;
 #pragma unroll
     for (int j = 0; j < DJ; ++j) {
       const int n = n0 + row0 + RS * j;
       const bool ok = mv & (n < a.N);
-      rd[j] = *(ok ? a.D + db + (long long)n * QQ : a.zero);
+      S.rd[j] = *(ok ? a.D + db + (long long)n * QQ : a.zero);
     }
     cqw += BMR;
     while (cqw >= a.Qw) {
@@ -506,11 +507,11 @@ wgrad_gemm_kernel(const WgradArgs a) {
       if (++cqh >= a.Qh) { cqh = 0; ++cb; }
     }
   };
-  auto store_step = [&](int buf) __attribute__((always_inline)) {
+  auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int j = 0; j < GJ; ++j) sG[buf][(row0 + RS * j) * L + ml] = rg[j];
+    for (int j = 0; j < GJ; ++j) sG[buf][(row0 + RS * j) * L + ml] = S.rg[j];
 #pragma unroll
-    for (int j = 0; j < DJ; ++j) sD[buf][(row0 + RS * j) * L + ml] = rd[j];
+    for (int j = 0; j < DJ; ++j) sD[buf][(row0 + RS * j) * L + ml] = S.rd[j];
   };
 
   f32x16 acc[RK][RN];
@@ -522,15 +523,9 @@ wgrad_gemm_kernel(const WgradArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int nsteps = (mend > mbeg) ? (mend - mbeg + BMR - 1) / BMR : 0;
-  if (nsteps > 0) {
-    load_step(mbeg);
-    store_step(0);
-  }
-  __syncthreads();
   const int lk = lane >> 5, lc = lane & 31;
-  for (int s = 0; s < nsteps; ++s) {
-    const int cur = s & 1;
-    if (s + 1 < nsteps) load_step(mbeg + (s + 1) * BMR);
+  // one step: MFMAs over LDS[cur]
+  auto compute = [&](int cur) __attribute__((always_inline)) {
     // Reduction index of MFMA kk (0..BMR/2-1) for lane half lk is m = kk + (BMR/2)*lk,
     // so k-pairs 2q and 2q+1 of one operand row come from ONE ds_read_b64. The
     // step's fragments are fetched in two fenced halves (second half's reads
@@ -571,9 +566,28 @@ wgrad_gemm_kernel(const WgradArgs a) {
       if (q == HQ - 1) __builtin_amdgcn_sched_barrier(0);
     }
     __builtin_amdgcn_sched_barrier(0);   // keep the LDS writes (and their vmcnt) after the MFMAs
-    if (s + 1 < nsteps) store_step(cur ^ 1);
+  };
+  // prologue: step 0 -> LDS[0]; step 1 in flight in st1
+  if (nsteps > 0) {
+    load_step(st0, mbeg);
+    store_step(st0, 0);
+  }
+  if (nsteps > 1) load_step(st1, mbeg + BMR);
+  __syncthreads();
+  int s = 0;
+  for (; s + 1 < nsteps; s += 2) {
+    // even step: consume LDS[0]; st1 holds step s+1; load s+2 into st0
+    if (s + 2 < nsteps) load_step(st0, mbeg + (s + 2) * BMR);
+    compute(0);
+    store_step(st1, 1);
+    __syncthreads();
+    // odd step: consume LDS[1]; st0 holds step s+2; load s+3 into st1
+    if (s + 3 < nsteps) load_step(st1, mbeg + (s + 3) * BMR);
+    compute(1);
+    if (s + 2 < nsteps) store_step(st0, 0);
     __syncthreads();
   }
+  if (s < nsteps) compute(0);   // odd step count: the last step sits in LDS[0]
   // acc[i][j][r]: row k = 32i + (r&3) + 8(r>>2) + 4*lk, col n = 32j + lc
   float* out = a.slab + (long long)split * a.Kp * a.Np;
 #pragma unroll

@@ -186,13 +186,13 @@ class _ComplexBN(torch.autograd.Function):
                 "se_cbn_fwd")
         if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write
             _TIMER.end("cbn_fwd", t0, 0.0, 4.0 * x.numel() * (3 if training else 2))
-        ctx.save_for_backward(x, y, save, *(params or ()))
+        ctx.save_for_backward(x, save, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         return y
 
     @staticmethod
     def backward(ctx, gy):
-        x, y, save, *params = ctx.saved_tensors
+        x, save, *params = ctx.saved_tensors
         training, act, slope, affine = ctx.cfg
         gy = gy.contiguous()
         b, c = x.shape[:2]
@@ -202,12 +202,12 @@ class _ComplexBN(torch.autograd.Function):
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(lib.se_cbn_bwd(gy.data_ptr(), y.data_ptr(), x.data_ptr(), dx.data_ptr(), b, c, hw,
+        N.check(lib.se_cbn_bwd(gy.data_ptr(), None, x.data_ptr(), dx.data_ptr(), b, c, hw,
                                N.ptr_array(params if affine else None), save.data_ptr(),
                                N.ptr_array(dparams), training, act, slope, ws.data_ptr(),
                                ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
-        if t0 is not None:   # (gy, y, x) read twice + dx written
-            _TIMER.end("cbn_bwd", t0, 0.0, 4.0 * x.numel() * 7)
+        if t0 is not None:   # (gy, x) read twice + dx written
+            _TIMER.end("cbn_bwd", t0, 0.0, 4.0 * x.numel() * 5)
         g = dparams or [None] * 5
         return (dx, *g, None, None, None, None, None, None, None)
 
