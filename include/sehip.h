@@ -233,6 +233,19 @@ int se_ccbam_bwd_dx(const float* gout, const float* dpooled, const short* idx,
                     const int* amax, float* dx, int B, int C, int HW,
                     void* stream);
 
+/* ------------------------------------------------------------------------
+ * Decoder skip join (models/_2206_07293_frcrn.py:93-100 + complex_concat,
+ * complex_nn.py:4-16): out = [x_re, s_re, x_im, s_im] on channels, with x
+ * [B, Cx, Fx, Tx] cropped / zero-padded at the end of each spatial dim to
+ * s's [F, T] (x[..., :-1] and F.pad(x, (0, 0, 0, 1)) in the reference).
+ * out: [B, Cx + Cs, F, T]. Backward writes gx over x's own grid (zeros where
+ * x was cropped) and gs.
+ * ------------------------------------------------------------------------ */
+int se_complex_join(const float* x, int Cx, int Fx, int Tx, const float* s,
+                    int Cs, int F, int T, float* out, int B, void* stream);
+int se_complex_join_bwd(const float* gout, float* gx, int Cx, int Fx, int Tx,
+                        float* gs, int Cs, int F, int T, int B, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -410,3 +410,37 @@ class _LstmLayer(torch.autograd.Function):
 def lstm_layer(x, w_ih, w_hh, b_ih=None, b_hh=None, rev_mask: int = 0):
     """h [L, B, T, H] of L stacked LSTMs over x ([B, T, I] shared or [L, B, T, I])."""
     return _LstmLayer.apply(x, w_ih, w_hh, b_ih, b_hh, rev_mask)
+
+
+# --------------------------------------------------------------------------
+# Decoder skip join (frcrn.py:93-100 + complex_concat) — se_complex_join*
+# --------------------------------------------------------------------------
+class _ComplexJoin(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, s):
+        N.require_device(x, s)
+        x, s = x.contiguous(), s.contiguous()
+        B, Cx, Fx, Tx = x.shape
+        _, Cs, Fs, Ts = s.shape
+        out = torch.empty((B, Cx + Cs, Fs, Ts), device=x.device, dtype=x.dtype)
+        N.check(N.lib().se_complex_join(x.data_ptr(), Cx, Fx, Tx, s.data_ptr(), Cs, Fs, Ts,
+                                        out.data_ptr(), B, N.stream_of(x)), "se_complex_join")
+        ctx.geom = (B, Cx, Fx, Tx, Cs, Fs, Ts)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        B, Cx, Fx, Tx, Cs, Fs, Ts = ctx.geom
+        gout = gout.contiguous()
+        gx = torch.empty((B, Cx, Fx, Tx), device=gout.device, dtype=gout.dtype)
+        gs = torch.empty((B, Cs, Fs, Ts), device=gout.device, dtype=gout.dtype)
+        N.check(N.lib().se_complex_join_bwd(gout.data_ptr(), gx.data_ptr(), Cx, Fx, Tx, gs.data_ptr(),
+                                            Cs, Fs, Ts, B, N.stream_of(gout)), "se_complex_join_bwd")
+        return gx, gs
+
+
+def complex_join(x, skip):
+    """complex_concat([align(x), skip]) where align crops x's trailing time
+    columns / zero-pads its trailing frequency rows to skip's grid
+    (frcrn.py:95-99), in one pass each way."""
+    return _ComplexJoin.apply(x, skip)

@@ -15,6 +15,7 @@ import torch.nn.functional as TF
 from ..ccbam import CCBAM
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLSTM,
                           complex_concat, norm_act, real_conv2d)
+from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -116,11 +117,11 @@ class Decoder(nn.Module):
     def forward(self, x, encoder_outputs):
         for attention, layer in zip(self.skip_connection_attention_layers, self.layers):
             skip = attention(encoder_outputs.pop())
-            if x.shape[-1] > skip.shape[-1]:          # frcrn.py:95-96
-                x = x[..., :-1]
-            if x.shape[-2] < skip.shape[-2]:          # frcrn.py:97-98
-                x = TF.pad(x, (0, 0, 0, 1))
-            x = layer(complex_concat([x, skip], dim=1))
+            # frcrn.py:95-99: x[..., :-1] if wider, F.pad(x, (0, 0, 0, 1)) if shorter, then
+            # complex_concat([x, skip]) — one fused pass each way (se_complex_join)
+            if x.shape[-1] - skip.shape[-1] not in (0, 1) or skip.shape[-2] - x.shape[-2] not in (0, 1):
+                raise ValueError(f"decoder/skip grids do not align: {tuple(x.shape)} vs {tuple(skip.shape)}")
+            x = layer(F.complex_join(x, skip))
         return x
 
 
