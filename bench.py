@@ -137,7 +137,8 @@ def main():
                 "traffic": _pmc_traffic("gather_gemm_kernel"),
                 "kernel": "gather_gemm_kernel (se_conv2d_fwd + se_conv2d_bwd_data, fp32 MFMA 32x32x2)",
                 "launch_calls": g["calls"], "avg_ms_per_call": round(g["ms"] / g["calls"], 4),
-                "algorithmic_flops_per_call": g["flops"] / g["calls"]}
+                "algorithmic_flops_per_call": g["flops"] / g["calls"],
+                "algorithmic_bytes_per_call": g["bytes"] / g["calls"]}
         st = kern.get("stft_fwd")
         if st:
             gbs = st["bytes"] / (st["ms"] * 1e-3) / 1e9

@@ -47,6 +47,19 @@ constexpr size_t kZeroBytes = 256;
 // ---------------------------------------------------------------------------
 // Gather-GEMM (forward and data-grad)
 // ---------------------------------------------------------------------------
+// XCD-aware workgroup order. Workgroups are dispatched round-robin over the 8
+// XCDs, each with its own L2, so consecutive linear ids land on different L2s
+// and neighbouring tiles (which share gathered input rows across taps, or the
+// D rows of one weight-grad split) miss each other's lines. This bijection on
+// [0, total) gives each XCD a contiguous range of logical tiles; it is a pure
+// relabelling, so results do not depend on the actual dispatch order.
+__device__ __forceinline__ int xcd_remap(int L, int total) {
+  constexpr int kXcd = 8;
+  const int xcd = L % kXcd, idx = L / kXcd;
+  const int q = total / kXcd, r = total % kXcd;
+  return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+}
+
 struct GatherArgs {
   const float* X;      // gathered tensor [B, Cg, Hi, Wi]
   const int4* ktab;    // [Kp] {c*Hi*Wi + offh*Wi + offw, offh, offw, 0}
@@ -87,7 +100,9 @@ gather_gemm_kernel(const GatherArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
-  const int m0 = blockIdx.x * BM, n0 = blockIdx.y * BN;
+  // logical tile: N-tiles of one M-tile adjacent, consecutive M-tiles on one XCD
+  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int m0 = (tile / gridDim.y) * BM, n0 = (tile % gridDim.y) * BN;
   const long long HiWi = (long long)a.Hi * a.Wi;
 
   // --- this thread's gather column (fixed for the whole K loop) ---
@@ -419,8 +434,11 @@ wgrad_gemm_kernel(const WgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = wave / WNn, wnn = wave % WNn;
-  const int k0 = blockIdx.x * BKO, n0 = blockIdx.y * BNO;
-  const int split = blockIdx.z;
+  // logical tile: every (k, n) tile of one m-split adjacent (they share D rows)
+  const int nkn = gridDim.x * gridDim.y;
+  const int tile = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, nkn * gridDim.z);
+  const int split = tile / nkn, kn = tile % nkn;
+  const int k0 = (kn % gridDim.x) * BKO, n0 = (kn / gridDim.x) * BNO;
   const int mbeg = split * a.m_per_split;
   const int mend = min(a.M, mbeg + a.m_per_split);
   const long long HiWi = (long long)a.Hi * a.Wi;

@@ -110,8 +110,9 @@ class _Conv2d(torch.autograd.Function):
         N.check(lib.se_conv2d_fwd(N.ctypes.byref(d), x.data_ptr(), wr.data_ptr(), N.ptr(wi),
                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(),
                                   N.stream_of(x)), "se_conv2d_fwd")
-        if t0 is not None:
-            _TIMER.end("conv_gather_gemm", t0, _conv_flops(d))
+        if t0 is not None:   # bytes: x read + y written + the weights, once
+            _TIMER.end("conv_gather_gemm", t0, _conv_flops(d),
+                       4.0 * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
         ctx.save_for_backward(x, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias = d, nbytes, br is not None
         return y
@@ -130,7 +131,8 @@ class _Conv2d(torch.autograd.Function):
                                            dx.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(gy)),
                     "se_conv2d_bwd_data")
             if t0 is not None:
-                _TIMER.end("conv_gather_gemm", t0, _conv_flops(d))
+                _TIMER.end("conv_gather_gemm", t0, _conv_flops(d),
+                           4.0 * (gy.numel() + dx.numel() + wr.numel() * (2 if wi is not None else 1)))
         if any(ctx.needs_input_grad[1:5]):
             dwr = torch.empty_like(wr)
             dwi = torch.empty_like(wi) if wi is not None else None
@@ -144,7 +146,8 @@ class _Conv2d(torch.autograd.Function):
                                              ws.data_ptr(), ws.numel(), N.stream_of(gy)),
                     "se_conv2d_bwd_weight")
             if t0 is not None:
-                _TIMER.end("conv_wgrad_gemm", t0, _conv_flops(d))
+                _TIMER.end("conv_wgrad_gemm", t0, _conv_flops(d),
+                           4.0 * (x.numel() + gy.numel() + wr.numel() * (2 if wi is not None else 1)))
         return dx, dwr, dwi, dbr, dbi, None
 
 
