@@ -15,7 +15,9 @@ import re
 import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsehip.so")
+# SEHIP_LIB may point at another in-tree build of the same library (A/B
+# measurement of kernel variants); the default is the package's own build.
+LIB_PATH = os.environ.get("SEHIP_LIB") or os.path.join(_HERE, "libsehip.so")
 HEADER_PATH = os.path.abspath(os.path.join(_HERE, "..", "..", "include", "sehip.h"))
 
 c_int = ctypes.c_int
