@@ -60,6 +60,12 @@ constexpr size_t kZeroBytes = 256;
 #ifndef SEHIP_IGLP
 #define SEHIP_IGLP 1
 #endif
+#ifndef SEHIP_IG_VMEM
+#define SEHIP_IG_VMEM 0x020   // group mask for the global loads (0x020 VMEM read, 0x010 any VMEM)
+#endif
+#ifndef SEHIP_IG_VALU
+#define SEHIP_IG_VALU 2       // VALU instructions per MFMA gap
+#endif
 
 __device__ __forceinline__ int xcd_remap(int L, int total) {
   constexpr int kXcd = 8;
@@ -264,8 +270,8 @@ gather_gemm_kernel(const GatherArgs a) {
     for (int i = 0; i < 4 * (kBK / 2); ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
-      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                // VALU
+      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(SEHIP_IG_VMEM, 1, 0);   // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, SEHIP_IG_VALU, 0);                // VALU
     }
 #endif
   };
@@ -665,8 +671,8 @@ wgrad_gemm_kernel(const WgradArgs a) {
     for (int i = 0; i < NM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);              // DS read / write
-      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // VMEM read
-      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);              // VALU
+      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(SEHIP_IG_VMEM, 1, 0);   // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, SEHIP_IG_VALU, 0);              // VALU
     }
 #endif
   };

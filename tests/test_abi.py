@@ -141,3 +141,19 @@ def test_asymmetric_padding_out_shape(tr, xs, pb, pe):
         xp = torch.nn.functional.pad(torch.zeros(xs), (pb[1], pe[1], pb[0], pe[0]))
         ref = tuple(torch.nn.Conv2d(xs[1], 6, k, stride=s, bias=False)(xp).shape[2:])
     assert (ho.value, wo.value) == tuple(ref)
+
+
+def test_ccbam_and_join_validation_need_no_gpu():
+    lib = N.lib()
+    assert lib.se_ccbam_workspace_size(64, 128, 158 * 403) > 0
+    assert lib.se_ccbam_workspace_size(64, 127, 100) == 0          # odd channel count
+    # (x, mean, max, amax, B, C, HW, stream): odd C -> SE_E_SHAPE, null -> SE_E_ARG
+    assert lib.se_ccbam_channel_pool(None, None, None, None, 2, 7, 10, None) == -2
+    assert lib.se_ccbam_channel_pool(None, None, None, None, 2, 8, 10, None) == -1
+    assert lib.se_ccbam_apply(None, None, None, None, 0, 8, 10, None) == -1
+    ws = lib.se_ccbam_workspace_size(2, 8, 10)
+    assert lib.se_ccbam_bwd_dca(None, None, None, None, None, 2, 8, 10, None, ws, None) == -1
+    # join: (x, Cx, Fx, Tx, s, Cs, F, T, out, B, stream)
+    assert lib.se_complex_join(None, 3, 4, 5, None, 4, 4, 5, None, 1, None) == -2   # odd Cx
+    assert lib.se_complex_join(None, 4, 4, 5, None, 4, 4, 5, None, 1, None) == -1   # null pointers
+    assert lib.se_complex_join_bwd(None, None, 4, 4, 5, None, 4, 0, 5, 1, None) == -1
