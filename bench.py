@@ -111,6 +111,24 @@ def main():
         elapsed = float(t.item())
     loss_v = float(loss)
     kern = timer.summary() if timer else {}
+    # ConvSTFT is a ~50 us kernel: per-call events inside the step also catch host
+    # launch gaps, so its roofline uses 20 back-to-back launches between one
+    # event pair, after the timed region (GPU-bound, comparable to rocprof's
+    # per-kernel average)
+    stft_burst_ms = None
+    if timer and rank == 0:
+        stft_mod = (model.module if hasattr(model, "module") else model).stft
+        with torch.no_grad():
+            x0 = batches[0][0]
+            stft_mod(x0)
+            torch.cuda.synchronize()
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(20):
+                stft_mod(x0)
+            e1.record()
+            torch.cuda.synchronize()
+            stft_burst_ms = e0.elapsed_time(e1) / 20
 
     if rank != 0:
         return
@@ -140,14 +158,16 @@ def main():
                 "algorithmic_flops_per_call": g["flops"] / g["calls"],
                 "algorithmic_bytes_per_call": g["bytes"] / g["calls"]}
         st = kern.get("stft_fwd")
-        if st:
-            gbs = st["bytes"] / (st["ms"] * 1e-3) / 1e9
+        if st and stft_burst_ms:
+            per_call = st["bytes"] / st["calls"]
+            gbs = per_call / (stft_burst_ms * 1e-3) / 1e9
             out["stft_roofline"] = {
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("stft_fwd_kernel"),
-                "kernel": "stft_fwd_kernel (se_stft_fwd)",
-                "avg_ms_per_call": round(st["ms"] / st["calls"], 4),
-                "algorithmic_bytes_per_call": st["bytes"] / st["calls"]}
+                "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": _pmc_traffic("stft_fwd_ip_kernel"),
+                "kernel": "stft_fwd_ip_kernel (se_stft_fwd)",
+                "avg_ms_per_call": round(stft_burst_ms, 4),
+                "timing": "20 back-to-back launches between one HIP event pair, after the timed region",
+                "algorithmic_bytes_per_call": per_call}
         out["op_breakdown"] = {
             k: {"calls": v["calls"], "ms_per_step": round(v["ms"] / args.steps, 3),
                 **({"tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {}),

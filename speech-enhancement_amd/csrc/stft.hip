@@ -179,11 +179,61 @@ __device__ float2* fft_pass(float2* a, float2* b, const float2* __restrict__ tw)
   }
 }
 
+// In-place variant of fft_pass: every thread first reads all its butterfly
+// inputs of the pass into registers, then (after a barrier) writes all outputs
+// into the SAME buffer. Half the LDS of the ping-pong form, so a block holds
+// twice the frames (16 at nfft 640) and writes 64-B row segments.
+template <int N, int P, int PS, int NS>
+__device__ void fft_pass_ip(float2* a, const float2* __restrict__ tw) {
+  constexpr CPlan pl = make_cplan(N);
+  if constexpr (PS < pl.npass) {
+    constexpr int R = pl.radix[PS], nbf = N / R, tstep = N / (NS * R);
+    constexpr int ITER = (P * nbf + kThreads - 1) / kThreads;
+    float2 v[ITER][5];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = threadIdx.x + it * kThreads;
+      if (P * nbf % kThreads == 0 || idx < P * nbf) {
+        const int pr = idx / nbf, j = idx - pr * nbf;
+        const float2* src = a + pr * N;
+        const int k = j % NS;
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[it][q] = src[j + q * nbf];
+        if constexpr (NS > 1) {
+#pragma unroll
+          for (int q = 1; q < R; ++q) v[it][q] = cmul(v[it][q], tw[q * k * tstep]);
+        }
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = threadIdx.x + it * kThreads;
+      if (P * nbf % kThreads == 0 || idx < P * nbf) {
+        const int pr = idx / nbf, j = idx - pr * nbf;
+        const int k = j % NS;
+        butterfly<R>(v[it], a + pr * N, (j / NS) * NS * R + k, NS);
+      }
+    }
+    __syncthreads();
+    fft_pass_ip<N, P, PS + 1, NS * R>(a, tw);
+  }
+}
+
 // FFT of P sequences: compile-time plan when CN != 0, else the runtime plan.
 template <int CN, int CP>
 __device__ __forceinline__ float2* fft_any(float2* a, float2* b, int P, const FftPlan& pl, const float2* tw) {
-  if constexpr (CN != 0) return fft_pass<CN, CP, 0, 1>(a, b, tw);
-  else return fft_forward(a, b, P, pl, tw);
+  if constexpr (CN != 0) {
+    // twiddles staged in LDS once per block: every pass reads them inside its
+    // barrier-separated loop, where a global (L2) read is latency on the
+    // critical path
+    __shared__ float2 stw[CN];
+    for (int i = threadIdx.x; i < CN; i += kThreads) stw[i] = tw[i];
+    __syncthreads();
+    return fft_pass<CN, CP, 0, 1>(a, b, stw);
+  } else {
+    return fft_forward(a, b, P, pl, tw);
+  }
 }
 
 __device__ __forceinline__ int reflect_index(int i, int L) {
@@ -262,6 +312,45 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
   __syncthreads();
   const float2* Z = fft_any<CN, CP>(A, Bf, P, a.pl, a.tw);
   unpack_store<CN, CP>(Z, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase);
+}
+
+// ConvSTFT with the in-place FFT: kPairsIP frame pairs per block in one LDS
+// buffer (compiled plans only). grid (ceil(T / 2P), B)
+constexpr int kPairsIP = 8;
+template <int CN>
+__global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a) {
+  constexpr int N = CN, P = kPairsIP;
+  __shared__ __attribute__((aligned(16))) float2 A[P * N];
+  __shared__ float2 stw[N];
+  const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
+  const float* x = a.x + (long long)b * a.L;
+  for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
+  // frame gather: all of a thread's loads are issued before any is used
+  // (compile-time trip count; branch-free clamped addresses and zero weights),
+  // so the block pays one memory latency instead of one per element
+  constexpr int IT = (P * N + kThreads - 1) / kThreads;
+  float ya[IT], yb[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    const int j = idx / N, n = idx - j * N;
+    const int ta = t0 + 2 * j, tb = ta + 1;
+    const bool ok = idx < P * N && n < a.win;
+    const int nn = ok ? n : 0;
+    const float w = ok ? a.window[nn] : 0.f;
+    const float xa = x[reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L)];
+    const float xb = x[reflect_index(min(tb, a.T - 1) * a.hop + nn - a.pad, a.L)];
+    ya[it] = ta < a.T ? w * xa : 0.f;
+    yb[it] = tb < a.T ? w * xb : 0.f;
+  }
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    if (idx < P * N) A[idx] = make_float2(ya[it], yb[it]);
+  }
+  __syncthreads();
+  fft_pass_ip<N, P, 0, 1>(A, stw);
+  unpack_store<CN, P>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase);
 }
 
 struct IstftArgs {
@@ -433,7 +522,13 @@ static bool make_plan(int N, FftPlan& pl) {
 // Frame pairs per block. kPairs (4) keeps a block's LDS at <= 40 KB for
 // nfft <= 640 so four blocks (16 waves) share a CU; larger nfft fall back to
 // what the LDS budget allows.
-constexpr int kPairs = 4;
+#ifndef SEHIP_STFT_IP
+#define SEHIP_STFT_IP 1      // ConvSTFT forward on the in-place FFT kernel
+#endif
+#ifndef SEHIP_STFT_PAIRS
+#define SEHIP_STFT_PAIRS 4
+#endif
+constexpr int kPairs = SEHIP_STFT_PAIRS;
 static int pick_pairs(int N) {
   const int p = kLdsBudget / (2 * N * (int)sizeof(float2));
   return std::max(1, std::min(kPairs, p));   // sums[] holds 2 floats for 32 frames
@@ -486,6 +581,19 @@ extern "C" int se_stft_fwd(const float* x, float* out0, float* out1, int B, int 
   a.L = L; a.win = win; a.hop = hop; a.T = T; a.pad = pad; a.mag_phase = mag_phase;
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
+  if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
+    // in-place FFT, 8 frame pairs per block (static LDS <= 45 KB)
+    const dim3 grid(se::ceil_div(T, 2 * kPairsIP), B);
+    switch (nfft) {
+      case 640: hipLaunchKernelGGL(stft_fwd_ip_kernel<640>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
+      case 512: hipLaunchKernelGGL(stft_fwd_ip_kernel<512>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
+      case 400: hipLaunchKernelGGL(stft_fwd_ip_kernel<400>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
+      case 320: hipLaunchKernelGGL(stft_fwd_ip_kernel<320>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
+      default: hipLaunchKernelGGL(stft_fwd_ip_kernel<256>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
+    }
+    SE_LAUNCH_CHECK();
+    return SE_OK;
+  }
   SE_STFT_DISPATCH(stft_fwd_kernel, nfft, a.P, dim3(se::ceil_div(T, 2 * a.P), B), shm, se::as_stream(stream), a);
   SE_LAUNCH_CHECK();
   return SE_OK;

