@@ -90,7 +90,8 @@ int se_istft_bwd(const float* gout, float* gspec, int B, int T, int win,
  * assembled in the workspace from the two nn.Conv2d / nn.ConvTranspose2d
  * weight tensors (real_conv.weight, imag_conv.weight). Transposed convs are
  * split into stride-phase classes so no MFMA work is spent on inserted zeros.
- * Arithmetic: fp32 in / fp32 accumulate on v_mfma_f32_32x32x2_f32.
+ * Arithmetic: fp32 in / fp32 accumulate; the MFMA form is chosen by
+ * se_conv2d_desc.math (below).
  * ------------------------------------------------------------------------ */
 typedef struct se_conv2d_desc {
   int batch;
@@ -109,7 +110,15 @@ typedef struct se_conv2d_desc {
                        * folds a zero pad of the input (e.g. FRCRN's causal
                        * F.pad(x, (1, 0)) before each encoder conv,
                        * frcrn.py:28-30) into the gather at no cost.          */
+  int math;           /* SE_MATH_F32 (0): fp32 operands on v_mfma_f32_32x32x2_f32
+                       * (exact fp32 products). SE_MATH_BF16X3 (1): each fp32
+                       * operand split as hi + lo bf16, a*b ~ ah*bh + ah*bl +
+                       * al*bh on v_mfma_f32_32x32x16_bf16, fp32 accumulate
+                       * (<= ~2^-15 relative per product; fp32 in / fp32 out).
+                       * Shapes the split kernels do not cover run SE_MATH_F32. */
 } se_conv2d_desc;
+
+enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1 };
 
 /* Output spatial size (nn.Conv2d / nn.ConvTranspose2d formulas). */
 int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w);

@@ -314,6 +314,7 @@ gather_gemm_kernel(const GatherArgs a) {
   if (kt < nk) compute(0);   // odd tile count: the last tile sits in LDS[0]
 
   // --- epilogue: lane -> m (coalesced along time), registers -> n ---
+  __syncthreads();                                 // every wave is done reading LDS[0]
   float* sBias = &sW[0][0][0];                     // reuse the drained weight tile
   for (int i = tid; i < BN; i += kThreads) {
     const int n = n0 + i;
@@ -806,6 +807,8 @@ __global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int
   }
 }
 
+#include "cconv_x3.hpp"
+
 // bias_full[n] for the fused complex conv: re = br - bi, im = bi + br.
 __global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
@@ -944,6 +947,7 @@ struct ConvGeom {
   int B, Ci, Hi, Wi, Co, Ho, Wo;
   int kh, kw, sh, sw, ph, pw, dh, dw, oph, opw, transposed, complex_w;
   int phe, pwe;   // end (bottom / right) padding; ph / pw are the begin offsets
+  int math;       // SE_MATH_F32 / SE_MATH_BF16X3
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -954,6 +958,8 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.oph = d->out_pad_h; g.opw = d->out_pad_w; g.transposed = d->transposed; g.complex_w = d->complex_weights;
   g.phe = d->pad_h_end < 0 ? g.ph : d->pad_h_end;
   g.pwe = d->pad_w_end < 0 ? g.pw : d->pad_w_end;
+  g.math = d->math;
+  if (g.math != SE_MATH_F32 && g.math != SE_MATH_BF16X3) return SE_E_ARG;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
     return SE_E_ARG;
@@ -1089,15 +1095,22 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     hipLaunchKernelGGL(prep_bias_kernel, dim3(se::ceil_div(N, 256)), dim3(256), 0, st,
                        bias_br, bias_bi, N, g.complex_w, bias_full);
   }
+  // split-bf16 GEMM for the 128-column tiles (N > 64); other shapes stay fp32
+  const bool x3 = g.math == SE_MATH_BF16X3 && N > 64;
   for (const auto& c : cls) {
     float* Wp = (float*)p;
-    p = align256(p + (size_t)c.Kp * ldw * sizeof(float));
+    p = align256(p + (size_t)c.Kp * ldw * sizeof(float));   // = the split image's size
     int4* ktab = (int4*)p;
     p = align256(p + (size_t)c.Kp * sizeof(int4));
     const long long tot = (long long)c.Kp * ldw;
-    hipLaunchKernelGGL(prep_class_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
-                       dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, pass == kData ? 1 : 0,
-                       Wp, ktab);
+    if (x3)
+      hipLaunchKernelGGL(prep_class_x3_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
+                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
+                         pass == kData ? 1 : 0, (unsigned short*)Wp, ktab);
+    else
+      hipLaunchKernelGGL(prep_class_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
+                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, pass == kData ? 1 : 0,
+                         Wp, ktab);
     GatherArgs a{};
     a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.zero = zero; a.Y = Y;
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
@@ -1121,7 +1134,11 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       const long long span = (bm + qhw - 1) / qhw + 1;
       const bool tu = (Cg % kBK == 0) && span * Cg * (long long)Hi * Wi * 4 < (1ll << 31) &&
                       (long long)c.Kp * ldw * 4 < (1ll << 31);
-      if (ldw == 64) {
+      if (x3) {
+        dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
+        if (tu) hipLaunchKernelGGL(gather_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL(gather_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
+      } else if (ldw == 64) {
         dim3 grid(se::ceil_div(M, 256), 1);
         if (tu) hipLaunchKernelGGL((gather_gemm_kernel<64, 256, 1, 4, true>), grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((gather_gemm_kernel<64, 256, 1, 4, false>), grid, dim3(kThreads), 0, st, a);

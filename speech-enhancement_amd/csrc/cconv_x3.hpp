@@ -1,0 +1,284 @@
+// Split-bf16 ("bf16x3") variants of the conv GEMMs (included by cconv.hip,
+// inside its anonymous namespace, after GatherArgs / xcd_remap).
+//
+// gfx950 has no TF32/xf32 MFMA: fp32-input MFMA (v_mfma_f32_32x32x2_f32) runs
+// at the fp32 vector rate, 1/16 of the bf16 MFMA rate. Each fp32 operand is
+// split into two bf16 terms, x = hi + lo + e with hi = bf16_rne(x),
+// lo = bf16_rne(x - hi) (x - hi is exact in fp32), |e| <= 2^-17 |x|, and
+//   a*b ~= ah*bh + ah*bl + al*bh        (dropped: al*bl, |.| <= 2^-16 |ab|)
+// is accumulated in fp32 by three v_mfma_f32_32x32x16_bf16 (products of two
+// bf16 are exact in the fp32 accumulator). Per-product error <= ~2^-15 |ab|,
+// rms ~6e-6 |ab| on random data: fp32-class accuracy for the north star's
+// 1e-4 relative bar at 3/16 of the fp32 MFMA cycles per FLOP.
+//
+// Operand lane map of v_mfma_f32_32x32x16_bf16: lane l (r = l & 31,
+// h = l >> 5) holds A[row r][k = 8h + j] and B[k = 8h + j][col r] in element
+// j. The accumulator map is the one of the fp32 32x32x2 form, so the
+// epilogue is shared with gather_gemm_kernel.
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// (x0, x1) -> packed bf16 hi pair and lo pair (element 0 in the low half).
+__device__ __forceinline__ void split_bf16x2(float x0, float x1, unsigned& hi, unsigned& lo) {
+  hi = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0, x1}, bf16x2));
+  const float h0 = __builtin_bit_cast(float, hi << 16);
+  const float h1 = __builtin_bit_cast(float, hi & 0xffff0000u);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){x0 - h0, x1 - h1}, bf16x2));
+}
+
+__device__ __forceinline__ unsigned short bf16_bits(float x) {
+  return __builtin_bit_cast(unsigned short, (__bf16)x);
+}
+
+// LDS / pre-tiled weight image of one operand tile: [plane (hi, lo)][row][4
+// chunks of 8 bf16 = 16 B], chunk c of row `row` stored at c ^ ((row >> 2) & 3).
+// 64-B rows, XOR swizzle: ds_read_b128 fragment reads (lane -> row r, chunk
+// 2ks + h) are conflict-free in all four 16-lane groups.
+__device__ __forceinline__ int x3_chunk(int row, int c) { return c ^ ((row >> 2) & 3); }
+
+constexpr int kX3BN = 128, kX3BM = 128;
+constexpr int kX3TileU4 = 2 * 128 * 4;   // u32x4 per (k-step, n-tile) weight image = 16 KB
+
+// Pre-tiled split weight: Wt[(s * NT + t) * kX3TileU4 + (plane * 128 + n) * 4 + x3_chunk(n, c)]
+// holds bf16 element e of k = 32 s + 8 c + e, column n0 = 128 t + n. Also ktab
+// (as prep_class_kernel).
+__global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, int Kp, int NT,
+                                     int Hi, int Wi, int data_grad, unsigned short* Wt, int4* ktab) {
+  const int K = taps.n * Cg;
+  const long long total = (long long)Kp * NT * 128;   // one thread per (k, n)
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(idx % Kp);                    // k fastest: a thread group fills rows
+    const int n = (int)(idx / Kp);
+    float v = 0.f;
+    if (k < K && n < N) {
+      const int t = k / Cg, c = k % Cg;
+      const int ci = data_grad ? n : c, co = data_grad ? c : n;
+      v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
+    }
+    const float h = (float)(__bf16)v;
+    const unsigned short hb = bf16_bits(v), lb = bf16_bits(v - h);
+    const int s = k >> 5, kc = (k >> 3) & 3, e = k & 7;
+    const int tn = n >> 7, nl = n & 127;
+    const long long base = ((long long)s * NT + tn) * kX3TileU4 * 8;   // in bf16 units
+    const long long off = ((long long)nl * 4 + x3_chunk(nl, kc)) * 8 + e;
+    Wt[base + off] = hb;
+    Wt[base + 128 * 4 * 8 + off] = lb;
+    if (n == 0) {
+      int4 q;
+      if (k < K) {
+        const int t = k / Cg, c = k % Cg;
+        q.x = (int)((long long)c * Hi * Wi + (long long)taps.offh[t] * Wi + taps.offw[t]);
+        q.y = taps.offh[t];
+        q.z = taps.offw[t];
+      } else {
+        q.x = 0; q.y = kInvalidOff; q.z = 0;
+      }
+      q.w = 0;
+      ktab[k] = q;
+    }
+  }
+}
+
+// Gather GEMM, split-bf16: same contraction, tiling and epilogue as
+// gather_gemm_kernel<128, 128, 2, 2, TU>. a.Wp points at the pre-tiled split
+// weight (prep_class_x3_kernel), a.ldw = 128 * gridDim.y.
+// Per K-step (BK = 32) a wave issues 2 k-substeps x 2 x 2 blocks x 3 terms =
+// 24 MFMAs of 32 cycles; each thread gathers 16 consecutive k of one m column
+// (k = k0 + 16 * akr + j), splits them in registers and writes 4 ds_write_b128.
+template <bool TU>
+__global__ void __launch_bounds__(kThreads, 2)
+gather_x3_kernel(const GatherArgs a) {
+  constexpr int BN = kX3BN, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
+  constexpr int AJ = 16;                          // gathered k per thread per step
+  __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * BM * 4];
+  __shared__ __attribute__((aligned(16))) u32x4 sW[2][2 * BN * 4];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM;
+  const int NT = gridDim.y;
+  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int mt = tile / NT, nt = tile % NT;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long long HiWi = (long long)a.Hi * a.Wi;
+
+  const int am = tid % BM;
+  const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // 0 or 1 (wave-uniform)
+  const int m = m0 + am;
+  const bool mval = m < a.M;
+  int hb = 0, wb = 0;
+  long long xbase = 0;
+  if (mval) {
+    const int qhw = a.Qh * a.Qw;
+    const int b = m / qhw, r = m - b * qhw;
+    const int qh = r / a.Qw, qw = r - qh * a.Qw;
+    hb = qh * a.sh;
+    wb = qw * a.sw;
+    xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+  }
+  struct Stage { float ra[AJ]; u32x4 rw[4]; };
+  Stage s0, s1;
+  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  const int b0 = m0 / (a.Qh * a.Qw);
+  __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.X + (long long)b0 * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * kX3TileU4 + tid;
+  int xoff = 0;
+  if constexpr (TU) {
+    if (mval) {
+      const int b = m / (a.Qh * a.Qw);
+      xoff = (int)(((long long)(b - b0) * a.Cg * HiWi + (long long)hb * a.Wi + wb) * 4);
+    }
+  }
+  auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
+    if constexpr (TU) {
+      const int4 e0 = a.ktab[k0];                 // the step's tap (uniform)
+      const int tap = k0 / a.Cg;
+      const int c0 = k0 - tap * a.Cg + AJ * akr;
+      const int hi = hb + e0.y, wi = wb + e0.z;
+      const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      const int vo = ok ? xoff + (e0.y * a.Wi + e0.z) * 4 : (int)0x80000000;
+      const int cs = (int)(HiWi * 4);
+#pragma unroll
+      for (int j = 0; j < AJ; ++j)
+        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (c0 + j) * cs, 0));
+    } else {
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        const int4 e = a.ktab[k0 + AJ * akr + j];   // uniform index -> s_load
+        const int hi = hb + e.y, wi = wb + e.z;
+        const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+        st.ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
+      }
+    }
+    const u32x4* src = wt + (long long)(k0 >> 5) * NT * kX3TileU4;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) st.rw[j] = src[kThreads * j];
+  };
+  const int swz = (am >> 2) & 3;
+  auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      u32x4 H, L;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        unsigned h, l;
+        split_bf16x2(st.ra[8 * q + 2 * e], st.ra[8 * q + 2 * e + 1], h, l);
+        H[e] = h;
+        L[e] = l;
+      }
+      const int c = (2 * akr + q) ^ swz;
+      sA[buf][am * 4 + c] = H;
+      sA[buf][BM * 4 + am * 4 + c] = L;
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sW[buf][tid + kThreads * j] = st.rw[j];
+  };
+
+  f32x16 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int j = 0; j < RM; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lh = lane >> 5, lr = lane & 31;
+  const int fsw = (lr >> 2) & 3;
+  auto compute = [&](int cur) __attribute__((always_inline)) {
+    u32x4 wf[2][RN][2], af[2][RM][2];   // [ks][block][plane]
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      const int c = (2 * ks + lh) ^ fsw;
+#pragma unroll
+      for (int i = 0; i < RN; ++i)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          wf[ks][i][p] = sW[cur][(p * BN + wn * TN + 32 * i + lr) * 4 + c];
+#pragma unroll
+      for (int j = 0; j < RM; ++j)
+#pragma unroll
+        for (int p = 0; p < 2; ++p)
+          af[ks][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
+    }
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int t = 0; t < 3; ++t)      // terms: hi*hi, hi*lo, lo*hi
+#pragma unroll
+        for (int i = 0; i < RN; ++i)
+#pragma unroll
+          for (int j = 0; j < RM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+                __builtin_bit_cast(bf16x8, wf[ks][i][t == 2 ? 1 : 0]),
+                __builtin_bit_cast(bf16x8, af[ks][j][t == 1 ? 1 : 0]), acc[i][j], 0, 0, 0);
+  };
+  auto interleave = [&]() __attribute__((always_inline)) {
+#if SEHIP_IGLP
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);                  // first k-substep fragments
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
+      if (i < 20) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
+    }
+#endif
+  };
+
+  const int nk = a.Kp / kBK;
+  load_tile(s0, 0);
+  store_tile(s0, 0);
+  if (nk > 1) load_tile(s1, kBK);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    load_tile(s0, min(kt + 2, nk - 1) * kBK);
+    compute(0);
+    store_tile(s1, 1);
+    interleave();
+    __syncthreads();
+    load_tile(s1, min(kt + 3, nk - 1) * kBK);
+    compute(1);
+    store_tile(s0, 0);
+    interleave();
+    __syncthreads();
+  }
+  if (kt < nk) compute(0);
+
+  // --- epilogue (as gather_gemm_kernel) ---
+  __syncthreads();
+  float* sBias = reinterpret_cast<float*>(&sW[0][0]);
+  for (int i = tid; i < BN; i += kThreads) {
+    const int n = n0 + i;
+    sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+  }
+  __syncthreads();
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  const bool full_n = n0 + BN <= a.N;
+#pragma unroll
+  for (int j = 0; j < RM; ++j) {
+    const int mm = m0 + wm * TM + 32 * j + lr;
+    if (mm >= a.M) continue;
+    const int qhw = a.Qh * a.Qw;
+    const int b = mm / qhw, r = mm - b * qhw;
+    const int qh = r / a.Qw, qw = r - qh * a.Qw;
+    const int nl0 = wn * TN + 4 * lh;
+    float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
+                (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int r2 = 0; r2 < 16; ++r2) {
+        const int nl = 32 * i + (r2 & 3) + 8 * (r2 >> 2);
+        if (full_n || n0 + nl0 + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
+      }
+  }
+}

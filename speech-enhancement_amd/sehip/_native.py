@@ -34,7 +34,7 @@ class ConvDesc(ctypes.Structure):
         "batch", "in_channels", "in_h", "in_w", "out_channels",
         "kernel_h", "kernel_w", "stride_h", "stride_w", "pad_h", "pad_w",
         "dil_h", "dil_w", "out_pad_h", "out_pad_w", "transposed",
-        "complex_weights", "pad_h_end", "pad_w_end")]
+        "complex_weights", "pad_h_end", "pad_w_end", "math")]
 
 
 _P = c_void_p

@@ -6,6 +6,8 @@ HIP stream. There is no CPU path: CPU tensors raise.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _native as N
@@ -52,6 +54,24 @@ class OpTimer:
 
 _TIMER: OpTimer | None = None
 
+# MFMA form of the conv GEMMs (se_conv2d_desc.math): "f32" = exact fp32
+# products on v_mfma_f32_32x32x2_f32; "bf16x3" = split-bf16 operands
+# (hi*hi + hi*lo + lo*hi) on v_mfma_f32_32x32x16_bf16, fp32 accumulate.
+# Initial value from SEHIP_CONV_MATH; set_conv_math() changes it.
+_MATH_CODES = {"f32": 0, "bf16x3": 1}
+_CONV_MATH = _MATH_CODES[os.environ.get("SEHIP_CONV_MATH", "f32")]
+
+
+def set_conv_math(mode: str) -> None:
+    global _CONV_MATH
+    if mode not in _MATH_CODES:
+        raise ValueError(f"conv math must be one of {sorted(_MATH_CODES)} (got {mode!r})")
+    _CONV_MATH = _MATH_CODES[mode]
+
+
+def get_conv_math() -> str:
+    return {v: k for k, v in _MATH_CODES.items()}[_CONV_MATH]
+
 
 def set_op_timer(t: OpTimer | None):
     global _TIMER
@@ -87,6 +107,7 @@ def conv_desc(x_shape, out_channels, kernel, stride, padding, dilation, output_p
     d.out_pad_h, d.out_pad_w = output_padding
     d.transposed, d.complex_weights = int(transposed), int(complex_w)
     d.pad_h_end, d.pad_w_end = (-1, -1) if padding_end is None else padding_end
+    d.math = _CONV_MATH
     return d
 
 

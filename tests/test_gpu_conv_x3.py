@@ -1,0 +1,84 @@
+"""GPU parity of the split-bf16 ("bf16x3", se_conv2d_desc.math = 1) conv
+GEMMs: FRCRN layer geometries and the golden conv cases against the fp64
+oracle (complex_nn.py:52-91 in the reference's four-real-conv form).
+
+bf16x3 drops the lo*lo term and rounds lo to bf16: <= ~2^-15 relative per
+product, ~6e-6 rms on random data. Gate: rel-L2 < 3e-5 per tensor, and
+within 30x of the exact-fp32 path's own error against fp64."""
+import pytest
+import torch
+
+from conftest import golden, rel_l2
+import paramfill
+from oracle import complex_nn as O_cnn
+
+pytestmark = pytest.mark.gpu
+
+TOL = 3e-5
+
+LAYERS = [
+    ("enc1", False, 128, 128, (2, 128, 158, 41), (2, 1)),
+    ("enc5", False, 128, 128, (2, 128, 7, 41), (2, 1)),
+    ("dec0", True, 256, 128, (2, 256, 2, 40), (2, 1)),
+    ("dec5", True, 256, 128, (2, 256, 158, 40), (2, 1)),
+    ("dec_odd", True, 256, 192, (3, 256, 9, 37), (2, 1)),   # N = 192: partial n-tile
+    ("s22", False, 128, 256, (2, 128, 33, 29), (2, 2)),     # two n-tiles, stride 2 in time
+]
+
+
+def _hip(F, m, x, gy, transposed, stride, math):
+    F.set_conv_math(math)
+    try:
+        wr = m.real_conv.weight.detach().float().cuda().requires_grad_(True)
+        wi = m.imag_conv.weight.detach().float().cuda().requires_grad_(True)
+        xg = x.float().cuda().requires_grad_(True)
+        y = F.conv2d(xg, wr, wi, out_channels=2 * m.real_conv.out_channels,
+                     kernel=m.real_conv.kernel_size, stride=stride, transposed=transposed)
+        y.backward(gy.float().cuda())
+        torch.cuda.synchronize()
+        return dict(y=y.detach().cpu(), dx=xg.grad.cpu(), dwr=wr.grad.cpu(), dwi=wi.grad.cpu())
+    finally:
+        F.set_conv_math("f32")
+
+
+@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", LAYERS)
+def test_bf16x3_layer_vs_fp64_oracle(name, tr, cin, cout, shape, stride, gpu_device):
+    from sehip import functional as F
+    cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
+    m = paramfill.fill_(cls(cin, cout, (5, 2), stride=stride, bias=False), seed=7).double()
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(*shape, generator=gen, dtype=torch.float64)
+    xo = x.clone().requires_grad_(True)
+    yo = m(xo)
+    gy = torch.randn(yo.shape, generator=gen, dtype=torch.float64)
+    yo.backward(gy)
+    ref = dict(y=yo.detach(), dx=xo.grad, dwr=m.real_conv.weight.grad, dwi=m.imag_conv.weight.grad)
+    exact = _hip(F, m, x, gy, tr, stride, "f32")
+    split = _hip(F, m, x, gy, tr, stride, "bf16x3")
+    for k, r in ref.items():
+        e32 = rel_l2(exact[k].numpy(), r.numpy())
+        ex3 = rel_l2(split[k].numpy(), r.numpy())
+        print(f"{name} {k}: f32 {e32:.2e}  bf16x3 {ex3:.2e}")
+        assert ex3 < TOL, (name, k, ex3)
+        assert ex3 < max(30 * e32, 1e-6), (name, k, ex3, e32)
+
+
+CONV_CASES = [
+    ("enc", False, 16, 12, (5, 2), dict(stride=(2, 1), bias=False)),
+    ("dec", True, 16, 12, (5, 2), dict(stride=(2, 1), bias=False)),
+]
+
+
+@pytest.mark.parametrize("i,case", [(0, CONV_CASES[0]), (3, CONV_CASES[1])])
+def test_bf16x3_small_channels_match_golden(i, case, gpu_device):
+    """Shapes outside the split kernels' tiles (N <= 64) run the fp32 GEMM in
+    bf16x3 mode too: same goldens, same 1e-5 bar as test_gpu_cconv."""
+    from sehip import functional as F
+    g = golden("cconv")
+    name, tr, cin, cout, k, kw = case
+    cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
+    m = paramfill.fill_(cls(cin, cout, k, **kw), seed=i)
+    r = _hip(F, m, torch.from_numpy(g[f"{name}_x"]), torch.from_numpy(g[f"{name}_gy"]), tr,
+             kw["stride"], "bf16x3")
+    for key in ("y", "dx", "dwr", "dwi"):
+        assert rel_l2(r[key].numpy(), g[f"{name}_{key}"]) < 1e-5, (name, key)

@@ -15,6 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--layers", default="enc1,dec5")
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--passes", default="fwd,data,weight")
+ap.add_argument("--math", default="f32,bf16x3", help="conv math modes to time (se_conv2d_desc.math)")
 args = ap.parse_args()
 dev = torch.device("cuda")
 for name in args.layers.split(","):
@@ -24,6 +25,7 @@ for name in args.layers.split(","):
     wr = torch.randn(wshape, device=dev) * 0.05
     wi = torch.randn(wshape, device=dev) * 0.05
     d = F.conv_desc(shape, cout, (5, 2), (2, 1), (0, 0), (1, 1), (0, 0), tr, True)
+    d.math = 0
     lib = F.N.lib()
     ho, wo = F.N.c_int(), F.N.c_int()
     lib.se_conv2d_out_shape(F.N.ctypes.byref(d), F.N.ctypes.byref(ho), F.N.ctypes.byref(wo))
@@ -38,13 +40,25 @@ for name in args.layers.split(","):
         "data": lambda: lib.se_conv2d_bwd_data(F.N.ctypes.byref(d), y.data_ptr(), wr.data_ptr(), wi.data_ptr(), dx.data_ptr(), ws.data_ptr(), ws.numel(), st),
         "weight": lambda: lib.se_conv2d_bwd_weight(F.N.ctypes.byref(d), x.data_ptr(), y.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), None, None, ws.data_ptr(), ws.numel(), st),
     }
+    outs = {"fwd": lambda: y, "data": lambda: dx, "weight": lambda: dwr}
+    y0 = y.clone()
     for p in args.passes.split(","):
         f = calls[p]
-        assert f() == 0
-        torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for _ in range(args.iters):
-            f()
-        torch.cuda.synchronize()
-        dt = (time.perf_counter() - t0) / args.iters
-        print(f"{name:5s} {p:6s} {dt*1e3:8.2f} ms  {fl/dt/1e12:7.1f} TF", flush=True)
+        ref = None
+        for mname in args.math.split(","):
+            d.math = F._MATH_CODES[mname]
+            if p == "fwd":
+                y.copy_(y0)   # the data-grad pass reads y as dy
+            assert f() == 0
+            torch.cuda.synchronize()
+            out = outs[p]().clone()
+            err = "" if ref is None else f"  rel-L2 vs {args.math.split(',')[0]} {((out - ref).norm() / ref.norm()).item():.2e}"
+            ref = out if ref is None else ref
+            t0 = time.perf_counter()
+            for _ in range(args.iters):
+                f()
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / args.iters
+            print(f"{name:5s} {p:6s} {mname:6s} {dt*1e3:8.2f} ms  {fl/dt/1e12:7.1f} TF{err}", flush=True)
+        if p == "fwd":
+            y.copy_(y0)
