@@ -4,7 +4,10 @@
 One step = one FRCRN training iteration (trainer.py:99-124 + 210-221:
 forward, SI-SNR, backward, clip_grad_norm_(0.5), AdamW) on 64 synthetic
 4 s @ 16 kHz noisy/clean pairs per GPU, inputs resident in HBM.
-fp32 throughout (the reference's precision; parity is judged at 1e-4 fp32).
+fp32 storage and accumulation throughout (the reference's precision; parity
+is judged at 1e-4 fp32). The conv GEMMs' MFMA form follows SEHIP_CONV_MATH /
+--math (default: exact fp32 forward, split-bf16 data/weight-grad GEMMs); the
+all-fp32 step is timed beside it (`f32_exact`).
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -30,6 +33,17 @@ import torch  # noqa: E402
 
 METRIC = "utterances/sec (4s@16kHz) FRCRN train at 1/2/4/8 MI355X"
 FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-in MFMA dense peak
+BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 MFMA dense peak (no sparsity)
+KERNEL_OF = {   # OpTimer tag -> (rocprof kernel name, description)
+    "conv_fwd_f32": ("gather_gemm_kernel", "gather_gemm_kernel (se_conv2d_fwd, fp32 MFMA 32x32x2)"),
+    "conv_data_f32": ("gather_gemm_kernel", "gather_gemm_kernel (se_conv2d_bwd_data, fp32 MFMA 32x32x2)"),
+    "conv_fwd_bf16x3": ("gather_x3_kernel", "gather_x3_kernel (se_conv2d_fwd, split-bf16 MFMA 32x32x16 x3)"),
+    "conv_data_bf16x3": ("gather_x3_kernel",
+                         "gather_x3_kernel (se_conv2d_bwd_data, split-bf16 MFMA 32x32x16 x3)"),
+    "conv_wgrad_f32": ("wgrad_gemm_kernel", "wgrad_gemm_kernel (se_conv2d_bwd_weight, fp32 MFMA 32x32x2)"),
+    "conv_wgrad_bf16x3": ("wgrad_x3_kernel",
+                          "wgrad_x3_kernel (se_conv2d_bwd_weight, split-bf16 MFMA 32x32x16 x3)"),
+}
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
 SR, SECONDS = 16000, 4
 
@@ -44,6 +58,11 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-op-timing", action="store_true")
+    ap.add_argument("--no-compare-f32", dest="compare_f32", action="store_false",
+                    help="skip the all-fp32 comparison run")
+    ap.add_argument("--math", default=os.environ.get("SEHIP_CONV_MATH"),
+                    help="conv GEMM MFMA form (se_conv2d_desc.math): f32, bf16x3, or per pass "
+                         "'fwd=bf16x3,data=f32,weight=bf16x3'")
     return ap.parse_args()
 
 
@@ -75,6 +94,8 @@ def main():
     from sehip.models import FRCRN
     from sehip.train import make_optimizer, setup_distributed, train_step, wrap_ddp
 
+    if args.math:
+        SF.set_conv_math(args.math)
     rank, world, local, device = setup_distributed()
     if device.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
@@ -130,6 +151,33 @@ def main():
             torch.cuda.synchronize()
             stft_burst_ms = e0.elapsed_time(e1) / 20
 
+    # the same step with every conv pass on the exact fp32 MFMA kernels (untimed by
+    # the op timer), for comparison with the default split-bf16 backward
+    f32_exact = None
+    if args.compare_f32 and SF.get_conv_math() != "f32":
+        mode = SF.get_conv_math()
+        SF.set_conv_math("f32")
+        noisy, clean = batches[0]
+        train_step(model, opt, noisy, clean)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        t1 = time.perf_counter()
+        for i in range(args.steps):
+            noisy, clean = batches[i % 2]
+            train_step(model, opt, noisy, clean)
+        torch.cuda.synchronize()
+        if dist:
+            dist.barrier()
+        e2 = time.perf_counter() - t1
+        if dist:
+            t = torch.tensor([e2], device=device, dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            e2 = float(t.item())
+        SF.set_conv_math(mode)
+        f32_exact = {"conv_math": "f32", "value": round(world * B * args.steps / e2, 3),
+                     "ms_per_step": round(1e3 * e2 / args.steps, 3)}
+
     if rank != 0:
         return
     value = world * B * args.steps / elapsed
@@ -144,19 +192,32 @@ def main():
                    "per_gpu_batch": B, "global_batch": B * world, "seq_len": L,
                    "parallelism": f"dp{world}"},
         "final_loss": round(loss_v, 4),
+        "conv_math": SF.get_conv_math(),
+        "conv_math_note": "fp32 storage and accumulation everywhere; 'bf16x3' passes split each fp32 "
+                          "operand into hi+lo bf16 and sum hi*hi+hi*lo+lo*hi on bf16 MFMA (4.5e-6 "
+                          "rel-L2 per conv vs fp64; tests/test_gpu_conv_x3.py); forward exact fp32",
     }
+    if f32_exact:
+        out["f32_exact"] = f32_exact
     if kern:
-        g = kern.get("conv_gather_gemm")
-        if g:
-            ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
-            out["roofline"] = {
-                "bound": "mfma", "achieved": round(ach, 2), "peak": FP32_MFMA_PEAK_TFLOPS,
-                "unit": "TFLOP/s", "frac": round(ach / FP32_MFMA_PEAK_TFLOPS, 4),
-                "traffic": _pmc_traffic("gather_gemm_kernel"),
-                "kernel": "gather_gemm_kernel (se_conv2d_fwd + se_conv2d_bwd_data, fp32 MFMA 32x32x2)",
-                "launch_calls": g["calls"], "avg_ms_per_call": round(g["ms"] / g["calls"], 4),
-                "algorithmic_flops_per_call": g["flops"] / g["calls"],
-                "algorithmic_bytes_per_call": g["bytes"] / g["calls"]}
+        # dominant GEMM kernel = the conv pass/kernel with the most time in the step
+        convs = {k: v for k, v in kern.items() if k.startswith("conv_") and v["flops"]}
+        tag = max(convs, key=lambda k: convs[k]["ms"])
+        g = convs[tag]
+        ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
+        split = tag.endswith("bf16x3")
+        peak = BF16_MFMA_PEAK_TFLOPS / 3 if split else FP32_MFMA_PEAK_TFLOPS
+        out["roofline"] = {
+            "bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
+            "unit": "TFLOP/s", "frac": round(ach / peak, 4),
+            "traffic": _pmc_traffic(KERNEL_OF[tag][0]),
+            "kernel": KERNEL_OF[tag][1], "timer_tag": tag,
+            "launch_calls": g["calls"], "avg_ms_per_call": round(g["ms"] / g["calls"], 4),
+            "algorithmic_flops_per_call": g["flops"] / g["calls"],
+            "algorithmic_bytes_per_call": g["bytes"] / g["calls"],
+            "flops_convention": "algorithmic fp32 conv FLOPs (torch FlopCounterMode formula)"
+                                + ("; peak = bf16 dense MFMA peak / 3 MFMA terms per fp32 product"
+                                   if split else "")}
         st = kern.get("stft_fwd")
         if st and stft_burst_ms:
             per_call = st["bytes"] / st["calls"]

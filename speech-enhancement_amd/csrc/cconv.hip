@@ -1244,6 +1244,10 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
     dim3 grid(w.c.Kp / 128, 1, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
+  } else if (g.math == SE_MATH_BF16X3) {
+    dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
+    if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
   } else {
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2, 32, true>), grid, dim3(kThreads), 0, st, a);

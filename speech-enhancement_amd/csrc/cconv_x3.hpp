@@ -282,3 +282,239 @@ gather_x3_kernel(const GatherArgs a) {
       }
   }
 }
+
+// ---------------------------------------------------------------------------
+// Weight-grad reduction GEMM, split-bf16: dWp[k, n] = sum_m G[m, k] * D[m, n]
+// over one m-split per workgroup (same slabs / finish path as
+// wgrad_gemm_kernel<128, 128, 2, 2, 32, TU>).
+// The reduction index m is the MFMA k: a step of BMR = 32 positions is two
+// 16-deep k-substeps. Lanes load along m (coalesced along time); a half-wave
+// owns 16 consecutive G rows and 16 consecutive D rows, so a thread holds, per
+// position, 16 consecutive rows = two 16-B chunks of a [position][row] LDS
+// image (hi and lo planes). The MFMA fragments (row = lane, 8 positions) are
+// read back transposed with ds_read_b64_tr_b16 (gfx950), two per fragment.
+// Image rows are 256 B (128 bf16) with the XOR chunk swizzle below, which
+// keeps both the transposed reads and the b128 stores (nearly) conflict-free.
+// ---------------------------------------------------------------------------
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+__device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chunk ch of position row s
+  return 256 * s + 16 * (ch ^ (((s & 3) << 2) | ((s >> 2) & 3)));
+}
+
+template <bool TU>
+__global__ void __launch_bounds__(kThreads, 2)
+wgrad_x3_kernel(const WgradArgs a) {
+  constexpr int BKO = 128, BNO = 128, WNn = 2, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
+  constexpr int RJ = 16;                     // rows per thread per operand
+  constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2][4 * PLANE];   // G hi, G lo, D hi, D lo
+  __shared__ int4 sK[BKO];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wk = wave / WNn, wnn = wave % WNn;
+  const int nkn = gridDim.x * gridDim.y;
+  const int tile = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, nkn * gridDim.z);
+  const int split = tile / nkn, kn = tile % nkn;
+  const int k0 = (kn % gridDim.x) * BKO, n0 = (kn / gridDim.x) * BNO;
+  const int mbeg = split * a.m_per_split;
+  const int mend = min(a.M, mbeg + a.m_per_split);
+  const long long HiWi = (long long)a.Hi * a.Wi;
+  const long long QQ = (long long)a.Qh * a.Qw;
+  const int ml = lane & 31, lr = lane >> 5;
+  const int rbase = 32 * wave + RJ * lr;     // this thread's first G row / D row
+
+  for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab[k0 + i];
+  __syncthreads();
+
+  int cb, cqh, cqw;
+  {
+    const long long mm = mbeg + ml;
+    cb = (int)(mm / QQ);
+    const int r = (int)(mm - cb * QQ);
+    cqh = r / a.Qw;
+    cqw = r - cqh * a.Qw;
+  }
+  struct Stage { float rg[RJ], rd[RJ]; };
+  Stage st0, st1;
+  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  const int bfirst = (int)(mbeg / QQ);
+  __amdgpu_buffer_rsrc_t rg_src = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.X + (long long)bfirst * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  __amdgpu_buffer_rsrc_t rd_src = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.D + (long long)bfirst * a.N * QQ), (short)0, 0x7FFFFFFF, 0x00020000);
+  const int4 tap_e = a.ktab[k0];
+  const int cbase = k0 % a.Cg;
+  const bool one_wrap = a.Qw >= BMR;
+  auto advance = [&]() __attribute__((always_inline)) {
+    if (one_wrap) {
+      cqw += BMR;
+      const bool w1 = cqw >= a.Qw;
+      cqw -= w1 ? a.Qw : 0;
+      cqh += w1 ? 1 : 0;
+      const bool w2 = cqh >= a.Qh;
+      cqh = w2 ? 0 : cqh;
+      cb += w2 ? 1 : 0;
+    } else {
+      const int t = cqw + BMR;
+      const int dq = t / a.Qw;
+      cqw = t - dq * a.Qw;
+      const int u = cqh + dq;
+      const int db = u / a.Qh;
+      cqh = u - db * a.Qh;
+      cb += db;
+    }
+  };
+  auto load_step = [&](Stage& S, int mstep) __attribute__((always_inline)) {
+    const bool mv = mstep + ml < mend;
+    const int rb = cb - bfirst;
+    const int vd = mv ? (int)(((long long)rb * a.N * QQ + (long long)(n0 + RJ * lr) * QQ +
+                               (long long)cqh * a.Qw + cqw) * 4) : (int)0x80000000;
+    const int ds = (int)(QQ * 4);
+    if constexpr (TU) {
+      const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
+      const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      const int vg = ok ? (int)(((long long)rb * a.Cg * HiWi + (long long)(cbase + RJ * lr) * HiWi +
+                                 (long long)hi * a.Wi + wi) * 4) : (int)0x80000000;
+      const int gs = (int)(HiWi * 4);
+#pragma unroll
+      for (int j = 0; j < RJ; ++j)
+        S.rg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+            rg_src, vg, (32 * wave + j) * gs, 0));
+    } else {
+      const int hb = cqh * a.sh, wb = cqw * a.sw;
+      const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        const int4 e = sK[rbase + j];
+        const int hi = hb + e.y, wi = wb + e.z;
+        const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+        S.rg[j] = *(ok ? a.X + xb + e.x : a.zero);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < RJ; ++j) {
+      const bool nok = n0 + rbase + j < a.N;   // only the Np-padded tail fails
+      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+          rd_src, vd, (32 * wave + j) * ds, 0));
+      S.rd[j] = nok ? v : 0.f;
+    }
+    advance();
+  };
+  auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
+    unsigned char* base = sm[buf];
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      u32x4 GH, GL, DH, DL;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        unsigned h, l;
+        split_bf16x2(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], h, l);
+        GH[e] = h; GL[e] = l;
+        split_bf16x2(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], h, l);
+        DH[e] = h; DL[e] = l;
+      }
+      const int off = wx3_off(ml, rbase / 8 + q);
+      *reinterpret_cast<u32x4*>(base + 0 * PLANE + off) = GH;
+      *reinterpret_cast<u32x4*>(base + 1 * PLANE + off) = GL;
+      *reinterpret_cast<u32x4*>(base + 2 * PLANE + off) = DH;
+      *reinterpret_cast<u32x4*>(base + 3 * PLANE + off) = DL;
+    }
+  };
+
+  f32x16 acc[RK][RN];
+#pragma unroll
+  for (int i = 0; i < RK; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int nsteps = (mend > mbeg) ? (mend - mbeg + BMR - 1) / BMR : 0;
+  // transposed-read addressing (T10): group g = lane >> 4 takes columns
+  // 16 (g & 1) .. +15 of a 32-row block and positions 8 (g >> 1) + 0..3 / 4..7;
+  // lane 4q + p of the group addresses position row q, columns 4p .. 4p + 3
+  const int g = lane >> 4, gq = (lane >> 2) & 3, gp = lane & 3;
+  auto frag = [&](const unsigned char* plane, int row0, int pos0) __attribute__((always_inline)) {
+    const int c0 = (row0 + 16 * (g & 1)) >> 3;
+    const int s0 = pos0 + 8 * (g >> 1) + gq;
+    const s16x4 x0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(plane + wx3_off(s0, c0 + (gp >> 1)) + 8 * (gp & 1)));
+    const s16x4 x1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4*)(plane + wx3_off(s0 + 4, c0 + (gp >> 1)) + 8 * (gp & 1)));
+    return __builtin_bit_cast(bf16x8, __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7));
+  };
+  auto compute = [&](int cur) __attribute__((always_inline)) {
+    const unsigned char* base = sm[cur];
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 ga[RK][2], gb[RN][2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+#pragma unroll
+        for (int i = 0; i < RK; ++i) ga[i][p] = frag(base + p * PLANE, wk * TK + 32 * i, 16 * ks);
+#pragma unroll
+        for (int j = 0; j < RN; ++j) gb[j][p] = frag(base + (2 + p) * PLANE, wnn * TN + 32 * j, 16 * ks);
+      }
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < RK; ++i)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i][t == 2 ? 1 : 0], gb[j][t == 1 ? 1 : 0],
+                                                                acc[i][j], 0, 0, 0);
+    }
+  };
+  auto interleave = [&]() __attribute__((always_inline)) {
+#if SEHIP_IGLP
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
+      __builtin_amdgcn_sched_group_barrier(0x080, 2, 0);              // DS
+      __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);              // VALU
+    }
+#endif
+  };
+  if (nsteps > 0) {
+    load_step(st0, mbeg);
+    store_step(st0, 0);
+  }
+  if (nsteps > 1) load_step(st1, mbeg + BMR);
+  __syncthreads();
+  int s = 0;
+  for (; s + 1 < nsteps; s += 2) {
+    load_step(st0, mbeg + (s + 2) * BMR);
+    compute(0);
+    store_step(st1, 1);
+    interleave();
+    __syncthreads();
+    load_step(st1, mbeg + (s + 3) * BMR);
+    compute(1);
+    store_step(st0, 0);
+    interleave();
+    __syncthreads();
+  }
+  if (s < nsteps) compute(0);
+  float* out = a.slab + (long long)split * a.Kp * a.Np;
+  const int lk = lane >> 5, lc = lane & 31;
+#pragma unroll
+  for (int i = 0; i < RK; ++i)
+#pragma unroll
+    for (int j = 0; j < RN; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int k = k0 + wk * TK + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
+        const int n = n0 + wnn * TN + 32 * j + lc;
+        out[(long long)k * a.Np + n] = acc[i][j][r];
+      }
+}

@@ -27,6 +27,7 @@ LAYERS = [
 
 
 def _hip(F, m, x, gy, transposed, stride, math):
+    prev = F.get_conv_math()
     F.set_conv_math(math)
     try:
         wr = m.real_conv.weight.detach().float().cuda().requires_grad_(True)
@@ -38,7 +39,7 @@ def _hip(F, m, x, gy, transposed, stride, math):
         torch.cuda.synchronize()
         return dict(y=y.detach().cpu(), dx=xg.grad.cpu(), dwr=wr.grad.cpu(), dwi=wi.grad.cpu())
     finally:
-        F.set_conv_math("f32")
+        F.set_conv_math(prev)
 
 
 @pytest.mark.parametrize("name,tr,cin,cout,shape,stride", LAYERS)
