@@ -115,10 +115,13 @@ typedef struct se_conv2d_desc {
                        * operand split as hi + lo bf16, a*b ~ ah*bh + ah*bl +
                        * al*bh on v_mfma_f32_32x32x16_bf16, fp32 accumulate
                        * (<= ~2^-15 relative per product; fp32 in / fp32 out).
+                       * SE_MATH_BF16X6 (2): three-way split h + m + l, six
+                       * terms (hh, hm, mh, hl, lh, mm): fp32-class products;
+                       * gather passes only (weight-grad runs SE_MATH_F32).
                        * Shapes the split kernels do not cover run SE_MATH_F32. */
 } se_conv2d_desc;
 
-enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1 };
+enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2 };
 
 /* Output spatial size (nn.Conv2d / nn.ConvTranspose2d formulas). */
 int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w);

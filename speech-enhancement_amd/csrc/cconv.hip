@@ -959,7 +959,7 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.phe = d->pad_h_end < 0 ? g.ph : d->pad_h_end;
   g.pwe = d->pad_w_end < 0 ? g.pw : d->pad_w_end;
   g.math = d->math;
-  if (g.math != SE_MATH_F32 && g.math != SE_MATH_BF16X3) return SE_E_ARG;
+  if (g.math != SE_MATH_F32 && g.math != SE_MATH_BF16X3 && g.math != SE_MATH_BF16X6) return SE_E_ARG;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
     return SE_E_ARG;
@@ -1008,11 +1008,15 @@ static inline int ldw_for(int N) {
   return round_up(N, N <= 64 ? 64 : 128);
 }
 
+// bytes per (k, n) weight element in the workspace: fp32 (4), split bf16 hi/lo
+// (4) or the three-way split (6)
+constexpr size_t kWpBytesPerElem = 6;
+
 static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N) {
   size_t bytes = 0;
   const int ldw = ldw_for(N);
   for (const auto& c : cls) {
-    bytes += (size_t)c.Kp * ldw * sizeof(float);
+    bytes += (size_t)c.Kp * ldw * kWpBytesPerElem;
     bytes += (size_t)c.Kp * sizeof(int4);
   }
   bytes += (size_t)round_up(N, 128) * sizeof(float);  // bias_full
@@ -1097,13 +1101,18 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   }
   // split-bf16 GEMM for the 128-column tiles (N > 64); other shapes stay fp32
   const bool x3 = g.math == SE_MATH_BF16X3 && N > 64;
+  const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
   for (const auto& c : cls) {
     float* Wp = (float*)p;
-    p = align256(p + (size_t)c.Kp * ldw * sizeof(float));   // = the split image's size
+    p = align256(p + (size_t)c.Kp * ldw * kWpBytesPerElem);
     int4* ktab = (int4*)p;
     p = align256(p + (size_t)c.Kp * sizeof(int4));
     const long long tot = (long long)c.Kp * ldw;
-    if (x3)
+    if (x6)
+      hipLaunchKernelGGL(prep_class_x6_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
+                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
+                         pass == kData ? 1 : 0, (unsigned short*)Wp, ktab);
+    else if (x3)
       hipLaunchKernelGGL(prep_class_x3_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
                          pass == kData ? 1 : 0, (unsigned short*)Wp, ktab);
@@ -1134,7 +1143,11 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       const long long span = (bm + qhw - 1) / qhw + 1;
       const bool tu = (Cg % kBK == 0) && span * Cg * (long long)Hi * Wi * 4 < (1ll << 31) &&
                       (long long)c.Kp * ldw * 4 < (1ll << 31);
-      if (x3) {
+      if (x6) {
+        dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
+        if (tu) hipLaunchKernelGGL(gather_x6_kernel<true>, grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL(gather_x6_kernel<false>, grid, dim3(kThreads), 0, st, a);
+      } else if (x3) {
         dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
         if (tu) hipLaunchKernelGGL(gather_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL(gather_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);

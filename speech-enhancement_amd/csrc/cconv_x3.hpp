@@ -518,3 +518,255 @@ wgrad_x3_kernel(const WgradArgs a) {
         out[(long long)k * a.Np + n] = acc[i][j][r];
       }
 }
+
+// ---------------------------------------------------------------------------
+// Three-way split ("bf16x6"): x = h + m + l (each bf16, h = rne(x),
+// m = rne(x - h), l = rne(x - h - m); both subtractions exact), 24 significant
+// bits like fp32. Six MFMA terms keep every product of order >= 2^-16:
+//   hh + hm + mh + hl + lh + mm   (dropped: ml, lm ~ 2^-24, ll ~ 2^-32)
+// so the contraction is fp32-class (per-product error ~2^-23) at 6/16 of the
+// fp32 MFMA cycles. Used for the forward pass, whose activation perturbation
+// the ill-conditioned CBN parameter gradients amplify (tools/grad_modes.py).
+// Tiles as gather_x3_kernel but BK = 16 per step (3 planes x 32-B rows).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ void split3_bf16x2(float x0, float x1, unsigned& hi, unsigned& mid,
+                                              unsigned& lo) {
+  split_bf16x2(x0, x1, hi, mid);
+  const float m0 = __builtin_bit_cast(float, mid << 16);
+  const float m1 = __builtin_bit_cast(float, mid & 0xffff0000u);
+  const float h0 = __builtin_bit_cast(float, hi << 16);
+  const float h1 = __builtin_bit_cast(float, hi & 0xffff0000u);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector((f32x2){(x0 - h0) - m0, (x1 - h1) - m1}, bf16x2));
+}
+
+constexpr int kX6BK = 16;
+constexpr int kX6TileU4 = 3 * 128 * 2;   // u32x4 per (k-step, n-tile) weight image = 12 KB
+// 32-B rows (2 chunks): chunk c of row r at c ^ ((r >> 3) & 1) -> ds_read_b128
+// fragment reads conflict-free in every 16-lane group
+__device__ __forceinline__ int x6_chunk(int row, int c) { return c ^ ((row >> 3) & 1); }
+
+// Wt[(s * NT + t) * kX6TileU4 + (plane * 128 + n) * 2 + x6_chunk(n, c)]: element e of
+// k = 16 s + 8 c + e, column 128 t + n. Also ktab.
+__global__ void prep_class_x6_kernel(WeightView w, TapList taps, int Cg, int N, int Kp, int NT,
+                                     int Hi, int Wi, int data_grad, unsigned short* Wt, int4* ktab) {
+  const int K = taps.n * Cg;
+  const long long total = (long long)Kp * NT * 128;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(idx % Kp);
+    const int n = (int)(idx / Kp);
+    float v = 0.f;
+    if (k < K && n < N) {
+      const int t = k / Cg, c = k % Cg;
+      const int ci = data_grad ? n : c, co = data_grad ? c : n;
+      v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
+    }
+    const float h = (float)(__bf16)v;
+    const float mv = (float)(__bf16)(v - h);
+    const unsigned short hb = bf16_bits(v), mb = bf16_bits(v - h), lb = bf16_bits((v - h) - mv);
+    const int s = k >> 4, kc = (k >> 3) & 1, e = k & 7;
+    const int tn = n >> 7, nl = n & 127;
+    const long long base = ((long long)s * NT + tn) * kX6TileU4 * 8;
+    const long long off = ((long long)nl * 2 + x6_chunk(nl, kc)) * 8 + e;
+    Wt[base + off] = hb;
+    Wt[base + 128 * 2 * 8 + off] = mb;
+    Wt[base + 2 * 128 * 2 * 8 + off] = lb;
+    if (n == 0) {
+      int4 q;
+      if (k < K) {
+        const int t = k / Cg, c = k % Cg;
+        q.x = (int)((long long)c * Hi * Wi + (long long)taps.offh[t] * Wi + taps.offw[t]);
+        q.y = taps.offh[t];
+        q.z = taps.offw[t];
+      } else {
+        q.x = 0; q.y = kInvalidOff; q.z = 0;
+      }
+      q.w = 0;
+      ktab[k] = q;
+    }
+  }
+}
+
+template <bool TU>
+__global__ void __launch_bounds__(kThreads, 2)
+gather_x6_kernel(const GatherArgs a) {
+  constexpr int BN = kX3BN, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
+  constexpr int BK = kX6BK, AJ = 8;               // gathered k per thread per step
+  __shared__ __attribute__((aligned(16))) u32x4 sA[2][3 * BM * 2];
+  __shared__ __attribute__((aligned(16))) u32x4 sW[2][3 * BN * 2];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave / WM, wm = wave % WM;
+  const int NT = gridDim.y;
+  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
+  const int mt = tile / NT, nt = tile % NT;
+  const int m0 = mt * BM, n0 = nt * BN;
+  const long long HiWi = (long long)a.Hi * a.Wi;
+
+  const int am = tid % BM;
+  const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // 0 or 1 (wave-uniform)
+  const int m = m0 + am;
+  const bool mval = m < a.M;
+  int hb = 0, wb = 0;
+  long long xbase = 0;
+  if (mval) {
+    const int qhw = a.Qh * a.Qw;
+    const int b = m / qhw, r = m - b * qhw;
+    const int qh = r / a.Qw, qw = r - qh * a.Qw;
+    hb = qh * a.sh;
+    wb = qw * a.sw;
+    xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+  }
+  struct Stage { float ra[AJ]; u32x4 rw[3]; };
+  Stage s0, s1;
+  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
+    const unsigned long long v = (unsigned long long)p;
+    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
+    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
+    return (void*)(((unsigned long long)hi << 32) | lo);
+  };
+  const int b0 = m0 / (a.Qh * a.Qw);
+  __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      uniform_ptr(a.X + (long long)b0 * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * kX6TileU4 + tid;
+  int xoff = 0;
+  if constexpr (TU) {
+    if (mval) {
+      const int b = m / (a.Qh * a.Qw);
+      xoff = (int)(((long long)(b - b0) * a.Cg * HiWi + (long long)hb * a.Wi + wb) * 4);
+    }
+  }
+  auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
+    if constexpr (TU) {
+      const int4 e0 = a.ktab[k0];
+      const int tap = k0 / a.Cg;
+      const int c0 = k0 - tap * a.Cg + AJ * akr;
+      const int hi = hb + e0.y, wi = wb + e0.z;
+      const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      const int vo = ok ? xoff + (e0.y * a.Wi + e0.z) * 4 : (int)0x80000000;
+      const int cs = (int)(HiWi * 4);
+#pragma unroll
+      for (int j = 0; j < AJ; ++j)
+        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (c0 + j) * cs, 0));
+    } else {
+#pragma unroll
+      for (int j = 0; j < AJ; ++j) {
+        const int4 e = a.ktab[k0 + AJ * akr + j];
+        const int hi = hb + e.y, wi = wb + e.z;
+        const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+        st.ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
+      }
+    }
+    const u32x4* src = wt + (long long)(k0 / BK) * NT * kX6TileU4;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) st.rw[j] = src[kThreads * j];
+  };
+  const int wchunk = x6_chunk(am, akr);
+  auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
+    u32x4 H, M, L;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned h, mm, l;
+      split3_bf16x2(st.ra[2 * e], st.ra[2 * e + 1], h, mm, l);
+      H[e] = h; M[e] = mm; L[e] = l;
+    }
+    sA[buf][am * 2 + wchunk] = H;
+    sA[buf][BM * 2 + am * 2 + wchunk] = M;
+    sA[buf][2 * BM * 2 + am * 2 + wchunk] = L;
+#pragma unroll
+    for (int j = 0; j < 3; ++j) sW[buf][tid + kThreads * j] = st.rw[j];
+  };
+
+  f32x16 acc[RN][RM];
+#pragma unroll
+  for (int i = 0; i < RN; ++i)
+#pragma unroll
+    for (int j = 0; j < RM; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+
+  const int lh = lane >> 5, lr = lane & 31;
+  const int fc = x6_chunk(lr, lh);
+  auto compute = [&](int cur) __attribute__((always_inline)) {
+    u32x4 wf[RN][3], af[RM][3];   // [block][plane]
+#pragma unroll
+    for (int p = 0; p < 3; ++p) {
+#pragma unroll
+      for (int i = 0; i < RN; ++i) wf[i][p] = sW[cur][(p * BN + wn * TN + 32 * i + lr) * 2 + fc];
+#pragma unroll
+      for (int j = 0; j < RM; ++j) af[j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 2 + fc];
+    }
+    // terms (weight plane, activation plane), small terms first
+    constexpr int TA[6] = {1, 2, 0, 1, 0, 0};
+    constexpr int TB[6] = {1, 0, 2, 0, 1, 0};
+#pragma unroll
+    for (int t = 0; t < 6; ++t)
+#pragma unroll
+      for (int i = 0; i < RN; ++i)
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
+              __builtin_bit_cast(bf16x8, wf[i][TA[t]]), __builtin_bit_cast(bf16x8, af[j][TB[t]]),
+              acc[i][j], 0, 0, 0);
+  };
+  auto interleave = [&]() __attribute__((always_inline)) {
+#if SEHIP_IGLP
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
+#pragma unroll
+    for (int i = 0; i < 24; ++i) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
+      if (i < 14) __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);    // DS
+      if (i < 11) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
+    }
+#endif
+  };
+
+  const int nk = a.Kp / BK;
+  load_tile(s0, 0);
+  store_tile(s0, 0);
+  if (nk > 1) load_tile(s1, BK);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    load_tile(s0, min(kt + 2, nk - 1) * BK);
+    compute(0);
+    store_tile(s1, 1);
+    interleave();
+    __syncthreads();
+    load_tile(s1, min(kt + 3, nk - 1) * BK);
+    compute(1);
+    store_tile(s0, 0);
+    interleave();
+    __syncthreads();
+  }
+  if (kt < nk) compute(0);
+
+  __syncthreads();
+  float* sBias = reinterpret_cast<float*>(&sW[0][0]);
+  for (int i = tid; i < BN; i += kThreads) {
+    const int n = n0 + i;
+    sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
+  }
+  __syncthreads();
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  const bool full_n = n0 + BN <= a.N;
+#pragma unroll
+  for (int j = 0; j < RM; ++j) {
+    const int mm = m0 + wm * TM + 32 * j + lr;
+    if (mm >= a.M) continue;
+    const int qhw = a.Qh * a.Qw;
+    const int b = mm / qhw, r = mm - b * qhw;
+    const int qh = r / a.Qw, qw = r - qh * a.Qw;
+    const int nl0 = wn * TN + 4 * lh;
+    float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
+                (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int r2 = 0; r2 < 16; ++r2) {
+        const int nl = 32 * i + (r2 & 3) + 8 * (r2 >> 2);
+        if (full_n || n0 + nl0 + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
+      }
+  }
+}

@@ -59,7 +59,7 @@ _TIMER: OpTimer | None = None
 # (hi*hi + hi*lo + lo*hi) on v_mfma_f32_32x32x16_bf16, fp32 accumulate.
 # Initial value from SEHIP_CONV_MATH ("f32", "bf16x3", or per pass as
 # "fwd=bf16x3,data=f32,weight=bf16x3"); set_conv_math() changes it.
-_MATH_CODES = {"f32": 0, "bf16x3": 1}
+_MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2}
 _PASSES = ("fwd", "data", "weight")
 _CONV_MATH = {p: 0 for p in _PASSES}
 
@@ -112,6 +112,7 @@ def _gemm_tag(pass_name, d):
     if pass_name == "weight":
         n = d.in_channels if tr else d.out_channels          # channels of the direct operand
         kind = "smalln" if n <= 8 else (names[_CONV_MATH["weight"]] if n > 32 else "f32")
+        kind = "f32" if kind == "bf16x6" else kind
         return f"conv_wgrad_{kind}"
     n = d.out_channels if pass_name == "fwd" else d.in_channels
     kind = "smalln" if n <= 16 else (names[_CONV_MATH[pass_name]] if n > 64 else "f32")

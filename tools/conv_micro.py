@@ -15,7 +15,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument("--layers", default="enc1,dec5")
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--passes", default="fwd,data,weight")
-ap.add_argument("--math", default="f32,bf16x3", help="conv math modes to time (se_conv2d_desc.math)")
+ap.add_argument("--math", default="f32,bf16x3,bf16x6", help="conv math modes to time (se_conv2d_desc.math)")
 args = ap.parse_args()
 dev = torch.device("cuda")
 for name in args.layers.split(","):
