@@ -38,6 +38,9 @@ KERNEL_OF = {   # OpTimer tag -> (rocprof kernel name, description)
     "conv_fwd_f32": ("gather_gemm_kernel", "gather_gemm_kernel (se_conv2d_fwd, fp32 MFMA 32x32x2)"),
     "conv_data_f32": ("gather_gemm_kernel", "gather_gemm_kernel (se_conv2d_bwd_data, fp32 MFMA 32x32x2)"),
     "conv_fwd_bf16x3": ("gather_x3_kernel", "gather_x3_kernel (se_conv2d_fwd, split-bf16 MFMA 32x32x16 x3)"),
+    "conv_fwd_bf16x6": ("gather_x6_kernel", "gather_x6_kernel (se_conv2d_fwd, 3-way split-bf16 MFMA 32x32x16 x6)"),
+    "conv_data_bf16x6": ("gather_x6_kernel",
+                         "gather_x6_kernel (se_conv2d_bwd_data, 3-way split-bf16 MFMA 32x32x16 x6)"),
     "conv_data_bf16x3": ("gather_x3_kernel",
                          "gather_x3_kernel (se_conv2d_bwd_data, split-bf16 MFMA 32x32x16 x3)"),
     "conv_wgrad_f32": ("wgrad_gemm_kernel", "wgrad_gemm_kernel (se_conv2d_bwd_weight, fp32 MFMA 32x32x2)"),
@@ -195,7 +198,9 @@ def main():
         "conv_math": SF.get_conv_math(),
         "conv_math_note": "fp32 storage and accumulation everywhere; 'bf16x3' passes split each fp32 "
                           "operand into hi+lo bf16 and sum hi*hi+hi*lo+lo*hi on bf16 MFMA (4.5e-6 "
-                          "rel-L2 per conv vs fp64; tests/test_gpu_conv_x3.py); forward exact fp32",
+                          "rel-L2 per conv vs fp64); 'bf16x6' splits three ways and sums the six "
+                          "terms of order >= 2^-16 (5.5e-7 vs fp64, fp32 MFMA path 6.4e-7); "
+                          "tests/test_gpu_conv_x3.py",
     }
     if f32_exact:
         out["f32_exact"] = f32_exact
@@ -205,8 +210,9 @@ def main():
         tag = max(convs, key=lambda k: convs[k]["ms"])
         g = convs[tag]
         ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
-        split = tag.endswith("bf16x3")
-        peak = BF16_MFMA_PEAK_TFLOPS / 3 if split else FP32_MFMA_PEAK_TFLOPS
+        terms = 3 if tag.endswith("bf16x3") else 6 if tag.endswith("bf16x6") else 0
+        split = terms > 0
+        peak = BF16_MFMA_PEAK_TFLOPS / terms if split else FP32_MFMA_PEAK_TFLOPS
         out["roofline"] = {
             "bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1),
             "unit": "TFLOP/s", "frac": round(ach / peak, 4),
@@ -216,7 +222,7 @@ def main():
             "algorithmic_flops_per_call": g["flops"] / g["calls"],
             "algorithmic_bytes_per_call": g["bytes"] / g["calls"],
             "flops_convention": "algorithmic fp32 conv FLOPs (torch FlopCounterMode formula)"
-                                + ("; peak = bf16 dense MFMA peak / 3 MFMA terms per fp32 product"
+                                + (f"; peak = bf16 dense MFMA peak / {terms} MFMA terms per fp32 product"
                                    if split else "")}
         st = kern.get("stft_fwd")
         if st and stft_burst_ms:
