@@ -6,8 +6,9 @@ forward, SI-SNR, backward, clip_grad_norm_(0.5), AdamW) on 64 synthetic
 4 s @ 16 kHz noisy/clean pairs per GPU, inputs resident in HBM.
 fp32 storage and accumulation throughout (the reference's precision; parity
 is judged at 1e-4 fp32). The conv GEMMs' MFMA form follows SEHIP_CONV_MATH /
---math (default: exact fp32 forward, split-bf16 data/weight-grad GEMMs); the
-all-fp32 step is timed beside it (`f32_exact`).
+--math (default: three-way split-bf16 forward, fp32-class; two-way split
+data/weight-grad GEMMs); the all-fp32-MFMA step (`f32_exact`) and the one-term
+bf16 step (`other_conv_math`) are timed beside it.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -46,7 +47,11 @@ KERNEL_OF = {   # OpTimer tag -> (rocprof kernel name, description)
     "conv_wgrad_f32": ("wgrad_gemm_kernel", "wgrad_gemm_kernel (se_conv2d_bwd_weight, fp32 MFMA 32x32x2)"),
     "conv_wgrad_bf16x3": ("wgrad_x3_kernel",
                           "wgrad_x3_kernel (se_conv2d_bwd_weight, split-bf16 MFMA 32x32x16 x3)"),
+    "conv_fwd_bf16": ("gather_x3_kernel", "gather_x3_kernel<TERMS=1> (se_conv2d_fwd, bf16 MFMA 32x32x16)"),
+    "conv_data_bf16": ("gather_x3_kernel", "gather_x3_kernel<TERMS=1> (se_conv2d_bwd_data, bf16 MFMA 32x32x16)"),
+    "conv_wgrad_bf16": ("wgrad_x3_kernel", "wgrad_x3_kernel<TERMS=1> (se_conv2d_bwd_weight, bf16 MFMA 32x32x16)"),
 }
+TERMS_OF = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}   # MFMA terms per fp32 product (peak divisor)
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
 SR, SECONDS = 16000, 4
 
@@ -61,8 +66,11 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-op-timing", action="store_true")
-    ap.add_argument("--no-compare-f32", dest="compare_f32", action="store_false",
-                    help="skip the all-fp32 comparison run")
+    ap.add_argument("--compare", default="f32,bf16",
+                    help="conv math modes timed beside the default step (untimed by the op timer): "
+                         "all-fp32 MFMA and the one-term bf16 GEMMs; '' for none")
+    ap.add_argument("--no-compare", "--no-compare-f32", dest="compare", action="store_const", const="",
+                    help="skip the comparison runs")
     ap.add_argument("--math", default=os.environ.get("SEHIP_CONV_MATH"),
                     help="conv GEMM MFMA form (se_conv2d_desc.math): f32, bf16x3, or per pass "
                          "'fwd=bf16x3,data=f32,weight=bf16x3'")
@@ -154,12 +162,13 @@ def main():
             torch.cuda.synchronize()
             stft_burst_ms = e0.elapsed_time(e1) / 20
 
-    # the same step with every conv pass on the exact fp32 MFMA kernels (untimed by
-    # the op timer), for comparison with the default split-bf16 backward
-    f32_exact = None
-    if args.compare_f32 and SF.get_conv_math() != "f32":
-        mode = SF.get_conv_math()
-        SF.set_conv_math("f32")
+    # the same step with every conv pass in another MFMA form (untimed by the op
+    # timer): "f32" = exact fp32 products everywhere; "bf16" = one-term bf16
+    # operands (fp32 storage/accumulation), the speed form of SURVEY §8d config 4
+    compare = {}
+    default_mode = SF.get_conv_math()
+    for mode in [m for m in args.compare.split(",") if m and m != default_mode]:
+        SF.set_conv_math(mode)
         noisy, clean = batches[0]
         train_step(model, opt, noisy, clean)
         torch.cuda.synchronize()
@@ -168,7 +177,7 @@ def main():
         t1 = time.perf_counter()
         for i in range(args.steps):
             noisy, clean = batches[i % 2]
-            train_step(model, opt, noisy, clean)
+            lc = train_step(model, opt, noisy, clean)
         torch.cuda.synchronize()
         if dist:
             dist.barrier()
@@ -177,9 +186,9 @@ def main():
             t = torch.tensor([e2], device=device, dtype=torch.float64)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             e2 = float(t.item())
-        SF.set_conv_math(mode)
-        f32_exact = {"conv_math": "f32", "value": round(world * B * args.steps / e2, 3),
-                     "ms_per_step": round(1e3 * e2 / args.steps, 3)}
+        compare[mode] = {"conv_math": mode, "value": round(world * B * args.steps / e2, 3),
+                         "ms_per_step": round(1e3 * e2 / args.steps, 3), "final_loss": round(float(lc), 4)}
+    SF.set_conv_math(default_mode)
 
     if rank != 0:
         return
@@ -202,15 +211,17 @@ def main():
                           "terms of order >= 2^-16 (5.5e-7 vs fp64, fp32 MFMA path 6.4e-7); "
                           "tests/test_gpu_conv_x3.py",
     }
-    if f32_exact:
-        out["f32_exact"] = f32_exact
+    if "f32" in compare:
+        out["f32_exact"] = compare.pop("f32")
+    if compare:
+        out["other_conv_math"] = list(compare.values())
     if kern:
         # dominant GEMM kernel = the conv pass/kernel with the most time in the step
         convs = {k: v for k, v in kern.items() if k.startswith("conv_") and v["flops"]}
         tag = max(convs, key=lambda k: convs[k]["ms"])
         g = convs[tag]
         ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
-        terms = 3 if tag.endswith("bf16x3") else 6 if tag.endswith("bf16x6") else 0
+        terms = TERMS_OF.get(tag.rsplit("_", 1)[-1], 0)
         split = terms > 0
         peak = BF16_MFMA_PEAK_TFLOPS / terms if split else FP32_MFMA_PEAK_TFLOPS
         out["roofline"] = {

@@ -118,10 +118,13 @@ typedef struct se_conv2d_desc {
                        * SE_MATH_BF16X6 (2): three-way split h + m + l, six
                        * terms (hh, hm, mh, hl, lh, mm): fp32-class products;
                        * gather passes only (weight-grad runs SE_MATH_F32).
+                       * SE_MATH_BF16 (3): operands rounded to bf16, one MFMA
+                       * term, fp32 accumulate and storage (the arithmetic of a
+                       * bf16 autocast conv; BASELINE configs 2/3).
                        * Shapes the split kernels do not cover run SE_MATH_F32. */
 } se_conv2d_desc;
 
-enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2 };
+enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3 };
 
 /* Output spatial size (nn.Conv2d / nn.ConvTranspose2d formulas). */
 int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w);

@@ -959,7 +959,7 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.phe = d->pad_h_end < 0 ? g.ph : d->pad_h_end;
   g.pwe = d->pad_w_end < 0 ? g.pw : d->pad_w_end;
   g.math = d->math;
-  if (g.math != SE_MATH_F32 && g.math != SE_MATH_BF16X3 && g.math != SE_MATH_BF16X6) return SE_E_ARG;
+  if (g.math < SE_MATH_F32 || g.math > SE_MATH_BF16) return SE_E_ARG;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
     return SE_E_ARG;
@@ -1099,8 +1099,9 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     hipLaunchKernelGGL(prep_bias_kernel, dim3(se::ceil_div(N, 256)), dim3(256), 0, st,
                        bias_br, bias_bi, N, g.complex_w, bias_full);
   }
-  // split-bf16 GEMM for the 128-column tiles (N > 64); other shapes stay fp32
-  const bool x3 = g.math == SE_MATH_BF16X3 && N > 64;
+  // split-bf16 / bf16 GEMM for the 128-column tiles (N > 64); other shapes stay fp32
+  const bool bf1 = g.math == SE_MATH_BF16 && N > 64;             // one term: hi*hi
+  const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1;   // prep / tiles shared
   const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
   for (const auto& c : cls) {
     float* Wp = (float*)p;
@@ -1147,6 +1148,10 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
         dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
         if (tu) hipLaunchKernelGGL(gather_x6_kernel<true>, grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL(gather_x6_kernel<false>, grid, dim3(kThreads), 0, st, a);
+      } else if (bf1) {
+        dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
+        if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
+        else hipLaunchKernelGGL((gather_x3_kernel<false, 1>), grid, dim3(kThreads), 0, st, a);
       } else if (x3) {
         dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
         if (tu) hipLaunchKernelGGL(gather_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
@@ -1261,6 +1266,10 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
     if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
+  } else if (g.math == SE_MATH_BF16) {
+    dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
+    if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1>), grid, dim3(kThreads), 0, st, a);
   } else {
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 128, 2, 2, 32, true>), grid, dim3(kThreads), 0, st, a);

@@ -88,9 +88,14 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // Per K-step (BK = 32) a wave issues 2 k-substeps x 2 x 2 blocks x 3 terms =
 // 24 MFMAs of 32 cycles; each thread gathers 16 consecutive k of one m column
 // (k = k0 + 16 * akr + j), splits them in registers and writes 4 ds_write_b128.
-template <bool TU>
+// TERMS = 1 is the plain bf16 GEMM (SE_MATH_BF16: operands rounded to bf16,
+// fp32 accumulate, the arithmetic of autocast's bf16 conv): only the hi planes
+// are staged and read.
+template <bool TU, int TERMS = 3>
 __global__ void __launch_bounds__(kThreads, 2)
 gather_x3_kernel(const GatherArgs a) {
+  static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
+  constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
   constexpr int BN = kX3BN, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
   constexpr int AJ = 16;                          // gathered k per thread per step
   __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * BM * 4];
@@ -160,7 +165,7 @@ gather_x3_kernel(const GatherArgs a) {
     }
     const u32x4* src = wt + (long long)(k0 >> 5) * NT * kX3TileU4;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) st.rw[j] = src[kThreads * j];
+    for (int j = 0; j < 2 * PL; ++j) st.rw[j] = src[kThreads * j];   // hi plane first
   };
   const int swz = (am >> 2) & 3;
   auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
@@ -176,10 +181,10 @@ gather_x3_kernel(const GatherArgs a) {
       }
       const int c = (2 * akr + q) ^ swz;
       sA[buf][am * 4 + c] = H;
-      sA[buf][BM * 4 + am * 4 + c] = L;
+      if constexpr (PL == 2) sA[buf][BM * 4 + am * 4 + c] = L;
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) sW[buf][tid + kThreads * j] = st.rw[j];
+    for (int j = 0; j < 2 * PL; ++j) sW[buf][tid + kThreads * j] = st.rw[j];
   };
 
   f32x16 acc[RN][RM];
@@ -193,25 +198,25 @@ gather_x3_kernel(const GatherArgs a) {
   const int lh = lane >> 5, lr = lane & 31;
   const int fsw = (lr >> 2) & 3;
   auto compute = [&](int cur) __attribute__((always_inline)) {
-    u32x4 wf[2][RN][2], af[2][RM][2];   // [ks][block][plane]
+    u32x4 wf[2][RN][PL], af[2][RM][PL];   // [ks][block][plane]
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c = (2 * ks + lh) ^ fsw;
 #pragma unroll
       for (int i = 0; i < RN; ++i)
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < PL; ++p)
           wf[ks][i][p] = sW[cur][(p * BN + wn * TN + 32 * i + lr) * 4 + c];
 #pragma unroll
       for (int j = 0; j < RM; ++j)
 #pragma unroll
-        for (int p = 0; p < 2; ++p)
+        for (int p = 0; p < PL; ++p)
           af[ks][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
     }
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-      for (int t = 0; t < 3; ++t)      // terms: hi*hi, hi*lo, lo*hi
+      for (int t = 0; t < TERMS; ++t)  // terms: hi*hi, hi*lo, lo*hi
 #pragma unroll
         for (int i = 0; i < RN; ++i)
 #pragma unroll
@@ -303,9 +308,11 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
   return 256 * s + 16 * (ch ^ (((s & 3) << 2) | ((s >> 2) & 3)));
 }
 
-template <bool TU>
+template <bool TU, int TERMS = 3>
 __global__ void __launch_bounds__(kThreads, 2)
 wgrad_x3_kernel(const WgradArgs a) {
+  static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
+  constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
   constexpr int BKO = 128, BNO = 128, WNn = 2, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
   constexpr int RJ = 16;                     // rows per thread per operand
   constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
@@ -423,9 +430,11 @@ wgrad_x3_kernel(const WgradArgs a) {
       }
       const int off = wx3_off(ml, rbase / 8 + q);
       *reinterpret_cast<u32x4*>(base + 0 * PLANE + off) = GH;
-      *reinterpret_cast<u32x4*>(base + 1 * PLANE + off) = GL;
       *reinterpret_cast<u32x4*>(base + 2 * PLANE + off) = DH;
-      *reinterpret_cast<u32x4*>(base + 3 * PLANE + off) = DL;
+      if constexpr (PL == 2) {
+        *reinterpret_cast<u32x4*>(base + 1 * PLANE + off) = GL;
+        *reinterpret_cast<u32x4*>(base + 3 * PLANE + off) = DL;
+      }
     }
   };
 
@@ -455,16 +464,16 @@ wgrad_x3_kernel(const WgradArgs a) {
     const unsigned char* base = sm[cur];
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
-      bf16x8 ga[RK][2], gb[RN][2];
+      bf16x8 ga[RK][PL], gb[RN][PL];
 #pragma unroll
-      for (int p = 0; p < 2; ++p) {
+      for (int p = 0; p < PL; ++p) {
 #pragma unroll
         for (int i = 0; i < RK; ++i) ga[i][p] = frag(base + p * PLANE, wk * TK + 32 * i, 16 * ks);
 #pragma unroll
         for (int j = 0; j < RN; ++j) gb[j][p] = frag(base + (2 + p) * PLANE, wnn * TN + 32 * j, 16 * ks);
       }
 #pragma unroll
-      for (int t = 0; t < 3; ++t)
+      for (int t = 0; t < TERMS; ++t)
 #pragma unroll
         for (int i = 0; i < RK; ++i)
 #pragma unroll

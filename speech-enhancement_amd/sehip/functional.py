@@ -57,9 +57,12 @@ _TIMER: OpTimer | None = None
 # MFMA form of the conv GEMMs (se_conv2d_desc.math), per pass: "f32" = exact
 # fp32 products on v_mfma_f32_32x32x2_f32; "bf16x3" = split-bf16 operands
 # (hi*hi + hi*lo + lo*hi) on v_mfma_f32_32x32x16_bf16, fp32 accumulate.
+# "bf16x6" = three-way split, six terms (fp32-class); "bf16" = operands rounded
+# to bf16, one term (the low-precision configs' arithmetic: BASELINE configs
+# 2/3, judged against the fp32 oracle with the reference's own bf16 drift).
 # Initial value from SEHIP_CONV_MATH ("f32", "bf16x3", or per pass as
 # "fwd=bf16x3,data=f32,weight=bf16x3"); set_conv_math() changes it.
-_MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2}
+_MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2, "bf16": 3}
 _PASSES = ("fwd", "data", "weight")
 _CONV_MATH = {p: 0 for p in _PASSES}
 

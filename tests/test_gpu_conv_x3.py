@@ -69,6 +69,31 @@ def test_bf16x3_layer_vs_fp64_oracle(name, tr, cin, cout, shape, stride, gpu_dev
         assert ex6 < max(3 * e32, 1e-6), (name, k, ex6, e32)
 
 
+BF16_TOL = 1e-2   # one bf16 rounding per operand: ~2^-9 relative, rms ~3e-3 on random data
+
+
+@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", LAYERS[:4])
+def test_bf16_layer_vs_fp64_oracle(name, tr, cin, cout, shape, stride, gpu_device):
+    """SE_MATH_BF16 (one MFMA term, operands rounded to bf16, fp32 accumulate):
+    every pass within bf16 rounding of fp64, and measurably coarser than
+    bf16x3 (so the one-term kernels really ran)."""
+    from sehip import functional as F
+    cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
+    m = paramfill.fill_(cls(cin, cout, (5, 2), stride=stride, bias=False), seed=7).double()
+    gen = torch.Generator().manual_seed(3)
+    x = torch.randn(*shape, generator=gen, dtype=torch.float64)
+    xo = x.clone().requires_grad_(True)
+    yo = m(xo)
+    gy = torch.randn(yo.shape, generator=gen, dtype=torch.float64)
+    yo.backward(gy)
+    ref = dict(y=yo.detach(), dx=xo.grad, dwr=m.real_conv.weight.grad, dwi=m.imag_conv.weight.grad)
+    b1 = _hip(F, m, x, gy, tr, stride, "bf16")
+    for k, r in ref.items():
+        e = rel_l2(b1[k].numpy(), r.numpy())
+        print(f"{name} {k}: bf16 {e:.2e}")
+        assert 1e-4 < e < BF16_TOL, (name, k, e)
+
+
 CONV_CASES = [
     ("enc", False, 16, 12, (5, 2), dict(stride=(2, 1), bias=False)),
     ("dec", True, 16, 12, (5, 2), dict(stride=(2, 1), bias=False)),
