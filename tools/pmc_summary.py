@@ -12,6 +12,9 @@ import collections, csv, json, os, re, sys
 
 def load(d, counter):
     path = os.path.join(d, "run_counter_collection.csv")
+    if not os.path.exists(path):   # rocprofv3 -d without -o: <d>/<host>/<pid>_counter_collection.csv
+        import glob
+        path = sorted(glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True))[-1]
     per = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
