@@ -85,6 +85,18 @@ struct GatherArgs {
   int N, Ho, Wo;
   int ph, pw, Sh, Sw, Qh, Qw, sh, sw;
   int Kp, ldw, M;
+  // FRCRN decoder skip join folded into the GEMM (se_conv2d_*_joined,
+  // frcrn.py:93-101): the joined tensor complex_concat([align(x), s]) has the
+  // channel chunks [x_re, s_re, x_im, s_im] of jh channels each and is never
+  // materialised. Gather side (jh > 0): X holds s (grid Hi x Wi, 2*jh channels
+  // per batch item), X2 holds x on its own grid H2 x W2 (rows >= H2 read as 0:
+  // F.pad; columns >= Wi are never read: x[..., :-1]).
+  const float* X2;
+  int jh, H2, W2;
+  // Output side (yjh > 0, data-grad): the chunks of Y go to Y (s chunks, grid
+  // Ho x Wo) and Y2 (x chunks, grid YH2 x YW2; rows >= YH2 are dropped).
+  float* Y2;
+  int yjh, YH2, YW2;
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -398,6 +410,10 @@ struct WgradArgs {
   int N, Qh, Qw, sh, sw;
   int Kp, Np, M;
   int m_per_split;     // multiple of the kernel's BMR (64)
+  // joined D (transposed conv over the decoder skip join, see GatherArgs):
+  // D holds s (2*djh channels, grid Qh x Qw), D2 holds x on DH2 x DW2.
+  const float* D2;
+  int djh, DH2, DW2;
 };
 
 // Small-N weight grad (N <= 8: FRCRN's final_conv 128->2 and the CCBAM spatial

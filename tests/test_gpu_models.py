@@ -47,16 +47,26 @@ def test_model_forward_golden(i, gpu_device):
 
 # BASELINE configs 2 (DCUNet-16 inference bf16) and 3 (DCCRN training bf16):
 # the conv GEMMs in SE_MATH_BF16 (operands rounded to bf16, fp32 accumulate and
-# storage). SURVEY.md §8c: the reference's own bf16 run of DCUNet-16 is 4.4e-2
-# rel-L2 off its fp32 output, so the bar is that drift, against the fp32 golden.
-BF16_DRIFT = 4.4e-2
+# storage). SURVEY.md §8c: low-precision configs are judged against the fp32
+# golden with the tolerance set by the oracle's own low-precision drift: the
+# oracle run in bf16 on the CPU (model.to(bfloat16), as the reference's bf16
+# run) on the same parameters and input.
+def _oracle_bf16_drift(i, mode, g):
+    from oracle import models as O
+    ctors = {1: lambda: O.DCCRN("dccrn-CL", 400, 100, 512), 2: lambda: O.DCUNet("dcunet16", 512, 128, 512)}
+    m = paramfill.fill_(ctors[i](), seed=20 + i).to(torch.bfloat16)
+    m = m.eval() if mode == "eval" else m.train()
+    with torch.no_grad():
+        spec, wav = m(torch.from_numpy(g["x"]).to(torch.bfloat16))
+    return (rel_l2(spec.float().numpy(), g[f"spec_{mode}"]), rel_l2(wav.float().numpy(), g[f"wav_{mode}"]))
 
 
 @pytest.mark.parametrize("i,mode", [(2, "eval"), (1, "train")])
-def test_bf16_configs_within_reference_bf16_drift(i, mode, gpu_device):
+def test_bf16_configs_within_oracle_bf16_drift(i, mode, gpu_device):
     from sehip import functional as F
     name, ctor = _models()[i]
     g = golden(f"model_{name}")
+    ds, dw = _oracle_bf16_drift(i, mode, g)
     prev = F.get_conv_math()
     F.set_conv_math("bf16")
     try:
@@ -74,8 +84,11 @@ def test_bf16_configs_within_reference_bf16_drift(i, mode, gpu_device):
         torch.cuda.synchronize()
         es = rel_l2(spec.detach().cpu().numpy(), g[f"spec_{mode}"])
         ew = rel_l2(wav.detach().cpu().numpy(), g[f"wav_{mode}"])
-        print(f"{name} {mode} bf16: spec {es:.2e} wav {ew:.2e}")
-        assert es < BF16_DRIFT and ew < BF16_DRIFT, (name, es, ew)
+        print(f"{name} {mode} bf16 GEMMs: spec {es:.2e} wav {ew:.2e}; "
+              f"oracle in bf16: spec {ds:.2e} wav {dw:.2e}")
+        # the two round at different points (bf16 storage everywhere vs bf16 GEMM
+        # operands only); measured 0.98x / 0.98x the oracle's drift on DCUNet-16
+        assert es < 1.25 * ds and ew < 1.25 * dw, (name, es, ew, ds, dw)
     finally:
         F.set_conv_math(prev)
 
