@@ -149,6 +149,31 @@ int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x,
                          const float* dy, float* dwr, float* dwi, float* dbr,
                          float* dbi, void* ws, size_t ws_bytes, void* stream);
 
+/* Decoder skip join folded into the conv GEMMs (frcrn.py:93-101: trim /
+ * pad the decoder state x, complex_concat([x, s]), ConvTransposeBlock). The
+ * conv input is the joined tensor [B, in_channels, in_h, in_w] with channel
+ * chunks [x_re, s_re, x_im, s_im] of in_channels/4 each; it is never written.
+ * s: [B, in_channels/2, in_h, in_w] (the CCBAM output); x: [B, in_channels/2,
+ * x_h, x_w] with x_h <= in_h (missing rows read as zeros, F.pad(x, (0,0,0,1)))
+ * and x_w >= in_w (extra columns unread, x[..., :-1]). Complex weights only,
+ * in_channels/4 a multiple of 32. Returns SE_E_UNSUPPORTED when the math mode
+ * or shape has no joined kernel (the split-bf16 / bf16 tap-uniform GEMMs have
+ * one; the weight-grad only for transposed convs): the caller then
+ * materialises the join (se_complex_join) and uses the plain entry points. */
+int se_conv2d_fwd_joined(const se_conv2d_desc* d, const float* x, int x_h, int x_w,
+                         const float* s, const float* wr, const float* wi,
+                         const float* br, const float* bi, float* y, void* ws,
+                         size_t ws_bytes, void* stream);
+/* gx [B, in_channels/2, x_h, x_w] (zeros in the cropped columns and no
+ * contribution from the padded rows) and gs [B, in_channels/2, in_h, in_w]. */
+int se_conv2d_bwd_data_joined(const se_conv2d_desc* d, const float* dy, const float* wr,
+                              const float* wi, float* gx, int x_h, int x_w, float* gs,
+                              void* ws, size_t ws_bytes, void* stream);
+int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float* x, int x_h, int x_w,
+                                const float* s, const float* dy, float* dwr, float* dwi,
+                                float* dbr, float* dbi, void* ws, size_t ws_bytes,
+                                void* stream);
+
 /* ------------------------------------------------------------------------
  * ComplexBatchNorm2d (complex_nn.py:148-329) with optional fused
  * LeakyReLU / ReLU (frcrn.py:22,34; ccbam.py:12,15).

@@ -1092,9 +1092,18 @@ static size_t wgrad_ws_bytes(const WgradPlan& w) {
 
 static inline char* align256(char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); }
 
+// Decoder skip join folded into a gather pass (se_conv2d_*_joined): X of the
+// pass is s, x2 is x on its own (h2, w2) grid (gather side); or Y of the pass
+// gets the s chunks and y2 the x chunks on (yh2, yw2) (output side).
+struct JoinIO {
+  const float* x2; int jh, h2, w2;
+  float* y2; int yjh, yh2, yw2;
+  const float* s;   // weight-grad: the skip (D of a transposed conv)
+};
+
 static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const float* wr,
                          const float* wi, const float* bias_br, const float* bias_bi, float* Y,
-                         void* ws, size_t ws_bytes, hipStream_t st) {
+                         void* ws, size_t ws_bytes, hipStream_t st, const JoinIO* jn = nullptr) {
   auto cls = plan_pass(g, pass);
   const int N = (pass == kFwd) ? g.Co : g.Ci;
   const int Cg = (pass == kFwd) ? g.Ci : g.Co;
@@ -1119,6 +1128,24 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const bool bf1 = g.math == SE_MATH_BF16 && N > 64;             // one term: hi*hi
   const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1;   // prep / tiles shared
   const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
+  const bool join_in = jn && jn->x2, join_out = jn && jn->y2;
+  const int cpb = join_in ? 2 * jn->jh : Cg;        // channels per batch item of X
+  // TU needs whole K-steps inside one tap and 32-bit buffer offsets over the
+  // batch items one M-tile can span (for both sources of a joined gather)
+  auto tu_of = [&](const ClassPlan& c) {
+    const long long qhw = (long long)c.h.Q * c.w.Q;
+    const int bm = ldw == 64 ? 256 : 128;
+    const long long span = (bm + qhw - 1) / qhw + 1;
+    bool ok = (Cg % kBK == 0) && span * cpb * (long long)Hi * Wi * 4 < (1ll << 31) &&
+              (long long)c.Kp * ldw * 4 < (1ll << 31);
+    if (join_in) ok = ok && span * cpb * (long long)jn->h2 * jn->w2 * 4 < (1ll << 31);
+    return ok;
+  };
+  if (jn) {   // the joined forms exist on the split-bf16 / bf16 tap-uniform kernels only
+    if (!(x3 || x6) || (join_out && x6)) return SE_E_UNSUPPORTED;
+    for (const auto& c : cls)
+      if (!tu_of(c)) return SE_E_UNSUPPORTED;
+  }
   for (const auto& c : cls) {
     float* Wp = (float*)p;
     p = align256(p + (size_t)c.Kp * ldw * kWpBytesPerElem);
@@ -1142,6 +1169,10 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
+    if (jn) {
+      a.X2 = jn->x2; a.jh = jn->jh; a.H2 = jn->h2; a.W2 = jn->w2;
+      a.Y2 = jn->y2; a.yjh = jn->yjh; a.YH2 = jn->yh2; a.YW2 = jn->yw2;
+    }
     const long long M = (long long)g.B * c.h.Q * c.w.Q;
     if (M > INT32_MAX) return SE_E_UNSUPPORTED;
     a.M = (int)M;
@@ -1153,24 +1184,23 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       else if (ldw <= 8) hipLaunchKernelGGL(gather_smalln_kernel<8>, grid, dim3(kThreads), sh, st, a);
       else hipLaunchKernelGGL(gather_smalln_kernel<16>, grid, dim3(kThreads), sh, st, a);
     } else {
-      // TU needs whole K-steps inside one tap and 32-bit buffer offsets over the
-      // batch items one M-tile can span
-      const long long qhw = (long long)c.h.Q * c.w.Q;
-      const int bm = ldw == 64 ? 256 : 128;
-      const long long span = (bm + qhw - 1) / qhw + 1;
-      const bool tu = (Cg % kBK == 0) && span * Cg * (long long)Hi * Wi * 4 < (1ll << 31) &&
-                      (long long)c.Kp * ldw * 4 < (1ll << 31);
+      const bool tu = tu_of(c);
       if (x6) {
         dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
-        if (tu) hipLaunchKernelGGL(gather_x6_kernel<true>, grid, dim3(kThreads), 0, st, a);
+        if (join_in) hipLaunchKernelGGL((gather_x6_kernel<true, true>), grid, dim3(kThreads), 0, st, a);
+        else if (tu) hipLaunchKernelGGL(gather_x6_kernel<true>, grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL(gather_x6_kernel<false>, grid, dim3(kThreads), 0, st, a);
       } else if (bf1) {
         dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
-        if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
+        if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 1>), grid, dim3(kThreads), 0, st, a);
+        else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 2>), grid, dim3(kThreads), 0, st, a);
+        else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL((gather_x3_kernel<false, 1>), grid, dim3(kThreads), 0, st, a);
       } else if (x3) {
         dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
-        if (tu) hipLaunchKernelGGL(gather_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
+        if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1>), grid, dim3(kThreads), 0, st, a);
+        else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2>), grid, dim3(kThreads), 0, st, a);
+        else if (tu) hipLaunchKernelGGL(gather_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
         else hipLaunchKernelGGL(gather_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
       } else if (ldw == 64) {
         dim3 grid(se::ceil_div(M, 256), 1);
@@ -1232,17 +1262,27 @@ extern "C" int se_conv2d_bwd_data(const se_conv2d_desc* d, const float* dy, cons
                        se::as_stream(stream));
 }
 
-extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, const float* dy,
-                                    float* dwr, float* dwi, float* dbr, float* dbi, void* ws,
-                                    size_t ws_bytes, void* stream) {
-  ConvGeom g;
-  int rc = geom_of(d, g);
-  if (rc) return rc;
-  if (!x || !dy || !dwr || !ws || (g.complex_w && !dwi) || (g.complex_w && dbr && !dbi))
-    return SE_E_ARG;
-  hipStream_t st = se::as_stream(stream);
+namespace {
+
+// Weight-grad pass. jn (transposed convs only): the conv's input x is the
+// decoder skip join, D = s with D2 = jn->x2 on (h2, w2) (se_conv2d_bwd_weight_joined).
+int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, float* dwi,
+               float* dbr, float* dbi, void* ws, size_t ws_bytes, hipStream_t st,
+               const JoinIO* jn = nullptr) {
   WgradPlan w = plan_wgrad(g);
   if (ws_bytes < wgrad_ws_bytes(w)) return SE_E_WORKSPACE;
+  const long long QQw = (long long)w.Qh * w.Qw;
+  const long long span_w = (w.m_per_split + QQw - 1) / QQw + 1;
+  // the split-bf16 / bf16 tile reads D rows in blocks of 16 (N % 16 == 0)
+  const bool split_ok = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16) && w.N % 16 == 0;
+  if (jn) {
+    const int dcpb = 2 * jn->jh;
+    const bool tu = g.transposed && (w.Cg % 128 == 0) &&
+                    span_w * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
+                    span_w * dcpb * QQw * 4 < (1ll << 31) &&
+                    span_w * dcpb * (long long)jn->h2 * jn->w2 * 4 < (1ll << 31);
+    if (!tu || !split_ok || w.N <= 32 || w.N != 4 * jn->jh) return SE_E_UNSUPPORTED;
+  }
   char* p = align256((char*)ws);
   const float* zero = (const float*)p;
   (void)hipMemsetAsync(p, 0, kZeroBytes, st);
@@ -1266,10 +1306,11 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
   a.Cg = w.Cg; a.Hi = w.Hi; a.Wi = w.Wi;
   a.N = w.N; a.Qh = w.Qh; a.Qw = w.Qw; a.sh = w.c.h.s; a.sw = w.c.w.s;
   a.Kp = w.c.Kp; a.Np = w.Np; a.M = w.M; a.m_per_split = w.m_per_split;
-  const long long QQ = (long long)w.Qh * w.Qw;
-  const long long span = (w.m_per_split + QQ - 1) / QQ + 1;
-  const bool tu = (w.Cg % 128 == 0) && span * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
-                  span * (long long)w.Np * QQ * 4 < (1ll << 31);
+  if (jn) {
+    a.D = jn->s; a.D2 = jn->x2; a.djh = jn->jh; a.DH2 = jn->h2; a.DW2 = jn->w2;
+  }
+  const bool tu = (w.Cg % 128 == 0) && span_w * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
+                  span_w * (long long)w.Np * QQw * 4 < (1ll << 31);
   if (w.N <= kSmallWgradN) {
     dim3 grid(w.c.Kp / 16, w.splits);
     if (w.Np == 4) hipLaunchKernelGGL(wgrad_smalln_kernel<4>, grid, dim3(kThreads), 0, st, a);
@@ -1278,13 +1319,15 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
     dim3 grid(w.c.Kp / 128, 1, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
-  } else if (g.math == SE_MATH_BF16X3) {
+  } else if (split_ok && g.math == SE_MATH_BF16X3) {
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
-    if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
+    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true>), grid, dim3(kThreads), 0, st, a);
+    else if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
-  } else if (g.math == SE_MATH_BF16) {
+  } else if (split_ok) {   // SE_MATH_BF16
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
-    if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
+    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true>), grid, dim3(kThreads), 0, st, a);
+    else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1>), grid, dim3(kThreads), 0, st, a);
   } else {
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
@@ -1320,4 +1363,79 @@ extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, con
     SE_LAUNCH_CHECK();
   }
   return SE_OK;
+}
+
+// Shape rules of the joined entry points: complex conv over the joined input
+// [B, Ci, Hi, Wi] = complex_concat([align(x), s]) with s [B, Ci/2, Hi, Wi] and
+// x [B, Ci/2, x_h, x_w], x_h <= Hi (missing rows: F.pad zeros), x_w >= Wi
+// (extra columns: x[..., :-1]); chunks of Ci/4 channels, a multiple of 32.
+int joined_geom(const ConvGeom& g, int x_h, int x_w) {
+  if (!g.complex_w) return SE_E_UNSUPPORTED;
+  if (x_h <= 0 || x_w <= 0 || x_h > g.Hi || x_w < g.Wi) return SE_E_SHAPE;
+  if (g.Ci % 4 || (g.Ci / 4) % 32) return SE_E_UNSUPPORTED;
+  return SE_OK;
+}
+
+}  // namespace
+
+extern "C" int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x, const float* dy,
+                                    float* dwr, float* dwi, float* dbr, float* dbi, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if (!x || !dy || !dwr || !ws || (g.complex_w && !dwi) || (g.complex_w && dbr && !dbi))
+    return SE_E_ARG;
+  return wgrad_pass(g, x, dy, dwr, dwi, dbr, dbi, ws, ws_bytes, se::as_stream(stream));
+}
+
+extern "C" int se_conv2d_fwd_joined(const se_conv2d_desc* d, const float* x, int x_h, int x_w,
+                                    const float* s, const float* wr, const float* wi,
+                                    const float* br, const float* bi, float* y, void* ws,
+                                    size_t ws_bytes, void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if ((rc = joined_geom(g, x_h, x_w))) return rc;
+  if (!x || !s || !wr || !wi || !y || !ws || (br && !bi)) return SE_E_ARG;
+  JoinIO jn{};
+  jn.x2 = x; jn.jh = g.Ci / 4; jn.h2 = x_h; jn.w2 = x_w;
+  return launch_gather(g, kFwd, s, wr, wi, br, bi, y, ws, ws_bytes, se::as_stream(stream), &jn);
+}
+
+extern "C" int se_conv2d_bwd_data_joined(const se_conv2d_desc* d, const float* dy, const float* wr,
+                                         const float* wi, float* gx, int x_h, int x_w, float* gs,
+                                         void* ws, size_t ws_bytes, void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if ((rc = joined_geom(g, x_h, x_w))) return rc;
+  if (!dy || !wr || !wi || !gx || !gs || !ws) return SE_E_ARG;
+  hipStream_t st = se::as_stream(stream);
+  JoinIO jn{};
+  jn.y2 = gx; jn.yjh = g.Ci / 4; jn.yh2 = x_h; jn.yw2 = x_w;
+  if ((rc = launch_gather(g, kData, dy, wr, wi, nullptr, nullptr, gs, ws, ws_bytes, st, &jn))) return rc;
+  // x's cropped columns (x[..., :-1]) get a zero gradient
+  if (x_w > g.Wi) {
+    const size_t rows = (size_t)g.B * (g.Ci / 2) * x_h;
+    if (hipMemset2DAsync(gx + g.Wi, (size_t)x_w * sizeof(float), 0, (size_t)(x_w - g.Wi) * sizeof(float),
+                         rows, st) != hipSuccess)
+      return SE_E_LAUNCH;
+  }
+  return SE_OK;
+}
+
+extern "C" int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float* x, int x_h, int x_w,
+                                           const float* s, const float* dy, float* dwr, float* dwi,
+                                           float* dbr, float* dbi, void* ws, size_t ws_bytes,
+                                           void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if ((rc = joined_geom(g, x_h, x_w))) return rc;
+  if (!x || !s || !dy || !dwr || !dwi || !ws || (dbr && !dbi)) return SE_E_ARG;
+  if (!g.transposed) return SE_E_UNSUPPORTED;   // a plain conv would gather the join as G
+  JoinIO jn{};
+  jn.s = s; jn.x2 = x; jn.jh = g.Ci / 4; jn.h2 = x_h; jn.w2 = x_w;
+  return wgrad_pass(g, s, dy, dwr, dwi, dbr, dbi, ws, ws_bytes, se::as_stream(stream), &jn);
 }

@@ -91,10 +91,14 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // TERMS = 1 is the plain bf16 GEMM (SE_MATH_BF16: operands rounded to bf16,
 // fp32 accumulate, the arithmetic of autocast's bf16 conv): only the hi planes
 // are staged and read.
-template <bool TU, int TERMS = 3>
+// JM: decoder skip join (GatherArgs::X2 / Y2): 0 none, 1 the gathered tensor
+// is the joined input (forward), 2 the output is split into the joined
+// input's two gradients (data-grad). Both need the TU path.
+template <bool TU, int TERMS = 3, int JM = 0>
 __global__ void __launch_bounds__(kThreads, 2)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
+  static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
   constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
   constexpr int BN = kX3BN, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
   constexpr int AJ = 16;                          // gathered k per thread per step
@@ -132,28 +136,46 @@ gather_x3_kernel(const GatherArgs a) {
     return (void*)(((unsigned long long)hi << 32) | lo);
   };
   const int b0 = m0 / (a.Qh * a.Qw);
+  const int cpb = JM == 1 ? 2 * a.jh : a.Cg;      // channels per batch item of X
+  const long long H2W2 = (long long)a.H2 * a.W2;
   __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(a.X + (long long)b0 * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+      uniform_ptr(a.X + (long long)b0 * cpb * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  __amdgpu_buffer_rsrc_t rx2 = rx;
+  if constexpr (JM == 1)
+    rx2 = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.X2 + (long long)b0 * cpb * H2W2), (short)0,
+                                            0x7FFFFFFF, 0x00020000);
   const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * kX3TileU4 + tid;
-  int xoff = 0;
+  int xoff = 0, xoff2 = 0;
   if constexpr (TU) {
     if (mval) {
       const int b = m / (a.Qh * a.Qw);
-      xoff = (int)(((long long)(b - b0) * a.Cg * HiWi + (long long)hb * a.Wi + wb) * 4);
+      xoff = (int)(((long long)(b - b0) * cpb * HiWi + (long long)hb * a.Wi + wb) * 4);
+      if constexpr (JM == 1) xoff2 = (int)(((long long)(b - b0) * cpb * H2W2 + (long long)hb * a.W2 + wb) * 4);
     }
   }
   auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
     if constexpr (TU) {
       const int4 e0 = a.ktab[k0];                 // the step's tap (uniform)
       const int tap = k0 / a.Cg;
-      const int c0 = k0 - tap * a.Cg + AJ * akr;
+      int c0 = k0 - tap * a.Cg;                   // the step's first channel (uniform)
       const int hi = hb + e0.y, wi = wb + e0.z;
-      const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      const int vo = ok ? xoff + (e0.y * a.Wi + e0.z) * 4 : (int)0x80000000;
-      const int cs = (int)(HiWi * 4);
+      bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      int vo = xoff + (e0.y * a.Wi + e0.z) * 4, cs = (int)(HiWi * 4);
+      __amdgpu_buffer_rsrc_t r = rx;
+      if constexpr (JM == 1) {                    // a K-step lies in one join chunk
+        const int q = c0 / a.jh;
+        const bool from_x = (q & 1) == 0;         // chunks [x_re, s_re, x_im, s_im]
+        c0 = (q >> 1) * a.jh + (c0 - q * a.jh);
+        ok &= !from_x | (hi < a.H2);              // F.pad rows of x read 0
+        vo = from_x ? xoff2 + (e0.y * a.W2 + e0.z) * 4 : vo;
+        cs = from_x ? (int)(H2W2 * 4) : cs;
+        r = from_x ? rx2 : rx;
+      }
+      vo = ok ? vo : (int)0x80000000;
+      c0 += AJ * akr;
 #pragma unroll
       for (int j = 0; j < AJ; ++j)
-        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (c0 + j) * cs, 0));
+        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, (c0 + j) * cs, 0));
     } else {
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {
@@ -276,6 +298,28 @@ gather_x3_kernel(const GatherArgs a) {
     const int b = mm / qhw, r = mm - b * qhw;
     const int qh = r / a.Qw, qw = r - qh * a.Qw;
     const int nl0 = wn * TN + 4 * lh;
+    if constexpr (JM == 2) {
+      // joined output: a 32-row block of n lies in one join chunk (yjh % 32 == 0);
+      // s chunks -> Y over Ho x Wo, x chunks -> Y2 over YH2 x YW2 (rows >= YH2,
+      // the F.pad rows, have no x gradient)
+      const int oh = a.ph + a.Sh * qh, ow = a.pw + a.Sw * qw;
+      const long long P2 = (long long)a.YH2 * a.YW2;
+      const int cpb = 2 * a.yjh;
+#pragma unroll
+      for (int i = 0; i < RN; ++i) {
+        const int nb = n0 + wn * TN + 32 * i;     // block's first channel (wave-uniform)
+        const int q = nb / a.yjh;
+        const int cb = (q >> 1) * a.yjh + (nb - q * a.yjh) + 4 * lh;
+        const bool to_x = (q & 1) == 0;
+        if (to_x && oh >= a.YH2) continue;
+        const long long pl = to_x ? P2 : HoWo;
+        float* yp = to_x ? a.Y2 + ((long long)b * cpb + cb) * P2 + (long long)oh * a.YW2 + ow
+                         : a.Y + ((long long)b * cpb + cb) * HoWo + (long long)oh * a.Wo + ow;
+#pragma unroll
+        for (int r2 = 0; r2 < 16; ++r2) yp[(long long)((r2 & 3) + 8 * (r2 >> 2)) * pl] = acc[i][j][r2];
+      }
+      continue;
+    }
     float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
                 (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
 #pragma unroll
@@ -308,7 +352,8 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
   return 256 * s + 16 * (ch ^ (((s & 3) << 2) | ((s >> 2) & 3)));
 }
 
-template <bool TU, int TERMS = 3>
+// DJ: D is the decoder skip join (WgradArgs::D2, a transposed conv's input).
+template <bool TU, int TERMS = 3, bool DJ = false>
 __global__ void __launch_bounds__(kThreads, 2)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
@@ -355,8 +400,14 @@ wgrad_x3_kernel(const WgradArgs a) {
   const int bfirst = (int)(mbeg / QQ);
   __amdgpu_buffer_rsrc_t rg_src = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr(a.X + (long long)bfirst * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  const int dcpb = DJ ? 2 * a.djh : a.N;         // channels per batch item of D
+  const long long QQ2 = (long long)a.DH2 * a.DW2;
   __amdgpu_buffer_rsrc_t rd_src = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(a.D + (long long)bfirst * a.N * QQ), (short)0, 0x7FFFFFFF, 0x00020000);
+      uniform_ptr(a.D + (long long)bfirst * dcpb * QQ), (short)0, 0x7FFFFFFF, 0x00020000);
+  __amdgpu_buffer_rsrc_t rd2_src = rd_src;
+  if constexpr (DJ)
+    rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.D2 + (long long)bfirst * dcpb * QQ2), (short)0,
+                                                0x7FFFFFFF, 0x00020000);
   const int4 tap_e = a.ktab[k0];
   const int cbase = k0 % a.Cg;
   const bool one_wrap = a.Qw >= BMR;
@@ -382,9 +433,31 @@ wgrad_x3_kernel(const WgradArgs a) {
   auto load_step = [&](Stage& S, int mstep) __attribute__((always_inline)) {
     const bool mv = mstep + ml < mend;
     const int rb = cb - bfirst;
-    const int vd = mv ? (int)(((long long)rb * a.N * QQ + (long long)(n0 + RJ * lr) * QQ +
-                               (long long)cqh * a.Qw + cqw) * 4) : (int)0x80000000;
-    const int ds = (int)(QQ * 4);
+    // D rows of this thread: n0 + rbase + j, j < RJ. The host runs this kernel
+    // only for N % 16 == 0, so a thread's rows are all inside N or all in the
+    // Np-padded tail; tail rows read 0 through an out-of-range voffset (they
+    // must not be read: past the last batch item they leave the allocation).
+    const bool dok = mv & (n0 + rbase < a.N);
+    int vd, ds = (int)(QQ * 4), srow = 32 * wave;
+    __amdgpu_buffer_rsrc_t rdr = rd_src;
+    if constexpr (DJ) {
+      // joined D: chunks [x_re, s_re, x_im, s_im] of djh rows; a wave's 32 rows
+      // lie in one chunk (djh % 32 == 0)
+      const int nb = n0 + 32 * wave;
+      const int q = nb / a.djh;
+      const bool from_x = (q & 1) == 0;
+      const int cr = (q >> 1) * a.djh + (nb - q * a.djh) + RJ * lr;   // row in its source
+      const bool okx = dok & (!from_x | (cqh < a.DH2));                // F.pad rows of x: 0
+      vd = from_x ? (int)(((long long)rb * dcpb * QQ2 + (long long)cr * QQ2 + (long long)cqh * a.DW2 + cqw) * 4)
+                  : (int)(((long long)rb * dcpb * QQ + (long long)cr * QQ + (long long)cqh * a.Qw + cqw) * 4);
+      vd = okx ? vd : (int)0x80000000;
+      ds = from_x ? (int)(QQ2 * 4) : ds;
+      rdr = from_x ? rd2_src : rd_src;
+      srow = 0;
+    } else {
+      vd = dok ? (int)(((long long)rb * a.N * QQ + (long long)(n0 + RJ * lr) * QQ +
+                        (long long)cqh * a.Qw + cqw) * 4) : (int)0x80000000;
+    }
     if constexpr (TU) {
       const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
       const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
@@ -407,12 +480,8 @@ wgrad_x3_kernel(const WgradArgs a) {
       }
     }
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-      const bool nok = n0 + rbase + j < a.N;   // only the Np-padded tail fails
-      const float v = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-          rd_src, vd, (32 * wave + j) * ds, 0));
-      S.rd[j] = nok ? v : 0.f;
-    }
+    for (int j = 0; j < RJ; ++j)
+      S.rd[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdr, vd, (srow + j) * ds, 0));
     advance();
   };
   auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
@@ -596,9 +665,11 @@ __global__ void prep_class_x6_kernel(WeightView w, TapList taps, int Cg, int N, 
   }
 }
 
-template <bool TU>
+// JG: the gathered tensor is the decoder skip join (as gather_x3_kernel JM = 1).
+template <bool TU, bool JG = false>
 __global__ void __launch_bounds__(kThreads, 2)
 gather_x6_kernel(const GatherArgs a) {
+  static_assert(!JG || TU, "the joined gather runs on the tap-uniform path");
   constexpr int BN = kX3BN, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
   constexpr int BK = kX6BK, AJ = 8;               // gathered k per thread per step
   __shared__ __attribute__((aligned(16))) u32x4 sA[2][3 * BM * 2];
@@ -635,28 +706,46 @@ gather_x6_kernel(const GatherArgs a) {
     return (void*)(((unsigned long long)hi << 32) | lo);
   };
   const int b0 = m0 / (a.Qh * a.Qw);
+  const int cpb = JG ? 2 * a.jh : a.Cg;           // channels per batch item of X
+  const long long H2W2 = (long long)a.H2 * a.W2;
   __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(a.X + (long long)b0 * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+      uniform_ptr(a.X + (long long)b0 * cpb * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+  __amdgpu_buffer_rsrc_t rx2 = rx;
+  if constexpr (JG)
+    rx2 = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.X2 + (long long)b0 * cpb * H2W2), (short)0,
+                                            0x7FFFFFFF, 0x00020000);
   const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * kX6TileU4 + tid;
-  int xoff = 0;
+  int xoff = 0, xoff2 = 0;
   if constexpr (TU) {
     if (mval) {
       const int b = m / (a.Qh * a.Qw);
-      xoff = (int)(((long long)(b - b0) * a.Cg * HiWi + (long long)hb * a.Wi + wb) * 4);
+      xoff = (int)(((long long)(b - b0) * cpb * HiWi + (long long)hb * a.Wi + wb) * 4);
+      if constexpr (JG) xoff2 = (int)(((long long)(b - b0) * cpb * H2W2 + (long long)hb * a.W2 + wb) * 4);
     }
   }
   auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
     if constexpr (TU) {
       const int4 e0 = a.ktab[k0];
       const int tap = k0 / a.Cg;
-      const int c0 = k0 - tap * a.Cg + AJ * akr;
+      int c0 = k0 - tap * a.Cg;
       const int hi = hb + e0.y, wi = wb + e0.z;
-      const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      const int vo = ok ? xoff + (e0.y * a.Wi + e0.z) * 4 : (int)0x80000000;
-      const int cs = (int)(HiWi * 4);
+      bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+      int vo = xoff + (e0.y * a.Wi + e0.z) * 4, cs = (int)(HiWi * 4);
+      __amdgpu_buffer_rsrc_t r = rx;
+      if constexpr (JG) {                         // a K-step lies in one join chunk
+        const int q = c0 / a.jh;
+        const bool from_x = (q & 1) == 0;         // chunks [x_re, s_re, x_im, s_im]
+        c0 = (q >> 1) * a.jh + (c0 - q * a.jh);
+        ok &= !from_x | (hi < a.H2);              // F.pad rows of x read 0
+        vo = from_x ? xoff2 + (e0.y * a.W2 + e0.z) * 4 : vo;
+        cs = from_x ? (int)(H2W2 * 4) : cs;
+        r = from_x ? rx2 : rx;
+      }
+      vo = ok ? vo : (int)0x80000000;
+      c0 += AJ * akr;
 #pragma unroll
       for (int j = 0; j < AJ; ++j)
-        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rx, vo, (c0 + j) * cs, 0));
+        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, (c0 + j) * cs, 0));
     } else {
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {

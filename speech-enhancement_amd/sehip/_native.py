@@ -52,6 +52,9 @@ _SIGNATURES = {
     "se_conv2d_fwd": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_weight": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
+    "se_conv2d_fwd_joined": (c_int, [_P, _P, c_int, c_int] + [_P] * 6 + [_P, c_size_t, _P]),
+    "se_conv2d_bwd_data_joined": (c_int, [_P] * 5 + [c_int, c_int, _P, _P, c_size_t, _P]),
+    "se_conv2d_bwd_weight_joined": (c_int, [_P, _P, c_int, c_int] + [_P] * 6 + [_P, c_size_t, _P]),
     "se_cbn_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P,
                            c_int, c_float, c_float, c_int, c_float, _P,

@@ -101,6 +101,16 @@ class _FusedComplexConv(nn.Module):
                      transposed=self.transposed)
         return rebuild(y)
 
+    def forward_joined(self, x, skip):
+        """self(complex_concat([align(x), skip])) with the FRCRN decoder's
+        trim / pad / concat (frcrn.py:93-100) folded into the GEMMs."""
+        c = self._geometry()
+        return F.conv2d_joined(x, skip, c.weight, self.imag_conv.weight, c.bias, self.imag_conv.bias,
+                               out_channels=2 * c.out_channels, kernel=c.kernel_size, stride=c.stride,
+                               padding=c.padding, dilation=c.dilation,
+                               output_padding=getattr(c, "output_padding", (0, 0)),
+                               transposed=self.transposed)
+
 
 class ComplexConv2d(_FusedComplexConv):
     """complex_nn.py:67-78."""

@@ -228,6 +228,116 @@ class _Conv2d(torch.autograd.Function):
         return dx, dwr, dwi, dbr, dbi, None
 
 
+SE_E_UNSUPPORTED = -3
+
+
+def _join_raw(x, s):
+    """complex_concat([align(x), s]) materialised (no autograd): the fallback
+    of the joined conv passes when no joined kernel covers the mode/shape."""
+    B, Cx, Fx, Tx = x.shape
+    _, Cs, F_, T = s.shape
+    out = torch.empty((B, Cx + Cs, F_, T), device=x.device, dtype=x.dtype)
+    N.check(N.lib().se_complex_join(x.data_ptr(), Cx, Fx, Tx, s.data_ptr(), Cs, F_, T, out.data_ptr(), B,
+                                    N.stream_of(x)), "se_complex_join")
+    return out
+
+
+class _ConvJoined(torch.autograd.Function):
+    """Complex (transposed) conv over complex_concat([align(x), s]) — the FRCRN
+    decoder's trim / pad / concat + ConvTransposeBlock conv (frcrn.py:93-101) —
+    without writing the joined tensor: the forward GEMM gathers from x and s,
+    the data-grad epilogue writes dx and ds directly, the weight-grad reads
+    both as its D operand (se_conv2d_*_joined). Modes or shapes without a
+    joined kernel (SE_E_UNSUPPORTED) materialise the join for that pass."""
+
+    @staticmethod
+    def forward(ctx, x, s, wr, wi, br, bi, geom):
+        out_channels, kernel, stride, padding, dilation, output_padding, transposed = geom
+        N.require_device(x, s, wr, wi, br, bi)
+        x, s = x.contiguous(), s.contiguous()
+        B, Cs, F_, T = s.shape
+        Fx, Tx = x.shape[2], x.shape[3]
+        d = conv_desc((B, 2 * Cs, F_, T), out_channels, kernel, stride, padding, dilation,
+                      output_padding, transposed, True)
+        lib = N.lib()
+        ho, wo = N.c_int(), N.c_int()
+        N.check(lib.se_conv2d_out_shape(N.ctypes.byref(d), N.ctypes.byref(ho), N.ctypes.byref(wo)),
+                "se_conv2d_out_shape")
+        y = torch.empty((B, out_channels, ho.value, wo.value), device=x.device, dtype=x.dtype)
+        nbytes = lib.se_conv2d_workspace_size(N.ctypes.byref(d))
+        ws = _workspace(nbytes, x.device)
+        st = N.stream_of(x)
+        t0 = _TIMER.begin() if _TIMER else None
+        rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
+                                      wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(),
+                                      ws.numel(), st)
+        if rc == SE_E_UNSUPPORTED:
+            rc = lib.se_conv2d_fwd(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), wr.data_ptr(), wi.data_ptr(),
+                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
+        N.check(rc, "se_conv2d_fwd_joined")
+        if t0 is not None:
+            _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
+                       4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
+        ctx.save_for_backward(x, s, wr, wi)
+        ctx.desc, ctx.nbytes, ctx.has_bias = d, nbytes, br is not None
+        return y
+
+    @staticmethod
+    def backward(ctx, gy):
+        x, s, wr, wi = ctx.saved_tensors
+        gy = gy.contiguous()
+        d, lib = ctx.desc, N.lib()
+        Fx, Tx = x.shape[2], x.shape[3]
+        ws = _workspace(ctx.nbytes, gy.device)
+        st = N.stream_of(gy)
+        gx = gs = dwr = dwi = dbr = dbi = None
+        if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
+            gx, gs = torch.empty_like(x), torch.empty_like(s)
+            t0 = _TIMER.begin() if _TIMER else None
+            rc = lib.se_conv2d_bwd_data_joined(_with_math(d, "data"), gy.data_ptr(), wr.data_ptr(), wi.data_ptr(),
+                                               gx.data_ptr(), Fx, Tx, gs.data_ptr(), ws.data_ptr(), ws.numel(), st)
+            if rc == SE_E_UNSUPPORTED:
+                dj = torch.empty((d.batch, d.in_channels, d.in_h, d.in_w), device=gy.device, dtype=gy.dtype)
+                N.check(lib.se_conv2d_bwd_data(N.ctypes.byref(d), gy.data_ptr(), wr.data_ptr(), wi.data_ptr(),
+                                               dj.data_ptr(), ws.data_ptr(), ws.numel(), st), "se_conv2d_bwd_data")
+                rc = lib.se_complex_join_bwd(dj.data_ptr(), gx.data_ptr(), x.shape[1], Fx, Tx, gs.data_ptr(),
+                                             s.shape[1], d.in_h, d.in_w, d.batch, st)
+            N.check(rc, "se_conv2d_bwd_data_joined")
+            if t0 is not None:
+                _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
+                           4.0 * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))
+        if any(ctx.needs_input_grad[2:6]):
+            dwr, dwi = torch.empty_like(wr), torch.empty_like(wi)
+            if ctx.has_bias:
+                nb = d.out_channels // 2
+                dbr = torch.empty(nb, device=gy.device, dtype=gy.dtype)
+                dbi = torch.empty(nb, device=gy.device, dtype=gy.dtype)
+            t0 = _TIMER.begin() if _TIMER else None
+            rc = lib.se_conv2d_bwd_weight_joined(_with_math(d, "weight"), x.data_ptr(), Fx, Tx, s.data_ptr(),
+                                                 gy.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr),
+                                                 N.ptr(dbi), ws.data_ptr(), ws.numel(), st)
+            if rc == SE_E_UNSUPPORTED:
+                rc = lib.se_conv2d_bwd_weight(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), gy.data_ptr(),
+                                              dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr), N.ptr(dbi),
+                                              ws.data_ptr(), ws.numel(), st)
+            N.check(rc, "se_conv2d_bwd_weight_joined")
+            if t0 is not None:
+                _TIMER.end(_gemm_tag("weight", d), t0, _conv_flops(d),
+                           4.0 * (x.numel() + s.numel() + gy.numel() + 2 * wr.numel()))
+        return gx, gs, dwr, dwi, dbr, dbi, None
+
+
+def conv2d_joined(x, s, wr, wi, br=None, bi=None, *, out_channels, kernel, stride=1, padding=0,
+                  dilation=1, output_padding=0, transposed=False):
+    """conv2d(complex_join(x, s), ...) with the join folded into the GEMMs.
+    x: [B, C, Fx, Tx] decoder state, s: [B, C, F, T] skip, Fx <= F, Tx >= T."""
+    if x.shape[1] != s.shape[1] or x.shape[2] > s.shape[2] or x.shape[3] < s.shape[3]:
+        raise ValueError(f"sehip conv2d_joined: cannot align {tuple(x.shape)} to {tuple(s.shape)}")
+    geom = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
+            _pair(output_padding), bool(transposed))
+    return _ConvJoined.apply(x, s, wr, wi, br, bi, geom)
+
+
 def conv2d(x, wr, wi=None, br=None, bi=None, *, out_channels, kernel, stride=1, padding=0,
            dilation=1, output_padding=0, transposed=False, padding_end=None):
     """Fused complex conv (wi given) or real conv (wi None) on the HIP path.

@@ -42,6 +42,15 @@ class _CausalConvBase(nn.Module):
         y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
         return norm_act(self.norm, self.act, y)
 
+    def forward_joined(self, x, skip):
+        """self(complex_join(x, skip)) (frcrn.py:95-101) without writing the
+        joined tensor: the conv GEMMs gather from x and skip directly."""
+        conv = self._conv()
+        if self.padding[1] or not isinstance(conv, (ComplexConv2d, ComplexConvTranspose2d)) \
+                or x.shape[1] != skip.shape[1]:
+            return self(F.complex_join(x, skip))
+        return norm_act(self.norm, self.act, conv.forward_joined(x, skip))
+
 
 def _make_block(block, transposed, in_channels, out_channels, kernel_size, padding, norm, act,
                 causal, is_complex, kwargs):
@@ -118,10 +127,11 @@ class Decoder(nn.Module):
         for attention, layer in zip(self.skip_connection_attention_layers, self.layers):
             skip = attention(encoder_outputs.pop())
             # frcrn.py:95-99: x[..., :-1] if wider, F.pad(x, (0, 0, 0, 1)) if shorter, then
-            # complex_concat([x, skip]) — one fused pass each way (se_complex_join)
+            # complex_concat([x, skip]): folded into the convT's GEMMs (se_conv2d_*_joined);
+            # modes without a joined kernel materialise it in one pass (se_complex_join)
             if x.shape[-1] - skip.shape[-1] not in (0, 1) or skip.shape[-2] - x.shape[-2] not in (0, 1):
                 raise ValueError(f"decoder/skip grids do not align: {tuple(x.shape)} vs {tuple(skip.shape)}")
-            x = layer(F.complex_join(x, skip))
+            x = layer.forward_joined(x, skip)
         return x
 
 

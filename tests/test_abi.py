@@ -143,6 +143,26 @@ def test_asymmetric_padding_out_shape(tr, xs, pb, pe):
     assert (ho.value, wo.value) == tuple(ref)
 
 
+def test_joined_conv_validation_needs_no_gpu():
+    """se_conv2d_*_joined shape rules (frcrn.py:95-100 alignments) are checked
+    on the host before any launch."""
+    lib = N.lib()
+    d = F.conv_desc((2, 256, 9, 37), 128, (5, 2), (2, 1), (0, 0), (1, 1), (0, 0), True, True)
+    b = ctypes.byref(d)
+    # x taller than the joined grid (only F.pad rows may be missing) -> SE_E_SHAPE
+    assert lib.se_conv2d_fwd_joined(b, None, 10, 38, None, None, None, None, None, None, None, 0, None) == -2
+    # x narrower than the joined grid (only x[..., :-1] crops) -> SE_E_SHAPE
+    assert lib.se_conv2d_bwd_data_joined(b, None, None, None, None, 9, 36, None, None, 0, None) == -2
+    # valid shapes, null pointers -> SE_E_ARG
+    assert lib.se_conv2d_fwd_joined(b, None, 8, 38, None, None, None, None, None, None, None, 0, None) == -1
+    assert lib.se_conv2d_bwd_weight_joined(b, None, 9, 37, None, None, None, None, None, None, None, 0,
+                                           None) == -1
+    # join chunks of 24 channels (not a multiple of 32): no joined kernel
+    d2 = F.conv_desc((2, 96, 9, 37), 128, (5, 2), (2, 1), (0, 0), (1, 1), (0, 0), True, True)
+    assert lib.se_conv2d_fwd_joined(ctypes.byref(d2), None, 9, 38, None, None, None, None, None, None, None, 0,
+                                    None) == -3
+
+
 def test_ccbam_and_join_validation_need_no_gpu():
     lib = N.lib()
     assert lib.se_ccbam_workspace_size(64, 128, 158 * 403) > 0

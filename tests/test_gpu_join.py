@@ -16,6 +16,73 @@ def _ref(x, s):
     return complex_concat([x, s], dim=1)
 
 
+JOINED = [   # (x shape, skip shape): decoder state vs skip, FRCRN alignments
+    ((2, 64, 9, 38), (2, 64, 9, 37)),            # time crop
+    ((2, 64, 8, 38), (2, 64, 9, 37)),            # time crop + frequency pad
+    ((3, 64, 7, 21), (3, 64, 7, 21)),            # aligned
+    ((2, 128, 17, 41), (2, 128, 17, 40)),        # FRCRN width (jh = 64)
+]
+
+
+@pytest.mark.parametrize("math", ["bf16x3", "fwd=bf16x6,data=bf16x3,weight=bf16x3", "bf16", "f32"])
+@pytest.mark.parametrize("xs,ss", JOINED)
+def test_joined_conv_matches_materialised_join(gpu_device, xs, ss, math):
+    """The decoder convT over complex_join(x, skip) with the join folded into
+    the GEMMs (se_conv2d_*_joined) gives bit-identical outputs and gradients to
+    the materialised join + plain conv (same K order, same MFMA sequence); f32
+    has no joined kernel and takes the materialising fallback."""
+    from sehip import functional as F
+    prev = F.get_conv_math()
+    F.set_conv_math(math)
+    try:
+        torch.manual_seed(1)
+        cin, cout = 2 * xs[1], 128
+        x, s = torch.randn(xs, device=gpu_device), torch.randn(ss, device=gpu_device)
+        wr = (torch.randn(cin // 2, cout // 2, 5, 2, device=gpu_device) * 0.05)
+        wi = (torch.randn(cin // 2, cout // 2, 5, 2, device=gpu_device) * 0.05)
+        kw = dict(out_channels=cout, kernel=(5, 2), stride=(2, 1), transposed=True)
+        outs = []
+        for joined in (False, True):
+            xa, sa = x.clone().requires_grad_(True), s.clone().requires_grad_(True)
+            wra, wia = wr.clone().requires_grad_(True), wi.clone().requires_grad_(True)
+            if joined:
+                y = F.conv2d_joined(xa, sa, wra, wia, **kw)
+            else:
+                y = F.conv2d(F.complex_join(xa, sa), wra, wia, **kw)
+            g = torch.randn(y.shape, device=gpu_device, generator=torch.Generator(gpu_device).manual_seed(5))
+            y.backward(g)
+            outs.append((y.detach(), xa.grad, sa.grad, wra.grad, wia.grad))
+        torch.cuda.synchronize()
+        for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), *outs):
+            assert torch.equal(a, b), (math, name, (a - b).abs().max().item())
+    finally:
+        F.set_conv_math(prev)
+
+
+def test_joined_entry_points_run_their_own_kernels(gpu_device):
+    """bf16x3 / bf16x6 / bf16 have joined kernels (rc 0, no fallback); f32 reports
+    SE_E_UNSUPPORTED so the host materialises the join."""
+    import ctypes
+    from sehip import functional as F, _native as N
+    B, C, F_, T = 2, 64, 9, 37
+    d = F.conv_desc((B, 2 * C, F_, T), 128, (5, 2), (2, 1), (0, 0), (1, 1), (0, 0), True, True)
+    lib = N.lib()
+    ho, wo = ctypes.c_int(), ctypes.c_int()
+    lib.se_conv2d_out_shape(ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo))
+    x = torch.randn(B, C, F_ - 1, T + 1, device=gpu_device)
+    s = torch.randn(B, C, F_, T, device=gpu_device)
+    w = torch.randn(C, 64, 5, 2, device=gpu_device)
+    y = torch.empty(B, 128, ho.value, wo.value, device=gpu_device)
+    ws = torch.empty(lib.se_conv2d_workspace_size(ctypes.byref(d)), dtype=torch.uint8, device=gpu_device)
+    st = N.stream_of(y)
+    for mode, want in (("bf16x3", 0), ("bf16x6", 0), ("bf16", 0), ("f32", -3)):
+        d.math = F._MATH_CODES[mode]
+        rc = lib.se_conv2d_fwd_joined(ctypes.byref(d), x.data_ptr(), F_ - 1, T + 1, s.data_ptr(), w.data_ptr(),
+                                      w.data_ptr(), None, None, y.data_ptr(), ws.data_ptr(), ws.numel(), st)
+        assert rc == want, (mode, rc)
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("xs,ss", [
     ((2, 8, 7, 14), (2, 6, 7, 13)),      # time crop only (every decoder layer)
     ((2, 8, 6, 14), (2, 8, 7, 13)),      # crop + freq pad (157 -> 158 in FRCRN)
