@@ -56,17 +56,35 @@ __device__ __forceinline__ void wait_vmcnt() {
 // Pull the rows this step will scalar-load into the scalar cache with one
 // s_load_dword per 64-B line, all in flight together, one wait: ONE L2 round
 // trip per step instead of one per kChunk chunk (the chunk loads then hit K$).
-template <int NLINES>
-__device__ __forceinline__ void warm_kcache(const float* row) {
+// The loads, their (discarded) destination and the lgkmcnt(0) wait are ONE asm
+// statement with an early-clobber output: as separate statements the compiler
+// saw the destination SGPR as dead right after each load and reused it for
+// address arithmetic while the load was still in flight; the late return then
+// overwrote a live scalar address (a wild s_load: memory-aperture violation
+// that came and went with the tensors' placement).
+__device__ __forceinline__ unsigned long long uniform_addr(const float* row) {
   const unsigned long long v = reinterpret_cast<unsigned long long>(row);
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
   const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  const unsigned long long u = ((unsigned long long)hi << 32) | lo;
-  unsigned dummy;
-#pragma unroll
-  for (int i = 0; i < NLINES; ++i) asm volatile("s_load_dword %0, %1, %2" : "=s"(dummy) : "s"(u), "n"(i * 64));
+  return ((unsigned long long)hi << 32) | lo;
 }
-__device__ __forceinline__ void wait_lgkm0() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+#define SE_WARM4(P) "s_load_dword %0, " P ", 0x0\n s_load_dword %0, " P ", 0x40\n " \
+                    "s_load_dword %0, " P ", 0x80\n s_load_dword %0, " P ", 0xc0\n "
+#define SE_WARM8(P) SE_WARM4(P) "s_load_dword %0, " P ", 0x100\n s_load_dword %0, " P ", 0x140\n " \
+                    "s_load_dword %0, " P ", 0x180\n s_load_dword %0, " P ", 0x1c0\n "
+// two rows (BS = 2) of NLINES 64-B lines each, then s_waitcnt lgkmcnt(0)
+template <int NLINES>
+__device__ __forceinline__ void warm_kcache2(const float* r0, const float* r1) {
+  static_assert(NLINES == 4 || NLINES == 8, "H = 64 or 128");
+  const unsigned long long u0 = uniform_addr(r0), u1 = uniform_addr(r1);
+  unsigned dummy;
+  if constexpr (NLINES == 8)
+    asm volatile(SE_WARM8("%1") SE_WARM8("%2") "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(dummy) : "s"(u0), "s"(u1) : "memory");
+  else
+    asm volatile(SE_WARM4("%1") SE_WARM4("%2") "s_waitcnt lgkmcnt(0)"
+                 : "=&s"(dummy) : "s"(u0), "s"(u1) : "memory");
+}
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
 
@@ -158,9 +176,8 @@ __global__ __launch_bounds__(4 * H) void lstm_fwd_kernel(LstmArgs a) {
       f32x2 acc[BS][2];
 #pragma unroll
       for (int b = 0; b < BS; ++b) acc[b][0] = acc[b][1] = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int b = 0; b < BS; ++b) warm_kcache<H * 4 / 64>(hb[b]);
-      wait_lgkm0();
+      static_assert(BS == 2, "warm_kcache2 pulls two rows");
+      warm_kcache2<H * 4 / 64>(hb[0], hb[1]);
 #pragma unroll
       for (int b = 0; b < BS; ++b)
 #pragma unroll
@@ -285,9 +302,8 @@ __global__ __launch_bounds__(4 * H) void lstm_bwd_kernel(LstmArgs a) {
     __syncthreads();
     {
       const float* grow = a.dgates + ((size_t)l * a.B * T + t) * G + rq * H;
-#pragma unroll
-      for (int b = 0; b < BS; ++b) warm_kcache<H * 4 / 64>(grow + (size_t)min(b0 + b, a.B - 1) * T * G);
-      wait_lgkm0();
+      static_assert(BS == 2, "warm_kcache2 pulls two rows");
+      warm_kcache2<H * 4 / 64>(grow + (size_t)min(b0, a.B - 1) * T * G, grow + (size_t)min(b0 + 1, a.B - 1) * T * G);
       f32x2 acc[BS][2];
 #pragma unroll
       for (int b = 0; b < BS; ++b) acc[b][0] = acc[b][1] = f32x2{0.f, 0.f};
