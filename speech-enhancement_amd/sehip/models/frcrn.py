@@ -8,6 +8,8 @@ pooling, pads/concats and the tanh mask are PyTorch device ops.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as TF
@@ -17,6 +19,23 @@ from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspos
                           complex_concat, norm_act, real_conv2d)
 from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
+
+
+_SIDE_STREAMS: dict = {}
+
+
+def _side_stream(dev):
+    s = _SIDE_STREAMS.get(dev)
+    if s is None:
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
+    return s
+
+
+def _overlap_ok(tensors) -> bool:
+    if not tensors or not tensors[0].is_cuda or os.environ.get("SEHIP_OVERLAP", "1") == "0":
+        return False
+    dist = torch.distributed
+    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
 
 
 class _CausalConvBase(nn.Module):
@@ -123,9 +142,35 @@ class Decoder(nn.Module):
                                                   padding=(0, 0), causal=True, is_complex=is_complex))
             c = out_channels
 
-    def forward(self, x, encoder_outputs):
+    def attend_skips(self, encoder_outputs):
+        """Start the six CCBAM skip gates (they depend only on the encoder outputs) on a side
+        HIP stream, so they run beside the latency-bound LSTM recurrence, which occupies half
+        the CUs; autograd runs their backward on the same side stream, beside the LSTM's BPTT.
+        Returns (gated skips in decoder order, side stream), or None to run them inline: off
+        the GPU, with SEHIP_OVERLAP=0, or under DDP (its gradient-ready hooks would see the
+        CCBAM parameter gradients on the side stream)."""
+        if not _overlap_ok(encoder_outputs):
+            return None
+        dev = encoder_outputs[0].device
+        main, side = torch.cuda.current_stream(dev), _side_stream(dev)
+        side.wait_stream(main)
+        gated = []
+        with torch.cuda.stream(side):
+            for attention, skip in zip(self.skip_connection_attention_layers, reversed(encoder_outputs)):
+                skip.record_stream(side)
+                gated.append(attention(skip))
+        return gated, side
+
+    def forward(self, x, encoder_outputs, attended=None):
+        if attended is not None:   # gated on the side stream (attend_skips): join it here
+            gated, side = attended
+            main = torch.cuda.current_stream(x.device)
+            main.wait_stream(side)
+            for g in gated:
+                g.record_stream(main)
+            gated = list(reversed(gated))   # popped from the end like encoder_outputs
         for attention, layer in zip(self.skip_connection_attention_layers, self.layers):
-            skip = attention(encoder_outputs.pop())
+            skip = gated.pop() if attended is not None else attention(encoder_outputs.pop())
             # frcrn.py:95-99: x[..., :-1] if wider, F.pad(x, (0, 0, 0, 1)) if shorter, then
             # complex_concat([x, skip]): folded into the convT's GEMMs (se_conv2d_*_joined);
             # modes without a joined kernel materialise it in one pass (se_complex_join)
@@ -155,10 +200,11 @@ class FRCRN(nn.Module):
         spec = self.stft(x)                                            # [B, N+2, T]
         noisy = spec.view(spec.shape[0], 2, half, spec.shape[-1])[:, :, 1:]   # drop DC (:123-127)
         h, skips = self.encoder(noisy.contiguous())
+        attended = self.decoder.attend_skips(skips)                    # side stream, beside the LSTM
         b, c, f, t = h.shape                                           # :133-137
         h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2))
         h = h.transpose(1, 2).reshape(b, c, f, t)
-        h = self.decoder(h, skips)
+        h = self.decoder(h, skips, attended)
         mask = torch.tanh(TF.pad(real_conv2d(self.final_conv, h), (0, 0, 1, 0)))   # :140-144
         est = TF.pad(mask * noisy, (0, 0, 1, 0))                       # :145-146 (DC back as 0)
         est = est.reshape(b, 2 * half, est.shape[-1])                  # cat(re, im) on dim 1 (:149-152)
