@@ -169,6 +169,26 @@ def test_frcrn_train_step_golden(gpu_device):
     assert torch.isfinite(l2)
 
 
+def test_frcrn_ccbam_side_stream_is_bit_identical(gpu_device, monkeypatch):
+    """The CCBAM skip gates on the side stream (beside the LSTM, forward and
+    backward) give bit-identical outputs, gradients and BN statistics to the
+    inline order."""
+    from sehip import models as M
+    from sehip.losses import SI_SNR_loss, pad_or_truncate_wav
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=4)
+    res = []
+    for overlap in ("0", "1"):
+        monkeypatch.setenv("SEHIP_OVERLAP", overlap)
+        m = paramfill.fill_(M.FRCRN(), seed=6).cuda().train()
+        _, wav = m(torch.from_numpy(noisy).cuda())
+        c = torch.from_numpy(clean).cuda()
+        SI_SNR_loss(pad_or_truncate_wav(wav, c), c).backward()
+        torch.cuda.synchronize()
+        res.append([wav.detach()] + [p.grad for p in m.parameters()] + list(m.buffers()))
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_frcrn_4s_vs_oracle(gpu_device):
     """Full-length (4 s) forward parity vs the oracle at B=2."""
     from sehip import models as M
