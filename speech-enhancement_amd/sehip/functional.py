@@ -6,6 +6,7 @@ HIP stream. There is no CPU path: CPU tensors raise.
 """
 from __future__ import annotations
 
+import contextlib
 import os
 
 import torch
@@ -19,6 +20,53 @@ def _pair(v):
 
 def _workspace(nbytes: int, device) -> torch.Tensor:
     return torch.empty(max(int(nbytes), 256), dtype=torch.uint8, device=device)
+
+
+# Deferred weight-grads: inside deferred_weight_grads(), every conv weight-grad
+# GEMM runs on a side HIP stream, so the (LDS/MFMA-bound) weight-grad of layer i
+# overlaps the data-grad chain and the HBM-bound CBN / CCBAM backward kernels of
+# the following layers on the main stream. Leaving the context makes the
+# current stream wait for the side stream (before clip_grad_norm / the
+# optimizer read the gradients).
+_DEFER: set | None = None
+_DEFER_STREAMS: dict = {}
+
+
+@contextlib.contextmanager
+def deferred_weight_grads(enabled: bool = True):
+    """Use around loss.backward() when every parameter .grad is None on entry
+    (zero_grad(set_to_none=True)) and no hook reads gradients during backward
+    (not under DDP): autograd sees the weight gradients as produced on the
+    current stream, and nothing may read them before the context exits."""
+    global _DEFER
+    if not enabled or _DEFER is not None:
+        yield
+        return
+    _DEFER = set()
+    try:
+        yield
+    finally:
+        pending, _DEFER = _DEFER, None
+        for side in pending:
+            torch.cuda.current_stream(side.device).wait_stream(side)
+
+
+def _wgrad_stream(*inputs):
+    """Context for a weight-grad launch: a no-op, or (deferred_weight_grads) the
+    device's side stream, after it waited for the current stream; the inputs are
+    recorded as used on it so the allocator keeps them until it is done."""
+    if _DEFER is None:
+        return contextlib.nullcontext()
+    dev = inputs[0].device
+    side = _DEFER_STREAMS.get(dev)
+    if side is None:
+        side = _DEFER_STREAMS[dev] = torch.cuda.Stream(dev)
+    side.wait_stream(torch.cuda.current_stream(dev))
+    for t in inputs:
+        if t is not None:
+            t.record_stream(side)
+    _DEFER.add(side)
+    return torch.cuda.stream(side)
 
 
 class OpTimer:
@@ -211,20 +259,23 @@ class _Conv2d(torch.autograd.Function):
                 _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
                            4.0 * (gy.numel() + dx.numel() + wr.numel() * (2 if wi is not None else 1)))
         if any(ctx.needs_input_grad[1:5]):
-            dwr = torch.empty_like(wr)
-            dwi = torch.empty_like(wi) if wi is not None else None
-            if ctx.has_bias:
-                nb = d.out_channels // 2 if d.complex_weights else d.out_channels
-                dbr = torch.empty(nb, device=gy.device, dtype=gy.dtype)
-                dbi = torch.empty(nb, device=gy.device, dtype=gy.dtype) if d.complex_weights else None
-            t0 = _TIMER.begin() if _TIMER else None
-            N.check(lib.se_conv2d_bwd_weight(_with_math(d, "weight"), x.data_ptr(), gy.data_ptr(),
-                                             dwr.data_ptr(), N.ptr(dwi), N.ptr(dbr), N.ptr(dbi),
-                                             ws.data_ptr(), ws.numel(), N.stream_of(gy)),
-                    "se_conv2d_bwd_weight")
-            if t0 is not None:
-                _TIMER.end(_gemm_tag("weight", d), t0, _conv_flops(d),
-                           4.0 * (x.numel() + gy.numel() + wr.numel() * (2 if wi is not None else 1)))
+            with _wgrad_stream(x, gy):
+                if _DEFER is not None:
+                    ws = _workspace(ctx.nbytes, gy.device)
+                dwr = torch.empty_like(wr)
+                dwi = torch.empty_like(wi) if wi is not None else None
+                if ctx.has_bias:
+                    nb = d.out_channels // 2 if d.complex_weights else d.out_channels
+                    dbr = torch.empty(nb, device=gy.device, dtype=gy.dtype)
+                    dbi = torch.empty(nb, device=gy.device, dtype=gy.dtype) if d.complex_weights else None
+                t0 = _TIMER.begin() if _TIMER else None
+                N.check(lib.se_conv2d_bwd_weight(_with_math(d, "weight"), x.data_ptr(), gy.data_ptr(),
+                                                 dwr.data_ptr(), N.ptr(dwi), N.ptr(dbr), N.ptr(dbi),
+                                                 ws.data_ptr(), ws.numel(), N.stream_of(gy)),
+                        "se_conv2d_bwd_weight")
+                if t0 is not None:
+                    _TIMER.end(_gemm_tag("weight", d), t0, _conv_flops(d),
+                               4.0 * (x.numel() + gy.numel() + wr.numel() * (2 if wi is not None else 1)))
         return dx, dwr, dwi, dbr, dbi, None
 
 
@@ -307,23 +358,27 @@ class _ConvJoined(torch.autograd.Function):
                 _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
                            4.0 * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))
         if any(ctx.needs_input_grad[2:6]):
-            dwr, dwi = torch.empty_like(wr), torch.empty_like(wi)
-            if ctx.has_bias:
-                nb = d.out_channels // 2
-                dbr = torch.empty(nb, device=gy.device, dtype=gy.dtype)
-                dbi = torch.empty(nb, device=gy.device, dtype=gy.dtype)
-            t0 = _TIMER.begin() if _TIMER else None
-            rc = lib.se_conv2d_bwd_weight_joined(_with_math(d, "weight"), x.data_ptr(), Fx, Tx, s.data_ptr(),
-                                                 gy.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr),
-                                                 N.ptr(dbi), ws.data_ptr(), ws.numel(), st)
-            if rc == SE_E_UNSUPPORTED:
-                rc = lib.se_conv2d_bwd_weight(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), gy.data_ptr(),
-                                              dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr), N.ptr(dbi),
-                                              ws.data_ptr(), ws.numel(), st)
-            N.check(rc, "se_conv2d_bwd_weight_joined")
-            if t0 is not None:
-                _TIMER.end(_gemm_tag("weight", d), t0, _conv_flops(d),
-                           4.0 * (x.numel() + s.numel() + gy.numel() + 2 * wr.numel()))
+            with _wgrad_stream(x, s, gy):
+                if _DEFER is not None:
+                    ws = _workspace(ctx.nbytes, gy.device)
+                st = N.stream_of(gy)
+                dwr, dwi = torch.empty_like(wr), torch.empty_like(wi)
+                if ctx.has_bias:
+                    nb = d.out_channels // 2
+                    dbr = torch.empty(nb, device=gy.device, dtype=gy.dtype)
+                    dbi = torch.empty(nb, device=gy.device, dtype=gy.dtype)
+                t0 = _TIMER.begin() if _TIMER else None
+                rc = lib.se_conv2d_bwd_weight_joined(_with_math(d, "weight"), x.data_ptr(), Fx, Tx, s.data_ptr(),
+                                                     gy.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr),
+                                                     N.ptr(dbi), ws.data_ptr(), ws.numel(), st)
+                if rc == SE_E_UNSUPPORTED:
+                    rc = lib.se_conv2d_bwd_weight(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), gy.data_ptr(),
+                                                  dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr), N.ptr(dbi),
+                                                  ws.data_ptr(), ws.numel(), st)
+                N.check(rc, "se_conv2d_bwd_weight_joined")
+                if t0 is not None:
+                    _TIMER.end(_gemm_tag("weight", d), t0, _conv_flops(d),
+                               4.0 * (x.numel() + s.numel() + gy.numel() + 2 * wr.numel()))
         return gx, gs, dwr, dwi, dbr, dbi, None
 
 

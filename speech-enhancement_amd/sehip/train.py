@@ -28,13 +28,27 @@ def make_optimizer(model, **overrides):
     return torch.optim.AdamW(model.parameters(), **kw)
 
 
+def _defer_ok(model) -> bool:
+    """Deferred weight-grads (functional.deferred_weight_grads) need every .grad
+    None on entry and no gradient hooks during backward: not under DDP, and
+    only on the GPU."""
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return False
+    p = next(model.parameters(), None)
+    return p is not None and p.is_cuda and all(q.grad is None for q in model.parameters()) \
+        and os.environ.get("SEHIP_OVERLAP", "1") != "0"
+
+
 def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
     """One optimisation step; returns the (device) loss, no host sync."""
+    from .functional import deferred_weight_grads
     _, wav = model(noisy)
     target = reshape_wav_to_mono(clean)
     est = pad_or_truncate_wav(reshape_wav_to_mono(wav), target)
     loss = SI_SNR_loss(est, target)
-    loss.backward()
+    with deferred_weight_grads(_defer_ok(model)):
+        loss.backward()
     if clip_norm:
         torch.nn.utils.clip_grad_norm_(model.parameters(), clip_norm)
     optimizer.step()

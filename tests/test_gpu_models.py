@@ -189,6 +189,26 @@ def test_frcrn_ccbam_side_stream_is_bit_identical(gpu_device, monkeypatch):
         assert torch.equal(a, b)
 
 
+def test_train_step_deferred_weight_grads_bit_identical(gpu_device, monkeypatch):
+    """train_step with the conv weight-grads on the side stream
+    (functional.deferred_weight_grads) and the CCBAM side stream: two steps give
+    bit-identical parameters and losses to the all-inline order."""
+    from sehip import models as M
+    from sehip.train import make_optimizer, train_step
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=8)
+    x, c = torch.from_numpy(noisy).cuda(), torch.from_numpy(clean).cuda()
+    res = []
+    for overlap in ("0", "1"):
+        monkeypatch.setenv("SEHIP_OVERLAP", overlap)
+        m = paramfill.fill_(M.FRCRN(), seed=9).cuda().train()
+        opt = make_optimizer(m)
+        losses = [train_step(m, opt, x, c) for _ in range(2)]
+        torch.cuda.synchronize()
+        res.append(losses + [p.detach().clone() for p in m.parameters()])
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
+
+
 def test_frcrn_4s_vs_oracle(gpu_device):
     """Full-length (4 s) forward parity vs the oracle at B=2."""
     from sehip import models as M
