@@ -217,7 +217,11 @@ def main():
         out["other_conv_math"] = list(compare.values())
     if kern:
         # dominant GEMM kernel = the conv pass/kernel with the most time in the step
-        convs = {k: v for k, v in kern.items() if k.startswith("conv_") and v["flops"]}
+        # among those on the main stream: the deferred weight-grads run on a side
+        # stream beside the data-grad / CBN chain, so their event spans include
+        # time the CUs spent on the other stream (op_breakdown marks them)
+        convs = {k: v for k, v in kern.items() if k.startswith("conv_") and v["flops"]
+                 and not v["side_calls"]}
         tag = max(convs, key=lambda k: convs[k]["ms"])
         g = convs[tag]
         ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
@@ -249,7 +253,8 @@ def main():
         out["op_breakdown"] = {
             k: {"calls": v["calls"], "ms_per_step": round(v["ms"] / args.steps, 3),
                 **({"tflops": round(v["flops"] / (v["ms"] * 1e-3) / 1e12, 2)} if v["flops"] else {}),
-                **({"gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} if v["bytes"] else {})}
+                **({"gbs": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} if v["bytes"] else {}),
+                **({"side_stream_calls": v["side_calls"]} if v["side_calls"] else {})}
             for k, v in kern.items()}
         total_conv = sum(v["flops"] for k, v in kern.items() if k.startswith("conv"))
         out["conv_flops_per_utt"] = total_conv / (B * args.steps)

@@ -1101,6 +1101,22 @@ struct JoinIO {
   const float* s;   // weight-grad: the skip (D of a transposed conv)
 };
 
+// Split-GEMM workgroup width: 2 = 256-column tiles of 8 waves where the padded
+// column count is a multiple of 256, 1 = 128-column tiles of 4 waves
+// (SEHIP_GEMM_NW; read once).
+static bool env_flag_off(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] == '0';
+}
+
+static int gemm_nw() {
+  static const int nw = [] {
+    const char* e = std::getenv("SEHIP_GEMM_NW");
+    return (e && std::atoi(e) == 1) ? 1 : 2;
+  }();
+  return nw;
+}
+
 static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const float* wr,
                          const float* wi, const float* bias_br, const float* bias_bi, float* Y,
                          void* ws, size_t ws_bytes, hipStream_t st, const JoinIO* jn = nullptr) {
@@ -1146,6 +1162,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     for (const auto& c : cls)
       if (!tu_of(c)) return SE_E_UNSUPPORTED;
   }
+  // split kernels: channel-block-major K order where Cg allows (split_k)
+  const int kblk = (Cg % 32 == 0 && !env_flag_off("SEHIP_KORDER")) ? 32 : 0;
   for (const auto& c : cls) {
     float* Wp = (float*)p;
     p = align256(p + (size_t)c.Kp * ldw * kWpBytesPerElem);
@@ -1155,11 +1173,11 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     if (x6)
       hipLaunchKernelGGL(prep_class_x6_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, (unsigned short*)Wp, ktab);
+                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab);
     else if (x3)
       hipLaunchKernelGGL(prep_class_x3_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, (unsigned short*)Wp, ktab);
+                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab);
     else
       hipLaunchKernelGGL(prep_class_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, pass == kData ? 1 : 0,
@@ -1185,23 +1203,34 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       else hipLaunchKernelGGL(gather_smalln_kernel<16>, grid, dim3(kThreads), sh, st, a);
     } else {
       const bool tu = tu_of(c);
+      // 256-column workgroups (NW = 2) where the padded column count allows
+      const bool wide = (ldw % 256 == 0) && gemm_nw() == 2;
+      const dim3 grid(se::ceil_div(M, kX3BM), ldw / (wide ? 2 * kX3BN : kX3BN));
+      const dim3 blk(wide ? 2 * kThreads : kThreads);
       if (x6) {
-        dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
-        if (join_in) hipLaunchKernelGGL((gather_x6_kernel<true, true>), grid, dim3(kThreads), 0, st, a);
-        else if (tu) hipLaunchKernelGGL(gather_x6_kernel<true>, grid, dim3(kThreads), 0, st, a);
-        else hipLaunchKernelGGL(gather_x6_kernel<false>, grid, dim3(kThreads), 0, st, a);
-      } else if (bf1) {
-        dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
-        if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 1>), grid, dim3(kThreads), 0, st, a);
-        else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 2>), grid, dim3(kThreads), 0, st, a);
-        else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
-        else hipLaunchKernelGGL((gather_x3_kernel<false, 1>), grid, dim3(kThreads), 0, st, a);
+        if (wide) {
+          if (join_in) hipLaunchKernelGGL((gather_x6_kernel<true, true, 2>), grid, blk, 0, st, a);
+          else if (tu) hipLaunchKernelGGL((gather_x6_kernel<true, false, 2>), grid, blk, 0, st, a);
+          else hipLaunchKernelGGL((gather_x6_kernel<false, false, 2>), grid, blk, 0, st, a);
+        } else {
+          if (join_in) hipLaunchKernelGGL((gather_x6_kernel<true, true>), grid, blk, 0, st, a);
+          else if (tu) hipLaunchKernelGGL(gather_x6_kernel<true>, grid, blk, 0, st, a);
+          else hipLaunchKernelGGL(gather_x6_kernel<false>, grid, blk, 0, st, a);
+        }
       } else if (x3) {
-        dim3 grid(se::ceil_div(M, kX3BM), ldw / kX3BN);
-        if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1>), grid, dim3(kThreads), 0, st, a);
-        else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2>), grid, dim3(kThreads), 0, st, a);
-        else if (tu) hipLaunchKernelGGL(gather_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
-        else hipLaunchKernelGGL(gather_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
+        const int terms = bf1 ? 1 : 3;
+#define SE_X3_LAUNCH(T, NWV)                                                                            \
+  do {                                                                                                 \
+    if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, T, 1, NWV>), grid, blk, 0, st, a);         \
+    else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, T, 2, NWV>), grid, blk, 0, st, a);   \
+    else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, T, 0, NWV>), grid, blk, 0, st, a);         \
+    else hipLaunchKernelGGL((gather_x3_kernel<false, T, 0, NWV>), grid, blk, 0, st, a);                \
+  } while (0)
+        if (terms == 1 && wide) SE_X3_LAUNCH(1, 2);
+        else if (terms == 1) SE_X3_LAUNCH(1, 1);
+        else if (wide) SE_X3_LAUNCH(3, 2);
+        else SE_X3_LAUNCH(3, 1);
+#undef SE_X3_LAUNCH
       } else if (ldw == 64) {
         dim3 grid(se::ceil_div(M, 256), 1);
         if (tu) hipLaunchKernelGGL((gather_gemm_kernel<64, 256, 1, 4, true>), grid, dim3(kThreads), 0, st, a);

@@ -39,13 +39,31 @@ __device__ __forceinline__ unsigned short bf16_bits(float x) {
 __device__ __forceinline__ int x3_chunk(int row, int c) { return c ^ ((row >> 2) & 3); }
 
 constexpr int kX3BN = 128, kX3BM = 128;
+
+// K order of the split GEMMs' weight image / ktab. kblk = 0: tap-major,
+// k = tap * Cg + c. kblk = 32 (Cg % 32 == 0): channel-block-major, k =
+// ((c / 32) * taps + tap) * 32 + c % 32, so a tile visits every tap of a
+// 32-channel block in consecutive K-steps and the block's input rows are
+// re-read from L2 instead of after a sweep over all Cg channels (which
+// evicts them). ktab[k].w holds the channel c.
+__device__ __forceinline__ void split_k(int k, int Cg, int ntaps, int kblk, int& t, int& c) {
+  if (kblk) {
+    const int s = k / kblk, cl = k - s * kblk;
+    t = s % ntaps;
+    c = (s / ntaps) * kblk + cl;
+  } else {
+    t = k / Cg;
+    c = k - t * Cg;
+  }
+}
 constexpr int kX3TileU4 = 2 * 128 * 4;   // u32x4 per (k-step, n-tile) weight image = 16 KB
 
 // Pre-tiled split weight: Wt[(s * NT + t) * kX3TileU4 + (plane * 128 + n) * 4 + x3_chunk(n, c)]
 // holds bf16 element e of k = 32 s + 8 c + e, column n0 = 128 t + n. Also ktab
 // (as prep_class_kernel).
 __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, int Kp, int NT,
-                                     int Hi, int Wi, int data_grad, unsigned short* Wt, int4* ktab) {
+                                     int Hi, int Wi, int data_grad, int kblk, unsigned short* Wt,
+                                     int4* ktab) {
   const int K = taps.n * Cg;
   const long long total = (long long)Kp * NT * 128;   // one thread per (k, n)
   for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -54,7 +72,8 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
     const int n = (int)(idx / Kp);
     float v = 0.f;
     if (k < K && n < N) {
-      const int t = k / Cg, c = k % Cg;
+      int t, c;
+      split_k(k, Cg, taps.n, kblk, t, c);
       const int ci = data_grad ? n : c, co = data_grad ? c : n;
       v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
     }
@@ -68,15 +87,17 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
     Wt[base + 128 * 4 * 8 + off] = lb;
     if (n == 0) {
       int4 q;
+      q.w = 0;
       if (k < K) {
-        const int t = k / Cg, c = k % Cg;
+        int t, c;
+        split_k(k, Cg, taps.n, kblk, t, c);
         q.x = (int)((long long)c * Hi * Wi + (long long)taps.offh[t] * Wi + taps.offw[t]);
         q.y = taps.offh[t];
         q.z = taps.offw[t];
+        q.w = c;
       } else {
         q.x = 0; q.y = kInvalidOff; q.z = 0;
       }
-      q.w = 0;
       ktab[k] = q;
     }
   }
@@ -94,27 +115,33 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // JM: decoder skip join (GatherArgs::X2 / Y2): 0 none, 1 the gathered tensor
 // is the joined input (forward), 2 the output is split into the joined
 // input's two gradients (data-grad). Both need the TU path.
-template <bool TU, int TERMS = 3, int JM = 0>
-__global__ void __launch_bounds__(kThreads, 2)
+// NW: 128-column weight tiles per workgroup. NW = 2 is a 256 (n) x 128 (m)
+// tile of 8 waves (one workgroup per CU): each gathered activation is loaded
+// and split once per 256 output columns instead of once per 128.
+template <bool TU, int TERMS = 3, int JM = 0, int NW = 1>
+__global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
   static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
+  static_assert(NW == 1 || NW == 2, "128 or 256 columns per workgroup");
   constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
-  constexpr int BN = kX3BN, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
-  constexpr int AJ = 16;                          // gathered k per thread per step
+  constexpr int THR = kThreads * NW;
+  constexpr int BN = kX3BN * NW, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
+  constexpr int AJ = 16 / NW;                     // gathered k per thread per step
+  constexpr int CPT = AJ / 8;                     // 16-B chunks per plane per thread
   __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * BM * 4];
-  __shared__ __attribute__((aligned(16))) u32x4 sW[2][2 * BN * 4];
+  __shared__ __attribute__((aligned(16))) u32x4 sW[2][2 * BN * 4];   // [t][plane][128 rows][4]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
-  const int NT = gridDim.y;
+  const int NT = gridDim.y;                       // workgroup column tiles (BN wide)
   const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int mt = tile / NT, nt = tile % NT;
   const int m0 = mt * BM, n0 = nt * BN;
   const long long HiWi = (long long)a.Hi * a.Wi;
 
   const int am = tid % BM;
-  const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // 0 or 1 (wave-uniform)
+  const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // 0 .. 2 NW - 1 (wave-uniform)
   const int m = m0 + am;
   const bool mval = m < a.M;
   int hb = 0, wb = 0;
@@ -144,7 +171,10 @@ gather_x3_kernel(const GatherArgs a) {
   if constexpr (JM == 1)
     rx2 = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.X2 + (long long)b0 * cpb * H2W2), (short)0,
                                             0x7FFFFFFF, 0x00020000);
-  const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * kX3TileU4 + tid;
+  // this workgroup's NW consecutive 128-column images of one k-step; a
+  // thread's element e = tid + THR j (j < 2 PL) of [t][plane][row][4]; with
+  // one plane (PL = 1) the lo planes are skipped
+  const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * NW * kX3TileU4;
   int xoff = 0, xoff2 = 0;
   if constexpr (TU) {
     if (mval) {
@@ -155,9 +185,8 @@ gather_x3_kernel(const GatherArgs a) {
   }
   auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
     if constexpr (TU) {
-      const int4 e0 = a.ktab[k0];                 // the step's tap (uniform)
-      const int tap = k0 / a.Cg;
-      int c0 = k0 - tap * a.Cg;                   // the step's first channel (uniform)
+      const int4 e0 = a.ktab[k0];                 // the step's tap and first channel (uniform)
+      int c0 = e0.w;
       const int hi = hb + e0.y, wi = wb + e0.z;
       bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
       int vo = xoff + (e0.y * a.Wi + e0.z) * 4, cs = (int)(HiWi * 4);
@@ -185,14 +214,17 @@ gather_x3_kernel(const GatherArgs a) {
         st.ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
       }
     }
-    const u32x4* src = wt + (long long)(k0 >> 5) * NT * kX3TileU4;
+    const u32x4* src = wt + (long long)(k0 >> 5) * NT * NW * kX3TileU4;
 #pragma unroll
-    for (int j = 0; j < 2 * PL; ++j) st.rw[j] = src[kThreads * j];   // hi plane first
+    for (int j = 0; j < 2 * PL; ++j) {
+      const int e = tid + THR * j;
+      st.rw[j] = src[PL == 2 ? e : e + (e >> 9) * 512];
+    }
   };
   const int swz = (am >> 2) & 3;
   auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < CPT; ++q) {
       u32x4 H, L;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -201,12 +233,12 @@ gather_x3_kernel(const GatherArgs a) {
         H[e] = h;
         L[e] = l;
       }
-      const int c = (2 * akr + q) ^ swz;
+      const int c = (CPT * akr + q) ^ swz;
       sA[buf][am * 4 + c] = H;
       if constexpr (PL == 2) sA[buf][BM * 4 + am * 4 + c] = L;
     }
 #pragma unroll
-    for (int j = 0; j < 2 * PL; ++j) sW[buf][tid + kThreads * j] = st.rw[j];
+    for (int j = 0; j < 2 * PL; ++j) sW[buf][tid + THR * j] = st.rw[j];
   };
 
   f32x16 acc[RN][RM];
@@ -225,10 +257,12 @@ gather_x3_kernel(const GatherArgs a) {
     for (int ks = 0; ks < 2; ++ks) {
       const int c = (2 * ks + lh) ^ fsw;
 #pragma unroll
-      for (int i = 0; i < RN; ++i)
+      for (int i = 0; i < RN; ++i) {
+        const int n = wn * TN + 32 * i;           // block's first column (uniform)
 #pragma unroll
         for (int p = 0; p < PL; ++p)
-          wf[ks][i][p] = sW[cur][(p * BN + wn * TN + 32 * i + lr) * 4 + c];
+          wf[ks][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+      }
 #pragma unroll
       for (int j = 0; j < RM; ++j)
 #pragma unroll
@@ -254,7 +288,7 @@ gather_x3_kernel(const GatherArgs a) {
     for (int i = 0; i < 24; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
-      if (i < 20) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // global load
+      if (i < AJ + 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
     }
 #endif
@@ -283,7 +317,7 @@ gather_x3_kernel(const GatherArgs a) {
   // --- epilogue (as gather_gemm_kernel) ---
   __syncthreads();
   float* sBias = reinterpret_cast<float*>(&sW[0][0]);
-  for (int i = tid; i < BN; i += kThreads) {
+  for (int i = tid; i < BN; i += THR) {
     const int n = n0 + i;
     sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   }
@@ -626,7 +660,8 @@ __device__ __forceinline__ int x6_chunk(int row, int c) { return c ^ ((row >> 3)
 // Wt[(s * NT + t) * kX6TileU4 + (plane * 128 + n) * 2 + x6_chunk(n, c)]: element e of
 // k = 16 s + 8 c + e, column 128 t + n. Also ktab.
 __global__ void prep_class_x6_kernel(WeightView w, TapList taps, int Cg, int N, int Kp, int NT,
-                                     int Hi, int Wi, int data_grad, unsigned short* Wt, int4* ktab) {
+                                     int Hi, int Wi, int data_grad, int kblk, unsigned short* Wt,
+                                     int4* ktab) {
   const int K = taps.n * Cg;
   const long long total = (long long)Kp * NT * 128;
   for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
@@ -635,7 +670,8 @@ __global__ void prep_class_x6_kernel(WeightView w, TapList taps, int Cg, int N, 
     const int n = (int)(idx / Kp);
     float v = 0.f;
     if (k < K && n < N) {
-      const int t = k / Cg, c = k % Cg;
+      int t, c;
+      split_k(k, Cg, taps.n, kblk, t, c);
       const int ci = data_grad ? n : c, co = data_grad ? c : n;
       v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
     }
@@ -651,40 +687,46 @@ __global__ void prep_class_x6_kernel(WeightView w, TapList taps, int Cg, int N, 
     Wt[base + 2 * 128 * 2 * 8 + off] = lb;
     if (n == 0) {
       int4 q;
+      q.w = 0;
       if (k < K) {
-        const int t = k / Cg, c = k % Cg;
+        int t, c;
+        split_k(k, Cg, taps.n, kblk, t, c);
         q.x = (int)((long long)c * Hi * Wi + (long long)taps.offh[t] * Wi + taps.offw[t]);
         q.y = taps.offh[t];
         q.z = taps.offw[t];
+        q.w = c;
       } else {
         q.x = 0; q.y = kInvalidOff; q.z = 0;
       }
-      q.w = 0;
       ktab[k] = q;
     }
   }
 }
 
 // JG: the gathered tensor is the decoder skip join (as gather_x3_kernel JM = 1).
-template <bool TU, bool JG = false>
-__global__ void __launch_bounds__(kThreads, 2)
+// NW: 128-column weight tiles per workgroup (as gather_x3_kernel); with NW = 2
+// a thread gathers 4 k per step and writes half-chunks (ds_write_b64).
+template <bool TU, bool JG = false, int NW = 1>
+__global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x6_kernel(const GatherArgs a) {
   static_assert(!JG || TU, "the joined gather runs on the tap-uniform path");
-  constexpr int BN = kX3BN, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
-  constexpr int BK = kX6BK, AJ = 8;               // gathered k per thread per step
+  static_assert(NW == 1 || NW == 2, "128 or 256 columns per workgroup");
+  constexpr int THR = kThreads * NW;
+  constexpr int BN = kX3BN * NW, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
+  constexpr int BK = kX6BK, AJ = 8 / NW;          // gathered k per thread per step
   __shared__ __attribute__((aligned(16))) u32x4 sA[2][3 * BM * 2];
-  __shared__ __attribute__((aligned(16))) u32x4 sW[2][3 * BN * 2];
+  __shared__ __attribute__((aligned(16))) u32x4 sW[2][3 * BN * 2];   // [t][plane][128 rows][2]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
-  const int NT = gridDim.y;
+  const int NT = gridDim.y;                       // workgroup column tiles (BN wide)
   const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
   const int mt = tile / NT, nt = tile % NT;
   const int m0 = mt * BM, n0 = nt * BN;
   const long long HiWi = (long long)a.Hi * a.Wi;
 
   const int am = tid % BM;
-  const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // 0 or 1 (wave-uniform)
+  const int akr = __builtin_amdgcn_readfirstlane(tid / BM);   // 0 .. 2 NW - 1 (wave-uniform)
   const int m = m0 + am;
   const bool mval = m < a.M;
   int hb = 0, wb = 0;
@@ -714,7 +756,7 @@ gather_x6_kernel(const GatherArgs a) {
   if constexpr (JG)
     rx2 = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.X2 + (long long)b0 * cpb * H2W2), (short)0,
                                             0x7FFFFFFF, 0x00020000);
-  const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * kX6TileU4 + tid;
+  const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * NW * kX6TileU4 + tid;
   int xoff = 0, xoff2 = 0;
   if constexpr (TU) {
     if (mval) {
@@ -725,9 +767,8 @@ gather_x6_kernel(const GatherArgs a) {
   }
   auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
     if constexpr (TU) {
-      const int4 e0 = a.ktab[k0];
-      const int tap = k0 / a.Cg;
-      int c0 = k0 - tap * a.Cg;
+      const int4 e0 = a.ktab[k0];                 // the step's tap and first channel (uniform)
+      int c0 = e0.w;
       const int hi = hb + e0.y, wi = wb + e0.z;
       bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
       int vo = xoff + (e0.y * a.Wi + e0.z) * 4, cs = (int)(HiWi * 4);
@@ -755,24 +796,39 @@ gather_x6_kernel(const GatherArgs a) {
         st.ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
       }
     }
-    const u32x4* src = wt + (long long)(k0 / BK) * NT * kX6TileU4;
+    const u32x4* src = wt + (long long)(k0 / BK) * NT * NW * kX6TileU4;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) st.rw[j] = src[kThreads * j];
+    for (int j = 0; j < 3; ++j) st.rw[j] = src[THR * j];
   };
-  const int wchunk = x6_chunk(am, akr);
+  const int wchunk = x6_chunk(am, AJ == 8 ? akr : akr >> 1);
   auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
-    u32x4 H, M, L;
+    if constexpr (AJ == 8) {
+      u32x4 H, M, L;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      unsigned h, mm, l;
-      split3_bf16x2(st.ra[2 * e], st.ra[2 * e + 1], h, mm, l);
-      H[e] = h; M[e] = mm; L[e] = l;
+      for (int e = 0; e < 4; ++e) {
+        unsigned h, mm, l;
+        split3_bf16x2(st.ra[2 * e], st.ra[2 * e + 1], h, mm, l);
+        H[e] = h; M[e] = mm; L[e] = l;
+      }
+      sA[buf][am * 2 + wchunk] = H;
+      sA[buf][BM * 2 + am * 2 + wchunk] = M;
+      sA[buf][2 * BM * 2 + am * 2 + wchunk] = L;
+    } else {                                      // half a chunk: k 4 (akr & 1) .. + 3
+      typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+      u32x2v H, M, L;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        unsigned h, mm, l;
+        split3_bf16x2(st.ra[2 * e], st.ra[2 * e + 1], h, mm, l);
+        H[e] = h; M[e] = mm; L[e] = l;
+      }
+      const int half = akr & 1;
+      reinterpret_cast<u32x2v*>(&sA[buf][am * 2 + wchunk])[half] = H;
+      reinterpret_cast<u32x2v*>(&sA[buf][BM * 2 + am * 2 + wchunk])[half] = M;
+      reinterpret_cast<u32x2v*>(&sA[buf][2 * BM * 2 + am * 2 + wchunk])[half] = L;
     }
-    sA[buf][am * 2 + wchunk] = H;
-    sA[buf][BM * 2 + am * 2 + wchunk] = M;
-    sA[buf][2 * BM * 2 + am * 2 + wchunk] = L;
 #pragma unroll
-    for (int j = 0; j < 3; ++j) sW[buf][tid + kThreads * j] = st.rw[j];
+    for (int j = 0; j < 3; ++j) sW[buf][tid + THR * j] = st.rw[j];
   };
 
   f32x16 acc[RN][RM];
@@ -790,7 +846,10 @@ gather_x6_kernel(const GatherArgs a) {
 #pragma unroll
     for (int p = 0; p < 3; ++p) {
 #pragma unroll
-      for (int i = 0; i < RN; ++i) wf[i][p] = sW[cur][(p * BN + wn * TN + 32 * i + lr) * 2 + fc];
+      for (int i = 0; i < RN; ++i) {
+        const int n = wn * TN + 32 * i;           // block's first column (uniform)
+        wf[i][p] = sW[cur][(((n >> 7) * 3 + p) * 128 + (n & 127) + lr) * 2 + fc];
+      }
 #pragma unroll
       for (int j = 0; j < RM; ++j) af[j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 2 + fc];
     }
@@ -814,7 +873,7 @@ gather_x6_kernel(const GatherArgs a) {
     for (int i = 0; i < 24; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       if (i < 14) __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);    // DS
-      if (i < 11) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);    // global load
+      if (i < AJ + 3) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
     }
 #endif
@@ -842,7 +901,7 @@ gather_x6_kernel(const GatherArgs a) {
 
   __syncthreads();
   float* sBias = reinterpret_cast<float*>(&sW[0][0]);
-  for (int i = tid; i < BN; i += kThreads) {
+  for (int i = tid; i < BN; i += THR) {
     const int n = n0 + i;
     sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   }

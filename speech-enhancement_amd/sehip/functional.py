@@ -86,14 +86,16 @@ class OpTimer:
     def end(self, tag, start, flops=0.0, nbytes=0.0):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        self.records.append((tag, start, ev, float(flops), float(nbytes)))
+        side = torch.cuda.current_stream() != torch.cuda.default_stream()
+        self.records.append((tag, start, ev, float(flops), float(nbytes), side))
 
     def summary(self):
         torch.cuda.synchronize()
         out = {}
-        for tag, a, b, fl, nb in self.records:
-            d = out.setdefault(tag, dict(calls=0, ms=0.0, flops=0.0, bytes=0.0))
+        for tag, a, b, fl, nb, side in self.records:
+            d = out.setdefault(tag, dict(calls=0, ms=0.0, flops=0.0, bytes=0.0, side_calls=0))
             d["calls"] += 1
+            d["side_calls"] += int(side)   # on a side stream, sharing the CUs with the main one
             d["ms"] += a.elapsed_time(b)
             d["flops"] += fl
             d["bytes"] += nb
