@@ -212,6 +212,18 @@ int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
                int act, float slope, void* ws, size_t ws_bytes,
                void* stream);
 
+/* Backward of a forked output: y feeds two consumers (FRCRN's encoder block
+ * output is the next encoder conv's input and the decoder skip, frcrn.py:70-75,
+ * 93-95), so dL/dy = gy + gy2. The sum is formed on the fly in both passes;
+ * autograd's separate gradient-accumulation add (2 reads + 1 write of an
+ * activation-sized tensor) is never run. gy2 must not be NULL. Otherwise as
+ * se_cbn_bwd. */
+int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, float* dx,
+                int B, int C, int HW, const float* const* params,
+                const float* save, float* const* dparams, int training,
+                int act, float slope, void* ws, size_t ws_bytes,
+                void* stream);
+
 /* ------------------------------------------------------------------------
  * LSTM recurrence (torch.nn.LSTM as used by ComplexLSTM, complex_nn.py:115-145)
  *

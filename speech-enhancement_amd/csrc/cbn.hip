@@ -147,10 +147,12 @@ cbn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int 
   }
 }
 
-// Backward moments: g = gy * act'(y), xt = x - M.
+// Backward moments: g = (gy [+ gy2]) * act'(z), xt = x - M. gy2 (G2) is a second
+// gradient of the same output (a forked output, se_cbn_bwd2): summed on the fly.
 // sums: gr, gi, gr*xtr, gr*xti, gi*xtr, gi*xti
+template <bool G2>
 __global__ void __launch_bounds__(kThreads)
-cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
                        const float* __restrict__ x, int B, int C, int HW, int P,
                        const float* __restrict__ save, int act, float slope, double* part) {
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
@@ -166,8 +168,8 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ y
     for (int i = sg * kSeg + threadIdx.x; i < i1; i += kThreads) {
       const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
       const float zr = zrr * xr + zri * xi + br, zi = zir * xr + zii * xi + bi;   // = forward pre-activation
-      const float gr = gy[offr + i] * act_grad(zr, act, slope);
-      const float gi = gy[offi + i] * act_grad(zi, act, slope);
+      const float gr = (G2 ? gy[offr + i] + gy2[offr + i] : gy[offr + i]) * act_grad(zr, act, slope);
+      const float gi = (G2 ? gy[offi + i] + gy2[offi + i] : gy[offi + i]) * act_grad(zi, act, slope);
       v[0] += gr; v[1] += gi;
       v[2] += (double)gr * xr; v[3] += (double)gr * xi;
       v[4] += (double)gi * xr; v[5] += (double)gi * xi;
@@ -240,8 +242,9 @@ __global__ void cbn_bwd_finalize_kernel(const double* part, int P, double count,
   }
 }
 
+template <bool G2>
 __global__ void __launch_bounds__(kThreads)
-cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ y,
+cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
                      const float* __restrict__ x, float* __restrict__ dx, int C, int HW,
                      const float* __restrict__ coef, int act, float slope) {
   const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
@@ -258,8 +261,8 @@ cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ y,
     if (i < HW) {
       const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
       const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
-      const float gr = gy[offr + i] * act_grad(zr, act, slope) - gbr;
-      const float gi = gy[offi + i] * act_grad(zi, act, slope) - gbi;
+      const float gr = (G2 ? gy[offr + i] + gy2[offr + i] : gy[offr + i]) * act_grad(zr, act, slope) - gbr;
+      const float gi = (G2 ? gy[offi + i] + gy2[offi + i] : gy[offi + i]) * act_grad(zi, act, slope) - gbi;
       dx[offr + i] = a00 * gr + a01 * gi + grr * xr + gri * xi;
       dx[offi + i] = a10 * gr + a11 * gi + gri * xr + gii * xi;
     }
@@ -309,11 +312,11 @@ extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
   return SE_OK;
 }
 
-extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx, int B,
-                          int C, int HW, const float* const* params, const float* save,
-                          float* const* dparams, int training, int act, float slope, void* ws,
-                          size_t ws_bytes, void* stream) {
-  (void)y;   // not read: act' is recomputed from x (see the file comment); may be NULL
+namespace {
+
+int cbn_bwd_impl(const float* gy, const float* gy2, const float* x, float* dx, int B, int C,
+                 int HW, const float* const* params, const float* save, float* const* dparams,
+                 int training, int act, float slope, void* ws, size_t ws_bytes, void* stream) {
   if (!gy || !x || !dx || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0) return SE_E_ARG;
   if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
@@ -325,14 +328,46 @@ extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float
   MPtr5 dp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (dparams) for (int k = 0; k < 5; ++k) dp.p[k] = dparams[k];
-  hipLaunchKernelGGL(cbn_bwd_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, gy, y, x, B, C,
-                     HW, P, save, act, slope, part);
+  if (gy2)
+    hipLaunchKernelGGL(cbn_bwd_moments_kernel<true>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2, x,
+                       B, C, HW, P, save, act, slope, part);
+  else
+    hipLaunchKernelGGL(cbn_bwd_moments_kernel<false>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2,
+                       x, B, C, HW, P, save, act, slope, part);
   SE_LAUNCH_CHECK();
   hipLaunchKernelGGL(cbn_bwd_finalize_kernel, dim3(1), dim3(256), 0, st, part, P, (double)B * HW,
                      Cc, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, coef);
   SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cbn_bwd_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), Cc, B),
-                     dim3(kThreads), 0, st, gy, y, x, dx, C, HW, coef, act, slope);
+  const dim3 grid(se::ceil_div(HW, kThreads * 4), Cc, B);
+  if (gy2)
+    hipLaunchKernelGGL(cbn_bwd_apply_kernel<true>, grid, dim3(kThreads), 0, st, gy, gy2, x, dx, C,
+                       HW, coef, act, slope);
+  else
+    hipLaunchKernelGGL(cbn_bwd_apply_kernel<false>, grid, dim3(kThreads), 0, st, gy, gy2, x, dx, C,
+                       HW, coef, act, slope);
   SE_LAUNCH_CHECK();
   return SE_OK;
+}
+
+}  // namespace
+
+extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx, int B,
+                          int C, int HW, const float* const* params, const float* save,
+                          float* const* dparams, int training, int act, float slope, void* ws,
+                          size_t ws_bytes, void* stream) {
+  (void)y;   // not read: act' is recomputed from x (see the file comment); may be NULL
+  return cbn_bwd_impl(gy, nullptr, x, dx, B, C, HW, params, save, dparams, training, act, slope,
+                      ws, ws_bytes, stream);
+}
+
+// Forked output (the encoder block's y feeds the next conv AND the decoder skip):
+// gy + gy2 is summed inside both passes instead of by a separate add of two
+// activation-sized tensors (3 passes) before the backward.
+extern "C" int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, float* dx, int B,
+                           int C, int HW, const float* const* params, const float* save,
+                           float* const* dparams, int training, int act, float slope, void* ws,
+                           size_t ws_bytes, void* stream) {
+  if (!gy2) return SE_E_ARG;
+  return cbn_bwd_impl(gy, gy2, x, dx, B, C, HW, params, save, dparams, training, act, slope, ws,
+                      ws_bytes, stream);
 }

@@ -285,14 +285,15 @@ class ComplexBatchNorm2d(nn.Module):
                 self.Wrr.fill_(1); self.Wii.fill_(1)
                 self.Wri.uniform_(-.9, +.9)
 
-    def forward_act(self, x, act=F.ACT_NONE, slope=0.0):
-        """BN followed by a fused activation (LeakyReLU / ReLU)."""
+    def forward_act(self, x, act=F.ACT_NONE, slope=0.0, fork=False):
+        """BN followed by a fused activation (LeakyReLU / ReLU). fork=True returns
+        (y, alias of y) for two consumers (see functional.complex_batch_norm)."""
         running = (self.RMr, self.RMi, self.RVrr, self.RVri, self.RVii) if self.track_running_stats else None
         training = self.training or not self.track_running_stats    # complex_nn.py:234
         return F.complex_batch_norm(
             x, self.Wrr, self.Wri, self.Wii, self.Br, self.Bi, running,
             self.num_batches_tracked if self.track_running_stats else None,
-            training, self.eps, self.momentum, act, slope)
+            training, self.eps, self.momentum, act, slope, fork)
 
     def forward(self, inputs):
         return self.forward_act(inputs)
@@ -302,17 +303,20 @@ class ComplexBatchNorm2d(nn.Module):
                 "track_running_stats={track_running_stats}".format(**self.__dict__))
 
 
-def norm_act(norm: nn.Module, act: nn.Module, x):
+def norm_act(norm: nn.Module, act: nn.Module, x, fork: bool = False):
     """act(norm(x)) with the activation fused into the CBN kernel when both are
-    the kinds the kernel knows; otherwise the two modules are applied in turn."""
+    the kinds the kernel knows; otherwise the two modules are applied in turn.
+    fork=True returns (y, y2) for two consumers of y: with the CBN kernel y2 is an
+    alias whose gradient the CBN backward sums itself; otherwise y2 is y."""
     if isinstance(norm, ComplexBatchNorm2d):
         if isinstance(act, nn.LeakyReLU):
-            return norm.forward_act(x, F.ACT_LEAKY, act.negative_slope)
+            return norm.forward_act(x, F.ACT_LEAKY, act.negative_slope, fork)
         if isinstance(act, nn.ReLU):
-            return norm.forward_act(x, F.ACT_RELU, 0.0)
+            return norm.forward_act(x, F.ACT_RELU, 0.0, fork)
         if isinstance(act, nn.Identity):
-            return norm.forward_act(x)
-    return act(norm(x))
+            return norm.forward_act(x, fork=fork)
+    y = act(norm(x))
+    return (y, y) if fork else y
 
 
 class ComplexPReLU(nn.Module):

@@ -414,7 +414,8 @@ ACT_NONE, ACT_LEAKY, ACT_RELU = 0, 1, 2
 
 class _ComplexBN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum, act, slope):
+    def forward(ctx, x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum, act, slope,
+                fork=False):
         N.require_device(x, wrr)
         x = x.contiguous()
         b, c = x.shape[:2]
@@ -435,13 +436,21 @@ class _ComplexBN(torch.autograd.Function):
             _TIMER.end("cbn_fwd", t0, 0.0, 4.0 * x.numel() * (3 if training else 2))
         ctx.save_for_backward(x, save, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
+        if fork:   # (y, alias of y): two consumers, two gradients summed inside se_cbn_bwd2
+            ctx.set_materialize_grads(False)
+            return y, y.view(y.shape)
         return y
 
     @staticmethod
-    def backward(ctx, gy):
+    def backward(ctx, gy, gy2=None):
         x, save, *params = ctx.saved_tensors
         training, act, slope, affine = ctx.cfg
+        if gy is None:
+            gy, gy2 = gy2, None
+        if gy is None:
+            return (None,) * 14
         gy = gy.contiguous()
+        gy2 = gy2.contiguous() if gy2 is not None else None
         b, c = x.shape[:2]
         hw = x[0, 0].numel()
         dx = torch.empty_like(x)
@@ -449,22 +458,30 @@ class _ComplexBN(torch.autograd.Function):
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(lib.se_cbn_bwd(gy.data_ptr(), None, x.data_ptr(), dx.data_ptr(), b, c, hw,
-                               N.ptr_array(params if affine else None), save.data_ptr(),
-                               N.ptr_array(dparams), training, act, slope, ws.data_ptr(),
-                               ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
-        if t0 is not None:   # (gy, x) read twice + dx written
-            _TIMER.end("cbn_bwd", t0, 0.0, 4.0 * x.numel() * 5)
+        if gy2 is None:
+            N.check(lib.se_cbn_bwd(gy.data_ptr(), None, x.data_ptr(), dx.data_ptr(), b, c, hw,
+                                   N.ptr_array(params if affine else None), save.data_ptr(),
+                                   N.ptr_array(dparams), training, act, slope, ws.data_ptr(),
+                                   ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
+        else:
+            N.check(lib.se_cbn_bwd2(gy.data_ptr(), gy2.data_ptr(), x.data_ptr(), dx.data_ptr(), b,
+                                    c, hw, N.ptr_array(params if affine else None),
+                                    save.data_ptr(), N.ptr_array(dparams), training, act, slope,
+                                    ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd2")
+        if t0 is not None:   # (gy [, gy2], x) read twice + dx written
+            _TIMER.end("cbn_bwd", t0, 0.0, 4.0 * x.numel() * (5 if gy2 is None else 7))
         g = dparams or [None] * 5
-        return (dx, *g, None, None, None, None, None, None, None)
+        return (dx, *g, None, None, None, None, None, None, None, None)
 
 
 def complex_batch_norm(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
-                       act=ACT_NONE, slope=0.0):
+                       act=ACT_NONE, slope=0.0, fork=False):
     """ComplexBatchNorm2d forward (+ optional fused activation) on the HIP path.
-    running: (RMr, RMi, RVrr, RVri, RVii) or None; nbt: int64 tensor or None."""
+    running: (RMr, RMi, RVrr, RVri, RVii) or None; nbt: int64 tensor or None.
+    fork=True returns (y, alias of y) for two consumers: their two gradients are summed inside
+    the backward kernels (se_cbn_bwd2) instead of by autograd's accumulation add."""
     return _ComplexBN.apply(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
-                            act, slope)
+                            act, slope, fork)
 
 
 # --------------------------------------------------------------------------

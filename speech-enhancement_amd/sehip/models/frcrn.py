@@ -47,7 +47,7 @@ class _CausalConvBase(nn.Module):
     def _conv(self):
         return getattr(self, self.conv_attr)
 
-    def forward(self, x):
+    def forward(self, x, fork: bool = False):
         lp = self.padding[1]
         pad = (lp, 0 if self.causal else lp, 0, 0)
         conv = self._conv()
@@ -59,7 +59,7 @@ class _CausalConvBase(nn.Module):
             pad = None
         # the time pad of a plain conv is folded into its (asymmetric) padding
         y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
-        return norm_act(self.norm, self.act, y)
+        return norm_act(self.norm, self.act, y, fork)
 
     def forward_joined(self, x, skip):
         """self(complex_join(x, skip)) (frcrn.py:95-101) without writing the
@@ -120,10 +120,12 @@ class Encoder(nn.Module):
                       causal=True, is_complex=is_complex) for i in range(num_repeats))
 
     def forward(self, x):
+        # each block output feeds the next block and a decoder skip (frcrn.py:70-75): forked in
+        # the CBN so the two gradients are summed inside its backward (se_cbn_bwd2)
         skips = []
         for layer in self.layers:
-            x = layer(x)
-            skips.append(x)
+            x, skip = layer(x, fork=True)
+            skips.append(skip)
         return x, skips
 
 

@@ -75,3 +75,32 @@ def test_cbn_whitening_full_size(gpu_device):
     assert (yr.pow(2).mean(dim=(0, 2, 3)) - 1).abs().max() < 1e-3
     assert (yi.pow(2).mean(dim=(0, 2, 3)) - 1).abs().max() < 1e-3
     assert (yr * yi).mean(dim=(0, 2, 3)).abs().max() < 1e-3
+
+
+@pytest.mark.parametrize("used", ["both", "first", "second"])
+def test_cbn_fork_sums_both_gradients(used, gpu_device):
+    """fork=True (FRCRN encoder outputs: next conv + decoder skip) sums the two output
+    gradients inside se_cbn_bwd2; bit-identical to autograd's add followed by se_cbn_bwd,
+    and either consumer alone (the other gradient absent) matches the plain backward."""
+    from sehip.complex_nn import ComplexBatchNorm2d, norm_act
+    gen = torch.Generator().manual_seed(11)
+    x = (torch.randn(4, 128, 13, 37, generator=gen) * 1.5 + 0.3).cuda()
+    g1 = torch.randn(x.shape, generator=gen).cuda()
+    g2 = torch.randn(x.shape, generator=gen).cuda()
+    grads = {"both": (g1, g2), "first": (g1, None), "second": (None, g2)}[used]
+    act = torch.nn.LeakyReLU(0.2)
+
+    m0 = paramfill.fill_(ComplexBatchNorm2d(128), seed=4).cuda().train()
+    x0 = x.clone().requires_grad_(True)
+    y0 = norm_act(m0, act, x0)
+    y0.backward(sum(g for g in grads if g is not None))
+
+    m1 = paramfill.fill_(ComplexBatchNorm2d(128), seed=4).cuda().train()
+    x1 = x.clone().requires_grad_(True)
+    ya, yb = norm_act(m1, act, x1, fork=True)
+    assert yb.data_ptr() == ya.data_ptr() and torch.equal(ya, y0)
+    outs = [(t, g) for t, g in zip((ya, yb), grads) if g is not None]
+    torch.autograd.backward([t for t, _ in outs], [g for _, g in outs])
+    assert torch.equal(x1.grad, x0.grad)
+    for n in ("Wrr", "Wri", "Wii", "Br", "Bi"):
+        assert torch.equal(getattr(m1, n).grad, getattr(m0, n).grad), n
