@@ -208,7 +208,9 @@ def main():
         "conv_math_note": "fp32 storage and accumulation everywhere; 'bf16x3' passes split each fp32 "
                           "operand into hi+lo bf16 and sum hi*hi+hi*lo+lo*hi on bf16 MFMA (4.5e-6 "
                           "rel-L2 per conv vs fp64); 'bf16x6' splits three ways and sums the six "
-                          "terms of order >= 2^-16 (5.5e-7 vs fp64, fp32 MFMA path 6.4e-7); "
+                          "terms of order >= 2^-16 (5.5e-7 vs fp64, fp32 MFMA path 6.4e-7); 'fwd_dec' "
+                          "overrides the forward of transposed convs with >= fwd_dec_min_h input rows "
+                          "(FRCRN's last decoder layer); "
                           "tests/test_gpu_conv_x3.py",
     }
     if "f32" in compare:

@@ -236,6 +236,23 @@ __device__ __forceinline__ float2* fft_any(float2* a, float2* b, int P, const Ff
   }
 }
 
+// XCD-aware (frame block, utterance) of a (ceil(T / frames), B) grid: dispatch
+// round-robins consecutive workgroups over the 8 XCDs, so the two blocks that
+// write the 64-B halves of one 128-B spectrum row segment would sit on
+// different XCDs and each L2 would write back a partial line. The bijective
+// remap gives consecutive frame blocks of an utterance to one XCD, dispatched
+// back to back, so the halves merge in that L2 before write-back.
+__device__ __forceinline__ void xcd_frame_block(int& tb, int& b) {
+  constexpr int kXcd = 8;
+  const int total = gridDim.x * gridDim.y;
+  const int L = blockIdx.y * gridDim.x + blockIdx.x;
+  const int xcd = L % kXcd, idx = L / kXcd;
+  const int q = total / kXcd, r = total % kXcd;
+  const int t = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+  b = t / gridDim.x;
+  tb = t - b * gridDim.x;
+}
+
 __device__ __forceinline__ int reflect_index(int i, int L) {
   if (i < 0) i = -i;
   if (i >= L) i = 2 * (L - 1) - i;
@@ -322,7 +339,9 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   constexpr int N = CN, P = kPairsIP;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
   __shared__ float2 stw[N];
-  const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int t0 = tb * 2 * P;
   const float* x = a.x + (long long)b * a.L;
   for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
   // frame gather: all of a thread's loads are issued before any is used
@@ -458,7 +477,9 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) 
   const int N = CN ? CN : a.pl.N, P = CP ? CP : a.P;
   float2* A = lds;
   float2* Bf = lds + P * N;
-  const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int t0 = tb * 2 * P;
   const float* g = a.in + (long long)b * a.out_len;
   for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) {
     const int j = idx / N, n = idx - j * N;

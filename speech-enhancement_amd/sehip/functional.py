@@ -115,12 +115,17 @@ _TIMER: OpTimer | None = None
 _MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2, "bf16": 3}
 _PASSES = ("fwd", "data", "weight")
 _CONV_MATH = {p: 0 for p in _PASSES}
+# Optional override for the forward passes of transposed convs (the decoder) whose
+# input grid has at least _FWD_DEC[1] rows: key "fwd_dec" of the mode string
+# (None = follow "fwd"); min rows from "fwd_dec_min_h" or SEHIP_FWD_DEC_MIN_H.
+_FWD_DEC: list = [None, 0]
 
 
 def set_conv_math(mode: str, **passes: str) -> None:
     """set_conv_math("bf16x3") sets every pass; keyword overrides per pass
     (fwd=, data=, weight=). A mode string may also be the per-pass form
-    "fwd=bf16x3,data=f32,weight=bf16x3"."""
+    "fwd=bf16x3,data=f32,weight=bf16x3". Optional keys: fwd_dec=<mode> for the
+    forward of transposed convs with at least fwd_dec_min_h input rows."""
     spec = {}
     if "=" in mode:
         for item in mode.split(","):
@@ -129,13 +134,19 @@ def set_conv_math(mode: str, **passes: str) -> None:
     else:
         spec = {p: mode for p in _PASSES}
     spec.update(passes)
+    dec = spec.pop("fwd_dec", None)
+    dec_h = int(spec.pop("fwd_dec_min_h", os.environ.get("SEHIP_FWD_DEC_MIN_H", 0)))
     for k, v in spec.items():
         if k not in _PASSES:
             raise ValueError(f"conv pass must be one of {_PASSES} (got {k!r})")
         if v not in _MATH_CODES:
             raise ValueError(f"conv math must be one of {sorted(_MATH_CODES)} (got {v!r})")
+    if dec is not None and dec not in _MATH_CODES:
+        raise ValueError(f"conv math must be one of {sorted(_MATH_CODES)} (got {dec!r})")
     for k, v in spec.items():
         _CONV_MATH[k] = _MATH_CODES[v]
+    _FWD_DEC[0] = None if dec is None else _MATH_CODES[dec]
+    _FWD_DEC[1] = dec_h
 
 
 # Default: three-way split (fp32-class) forward, two-way split data- and
@@ -146,7 +157,13 @@ def set_conv_math(mode: str, **passes: str) -> None:
 # the ill-conditioned CBN parameter gradients past the per-tensor gate, while
 # bf16x6 (5.5e-7 per conv, below the fp32 MFMA path's 6.4e-7) keeps them there
 # (median 6.0e-5, worst 0.59).
-DEFAULT_CONV_MATH = "fwd=bf16x6,data=bf16x3,weight=bf16x3"
+# The one exception is the last decoder layer's forward (input grid >= 158 rows:
+# FRCRN's dec5, 40 % of the forward FLOPs), whose output reaches the mask without
+# passing another CBN's statistics: bf16x3 there keeps every gradient inside its
+# gate (worst 0.52 of it, median 7.9e-5; bf16x3 from 77 rows on puts one CCBAM
+# CBN Wri past it) and the enhanced wav at 5.9e-6 of the oracle (1e-4 bar), for
+# +4.5 % utt/s (tools/gpu_fwd_dec.sh: 542.8 vs 519.3).
+DEFAULT_CONV_MATH = "fwd=bf16x6,data=bf16x3,weight=bf16x3,fwd_dec=bf16x3,fwd_dec_min_h=158"
 set_conv_math(os.environ.get("SEHIP_CONV_MATH", DEFAULT_CONV_MATH))
 
 
@@ -154,9 +171,18 @@ def get_conv_math() -> str:
     """The current mode: one name when every pass agrees, else the per-pass form."""
     names = {v: k for k, v in _MATH_CODES.items()}
     modes = [names[_CONV_MATH[p]] for p in _PASSES]
+    if _FWD_DEC[0] is not None:
+        return ",".join(f"{p}={m}" for p, m in zip(_PASSES, modes)) + \
+            f",fwd_dec={names[_FWD_DEC[0]]},fwd_dec_min_h={_FWD_DEC[1]}"
     if len(set(modes)) == 1:
         return modes[0]
     return ",".join(f"{p}={m}" for p, m in zip(_PASSES, modes))
+
+
+def _pass_math(pass_name, d) -> int:
+    if pass_name == "fwd" and _FWD_DEC[0] is not None and d.transposed and d.in_h >= _FWD_DEC[1]:
+        return _FWD_DEC[0]
+    return _CONV_MATH[pass_name]
 
 
 def _gemm_tag(pass_name, d):
@@ -170,12 +196,12 @@ def _gemm_tag(pass_name, d):
         kind = "f32" if kind == "bf16x6" else kind
         return f"conv_wgrad_{kind}"
     n = d.out_channels if pass_name == "fwd" else d.in_channels
-    kind = "smalln" if n <= 16 else (names[_CONV_MATH[pass_name]] if n > 64 else "f32")
+    kind = "smalln" if n <= 16 else (names[_pass_math(pass_name, d)] if n > 64 else "f32")
     return f"conv_{pass_name}_{kind}"
 
 
 def _with_math(d, pass_name):
-    d.math = _CONV_MATH[pass_name]
+    d.math = _pass_math(pass_name, d)
     return N.ctypes.byref(d)
 
 
