@@ -412,8 +412,9 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
   const int N = CN ? CN : a.pl.N, P = CP ? CP : a.P, half = N / 2 + 1;
   float2* A = lds;
   float2* Bf = lds + P * N;
-  const int b = blockIdx.y;
-  const int s0 = a.offset + blockIdx.x * a.FT * a.hop;
+  int sb, b;
+  xcd_frame_block(sb, b);   // neighbouring sample tiles read the two halves of a row line
+  const int s0 = a.offset + sb * a.FT * a.hop;
   const int s1 = min(s0 + a.FT * a.hop, a.offset + a.out_len);
   const int t_lo = max(0, ceil_div_i(s0 - a.win + 1, a.hop));
   const int t_hi = min(a.T - 1, floor_div(s1 - 1, a.hop));
