@@ -17,6 +17,8 @@
 // is written exactly once, coalesced, with no atomics and no frame buffer.
 #include "common.hpp"
 
+#include <cstdlib>
+
 #include <algorithm>
 #include <cmath>
 
@@ -333,10 +335,14 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
 
 // ConvSTFT with the in-place FFT: kPairsIP frame pairs per block in one LDS
 // buffer (compiled plans only). grid (ceil(T / 2P), B)
-constexpr int kPairsIP = 8;
-template <int CN>
+// 4 pairs (8 frames, 25 KB of LDS, 6 blocks per CU) measured fastest at the FRCRN
+// bench shape: 36.9 us per launch vs 46.9 (8 pairs), 40.0 (2), 89.8 (16)
+// (tools/stft_micro.py; the XCD-aware block order merges the 32-B row segments
+// of neighbouring blocks in one L2)
+constexpr int kPairsIP = 4;
+template <int CN, int P = kPairsIP>
 __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a) {
-  constexpr int N = CN, P = kPairsIP;
+  constexpr int N = CN;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
   __shared__ float2 stw[N];
   int tb, b;
@@ -604,15 +610,31 @@ extern "C" int se_stft_fwd(const float* x, float* out0, float* out1, int B, int 
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
   if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
-    // in-place FFT, 8 frame pairs per block (static LDS <= 45 KB)
-    const dim3 grid(se::ceil_div(T, 2 * kPairsIP), B);
+    // in-place FFT, kPairsIP frame pairs per block (static LDS <= 25 KB at the default)
+    // frame pairs per block: kPairsIP, or SEHIP_STFT_IP_PAIRS = 2 / 4 / 8 / 16 (A/B knob)
+    static const int ip_pairs = [] {
+      const char* e = std::getenv("SEHIP_STFT_IP_PAIRS");
+      const int v = e ? std::atoi(e) : kPairsIP;
+      return (v == 2 || v == 4 || v == 8 || v == 16) ? v : kPairsIP;
+    }();
+    const int P = ip_pairs;
+    const dim3 grid(se::ceil_div(T, 2 * P), B);
+    hipStream_t st = se::as_stream(stream);
+#define SE_STFT_IP(NF)                                                                              \
+  do {                                                                                              \
+    if (P == 2) hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 2>), grid, dim3(kThreads), 0, st, a);    \
+    else if (P == 4) hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 4>), grid, dim3(kThreads), 0, st, a); \
+    else if (P == 16) hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 16>), grid, dim3(kThreads), 0, st, a); \
+    else hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 8>), grid, dim3(kThreads), 0, st, a);           \
+  } while (0)
     switch (nfft) {
-      case 640: hipLaunchKernelGGL(stft_fwd_ip_kernel<640>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
-      case 512: hipLaunchKernelGGL(stft_fwd_ip_kernel<512>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
-      case 400: hipLaunchKernelGGL(stft_fwd_ip_kernel<400>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
-      case 320: hipLaunchKernelGGL(stft_fwd_ip_kernel<320>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
-      default: hipLaunchKernelGGL(stft_fwd_ip_kernel<256>, grid, dim3(kThreads), 0, se::as_stream(stream), a); break;
+      case 640: SE_STFT_IP(640); break;
+      case 512: SE_STFT_IP(512); break;
+      case 400: SE_STFT_IP(400); break;
+      case 320: SE_STFT_IP(320); break;
+      default: SE_STFT_IP(256); break;
     }
+#undef SE_STFT_IP
     SE_LAUNCH_CHECK();
     return SE_OK;
   }

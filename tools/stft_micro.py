@@ -1,0 +1,28 @@
+"""ConvSTFT / ConviSTFT fwd+bwd at the FRCRN bench shape (B=64, 4 s, 320/160/640):
+per-launch time over a burst of back-to-back launches and GB/s of the algorithmic
+bytes (wav read once + spectrum written once). SEHIP_STFT_IP_PAIRS picks the
+in-place kernel's frame pairs per block (A/B)."""
+import os, sys
+import torch
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "speech-enhancement_amd"))
+from sehip.conv_stft import ConvSTFT, ConviSTFT  # noqa: E402
+
+dev = torch.device("cuda")
+B, L = 64, 64000
+x = torch.randn(B, 1, L, device=dev) * 0.3
+st, ist = ConvSTFT(320, 160, 640).to(dev), ConviSTFT(320, 160, 640).to(dev)
+with torch.no_grad():
+    spec = st(x)
+    nbytes = 4 * (x.numel() + spec.numel())
+    for name, f in (("stft_fwd", lambda: st(x)), ("istft_fwd", lambda: ist(spec))):
+        for _ in range(5):
+            f()
+        torch.cuda.synchronize()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(50):
+            f()
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / 50
+        print(f"P={os.environ.get('SEHIP_STFT_IP_PAIRS', '8')} {name:9s} {ms * 1e3:7.1f} us  {nbytes / ms / 1e6:7.1f} GB/s", flush=True)
