@@ -30,6 +30,9 @@ def _workspace(nbytes: int, device) -> torch.Tensor:
 # optimizer read the gradients).
 _DEFER: set | None = None
 _DEFER_STREAMS: dict = {}
+# every side stream the path launches on (deferred weight-grads, CCBAM gates): the
+# OpTimer marks calls on them, whose event spans share the CUs with the main stream
+SIDE_STREAMS: list = []
 
 
 @contextlib.contextmanager
@@ -61,6 +64,7 @@ def _wgrad_stream(*inputs):
     side = _DEFER_STREAMS.get(dev)
     if side is None:
         side = _DEFER_STREAMS[dev] = torch.cuda.Stream(dev)
+        SIDE_STREAMS.append(side)
     side.wait_stream(torch.cuda.current_stream(dev))
     for t in inputs:
         if t is not None:
@@ -86,7 +90,8 @@ class OpTimer:
     def end(self, tag, start, flops=0.0, nbytes=0.0):
         ev = torch.cuda.Event(enable_timing=True)
         ev.record()
-        side = torch.cuda.current_stream() != torch.cuda.default_stream()
+        cur = torch.cuda.current_stream()
+        side = any(cur == t for t in SIDE_STREAMS)
         self.records.append((tag, start, ev, float(flops), float(nbytes), side))
 
     def summary(self):

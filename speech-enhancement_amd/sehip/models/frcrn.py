@@ -27,7 +27,10 @@ _SIDE_STREAMS: dict = {}
 def _side_stream(dev):
     s = _SIDE_STREAMS.get(dev)
     if s is None:
-        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
+        # SEHIP_CCBAM_PRIO: HIP stream priority of the CCBAM side stream (0 = default,
+        # negative = higher; see sehip.train.train_step)
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev, priority=int(os.environ.get("SEHIP_CCBAM_PRIO", "0")))
+        F.SIDE_STREAMS.append(s)
     return s
 
 
@@ -148,7 +151,7 @@ class Decoder(nn.Module):
         """Start the six CCBAM skip gates (they depend only on the encoder outputs) on a side
         HIP stream, so they run beside the latency-bound LSTM recurrence, which occupies half
         the CUs; autograd runs their backward on the same side stream, beside the LSTM's BPTT.
-        Returns (gated skips in decoder order, side stream), or None to run them inline: off
+        Returns (gated skips in decoder order, their ready events), or None to run them inline: off
         the GPU, with SEHIP_OVERLAP=0, or under DDP (its gradient-ready hooks would see the
         CCBAM parameter gradients on the side stream)."""
         if not _overlap_ok(encoder_outputs):
@@ -156,23 +159,29 @@ class Decoder(nn.Module):
         dev = encoder_outputs[0].device
         main, side = torch.cuda.current_stream(dev), _side_stream(dev)
         side.wait_stream(main)
-        gated = []
+        gated, ready = [], []
         with torch.cuda.stream(side):
             for attention, skip in zip(self.skip_connection_attention_layers, reversed(encoder_outputs)):
                 skip.record_stream(side)
                 gated.append(attention(skip))
-        return gated, side
+                ev = torch.cuda.Event()
+                ev.record(side)
+                ready.append(ev)   # the decoder waits per gate, not for all six
+        return gated, ready
 
     def forward(self, x, encoder_outputs, attended=None):
-        if attended is not None:   # gated on the side stream (attend_skips): join it here
-            gated, side = attended
+        if attended is not None:   # gated on the side stream (attend_skips)
+            gated, ready = (list(reversed(t)) for t in attended)   # popped like encoder_outputs
             main = torch.cuda.current_stream(x.device)
-            main.wait_stream(side)
-            for g in gated:
-                g.record_stream(main)
-            gated = list(reversed(gated))   # popped from the end like encoder_outputs
         for attention, layer in zip(self.skip_connection_attention_layers, self.layers):
-            skip = gated.pop() if attended is not None else attention(encoder_outputs.pop())
+            if attended is not None:
+                # join the side stream at this gate only: the later (larger) gates are still
+                # running beside this decoder layer
+                main.wait_event(ready.pop())
+                skip = gated.pop()
+                skip.record_stream(main)
+            else:
+                skip = attention(encoder_outputs.pop())
             # frcrn.py:95-99: x[..., :-1] if wider, F.pad(x, (0, 0, 0, 1)) if shorter, then
             # complex_concat([x, skip]): folded into the convT's GEMMs (se_conv2d_*_joined);
             # modes without a joined kernel materialise it in one pass (se_complex_join)
