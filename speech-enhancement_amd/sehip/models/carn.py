@@ -1,8 +1,10 @@
 """CARN / GCARN (drop-in for models/_2104_05267_carn.py).
 
-A real-valued conv U-Net over stacked re/im: only its spectral front and back
-end (ConvSTFT / ConviSTFT) belong to the complex stack and run on HIP
-kernels; the real convs, attention gates and LSTM are PyTorch device ops.
+A real-valued conv U-Net over stacked re/im. The spectral front and back end
+(ConvSTFT / ConviSTFT) and every real conv / transposed conv (encoder, GLU
+gates, decoder, attention gates) run on the HIP kernels (the real-weight form
+of the conv GEMMs, complex_nn.real_conv2d); BatchNorm, PReLU and the 512-wide
+LSTM are PyTorch device ops.
 """
 from __future__ import annotations
 
@@ -10,7 +12,13 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as TF
 
+from ..complex_nn import real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
+
+
+def _conv(m: nn.Module, x):
+    """A plain nn.Conv2d / nn.ConvTranspose2d on the HIP GEMM; any other module as is."""
+    return real_conv2d(m, x) if isinstance(m, (nn.Conv2d, nn.ConvTranspose2d)) else m(x)
 
 
 class ConvGLU(nn.Module):
@@ -22,7 +30,7 @@ class ConvGLU(nn.Module):
         self.conv2 = nn.Conv2d(in_channels, out_channels, kernel_size, **kwargs)
 
     def forward(self, x):
-        return self.conv1(x) * torch.sigmoid(self.conv2(x))
+        return _conv(self.conv1, x) * torch.sigmoid(_conv(self.conv2, x))
 
 
 class DeConvGLU(nn.Module):
@@ -34,7 +42,7 @@ class DeConvGLU(nn.Module):
         self.conv_transpose2 = nn.ConvTranspose2d(in_channels, out_channels, kernel_size, **kwargs)
 
     def forward(self, x):
-        return self.conv_transpose1(x) * torch.sigmoid(self.conv_transpose2(x))
+        return _conv(self.conv_transpose1, x) * torch.sigmoid(_conv(self.conv_transpose2, x))
 
 
 class ConvBlock(nn.Module):
@@ -48,7 +56,7 @@ class ConvBlock(nn.Module):
         self.act = nn.PReLU() if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(self.conv(x)))
+        return self.act(self.norm(_conv(self.conv, x)))
 
 
 class ConvTransposeBlock(nn.Module):
@@ -62,7 +70,7 @@ class ConvTransposeBlock(nn.Module):
         self.act = nn.PReLU() if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(self.conv_transposed(x)))
+        return self.act(self.norm(_conv(self.conv_transposed, x)))
 
 
 class Attention(nn.Module):
@@ -75,7 +83,7 @@ class Attention(nn.Module):
         self.conv3 = nn.Conv2d(in_channels * 2, in_channels, kernel_size=3, padding=1, bias=False)
 
     def forward(self, x_u, x_c):
-        gate = torch.sigmoid(self.conv3(torch.sigmoid(self.conv1(x_u) + self.conv2(x_c))))
+        gate = torch.sigmoid(_conv(self.conv3, torch.sigmoid(_conv(self.conv1, x_u) + _conv(self.conv2, x_c))))
         return gate * x_c
 
 

@@ -1,12 +1,14 @@
 """CRN (drop-in for models/_1809_01405_crn.py): magnitude-domain conv-LSTM
-that exercises the mag/phase API of ConvSTFT / ConviSTFT (HIP kernels); the
-real conv / LSTM body is PyTorch device ops."""
+that exercises the mag/phase API of ConvSTFT / ConviSTFT (HIP kernels); its
+real convs run on the real-weight form of the HIP conv GEMMs (real_conv2d), the
+BatchNorm / ELU / LSTM body on PyTorch device ops."""
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
 import torch.nn.functional as TF
 
+from ..complex_nn import real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -22,7 +24,7 @@ class ConvBlock(nn.Module):
         self.act = nn.ELU(alpha) if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(self.conv(x)[:, :, :-self.padding[0], :]))
+        return self.act(self.norm(real_conv2d(self.conv, x)[:, :, :-self.padding[0], :]))
 
 
 class ConvTransposeBlock(nn.Module):
@@ -37,7 +39,7 @@ class ConvTransposeBlock(nn.Module):
         self.act = nn.ELU(alpha) if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(self.conv_transposed(x)[:, :, :-1, :]))
+        return self.act(self.norm(real_conv2d(self.conv_transposed, x)[:, :, :-1, :]))
 
 
 class Encoder(nn.Module):

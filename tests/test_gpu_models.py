@@ -221,3 +221,28 @@ def test_frcrn_4s_vs_oracle(gpu_device):
         s, w = m(torch.from_numpy(noisy).cuda())
     assert rel_l2(s.cpu().numpy(), so.numpy()) < TOL
     assert rel_l2(w.cpu().numpy(), wo.numpy()) < TOL
+
+
+@pytest.mark.parametrize("i", [3, 5])
+def test_real_conv_models_backward_vs_oracle(i, gpu_device):
+    """CARN / CRN run their real convs on the HIP conv GEMMs (real_conv2d): the train-mode
+    forward + backward against the CPU oracle on the golden input (loss = <wav, r>)."""
+    from oracle import models as O
+    name, ctor = _models()[i]
+    octor = {3: lambda: O.CARN(320, 160, 512), 5: lambda: O.CRN(320, 160, 320)}[i]
+    g = golden(f"model_{name}")
+    x = torch.from_numpy(g["x"])
+    m = paramfill.fill_(ctor(), seed=20 + i).cuda().train()
+    mo = paramfill.fill_(octor(), seed=20 + i).train()
+    _, wav = m(x.cuda())
+    _, wo = mo(x)
+    r = torch.randn(wo.shape, generator=torch.Generator().manual_seed(3))
+    (wav * r.cuda()).sum().backward()
+    (wo * r).sum().backward()
+    assert rel_l2(wav.detach().cpu().numpy(), wo.detach().numpy()) < TOL
+    names = [n for n, p in mo.named_parameters() if p.grad is not None]
+    go = dict(mo.named_parameters())
+    gh = dict(m.named_parameters())
+    a = torch.cat([gh[n].grad.detach().cpu().flatten() for n in names])
+    b = torch.cat([go[n].grad.flatten() for n in names])
+    assert ((a - b).norm() / b.norm()).item() < 1e-3
