@@ -120,3 +120,50 @@ def test_input_pad_folded_into_conv(input_pad, gpu_device):
     rp = dict(ref.named_parameters())
     for n, p in mod.named_parameters():
         assert rel_l2(p.grad.cpu().numpy(), rp[n].grad.numpy()) < 1e-5, n
+
+
+# real-weight (nn.Conv2d / nn.ConvTranspose2d) geometries of CRN / CARN (real_conv2d),
+# against torch's CPU autograd in fp32; output_padding in either dim
+REAL_CASES = [
+    ("crn_enc", False, 16, 32, (2, 3), dict(stride=(1, 2), padding=(1, 0)), (2, 16, 6, 39)),
+    ("crn_dec3", True, 64, 16, (2, 3), dict(stride=(1, 2), output_padding=(0, 1)), (2, 64, 6, 19)),
+    ("crn_dec1", True, 256, 64, (2, 3), dict(stride=(1, 2)), (2, 256, 5, 9)),
+    ("carn_dec", True, 64, 32, (1, 3), dict(stride=(2, 1), padding=(0, 1), output_padding=(1, 0)), (2, 64, 9, 11)),
+    ("carn_att", False, 32, 64, (3, 3), dict(padding=(1, 1)), (2, 32, 17, 11)),
+    # CRN's decoder at the golden 1 s input (T = 101 frames)
+    ("crn_dec2_full", True, 128, 32, (2, 3), dict(stride=(1, 2)), (2, 128, 101, 19)),
+    ("crn_dec3_full", True, 64, 16, (2, 3), dict(stride=(1, 2), output_padding=(0, 1)), (2, 64, 101, 39)),
+    ("crn_dec4_full", True, 32, 1, (2, 3), dict(stride=(1, 2)), (2, 32, 101, 80)),
+    ("crn_enc1_full", False, 16, 32, (2, 3), dict(stride=(1, 2), padding=(1, 0)), (2, 16, 101, 80)),
+]
+
+
+@pytest.mark.parametrize("case", REAL_CASES, ids=[c[0] for c in REAL_CASES])
+def test_real_conv_geometries_vs_torch(case, gpu_device):
+    from sehip import functional as F
+    from sehip.complex_nn import real_conv2d
+    name, tr, cin, cout, k, kw, shape = case
+    cls = torch.nn.ConvTranspose2d if tr else torch.nn.Conv2d
+    torch.manual_seed(7)
+    m = cls(cin, cout, k, bias=True, **kw)
+    x = torch.randn(shape)
+    xo = x.clone().requires_grad_(True)
+    yo = m(xo)
+    gy = torch.randn(yo.shape)
+    yo.backward(gy)
+    prev = F.get_conv_math()
+    try:
+        F.set_conv_math("f32")
+        mc = cls(cin, cout, k, bias=True, **kw)
+        mc.load_state_dict(m.state_dict())
+        mc = mc.cuda()
+        xg = x.cuda().requires_grad_(True)
+        y = real_conv2d(mc, xg)
+        y.backward(gy.cuda())
+    finally:
+        F.set_conv_math(prev)
+    assert y.shape == yo.shape
+    assert rel_l2(y.detach().cpu().numpy(), yo.detach().numpy()) < 1e-5, (name, "y")
+    assert rel_l2(xg.grad.cpu().numpy(), xo.grad.numpy()) < 1e-5, (name, "dx")
+    assert rel_l2(mc.weight.grad.cpu().numpy(), m.weight.grad.numpy()) < 1e-5, (name, "dw")
+    assert rel_l2(mc.bias.grad.cpu().numpy(), m.bias.grad.numpy()) < 1e-5, (name, "db")

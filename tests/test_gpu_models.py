@@ -225,24 +225,35 @@ def test_frcrn_4s_vs_oracle(gpu_device):
 
 @pytest.mark.parametrize("i", [3, 5])
 def test_real_conv_models_backward_vs_oracle(i, gpu_device):
-    """CARN / CRN run their real convs on the HIP conv GEMMs (real_conv2d): the train-mode
-    forward + backward against the CPU oracle on the golden input (loss = <wav, r>)."""
+    """CARN / CRN run their real convs on the HIP conv GEMMs (real_conv2d): train-mode
+    forward + backward against the CPU oracle on the golden input (loss = <wav, r>).
+    Their BatchNorm2d / PReLU / ELU / LSTM stay PyTorch ops, whose GPU (MIOpen) backward
+    is itself not CPU-exact (CRN: nn.BatchNorm2d's input gradient at decoder layer 2
+    is 4.5e-4 off the CPU, tools/crn_act_diag.py), so the gradient gate is 3x the
+    error of the oracle's own modules run on the GPU, floored at 1e-3."""
     from oracle import models as O
     name, ctor = _models()[i]
     octor = {3: lambda: O.CARN(320, 160, 512), 5: lambda: O.CRN(320, 160, 320)}[i]
     g = golden(f"model_{name}")
     x = torch.from_numpy(g["x"])
-    m = paramfill.fill_(ctor(), seed=20 + i).cuda().train()
-    mo = paramfill.fill_(octor(), seed=20 + i).train()
-    _, wav = m(x.cuda())
-    _, wo = mo(x)
-    r = torch.randn(wo.shape, generator=torch.Generator().manual_seed(3))
-    (wav * r.cuda()).sum().backward()
-    (wo * r).sum().backward()
-    assert rel_l2(wav.detach().cpu().numpy(), wo.detach().numpy()) < TOL
-    names = [n for n, p in mo.named_parameters() if p.grad is not None]
-    go = dict(mo.named_parameters())
-    gh = dict(m.named_parameters())
-    a = torch.cat([gh[n].grad.detach().cpu().flatten() for n in names])
-    b = torch.cat([go[n].grad.flatten() for n in names])
-    assert ((a - b).norm() / b.norm()).item() < 1e-3
+    r = None
+
+    def grads(m, dev):
+        nonlocal r
+        _, w = m(x.to(dev))
+        if r is None:
+            r = torch.randn(w.shape, generator=torch.Generator().manual_seed(3))
+        (w * r.to(dev)).sum().backward()
+        return w.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()
+                                  if p.grad is not None}
+
+    wo, go = grads(paramfill.fill_(octor(), seed=20 + i).train(), "cpu")
+    _, gt = grads(paramfill.fill_(octor(), seed=20 + i).cuda().train(), "cuda")   # torch on the GPU
+    wh, gh = grads(paramfill.fill_(ctor(), seed=20 + i).cuda().train(), "cuda")   # sehip
+    assert rel_l2(wh.numpy(), wo.numpy()) < TOL
+    names = sorted(go)
+    cat = lambda d: torch.cat([d[n].flatten() for n in names])
+    b = cat(go)
+    e_hip = ((cat(gh) - b).norm() / b.norm()).item()
+    e_torch = ((cat(gt) - b).norm() / b.norm()).item()
+    assert e_hip < max(3 * e_torch, 1e-3), (name, e_hip, e_torch)
