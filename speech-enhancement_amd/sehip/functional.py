@@ -33,6 +33,9 @@ _DEFER_STREAMS: dict = {}
 # every side stream the path launches on (deferred weight-grads, CCBAM gates): the
 # OpTimer marks calls on them, whose event spans share the CUs with the main stream
 SIDE_STREAMS: list = []
+# set by sehip.train.wrap_ddp when a hook-based torch DDP wraps the model: its
+# per-parameter gradient hooks rule out the side streams (frcrn._overlap_ok)
+DDP_HOOKS: list = [False]
 
 
 @contextlib.contextmanager

@@ -35,10 +35,11 @@ def _side_stream(dev):
 
 
 def _overlap_ok(tensors) -> bool:
+    """Side streams on: GPU tensors, SEHIP_OVERLAP != 0, and no hook-based torch DDP
+    (sehip.train.FlatDataParallel reduces after backward and keeps them)."""
     if not tensors or not tensors[0].is_cuda or os.environ.get("SEHIP_OVERLAP", "1") == "0":
         return False
-    dist = torch.distributed
-    return not (dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1)
+    return not F.DDP_HOOKS[0]
 
 
 class _CausalConvBase(nn.Module):

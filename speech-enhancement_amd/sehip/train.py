@@ -30,10 +30,10 @@ def make_optimizer(model, **overrides):
 
 def _defer_ok(model) -> bool:
     """Deferred weight-grads (functional.deferred_weight_grads) need every .grad
-    None on entry and no gradient hooks during backward: not under DDP, and
-    only on the GPU."""
-    import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    None on entry and no gradient hooks during backward: not under hook-based DDP
+    (FlatDataParallel reduces after backward and is fine), and only on the GPU."""
+    from torch.nn.parallel import DistributedDataParallel as DDP
+    if isinstance(model, DDP):
         return False
     p = next(model.parameters(), None)
     return p is not None and p.is_cuda and all(q.grad is None for q in model.parameters()) \
@@ -78,6 +78,7 @@ def _train_step(model, optimizer, noisy, clean, clip_norm):
     loss = SI_SNR_loss(est, target)
     with deferred_weight_grads(_defer_ok(model)):
         loss.backward()
+    finish_grads(model)
     if clip_norm:
         torch.nn.utils.clip_grad_norm_(model.parameters(), clip_norm)
     optimizer.step()
@@ -98,7 +99,8 @@ def setup_distributed(backend: str | None = None):
     else:
         device = torch.device("cpu")
     if world > 1 and not dist.is_initialized():
-        backend = backend or ("nccl" if device.type == "cuda" else "gloo")
+        # SEHIP_DIST_BACKEND: override (e.g. gloo to rehearse ranks sharing one GPU)
+        backend = backend or os.environ.get("SEHIP_DIST_BACKEND") or ("nccl" if device.type == "cuda" else "gloo")
         kw = dict(backend=backend, rank=rank, world_size=world)
         if device.type == "cuda":
             kw["device_id"] = device
@@ -106,10 +108,78 @@ def setup_distributed(backend: str | None = None):
     return rank, world, local, device
 
 
-def wrap_ddp(model, device):
+class FlatDataParallel(torch.nn.Module):
+    """Data parallelism with ONE gradient all-reduce after backward (RCCL over xGMI).
+
+    Same semantics as DistributedDataParallel's defaults: parameters and buffers
+    broadcast from rank 0 at construction, buffers (the CBN running statistics)
+    broadcast from rank 0 at every forward, gradients averaged over ranks. The
+    difference is where the reduction happens: DDP hooks every parameter's
+    gradient and all-reduces 4-MB buckets during backward, which rules out the
+    side streams of this path (the deferred weight-grads and the CCBAM gates: a
+    hook would read a gradient its side-stream kernel has not written yet). The
+    whole FRCRN gradient is 7.7 MB, a ~0.2 ms ring all-reduce against a ~120 ms
+    step, so nothing is lost by reducing it once at the end, flattened, after the
+    side streams have joined (train_step -> finish_grads)."""
+
+    def __init__(self, module, process_group=None):
+        super().__init__()
+        import torch.distributed as dist
+        self.module = module
+        self.process_group = process_group
+        self.world = dist.get_world_size(process_group)
+        self._broadcast(list(module.parameters()) + list(module.buffers()))
+
+    def _broadcast(self, tensors):
+        """Rank 0's values, one coalesced broadcast per dtype (as DDP's buffer sync)."""
+        import torch.distributed as dist
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+        by_dtype: dict = {}
+        for t in tensors:
+            by_dtype.setdefault(t.dtype, []).append(t)
+        with torch.no_grad():
+            for ts in by_dtype.values():
+                flat = _flatten_dense_tensors([t.detach() for t in ts])
+                dist.broadcast(flat, 0, group=self.process_group)
+                for t, v in zip(ts, _unflatten_dense_tensors(flat, ts)):
+                    t.copy_(v)
+
+    def forward(self, *args, **kwargs):
+        self._broadcast(list(self.module.buffers()))
+        return self.module(*args, **kwargs)
+
+    def allreduce_grads(self):
+        import torch.distributed as dist
+        from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
+        grads = [p.grad for p in self.module.parameters() if p.grad is not None]
+        if not grads:
+            return
+        flat = _flatten_dense_tensors(grads)
+        dist.all_reduce(flat, group=self.process_group)
+        flat.div_(self.world)
+        for g, r in zip(grads, _unflatten_dense_tensors(flat, grads)):
+            g.copy_(r)
+
+
+def finish_grads(model):
+    """After backward: FlatDataParallel's gradient all-reduce (a no-op otherwise)."""
+    if isinstance(model, FlatDataParallel):
+        model.allreduce_grads()
+
+
+def wrap_ddp(model, device, mode: str | None = None):
+    """Data-parallel wrapper for world > 1 (identity otherwise). mode (or SEHIP_DP):
+    "flat" (default) = FlatDataParallel, one all-reduce after backward, side streams
+    kept; "ddp" = torch DistributedDataParallel (4-MB buckets during backward, side
+    streams off)."""
     import torch.distributed as dist
     if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
         return model
+    mode = mode or os.environ.get("SEHIP_DP", "flat")
+    if mode == "flat":
+        return FlatDataParallel(model)
     from torch.nn.parallel import DistributedDataParallel as DDP
+    from . import functional as F
+    F.DDP_HOOKS[0] = True   # gradient hooks during backward: no side streams (frcrn._overlap_ok)
     ids = [device.index] if device.type == "cuda" else None
     return DDP(model, device_ids=ids, bucket_cap_mb=4, gradient_as_bucket_view=True)

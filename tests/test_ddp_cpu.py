@@ -29,23 +29,24 @@ def _shard(rank):
     return torch.from_numpy(noisy), torch.from_numpy(clean)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
     torch.set_num_threads(2)
     from oracle import models as O
-    from sehip.train import setup_distributed, wrap_ddp, train_step
+    from sehip.train import FlatDataParallel, finish_grads, setup_distributed, wrap_ddp, train_step
     r, w, _, dev = setup_distributed(backend="gloo")
     assert (r, w, dev.type) == (rank, world, "cpu")
     model = paramfill.fill_(O.FRCRN(), seed=7).train()
-    ddp = wrap_ddp(model, dev)
-    assert isinstance(ddp, torch.nn.parallel.DistributedDataParallel)
+    ddp = wrap_ddp(model, dev, mode)
+    assert isinstance(ddp, FlatDataParallel if mode == "flat" else torch.nn.parallel.DistributedDataParallel)
     noisy, clean = _shard(rank)
     # grads of one step without the optimiser update (clip disabled, lr 0)
     opt = torch.optim.SGD(ddp.parameters(), lr=0.0)
     _, wav = ddp(noisy)
     from sehip.losses import SI_SNR_loss
     SI_SNR_loss(wav, clean).backward()
+    finish_grads(ddp)
     grads = {n: p.grad.clone() for n, p in model.named_parameters()}
     torch.save({"grads": grads, "RMr": model.encoder.layers[0].norm.RMr.clone()},
                os.path.join(out_dir, f"rank{rank}.pt"))
@@ -56,9 +57,10 @@ def _worker(rank, world, port, out_dir):
     torch.distributed.destroy_process_group()
 
 
-def test_ddp_gloo_world2_grad_average(tmp_path):
+@pytest.mark.parametrize("mode", ["flat", "ddp"])
+def test_ddp_gloo_world2_grad_average(tmp_path, mode):
     world, port = 2, _free_port()
-    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
     res = [torch.load(tmp_path / f"rank{r}.pt", weights_only=True) for r in range(world)]
     # replicas agree exactly after the all-reduce
     for n in res[0]["grads"]:

@@ -26,26 +26,29 @@ def _shard(rank):
     return torch.from_numpy(noisy), torch.from_numpy(clean)
 
 
-def _worker(rank, world, port, out_dir):
+def _worker(rank, world, port, out_dir, mode):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
                       WORLD_SIZE=str(world), LOCAL_RANK="0")
     from sehip.models import FRCRN
     from sehip.losses import SI_SNR_loss
-    from sehip.train import setup_distributed, wrap_ddp
+    from sehip.train import finish_grads, setup_distributed, wrap_ddp
     _, _, _, dev = setup_distributed(backend="gloo")
     model = paramfill.fill_(FRCRN(), seed=9).to(dev).train()
-    ddp = wrap_ddp(model, dev)
+    ddp = wrap_ddp(model, dev, mode)
     noisy, clean = (t.to(dev) for t in _shard(rank))
     _, wav = ddp(noisy)
     SI_SNR_loss(wav, clean).backward()
+    finish_grads(ddp)
+    torch.cuda.synchronize()
     torch.save({n: p.grad.detach().cpu() for n, p in model.named_parameters()},
                os.path.join(out_dir, f"g{rank}.pt"))
     torch.distributed.destroy_process_group()
 
 
-def test_ddp_two_ranks_one_gpu(tmp_path, gpu_device):
+@pytest.mark.parametrize("mode", ["flat", "ddp"])
+def test_ddp_two_ranks_one_gpu(tmp_path, gpu_device, mode):
     world, port = 2, _free_port()
-    mp.spawn(_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    mp.spawn(_worker, args=(world, port, str(tmp_path), mode), nprocs=world, join=True)
     g = [torch.load(tmp_path / f"g{r}.pt", weights_only=True) for r in range(world)]
     from sehip.models import FRCRN
     from sehip.losses import SI_SNR_loss
