@@ -109,18 +109,75 @@ struct CPlan {
   int npass;
   int radix[kMaxPasses];
 };
+// Radix 8 and 10 first (640 = 8*8*10, 512 = 8*8*8, 400 = 8*10*5, 320 = 8*8*5,
+// 256 = 8*8*4): three barrier-separated passes instead of five for nfft 640.
 constexpr CPlan make_cplan(int N) {
   CPlan p{};
   int n = N;
-  const int order[4] = {4, 2, 3, 5};
-  for (int oi = 0; oi < 4; ++oi)
+  const int order[6] = {8, 10, 4, 2, 3, 5};
+  for (int oi = 0; oi < 6; ++oi)
     while (n > 1 && n % order[oi] == 0 && p.npass < kMaxPasses) { p.radix[p.npass++] = order[oi]; n /= order[oi]; }
   return p;
 }
+constexpr int kMaxRadix = 10;
+
+// 5-point DFT of (a0..a4) -> (x0..x4) (forward sign)
+__device__ __forceinline__ void dft5(float2 a0, float2 a1, float2 a2, float2 a3, float2 a4, float2 (&x)[5]) {
+  const float c1 = 0.30901699437494742410f, c2 = -0.80901699437494742410f;
+  const float s1 = 0.95105651629515357212f, s2 = 0.58778525229247312917f;
+  const float2 t1 = cadd(a1, a4), t2 = cadd(a2, a3);
+  const float2 t3 = csub(a1, a4), t4 = csub(a2, a3);
+  const float2 p1 = cadd(a0, cadd(cscale(t1, c1), cscale(t2, c2)));
+  const float2 p2 = cadd(a0, cadd(cscale(t1, c2), cscale(t2, c1)));
+  const float2 q1 = mul_mi(cadd(cscale(t3, s1), cscale(t4, s2)));
+  const float2 q2 = mul_mi(csub(cscale(t3, s2), cscale(t4, s1)));
+  x[0] = cadd(a0, cadd(t1, t2));
+  x[1] = cadd(p1, q1);
+  x[4] = csub(p1, q1);
+  x[2] = cadd(p2, q2);
+  x[3] = csub(p2, q2);
+}
 
 template <int R>
-__device__ __forceinline__ void butterfly(float2 (&v)[5], float2* dst, int d, int Ns) {
-  if constexpr (R == 2) {
+__device__ __forceinline__ void butterfly(float2 (&v)[kMaxRadix], float2* dst, int d, int Ns) {
+  if constexpr (R == 8) {
+    // X_k = E_k + W8^k O_k, X_{k+4} = E_k - W8^k O_k (E, O: 4-point DFTs of even / odd inputs)
+    const float r = 0.70710678118654752440f;
+    const float2 a0 = cadd(v[0], v[4]), a1 = csub(v[0], v[4]);
+    const float2 a2 = cadd(v[2], v[6]), a3 = mul_mi(csub(v[2], v[6]));
+    const float2 a4 = cadd(v[1], v[5]), a5 = csub(v[1], v[5]);
+    const float2 a6 = cadd(v[3], v[7]), a7 = mul_mi(csub(v[3], v[7]));
+    const float2 e0 = cadd(a0, a2), e2 = csub(a0, a2), e1 = cadd(a1, a3), e3 = csub(a1, a3);
+    const float2 o0 = cadd(a4, a6), o2 = csub(a4, a6), o1 = cadd(a5, a7), o3 = csub(a5, a7);
+    const float2 w1 = make_float2(r * (o1.x + o1.y), r * (o1.y - o1.x));     // W8^1 o1, W8 = (1 - i)/sqrt2
+    const float2 w2 = mul_mi(o2);                                            // W8^2 = -i
+    const float2 w3 = make_float2(r * (o3.y - o3.x), -r * (o3.x + o3.y));    // W8^3 = (-1 - i)/sqrt2
+    dst[d] = cadd(e0, o0);
+    dst[d + 4 * Ns] = csub(e0, o0);
+    dst[d + Ns] = cadd(e1, w1);
+    dst[d + 5 * Ns] = csub(e1, w1);
+    dst[d + 2 * Ns] = cadd(e2, w2);
+    dst[d + 6 * Ns] = csub(e2, w2);
+    dst[d + 3 * Ns] = cadd(e3, w3);
+    dst[d + 7 * Ns] = csub(e3, w3);
+  } else if constexpr (R == 10) {
+    // X_k = E_{k mod 5} + W10^k O_{k mod 5} (E, O: 5-point DFTs of even / odd inputs);
+    // W10^5 = -1, so X_{k+5} = E_k - W10^k O_k
+    float2 E[5], O[5];
+    dft5(v[0], v[2], v[4], v[6], v[8], E);
+    dft5(v[1], v[3], v[5], v[7], v[9], O);
+    const float2 W[5] = {make_float2(1.f, 0.f),
+                         make_float2(0.80901699437494742410f, -0.58778525229247312917f),
+                         make_float2(0.30901699437494742410f, -0.95105651629515357212f),
+                         make_float2(-0.30901699437494742410f, -0.95105651629515357212f),
+                         make_float2(-0.80901699437494742410f, -0.58778525229247312917f)};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float2 t = k ? cmul(O[k], W[k]) : O[0];
+      dst[d + k * Ns] = cadd(E[k], t);
+      dst[d + (k + 5) * Ns] = csub(E[k], t);
+    }
+  } else if constexpr (R == 2) {
     dst[d] = cadd(v[0], v[1]);
     dst[d + Ns] = csub(v[0], v[1]);
   } else if constexpr (R == 4) {
@@ -167,7 +224,7 @@ __device__ float2* fft_pass(float2* a, float2* b, const float2* __restrict__ tw)
       const float2* src = a + pr * N;
       float2* dst = b + pr * N;
       const int k = j % NS;
-      float2 v[5];
+      float2 v[kMaxRadix];
 #pragma unroll
       for (int q = 0; q < R; ++q) v[q] = src[j + q * nbf];
       if constexpr (NS > 1) {
@@ -191,7 +248,7 @@ __device__ void fft_pass_ip(float2* a, const float2* __restrict__ tw) {
   if constexpr (PS < pl.npass) {
     constexpr int R = pl.radix[PS], nbf = N / R, tstep = N / (NS * R);
     constexpr int ITER = (P * nbf + kThreads - 1) / kThreads;
-    float2 v[ITER][5];
+    float2 v[ITER][kMaxRadix];
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int idx = threadIdx.x + it * kThreads;
