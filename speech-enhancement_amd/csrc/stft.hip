@@ -445,13 +445,15 @@ struct IstftArgs {
 };
 
 // Sums of v[f][n] over even / odd n < win for every frame f (one wave per frame).
-__device__ void parity_sums(const float2* V, int P, int N, int win, float* sums /*[2P][2]*/) {
+// ysign scales the odd frames (the .y lanes), so a conjugate needs no separate pass.
+__device__ void parity_sums(const float2* V, int P, int N, int win, float* sums /*[2P][2]*/,
+                            float ysign = 1.f) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   for (int f = wave; f < 2 * P; f += nw) {
     const float2* v = V + (f >> 1) * N;
     float se = 0.f, so = 0.f;
     for (int n = lane; n < win; n += 64) {
-      const float val = (f & 1) ? v[n].y : v[n].x;
+      const float val = (f & 1) ? ysign * v[n].y : v[n].x;
       if (n & 1) so += val; else se += val;
     }
     se = se::wave_sum(se);
@@ -504,17 +506,15 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
   }
   __syncthreads();
   float2* R = fft_any<CN, CP>(A, Bf, P, a.pl, a.tw);
-  // z = conj(R): z_a = R.x, z_b = -R.y. Fold the sign into the sums/application.
-  for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) R[idx].y = -R[idx].y;
-  __syncthreads();
-  parity_sums(R, P, N, a.win, sums);
+  // z = conj(R): z_a = R.x, z_b = -R.y; the sign is folded into the sums and the frames.
+  parity_sums(R, P, N, a.win, sums, -1.f);
   const float ah = 0.5f * N, inv_a = 1.f / ah;
   const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
   float* fr = reinterpret_cast<float*>(R == A ? Bf : A);   // [2P][win] frames
   for (int idx = threadIdx.x; idx < 2 * P * a.win; idx += blockDim.x) {
     const int f = idx / a.win, n = idx - f * a.win;
     const float2 z = R[(f >> 1) * N + n];
-    const float v = (f & 1) ? z.y : z.x;
+    const float v = (f & 1) ? -z.y : z.x;
     fr[idx] = a.window[n] * apply_g(v, n, sums[2 * f], sums[2 * f + 1], inv_a, ce, co);
   }
   __syncthreads();
