@@ -533,6 +533,82 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
   }
 }
 
+// ConviSTFT forward on the in-place FFT (compiled plans): one P*N float2 LDS
+// buffer holds the packed spectra, their FFT and then the windowed synthesis
+// frames (written over it through registers), so a block needs ~half the LDS of
+// istft_fwd_kernel and twice as many blocks share a CU. grid (ceil(out_len / (FT*hop)), B)
+template <int CN, int P>
+__global__ void __launch_bounds__(kThreads) istft_fwd_ip_kernel(const IstftArgs a) {
+  constexpr int N = CN, half = N / 2 + 1;
+  __shared__ __attribute__((aligned(16))) float2 A[P * N];
+  __shared__ float2 stw[N];
+  __shared__ float sums[4 * P];
+  int sb, b;
+  xcd_frame_block(sb, b);
+  const int s0 = a.offset + sb * a.FT * a.hop;
+  const int s1 = min(s0 + a.FT * a.hop, a.offset + a.out_len);
+  const int t_lo = max(0, ceil_div_i(s0 - a.win + 1, a.hop));
+  const int t_hi = min(a.T - 1, floor_div(s1 - 1, a.hop));
+  const float* spec = a.in + (long long)b * 2 * half * a.T;
+  for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
+  // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
+  for (int idx = threadIdx.x; idx < half * P; idx += kThreads) {
+    const int k = idx / P, j = idx - k * P;
+    const int ta = t_lo + 2 * j, tb = ta + 1;
+    float2 xa = make_float2(0.f, 0.f), xb = xa;
+    if (ta <= t_hi) xa = make_float2(spec[(long long)k * a.T + ta], spec[(long long)(half + k) * a.T + ta]);
+    if (tb <= t_hi) xb = make_float2(spec[(long long)k * a.T + tb], spec[(long long)(half + k) * a.T + tb]);
+    float2* c = A + j * N;
+    if (k == 0 || k == N / 2) {
+      c[k] = make_float2(xa.x, -xb.x);
+    } else {
+      c[k] = make_float2(0.5f * (xa.x - xb.y), -0.5f * (xa.y + xb.x));
+      c[N - k] = make_float2(0.5f * (xa.x + xb.y), 0.5f * (xa.y - xb.x));
+    }
+  }
+  __syncthreads();
+  fft_pass_ip<N, P, 0, 1>(A, stw);
+  // z = conj(A): z_a = A.x, z_b = -A.y
+  parity_sums(A, P, N, a.win, sums, -1.f);
+  const float ah = 0.5f * N, inv_a = 1.f / ah;
+  const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
+  // frames fr[f][n] (n < win) over the same buffer: read all, barrier, write all
+  constexpr int IT = (2 * P * N + kThreads - 1) / kThreads;
+  float v[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    const int f = idx / N, n = idx - f * N;
+    v[it] = 0.f;
+    if (idx < 2 * P * N && n < a.win) {
+      const float2 z = A[(f >> 1) * N + n];
+      v[it] = a.window[n] * apply_g((f & 1) ? -z.y : z.x, n, sums[2 * f], sums[2 * f + 1], inv_a, ce, co);
+    }
+  }
+  __syncthreads();
+  float* fr = reinterpret_cast<float*>(A);   // [2P][win]
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    const int f = idx / N, n = idx - f * N;
+    if (idx < 2 * P * N && n < a.win) fr[f * a.win + n] = v[it];
+  }
+  __syncthreads();
+  float* out = a.out + (long long)b * a.out_len;
+  for (int s = s0 + threadIdx.x; s < s1; s += kThreads) {
+    const int tb0 = max(t_lo, ceil_div_i(s - a.win + 1, a.hop));
+    const int tb1 = min(t_hi, floor_div(s, a.hop));
+    float acc = 0.f, cf = 0.f;
+    for (int t = tb0; t <= tb1; ++t) {
+      const int n = s - t * a.hop;
+      const float w = a.window[n];
+      acc += fr[(t - t_lo) * a.win + n];
+      cf += w * w;
+    }
+    out[s - a.offset] = acc / (cf + 1e-8f);
+  }
+}
+
 // Adjoint of istft_fwd. grid (ceil(T / 2P), B)
 template <int CN, int CP>
 __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) {
@@ -724,6 +800,37 @@ extern "C" int se_istft_fwd(const float* spec, float* out, int B, int T, int win
   if (!spec || !out || !window || !twiddle) return SE_E_ARG;
   if (out_len == 0) return SE_OK;
   a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle;
+  if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
+    // in-place FFT, SEHIP_ISTFT_IP_PAIRS = 4 / 8 frame pairs per block (A/B knob)
+    static const int ip_pairs = [] {
+      const char* e = std::getenv("SEHIP_ISTFT_IP_PAIRS");
+      const int v = e ? std::atoi(e) : kPairsIP;
+      return (v == 4 || v == 8) ? v : kPairsIP;
+    }();
+    const int P = ip_pairs;
+    a.P = P;
+    a.FT = 2 * P - 1 - (win - 1) / hop;
+    if (a.FT >= 1) {
+      const dim3 grid(se::ceil_div(out_len, a.FT * hop), B);
+      hipStream_t st = se::as_stream(stream);
+#define SE_ISTFT_IP(NF)                                                                             \
+  do {                                                                                              \
+    if (P == 8) hipLaunchKernelGGL((istft_fwd_ip_kernel<NF, 8>), grid, dim3(kThreads), 0, st, a);   \
+    else hipLaunchKernelGGL((istft_fwd_ip_kernel<NF, 4>), grid, dim3(kThreads), 0, st, a);          \
+  } while (0)
+      switch (nfft) {
+        case 640: SE_ISTFT_IP(640); break;
+        case 512: SE_ISTFT_IP(512); break;
+        case 400: SE_ISTFT_IP(400); break;
+        case 320: SE_ISTFT_IP(320); break;
+        default: SE_ISTFT_IP(256); break;
+      }
+#undef SE_ISTFT_IP
+      SE_LAUNCH_CHECK();
+      return SE_OK;
+    }
+    istft_setup(B, T, win, hop, nfft, offset, out_len, a);   // FT too small at this P: generic kernel
+  }
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
   SE_STFT_DISPATCH(istft_fwd_kernel, nfft, a.P, dim3(se::ceil_div(out_len, a.FT * hop), B), shm,
                    se::as_stream(stream), a);
