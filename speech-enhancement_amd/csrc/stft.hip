@@ -663,6 +663,61 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) 
   unpack_store<CN, CP>(Z, P, N, t0, a.T, b, a.out, nullptr, 0);
 }
 
+// istft_bwd on the in-place FFT (compiled plans): one P*N float2 LDS buffer,
+// static LDS, twice the resident blocks of the ping-pong form. grid (ceil(T / 2P), B)
+template <int CN, int P>
+__global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs a) {
+  constexpr int N = CN;
+  __shared__ __attribute__((aligned(16))) float2 A[P * N];
+  __shared__ float2 stw[N];
+  __shared__ float sums[4 * P];
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int t0 = tb * 2 * P;
+  const float* g = a.in + (long long)b * a.out_len;
+  for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
+  for (int idx = threadIdx.x; idx < P * N; idx += kThreads) {
+    const int j = idx / N, n = idx - j * N;
+    float va = 0.f, vb = 0.f;
+    if (n < a.win) {
+      const float w = a.window[n];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int t = t0 + 2 * j + h;
+        if (t >= a.T) continue;
+        const int u = t * a.hop + n;
+        if (u < a.offset || u >= a.offset + a.out_len) continue;
+        // OLA normaliser at u (window^2 summed over covering frames)
+        const int tb0 = max(0, ceil_div_i(u - a.win + 1, a.hop));
+        const int tb1 = min(a.T - 1, floor_div(u, a.hop));
+        float cf = 0.f;
+        for (int tt = tb0; tt <= tb1; ++tt) {
+          const float ww = a.window[u - tt * a.hop];
+          cf += ww * ww;
+        }
+        const float v = w * g[u - a.offset] / (cf + 1e-8f);
+        if (h == 0) va = v; else vb = v;
+      }
+    }
+    A[idx] = make_float2(va, vb);
+  }
+  __syncthreads();
+  parity_sums(A, P, N, a.win, sums);
+  const float ah = 0.5f * N, inv_a = 1.f / ah;
+  const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
+  for (int idx = threadIdx.x; idx < P * N; idx += kThreads) {
+    const int j = idx / N, n = idx - j * N;
+    if (n < a.win) {
+      const float2 v = A[idx];
+      A[idx] = make_float2(apply_g(v.x, n, sums[4 * j], sums[4 * j + 1], inv_a, ce, co),
+                           apply_g(v.y, n, sums[4 * j + 2], sums[4 * j + 3], inv_a, ce, co));
+    }
+  }
+  __syncthreads();
+  fft_pass_ip<N, P, 0, 1>(A, stw);
+  unpack_store<N, P>(A, P, N, t0, a.T, b, a.out, nullptr, 0);
+}
+
 // ---------------------------------------------------------------------------
 static bool make_plan(int N, FftPlan& pl) {
   if (N < 2 || N > 1024) return false;
@@ -846,6 +901,32 @@ extern "C" int se_istft_bwd(const float* gout, float* gspec, int B, int T, int w
   if (rc) return rc;
   if (!gout || !gspec || !window || !twiddle) return SE_E_ARG;
   a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle;
+  if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
+    // in-place FFT, SEHIP_ISTFT_IP_PAIRS = 4 / 8 frame pairs per block (A/B knob)
+    static const int ip_pairs = [] {
+      const char* e = std::getenv("SEHIP_ISTFT_IP_PAIRS");
+      const int v = e ? std::atoi(e) : kPairsIP;
+      return (v == 4 || v == 8) ? v : kPairsIP;
+    }();
+    const int P = ip_pairs;
+    const dim3 grid(se::ceil_div(T, 2 * P), B);
+    hipStream_t st = se::as_stream(stream);
+#define SE_ISTFT_BWD_IP(NF)                                                                         \
+  do {                                                                                              \
+    if (P == 8) hipLaunchKernelGGL((istft_bwd_ip_kernel<NF, 8>), grid, dim3(kThreads), 0, st, a);   \
+    else hipLaunchKernelGGL((istft_bwd_ip_kernel<NF, 4>), grid, dim3(kThreads), 0, st, a);          \
+  } while (0)
+    switch (nfft) {
+      case 640: SE_ISTFT_BWD_IP(640); break;
+      case 512: SE_ISTFT_BWD_IP(512); break;
+      case 400: SE_ISTFT_BWD_IP(400); break;
+      case 320: SE_ISTFT_BWD_IP(320); break;
+      default: SE_ISTFT_BWD_IP(256); break;
+    }
+#undef SE_ISTFT_BWD_IP
+    SE_LAUNCH_CHECK();
+    return SE_OK;
+  }
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
   SE_STFT_DISPATCH(istft_bwd_kernel, nfft, a.P, dim3(se::ceil_div(T, 2 * a.P), B), shm, se::as_stream(stream), a);
   SE_LAUNCH_CHECK();

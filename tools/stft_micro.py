@@ -13,8 +13,14 @@ x = torch.randn(B, 1, L, device=dev) * 0.3
 st, ist = ConvSTFT(320, 160, 640).to(dev), ConviSTFT(320, 160, 640).to(dev)
 with torch.no_grad():
     spec = st(x)
-    nbytes = 4 * (x.numel() + spec.numel())
-    for name, f in (("stft_fwd", lambda: st(x)), ("istft_fwd", lambda: ist(spec))):
+nbytes = 4 * (x.numel() + spec.numel())
+sr = spec.clone().requires_grad_(True)
+y = ist(sr)
+gy = torch.randn_like(y)
+# istft_bwd: autograd.grad (no .grad accumulation) runs se_istft_bwd alone
+with torch.no_grad():
+    for name, f in (("stft_fwd", lambda: st(x)), ("istft_fwd", lambda: ist(spec)),
+                    ("istft_bwd", lambda: torch.autograd.grad(y, sr, gy, retain_graph=True))):
         for _ in range(5):
             f()
         torch.cuda.synchronize()
@@ -25,4 +31,4 @@ with torch.no_grad():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 50
-        print(f"P={os.environ.get('SEHIP_STFT_IP_PAIRS', '8')} {name:9s} {ms * 1e3:7.1f} us  {nbytes / ms / 1e6:7.1f} GB/s", flush=True)
+        print(f"P={os.environ.get('SEHIP_STFT_IP_PAIRS', '4')} {name:9s} {ms * 1e3:7.1f} us  {nbytes / ms / 1e6:7.1f} GB/s", flush=True)
