@@ -551,13 +551,29 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_ip_kernel(const IstftArgs 
   const int t_hi = min(a.T - 1, floor_div(s1 - 1, a.hop));
   const float* spec = a.in + (long long)b * 2 * half * a.T;
   for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
+  // spectrum gather: all of a thread's loads are issued before any is used
+  // (compile-time trip count, clamped addresses, zeroed after the load)
+  constexpr int GT = (half * P + kThreads - 1) / kThreads;
+  float2 ga[GT], gb[GT];
+#pragma unroll
+  for (int it = 0; it < GT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    const int k = min(idx / P, half - 1), j = idx % P;
+    const int ta = min(t_lo + 2 * j, t_hi), tb = min(t_lo + 2 * j + 1, t_hi);
+    const float* re = spec + (long long)k * a.T;
+    const float* im = spec + (long long)(half + k) * a.T;
+    ga[it] = make_float2(re[ta], im[ta]);
+    gb[it] = make_float2(re[tb], im[tb]);
+  }
   // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
-  for (int idx = threadIdx.x; idx < half * P; idx += kThreads) {
+#pragma unroll
+  for (int it = 0; it < GT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    if (idx >= half * P) break;
     const int k = idx / P, j = idx - k * P;
     const int ta = t_lo + 2 * j, tb = ta + 1;
-    float2 xa = make_float2(0.f, 0.f), xb = xa;
-    if (ta <= t_hi) xa = make_float2(spec[(long long)k * a.T + ta], spec[(long long)(half + k) * a.T + ta]);
-    if (tb <= t_hi) xb = make_float2(spec[(long long)k * a.T + tb], spec[(long long)(half + k) * a.T + tb]);
+    const float2 zero = make_float2(0.f, 0.f);
+    const float2 xa = ta <= t_hi ? ga[it] : zero, xb = tb <= t_hi ? gb[it] : zero;
     float2* c = A + j * N;
     if (k == 0 || k == N / 2) {
       c[k] = make_float2(xa.x, -xb.x);
