@@ -686,17 +686,39 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
   constexpr int N = CN;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
   __shared__ float2 stw[N];
+  __shared__ float swin[N];
   __shared__ float sums[4 * P];
   int tb, b;
   xcd_frame_block(tb, b);
   const int t0 = tb * 2 * P;
   const float* g = a.in + (long long)b * a.out_len;
-  for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
-  for (int idx = threadIdx.x; idx < P * N; idx += kThreads) {
+  for (int i = threadIdx.x; i < N; i += kThreads) {
+    stw[i] = a.tw[i];
+    swin[i] = i < a.win ? a.window[i] : 0.f;
+  }
+  // gradient gather: all of a thread's loads are issued first (compile-time trip
+  // count, clamped addresses, masked after the load); the window is read from LDS
+  constexpr int IT = (P * N + kThreads - 1) / kThreads;
+  float ga[IT][2];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    const int j = idx / N, n = idx - j * N;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = (t0 + 2 * j + h) * a.hop + n;
+      ga[it][h] = a.out_len > 0 ? g[min(max(u - a.offset, 0), a.out_len - 1)] : 0.f;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int idx = threadIdx.x + it * kThreads;
+    if (P * N % kThreads != 0 && idx >= P * N) break;
     const int j = idx / N, n = idx - j * N;
     float va = 0.f, vb = 0.f;
     if (n < a.win) {
-      const float w = a.window[n];
+      const float w = swin[n];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         const int t = t0 + 2 * j + h;
@@ -708,10 +730,10 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
         const int tb1 = min(a.T - 1, floor_div(u, a.hop));
         float cf = 0.f;
         for (int tt = tb0; tt <= tb1; ++tt) {
-          const float ww = a.window[u - tt * a.hop];
+          const float ww = swin[u - tt * a.hop];
           cf += ww * ww;
         }
-        const float v = w * g[u - a.offset] / (cf + 1e-8f);
+        const float v = w * ga[it][h] / (cf + 1e-8f);
         if (h == 0) va = v; else vb = v;
       }
     }
