@@ -6,9 +6,11 @@ forward, SI-SNR, backward, clip_grad_norm_(0.5), AdamW) on 64 synthetic
 4 s @ 16 kHz noisy/clean pairs per GPU, inputs resident in HBM.
 fp32 storage and accumulation throughout (the reference's precision; parity
 is judged at 1e-4 fp32). The conv GEMMs' MFMA form follows SEHIP_CONV_MATH /
---math (default: three-way split-bf16 forward, fp32-class; two-way split
-data/weight-grad GEMMs); the all-fp32-MFMA step (`f32_exact`) and the one-term
-bf16 step (`other_conv_math`) are timed beside it.
+--math; the default "f16x3" (scaled split-fp16, three MFMA terms) is
+fp32-class on every pass: each pass's error against fp64 is 0.63-0.70x the
+exact-fp32 MFMA path's (tests/test_gpu_conv_x3.py). The all-fp32-MFMA step
+(`f32_exact`) and the coarser split-bf16 / one-term bf16 steps
+(`other_conv_math`) are timed beside it.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
@@ -50,8 +52,13 @@ KERNEL_OF = {   # OpTimer tag -> (rocprof kernel name, description)
     "conv_fwd_bf16": ("gather_x3_kernel", "gather_x3_kernel<TERMS=1> (se_conv2d_fwd, bf16 MFMA 32x32x16)"),
     "conv_data_bf16": ("gather_x3_kernel", "gather_x3_kernel<TERMS=1> (se_conv2d_bwd_data, bf16 MFMA 32x32x16)"),
     "conv_wgrad_bf16": ("wgrad_x3_kernel", "wgrad_x3_kernel<TERMS=1> (se_conv2d_bwd_weight, bf16 MFMA 32x32x16)"),
+    "conv_fwd_f16x3": ("gather_x3_kernel", "gather_x3_kernel<F16> (se_conv2d_fwd, scaled split-fp16 MFMA 32x32x16 x3)"),
+    "conv_data_f16x3": ("gather_x3_kernel",
+                        "gather_x3_kernel<F16> (se_conv2d_bwd_data, scaled split-fp16 MFMA 32x32x16 x3)"),
+    "conv_wgrad_f16x3": ("wgrad_x3_kernel",
+                         "wgrad_x3_kernel<F16> (se_conv2d_bwd_weight, scaled split-fp16 MFMA 32x32x16 x3)"),
 }
-TERMS_OF = {"bf16x3": 3, "bf16x6": 6, "bf16": 1}   # MFMA terms per fp32 product (peak divisor)
+TERMS_OF = {"bf16x3": 3, "bf16x6": 6, "bf16": 1, "f16x3": 3}   # MFMA terms per fp32 product (peak divisor)
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
 SR, SECONDS = 16000, 4
 
@@ -66,9 +73,9 @@ def parse():
     ap.add_argument("--cpu-batch", type=int, default=4)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-op-timing", action="store_true")
-    ap.add_argument("--compare", default="f32,bf16",
-                    help="conv math modes timed beside the default step (untimed by the op timer): "
-                         "all-fp32 MFMA and the one-term bf16 GEMMs; '' for none")
+    ap.add_argument("--compare", default="f32;bf16x3;bf16",
+                    help="';'-separated conv math modes timed beside the default step (untimed by the "
+                         "op timer): all-fp32 MFMA and the one-term bf16 GEMMs; '' for none")
     ap.add_argument("--no-compare", "--no-compare-f32", dest="compare", action="store_const", const="",
                     help="skip the comparison runs")
     ap.add_argument("--math", default=os.environ.get("SEHIP_CONV_MATH"),
@@ -167,7 +174,7 @@ def main():
     # operands (fp32 storage/accumulation), the speed form of SURVEY §8d config 4
     compare = {}
     default_mode = SF.get_conv_math()
-    for mode in [m for m in args.compare.split(",") if m and m != default_mode]:
+    for mode in [m for m in args.compare.split(";") if m and m != default_mode]:
         SF.set_conv_math(mode)
         noisy, clean = batches[0]
         train_step(model, opt, noisy, clean)
@@ -196,7 +203,7 @@ def main():
     out = {
         "metric": METRIC, "value": round(value, 3), "unit": "utterances/sec", "n_gpus": world,
         "steps": args.steps, "warmup": args.warmup, "ms_per_step": round(1e3 * elapsed / args.steps, 3),
-        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": _dtype_label(SF.get_conv_math()),
         "data": "synthetic: on-device 4 s @ 16 kHz harmonic+AM clean / Gaussian-noise pairs at "
                 "SNR U{-5..20} dB, random-init FRCRN (no datasets/checkpoints offline)",
         "config": {"workload": "FRCRN train step: fwd + SI-SNR + bwd + clip_grad_norm 0.5 + AdamW "
@@ -205,13 +212,12 @@ def main():
                    "parallelism": f"dp{world}"},
         "final_loss": round(loss_v, 4),
         "conv_math": SF.get_conv_math(),
-        "conv_math_note": "fp32 storage and accumulation everywhere; 'bf16x3' passes split each fp32 "
-                          "operand into hi+lo bf16 and sum hi*hi+hi*lo+lo*hi on bf16 MFMA (4.5e-6 "
-                          "rel-L2 per conv vs fp64); 'bf16x6' splits three ways and sums the six "
-                          "terms of order >= 2^-16 (5.5e-7 vs fp64, fp32 MFMA path 6.4e-7); 'fwd_dec' "
-                          "overrides the forward of transposed convs with >= fwd_dec_min_h input rows "
-                          "(FRCRN's last decoder layer); "
-                          "tests/test_gpu_conv_x3.py",
+        "conv_math_note": "fp32 storage and accumulation everywhere; 'f16x3' scales each operand by a "
+                          "per-tensor power of two, splits it into hi+lo fp16 and sums hi*hi+hi*lo+lo*hi "
+                          "on fp16 MFMA (4.0e-7 rel-L2 per conv vs fp64; the exact-fp32 MFMA path "
+                          "6.4e-7): fp32-class, so the step's conv FLOP rate may exceed the 157.3 TF "
+                          "fp32 MFMA peak; 'bf16x3' = hi+lo bf16 (4.5e-6, not fp32-class); 'bf16x6' = "
+                          "three-way bf16 split, six terms (5.5e-7); tests/test_gpu_conv_x3.py",
     }
     if "f32" in compare:
         out["f32_exact"] = compare.pop("f32")
@@ -263,6 +269,22 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_steps)
     print(json.dumps(out), flush=True)
+
+
+FP32_CLASS = {"f32", "f16x3", "bf16x6"}   # per-conv error at or below the exact-fp32 MFMA path's
+
+
+def _dtype_label(mode):
+    """The arithmetic the step computes in: "f32" only for exact fp32 products;
+    fp32-class emulations name their split form; anything coarser is labelled
+    by its narrowest pass."""
+    modes = {kv.split("=")[1] for kv in mode.split(",") if "=" in kv and not kv.startswith("fwd_dec_min")} \
+        if "=" in mode else {mode}
+    if modes == {"f32"}:
+        return "f32"
+    if modes <= FP32_CLASS:
+        return "f32-class (" + "+".join(sorted(modes - {"f32"})) + " split MFMA, fp32 storage/accumulate)"
+    return "mixed (" + "+".join(sorted(modes)) + "; not fp32-class)"
 
 
 def _pmc_traffic(kernel):

@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 1
+#define SEHIP_ABI_VERSION 2
 
 enum {
   SE_OK = 0,
@@ -121,10 +121,33 @@ typedef struct se_conv2d_desc {
                        * SE_MATH_BF16 (3): operands rounded to bf16, one MFMA
                        * term, fp32 accumulate and storage (the arithmetic of a
                        * bf16 autocast conv; BASELINE configs 2/3).
+                       * SE_MATH_F16X3 (4): scaled split-fp16. Each operand is
+                       * multiplied by a power of two s (per tensor, from its
+                       * max |.|: max|x| * s < 2^14) and split as hi + lo fp16
+                       * (both round-to-nearest), a*b ~ ah*bh + ah*bl + al*bh on
+                       * v_mfma_f32_32x32x16_f16, fp32 accumulate, the result
+                       * multiplied back by 1/(s_a s_b) (exact). Per-product error
+                       * <= ~2^-21 relative plus ~2^-38 max|a| |b| for elements
+                       * below 2^-17 max|a|: fp32-class (tests/test_gpu_conv_x3.py
+                       * asserts each pass at or below the SE_MATH_F32 path's
+                       * error vs fp64) at the cost of bf16x3.
                        * Shapes the split kernels do not cover run SE_MATH_F32. */
+  /* SE_MATH_F16X3 only: device pointers to ONE fp32 upper bound of max |.| of
+   * the conv input x (for the joined entry points: over x and s) and of dy.
+   * The bound may exceed the true maximum by up to ~2^10 without measurable
+   * loss; it must not be below it. NULL = the call computes it (one extra read
+   * of the tensor). Producers that already pass over the tensor (ComplexBN's
+   * apply, se_amax) fill it for free. */
+  const float* x_amax;
+  const float* dy_amax;
 } se_conv2d_desc;
 
-enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3 };
+enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3,
+       SE_MATH_F16X3 = 4 };
+
+/* amax[0] = max(amax[0], max_i |x[i]|) over n elements (atomic; zero amax[0]
+ * first for a fresh maximum). The scale source of SE_MATH_F16X3. */
+int se_amax(const float* x, long long n, float* amax, void* stream);
 
 /* Output spatial size (nn.Conv2d / nn.ConvTranspose2d formulas). */
 int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w);
@@ -187,29 +210,35 @@ int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float* x, int x_h
  * running: host array of 5 device pointers RMr, RMi, RVrr, RVri, RVii, or
  *          NULL when track_running_stats=False; updated in place in training.
  * nbt    : device int64 num_batches_tracked (NULL if not tracking).
- * save   : device fp32 [16*Cc] per-channel state for se_cbn_bwd.
+ * save   : device fp32 [SE_CBN_SAVE_FLOATS*Cc] per-channel state for se_cbn_bwd.
  * act    : 0 none, 1 LeakyReLU(slope), 2 ReLU (applied after the affine).
  * training: 1 = batch statistics (+ running update when running != NULL),
  *          0 = running statistics.
  * momentum < 0 means "None" (cumulative average, complex_nn.py:223-224).
+ * y_amax : device fp32 [1] or NULL. Training only: receives an upper bound of
+ *          max |y| (from the moments pass's per-channel extrema, no extra
+ *          pass), the se_conv2d_desc.x_amax of a SE_MATH_F16X3 consumer.
  * ------------------------------------------------------------------------ */
+#define SE_CBN_SAVE_FLOATS 20
 size_t se_cbn_workspace_size(int B, int C, int HW);
 
 int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
                const float* const* params, float* const* running,
                int64_t* nbt, float* save, int training, float eps,
-               float momentum, int act, float slope, void* ws,
+               float momentum, int act, float slope, float* y_amax, void* ws,
                size_t ws_bytes, void* stream);
 
 /* Backward. gy = dL/dy (after the activation), x = forward input. y (the
  * forward output) is NOT read and may be NULL: the activation derivative is
  * taken from the pre-activation Z(x - M) + B recomputed from x and `save`.
  * dx is overwritten. dparams: host array of 5 device pointers dWrr, dWri,
- * dWii, dBr, dBi (overwritten), or NULL. */
+ * dWii, dBr, dBi (overwritten), or NULL. dx_amax: device fp32 [1] or NULL;
+ * training only: an upper bound of max |dx| (the se_conv2d_desc.dy_amax of the
+ * producing conv's SE_MATH_F16X3 backward). */
 int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
                int B, int C, int HW, const float* const* params,
                const float* save, float* const* dparams, int training,
-               int act, float slope, void* ws, size_t ws_bytes,
+               int act, float slope, float* dx_amax, void* ws, size_t ws_bytes,
                void* stream);
 
 /* Backward of a forked output: y feeds two consumers (FRCRN's encoder block
@@ -221,7 +250,7 @@ int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
 int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, float* dx,
                 int B, int C, int HW, const float* const* params,
                 const float* save, float* const* dparams, int training,
-                int act, float slope, void* ws, size_t ws_bytes,
+                int act, float slope, float* dx_amax, void* ws, size_t ws_bytes,
                 void* stream);
 
 /* ------------------------------------------------------------------------

@@ -11,6 +11,15 @@
 // recomputed from x with the forward's own expression, so y is never read
 // (2 of the 7 backward passes over the activation of the old design).
 // All kernels stream the channel planes contiguously (HBM-bound).
+//
+// Scale sources of the SE_MATH_F16X3 conv GEMMs (se_conv2d_desc.x_amax /
+// dy_amax): the moments passes also keep per-channel extrema (forward: min and
+// max of x; backward: max |g|), and the 1-block finalize kernels turn them into
+// an upper bound of max |y| (forward) or max |dx| (backward) over the whole
+// tensor, e.g. |y_r| <= |Zrr| max|x_r - Mr| + |Zri| max|x_i - Mi| + |Br| (the
+// activations never increase a magnitude). No extra pass, no atomics; the bound
+// is within a small factor of the true maximum, which the scaled split-fp16
+// GEMMs absorb without loss.
 #include "common.hpp"
 
 #include <algorithm>
@@ -19,10 +28,23 @@ namespace {
 
 constexpr int kThreads = 256;
 constexpr int kSeg = 8192;   // elements of one (b, c) plane per reduction row
-constexpr int kSave = 16;    // floats of per-channel state
-// save layout
+constexpr int kSave = 20;    // floats of per-channel state (SE_CBN_SAVE_FLOATS)
+// save layout (S_DR / S_DI: max |x_r - Mr|, max |x_i - Mi| of the training batch)
 enum { S_MR = 0, S_MI, S_VRR, S_VRI, S_VII, S_URR, S_URI, S_UII,
-       S_ZRR, S_ZRI, S_ZIR, S_ZII, S_BR, S_BI, S_S, S_T };
+       S_ZRR, S_ZRI, S_ZIR, S_ZII, S_BR, S_BI, S_S, S_T, S_DR, S_DI, S_PAD0, S_PAD1 };
+static_assert(kSave == SE_CBN_SAVE_FLOATS, "save layout");
+
+// block-wide max of v (all threads call); thread 0 gets the result
+__device__ __forceinline__ float block_max(float v) {
+  __shared__ float red[kThreads / 64];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  if (threadIdx.x == 0)
+    for (int w = 1; w < (int)(blockDim.x + 63) / 64; ++w) v = fmaxf(v, red[w]);
+  return v;
+}
 
 struct Ptr5 { const float* p[5]; };
 struct MPtr5 { float* p[5]; };
@@ -51,29 +73,40 @@ __device__ __forceinline__ float act_grad(float y, int act, float slope) {
 }
 
 // grid (Cc, P). Row r = (b, segment) of channel c; rows strided over P.
+// ext[(c * P + p) * 4 + {0..3}] = max x_r, -min x_r, max x_i, -min x_i
 __global__ void __launch_bounds__(kThreads)
-cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, double* part) {
+cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, double* part, float* ext) {
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
   const int nseg = (HW + kSeg - 1) / kSeg;
   double v[5] = {0, 0, 0, 0, 0};
+  float e[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int row = p; row < B * nseg; row += P) {
     const int b = row / nseg, sg = row - b * nseg;
     const float* xr = x + ((long long)b * C + c) * HW;
     const float* xi = x + ((long long)b * C + Cc + c) * HW;
     const int i1 = min(HW, (sg + 1) * kSeg);
     for (int i = sg * kSeg + threadIdx.x; i < i1; i += kThreads) {
-      const double r = xr[i], m = xi[i];
+      const float fr = xr[i], fm = xi[i];
+      e[0] = fmaxf(e[0], fr); e[1] = fmaxf(e[1], -fr); e[2] = fmaxf(e[2], fm); e[3] = fmaxf(e[3], -fm);
+      const double r = fr, m = fm;
       v[0] += r; v[1] += m; v[2] += r * r; v[3] += r * m; v[4] += m * m;
     }
   }
   block_reduce_store<5>(v, part + ((long long)c * P + p) * 5);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    __syncthreads();
+    const float m = block_max(e[k]);
+    if (threadIdx.x == 0) ext[((long long)c * P + p) * 4 + k] = m;
+  }
 }
 
 // One block; channel c per thread (strided).
-__global__ void cbn_finalize_kernel(const double* part, int P, double count, int Cc,
+__global__ void cbn_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
                                     Ptr5 params, int affine, MPtr5 running, int has_running,
                                     int64_t* nbt, float* save, int training, float eps,
-                                    float momentum) {
+                                    float momentum, float* y_amax) {
+  float ybound = 0.f;   // upper bound of max |y| over every channel (training)
   float factor = 0.f;
   if (training && has_running) {
     factor = momentum >= 0.f ? momentum : (float)(1.0 / (double)(nbt ? (*nbt + 1) : 1));
@@ -117,7 +150,25 @@ __global__ void cbn_finalize_kernel(const double* part, int P, double count, int
     o[S_URR] = (float)urr; o[S_URI] = (float)uri; o[S_UII] = (float)uii;
     o[S_ZRR] = (float)zrr; o[S_ZRI] = (float)zri; o[S_ZIR] = (float)zir; o[S_ZII] = (float)zii;
     o[S_BR] = (float)br; o[S_BI] = (float)bi; o[S_S] = (float)s; o[S_T] = (float)t;
+    float dr = INFINITY, di = INFINITY;   // eval: the batch extrema are unknown
+    if (training) {
+      float xmax_r = -INFINITY, xmin_r = -INFINITY, xmax_i = -INFINITY, xmin_i = -INFINITY;
+      for (int p = 0; p < P; ++p) {
+        const float* q = ext + ((long long)c * P + p) * 4;
+        xmax_r = fmaxf(xmax_r, q[0]); xmin_r = fmaxf(xmin_r, q[1]);
+        xmax_i = fmaxf(xmax_i, q[2]); xmin_i = fmaxf(xmin_i, q[3]);
+      }
+      // max |x - M| (xmin_* hold -min); rounded up so the bound stays a bound
+      dr = fmaxf(xmax_r - (float)mr, xmin_r + (float)mr) * 1.0001f;
+      di = fmaxf(xmax_i - (float)mi, xmin_i + (float)mi) * 1.0001f;
+      const float yr = fabsf((float)zrr) * dr + fabsf((float)zri) * di + fabsf((float)br);
+      const float yi = fabsf((float)zir) * dr + fabsf((float)zii) * di + fabsf((float)bi);
+      ybound = fmaxf(ybound, fmaxf(yr, yi) * 1.0001f);
+    }
+    o[S_DR] = dr; o[S_DI] = di; o[S_PAD0] = o[S_PAD1] = 0.f;
   }
+  ybound = block_max(ybound);
+  if (threadIdx.x == 0 && training && y_amax) *y_amax = ybound;
   __syncthreads();
   if (threadIdx.x == 0 && training && has_running && nbt) *nbt += 1;
 }
@@ -154,10 +205,11 @@ template <bool G2>
 __global__ void __launch_bounds__(kThreads)
 cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
                        const float* __restrict__ x, int B, int C, int HW, int P,
-                       const float* __restrict__ save, int act, float slope, double* part) {
+                       const float* __restrict__ save, int act, float slope, double* part, float* ext) {
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
   const int nseg = (HW + kSeg - 1) / kSeg;
   const float* sv = save + c * kSave;
+  float gmr = 0.f, gmi = 0.f;   // max |g_r|, max |g_i| (the dx bound)
   const float mr = sv[S_MR], mi = sv[S_MI];
   const float zrr = sv[S_ZRR], zri = sv[S_ZRI], zir = sv[S_ZIR], zii = sv[S_ZII], br = sv[S_BR], bi = sv[S_BI];
   double v[6] = {0, 0, 0, 0, 0, 0};
@@ -170,21 +222,31 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
       const float zr = zrr * xr + zri * xi + br, zi = zir * xr + zii * xi + bi;   // = forward pre-activation
       const float gr = (G2 ? gy[offr + i] + gy2[offr + i] : gy[offr + i]) * act_grad(zr, act, slope);
       const float gi = (G2 ? gy[offi + i] + gy2[offi + i] : gy[offi + i]) * act_grad(zi, act, slope);
+      gmr = fmaxf(gmr, fabsf(gr)); gmi = fmaxf(gmi, fabsf(gi));
       v[0] += gr; v[1] += gi;
       v[2] += (double)gr * xr; v[3] += (double)gr * xi;
       v[4] += (double)gi * xr; v[5] += (double)gi * xi;
     }
   }
   block_reduce_store<6>(v, part + ((long long)c * P + p) * 6);
+  __syncthreads();
+  gmr = block_max(gmr);
+  __syncthreads();
+  gmi = block_max(gmi);
+  if (threadIdx.x == 0) {
+    ext[((long long)c * P + p) * 2 + 0] = gmr;
+    ext[((long long)c * P + p) * 2 + 1] = gmi;
+  }
 }
 
 // coef layout per channel (16 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi Br Bi pad
 constexpr int kCoef = 16;
 
-__global__ void cbn_bwd_finalize_kernel(const double* part, int P, double count, int Cc,
+__global__ void cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
                                         const float* save, Ptr5 params, int affine,
                                         MPtr5 dparams, int has_dparams, int training,
-                                        float* coef) {
+                                        float* coef, float* dx_amax) {
+  float dbound = 0.f;   // upper bound of max |dx| over every channel (training)
   for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
     double sm[6] = {0, 0, 0, 0, 0, 0};
     for (int p = 0; p < P; ++p)
@@ -239,7 +301,22 @@ __global__ void cbn_bwd_finalize_kernel(const double* part, int P, double count,
     o[6] = (float)grr; o[7] = (float)gri; o[8] = (float)gii;
     o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = s[S_BR]; o[12] = s[S_BI];
     o[13] = o[14] = o[15] = 0.f;
+    if (training) {   // dx = Z^T (g - gb) + Gamma (x - M), bounded term by term
+      float gr = 0.f, gi = 0.f;
+      for (int p = 0; p < P; ++p) {
+        gr = fmaxf(gr, ext[((long long)c * P + p) * 2 + 0]);
+        gi = fmaxf(gi, ext[((long long)c * P + p) * 2 + 1]);
+      }
+      gr += fabsf(o[4]);
+      gi += fabsf(o[5]);
+      const float dr = s[S_DR], di = s[S_DI];
+      const float br = fabsf(o[0]) * gr + fabsf(o[1]) * gi + fabsf(o[6]) * dr + fabsf(o[7]) * di;
+      const float bi = fabsf(o[2]) * gr + fabsf(o[3]) * gi + fabsf(o[7]) * dr + fabsf(o[8]) * di;
+      dbound = fmaxf(dbound, fmaxf(br, bi) * 1.0001f);
+    }
   }
+  dbound = block_max(dbound);
+  if (threadIdx.x == 0 && training && dx_amax) *dx_amax = dbound;
 }
 
 template <bool G2>
@@ -280,13 +357,19 @@ extern "C" size_t se_cbn_workspace_size(int B, int C, int HW) {
   if (B <= 0 || C <= 0 || HW <= 0) return 0;
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
-  return (size_t)Cc * P * 6 * sizeof(double) + (size_t)Cc * kCoef * sizeof(float) + 512;
+  return (size_t)Cc * P * 6 * sizeof(double) + (size_t)Cc * kCoef * sizeof(float) +
+         (size_t)Cc * P * 4 * sizeof(float) + 512;
+}
+
+// per-(channel, partition) extrema of the moments passes, after part and coef
+static float* ext_of(void* ws, int Cc, int P) {
+  return (float*)((char*)ws + (size_t)Cc * P * 6 * sizeof(double) + (size_t)Cc * kCoef * sizeof(float));
 }
 
 extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
                           const float* const* params, float* const* running, int64_t* nbt,
                           float* save, int training, float eps, float momentum, int act,
-                          float slope, void* ws, size_t ws_bytes, void* stream) {
+                          float slope, float* y_amax, void* ws, size_t ws_bytes, void* stream) {
   if (!x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || act < 0 || act > 2)
     return SE_E_ARG;
   if (!training && !running) return SE_E_ARG;  // eval needs running statistics
@@ -295,16 +378,17 @@ extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
   double* part = (double*)ws;
+  float* ext = ext_of(ws, Cc, P);
   Ptr5 pp{};
   MPtr5 rp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (running) for (int k = 0; k < 5; ++k) rp.p[k] = running[k];
   if (training) {
-    hipLaunchKernelGGL(cbn_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part);
+    hipLaunchKernelGGL(cbn_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part, ext);
     SE_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(cbn_finalize_kernel, dim3(1), dim3(256), 0, st, part, P, (double)B * HW, Cc,
-                     pp, params ? 1 : 0, rp, running ? 1 : 0, nbt, save, training, eps, momentum);
+  hipLaunchKernelGGL(cbn_finalize_kernel, dim3(1), dim3(256), 0, st, part, ext, P, (double)B * HW, Cc,
+                     pp, params ? 1 : 0, rp, running ? 1 : 0, nbt, save, training, eps, momentum, y_amax);
   SE_LAUNCH_CHECK();
   hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), Cc, B), dim3(kThreads),
                      0, st, x, y, C, HW, save, act, slope);
@@ -316,7 +400,8 @@ namespace {
 
 int cbn_bwd_impl(const float* gy, const float* gy2, const float* x, float* dx, int B, int C,
                  int HW, const float* const* params, const float* save, float* const* dparams,
-                 int training, int act, float slope, void* ws, size_t ws_bytes, void* stream) {
+                 int training, int act, float slope, float* dx_amax, void* ws, size_t ws_bytes,
+                 void* stream) {
   if (!gy || !x || !dx || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0) return SE_E_ARG;
   if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
@@ -324,19 +409,20 @@ int cbn_bwd_impl(const float* gy, const float* gy2, const float* x, float* dx, i
   const int P = pick_P(B, Cc, HW);
   double* part = (double*)ws;
   float* coef = (float*)((char*)ws + (size_t)Cc * P * 6 * sizeof(double));
+  float* ext = ext_of(ws, Cc, P);
   Ptr5 pp{};
   MPtr5 dp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (dparams) for (int k = 0; k < 5; ++k) dp.p[k] = dparams[k];
   if (gy2)
     hipLaunchKernelGGL(cbn_bwd_moments_kernel<true>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2, x,
-                       B, C, HW, P, save, act, slope, part);
+                       B, C, HW, P, save, act, slope, part, ext);
   else
     hipLaunchKernelGGL(cbn_bwd_moments_kernel<false>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2,
-                       x, B, C, HW, P, save, act, slope, part);
+                       x, B, C, HW, P, save, act, slope, part, ext);
   SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cbn_bwd_finalize_kernel, dim3(1), dim3(256), 0, st, part, P, (double)B * HW,
-                     Cc, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, coef);
+  hipLaunchKernelGGL(cbn_bwd_finalize_kernel, dim3(1), dim3(256), 0, st, part, ext, P, (double)B * HW,
+                     Cc, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, dx_amax);
   SE_LAUNCH_CHECK();
   const dim3 grid(se::ceil_div(HW, kThreads * 4), Cc, B);
   if (gy2)
@@ -353,11 +439,11 @@ int cbn_bwd_impl(const float* gy, const float* gy2, const float* x, float* dx, i
 
 extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx, int B,
                           int C, int HW, const float* const* params, const float* save,
-                          float* const* dparams, int training, int act, float slope, void* ws,
-                          size_t ws_bytes, void* stream) {
+                          float* const* dparams, int training, int act, float slope,
+                          float* dx_amax, void* ws, size_t ws_bytes, void* stream) {
   (void)y;   // not read: act' is recomputed from x (see the file comment); may be NULL
   return cbn_bwd_impl(gy, nullptr, x, dx, B, C, HW, params, save, dparams, training, act, slope,
-                      ws, ws_bytes, stream);
+                      dx_amax, ws, ws_bytes, stream);
 }
 
 // Forked output (the encoder block's y feeds the next conv AND the decoder skip):
@@ -365,9 +451,9 @@ extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float
 // activation-sized tensors (3 passes) before the backward.
 extern "C" int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, float* dx, int B,
                            int C, int HW, const float* const* params, const float* save,
-                           float* const* dparams, int training, int act, float slope, void* ws,
-                           size_t ws_bytes, void* stream) {
+                           float* const* dparams, int training, int act, float slope,
+                           float* dx_amax, void* ws, size_t ws_bytes, void* stream) {
   if (!gy2) return SE_E_ARG;
-  return cbn_bwd_impl(gy, gy2, x, dx, B, C, HW, params, save, dparams, training, act, slope, ws,
-                      ws_bytes, stream);
+  return cbn_bwd_impl(gy, gy2, x, dx, B, C, HW, params, save, dparams, training, act, slope,
+                      dx_amax, ws, ws_bytes, stream);
 }

@@ -43,6 +43,7 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // selecting after the load: the loaded register then feeds the LDS write
 // directly and the load stays in flight across the MFMA loop.
 constexpr size_t kZeroBytes = 256;
+constexpr size_t kAmaxBytes = 256;   // SE_MATH_F16X3 max |.| slots, zeroed with the zero page
 
 // ---------------------------------------------------------------------------
 // Gather-GEMM (forward and data-grad)
@@ -97,6 +98,9 @@ struct GatherArgs {
   // Ho x Wo) and Y2 (x chunks, grid YH2 x YW2; rows >= YH2 are dropped).
   float* Y2;
   int yjh, YH2, YW2;
+  // SE_MATH_F16X3: device max |.| of the gathered tensor(s) and of the weights
+  const float* amax_a;
+  const float* amax_w;
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -414,6 +418,9 @@ struct WgradArgs {
   // D holds s (2*djh channels, grid Qh x Qw), D2 holds x on DH2 x DW2.
   const float* D2;
   int djh, DH2, DW2;
+  // SE_MATH_F16X3: device max |.| of G (the gathered tensor) and of D (both sources)
+  const float* amax_g;
+  const float* amax_d;
 };
 
 // Small-N weight grad (N <= 8: FRCRN's final_conv 128->2 and the CCBAM spatial
@@ -963,7 +970,9 @@ struct ConvGeom {
   int B, Ci, Hi, Wi, Co, Ho, Wo;
   int kh, kw, sh, sw, ph, pw, dh, dw, oph, opw, transposed, complex_w;
   int phe, pwe;   // end (bottom / right) padding; ph / pw are the begin offsets
-  int math;       // SE_MATH_F32 / SE_MATH_BF16X3
+  int math;       // SE_MATH_*
+  const float* x_amax;    // SE_MATH_F16X3 scale sources from the caller (or nullptr)
+  const float* dy_amax;
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -975,7 +984,9 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.phe = d->pad_h_end < 0 ? g.ph : d->pad_h_end;
   g.pwe = d->pad_w_end < 0 ? g.pw : d->pad_w_end;
   g.math = d->math;
-  if (g.math < SE_MATH_F32 || g.math > SE_MATH_BF16) return SE_E_ARG;
+  g.x_amax = d->x_amax;
+  g.dy_amax = d->dy_amax;
+  if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16X3) return SE_E_ARG;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
     return SE_E_ARG;
@@ -1036,7 +1047,7 @@ static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N) {
     bytes += (size_t)c.Kp * sizeof(int4);
   }
   bytes += (size_t)round_up(N, 128) * sizeof(float);  // bias_full
-  return bytes + kZeroBytes + 512;
+  return bytes + kZeroBytes + kAmaxBytes + 512;
 }
 
 constexpr int kSmallWgradN = 8;   // N at or below: wgrad_smalln_kernel
@@ -1087,7 +1098,15 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
 
 static size_t wgrad_ws_bytes(const WgradPlan& w) {
   return (size_t)w.splits * w.c.Kp * w.Np * sizeof(float) + (size_t)w.c.Kp * sizeof(int4) +
-         kZeroBytes + 512;
+         kZeroBytes + kAmaxBytes + 512;
+}
+
+// SE_MATH_F16X3 scale sources: max |.| of each listed tensor into one slot
+// (zeroed with the workspace's zero page). A caller-supplied bound skips the pass.
+static void launch_amax(const float* x, long long n, float* slot, hipStream_t st) {
+  if (n <= 0) return;
+  const long long blocks = std::min<long long>(std::max<long long>((n / 4 + 255) / 256, 1), 2048);
+  hipLaunchKernelGGL(amax_kernel, dim3((unsigned)blocks), dim3(256), 0, st, x, n, (unsigned*)slot);
 }
 
 static inline char* align256(char* p) { return (char*)(((uintptr_t)p + 255) & ~(uintptr_t)255); }
@@ -1131,8 +1150,9 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
 
   char* p = align256((char*)ws);
   const float* zero = (const float*)p;
-  (void)hipMemsetAsync(p, 0, kZeroBytes, st);
-  p = align256(p + kZeroBytes);
+  float* amax_slot = (float*)(p + kZeroBytes);   // [0] weights, [1] gathered tensor
+  (void)hipMemsetAsync(p, 0, kZeroBytes + kAmaxBytes, st);
+  p = align256(p + kZeroBytes + kAmaxBytes);
   float* bias_full = nullptr;
   if (pass == kFwd && bias_br) {
     bias_full = (float*)p;
@@ -1140,10 +1160,23 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     hipLaunchKernelGGL(prep_bias_kernel, dim3(se::ceil_div(N, 256)), dim3(256), 0, st,
                        bias_br, bias_bi, N, g.complex_w, bias_full);
   }
-  // split-bf16 / bf16 GEMM for the 128-column tiles (N > 64); other shapes stay fp32
+  // split-bf16 / bf16 / split-fp16 GEMM for the 128-column tiles (N > 64); other
+  // shapes stay fp32
   const bool bf1 = g.math == SE_MATH_BF16 && N > 64;             // one term: hi*hi
-  const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1;   // prep / tiles shared
+  const bool f16 = g.math == SE_MATH_F16X3 && N > 64;            // scaled split-fp16
+  const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1 || f16;   // prep / tiles shared
   const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
+  const float* amax_a = pass == kFwd ? g.x_amax : g.dy_amax;
+  if (f16) {
+    const long long nw = (long long)(g.complex_w ? g.Ci / 2 : g.Ci) * (g.complex_w ? g.Co / 2 : g.Co) * g.kh * g.kw;
+    launch_amax(wr, nw, amax_slot, st);
+    if (g.complex_w) launch_amax(wi, nw, amax_slot, st);
+    if (!amax_a) {
+      launch_amax(X, (long long)g.B * (jn && jn->x2 ? 2 * jn->jh : Cg) * Hi * Wi, amax_slot + 1, st);
+      if (jn && jn->x2) launch_amax(jn->x2, (long long)g.B * 2 * jn->jh * jn->h2 * jn->w2, amax_slot + 1, st);
+      amax_a = amax_slot + 1;
+    }
+  }
   const bool join_in = jn && jn->x2, join_out = jn && jn->y2;
   const int cpb = join_in ? 2 * jn->jh : Cg;        // channels per batch item of X
   // TU needs whole K-steps inside one tap and 32-bit buffer offsets over the
@@ -1174,16 +1207,21 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       hipLaunchKernelGGL(prep_class_x6_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
                          pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab);
-    else if (x3)
-      hipLaunchKernelGGL(prep_class_x3_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
+    else if (f16)
+      hipLaunchKernelGGL(prep_class_x3_kernel<true>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab);
+                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, (const float*)amax_slot);
+    else if (x3)
+      hipLaunchKernelGGL(prep_class_x3_kernel<false>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
+                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
+                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, (const float*)nullptr);
     else
       hipLaunchKernelGGL(prep_class_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, pass == kData ? 1 : 0,
                          Wp, ktab);
     GatherArgs a{};
     a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.zero = zero; a.Y = Y;
+    a.amax_a = amax_a; a.amax_w = amax_slot;
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
@@ -1219,17 +1257,19 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
         }
       } else if (x3) {
         const int terms = bf1 ? 1 : 3;
-#define SE_X3_LAUNCH(T, NWV)                                                                            \
-  do {                                                                                                 \
-    if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, T, 1, NWV>), grid, blk, 0, st, a);         \
-    else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, T, 2, NWV>), grid, blk, 0, st, a);   \
-    else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, T, 0, NWV>), grid, blk, 0, st, a);         \
-    else hipLaunchKernelGGL((gather_x3_kernel<false, T, 0, NWV>), grid, blk, 0, st, a);                \
+#define SE_X3_LAUNCH(T, NWV, F)                                                                            \
+  do {                                                                                                    \
+    if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, T, 1, NWV, F>), grid, blk, 0, st, a);         \
+    else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, T, 2, NWV, F>), grid, blk, 0, st, a);   \
+    else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, T, 0, NWV, F>), grid, blk, 0, st, a);         \
+    else hipLaunchKernelGGL((gather_x3_kernel<false, T, 0, NWV, F>), grid, blk, 0, st, a);                \
   } while (0)
-        if (terms == 1 && wide) SE_X3_LAUNCH(1, 2);
-        else if (terms == 1) SE_X3_LAUNCH(1, 1);
-        else if (wide) SE_X3_LAUNCH(3, 2);
-        else SE_X3_LAUNCH(3, 1);
+        if (f16 && wide) SE_X3_LAUNCH(3, 2, true);
+        else if (f16) SE_X3_LAUNCH(3, 1, true);
+        else if (terms == 1 && wide) SE_X3_LAUNCH(1, 2, false);
+        else if (terms == 1) SE_X3_LAUNCH(1, 1, false);
+        else if (wide) SE_X3_LAUNCH(3, 2, false);
+        else SE_X3_LAUNCH(3, 1, false);
 #undef SE_X3_LAUNCH
       } else if (ldw == 64) {
         dim3 grid(se::ceil_div(M, 256), 1);
@@ -1251,6 +1291,13 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+extern "C" int se_amax(const float* x, long long n, float* amax, void* stream) {
+  if (!x || !amax || n < 0) return SE_E_ARG;
+  launch_amax(x, n, amax, se::as_stream(stream));
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
 extern "C" int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w) {
   ConvGeom g;
   const int rc = geom_of(d, g);
@@ -1303,7 +1350,8 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   const long long QQw = (long long)w.Qh * w.Qw;
   const long long span_w = (w.m_per_split + QQw - 1) / QQw + 1;
   // the split-bf16 / bf16 tile reads D rows in blocks of 16 (N % 16 == 0)
-  const bool split_ok = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16) && w.N % 16 == 0;
+  const bool split_ok = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3) &&
+                        w.N % 16 == 0;
   if (jn) {
     const int dcpb = 2 * jn->jh;
     const bool tu = g.transposed && (w.Cg % 128 == 0) &&
@@ -1314,8 +1362,9 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   }
   char* p = align256((char*)ws);
   const float* zero = (const float*)p;
-  (void)hipMemsetAsync(p, 0, kZeroBytes, st);
-  p = align256(p + kZeroBytes);
+  float* amax_slot = (float*)(p + kZeroBytes);   // [0] x (joined: x and s), [1] dy
+  (void)hipMemsetAsync(p, 0, kZeroBytes + kAmaxBytes, st);
+  p = align256(p + kZeroBytes + kAmaxBytes);
   float* slab = (float*)p;
   p = align256(p + (size_t)w.splits * w.c.Kp * w.Np * sizeof(float));
   int4* ktab = (int4*)p;
@@ -1338,6 +1387,26 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   if (jn) {
     a.D = jn->s; a.D2 = jn->x2; a.djh = jn->jh; a.DH2 = jn->h2; a.DW2 = jn->w2;
   }
+  const bool f16 = split_ok && g.math == SE_MATH_F16X3 && w.N > 32;
+  if (f16) {   // scale sources of x (conv input) and dy, unless the caller has them
+    const float* xa = g.x_amax;
+    const float* da = g.dy_amax;
+    if (!xa) {
+      if (jn) {
+        launch_amax(jn->s, (long long)g.B * 2 * jn->jh * g.Hi * g.Wi, amax_slot, st);
+        launch_amax(jn->x2, (long long)g.B * 2 * jn->jh * jn->h2 * jn->w2, amax_slot, st);
+      } else {
+        launch_amax(x, (long long)g.B * g.Ci * g.Hi * g.Wi, amax_slot, st);
+      }
+      xa = amax_slot;
+    }
+    if (!da) {
+      launch_amax(dy, (long long)g.B * g.Co * g.Ho * g.Wo, amax_slot + 1, st);
+      da = amax_slot + 1;
+    }
+    a.amax_g = g.transposed ? da : xa;
+    a.amax_d = g.transposed ? xa : da;
+  }
   const bool tu = (w.Cg % 128 == 0) && span_w * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
                   span_w * (long long)w.Np * QQw * 4 < (1ll << 31);
   if (w.N <= kSmallWgradN) {
@@ -1348,6 +1417,11 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     dim3 grid(w.c.Kp / 128, 1, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
+  } else if (f16) {
+    dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
+    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true>), grid, dim3(kThreads), 0, st, a);
+    else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true>), grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.math == SE_MATH_BF16X3) {
     dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true>), grid, dim3(kThreads), 0, st, a);

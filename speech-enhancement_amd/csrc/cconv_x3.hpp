@@ -32,6 +32,84 @@ __device__ __forceinline__ unsigned short bf16_bits(float x) {
   return __builtin_bit_cast(unsigned short, (__bf16)x);
 }
 
+// ---------------------------------------------------------------------------
+// Scaled split-fp16 ("f16x3", SE_MATH_F16X3). fp16 keeps 11 significant bits
+// (bf16: 8), so hi + lo carry 22 bits and the dropped lo*lo term is ~2^-22
+// relative: fp32-class products at the cost of bf16x3. fp16's narrow exponent
+// range is handled by a per-tensor power-of-two scale s = 2^(kF16Top - e),
+// max|x| < 2^e, so every scaled value is below 2^14 (fp16 max 65504) and
+// values down to 2^-17 max|x| keep a normal lo part. Scaling by a power of
+// two is exact; the accumulator is multiplied back by 2^(ea + eb - 2 kF16Top)
+// (v_ldexp_f32, exact) in the epilogue.
+// ---------------------------------------------------------------------------
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+constexpr int kF16Top = 14;
+
+// e with *amax < 2^e (from the fp32 exponent field; 0 and denormals -> -126),
+// clamped so that 2^(kF16Top - e) is a normal float
+__device__ __forceinline__ int amax_exp(const float* amax) {
+  const unsigned bits = __builtin_bit_cast(unsigned, *amax) & 0x7fffffffu;
+  const int e = (int)(bits >> 23) - 126;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
+__device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }
+
+// (x0, x1) * s -> packed fp16 hi pair and lo pair (element 0 in the low half);
+// v_cvt_pk_f16_f32 rounds to nearest even, s * x - hi is one exact FMA
+__device__ __forceinline__ void split_f16x2(float x0, float x1, float s, unsigned& hi, unsigned& lo) {
+  const f32x2 v = (f32x2){x0, x1} * s;
+  const f16x2 h = __builtin_convertvector(v, f16x2);
+  hi = __builtin_bit_cast(unsigned, h);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2));
+}
+
+// one 32x32x16 MFMA on a pair of 16-B operand fragments: fp16 or bf16 elements
+template <bool F16>
+__device__ __forceinline__ f32x16 mfma_32x32x16(u32x4 a, u32x4 b, f32x16 c) {
+  if constexpr (F16)
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b),
+                                                  c, 0, 0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b),
+                                                   c, 0, 0, 0);
+}
+
+// split of an operand pair into (hi, lo) planes: bf16, or scaled fp16
+template <bool F16>
+__device__ __forceinline__ void split2(float x0, float x1, float s, unsigned& hi, unsigned& lo) {
+  if constexpr (F16) split_f16x2(x0, x1, s, hi, lo);
+  else split_bf16x2(x0, x1, hi, lo);
+}
+
+// Per-tensor max |x| (SE_MATH_F16X3 scale source): atomic max of the fp32
+// bit patterns (non-negative floats order as unsigned ints) into *out, which
+// the caller zeroes first. Vectorised when x is 16-B aligned.
+__global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, long long n, unsigned* out) {
+  float m = 0.f;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i0 = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (((unsigned long long)x & 15) == 0) {
+    const long long n4 = n >> 2;
+    const f32x4* x4 = reinterpret_cast<const f32x4*>(x);
+    for (long long i = i0; i < n4; i += stride) {
+      const f32x4 v = x4[i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(v[0]), fabsf(v[1])), fmaxf(fabsf(v[2]), fabsf(v[3]))));
+    }
+    for (long long i = 4 * n4 + i0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  } else {
+    for (long long i = i0; i < n; i += stride) m = fmaxf(m, fabsf(x[i]));
+  }
+  // (a NaN element is dropped by fmaxf; it still poisons the GEMM itself)
+  unsigned b = __builtin_bit_cast(unsigned, m);
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const unsigned v = __shfl_xor(b, o);
+    b = v > b ? v : b;
+  }
+  if ((threadIdx.x & 63) == 0 && b) atomicMax(out, b);
+}
+
 // LDS / pre-tiled weight image of one operand tile: [plane (hi, lo)][row][4
 // chunks of 8 bf16 = 16 B], chunk c of row `row` stored at c ^ ((row >> 2) & 3).
 // 64-B rows, XOR swizzle: ds_read_b128 fragment reads (lane -> row r, chunk
@@ -61,10 +139,13 @@ constexpr int kX3TileU4 = 2 * 128 * 4;   // u32x4 per (k-step, n-tile) weight im
 // Pre-tiled split weight: Wt[(s * NT + t) * kX3TileU4 + (plane * 128 + n) * 4 + x3_chunk(n, c)]
 // holds bf16 element e of k = 32 s + 8 c + e, column n0 = 128 t + n. Also ktab
 // (as prep_class_kernel).
+// F16: scaled split-fp16 planes (amax_w = max |weight|, see amax_exp)
+template <bool F16 = false>
 __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, int Kp, int NT,
                                      int Hi, int Wi, int data_grad, int kblk, unsigned short* Wt,
-                                     int4* ktab) {
+                                     int4* ktab, const float* amax_w) {
   const int K = taps.n * Cg;
+  const float sw = F16 ? pow2f(kF16Top - amax_exp(amax_w)) : 1.f;
   const long long total = (long long)Kp * NT * 128;   // one thread per (k, n)
   for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
@@ -77,8 +158,17 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
       const int ci = data_grad ? n : c, co = data_grad ? c : n;
       v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
     }
-    const float h = (float)(__bf16)v;
-    const unsigned short hb = bf16_bits(v), lb = bf16_bits(v - h);
+    unsigned short hb, lb;
+    if constexpr (F16) {
+      const float vs = v * sw;
+      const _Float16 h16 = (_Float16)vs;
+      hb = __builtin_bit_cast(unsigned short, h16);
+      lb = __builtin_bit_cast(unsigned short, (_Float16)(vs - (float)h16));
+    } else {
+      const float h = (float)(__bf16)v;
+      hb = bf16_bits(v);
+      lb = bf16_bits(v - h);
+    }
     const int s = k >> 5, kc = (k >> 3) & 3, e = k & 7;
     const int tn = n >> 7, nl = n & 127;
     const long long base = ((long long)s * NT + tn) * kX3TileU4 * 8;   // in bf16 units
@@ -118,10 +208,13 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // NW: 128-column weight tiles per workgroup. NW = 2 is a 256 (n) x 128 (m)
 // tile of 8 waves (one workgroup per CU): each gathered activation is loaded
 // and split once per 256 output columns instead of once per 128.
-template <bool TU, int TERMS = 3, int JM = 0, int NW = 1>
+// F16: scaled split-fp16 operands (SE_MATH_F16X3; a.amax_a / a.amax_w give the
+// per-tensor scales of the gathered tensor and the weights).
+template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false>
 __global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
+  static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
   static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
   static_assert(NW == 1 || NW == 2, "128 or 256 columns per workgroup");
   constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
@@ -153,6 +246,13 @@ gather_x3_kernel(const GatherArgs a) {
     hb = qh * a.sh;
     wb = qw * a.sw;
     xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
+  }
+  float sa = 1.f;   // F16: activation scale; the epilogue multiplies by 2^ush
+  int ush = 0;
+  if constexpr (F16) {
+    const int ea = amax_exp(a.amax_a);
+    sa = pow2f(kF16Top - ea);
+    ush = ea + amax_exp(a.amax_w) - 2 * kF16Top;
   }
   struct Stage { float ra[AJ]; u32x4 rw[4]; };
   Stage s0, s1;
@@ -229,7 +329,7 @@ gather_x3_kernel(const GatherArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         unsigned h, l;
-        split_bf16x2(st.ra[8 * q + 2 * e], st.ra[8 * q + 2 * e + 1], h, l);
+        split2<F16>(st.ra[8 * q + 2 * e], st.ra[8 * q + 2 * e + 1], sa, h, l);
         H[e] = h;
         L[e] = l;
       }
@@ -277,9 +377,7 @@ gather_x3_kernel(const GatherArgs a) {
         for (int i = 0; i < RN; ++i)
 #pragma unroll
           for (int j = 0; j < RM; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(
-                __builtin_bit_cast(bf16x8, wf[ks][i][t == 2 ? 1 : 0]),
-                __builtin_bit_cast(bf16x8, af[ks][j][t == 1 ? 1 : 0]), acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma_32x32x16<F16>(wf[ks][i][t == 2 ? 1 : 0], af[ks][j][t == 1 ? 1 : 0], acc[i][j]);
   };
   auto interleave = [&]() __attribute__((always_inline)) {
 #if SEHIP_IGLP
@@ -313,6 +411,14 @@ gather_x3_kernel(const GatherArgs a) {
     __syncthreads();
   }
   if (kt < nk) compute(0);
+  if constexpr (F16) {   // undo the operand scales (exact)
+#pragma unroll
+    for (int i = 0; i < RN; ++i)
+#pragma unroll
+      for (int j = 0; j < RM; ++j)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], ush);
+  }
 
   // --- epilogue (as gather_gemm_kernel) ---
   __syncthreads();
@@ -387,10 +493,12 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 }
 
 // DJ: D is the decoder skip join (WgradArgs::D2, a transposed conv's input).
-template <bool TU, int TERMS = 3, bool DJ = false>
+// F16: scaled split-fp16 operands (SE_MATH_F16X3; a.amax_g / a.amax_d).
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false>
 __global__ void __launch_bounds__(kThreads, 2)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
+  static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
   constexpr int BKO = 128, BNO = 128, WNn = 2, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
   constexpr int RJ = 16;                     // rows per thread per operand
@@ -414,6 +522,14 @@ wgrad_x3_kernel(const WgradArgs a) {
 
   for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab[k0 + i];
   __syncthreads();
+  float sg = 1.f, sd = 1.f;   // F16: operand scales; the slab gets acc * 2^ush
+  int ush = 0;
+  if constexpr (F16) {
+    const int eg = amax_exp(a.amax_g), ed = amax_exp(a.amax_d);
+    sg = pow2f(kF16Top - eg);
+    sd = pow2f(kF16Top - ed);
+    ush = eg + ed - 2 * kF16Top;
+  }
 
   int cb, cqh, cqw;
   {
@@ -526,9 +642,9 @@ wgrad_x3_kernel(const WgradArgs a) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         unsigned h, l;
-        split_bf16x2(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], h, l);
+        split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
         GH[e] = h; GL[e] = l;
-        split_bf16x2(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], h, l);
+        split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
         DH[e] = h; DL[e] = l;
       }
       const int off = wx3_off(ml, rbase / 8 + q);
@@ -581,8 +697,8 @@ wgrad_x3_kernel(const WgradArgs a) {
         for (int i = 0; i < RK; ++i)
 #pragma unroll
           for (int j = 0; j < RN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ga[i][t == 2 ? 1 : 0], gb[j][t == 1 ? 1 : 0],
-                                                                acc[i][j], 0, 0, 0);
+            acc[i][j] = mfma_32x32x16<F16>(__builtin_bit_cast(u32x4, ga[i][t == 2 ? 1 : 0]),
+                                           __builtin_bit_cast(u32x4, gb[j][t == 1 ? 1 : 0]), acc[i][j]);
     }
   };
   auto interleave = [&]() __attribute__((always_inline)) {
@@ -627,7 +743,7 @@ wgrad_x3_kernel(const WgradArgs a) {
       for (int r = 0; r < 16; ++r) {
         const int k = k0 + wk * TK + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * lk;
         const int n = n0 + wnn * TN + 32 * j + lc;
-        out[(long long)k * a.Np + n] = acc[i][j][r];
+        out[(long long)k * a.Np + n] = F16 ? __builtin_ldexpf(acc[i][j][r], ush) : acc[i][j][r];
       }
 }
 

@@ -34,10 +34,12 @@ class ConvDesc(ctypes.Structure):
         "batch", "in_channels", "in_h", "in_w", "out_channels",
         "kernel_h", "kernel_w", "stride_h", "stride_w", "pad_h", "pad_w",
         "dil_h", "dil_w", "out_pad_h", "out_pad_w", "transposed",
-        "complex_weights", "pad_h_end", "pad_w_end", "math")]
+        "complex_weights", "pad_h_end", "pad_w_end", "math")] + [
+        ("x_amax", c_void_p), ("dy_amax", c_void_p)]   # SE_MATH_F16X3 scale sources (or NULL)
 
 
 _P = c_void_p
+CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
     "se_abi_version": (c_int, []),
@@ -48,6 +50,7 @@ _SIGNATURES = {
     "se_istft_fwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
     "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
     "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
+    "se_amax": (c_int, [_P, ctypes.c_longlong, _P, _P]),
     "se_conv2d_workspace_size": (c_size_t, [_P]),
     "se_conv2d_fwd": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),
@@ -57,12 +60,12 @@ _SIGNATURES = {
     "se_conv2d_bwd_weight_joined": (c_int, [_P, _P, c_int, c_int] + [_P] * 6 + [_P, c_size_t, _P]),
     "se_cbn_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P,
-                           c_int, c_float, c_float, c_int, c_float, _P,
+                           c_int, c_float, c_float, c_int, c_float, _P, _P,
                            c_size_t, _P]),
     "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP,
-                           c_int, c_int, c_float, _P, c_size_t, _P]),
+                           c_int, c_int, c_float, _P, _P, c_size_t, _P]),
     "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP,
-                            c_int, c_int, c_float, _P, c_size_t, _P]),
+                            c_int, c_int, c_float, _P, _P, c_size_t, _P]),
     "se_lstm_supported": (c_int, [c_int]),
     "se_lstm_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P, _P] + [c_int] * 4
                     + [ctypes.c_uint, _P]),

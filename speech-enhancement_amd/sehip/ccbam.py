@@ -120,6 +120,9 @@ class _CCBAMFn(torch.autograd.Function):
         out = torch.empty_like(x)
         _call(lib.se_ccbam_apply, "se_ccbam_apply", x.data_ptr(), ca.data_ptr(), sa.data_ptr(),
               out.data_ptr(), B, C, HW, st)
+        xa = F.amax_get(x)
+        if xa is not None:   # ca, sa in (0, 1): |x ca + sa| <= max |x| + 1 (F16X3 scale source)
+            F.amax_put(out, xa + 1.0)
         if need_grad:
             ctx.save_for_backward(x, idx, amax)
             ctx.graphs = (pooled, ca, Pl, sa)

@@ -10,6 +10,7 @@ import contextlib
 import os
 
 import torch
+from torch.multiprocessing.reductions import StorageWeakRef
 
 from . import _native as N
 
@@ -118,9 +119,13 @@ _TIMER: OpTimer | None = None
 # "bf16x6" = three-way split, six terms (fp32-class); "bf16" = operands rounded
 # to bf16, one term (the low-precision configs' arithmetic: BASELINE configs
 # 2/3, judged against the fp32 oracle with the reference's own bf16 drift).
+# "f16x3" = per-tensor power-of-two scaled split-fp16 (hi + lo, three terms on
+# v_mfma_f32_32x32x16_f16): 22 significant bits per operand, fp32-class
+# (tests/test_gpu_conv_x3.py holds every pass at or below the exact-fp32 MFMA
+# path's error against fp64) at the MFMA cost of bf16x3.
 # Initial value from SEHIP_CONV_MATH ("f32", "bf16x3", or per pass as
 # "fwd=bf16x3,data=f32,weight=bf16x3"); set_conv_math() changes it.
-_MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2, "bf16": 3}
+_MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2, "bf16": 3, "f16x3": 4}
 _PASSES = ("fwd", "data", "weight")
 _CONV_MATH = {p: 0 for p in _PASSES}
 # Optional override for the forward passes of transposed convs (the decoder) whose
@@ -157,21 +162,13 @@ def set_conv_math(mode: str, **passes: str) -> None:
     _FWD_DEC[1] = dec_h
 
 
-# Default: three-way split (fp32-class) forward, two-way split data- and
-# weight-grad GEMMs. tools/grad_modes.py on the golden FRCRN train step:
-# bf16x3 in the two backward passes leaves the gradients as close to the fp64
-# oracle as the all-fp32 path (median 5.7e-5 vs 5.7e-5, worst tensor at 0.55
-# of its gate); in the forward, bf16x3's ~1e-5 activation perturbation moves
-# the ill-conditioned CBN parameter gradients past the per-tensor gate, while
-# bf16x6 (5.5e-7 per conv, below the fp32 MFMA path's 6.4e-7) keeps them there
-# (median 6.0e-5, worst 0.59).
-# The one exception is the last decoder layer's forward (input grid >= 158 rows:
-# FRCRN's dec5, 40 % of the forward FLOPs), whose output reaches the mask without
-# passing another CBN's statistics: bf16x3 there keeps every gradient inside its
-# gate (worst 0.52 of it, median 7.9e-5; bf16x3 from 77 rows on puts one CCBAM
-# CBN Wri past it) and the enhanced wav at 5.9e-6 of the oracle (1e-4 bar), for
-# +4.5 % utt/s (tools/gpu_fwd_dec.sh: 542.8 vs 519.3).
-DEFAULT_CONV_MATH = "fwd=bf16x6,data=bf16x3,weight=bf16x3,fwd_dec=bf16x3,fwd_dec_min_h=158"
+# Default: scaled split-fp16 on every pass. It is fp32-class: against fp64, each
+# pass at every FRCRN layer shape lands at 0.63-0.70x the exact-fp32 MFMA
+# path's own error (tests/test_gpu_conv_x3.py, test_gpu_cconv.py), at the MFMA
+# cost of bf16x3. The faster, coarser forms are opt-in (set_conv_math /
+# SEHIP_CONV_MATH): "bf16x3" (~7x the fp32 path's per-conv error), and "bf16"
+# (the low-precision configs' arithmetic).
+DEFAULT_CONV_MATH = "f16x3"
 set_conv_math(os.environ.get("SEHIP_CONV_MATH", DEFAULT_CONV_MATH))
 
 
@@ -185,6 +182,60 @@ def get_conv_math() -> str:
     if len(set(modes)) == 1:
         return modes[0]
     return ",".join(f"{p}={m}" for p, m in zip(_PASSES, modes))
+
+
+# --------------------------------------------------------------------------
+# Scale sources of the SE_MATH_F16X3 GEMMs: an upper bound of max |t| per
+# tensor (device fp32 [1]). Producers that pass over a tensor anyway register
+# one (ComplexBN forward: its output; ComplexBN backward: its input gradient,
+# which is the producing conv's dy; CCBAM: its output); a conv pass that finds
+# none computes it with se_amax (one read). Entries are keyed by the tensor's
+# address and hold only a weak reference to its storage: an entry matches a
+# tensor only while that storage is alive, with the same shape and version
+# counter, so neither reuse of freed memory nor an in-place write can pair a
+# tensor with a stale bound, and the table keeps nothing alive.
+# --------------------------------------------------------------------------
+F16X3 = 4
+_AMAX: dict = {}
+
+
+def amax_put(t: torch.Tensor, amax: torch.Tensor) -> None:
+    if len(_AMAX) > 256:
+        for k in [k for k, e in _AMAX.items() if e[1].expired()]:
+            del _AMAX[k]
+    _AMAX[t.data_ptr()] = (amax, StorageWeakRef(t.untyped_storage()), tuple(t.shape), t._version)
+
+
+def amax_get(t: torch.Tensor):
+    e = _AMAX.get(t.data_ptr())
+    if e is None or e[1].expired() or e[2] != tuple(t.shape) or e[3] != t._version:
+        return None
+    return e[0]
+
+
+def amax_of(t: torch.Tensor) -> torch.Tensor:
+    """The registered bound of max |t|, else max |t| computed now (and registered)."""
+    a = amax_get(t)
+    if a is None:
+        a = torch.zeros(1, device=t.device, dtype=torch.float32)
+        N.check(N.lib().se_amax(t.data_ptr(), t.numel(), a.data_ptr(), N.stream_of(t)), "se_amax")
+        amax_put(t, a)
+    return a
+
+
+def new_amax(device) -> torch.Tensor:
+    return torch.empty(1, device=device, dtype=torch.float32)
+
+
+def _f16_operands(d):
+    """(x, dy) -> whether a SE_MATH_F16X3 GEMM of this conv reads that operand's
+    scale: the split kernels' shape rules of cconv.hip (gather N > 64, weight-grad
+    N > 32 and N % 16 == 0)."""
+    fwd = _pass_math("fwd", d) == F16X3 and d.out_channels > 64
+    data = _pass_math("data", d) == F16X3 and d.in_channels > 64
+    n = d.in_channels if d.transposed else d.out_channels
+    wgt = _CONV_MATH["weight"] == F16X3 and n > 32 and n % 16 == 0
+    return fwd or wgt, data or wgt
 
 
 def _pass_math(pass_name, d) -> int:
@@ -267,6 +318,8 @@ class _Conv2d(torch.autograd.Function):
         y = torch.empty((x.shape[0], out_channels, ho.value, wo.value), device=x.device, dtype=x.dtype)
         nbytes = lib.se_conv2d_workspace_size(N.ctypes.byref(d))
         ws = _workspace(nbytes, x.device)
+        xa = amax_of(x) if _f16_operands(d)[0] else None
+        d.x_amax = N.ptr(xa)
         t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_conv2d_fwd(_with_math(d, "fwd"), x.data_ptr(), wr.data_ptr(), N.ptr(wi),
                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(),
@@ -275,7 +328,7 @@ class _Conv2d(torch.autograd.Function):
             _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
                        4.0 * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
         ctx.save_for_backward(x, wr, wi)
-        ctx.desc, ctx.nbytes, ctx.has_bias = d, nbytes, br is not None
+        ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax = d, nbytes, br is not None, xa
         return y
 
     @staticmethod
@@ -284,6 +337,8 @@ class _Conv2d(torch.autograd.Function):
         gy = gy.contiguous()
         d, lib = ctx.desc, N.lib()
         ws = _workspace(ctx.nbytes, gy.device)
+        ga = amax_of(gy) if _f16_operands(d)[1] else None
+        d.x_amax, d.dy_amax = N.ptr(ctx.x_amax), N.ptr(ga)
         dx = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
@@ -295,9 +350,11 @@ class _Conv2d(torch.autograd.Function):
                 _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
                            4.0 * (gy.numel() + dx.numel() + wr.numel() * (2 if wi is not None else 1)))
         if any(ctx.needs_input_grad[1:5]):
-            with _wgrad_stream(x, gy):
+            with _wgrad_stream(x, gy, ctx.x_amax, ga):
                 if _DEFER is not None:
                     ws = _workspace(ctx.nbytes, gy.device)
+                if ctx.x_amax is None and _f16_operands(d)[0]:   # mode changed since forward
+                    d.x_amax = N.ptr(amax_of(x))
                 dwr = torch.empty_like(wr)
                 dwi = torch.empty_like(wi) if wi is not None else None
                 if ctx.has_bias:
@@ -354,6 +411,9 @@ class _ConvJoined(torch.autograd.Function):
         nbytes = lib.se_conv2d_workspace_size(N.ctypes.byref(d))
         ws = _workspace(nbytes, x.device)
         st = N.stream_of(x)
+        # scale source of the joined input: max of the two sources' bounds
+        xa = torch.maximum(amax_of(x), amax_of(s)) if _f16_operands(d)[0] else None
+        d.x_amax = N.ptr(xa)
         t0 = _TIMER.begin() if _TIMER else None
         rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
                                       wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(),
@@ -366,7 +426,7 @@ class _ConvJoined(torch.autograd.Function):
             _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
                        4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
         ctx.save_for_backward(x, s, wr, wi)
-        ctx.desc, ctx.nbytes, ctx.has_bias = d, nbytes, br is not None
+        ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax = d, nbytes, br is not None, xa
         return y
 
     @staticmethod
@@ -377,6 +437,11 @@ class _ConvJoined(torch.autograd.Function):
         Fx, Tx = x.shape[2], x.shape[3]
         ws = _workspace(ctx.nbytes, gy.device)
         st = N.stream_of(gy)
+        ga = amax_of(gy) if _f16_operands(d)[1] else None
+        xa = ctx.x_amax
+        if xa is None and _f16_operands(d)[0]:   # mode changed since forward
+            xa = torch.maximum(amax_of(x), amax_of(s))
+        d.x_amax, d.dy_amax = N.ptr(xa), N.ptr(ga)
         gx = gs = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             gx, gs = torch.empty_like(x), torch.empty_like(s)
@@ -394,7 +459,7 @@ class _ConvJoined(torch.autograd.Function):
                 _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
                            4.0 * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))
         if any(ctx.needs_input_grad[2:6]):
-            with _wgrad_stream(x, s, gy):
+            with _wgrad_stream(x, s, gy, xa, ga):
                 if _DEFER is not None:
                     ws = _workspace(ctx.nbytes, gy.device)
                 st = N.stream_of(gy)
@@ -455,17 +520,20 @@ class _ComplexBN(torch.autograd.Function):
         b, c = x.shape[:2]
         hw = x[0, 0].numel()
         y = torch.empty_like(x)
-        save = torch.empty(16 * (c // 2), device=x.device, dtype=torch.float32)
+        save = torch.empty(N.CBN_SAVE_FLOATS * (c // 2), device=x.device, dtype=torch.float32)
         params = (wrr, wri, wii, br, bi) if wrr is not None else None
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
         mom = -1.0 if momentum is None else float(momentum)
+        ya = new_amax(x.device) if training else None   # bound of max |y| (F16X3 consumers)
         t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
                                N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
                                save.data_ptr(), int(training), float(eps), mom, int(act),
-                               float(slope), ws.data_ptr(), ws.numel(), N.stream_of(x)),
+                               float(slope), N.ptr(ya), ws.data_ptr(), ws.numel(), N.stream_of(x)),
                 "se_cbn_fwd")
+        if ya is not None:
+            amax_put(y, ya)
         if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write
             _TIMER.end("cbn_fwd", t0, 0.0, 4.0 * x.numel() * (3 if training else 2))
         ctx.save_for_backward(x, save, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
@@ -491,17 +559,20 @@ class _ComplexBN(torch.autograd.Function):
         dparams = [torch.empty_like(p) for p in params] if affine else None
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
+        dxa = new_amax(x.device) if training else None   # bound of max |dx| (the conv's dy)
         t0 = _TIMER.begin() if _TIMER else None
         if gy2 is None:
             N.check(lib.se_cbn_bwd(gy.data_ptr(), None, x.data_ptr(), dx.data_ptr(), b, c, hw,
                                    N.ptr_array(params if affine else None), save.data_ptr(),
-                                   N.ptr_array(dparams), training, act, slope, ws.data_ptr(),
-                                   ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
+                                   N.ptr_array(dparams), training, act, slope, N.ptr(dxa),
+                                   ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
         else:
             N.check(lib.se_cbn_bwd2(gy.data_ptr(), gy2.data_ptr(), x.data_ptr(), dx.data_ptr(), b,
                                     c, hw, N.ptr_array(params if affine else None),
                                     save.data_ptr(), N.ptr_array(dparams), training, act, slope,
-                                    ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd2")
+                                    N.ptr(dxa), ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd2")
+        if dxa is not None:
+            amax_put(dx, dxa)
         if t0 is not None:   # (gy [, gy2], x) read twice + dx written
             _TIMER.end("cbn_bwd", t0, 0.0, 4.0 * x.numel() * (5 if gy2 is None else 7))
         g = dparams or [None] * 5

@@ -77,6 +77,40 @@ def test_cbn_whitening_full_size(gpu_device):
     assert (yr * yi).mean(dim=(0, 2, 3)).abs().max() < 1e-3
 
 
+@pytest.mark.parametrize("act", [0, 1, 2])
+def test_cbn_amax_bounds(act, gpu_device):
+    """The SE_MATH_F16X3 scale sources se_cbn_fwd / se_cbn_bwd emit with no extra
+    pass: an upper bound of max |y| and of max |dx| (never below the true
+    maximum, at most a small factor above it)."""
+    from sehip import functional as F
+    from sehip.complex_nn import ComplexBatchNorm2d
+    seen = {}
+
+    class Probe(torch.autograd.Function):   # sees dx with the address the CBN backward registered
+        @staticmethod
+        def forward(ctx, t):
+            return t.view(t.shape)
+
+        @staticmethod
+        def backward(ctx, g):
+            seen["dx"], seen["dx_amax"] = g.clone(), F.amax_get(g)
+            return g
+
+    m = paramfill.fill_(ComplexBatchNorm2d(128), seed=3).cuda().train()
+    gen = torch.Generator(device=gpu_device).manual_seed(9)
+    x = (torch.randn(4, 128, 37, 50, device=gpu_device, generator=gen) * 3 + 0.5).requires_grad_(True)
+    y = m.forward_act(Probe.apply(x), act, 0.2)
+    ya = F.amax_get(y)
+    assert ya is not None
+    true_y = y.detach().abs().max().item()
+    assert true_y <= ya.item() <= 4 * true_y, (true_y, ya.item())
+    gy = torch.randn(y.shape, device=gpu_device, generator=gen) * 1e-7
+    y.backward(gy)
+    assert seen["dx_amax"] is not None
+    true_dx = seen["dx"].abs().max().item()
+    assert true_dx <= seen["dx_amax"].item() <= 16 * true_dx, (true_dx, seen["dx_amax"].item())
+
+
 @pytest.mark.parametrize("used", ["both", "first", "second"])
 def test_cbn_fork_sums_both_gradients(used, gpu_device):
     """fork=True (FRCRN encoder outputs: next conv + decoder skip) sums the two output

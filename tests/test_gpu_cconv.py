@@ -76,23 +76,37 @@ FRCRN_LAYERS = [
 ]
 
 
+# fp32-class modes at 1e-5 against the fp64 oracle; bf16x3 (two-term split bf16) at 3e-5
+MATH_TOL = {"f32": 1e-5, "f16x3": 1e-5, "bf16x6": 1e-5, "bf16x3": 3e-5}
+
+
+@pytest.mark.parametrize("math", sorted(MATH_TOL))
 @pytest.mark.parametrize("name,tr,cin,cout,shape", FRCRN_LAYERS)
-def test_frcrn_layer_vs_oracle(name, tr, cin, cout, shape, gpu_device):
+def test_frcrn_layer_vs_oracle(name, tr, cin, cout, shape, math, gpu_device):
+    """Every FRCRN encoder/decoder layer shape, every pass, each MFMA form
+    against the fp64 oracle (bf16x6 has no weight-grad kernel: f32 there)."""
     from sehip import functional as F
     cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
-    m = paramfill.fill_(cls(cin, cout, (5, 2), stride=(2, 1), bias=False), seed=7)
+    m = paramfill.fill_(cls(cin, cout, (5, 2), stride=(2, 1), bias=False), seed=7).double()
     gen = torch.Generator().manual_seed(3)
-    x = torch.randn(*shape, generator=gen)
+    x = torch.randn(*shape, generator=gen, dtype=torch.float64)
     xo = x.clone().requires_grad_(True)
     yo = m(xo)
-    gy = torch.randn(yo.shape, generator=gen)
+    gy = torch.randn(yo.shape, generator=gen, dtype=torch.float64)
     yo.backward(gy)
-    r = _run(F, m, x, gy, tr, dict(stride=(2, 1)))
-    assert rel_l2(r["y"].numpy(), yo.detach().numpy()) < 1e-5
-    assert rel_l2(r["dwr"].numpy(), m.real_conv.weight.grad.numpy()) < 1e-5
-    assert rel_l2(r["dwi"].numpy(), m.imag_conv.weight.grad.numpy()) < 1e-5
-    if name != "enc0":
-        assert rel_l2(r["dx"].numpy(), xo.grad.numpy()) < 1e-5
+    ref = dict(y=yo.detach().numpy(), dx=xo.grad.numpy(), dwr=m.real_conv.weight.grad.numpy().copy(),
+               dwi=m.imag_conv.weight.grad.numpy().copy())
+    prev = F.get_conv_math()
+    try:
+        F.set_conv_math(math if math != "bf16x6" else "fwd=bf16x6,data=bf16x6,weight=f32")
+        r = _run(F, m.float(), x.float(), gy.float(), tr, dict(stride=(2, 1)))
+    finally:
+        F.set_conv_math(prev)
+    tol = MATH_TOL[math]
+    errs = {k: rel_l2(r[k].numpy(), ref[k]) for k in ("y", "dwr", "dwi") + (("dx",) if name != "enc0" else ())}
+    print(name, math, {k: f"{v:.2e}" for k, v in errs.items()})
+    for k, e in errs.items():
+        assert e < tol, (name, math, k, e)
 
 
 @pytest.mark.parametrize("input_pad", [(1, 0, 0, 0), (2, 1, 1, 3), (0, 3, 2, 0)])

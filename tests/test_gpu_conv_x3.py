@@ -1,11 +1,16 @@
-"""GPU parity of the split-bf16 conv GEMMs ("bf16x3", se_conv2d_desc.math = 1;
-"bf16x6", math = 2): FRCRN layer geometries and the golden conv cases against the fp64
-oracle (complex_nn.py:52-91 in the reference's four-real-conv form).
+"""GPU parity of the split conv GEMMs against the fp64 oracle
+(complex_nn.py:52-91 in the reference's four-real-conv form) at FRCRN layer
+geometries and the golden conv cases, every pass (y, dx, dwr, dwi):
 
-bf16x3 drops the lo*lo term and rounds lo to bf16: <= ~2^-15 relative per
-product, ~6e-6 rms on random data. Gate: rel-L2 < 3e-5 per tensor, and
-within 30x of the exact-fp32 path's own error against fp64. bf16x6 (three-way
-split, six terms) must be within 3x of the exact-fp32 path."""
+* "f32" (math 0, v_mfma_f32_32x32x2_f32): the exact-fp32 path, pinned
+  absolutely at rel-L2 < 1e-5.
+* "f16x3" (math 4, scaled split-fp16, three terms): fp32-class — at or below
+  1.25x the exact-fp32 path's own error (and < 1e-5), and scale-invariant
+  (inputs scaled by 2^-40 .. 2^30 keep that error).
+* "bf16x6" (math 2, three-way split bf16, six terms; gather passes): within 3x
+  of the exact-fp32 path.
+* "bf16x3" (math 1): drops lo*lo and rounds lo to bf16, <= ~2^-15 relative per
+  product, ~6e-6 rms: rel-L2 < 3e-5 and within 30x of the exact-fp32 path."""
 import pytest
 import torch
 
@@ -43,30 +48,60 @@ def _hip(F, m, x, gy, transposed, stride, math):
         F.set_conv_math(prev)
 
 
-@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", LAYERS)
-def test_bf16x3_layer_vs_fp64_oracle(name, tr, cin, cout, shape, stride, gpu_device):
-    from sehip import functional as F
+def _fp64_ref(name, tr, cin, cout, shape, stride, x_scale=1.0, gy_scale=1.0):
     cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
     m = paramfill.fill_(cls(cin, cout, (5, 2), stride=stride, bias=False), seed=7).double()
     gen = torch.Generator().manual_seed(3)
-    x = torch.randn(*shape, generator=gen, dtype=torch.float64)
+    x = torch.randn(*shape, generator=gen, dtype=torch.float64) * x_scale
     xo = x.clone().requires_grad_(True)
     yo = m(xo)
-    gy = torch.randn(yo.shape, generator=gen, dtype=torch.float64)
+    gy = torch.randn(yo.shape, generator=gen, dtype=torch.float64) * gy_scale
     yo.backward(gy)
     ref = dict(y=yo.detach(), dx=xo.grad, dwr=m.real_conv.weight.grad, dwi=m.imag_conv.weight.grad)
+    return m, x, gy, ref
+
+
+F16_VS_F32 = 1.25   # f16x3 error may exceed the exact-fp32 path's by at most 25 %
+
+
+@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", LAYERS)
+def test_split_layer_vs_fp64_oracle(name, tr, cin, cout, shape, stride, gpu_device):
+    from sehip import functional as F
+    m, x, gy, ref = _fp64_ref(name, tr, cin, cout, shape, stride)
     exact = _hip(F, m, x, gy, tr, stride, "f32")
     split = _hip(F, m, x, gy, tr, stride, "bf16x3")
     split6 = _hip(F, m, x, gy, tr, stride, "fwd=bf16x6,data=bf16x6,weight=f32")
+    f16 = _hip(F, m, x, gy, tr, stride, "f16x3")
     for k, r in ref.items():
         e32 = rel_l2(exact[k].numpy(), r.numpy())
         ex3 = rel_l2(split[k].numpy(), r.numpy())
         ex6 = rel_l2(split6[k].numpy(), r.numpy())
-        print(f"{name} {k}: f32 {e32:.2e}  bf16x3 {ex3:.2e}  bf16x6 {ex6:.2e}")
+        e16 = rel_l2(f16[k].numpy(), r.numpy())
+        print(f"{name} {k}: f32 {e32:.2e}  f16x3 {e16:.2e}  bf16x6 {ex6:.2e}  bf16x3 {ex3:.2e}")
+        assert e32 < 1e-5, (name, k, e32)                       # the exact-fp32 path, absolutely
+        assert e16 < 1e-5 and e16 <= max(F16_VS_F32 * e32, 1e-7), (name, k, e16, e32)
         assert ex3 < TOL, (name, k, ex3)
         assert ex3 < max(30 * e32, 1e-6), (name, k, ex3, e32)
         # three-way split: fp32-class (within 3x of the exact-fp32 MFMA path)
         assert ex6 < max(3 * e32, 1e-6), (name, k, ex6, e32)
+
+
+@pytest.mark.parametrize("x_scale,gy_scale", [(2.0 ** -40, 2.0 ** -30), (2.0 ** 30, 2.0 ** 20),
+                                              (1.0, 2.0 ** -60)])
+@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", [LAYERS[1], LAYERS[3]])
+def test_f16x3_is_scale_invariant(name, tr, cin, cout, shape, stride, x_scale, gy_scale, gpu_device):
+    """The per-tensor power-of-two scales keep fp16's exponent range out of the
+    result: activations and gradients of any magnitude (SI-SNR gradients reach
+    1e-9 and below) keep the fp32-class error."""
+    from sehip import functional as F
+    m, x, gy, ref = _fp64_ref(name, tr, cin, cout, shape, stride, x_scale, gy_scale)
+    exact = _hip(F, m, x, gy, tr, stride, "f32")
+    f16 = _hip(F, m, x, gy, tr, stride, "f16x3")
+    for k, r in ref.items():
+        e32 = rel_l2(exact[k].numpy(), r.numpy())
+        e16 = rel_l2(f16[k].numpy(), r.numpy())
+        print(f"{name} x*{x_scale:.1e} gy*{gy_scale:.1e} {k}: f32 {e32:.2e}  f16x3 {e16:.2e}")
+        assert e16 < 1e-5 and e16 <= max(F16_VS_F32 * e32, 1e-7), (name, k, e16, e32)
 
 
 BF16_TOL = 1e-2   # one bf16 rounding per operand: ~2^-9 relative, rms ~3e-3 on random data

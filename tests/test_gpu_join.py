@@ -59,6 +59,50 @@ def test_joined_conv_matches_materialised_join(gpu_device, xs, ss, math):
         F.set_conv_math(prev)
 
 
+JOIN_TOL = {"f32": 1e-5, "f16x3": 1e-5, "fwd=bf16x6,data=bf16x3,weight=bf16x3": 3e-5, "bf16x3": 3e-5}
+
+
+@pytest.mark.parametrize("math", sorted(JOIN_TOL))
+@pytest.mark.parametrize("xs,ss", [((2, 128, 17, 41), (2, 128, 17, 40)),     # dec3-like: time crop
+                                   ((2, 128, 77, 41), (2, 128, 78, 40))])    # dec5-like: crop + freq pad
+def test_joined_conv_vs_fp64_oracle(gpu_device, xs, ss, math):
+    """The joined decoder passes (forward, both input gradients, both weight
+    gradients) against the fp64 oracle of the reference's trim / pad /
+    complex_concat + ComplexConvTranspose2d (frcrn.py:93-101), per MFMA form:
+    fp32-class forms at 1e-5, the bf16x3 passes at 3e-5."""
+    from oracle import complex_nn as O_cnn
+    import paramfill
+    from conftest import rel_l2
+    from sehip import functional as F
+    cin, cout = 2 * xs[1], 128
+    m = paramfill.fill_(O_cnn.ComplexConvTranspose2d(cin, cout, (5, 2), stride=(2, 1), bias=False), seed=4).double()
+    gen = torch.Generator().manual_seed(2)
+    x = torch.randn(xs, generator=gen, dtype=torch.float64)
+    s = torch.randn(ss, generator=gen, dtype=torch.float64)
+    xo, so = x.clone().requires_grad_(True), s.clone().requires_grad_(True)
+    yo = m(_ref(xo, so))
+    g = torch.randn(yo.shape, generator=gen, dtype=torch.float64)
+    yo.backward(g)
+    ref = dict(y=yo.detach(), dx=xo.grad, ds=so.grad, dwr=m.real_conv.weight.grad, dwi=m.imag_conv.weight.grad)
+    prev = F.get_conv_math()
+    F.set_conv_math(math)
+    try:
+        xa = x.float().to(gpu_device).requires_grad_(True)
+        sa = s.float().to(gpu_device).requires_grad_(True)
+        wr = m.real_conv.weight.detach().float().to(gpu_device).requires_grad_(True)
+        wi = m.imag_conv.weight.detach().float().to(gpu_device).requires_grad_(True)
+        y = F.conv2d_joined(xa, sa, wr, wi, out_channels=cout, kernel=(5, 2), stride=(2, 1), transposed=True)
+        y.backward(g.float().to(gpu_device))
+        torch.cuda.synchronize()
+        got = dict(y=y.detach(), dx=xa.grad, ds=sa.grad, dwr=wr.grad, dwi=wi.grad)
+    finally:
+        F.set_conv_math(prev)
+    for k, r in ref.items():
+        e = rel_l2(got[k].cpu().numpy(), r.numpy())
+        print(math, xs, k, f"{e:.2e}")
+        assert e < JOIN_TOL[math], (math, k, e)
+
+
 def test_joined_entry_points_run_their_own_kernels(gpu_device):
     """bf16x3 / bf16x6 / bf16 have joined kernels (rc 0, no fallback); f32 reports
     SE_E_UNSUPPORTED so the host materialises the join."""
@@ -75,7 +119,7 @@ def test_joined_entry_points_run_their_own_kernels(gpu_device):
     y = torch.empty(B, 128, ho.value, wo.value, device=gpu_device)
     ws = torch.empty(lib.se_conv2d_workspace_size(ctypes.byref(d)), dtype=torch.uint8, device=gpu_device)
     st = N.stream_of(y)
-    for mode, want in (("bf16x3", 0), ("bf16x6", 0), ("bf16", 0), ("f32", -3)):
+    for mode, want in (("bf16x3", 0), ("bf16x6", 0), ("bf16", 0), ("f16x3", 0), ("f32", -3)):
         d.math = F._MATH_CODES[mode]
         rc = lib.se_conv2d_fwd_joined(ctypes.byref(d), x.data_ptr(), F_ - 1, T + 1, s.data_ptr(), w.data_ptr(),
                                       w.data_ptr(), None, None, y.data_ptr(), ws.data_ptr(), ws.numel(), st)
