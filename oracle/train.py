@@ -44,3 +44,33 @@ def train_step(model, optimizer, noisy, clean, clip_norm=0.5):
     optimizer.step()
     optimizer.zero_grad()
     return loss.detach(), total
+
+
+def initialize_params(model, nonlinearity="relu"):
+    """utils.py:47-84 (weight_norm=False, as train.py:38 calls it): kaiming-normal
+    for every Conv1d/Conv2d/ConvTranspose1d/ConvTranspose2d/Linear weight (zero
+    bias), xavier-uniform W_ih / orthogonal W_hh / zero biases for nn.LSTM, 1/0 for
+    BatchNorm1d/2d. Returns the qualified names of the modules it touched, in
+    visiting order (test infrastructure: the drop-in must expose the same ones)."""
+    nn = torch.nn
+    touched = []
+    for name, module in model.named_modules():
+        if isinstance(module, (nn.Conv1d, nn.Conv2d, nn.ConvTranspose1d, nn.ConvTranspose2d, nn.Linear)):
+            nn.init.kaiming_normal_(module.weight.data, nonlinearity=nonlinearity)
+            if module.bias is not None:
+                nn.init.zeros_(module.bias.data)
+        elif isinstance(module, nn.LSTM):
+            for pname, param in module.named_parameters():
+                if "weight_ih" in pname:
+                    nn.init.xavier_uniform_(param.data)
+                elif "weight_hh" in pname:
+                    nn.init.orthogonal_(param.data)
+                elif "bias" in pname:
+                    nn.init.zeros_(param.data)
+        elif isinstance(module, (nn.BatchNorm1d, nn.BatchNorm2d)):
+            nn.init.constant_(module.weight.data, 1)
+            nn.init.constant_(module.bias.data, 0)
+        else:
+            continue
+        touched.append(name)
+    return touched

@@ -878,9 +878,10 @@ static int istft_setup(int B, int T, int win, int hop, int nfft, int offset, int
   if (offset + out_len > (T - 1) * hop + win) return SE_E_SHAPE;
   a.T = T; a.win = win; a.hop = hop; a.offset = offset; a.out_len = out_len;
   a.P = pick_pairs(nfft); a.pl = pl;
-  // output tile: the covering frames of FT*hop samples must fit in 2P
+  // output tile of the generic forward kernel: the covering frames of FT*hop
+  // samples must fit in 2P (checked where that kernel launches; the in-place
+  // kernels use their own P, the adjoint tiles by frames)
   a.FT = 2 * a.P - 1 - (win - 1) / hop;
-  if (a.FT < 1) return SE_E_UNSUPPORTED;
   return SE_OK;
 }
 
@@ -924,6 +925,7 @@ extern "C" int se_istft_fwd(const float* spec, float* out, int B, int T, int win
     }
     istft_setup(B, T, win, hop, nfft, offset, out_len, a);   // FT too small at this P: generic kernel
   }
+  if (a.FT < 1) return SE_E_UNSUPPORTED;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
   SE_STFT_DISPATCH(istft_fwd_kernel, nfft, a.P, dim3(se::ceil_div(out_len, a.FT * hop), B), shm,
                    se::as_stream(stream), a);

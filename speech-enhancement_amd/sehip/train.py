@@ -149,11 +149,19 @@ class FlatDataParallel(torch.nn.Module):
         return self.module(*args, **kwargs)
 
     def allreduce_grads(self):
+        """Every trainable parameter takes part, in parameter order, so each rank
+        contributes an identically laid-out buffer even if a parameter went
+        unused on some rank (its gradient enters as zeros and, as under DDP,
+        every rank then holds the averaged gradient)."""
         import torch.distributed as dist
         from torch._utils import _flatten_dense_tensors, _unflatten_dense_tensors
-        grads = [p.grad for p in self.module.parameters() if p.grad is not None]
-        if not grads:
+        params = [p for p in self.module.parameters() if p.requires_grad]
+        if not params:
             return
+        for p in params:
+            if p.grad is None:
+                p.grad = torch.zeros_like(p)
+        grads = [p.grad for p in params]
         flat = _flatten_dense_tensors(grads)
         dist.all_reduce(flat, group=self.process_group)
         flat.div_(self.world)

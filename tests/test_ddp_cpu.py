@@ -84,3 +84,36 @@ def test_ddp_gloo_world2_grad_average(tmp_path, mode):
     assert worst < 1e-4, worst
     # per-rank BN statistics (no SyncBN): each rank updated its running mean from its own shard
     assert not torch.equal(res[0]["RMr"], res[1]["RMr"])
+
+
+def _unused_worker(rank, world, port, out_dir):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank))
+    from sehip.train import FlatDataParallel, setup_distributed
+    setup_distributed(backend="gloo")
+    torch.manual_seed(0)
+    net = torch.nn.ModuleDict({"a": torch.nn.Linear(4, 3), "b": torch.nn.Linear(4, 5), "c": torch.nn.Linear(4, 2)})
+    ddp = FlatDataParallel(net)
+    x = torch.full((2, 4), float(rank + 1))
+    # rank 0 leaves "b" unused, rank 1 leaves "c" unused: per-rank grad sets differ
+    out = net["a"](x).sum() + (net["c"](x).sum() if rank == 0 else net["b"](x).sum())
+    out.backward()
+    ddp.allreduce_grads()
+    torch.save({n: p.grad.clone() for n, p in net.named_parameters()}, os.path.join(out_dir, f"u{rank}.pt"))
+    torch.distributed.destroy_process_group()
+
+
+def test_flat_dp_unused_parameters_differ_by_rank(tmp_path):
+    """FlatDataParallel flattens every trainable parameter (zeros for a missing
+    gradient), so ranks whose unused-parameter sets differ still all-reduce
+    identically laid-out buffers: every rank ends with the DDP average."""
+    world, port = 2, _free_port()
+    mp.spawn(_unused_worker, args=(world, port, str(tmp_path)), nprocs=world, join=True)
+    g = [torch.load(tmp_path / f"u{r}.pt", weights_only=True) for r in range(world)]
+    for n in g[0]:
+        assert torch.equal(g[0][n], g[1][n]), n
+    # d sum(W x) / dW = sum over the 2 rows of x = 2 (rank + 1); "b" got a gradient only on
+    # rank 1 (4), averaged with rank 0's zeros; "c" only on rank 0 (2); "a" on both (2, 4)
+    assert torch.allclose(g[0]["b.weight"], torch.full((5, 4), 4.0 / 2))
+    assert torch.allclose(g[0]["c.weight"], torch.full((2, 4), 2.0 / 2))
+    assert torch.allclose(g[0]["a.weight"], torch.full((3, 4), (2.0 + 4.0) / 2))

@@ -223,6 +223,29 @@ def test_frcrn_4s_vs_oracle(gpu_device):
     assert rel_l2(w.cpu().numpy(), wo.numpy()) < TOL
 
 
+def test_frcrn_b16_4s_train_forward_vs_oracle(gpu_device):
+    """Batch-coupled parity at scale: ComplexBN reduces over B x F x T per channel
+    (fp64 moments, extrema for the f16x3 scale bounds). B = 16 x 4 s train-mode
+    forward against the oracle (frcrn.py:119-155) at the 1e-4 bar, per utterance,
+    and every CBN's running statistics after the step."""
+    from sehip import models as M
+    from oracle import models as O
+    noisy, _ = paramfill.structured_pair(16, 64000, seed=12)
+    mo = paramfill.fill_(O.FRCRN(), seed=13).train()
+    m = paramfill.fill_(M.FRCRN(), seed=13).cuda().train()
+    with torch.no_grad():
+        so, wo = mo(torch.from_numpy(noisy))
+        s, w = m(torch.from_numpy(noisy).cuda())
+    s, w = s.cpu().numpy(), w.cpu().numpy()
+    for b in range(16):
+        assert rel_l2(s[b], so[b].numpy()) < TOL, b
+        assert rel_l2(w[b], wo[b].numpy()) < TOL, b
+    bo = dict(mo.named_buffers())
+    for n, buf in m.named_buffers():
+        if n.rsplit(".", 1)[-1] in ("RMr", "RMi", "RVrr", "RVri", "RVii"):
+            np.testing.assert_allclose(buf.cpu().numpy(), bo[n].numpy(), rtol=2e-4, atol=2e-6, err_msg=n)
+
+
 @pytest.mark.parametrize("i", [3, 5])
 def test_real_conv_models_backward_vs_oracle(i, gpu_device):
     """CARN / CRN run their real convs on the HIP conv GEMMs (real_conv2d): train-mode
