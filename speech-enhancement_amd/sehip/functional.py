@@ -244,19 +244,23 @@ def _pass_math(pass_name, d) -> int:
     return _CONV_MATH[pass_name]
 
 
-def _gemm_tag(pass_name, d):
+def _gemm_tag(pass_name, d, joined=False):
     """OpTimer tag of a conv pass by the kernel that runs it (cconv.hip's
-    dispatch): conv_{fwd,data,wgrad}_{f32,bf16x3,smalln}."""
+    dispatch): conv_{fwd,data,wgrad}[_joined]_{f32,f16x3,bf16x3,...,smalln}.
+    The decoder's joined passes (se_conv2d_*_joined) are tagged apart: each
+    such call is one launch of one kernel instantiation, so the bench can pair
+    their live event times with that instantiation's PMC traffic."""
     names = {v: k for k, v in _MATH_CODES.items()}
     tr = bool(d.transposed)
+    j = "_joined" if joined else ""
     if pass_name == "weight":
         n = d.in_channels if tr else d.out_channels          # channels of the direct operand
         kind = "smalln" if n <= 8 else (names[_CONV_MATH["weight"]] if n > 32 else "f32")
         kind = "f32" if kind == "bf16x6" else kind
-        return f"conv_wgrad_{kind}"
+        return f"conv_wgrad{j}_{kind}"
     n = d.out_channels if pass_name == "fwd" else d.in_channels
     kind = "smalln" if n <= 16 else (names[_pass_math(pass_name, d)] if n > 64 else "f32")
-    return f"conv_{pass_name}_{kind}"
+    return f"conv_{pass_name}{j}_{kind}"
 
 
 def _with_math(d, pass_name):
@@ -423,7 +427,7 @@ class _ConvJoined(torch.autograd.Function):
                                    N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
         N.check(rc, "se_conv2d_fwd_joined")
         if t0 is not None:
-            _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
+            _TIMER.end(_gemm_tag("fwd", d, joined=True), t0, _conv_flops(d),
                        4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
         ctx.save_for_backward(x, s, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax = d, nbytes, br is not None, xa
@@ -456,7 +460,7 @@ class _ConvJoined(torch.autograd.Function):
                                              s.shape[1], d.in_h, d.in_w, d.batch, st)
             N.check(rc, "se_conv2d_bwd_data_joined")
             if t0 is not None:
-                _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
+                _TIMER.end(_gemm_tag("data", d, joined=True), t0, _conv_flops(d),
                            4.0 * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))
         if any(ctx.needs_input_grad[2:6]):
             with _wgrad_stream(x, s, gy, xa, ga):
@@ -478,7 +482,7 @@ class _ConvJoined(torch.autograd.Function):
                                                   ws.data_ptr(), ws.numel(), st)
                 N.check(rc, "se_conv2d_bwd_weight_joined")
                 if t0 is not None:
-                    _TIMER.end(_gemm_tag("weight", d), t0, _conv_flops(d),
+                    _TIMER.end(_gemm_tag("weight", d, joined=True), t0, _conv_flops(d),
                                4.0 * (x.numel() + s.numel() + gy.numel() + 2 * wr.numel()))
         return gx, gs, dwr, dwi, dbr, dbi, None
 

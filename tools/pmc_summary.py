@@ -10,7 +10,26 @@ bytes -> doubled; both counters are in KiB.
 import collections, csv, json, os, re, sys
 
 
+def kernel_key(name):
+    """rocprof kernel name -> 'base<template args>' (as bench.py's _kernel_key)."""
+    name = name.replace("(anonymous namespace)::", "")
+    name = re.sub(r"^void\s+", "", name)
+    depth, end = 0, len(name)
+    for i, ch in enumerate(name):
+        if ch == "<":
+            depth += 1
+        elif ch == ">":
+            depth -= 1
+        elif ch == "(" and depth == 0:
+            end = i
+            break
+    name = name[:end].strip()
+    return name if "<" in name else name.split("::")[-1].strip()
+
+
 def load(d, counter):
+    """Per kernel: values of every dispatch, keyed by the exact instantiation and,
+    aggregated, by the base name."""
     path = os.path.join(d, "run_counter_collection.csv")
     if not os.path.exists(path):   # rocprofv3 -d without -o: <d>/<host>/<pid>_counter_collection.csv
         import glob
@@ -19,10 +38,12 @@ def load(d, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        name = r["Kernel_Name"].replace("(anonymous namespace)::", "")
-        name = re.sub(r"^void\s+", "", name)
-        name = re.split(r"[<(]", name)[0].split("::")[-1].strip()
-        per[name].append(float(r["Counter_Value"]) * 1024.0)
+        full = kernel_key(r["Kernel_Name"])
+        v = float(r["Counter_Value"]) * 1024.0
+        per[full].append(v)
+        base = full.split("<")[0].split("::")[-1].strip()
+        if base != full:
+            per[base].append(v)
     return per
 
 
@@ -40,8 +61,8 @@ def main():
         res[k] = {"launches": len(f), "fetch_bytes_per_launch_corrected": fb,
                   "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
-    for k in ("gather_gemm_kernel", "wgrad_gemm_kernel", "stft_fwd_kernel", "istft_fwd_kernel",
-              "cbn_apply_kernel"):
+    for k in ("gather_x3_kernel<true, 3, 2, 2, true>", "wgrad_x3_kernel<true, 3, true, true>",
+              "stft_fwd_ip_kernel", "istft_fwd_ip_kernel", "cbn_apply_kernel"):
         if k in res:
             print(k, {a: f"{b:.4g}" for a, b in res[k].items()})
 
