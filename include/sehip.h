@@ -327,6 +327,34 @@ int se_complex_join(const float* x, int Cx, int Fx, int Tx, const float* s,
 int se_complex_join_bwd(const float* gout, float* gx, int Cx, int Fx, int Tx,
                         float* gs, int Cs, int F, int T, int B, void* stream);
 
+/* ------------------------------------------------------------------------
+ * Data path: the reference mixes and crops on the host
+ * (mix_audio.py:87-123, audio_dataloader.py:29-50); here the per-sample work
+ * runs on the device and the host keeps only the random draws.
+ *
+ * se_mix_snr: get_noisy_data for B items at once. clean [B, Lc], noise [B, Ln]
+ * (one clip per item). Device int arrays from the host RNG: noise_start[B]
+ * (crop start when Ln > Lc, :88-93), snr_db[B] (randint(-20, 20), :98),
+ * nplace[B] (< 0: tiled repeat over floor(Lc/Ln')*Ln' samples, noise_repeat
+ * None, :116-121; >= 0: that many placements place[b*R + r] added in order,
+ * :108-115). scale[B] = (clean_rms / 10^(snr/20)) / noise_rms (:95-100);
+ * repeat_noise [B, Lc]; mix = clean + repeat_noise [B, Lc] (:123).
+ * se_crop_pad: AudioSpliter.split + default_collate over a ragged batch:
+ * out[b, t] = src[off[b] + start[b] + t] if start[b] + t < len[b] else 0,
+ * t < chunk (pad when len < chunk with start 0; crop at the host's random
+ * start otherwise). off, len, start: device arrays.
+ * se_pcm16_to_float: x / 32768 (torchaudio.load's normalisation);
+ * se_float_to_pcm16: clamp(rint(x * 32768), -32768, 32767) (PCM_S 16 save).
+ * ------------------------------------------------------------------------ */
+int se_mix_snr(const float* clean, const float* noise, int B, int Lc, int Ln,
+               const int* noise_start, const int* snr_db, const int* place,
+               const int* nplace, int R, float* mix, float* repeat_noise,
+               float* scale, void* stream);
+int se_crop_pad(const float* src, const long long* off, const int* len,
+                const int* start, int B, int chunk, float* out, void* stream);
+int se_pcm16_to_float(const int16_t* in, long long n, float* out, void* stream);
+int se_float_to_pcm16(const float* in, long long n, int16_t* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

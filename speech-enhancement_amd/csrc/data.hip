@@ -1,0 +1,146 @@
+// Data path of the training loop on the device.
+//
+// Replaces the host-side mixing of mix_audio.py:87-123 (get_noisy_data: noise
+// crop, RMS at a random integer SNR, tiled or randomly placed noise repeats,
+// mix = clean + noise) and the crop / pad collation of audio_dataloader.py:29-50
+// (AudioSpliter.split + default_collate), plus the PCM16 <-> float conversion
+// of the wav files the reference writes (mix_audio.py:144-146). The random
+// draws (crop starts, SNRs, placements) stay on the host, as the reference's
+// `random` calls, and arrive as small device arrays; the kernels do the
+// per-sample work: one HBM pass per output, no host round trip.
+#include "common.hpp"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+// grid (B): per item, sum clean^2 over Lc and noise^2 over the noise segment
+// [cs, cs + Lnp) in fp64; scale = (clean_rms / 10^(snr/20)) / noise_rms with
+// the reference's fp32 steps (get_rms :14-15, get_adjusted_rms :17-18, :100).
+__global__ void __launch_bounds__(kThreads)
+mix_scale_kernel(const float* __restrict__ clean, const float* __restrict__ noise, int Lc, int Ln,
+                 const int* __restrict__ noise_start, const int* __restrict__ snr_db, float* __restrict__ scale) {
+  const int b = blockIdx.x;
+  const int Lnp = Ln > Lc ? Lc : Ln;
+  const int cs = Ln > Lc ? noise_start[b] : 0;
+  const float* c = clean + (long long)b * Lc;
+  const float* n = noise + (long long)b * Ln + cs;
+  double sc = 0.0, sn = 0.0;
+  for (int t = threadIdx.x; t < Lc; t += kThreads) sc += (double)c[t] * c[t];
+  for (int t = threadIdx.x; t < Lnp; t += kThreads) sn += (double)n[t] * n[t];
+  __shared__ double red[2][kThreads / 64];
+  sc = se::wave_sum(sc);
+  sn = se::wave_sum(sn);
+  if ((threadIdx.x & 63) == 0) { red[0][threadIdx.x >> 6] = sc; red[1][threadIdx.x >> 6] = sn; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double a = 0, q = 0;
+    for (int w = 0; w < kThreads / 64; ++w) { a += red[0][w]; q += red[1][w]; }
+    const float clean_rms = sqrtf((float)(a / Lc));
+    const float noise_rms = sqrtf((float)(q / Lnp));
+    const float adjusted_rms = clean_rms / (float)pow(10.0, snr_db[b] / 20.0);
+    scale[b] = adjusted_rms / noise_rms;
+  }
+}
+
+// grid (ceil(Lc / (4 kThreads)), B). nplace[b] < 0: tiled repeat of the scaled
+// segment over floor(Lc / Lnp) * Lnp samples (noise_repeat None, :116-121);
+// else nplace[b] placements at place[b * R + r], added in order (:108-115).
+__global__ void __launch_bounds__(kThreads)
+mix_apply_kernel(const float* __restrict__ clean, const float* __restrict__ noise, int Lc, int Ln,
+                 const int* __restrict__ noise_start, const int* __restrict__ place, const int* __restrict__ nplace,
+                 int R, const float* __restrict__ scale, float* __restrict__ mix, float* __restrict__ rep) {
+  const int b = blockIdx.y;
+  const int Lnp = Ln > Lc ? Lc : Ln;
+  const int cs = Ln > Lc ? noise_start[b] : 0;
+  const float s = scale[b];
+  const float* c = clean + (long long)b * Lc;
+  const float* n = noise + (long long)b * Ln + cs;
+  const int np = nplace[b];
+  const int tiled_end = (Lc / Lnp) * Lnp;
+  for (int u = 0; u < 4; ++u) {
+    const int t = (blockIdx.x * 4 + u) * kThreads + threadIdx.x;
+    if (t >= Lc) return;
+    float r = 0.f;
+    if (np < 0) {
+      if (t < tiled_end) r = __fadd_rn(r, __fmul_rn(n[t % Lnp], s));   // adjusted = noise * scale, then +=
+    } else {
+      for (int k = 0; k < np; ++k) {
+        const int st = place[(long long)b * R + k];
+        if (t >= st && t < st + Lnp) r = __fadd_rn(r, __fmul_rn(n[t - st], s));
+      }
+    }
+    rep[(long long)b * Lc + t] = r;
+    mix[(long long)b * Lc + t] = __fadd_rn(c[t], r);
+  }
+}
+
+// grid (ceil(chunk / kThreads), B)
+__global__ void __launch_bounds__(kThreads)
+crop_pad_kernel(const float* __restrict__ src, const long long* __restrict__ off, const int* __restrict__ len,
+                const int* __restrict__ start, int chunk, float* __restrict__ out) {
+  const int b = blockIdx.y, t = blockIdx.x * kThreads + threadIdx.x;
+  if (t >= chunk) return;
+  const int s = start[b] + t;
+  out[(long long)b * chunk + t] = s < len[b] ? src[off[b] + s] : 0.f;
+}
+
+__global__ void pcm16_to_float_kernel(const int16_t* __restrict__ in, long long n, float* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    out[i] = (float)in[i] * (1.0f / 32768.0f);
+}
+
+__global__ void float_to_pcm16_kernel(const float* __restrict__ in, long long n, int16_t* __restrict__ out) {
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float v = rintf(in[i] * 32768.0f);
+    out[i] = (int16_t)fminf(fmaxf(v, -32768.0f), 32767.0f);
+  }
+}
+
+inline unsigned grid_of(long long n) {
+  const long long g = (n + kThreads - 1) / kThreads;
+  return (unsigned)(g < 8192 ? (g > 0 ? g : 1) : 8192);
+}
+
+}  // namespace
+
+extern "C" int se_mix_snr(const float* clean, const float* noise, int B, int Lc, int Ln, const int* noise_start,
+                          const int* snr_db, const int* place, const int* nplace, int R, float* mix,
+                          float* repeat_noise, float* scale, void* stream) {
+  if (!clean || !noise || !noise_start || !snr_db || !nplace || !mix || !repeat_noise || !scale) return SE_E_ARG;
+  if (B <= 0 || Lc <= 0 || Ln <= 0 || R < 0 || (R > 0 && !place)) return SE_E_ARG;
+  hipStream_t st = se::as_stream(stream);
+  hipLaunchKernelGGL(mix_scale_kernel, dim3(B), dim3(kThreads), 0, st, clean, noise, Lc, Ln, noise_start, snr_db,
+                     scale);
+  SE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(mix_apply_kernel, dim3(se::ceil_div(Lc, 4 * kThreads), B), dim3(kThreads), 0, st, clean,
+                     noise, Lc, Ln, noise_start, place, nplace, R, scale, mix, repeat_noise);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_crop_pad(const float* src, const long long* off, const int* len, const int* start, int B,
+                           int chunk, float* out, void* stream) {
+  if (!src || !off || !len || !start || !out || B < 0 || chunk <= 0) return SE_E_ARG;
+  if (B == 0) return SE_OK;
+  hipLaunchKernelGGL(crop_pad_kernel, dim3(se::ceil_div(chunk, kThreads), B), dim3(kThreads), 0,
+                     se::as_stream(stream), src, off, len, start, chunk, out);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_pcm16_to_float(const int16_t* in, long long n, float* out, void* stream) {
+  if (!in || !out || n < 0) return SE_E_ARG;
+  if (n == 0) return SE_OK;
+  hipLaunchKernelGGL(pcm16_to_float_kernel, dim3(grid_of(n)), dim3(kThreads), 0, se::as_stream(stream), in, n, out);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_float_to_pcm16(const float* in, long long n, int16_t* out, void* stream) {
+  if (!in || !out || n < 0) return SE_E_ARG;
+  if (n == 0) return SE_OK;
+  hipLaunchKernelGGL(float_to_pcm16_kernel, dim3(grid_of(n)), dim3(kThreads), 0, se::as_stream(stream), in, n, out);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}

@@ -51,6 +51,10 @@ _SIGNATURES = {
     "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
     "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
     "se_amax": (c_int, [_P, ctypes.c_longlong, _P, _P]),
+    "se_mix_snr": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P, _P]),
+    "se_crop_pad": (c_int, [_P, _P, _P, _P, c_int, c_int, _P, _P]),
+    "se_pcm16_to_float": (c_int, [_P, ctypes.c_longlong, _P, _P]),
+    "se_float_to_pcm16": (c_int, [_P, ctypes.c_longlong, _P, _P]),
     "se_conv2d_workspace_size": (c_size_t, [_P]),
     "se_conv2d_fwd": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),
@@ -129,15 +133,15 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
-def require_device(*ts: torch.Tensor) -> None:
+def require_device(*ts: torch.Tensor, dtype=torch.float32) -> None:
     for t in ts:
         if t is None:
             continue
         if not t.is_cuda:
             raise RuntimeError("sehip ops run on the GPU only (got a CPU tensor); "
                                "there is no CPU fallback in the product path")
-        if t.dtype != torch.float32:
-            raise RuntimeError(f"sehip ops take float32 tensors (got {t.dtype})")
+        if t.dtype != dtype:
+            raise RuntimeError(f"sehip ops take {dtype} tensors (got {t.dtype})")
 
 
 def ptr_array(ts):

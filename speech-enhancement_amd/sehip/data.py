@@ -37,3 +37,183 @@ def synthetic_pairs(batch: int, length: int = 64000, sr: int = 16000, seed: int 
     gain = torch.sqrt(p_c / (p_n * 10 ** (snr_db / 10)))
     noisy = clean + gain * noise
     return noisy, clean
+
+
+# --------------------------------------------------------------------------
+# Real-data path: the reference's mixer and collation
+# with the per-sample work on the device (csrc/data.hip). The random draws are
+# made on the host with a `random.Random` in the reference's order, so a seeded
+# run draws what the reference would; the kernels then mix / crop / pad.
+# --------------------------------------------------------------------------
+import random as _random
+import wave as _wave
+
+from . import _native as N
+
+
+def get_rms(signal: torch.Tensor) -> torch.Tensor:
+    """mix_audio.py:14-15."""
+    return torch.sqrt(torch.mean(signal ** 2, dim=-1, keepdim=True))
+
+
+def get_adjusted_rms(clean_rms, snr):
+    """mix_audio.py:17-18."""
+    return clean_rms / 10 ** (snr / 20)
+
+
+def _dev_ints(v, device):
+    return torch.tensor(v, dtype=torch.int32, device=device)
+
+
+def mix_batch(clean: torch.Tensor, noise: torch.Tensor, snr_db, noise_start=None, placements=None):
+    """Device mixing of B items (se_mix_snr): clean [B, Lc], noise [B, Ln] on the GPU;
+    snr_db: B ints; noise_start: B crop starts (used when Ln > Lc); placements: None
+    (tiled repeat, noise_repeat=None) or B lists of start indices (noise_repeat given).
+    Returns (mix, repeat_noise, scale) as mix_audio.py:95-123 computes them."""
+    N.require_device(clean, noise)
+    clean, noise = clean.contiguous().float(), noise.contiguous().float()
+    B, Lc = clean.shape
+    Ln = noise.shape[1]
+    if noise.shape[0] != B:
+        raise ValueError("sehip mix_batch: one noise clip per clean item")
+    dev = clean.device
+    starts = _dev_ints(list(noise_start) if noise_start is not None else [0] * B, dev)
+    snr = _dev_ints([int(s) for s in snr_db], dev)
+    if placements is None:
+        nplace, R, place = _dev_ints([-1] * B, dev), 0, None
+    else:
+        R = max(1, max(len(p) for p in placements))
+        flat = [p[r] if r < len(p) else 0 for p in placements for r in range(R)]
+        place, nplace = _dev_ints(flat, dev), _dev_ints([len(p) for p in placements], dev)
+    mix, rep = torch.empty_like(clean), torch.empty_like(clean)
+    scale = torch.empty(B, device=dev, dtype=torch.float32)
+    N.check(N.lib().se_mix_snr(clean.data_ptr(), noise.data_ptr(), B, Lc, Ln, starts.data_ptr(), snr.data_ptr(),
+                               N.ptr(place), nplace.data_ptr(), R, mix.data_ptr(), rep.data_ptr(),
+                               scale.data_ptr(), N.stream_of(clean)), "se_mix_snr")
+    return mix, rep, scale
+
+
+def get_noisy_data(clean_audio, noise_audio, noise_repeat=None, k=100, rng=None):
+    """mix_audio.py:20-149 for tensors already in memory (channels x samples or 1-D;
+    no resampling, no wav writing): k mixes of one clean / noise pair at random
+    integer SNRs in [-20, 20], drawn with `rng` (a random.Random, or the module
+    `random` as in the reference) in the reference's order. Mono downmix as
+    :65-69. Returns (clean_amp, noise_amp, outputs) with the reference's keys."""
+    rng = rng or _random
+    c = clean_audio[None] if clean_audio.dim() == 1 else clean_audio
+    n = noise_audio[None] if noise_audio.dim() == 1 else noise_audio
+    if c.shape[0] > 1:
+        c = c.mean(dim=0, keepdim=True)
+    if n.shape[0] > 1:
+        n = n.mean(dim=0, keepdim=True)
+    Lc, Ln = c.shape[1], n.shape[1]
+    Lnp = min(Ln, Lc)
+    starts, snrs, places, indices = [], [], [], []
+    for _ in range(k):                                   # :87-121, same draw order
+        starts.append(rng.randint(0, Ln - Lc) if Ln > Lc else 0)
+        snrs.append(rng.randint(-20, 20))
+        max_repeat = Lc // Lnp
+        if noise_repeat is not None:
+            p = [rng.randint(0, Lc - Lnp) for _ in range(min(noise_repeat, max_repeat))]
+            places.append(p)
+            indices.append([[s, s + Lnp] for s in p])
+        else:
+            indices.append([[i, i + Lnp] for i in range(0, max_repeat * Lnp, Lnp)])
+    mix, rep, _ = mix_batch(c.expand(k, Lc), n.expand(k, Ln), snrs, starts,
+                            places if noise_repeat is not None else None)
+    outputs = {"mixed_output": list(mix.unsqueeze(1).unbind(0)), "adjusted_noise": [n] * k,
+               "repeat_noise": list(rep.unsqueeze(1).unbind(0)), "noise_indices": indices, "snr": snrs}
+    return c, n, outputs
+
+
+class AudioSpliter:
+    """audio_dataloader.py:8-50: drop items shorter than least_samples, zero-pad
+    shorter than chunk_size, else a random chunk (the same start for mix and refs).
+    `plan` makes the host decisions in the reference's order; `collate` applies
+    them to a ragged batch on the device (se_crop_pad) and stacks like
+    default_collate: {'mix': [B, 1, chunk], 'ref': [[B, 1, chunk], ...]}."""
+
+    def __init__(self, chunk_size=32000, least_samples=16000, rng=None):
+        self.chunk_size, self.least_samples = chunk_size, least_samples
+        self.rng = rng or _random
+
+    def plan(self, lengths):
+        """[(keep, start)] per item (:32-48)."""
+        out = []
+        for L in lengths:
+            if L < self.least_samples:
+                out.append((False, 0))
+            elif L < self.chunk_size:
+                out.append((True, 0))
+            else:
+                out.append((True, self.rng.randint(0, L - self.chunk_size)))
+        return out
+
+    def collate(self, samples):
+        """samples: [{'mix': [1, L_i], 'ref': [[1, L_i], ...]}] on the GPU."""
+        plan = self.plan([s["mix"].shape[-1] for s in samples])
+        kept = [(s, st) for s, (keep, st) in zip(samples, plan) if keep]
+        if not kept:
+            return []
+        dev = kept[0][0]["mix"].device
+        lens = [s["mix"].shape[-1] for s, _ in kept]
+        offs = [0]
+        for L in lens[:-1]:
+            offs.append(offs[-1] + L)
+        off_t = torch.tensor(offs, dtype=torch.int64, device=dev)
+        len_t, st_t = _dev_ints(lens, dev), _dev_ints([st for _, st in kept], dev)
+
+        def crop(stream):
+            src = torch.cat([t.reshape(-1).float() for t in stream]).contiguous()
+            N.require_device(src)
+            out = torch.empty(len(kept), 1, self.chunk_size, device=dev, dtype=torch.float32)
+            N.check(N.lib().se_crop_pad(src.data_ptr(), off_t.data_ptr(), len_t.data_ptr(), st_t.data_ptr(),
+                                        len(kept), self.chunk_size, out.data_ptr(), N.stream_of(src)),
+                    "se_crop_pad")
+            return out
+
+        nref = len(kept[0][0]["ref"])
+        return {"mix": crop([s["mix"] for s, _ in kept]),
+                "ref": [crop([s["ref"][j] for s, _ in kept]) for j in range(nref)]}
+
+
+def pcm16_to_float(x: torch.Tensor) -> torch.Tensor:
+    """int16 samples -> float / 32768 (torchaudio.load's normalisation), on the device."""
+    N.require_device(x, dtype=torch.int16)
+    x = x.contiguous()
+    out = torch.empty(x.shape, device=x.device, dtype=torch.float32)
+    N.check(N.lib().se_pcm16_to_float(x.data_ptr(), x.numel(), out.data_ptr(), N.stream_of(x)),
+            "se_pcm16_to_float")
+    return out
+
+
+def float_to_pcm16(x: torch.Tensor) -> torch.Tensor:
+    """float -> int16 = clamp(rint(x * 32768)) (PCM_S 16-bit save, mix_audio.py:144-146)."""
+    N.require_device(x)
+    x = x.contiguous().float()
+    out = torch.empty(x.shape, device=x.device, dtype=torch.int16)
+    N.check(N.lib().se_float_to_pcm16(x.data_ptr(), x.numel(), out.data_ptr(), N.stream_of(x)),
+            "se_float_to_pcm16")
+    return out
+
+
+def load_wav(path, device="cuda") -> tuple[torch.Tensor, int]:
+    """PCM16 wav -> ([channels, samples] float on the device, sample rate)."""
+    with _wave.open(str(path), "rb") as f:
+        if f.getsampwidth() != 2:
+            raise ValueError(f"{path}: only 16-bit PCM wav is supported")
+        ch, sr, n = f.getnchannels(), f.getframerate(), f.getnframes()
+        raw = f.readframes(n)
+    pcm = torch.frombuffer(bytearray(raw), dtype=torch.int16).view(n, ch).t().contiguous()
+    return pcm16_to_float(pcm.to(device)), sr
+
+
+def save_wav(path, audio: torch.Tensor, sr: int) -> None:
+    """[channels, samples] (or [samples]) float on the device -> PCM16 wav."""
+    a = audio[None] if audio.dim() == 1 else audio
+    pcm = float_to_pcm16(a).cpu().t().contiguous()
+    with _wave.open(str(path), "wb") as f:
+        f.setnchannels(a.shape[0])
+        f.setsampwidth(2)
+        f.setframerate(int(sr))
+        f.writeframes(pcm.numpy().tobytes())

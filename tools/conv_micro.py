@@ -10,6 +10,7 @@ LAYERS = {  # name: (transposed, cin, cout, input shape)
     "enc1": (False, 128, 128, (64, 128, 158, 404)),
     "dec5": (True, 256, 128, (64, 256, 158, 403)),
     "dec3": (True, 256, 128, (64, 256, 37, 403)),
+    "enc4": (False, 128, 128, (64, 128, 17, 404)),
 }
 ap = argparse.ArgumentParser()
 ap.add_argument("--layers", default="enc1,dec5")
