@@ -52,6 +52,12 @@ def _stacked(x):
     return x, lambda y: y
 
 
+def _f32(t):
+    """fp16 / bf16 storage (the reference's model.half() / .to(bfloat16) configs)
+    runs on the fp32-storage kernels; results go back in the caller's dtype."""
+    return t if t is None or t.dtype == torch.float32 else t.float()
+
+
 def _check_even(n, what):
     assert n % 2 == 0, f"{what} must be a factor of 2, current channels: {n}"
     return n // 2
@@ -94,12 +100,12 @@ class _FusedComplexConv(nn.Module):
         xs, rebuild = _stacked(x)
         c = self._geometry()
         begin, end = _fold_pad(c.padding, input_pad, self.transposed)
-        y = F.conv2d(xs, c.weight, self.imag_conv.weight, c.bias, self.imag_conv.bias,
+        y = F.conv2d(_f32(xs), _f32(c.weight), _f32(self.imag_conv.weight), _f32(c.bias), _f32(self.imag_conv.bias),
                      out_channels=2 * c.out_channels, kernel=c.kernel_size, stride=c.stride,
                      padding=begin, padding_end=end, dilation=c.dilation,
                      output_padding=getattr(c, "output_padding", (0, 0)),
                      transposed=self.transposed)
-        return rebuild(y)
+        return rebuild(y.to(xs.dtype))
 
     def forward_joined(self, x, skip):
         """self(complex_concat([align(x), skip])) with the FRCRN decoder's
@@ -144,10 +150,11 @@ def real_conv2d(conv: nn.Module, x, input_pad=None):
     if conv.groups != 1 or isinstance(conv.padding, str):
         raise NotImplementedError("sehip real conv: groups / string padding")
     begin, end = _fold_pad(conv.padding, input_pad, tr)
-    return F.conv2d(x, conv.weight, None, conv.bias, None, out_channels=conv.out_channels,
-                    kernel=conv.kernel_size, stride=conv.stride, padding=begin, padding_end=end,
-                    dilation=conv.dilation, output_padding=getattr(conv, "output_padding", (0, 0)),
-                    transposed=tr)
+    y = F.conv2d(_f32(x), _f32(conv.weight), None, _f32(conv.bias), None, out_channels=conv.out_channels,
+                 kernel=conv.kernel_size, stride=conv.stride, padding=begin, padding_end=end,
+                 dilation=conv.dilation, output_padding=getattr(conv, "output_padding", (0, 0)),
+                 transposed=tr)
+    return y.to(x.dtype)
 
 
 # ------------------------------------------------------------- linear / LSTM

@@ -37,7 +37,25 @@ def _twiddles(nfft: int) -> torch.Tensor:
     return torch.from_numpy(np.stack([np.cos(ang), -np.sin(ang)], axis=1).astype(np.float32).reshape(-1))
 
 
-class ConvSTFT(nn.Module):
+class _KernelTables(nn.Module):
+    """Keeps the kernels' private fp32 tables (window, twiddles) in fp32 when the
+    module is cast (model.half() / .to(bfloat16), as the reference's low-precision
+    configs do): the state_dict buffers follow the cast like the reference's, the
+    tables the kernels read do not. Inputs of another float dtype are computed on
+    the fp32 kernels and returned in the caller's dtype."""
+
+    _tables = ("_win", "_tw")
+
+    def _apply(self, fn, *args, **kwargs):
+        keep = {n: getattr(self, n).detach().cpu().float() for n in self._tables}
+        super()._apply(fn, *args, **kwargs)
+        for n, v in keep.items():
+            buf = getattr(self, n)
+            setattr(self, n, v.to(buf.device))
+        return self
+
+
+class ConvSTFT(_KernelTables):
     """conv_stft.py:29-66 (analysis)."""
 
     def __init__(self, window_size, hop_size, fft_size=None, win_type="hann", center=True,
@@ -63,11 +81,14 @@ class ConvSTFT(nn.Module):
             raise RuntimeError(f"ConvSTFT expects [L], [B, L] or [B, 1, L], got {tuple(inputs.shape)}")
         if self.center and x.shape[-1] <= self.pad:
             raise RuntimeError(f"reflect padding {self.pad} needs an input longer than {self.pad}")
-        return F.stft(x, self._win, self._tw, self.window_size, self.hop_size, self.fft_size,
-                      self.center, self.return_mag_phase)
+        out = F.stft(x.float(), self._win, self._tw, self.window_size, self.hop_size, self.fft_size,
+                     self.center, self.return_mag_phase)
+        if x.dtype == torch.float32:
+            return out
+        return tuple(o.to(x.dtype) for o in out) if self.return_mag_phase else out.to(x.dtype)
 
 
-class ConviSTFT(nn.Module):
+class ConviSTFT(_KernelTables):
     """conv_stft.py:69-116 (synthesis with the pinv basis + window^2 OLA)."""
 
     def __init__(self, window_size, hop_size, fft_size=None, win_type="hann", center=True, fix=True):
@@ -77,6 +98,7 @@ class ConviSTFT(nn.Module):
         self.register_buffer("weight", weight)
         self.register_buffer("window", torch.from_numpy(w.astype(np.float32))[None, :, None])
         self.register_buffer("enframe", torch.eye(window_size)[:, None, :])
+        self.register_buffer("_win", torch.from_numpy(w.astype(np.float32)), persistent=False)
         self.register_buffer("_tw", _twiddles(self.fft_size), persistent=False)
         self.hop_size, self.window_size, self.center = hop_size, window_size, center
         self.pad = self.fft_size // 2
@@ -92,5 +114,6 @@ class ConviSTFT(nn.Module):
         else:
             offset = 0
             n = full if output_length is None else min(output_length, full)
-        return F.istft(inputs, self.window[0, :, 0], self._tw, self.window_size, self.hop_size,
-                       self.fft_size, offset, max(n, 0))
+        out = F.istft(inputs.float(), self._win, self._tw, self.window_size, self.hop_size,
+                      self.fft_size, offset, max(n, 0))
+        return out if inputs.dtype == torch.float32 else out.to(inputs.dtype)

@@ -1,0 +1,79 @@
+"""BASELINE.json configs 2, 3 and 5 on one MI355X, one JSON line each (bench.py
+is config 4, the headline). Synthetic inputs, random-init weights.
+
+  2: DCUNet-16 inference, 4 s @ 16 kHz, batch 16, bf16 GEMM operands (SE_MATH_BF16)
+  3: DCCRN-CL training step, 4 s @ 16 kHz, batch 64, bf16 GEMM operands
+  5: CARN fp16 storage (model.half()) inference on 30 s @ 48 kHz = [1, 1,440,000],
+     in 4 s chunks overlapping 50 ms (sehip/longform.py), and the same in fp32 and
+     as one unchunked sequence (T = 9002 frames)
+
+Usage: python tools/bench_configs.py [--configs 2,3,5] [--iters 5]"""
+import argparse, json, os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "speech-enhancement_amd"))
+import torch
+
+
+def timeit(fn, iters, warm=2):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--configs", default="2,3,5")
+    ap.add_argument("--iters", type=int, default=5)
+    a = ap.parse_args()
+    from sehip import functional as F, models as M, longform as L
+    from sehip.data import synthetic_pairs
+    from sehip.train import make_optimizer, train_step
+    dev = torch.device("cuda")
+    cfgs = a.configs.split(",")
+    if "2" in cfgs:
+        F.set_conv_math("bf16")
+        m = M.DCUNet("dcunet16", 512, 128, 512).to(dev).eval()
+        x, _ = synthetic_pairs(16, 64000, seed=5, device=dev)
+        with torch.no_grad():
+            dt = timeit(lambda: m(x), a.iters)
+        print(json.dumps({"config": 2, "workload": "DCUNet-16 inference 4 s @ 16 kHz, batch 16", "conv_math": "bf16",
+                          "value": round(16 / dt, 2), "unit": "utterances/sec", "ms_per_batch": round(dt * 1e3, 3)}),
+              flush=True)
+    if "3" in cfgs:
+        F.set_conv_math("bf16")
+        m = M.DCCRN("dccrn-CL", 400, 100, 512).to(dev).train()
+        opt = make_optimizer(m)
+        x, c = synthetic_pairs(64, 64000, seed=6, device=dev)
+        dt = timeit(lambda: train_step(m, opt, x, c), a.iters)
+        print(json.dumps({"config": 3, "workload": "DCCRN-CL train step 4 s @ 16 kHz, batch 64", "conv_math": "bf16",
+                          "value": round(64 / dt, 2), "unit": "utterances/sec", "ms_per_step": round(dt * 1e3, 3)}),
+              flush=True)
+    if "5" in cfgs:
+        F.set_conv_math(F.DEFAULT_CONV_MATH)
+        sr, secs = 48000, 30
+        x, _ = synthetic_pairs(1, sr * secs, sr=sr, seed=7, device=dev)
+        chunk, overlap = 4 * sr, sr // 20
+        for dtype, label in ((torch.float16, "fp16"), (torch.float32, "fp32")):
+            m = M.CARN(320, 160, 512).to(dev).eval().to(dtype)
+            xd = x.to(dtype)
+            dt = timeit(lambda: L.enhance_chunked(m, xd, chunk, overlap), a.iters, warm=1)
+            print(json.dumps({"config": 5, "workload": "CARN inference, 30 s @ 48 kHz [1, 1440000], 4 s chunks "
+                              "(50 ms cross-fade) as one batch of 8", "storage": label,
+                              "conv_math": F.get_conv_math(), "ms_per_utterance": round(dt * 1e3, 2),
+                              "realtime_factor": round(secs / dt, 1), "value": round(1 / dt, 3),
+                              "unit": "utterances/sec (30 s each)"}), flush=True)
+        m = M.CARN(320, 160, 512).to(dev).eval().half()
+        with torch.no_grad():
+            dt = timeit(lambda: m(x.half()), max(1, a.iters // 2), warm=1)
+        print(json.dumps({"config": 5, "workload": "CARN inference, 30 s @ 48 kHz as ONE sequence (T = 9002 frames)",
+                          "storage": "fp16", "ms_per_utterance": round(dt * 1e3, 2),
+                          "realtime_factor": round(secs / dt, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
