@@ -140,10 +140,25 @@ typedef struct se_conv2d_desc {
    * apply, se_amax) fill it for free. */
   const float* x_amax;
   const float* dy_amax;
+  /* SE_MATH_F16X3 only, optional: the conv input x (for the joined entry
+   * points: s in x_packed, x in x2_packed) and dy in CL16 form (se_pack_cl16,
+   * made with the x_amax / dy_amax bound passed here). When given, the
+   * forward / data-grad GEMMs stage them by LDS-DMA instead of gathering and
+   * splitting fp32. NULL = gather the fp32 tensor. */
+  const void* x_packed;
+  const void* x2_packed;
+  const void* dy_packed;
 } se_conv2d_desc;
 
 enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3,
        SE_MATH_F16X3 = 4 };
+
+/* CL16: x [B, C, H, W] fp32 -> two channels-last fp16 planes [2][B][H][W][C],
+ * hi = fp16(x s), lo = fp16(x s - hi), s = 2^(14 - e) with max|x| <= *amax < 2^e
+ * (the SE_MATH_F16X3 scale). C % 8 == 0. */
+size_t se_pack_cl16_bytes(int B, int C, int H, int W);
+int se_pack_cl16(const float* x, int B, int C, int H, int W, const float* amax,
+                 void* out, void* stream);
 
 /* amax[0] = max(amax[0], max_i |x[i]|) over n elements (atomic; zero amax[0]
  * first for a fresh maximum). The scale source of SE_MATH_F16X3. */

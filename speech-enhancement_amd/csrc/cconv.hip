@@ -101,6 +101,14 @@ struct GatherArgs {
   // SE_MATH_F16X3: device max |.| of the gathered tensor(s) and of the weights
   const float* amax_a;
   const float* amax_w;
+  // gather_pk_kernel: X / X2 are CL16 buffers (cconv_pk.hpp) with Cpk / Cpk2
+  // channels per position and pk_plane / pk_plane2 elements per plane
+  int Cpk, Cpk2;
+  long long pk_plane, pk_plane2;
+  // gather_pk_kernel: the K order (split_k) and per-tap input offsets, read as
+  // scalars from the kernel arguments
+  int ntaps, kblk;
+  int toffh[kMaxTaps], toffw[kMaxTaps];
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -421,6 +429,10 @@ struct WgradArgs {
   // SE_MATH_F16X3: device max |.| of G (the gathered tensor) and of D (both sources)
   const float* amax_g;
   const float* amax_d;
+  // wgrad_pk_kernel: X / D / D2 are CL16 buffers (cconv_pk.hpp) with these
+  // elements per plane; m_per_split counts output rows; per-tap input offsets
+  long long pk_plane_g, pk_plane_d, pk_plane_d2;
+  int toffh[kMaxTaps], toffw[kMaxTaps];
 };
 
 // Small-N weight grad (N <= 8: FRCRN's final_conv 128->2 and the CCBAM spatial
@@ -831,6 +843,7 @@ __global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int
 }
 
 #include "cconv_x3.hpp"
+#include "cconv_pk.hpp"
 
 // bias_full[n] for the fused complex conv: re = br - bi, im = bi + br.
 __global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out) {
@@ -973,6 +986,9 @@ struct ConvGeom {
   int math;       // SE_MATH_*
   const float* x_amax;    // SE_MATH_F16X3 scale sources from the caller (or nullptr)
   const float* dy_amax;
+  const void* x_packed;   // SE_MATH_F16X3 CL16 operands from the caller (or nullptr)
+  const void* x2_packed;
+  const void* dy_packed;
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -986,6 +1002,9 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.math = d->math;
   g.x_amax = d->x_amax;
   g.dy_amax = d->dy_amax;
+  g.x_packed = d->x_packed;
+  g.x2_packed = d->x2_packed;
+  g.dy_packed = d->dy_packed;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16X3) return SE_E_ARG;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
@@ -1167,6 +1186,11 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1 || f16;   // prep / tiles shared
   const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
   const float* amax_a = pass == kFwd ? g.x_amax : g.dy_amax;
+  // CL16 operands from the caller: the LDS-DMA kernel (gather_pk_kernel) on
+  // tap-uniform shapes; their scale is the caller's amax
+  const void* pk = pass == kFwd ? g.x_packed : g.dy_packed;
+  const void* pk2 = (pass == kFwd && jn && jn->x2) ? g.x2_packed : nullptr;
+  const bool packed = f16 && pk && amax_a && (!jn || !jn->x2 || pk2);
   if (f16) {
     const long long nw = (long long)(g.complex_w ? g.Ci / 2 : g.Ci) * (g.complex_w ? g.Co / 2 : g.Co) * g.kh * g.kw;
     launch_amax(wr, nw, amax_slot, st);
@@ -1241,6 +1265,36 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       else hipLaunchKernelGGL(gather_smalln_kernel<16>, grid, dim3(kThreads), sh, st, a);
     } else {
       const bool tu = tu_of(c);
+      if (packed && tu && ldw % 128 == 0) {
+        a.ntaps = c.taps.n;
+        a.kblk = kblk;
+        for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }
+        a.X = (const float*)pk;
+        a.Cpk = Cg;
+        a.pk_plane = (long long)g.B * Cg * Hi * Wi;
+        if (join_in) {
+          a.X = (const float*)pk;                 // packed s; x on its own grid
+          a.Cpk = 2 * jn->jh;
+          a.pk_plane = (long long)g.B * a.Cpk * Hi * Wi;
+          a.X2 = (const float*)pk2;
+          a.Cpk2 = 2 * jn->jh;
+          a.pk_plane2 = (long long)g.B * a.Cpk2 * jn->h2 * jn->w2;
+        }
+        const dim3 blk(kPkThreads);
+        if (ldw % 256 == 0) {           // 128 x 256 tiles
+          const dim3 grid(se::ceil_div(M, 128), ldw / 256);
+          if (join_in) hipLaunchKernelGGL((gather_pk_kernel<1, 128, 256>), grid, blk, 0, st, a);
+          else if (join_out) hipLaunchKernelGGL((gather_pk_kernel<2, 128, 256>), grid, blk, 0, st, a);
+          else hipLaunchKernelGGL((gather_pk_kernel<0, 128, 256>), grid, blk, 0, st, a);
+        } else {                        // 256 x 128 tiles
+          const dim3 grid(se::ceil_div(M, 256), ldw / 128);
+          if (join_in) hipLaunchKernelGGL((gather_pk_kernel<1, 256, 128>), grid, blk, 0, st, a);
+          else if (join_out) hipLaunchKernelGGL((gather_pk_kernel<2, 256, 128>), grid, blk, 0, st, a);
+          else hipLaunchKernelGGL((gather_pk_kernel<0, 256, 128>), grid, blk, 0, st, a);
+        }
+        SE_LAUNCH_CHECK();
+        continue;
+      }
       // 256-column workgroups (NW = 2) where the padded column count allows
       const bool wide = (ldw % 256 == 0) && gemm_nw() == 2;
       const dim3 grid(se::ceil_div(M, kX3BM), ldw / (wide ? 2 * kX3BN : kX3BN));
@@ -1291,6 +1345,21 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
+extern "C" size_t se_pack_cl16_bytes(int B, int C, int H, int W) {
+  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
+  return (size_t)2 * B * C * H * W * sizeof(_Float16);
+}
+
+extern "C" int se_pack_cl16(const float* x, int B, int C, int H, int W, const float* amax, void* out,
+                            void* stream) {
+  if (!x || !amax || !out || B <= 0 || C <= 0 || H <= 0 || W <= 0 || C % 8) return SE_E_ARG;
+  const int HW = H * W;
+  hipLaunchKernelGGL(pack_cl16_kernel, dim3(se::ceil_div(HW, 64), se::ceil_div(C, 64), B), dim3(256), 0,
+                     se::as_stream(stream), x, C, HW, amax, (_Float16*)out, (long long)B * C * HW);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
 extern "C" int se_amax(const float* x, long long n, float* amax, void* stream) {
   if (!x || !amax || n < 0) return SE_E_ARG;
   launch_amax(x, n, amax, se::as_stream(stream));
@@ -1409,7 +1478,33 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   }
   const bool tu = (w.Cg % 128 == 0) && span_w * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
                   span_w * (long long)w.Np * QQw * 4 < (1ll << 31);
-  if (w.N <= kSmallWgradN) {
+  // CL16 operands from the caller: G = packed dy (transposed) or x, D = the other
+  const void* pk_g = g.transposed ? g.dy_packed : g.x_packed;
+  const void* pk_d = g.transposed ? g.x_packed : g.dy_packed;
+  const bool packed = f16 && pk_g && pk_d && (!jn || (g.x2_packed && jn->jh % 8 == 0)) &&
+                      w.Cg % 128 == 0 && w.N % 128 == 0 && w.c.taps.n <= kMaxTaps;
+  if (packed) {
+    const int rows = g.B * w.Qh;
+    const int spr = se::ceil_div(w.Qw, 32);
+    const int tiles = (w.c.Kp / 128) * (w.Np / 128);
+    int splits = std::max(1, std::min(1024 / std::max(tiles, 1), rows * spr / 16));
+    splits = std::min(splits, w.splits);   // the slab was sized for w.splits
+    const int rps = se::ceil_div(rows, splits);
+    splits = se::ceil_div(rows, rps);
+    a.X = (const float*)pk_g; a.D = (const float*)pk_d;
+    a.m_per_split = rps;
+    a.pk_plane_g = (long long)g.B * w.Cg * w.Hi * w.Wi;
+    a.pk_plane_d = (long long)g.B * (jn ? 2 * jn->jh : w.N) * w.Qh * w.Qw;
+    if (jn) {
+      a.D2 = (const float*)g.x2_packed;
+      a.pk_plane_d2 = (long long)g.B * 2 * jn->jh * jn->h2 * jn->w2;
+    }
+    for (int t = 0; t < w.c.taps.n; ++t) { a.toffh[t] = w.c.taps.offh[t]; a.toffw[t] = w.c.taps.offw[t]; }
+    dim3 grid(w.c.Kp / 128, w.Np / 128, splits);
+    if (jn) hipLaunchKernelGGL(wgrad_pk_kernel<true>, grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL(wgrad_pk_kernel<false>, grid, dim3(kThreads), 0, st, a);
+    w.splits = splits;
+  } else if (w.N <= kSmallWgradN) {
     dim3 grid(w.c.Kp / 16, w.splits);
     if (w.Np == 4) hipLaunchKernelGGL(wgrad_smalln_kernel<4>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_smalln_kernel<8>, grid, dim3(kThreads), 0, st, a);

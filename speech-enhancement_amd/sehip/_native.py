@@ -35,7 +35,8 @@ class ConvDesc(ctypes.Structure):
         "kernel_h", "kernel_w", "stride_h", "stride_w", "pad_h", "pad_w",
         "dil_h", "dil_w", "out_pad_h", "out_pad_w", "transposed",
         "complex_weights", "pad_h_end", "pad_w_end", "math")] + [
-        ("x_amax", c_void_p), ("dy_amax", c_void_p)]   # SE_MATH_F16X3 scale sources (or NULL)
+        ("x_amax", c_void_p), ("dy_amax", c_void_p),   # SE_MATH_F16X3 scale sources (or NULL)
+        ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p)]   # CL16 operands (or NULL)
 
 
 _P = c_void_p
@@ -51,6 +52,8 @@ _SIGNATURES = {
     "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
     "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
     "se_amax": (c_int, [_P, ctypes.c_longlong, _P, _P]),
+    "se_pack_cl16_bytes": (c_size_t, [c_int] * 4),
+    "se_pack_cl16": (c_int, [_P] + [c_int] * 4 + [_P, _P, _P]),
     "se_mix_snr": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P, _P]),
     "se_crop_pad": (c_int, [_P, _P, _P, _P, c_int, c_int, _P, _P]),
     "se_pcm16_to_float": (c_int, [_P, ctypes.c_longlong, _P, _P]),
