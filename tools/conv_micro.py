@@ -70,7 +70,7 @@ for name in args.layers.split(","):
             torch.cuda.synchronize()
             # the packed weight-grad splits M by output rows: same products, other partial sums
             same = torch.equal(outs[pname](), ref) if pname != "weight" else \
-                f"rel-L2 {((outs[pname]() - ref).norm() / ref.norm()).item():.2e}
+                f"rel-L2 {((outs[pname]() - ref).norm() / ref.norm()).item():.2e}"
             t0 = time.perf_counter()
             for _ in range(args.iters):
                 calls[pname]()
