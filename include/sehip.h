@@ -294,6 +294,26 @@ int se_lstm_bwd(const float* dy, const float* w_hh, const float* gates,
                 const float* c, float* dgates, int L, int B, int T, int H,
                 unsigned rev_mask, void* stream);
 
+/* Wide hidden sizes, H in {256, 512} (CARN's nn.LSTM(512), models/
+ * _2104_05267_carn.py:132; replaces the MIOpen per-step kernels behind it):
+ * same arguments, layouts and results as se_lstm_fwd / se_lstm_bwd (no zero
+ * row; any B). W_hh is spread over a group of H/32 workgroups, each holding
+ * the gate rows (fwd) / columns (bwd) of 32 hidden units in registers; the
+ * group exchanges h_t / dgates_t through the outputs every step.
+ * sync  : device int[se_lstm_wide_sync_ints()] scratch (zeroed by the call)
+ * status: device int; set non-zero if a group barrier timed out (the outputs
+ *         are then NaN from that step on); never cleared by the library.
+ * SE_E_UNSUPPORTED when the groups cannot all be resident on the device at
+ * once (L * ceil(B / 8) * H / 32 > number of CUs). */
+int se_lstm_wide_supported(int hidden);
+int se_lstm_wide_sync_ints(void);
+int se_lstm_wide_fwd(const float* xproj, long long x_lstm_stride, int x_row_stride,
+                     const float* w_hh, float* h, float* c, float* gates, int L, int B,
+                     int T, int H, unsigned rev_mask, int* sync, int* status, void* stream);
+int se_lstm_wide_bwd(const float* dy, const float* w_hh, const float* gates,
+                     const float* c, float* dgates, int L, int B, int T, int H,
+                     unsigned rev_mask, int* sync, int* status, void* stream);
+
 /* ------------------------------------------------------------------------
  * Complex CBAM skip attention (models/modules/ccbam.py:28-106), the passes
  * over the full skip tensor x [B, C, HW] (C even, <= 512; channels [0, C/2)

@@ -77,6 +77,11 @@ _SIGNATURES = {
     "se_lstm_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P, _P] + [c_int] * 4
                     + [ctypes.c_uint, _P]),
     "se_lstm_bwd": (c_int, [_P] * 5 + [c_int] * 4 + [ctypes.c_uint, _P]),
+    "se_lstm_wide_supported": (c_int, [c_int]),
+    "se_lstm_wide_sync_ints": (c_int, []),
+    "se_lstm_wide_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P] + [c_int] * 4
+                         + [ctypes.c_uint, _P, _P, _P]),
+    "se_lstm_wide_bwd": (c_int, [_P] * 5 + [c_int] * 4 + [ctypes.c_uint, _P, _P, _P]),
     "se_ccbam_workspace_size": (c_size_t, [c_int] * 3),
     "se_ccbam_channel_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
     "se_ccbam_spatial_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),

@@ -173,16 +173,21 @@ class ComplexLinear(nn.Module):
         return merge_real_imag(x, self.real_linear(re), self.imag_linear(im), dim=-1)
 
 
+# hidden sizes of the HIP recurrence: se_lstm_* (64, 128), se_lstm_wide_* (256, 512)
+HIP_LSTM_HIDDEN = (64, 128, 256, 512)
+
+
 def _hip_lstm_ok(m: nn.LSTM) -> bool:
-    return (m.proj_size == 0 and m.hidden_size in (64, 128)
+    return (m.proj_size == 0 and m.hidden_size in HIP_LSTM_HIDDEN
             and (m.dropout == 0 or not m.training) and m.mode == "LSTM")
 
 
-def stacked_lstms(x, lstms, batch_first=True):
+def stacked_lstms(x, lstms, batch_first=True, with_state=False):
     """Run several nn.LSTMs (same shape) over the same input x on the HIP
     recurrence, all of them in the same launches: per layer one projection
     GEMM, one se_lstm_fwd over every (LSTM, direction), and in backward one
-    se_lstm_bwd. Returns one output per LSTM, shaped like nn.LSTM's output[0].
+    se_lstm_bwd. Returns one output per LSTM, shaped like nn.LSTM's output[0]
+    (with_state: and per LSTM nn.LSTM's (h_n, c_n), [layers * dirs, B, H]).
     The modules keep their own parameters (state_dict keys unchanged)."""
     m0 = lstms[0]
     nd = 2 if m0.bidirectional else 1
@@ -191,15 +196,19 @@ def stacked_lstms(x, lstms, batch_first=True):
     inp = xb.contiguous()                         # layer 0: [B, T, I] shared by every LSTM
     rev_mask = sum(1 << (i * nd + 1) for i in range(len(lstms))) if nd == 2 else 0
     out = None
+    h_last, c_last = [], []
     for k in range(m0.num_layers):
         sfx = [f"_l{k}", f"_l{k}_reverse"][:nd]
-        w_ih = torch.stack([getattr(m, "weight_ih" + s) for m in lstms for s in sfx])
-        w_hh = torch.stack([getattr(m, "weight_hh" + s) for m in lstms for s in sfx])
+        w_ih = torch.stack([_f32(getattr(m, "weight_ih" + s)) for m in lstms for s in sfx])
+        w_hh = torch.stack([_f32(getattr(m, "weight_hh" + s)) for m in lstms for s in sfx])
         b_ih = b_hh = None
         if m0.bias:
-            b_ih = torch.stack([getattr(m, "bias_ih" + s) for m in lstms for s in sfx])
-            b_hh = torch.stack([getattr(m, "bias_hh" + s) for m in lstms for s in sfx])
-        h = F.lstm_layer(inp, w_ih, w_hh, b_ih, b_hh, rev_mask)      # [len*nd, B, T, H]
+            b_ih = torch.stack([_f32(getattr(m, "bias_ih" + s)) for m in lstms for s in sfx])
+            b_hh = torch.stack([_f32(getattr(m, "bias_hh" + s)) for m in lstms for s in sfx])
+        h, c = F.lstm_layer(inp, w_ih, w_hh, b_ih, b_hh, rev_mask, with_cell=True)   # [len*nd, B, T, H]
+        if with_state:   # last step in processing order: t = T-1 forward, t = 0 reverse
+            h_last.append(torch.stack([h[i, :, 0 if i % nd else -1] for i in range(h.shape[0])]))
+            c_last.append(torch.stack([c[i, :, 0 if i % nd else -1] for i in range(c.shape[0])]))
         Bn, T = h.shape[1], h.shape[2]
         if nd == 2:   # per LSTM: cat(forward, reverse) on features, fed to both directions
             out = h.view(len(lstms), 2, Bn, T, H).permute(0, 2, 3, 1, 4).reshape(len(lstms), Bn, T, 2 * H)
@@ -210,7 +219,33 @@ def stacked_lstms(x, lstms, batch_first=True):
                 out = torch.nn.functional.dropout(out, m0.dropout, True)
             inp = out.repeat_interleave(nd, dim=0) if nd == 2 else out
     outs = list(out.unbind(0))
-    return outs if batch_first else [o.transpose(0, 1) for o in outs]
+    outs = outs if batch_first else [o.transpose(0, 1) for o in outs]
+    if not with_state:
+        return outs
+    # per LSTM: [layers * dirs, B, H] in nn.LSTM's (layer, direction) order
+    hs = torch.stack(h_last).view(m0.num_layers, len(lstms), nd, -1, H)
+    cs = torch.stack(c_last).view(m0.num_layers, len(lstms), nd, -1, H)
+    states = [(hs[:, i].reshape(m0.num_layers * nd, -1, H), cs[:, i].reshape(m0.num_layers * nd, -1, H))
+              for i in range(len(lstms))]
+    return outs, states
+
+
+class LSTM(nn.LSTM):
+    """torch.nn.LSTM (same constructor, parameters and state_dict keys) whose
+    recurrence runs on the HIP kernels (stacked_lstms) when the configuration
+    is covered: hidden 64 / 128 / 256 / 512, no proj_size, no initial state,
+    a dense [B, T, I] (batch_first) or [T, B, I] CUDA input. fp16 / bf16
+    parameters and inputs (model.half()) compute in fp32 and return the
+    caller's dtype. Anything else is nn.LSTM's own forward."""
+
+    def forward(self, input, hx=None):
+        if (hx is None and _hip_lstm_ok(self) and isinstance(input, torch.Tensor) and input.is_cuda
+                and input.dim() == 3):
+            dt = input.dtype
+            outs, states = stacked_lstms(_f32(input), [self], batch_first=self.batch_first, with_state=True)
+            h_n, c_n = states[0]
+            return outs[0].to(dt), (h_n.to(dt), c_n.to(dt))
+        return super().forward(input, hx)
 
 
 class ComplexLSTM(nn.Module):

@@ -686,7 +686,34 @@ def _zero_row(n: int, device) -> torch.Tensor:
 
 
 def lstm_supported(hidden: int) -> bool:
-    return bool(N.lib().se_lstm_supported(int(hidden)))
+    """H the HIP recurrence covers: 64 / 128 (se_lstm_*, one workgroup per
+    sequence pair) and 256 / 512 (se_lstm_wide_*, a group of H/32 workgroups)."""
+    return bool(N.lib().se_lstm_supported(int(hidden))) or bool(N.lib().se_lstm_wide_supported(int(hidden)))
+
+
+_WIDE: dict = {}
+
+
+def _wide_ws(device):
+    """Per-device (sync counters, status word) of se_lstm_wide_*. The status
+    word stays 0 unless a group barrier timed out (lstm_wide_status)."""
+    key = str(device)
+    w = _WIDE.get(key)
+    if w is None:
+        n = int(N.lib().se_lstm_wide_sync_ints())
+        w = _WIDE[key] = (torch.zeros(n, device=device, dtype=torch.int32),
+                          torch.zeros(1, device=device, dtype=torch.int32))
+    return w
+
+
+def lstm_wide_status(device="cuda") -> int:
+    """0 unless a se_lstm_wide_* group barrier timed out on `device` (then its
+    outputs were written as NaN). Synchronises."""
+    return int(_wide_ws(torch.device(device))[1].item())
+
+
+def _wide(H: int) -> bool:
+    return H in (256, 512)
 
 
 class _LstmLayer(torch.autograd.Function):
@@ -729,27 +756,45 @@ class _LstmLayer(torch.autograd.Function):
         c = torch.empty_like(h)
         gates = torch.empty((L, B, T, G), device=x.device, dtype=x.dtype)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(N.lib().se_lstm_fwd(xproj.data_ptr(), x_lstm, x_row, w_hh.data_ptr(),
-                                    _zero_row(H, x.device).data_ptr(), h.data_ptr(), c.data_ptr(),
-                                    gates.data_ptr(), L, B, T, H, int(rev_mask), N.stream_of(x)),
-                "se_lstm_fwd")
+        if _wide(H):
+            sync, status = _wide_ws(x.device)
+            N.check(N.lib().se_lstm_wide_fwd(xproj.data_ptr(), x_lstm, x_row, w_hh.data_ptr(), h.data_ptr(),
+                                             c.data_ptr(), gates.data_ptr(), L, B, T, H, int(rev_mask),
+                                             sync.data_ptr(), status.data_ptr(), N.stream_of(x)),
+                    "se_lstm_wide_fwd")
+        else:
+            N.check(N.lib().se_lstm_fwd(xproj.data_ptr(), x_lstm, x_row, w_hh.data_ptr(),
+                                        _zero_row(H, x.device).data_ptr(), h.data_ptr(), c.data_ptr(),
+                                        gates.data_ptr(), L, B, T, H, int(rev_mask), N.stream_of(x)),
+                    "se_lstm_fwd")
         if t0 is not None:
             _TIMER.end("lstm_fwd", t0, 2.0 * L * B * T * G * H, 4.0 * L * B * T * (G + 2 * G + 2 * H))
         ctx.save_for_backward(x, w_ih, w_hh, h, c, gates)
         ctx.rev_mask, ctx.has_b = int(rev_mask), (b_ih is not None, b_hh is not None)
-        return h
+        ctx.mark_non_differentiable(c)
+        ctx.set_materialize_grads(False)
+        return h, c
 
     @staticmethod
-    def backward(ctx, dh):
+    def backward(ctx, dh, dc):
+        if dc is not None:
+            raise NotImplementedError("sehip lstm: no gradient through the cell states (c_n)")
         x, w_ih, w_hh, h, c, gates = ctx.saved_tensors
         L, B, T, H = h.shape
         G, I = 4 * H, w_ih.shape[2]
-        dh = dh.contiguous()
+        dh = torch.zeros_like(h) if dh is None else dh.contiguous()
         dgates = torch.empty_like(gates)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(N.lib().se_lstm_bwd(dh.data_ptr(), w_hh.data_ptr(), gates.data_ptr(), c.data_ptr(),
-                                    dgates.data_ptr(), L, B, T, H, ctx.rev_mask, N.stream_of(dh)),
-                "se_lstm_bwd")
+        if _wide(H):
+            sync, status = _wide_ws(dh.device)
+            N.check(N.lib().se_lstm_wide_bwd(dh.data_ptr(), w_hh.data_ptr(), gates.data_ptr(), c.data_ptr(),
+                                             dgates.data_ptr(), L, B, T, H, ctx.rev_mask, sync.data_ptr(),
+                                             status.data_ptr(), N.stream_of(dh)),
+                    "se_lstm_wide_bwd")
+        else:
+            N.check(N.lib().se_lstm_bwd(dh.data_ptr(), w_hh.data_ptr(), gates.data_ptr(), c.data_ptr(),
+                                        dgates.data_ptr(), L, B, T, H, ctx.rev_mask, N.stream_of(dh)),
+                    "se_lstm_bwd")
         if t0 is not None:
             _TIMER.end("lstm_bwd", t0, 2.0 * L * B * T * G * H, 4.0 * L * B * T * (H + 2 * G + 2 * H))
         dg = dgates.reshape(L, B * T, G)
@@ -780,9 +825,11 @@ class _LstmLayer(torch.autograd.Function):
         return dx, dw_ih, dw_hh, db_ih, db_hh, None
 
 
-def lstm_layer(x, w_ih, w_hh, b_ih=None, b_hh=None, rev_mask: int = 0):
-    """h [L, B, T, H] of L stacked LSTMs over x ([B, T, I] shared or [L, B, T, I])."""
-    return _LstmLayer.apply(x, w_ih, w_hh, b_ih, b_hh, rev_mask)
+def lstm_layer(x, w_ih, w_hh, b_ih=None, b_hh=None, rev_mask: int = 0, with_cell: bool = False):
+    """h [L, B, T, H] of L stacked LSTMs over x ([B, T, I] shared or [L, B, T, I]);
+    with_cell: (h, c) with the cell states c (no gradient through c)."""
+    h, c = _LstmLayer.apply(x, w_ih, w_hh, b_ih, b_hh, rev_mask)
+    return (h, c) if with_cell else h
 
 
 # --------------------------------------------------------------------------

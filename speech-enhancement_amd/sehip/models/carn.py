@@ -3,8 +3,8 @@
 A real-valued conv U-Net over stacked re/im. The spectral front and back end
 (ConvSTFT / ConviSTFT) and every real conv / transposed conv (encoder, GLU
 gates, decoder, attention gates) run on the HIP kernels (the real-weight form
-of the conv GEMMs, complex_nn.real_conv2d); BatchNorm, PReLU and the 512-wide
-LSTM are PyTorch device ops.
+of the conv GEMMs, complex_nn.real_conv2d); BatchNorm and PReLU are PyTorch device ops; the
+LSTM (H = 512) runs on the wide HIP recurrence (complex_nn.LSTM -> se_lstm_wide_*).
 """
 from __future__ import annotations
 
@@ -12,7 +12,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as TF
 
-from ..complex_nn import real_conv2d
+from ..complex_nn import LSTM, real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -135,7 +135,7 @@ class CARN(nn.Module):
         self.istft = ConviSTFT(window_size, hop_size, fft_size)
         self.encoder = Encoder(in_channels=2, gate=gate)
         self.decoder = Decoder(in_channels=128, gate=gate)
-        self.lstm = nn.LSTM(input_size=lstm_channels, hidden_size=lstm_channels, num_layers=2, batch_first=True)
+        self.lstm = LSTM(input_size=lstm_channels, hidden_size=lstm_channels, num_layers=2, batch_first=True)
         self.linear = nn.Linear(in_features=fft_size, out_features=fft_size + 2)
 
     def forward(self, x):

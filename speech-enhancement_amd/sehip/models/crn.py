@@ -8,7 +8,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as TF
 
-from ..complex_nn import real_conv2d
+from ..complex_nn import LSTM, real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -86,7 +86,7 @@ class CRN(nn.Module):
         self.stft = ConvSTFT(window_size, hop_size, fft_size, return_mag_phase=True)
         self.istft = ConviSTFT(window_size, hop_size, fft_size)
         self.encoder = Encoder()
-        self.lstm_layers = nn.LSTM(input_size=1024, hidden_size=1024, num_layers=2, batch_first=True)
+        self.lstm_layers = LSTM(input_size=1024, hidden_size=1024, num_layers=2, batch_first=True)
         self.decoder = Decoder()
 
     def forward(self, x):

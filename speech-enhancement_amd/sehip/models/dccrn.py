@@ -6,7 +6,7 @@ import torch.nn as nn
 import torch.nn.functional as TF
 
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLinear,
-                          ComplexLSTM, complex_concat, norm_act, real_conv2d)
+                          ComplexLSTM, LSTM, complex_concat, norm_act, real_conv2d)
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -65,7 +65,7 @@ class LSTMBlock(nn.Module):
             self.layers.append(ComplexLSTM(nd * hidden_channels, hidden_channels, num_layers=1, **kwargs))
             self.layers.append(ComplexLinear(nd * hidden_channels, linear_channels))
         else:
-            self.layers.append(nn.LSTM(in_channels, hidden_channels, num_layers=num_layers, **kwargs))
+            self.layers.append(LSTM(in_channels, hidden_channels, num_layers=num_layers, **kwargs))
             self.layers.append(nn.Linear(nd * hidden_channels, linear_channels))
 
     def forward(self, x):
