@@ -315,6 +315,47 @@ int se_lstm_wide_bwd(const float* dy, const float* w_hh, const float* gates,
                      unsigned rev_mask, int* sync, int* status, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Train-step glue (trainer.py:99-124, :210-221)
+ *
+ * SI-SNR loss (losses.py:62-84) of B estimates against B targets [B, lt]
+ * with utils.py:111-121's pad / truncate folded in: estimate row b is
+ * est + b*est_stride, le samples (zero past le, ignored past lt).
+ * loss: device fp32 [1] = -mean_b 10 log10(signal / noise);
+ * save: device scratch of se_sisnr_save_bytes(B), kept for se_sisnr_bwd;
+ * grad_est: [B] rows of le (stride grad_stride) = grad_loss[0] * dloss/dest.
+ *
+ * Parameter update over a device table of slots (the concatenation of every
+ * tensor; offset = prefix sum of numel, slots in offset order):
+ * se_grad_sumsq   : sumsq[0] = sum of grad^2 (fp64, device; sumsq holds
+ *                   SE_SUMSQ_DOUBLES doubles: [1..] are per-workgroup
+ *                   partials, added in a fixed order: deterministic);
+ * se_clip_grads   : grads *= min(max_norm / (sqrt(*sumsq) + 1e-6), 1)
+ *                   (torch.nn.utils.clip_grad_norm_; total_norm -> [1] if set);
+ * se_adamw_step   : torch.optim.AdamW (amsgrad off) at step `step` (>= 1).
+ * ------------------------------------------------------------------------ */
+#define SE_SUMSQ_DOUBLES 2049
+typedef struct se_tensor_slot {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  long long numel;
+  long long offset;
+} se_tensor_slot;
+
+size_t se_sisnr_save_bytes(int B);
+int se_sisnr_fwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
+                 int zero_mean, float eps, float* loss, void* save, void* stream);
+int se_sisnr_bwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
+                 int zero_mean, float eps, const void* save, const float* grad_loss, float* grad_est,
+                 long long grad_stride, void* stream);
+int se_grad_sumsq(const se_tensor_slot* slots, int nslots, long long total, double* sumsq, void* stream);
+int se_clip_grads(const se_tensor_slot* slots, int nslots, long long total, const double* sumsq,
+                  float max_norm, float* total_norm, void* stream);
+int se_adamw_step(const se_tensor_slot* slots, int nslots, long long total, double lr, double beta1,
+                  double beta2, double eps, double weight_decay, long long step, void* stream);
+
+/* ------------------------------------------------------------------------
  * Complex CBAM skip attention (models/modules/ccbam.py:28-106), the passes
  * over the full skip tensor x [B, C, HW] (C even, <= 512; channels [0, C/2)
  * real, [C/2, C) imag). The shared MLP (ccbam.py:38-41) and the 4->2 k7

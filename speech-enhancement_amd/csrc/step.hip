@@ -1,0 +1,286 @@
+// Train-step glue: the loss and the parameter update of
+// one iteration of the reference's hot loop, as a handful of launches instead
+// of dozens of ATen reductions and foreach kernels.
+//
+//  * SI-SNR (losses.py:62-84) with utils.py:111-121's pad / truncate of the
+//    estimate folded into the reads: one workgroup per utterance (fp64 sums),
+//    one finalize launch for the batch mean; the backward is one elementwise
+//    pass from the saved per-utterance sums.
+//  * clip_grad_norm_(max_norm) + AdamW.step (trainer.py:216-221) over a device
+//    table of parameter slots (the virtual concatenation of every tensor):
+//    one sum-of-squares launch, one clip launch, one AdamW launch per step.
+#include "common.hpp"
+
+#include <cmath>
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 8192;     // elements per workgroup iteration of the slot kernels
+
+template <typename T>
+__device__ __forceinline__ T block_sum(T v, T* red) {
+  v = se::wave_sum(v);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
+  __syncthreads();
+  T s = 0;
+#pragma unroll
+  for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+  __syncthreads();
+  return s;
+}
+
+// per-utterance save: [0] mean e, [1] mean t, [2] dot (fp32), [3] |t|^2 (fp32),
+// [4] S, [5] N, [6] sum p, [7] sum (e' - p)  (doubles)
+constexpr int kSave = 8;
+
+__global__ void __launch_bounds__(kThreads)
+sisnr_items_kernel(const float* __restrict__ est, int le, long long est_stride, const float* __restrict__ tgt, int lt,
+                   int zero_mean, double* __restrict__ save) {
+  const int b = blockIdx.x;
+  const float* e = est + (long long)b * est_stride;
+  const float* t = tgt + (long long)b * lt;
+  const int ne = min(le, lt);                 // estimate samples inside the target length
+  __shared__ double red[kThreads / 64];
+  float me = 0.f, mt = 0.f;
+  if (zero_mean) {
+    double se_ = 0, st = 0;
+    for (int i = threadIdx.x; i < lt; i += kThreads) {
+      se_ += i < ne ? e[i] : 0.f;
+      st += t[i];
+    }
+    me = (float)(block_sum(se_, red) / lt);
+    mt = (float)(block_sum(st, red) / lt);
+  }
+  double dot = 0, tt = 0;
+  for (int i = threadIdx.x; i < lt; i += kThreads) {
+    const float ei = (i < ne ? e[i] : 0.f) - me, ti = t[i] - mt;
+    dot += (double)ei * ti;
+    tt += (double)ti * ti;
+  }
+  const float dotf = (float)block_sum(dot, red), ttf = (float)block_sum(tt, red);
+  double S = 0, Nn = 0, sp = 0, sr = 0;
+  for (int i = threadIdx.x; i < lt; i += kThreads) {
+    const float ei = (i < ne ? e[i] : 0.f) - me, ti = t[i] - mt;
+    const float p = dotf * ti / ttf;          // proj = sum(e*t) * t / t_energy
+    const float r = ei - p;
+    S += (double)p * p;
+    Nn += (double)r * r;
+    sp += p;
+    sr += r;
+  }
+  S = block_sum(S, red);
+  Nn = block_sum(Nn, red);
+  sp = block_sum(sp, red);
+  sr = block_sum(sr, red);
+  if (threadIdx.x == 0) {
+    double* s = save + (long long)b * kSave;
+    s[0] = me; s[1] = mt; s[2] = dotf; s[3] = ttf; s[4] = S; s[5] = Nn; s[6] = sp; s[7] = sr;
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+sisnr_finalize_kernel(const double* __restrict__ save, int B, float eps, float* __restrict__ loss) {
+  __shared__ double red[kThreads / 64];
+  double acc = 0;
+  for (int b = threadIdx.x; b < B; b += kThreads) {
+    const double* s = save + (long long)b * kSave;
+    const float sig = (float)s[4] + eps, noi = (float)s[5] + eps;
+    acc += (double)(10.f * log10f(sig / noi));
+  }
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) loss[0] = (float)(-acc / B);
+}
+
+// grid (ceil(le / kThreads / 4), B): d est[b, i] for i < le (0 past the target length)
+__global__ void __launch_bounds__(kThreads)
+sisnr_bwd_kernel(const float* __restrict__ est, int le, long long est_stride, const float* __restrict__ tgt, int lt,
+                 int B, int zero_mean, float eps, const double* __restrict__ save, const float* __restrict__ gloss,
+                 float* __restrict__ gest, long long g_stride) {
+  const int b = blockIdx.y;
+  const double* s = save + (long long)b * kSave;
+  const float me = (float)s[0], mt = (float)s[1], dotf = (float)s[2], ttf = (float)s[3];
+  const float sig = (float)s[4] + eps, noi = (float)s[5] + eps;
+  // L_b = 10 log10(sig / noi); loss = -mean_b L_b
+  const float k = -gloss[0] * 10.f / ((float)B * 2.302585093f);
+  const float cs = 2.f * k / sig, cn = -2.f * k / noi;      // dL/dp-part, dL/d(e'-p)-part
+  const float gmean = zero_mean ? (float)((cs * s[6] + cn * s[7]) / lt) : 0.f;
+  const float* e = est + (long long)b * est_stride;
+  const float* t = tgt + (long long)b * lt;
+  const int ne = min(le, lt);
+  for (int u = 0; u < 4; ++u) {
+    const int i = (blockIdx.x * 4 + u) * kThreads + threadIdx.x;
+    if (i >= le) return;
+    float g = 0.f;
+    if (i < ne) {
+      const float ei = e[i] - me, ti = t[i] - mt;
+      const float p = dotf * ti / ttf;
+      g = cs * p + cn * (ei - p) - gmean;
+    }
+    gest[(long long)b * g_stride + i] = g;
+  }
+}
+
+// ------------------------------------------------------------------ slots
+struct Slot {
+  float* param;
+  float* grad;
+  float* exp_avg;
+  float* exp_avg_sq;
+  long long numel;
+  long long offset;   // prefix sum of numel (slots in offset order)
+};
+static_assert(sizeof(Slot) == sizeof(se_tensor_slot), "Slot mirrors se_tensor_slot");
+
+__device__ __forceinline__ int find_slot(const Slot* slots, int n, long long pos) {
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (slots[mid].offset <= pos) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+// Visit every element of the concatenation: f(slot, index in slot).
+template <typename F>
+__device__ __forceinline__ void for_each_elem(const Slot* slots, int nslots, long long total, F f) {
+  for (long long c0 = (long long)blockIdx.x * kChunk; c0 < total; c0 += (long long)gridDim.x * kChunk) {
+    const long long c1 = min(total, c0 + kChunk);
+    int s = find_slot(slots, nslots, c0);
+    long long pos = c0;
+    while (pos < c1) {
+      const Slot sl = slots[s];
+      const long long end = min(c1, sl.offset + sl.numel);
+      for (long long i = pos + threadIdx.x; i < end; i += kThreads) f(sl, i - sl.offset);
+      pos = end;
+      ++s;
+    }
+  }
+}
+
+// per-workgroup partial sums into out[1 + blockIdx.x]; sumsq_final_kernel adds
+// them in a fixed order into out[0] (deterministic, unlike fp64 atomics)
+__global__ void __launch_bounds__(kThreads)
+sumsq_kernel(const Slot* __restrict__ slots, int nslots, long long total, double* __restrict__ out) {
+  __shared__ double red[kThreads / 64];
+  double acc = 0;
+  for_each_elem(slots, nslots, total, [&](const Slot& s, long long i) {
+    const float g = s.grad[i];
+    acc += (double)g * g;
+  });
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) out[1 + blockIdx.x] = acc;
+}
+
+__global__ void __launch_bounds__(kThreads)
+sumsq_final_kernel(double* __restrict__ out, int nparts) {
+  __shared__ double red[kThreads / 64];
+  double acc = 0;
+  for (int i = threadIdx.x; i < nparts; i += kThreads) acc += out[1 + i];
+  acc = block_sum(acc, red);
+  if (threadIdx.x == 0) out[0] = acc;
+}
+
+// torch.nn.utils.clip_grad_norm_: coef = max_norm / (total_norm + 1e-6),
+// clamped to 1, every gradient multiplied by it
+__global__ void __launch_bounds__(kThreads)
+clip_kernel(const Slot* __restrict__ slots, int nslots, long long total, const double* __restrict__ sumsq,
+            float max_norm, float* __restrict__ norm_out) {
+  const float tn = (float)sqrt(*sumsq);
+  const float coef = fminf(max_norm / (tn + 1e-6f), 1.f);
+  if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = tn;
+  for_each_elem(slots, nslots, total, [&](const Slot& s, long long i) { s.grad[i] *= coef; });
+}
+
+// torch.optim.AdamW (foreach form, amsgrad off):
+//   p *= 1 - lr wd;  m = lerp(m, g, 1 - b1);  v = b2 v + (1 - b2) g g
+//   p += -step_size * m / (sqrt(v) / bc2_sqrt + eps)
+__global__ void __launch_bounds__(kThreads)
+adamw_kernel(const Slot* __restrict__ slots, int nslots, long long total, float decay, float w1, float beta2,
+             float omb2, float bc2_sqrt, float eps, float neg_step) {
+  for_each_elem(slots, nslots, total, [&](const Slot& s, long long i) {
+    const float g = s.grad[i];
+    float p = s.param[i] * decay;
+    float m = s.exp_avg[i];
+    m = m + w1 * (g - m);                      // lerp, weight < 0.5 branch
+    float v = s.exp_avg_sq[i] * beta2;
+    v = v + omb2 * g * g;
+    const float denom = sqrtf(v) / bc2_sqrt + eps;
+    p = p + neg_step * m / denom;
+    s.param[i] = p;
+    s.exp_avg[i] = m;
+    s.exp_avg_sq[i] = v;
+  });
+}
+
+constexpr int kMaxSlotGrid = 2048;
+inline unsigned slot_grid(long long total) {
+  const long long g = (total + kChunk - 1) / kChunk;
+  return (unsigned)(g < kMaxSlotGrid ? (g > 0 ? g : 1) : kMaxSlotGrid);
+}
+
+}  // namespace
+
+extern "C" size_t se_sisnr_save_bytes(int B) { return (size_t)(B > 0 ? B : 0) * kSave * sizeof(double); }
+
+extern "C" int se_sisnr_fwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
+                            int zero_mean, float eps, float* loss, void* save, void* stream) {
+  if (!est || !target || !loss || !save || B <= 0 || le <= 0 || lt <= 0 || est_stride < le) return SE_E_ARG;
+  hipStream_t st = se::as_stream(stream);
+  hipLaunchKernelGGL(sisnr_items_kernel, dim3(B), dim3(kThreads), 0, st, est, le, est_stride, target, lt, zero_mean,
+                     (double*)save);
+  SE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sisnr_finalize_kernel, dim3(1), dim3(kThreads), 0, st, (const double*)save, B, eps, loss);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_sisnr_bwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
+                            int zero_mean, float eps, const void* save, const float* grad_loss, float* grad_est,
+                            long long grad_stride, void* stream) {
+  if (!est || !target || !save || !grad_loss || !grad_est || B <= 0 || le <= 0 || lt <= 0 || est_stride < le ||
+      grad_stride < le)
+    return SE_E_ARG;
+  hipLaunchKernelGGL(sisnr_bwd_kernel, dim3(se::ceil_div(le, 4 * kThreads), B), dim3(kThreads), 0,
+                     se::as_stream(stream), est, le, est_stride, target, lt, B, zero_mean, eps, (const double*)save,
+                     grad_loss, grad_est, grad_stride);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_grad_sumsq(const se_tensor_slot* slots, int nslots, long long total, double* sumsq, void* stream) {
+  if (!slots || !sumsq || nslots <= 0 || total < 0) return SE_E_ARG;
+  hipStream_t st = se::as_stream(stream);
+  if (total == 0) return hipMemsetAsync(sumsq, 0, sizeof(double), st) == hipSuccess ? SE_OK : SE_E_LAUNCH;
+  const unsigned grid = slot_grid(total);
+  static_assert(kMaxSlotGrid + 1 == SE_SUMSQ_DOUBLES, "partials fit the caller's buffer");
+  hipLaunchKernelGGL(sumsq_kernel, dim3(grid), dim3(kThreads), 0, st, (const Slot*)slots, nslots, total, sumsq);
+  SE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(kThreads), 0, st, sumsq, (int)grid);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_clip_grads(const se_tensor_slot* slots, int nslots, long long total, const double* sumsq,
+                             float max_norm, float* total_norm, void* stream) {
+  if (!slots || !sumsq || nslots <= 0 || total < 0) return SE_E_ARG;
+  if (total == 0) return SE_OK;
+  hipLaunchKernelGGL(clip_kernel, dim3(slot_grid(total)), dim3(kThreads), 0, se::as_stream(stream),
+                     (const Slot*)slots, nslots, total, sumsq, max_norm, total_norm);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_adamw_step(const se_tensor_slot* slots, int nslots, long long total, double lr, double beta1,
+                             double beta2, double eps, double weight_decay, long long step, void* stream) {
+  if (!slots || nslots <= 0 || total < 0 || step < 1) return SE_E_ARG;
+  if (total == 0) return SE_OK;
+  // host scalars as torch computes them (Python floats, then the kernel's fp32)
+  const double bc1 = 1.0 - std::pow(beta1, (double)step);
+  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  hipLaunchKernelGGL(adamw_kernel, dim3(slot_grid(total)), dim3(kThreads), 0, se::as_stream(stream),
+                     (const Slot*)slots, nslots, total, (float)(1.0 - lr * weight_decay), (float)(1.0 - beta1),
+                     (float)beta2, (float)(1.0 - beta2), (float)std::sqrt(bc2), (float)eps, (float)(-(lr / bc1)));
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}

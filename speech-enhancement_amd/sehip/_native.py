@@ -77,6 +77,13 @@ _SIGNATURES = {
     "se_lstm_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P, _P] + [c_int] * 4
                     + [ctypes.c_uint, _P]),
     "se_lstm_bwd": (c_int, [_P] * 5 + [c_int] * 4 + [ctypes.c_uint, _P]),
+    "se_sisnr_save_bytes": (c_size_t, [c_int]),
+    "se_sisnr_fwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P]),
+    "se_sisnr_bwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P,
+                             ctypes.c_longlong, _P]),
+    "se_grad_sumsq": (c_int, [_P, c_int, ctypes.c_longlong, _P, _P]),
+    "se_clip_grads": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_float, _P, _P]),
+    "se_adamw_step": (c_int, [_P, c_int, ctypes.c_longlong] + [ctypes.c_double] * 5 + [ctypes.c_longlong, _P]),
     "se_lstm_wide_supported": (c_int, [c_int]),
     "se_lstm_wide_sync_ints": (c_int, []),
     "se_lstm_wide_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P] + [c_int] * 4

@@ -16,16 +16,31 @@ import os
 
 import torch
 
-from .losses import SI_SNR_loss, pad_or_truncate_wav, reshape_wav_to_mono
+from . import optim as _optim
+from .losses import si_snr_loss_aligned
 
 ADAMW = dict(lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2)   # hparams/*.py
 CLIP_NORM = 0.5                                                           # hyperparams.py:10
 
 
 def make_optimizer(model, **overrides):
+    """AdamW with the reference's hyper-parameters: sehip.optim.AdamW (one HIP
+    launch per step) for CUDA fp32 parameters, torch.optim.AdamW otherwise."""
     kw = dict(ADAMW)
     kw.update(overrides)
-    return torch.optim.AdamW(model.parameters(), **kw)
+    params = list(model.parameters())
+    if params and all(p.is_cuda and p.dtype == torch.float32 for p in params):
+        return _optim.AdamW(params, **kw)
+    return torch.optim.AdamW(params, **kw)
+
+
+def _clip(model, clip_norm):
+    """clip_grad_norm_(model.parameters(), clip_norm) (trainer.py:216-218): the
+    HIP slot kernels for fp32 CUDA gradients."""
+    grads = [p.grad for p in model.parameters() if p.grad is not None]
+    if grads and all(g.is_cuda and g.dtype == torch.float32 and g.is_contiguous() for g in grads):
+        return _optim.clip_grad_norm_(model.parameters(), clip_norm)
+    return torch.nn.utils.clip_grad_norm_(model.parameters(), clip_norm)
 
 
 def _defer_ok(model) -> bool:
@@ -73,14 +88,12 @@ def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
 def _train_step(model, optimizer, noisy, clean, clip_norm):
     from .functional import deferred_weight_grads
     _, wav = model(noisy)
-    target = reshape_wav_to_mono(clean)
-    est = pad_or_truncate_wav(reshape_wav_to_mono(wav), target)
-    loss = SI_SNR_loss(est, target)
+    loss = si_snr_loss_aligned(wav, clean)     # mono reshape + pad / truncate + SI-SNR
     with deferred_weight_grads(_defer_ok(model)):
         loss.backward()
     finish_grads(model)
     if clip_norm:
-        torch.nn.utils.clip_grad_norm_(model.parameters(), clip_norm)
+        _clip(model, clip_norm)
     optimizer.step()
     optimizer.zero_grad(set_to_none=True)
     return loss.detach()

@@ -1,0 +1,145 @@
+"""Train-step glue on the HIP kernels (csrc/step.hip):
+SI-SNR loss forward/backward with the pad / truncate folded in
+(losses.py:62-84, utils.py:105-121), clip_grad_norm_ and AdamW
+(trainer.py:216-221).
+
+Oracle: oracle/train.py's restatement of the reference loss (checked against
+the reference's train-step golden in test_oracle_golden.py), evaluated in
+fp64 on the CPU with autograd; torch.nn.utils.clip_grad_norm_ and
+torch.optim.AdamW (fp32, the ops the reference calls) on the same GPU for the
+update. Tolerances: loss |d| <= 1e-5 |loss| + 1e-5 (fp64 sums vs fp32
+rounding of the reference formula), gradients rel-L2 <= 1e-5; clip and AdamW
+per element <= 1e-6 relative (same fp32 formulas, fp64 norm)."""
+import pytest
+import torch
+
+from conftest import rel_l2
+
+pytestmark = pytest.mark.gpu
+
+
+def _rel(a, b):
+    return rel_l2(a.detach().double().cpu().numpy(), b.detach().double().cpu().numpy())
+
+
+@pytest.mark.parametrize("B,le,lt,zero_mean,chan", [
+    (4, 16000, 16000, False, False),
+    (3, 15840, 16000, False, True),     # estimate shorter: zero-padded (iSTFT length)
+    (2, 16400, 16000, True, False),     # estimate longer: truncated; zero-mean form
+    (1, 64000, 64000, False, False),
+    (64, 64000, 64000, False, True),    # the bench batch, [B, 1, L] estimate
+])
+def test_sisnr_matches_oracle(gpu_device, B, le, lt, zero_mean, chan):
+    from oracle.train import pad_or_truncate_wav as o_pad, si_snr_loss as o_loss
+    from sehip.losses import si_snr_loss_aligned
+    g = torch.Generator().manual_seed(B * 7 + le)
+    tgt = torch.randn(B, lt, generator=g) * 0.3
+    est = torch.randn(B, le, generator=g) * 0.2
+    est[:, :min(le, lt)] += 0.8 * tgt[:, :min(le, lt)]
+    e64 = est.double().requires_grad_(True)
+    ref = o_loss(o_pad(e64, tgt.double()), tgt.double(), zero_mean=zero_mean)
+    ref.backward()
+    ed = est.to(gpu_device)
+    ed = (ed[:, None] if chan else ed).requires_grad_(True)
+    loss = si_snr_loss_aligned(ed, tgt.to(gpu_device), zero_mean=zero_mean)
+    assert loss.shape == ()
+    assert abs(loss.item() - ref.item()) <= 1e-5 * abs(ref.item()) + 1e-5
+    loss.backward()
+    gd = ed.grad.reshape(B, le)
+    assert _rel(gd, e64.grad) < 1e-5
+    if le > lt:
+        assert torch.count_nonzero(gd[:, lt:]) == 0
+
+
+def test_sisnr_drop_in_equal_lengths(gpu_device):
+    """SI_SNR_loss (the reference's signature) on [B, L] CUDA fp32 uses the kernel
+    and agrees with the plain-PyTorch fp32 formula."""
+    from sehip.losses import SI_SNR_loss
+    torch.manual_seed(0)
+    t = torch.randn(8, 4000, device=gpu_device)
+    e = (0.7 * t + 0.3 * torch.randn_like(t)).requires_grad_(True)
+    loss = SI_SNR_loss(e, t)
+    te = t.pow(2).sum(1, keepdim=True)
+    e2 = e.detach().clone().requires_grad_(True)
+    proj = (e2 * t).sum(1, keepdim=True) * t / te
+    ref = -torch.mean(10 * torch.log10((proj.pow(2).sum(1) + 1e-8) / ((e2 - proj).pow(2).sum(1) + 1e-8)))
+    assert abs(loss.item() - ref.item()) < 1e-5 * abs(ref.item())
+    loss.backward()
+    ref.backward()
+    assert _rel(e.grad, e2.grad) < 1e-5
+
+
+def _params(dev, seed):
+    g = torch.Generator().manual_seed(seed)
+    shapes = [(64, 128, 5, 2), (64,), (1,), (3, 7), (1024, 257), (2,)]
+    ps = [torch.nn.Parameter(torch.randn(s, generator=g).to(dev)) for s in shapes]
+    for p in ps:
+        p.grad = (torch.randn(p.shape, generator=g) * 0.05).to(dev)
+    return ps
+
+
+def test_clip_grad_norm_matches_torch(gpu_device):
+    from sehip.optim import clip_grad_norm_
+    for max_norm in (0.5, 1e6):          # clipping and not clipping (coef clamped to 1)
+        a, b = _params(gpu_device, 1), _params(gpu_device, 1)
+        ta = torch.nn.utils.clip_grad_norm_(a, max_norm)
+        tb = clip_grad_norm_(b, max_norm)
+        assert abs(ta.item() - tb.item()) <= 1e-6 * ta.item()
+        for pa, pb in zip(a, b):
+            assert torch.allclose(pa.grad, pb.grad, rtol=1e-6, atol=0)
+
+
+def test_adamw_matches_torch_over_steps(gpu_device):
+    from sehip.optim import AdamW
+    a, b = _params(gpu_device, 2), _params(gpu_device, 2)
+    oa = torch.optim.AdamW(a, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2)
+    ob = AdamW(b, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2)
+    g = torch.Generator().manual_seed(3)
+    for step in range(4):
+        oa.step()
+        ob.step()
+        for pa, pb in zip(a, b):
+            d = (pa - pb).abs().max().item()
+            assert d <= 1e-6 * max(pa.abs().max().item(), 1.0), (step, d)
+            ng = (torch.randn(pa.shape, generator=g) * 0.05).to(gpu_device)
+            pa.grad.copy_(ng)
+            pb.grad.copy_(ng)
+    # state layout interchangeable with torch's
+    sa, sb = oa.state_dict(), ob.state_dict()
+    assert set(sa["state"][0]) == set(sb["state"][0])
+    oc = torch.optim.AdamW(_params(gpu_device, 2), lr=1e-3)
+    oc.load_state_dict(sb)
+    assert float(oc.state_dict()["state"][0]["step"]) == 4.0
+
+
+def test_train_step_uses_fused_glue(gpu_device):
+    """sehip.train.make_optimizer returns the fused AdamW for CUDA fp32 models,
+    and a FRCRN train step through it equals the same step through torch's
+    clip + AdamW to within fp32 rounding."""
+    from sehip import models as M
+    from sehip import optim
+    from sehip.train import make_optimizer, train_step, ADAMW, CLIP_NORM
+    from sehip.losses import SI_SNR_loss, pad_or_truncate_wav, reshape_wav_to_mono
+    import paramfill
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=11)
+    x, c = torch.from_numpy(noisy).to(gpu_device), torch.from_numpy(clean).to(gpu_device)
+    m1 = paramfill.fill_(M.FRCRN(), seed=12).to(gpu_device).train()
+    m2 = paramfill.fill_(M.FRCRN(), seed=12).to(gpu_device).train()
+    o1 = make_optimizer(m1)
+    assert isinstance(o1, optim.AdamW)
+    l1 = train_step(m1, o1, x, c)
+    o2 = torch.optim.AdamW(m2.parameters(), **ADAMW)
+    _, wav = m2(x)
+    t = reshape_wav_to_mono(c)
+    l2 = SI_SNR_loss(pad_or_truncate_wav(reshape_wav_to_mono(wav), t).contiguous().clone(), t.clone())
+    l2.backward()
+    torch.nn.utils.clip_grad_norm_(m2.parameters(), CLIP_NORM)
+    o2.step()
+    assert abs(l1.item() - l2.item()) < 1e-5 * abs(l2.item()) + 1e-6
+    # A first AdamW step moves each parameter by ~lr * g / (|g| + eps): where
+    # |g| is near eps, fp32-rounding-level gradient differences (fp64 vs fp32
+    # norm in the clip) move the update by a fraction of lr. So: every
+    # element within one step size, and almost all within 1e-6.
+    d = torch.cat([(p1 - p2).abs().flatten() for p1, p2 in zip(m1.parameters(), m2.parameters())])
+    assert d.max().item() <= 2 * ADAMW["lr"]
+    assert (d > 1e-6).float().mean().item() < 1e-3
