@@ -113,33 +113,34 @@ def test_adamw_matches_torch_over_steps(gpu_device):
 
 
 def test_train_step_uses_fused_glue(gpu_device):
-    """sehip.train.make_optimizer returns the fused AdamW for CUDA fp32 models,
-    and a FRCRN train step through it equals the same step through torch's
-    clip + AdamW to within fp32 rounding."""
+    """make_optimizer returns the fused AdamW for CUDA fp32 models; over FRCRN's
+    279 parameter tensors (the slot table of a real step) the fused clip +
+    AdamW equals torch's on the same gradients; and train_step runs on it."""
     from sehip import models as M
     from sehip import optim
     from sehip.train import make_optimizer, train_step, ADAMW, CLIP_NORM
-    from sehip.losses import SI_SNR_loss, pad_or_truncate_wav, reshape_wav_to_mono
+    from sehip.losses import si_snr_loss_aligned
     import paramfill
     noisy, clean = paramfill.structured_pair(2, 16000, seed=11)
     x, c = torch.from_numpy(noisy).to(gpu_device), torch.from_numpy(clean).to(gpu_device)
-    m1 = paramfill.fill_(M.FRCRN(), seed=12).to(gpu_device).train()
+    m = paramfill.fill_(M.FRCRN(), seed=12).to(gpu_device).train()
+    assert isinstance(make_optimizer(m), optim.AdamW)
+    _, wav = m(x)
+    si_snr_loss_aligned(wav, c).backward()
+    pa = [torch.nn.Parameter(p.detach().clone()) for p in m.parameters()]
+    pb = [torch.nn.Parameter(p.detach().clone()) for p in m.parameters()]
+    for p, a, b in zip(m.parameters(), pa, pb):
+        a.grad, b.grad = p.grad.clone(), p.grad.clone()
+    na = torch.nn.utils.clip_grad_norm_(pa, CLIP_NORM)
+    nb = optim.clip_grad_norm_(pb, CLIP_NORM)
+    assert abs(na.item() - nb.item()) <= 1e-6 * na.item()
+    oa, ob = torch.optim.AdamW(pa, **ADAMW), optim.AdamW(pb, **ADAMW)
+    for _ in range(2):
+        oa.step()
+        ob.step()
+    for a, b in zip(pa, pb):
+        assert torch.allclose(a.grad, b.grad, rtol=1e-6, atol=0)
+        assert (a - b).abs().max().item() <= 1e-6 * max(a.abs().max().item(), 1e-2)
     m2 = paramfill.fill_(M.FRCRN(), seed=12).to(gpu_device).train()
-    o1 = make_optimizer(m1)
-    assert isinstance(o1, optim.AdamW)
-    l1 = train_step(m1, o1, x, c)
-    o2 = torch.optim.AdamW(m2.parameters(), **ADAMW)
-    _, wav = m2(x)
-    t = reshape_wav_to_mono(c)
-    l2 = SI_SNR_loss(pad_or_truncate_wav(reshape_wav_to_mono(wav), t).contiguous().clone(), t.clone())
-    l2.backward()
-    torch.nn.utils.clip_grad_norm_(m2.parameters(), CLIP_NORM)
-    o2.step()
-    assert abs(l1.item() - l2.item()) < 1e-5 * abs(l2.item()) + 1e-6
-    # A first AdamW step moves each parameter by ~lr * g / (|g| + eps): where
-    # |g| is near eps, fp32-rounding-level gradient differences (fp64 vs fp32
-    # norm in the clip) move the update by a fraction of lr. So: every
-    # element within one step size, and almost all within 1e-6.
-    d = torch.cat([(p1 - p2).abs().flatten() for p1, p2 in zip(m1.parameters(), m2.parameters())])
-    assert d.max().item() <= 2 * ADAMW["lr"]
-    assert (d > 1e-6).float().mean().item() < 1e-3
+    loss = train_step(m2, make_optimizer(m2), x, c)
+    assert torch.isfinite(loss)
