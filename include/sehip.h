@@ -315,6 +315,30 @@ int se_lstm_wide_bwd(const float* dy, const float* w_hh, const float* gates,
                      unsigned rev_mask, int* sync, int* status, void* stream);
 
 /* ------------------------------------------------------------------------
+ * Real BatchNorm2d + activation (CARN / GCARN ConvBlock: BatchNorm2d + PReLU,
+ * models/_2104_05267_carn.py:30-56; CRN ConvBlock: BatchNorm2d + ELU,
+ * models/_1809_01405_crn.py:9-45), fwd (training: batch statistics + running
+ * stat update with a float momentum; eval: running stats) and bwd.
+ * x     : B*C planes of HW contiguous floats, plane (b, c) at
+ *         x + (b*C + c)*x_plane_stride (a row-cropped view qualifies)
+ * y, gy, dx : contiguous [B][C][HW]
+ * weight, bias : [C] or NULL (affine=False); dweight / dbias likewise
+ * act   : 0 none, 1 PReLU (act_param [1] or [C] when act_per_channel),
+ *         2 ELU(elu_alpha); dact_param: the PReLU weight gradient
+ * save  : device fp32 [2C] = {mean, invstd} used, written by se_bn_fwd
+ * ws    : se_bn_workspace_size(B, C) bytes (training fwd and every bwd)
+ * ------------------------------------------------------------------------ */
+size_t se_bn_workspace_size(int B, int C);
+int se_bn_fwd(const float* x, long long x_plane_stride, int B, int C, int HW, const float* weight,
+              const float* bias, float* running_mean, float* running_var, int training, float momentum,
+              float eps, int act, const float* act_param, int act_per_channel, float elu_alpha, float* y,
+              float* save, void* ws, size_t ws_bytes, void* stream);
+int se_bn_bwd(const float* gy, const float* x, long long x_plane_stride, int B, int C, int HW,
+              const float* weight, const float* bias, const float* save, int training, int act,
+              const float* act_param, int act_per_channel, float elu_alpha, float* dx, float* dweight,
+              float* dbias, float* dact_param, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------
  * Train-step glue (trainer.py:99-124, :210-221)
  *
  * SI-SNR loss (losses.py:62-84) of B estimates against B targets [B, lt]

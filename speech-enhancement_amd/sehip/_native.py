@@ -77,6 +77,11 @@ _SIGNATURES = {
     "se_lstm_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P, _P] + [c_int] * 4
                     + [ctypes.c_uint, _P]),
     "se_lstm_bwd": (c_int, [_P] * 5 + [c_int] * 4 + [ctypes.c_uint, _P]),
+    "se_bn_workspace_size": (c_size_t, [c_int, c_int]),
+    "se_bn_fwd": (c_int, [_P, ctypes.c_longlong, c_int, c_int, c_int, _P, _P, _P, _P, c_int, c_float, c_float,
+                          c_int, _P, c_int, c_float, _P, _P, _P, c_size_t, _P]),
+    "se_bn_bwd": (c_int, [_P, _P, ctypes.c_longlong, c_int, c_int, c_int, _P, _P, _P, c_int, c_int, _P, c_int,
+                          c_float, _P, _P, _P, _P, _P, c_size_t, _P]),
     "se_sisnr_save_bytes": (c_size_t, [c_int]),
     "se_sisnr_fwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P]),
     "se_sisnr_bwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P,

@@ -3,8 +3,9 @@
 A real-valued conv U-Net over stacked re/im. The spectral front and back end
 (ConvSTFT / ConviSTFT) and every real conv / transposed conv (encoder, GLU
 gates, decoder, attention gates) run on the HIP kernels (the real-weight form
-of the conv GEMMs, complex_nn.real_conv2d); BatchNorm and PReLU are PyTorch device ops; the
-LSTM (H = 512) runs on the wide HIP recurrence (complex_nn.LSTM -> se_lstm_wide_*).
+of the conv GEMMs, complex_nn.real_conv2d); BatchNorm2d + PReLU run as one fused
+HIP pass each way (norm.bn_act -> se_bn_*); the LSTM (H = 512) runs on the wide
+HIP recurrence (complex_nn.LSTM -> se_lstm_wide_*).
 """
 from __future__ import annotations
 
@@ -14,6 +15,7 @@ import torch.nn.functional as TF
 
 from ..complex_nn import LSTM, real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
+from ..norm import bn_act
 
 
 def _conv(m: nn.Module, x):
@@ -56,7 +58,7 @@ class ConvBlock(nn.Module):
         self.act = nn.PReLU() if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(_conv(self.conv, x)))
+        return bn_act(self.norm, self.act, _conv(self.conv, x))
 
 
 class ConvTransposeBlock(nn.Module):
@@ -70,7 +72,7 @@ class ConvTransposeBlock(nn.Module):
         self.act = nn.PReLU() if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(_conv(self.conv_transposed, x)))
+        return bn_act(self.norm, self.act, _conv(self.conv_transposed, x))
 
 
 class Attention(nn.Module):

@@ -1,7 +1,8 @@
 """CRN (drop-in for models/_1809_01405_crn.py): magnitude-domain conv-LSTM
 that exercises the mag/phase API of ConvSTFT / ConviSTFT (HIP kernels); its
-real convs run on the real-weight form of the HIP conv GEMMs (real_conv2d), the
-BatchNorm / ELU / LSTM body on PyTorch device ops."""
+real convs run on the real-weight form of the HIP conv GEMMs (real_conv2d),
+BatchNorm2d + ELU as one fused HIP pass each way (norm.bn_act); the 1024-wide
+LSTM stays nn.LSTM (MIOpen): wider than the HIP recurrences (64-512)."""
 from __future__ import annotations
 
 import torch
@@ -10,6 +11,7 @@ import torch.nn.functional as TF
 
 from ..complex_nn import LSTM, real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
+from ..norm import bn_act
 
 
 class ConvBlock(nn.Module):
@@ -24,7 +26,7 @@ class ConvBlock(nn.Module):
         self.act = nn.ELU(alpha) if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(real_conv2d(self.conv, x)[:, :, :-self.padding[0], :]))
+        return bn_act(self.norm, self.act, real_conv2d(self.conv, x)[:, :, :-self.padding[0], :])
 
 
 class ConvTransposeBlock(nn.Module):
@@ -39,7 +41,7 @@ class ConvTransposeBlock(nn.Module):
         self.act = nn.ELU(alpha) if act else nn.Identity()
 
     def forward(self, x):
-        return self.act(self.norm(real_conv2d(self.conv_transposed, x)[:, :, :-1, :]))
+        return bn_act(self.norm, self.act, real_conv2d(self.conv_transposed, x)[:, :, :-1, :])
 
 
 class Encoder(nn.Module):
