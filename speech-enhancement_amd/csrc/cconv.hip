@@ -58,6 +58,9 @@ constexpr size_t kAmaxBytes = 256;   // SE_MATH_F16X3 max |.| slots, zeroed with
 // non-MFMA instructions are interleaved into the MFMA gaps by
 // sched_group_barrier groups (gather fwd/dgrad +6-9 %, weight-grad +6 % over the
 // fenced schedule; build with -DSEHIP_IGLP=0 for the fenced variant).
+#ifndef SEHIP_GEMM_PROBE   // 1 / 2: measurement probes of gather_x3_kernel<..., BMX = 2> (variant builds only)
+#define SEHIP_GEMM_PROBE 0
+#endif
 #ifndef SEHIP_IGLP
 #define SEHIP_IGLP 1
 #endif
@@ -1147,6 +1150,17 @@ static bool env_flag_off(const char* name) {
   return e && e[0] == '0';
 }
 
+// Rows per split-fp16 workgroup tile with 256 columns: 128 (default) or 256
+// (SEHIP_GEMM_BM=256: gather_x3_kernel<..., BMX = 2>, bit-identical; measured
+// no faster at dec5; read once).
+static int gemm_bm() {
+  static const int bm = [] {
+    const char* e = std::getenv("SEHIP_GEMM_BM");
+    return (e && std::atoi(e) == 256) ? 256 : 128;
+  }();
+  return bm;
+}
+
 static int gemm_nw() {
   static const int nw = [] {
     const char* e = std::getenv("SEHIP_GEMM_NW");
@@ -1318,7 +1332,12 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, T, 0, NWV, F>), grid, blk, 0, st, a);         \
     else hipLaunchKernelGGL((gather_x3_kernel<false, T, 0, NWV, F>), grid, blk, 0, st, a);                \
   } while (0)
-        if (f16 && wide) SE_X3_LAUNCH(3, 2, true);
+        if (f16 && wide && gemm_bm() == 256 && tu) {   // 256 x 256 tiles (BMX = 2)
+          const dim3 g2(se::ceil_div(M, 2 * kX3BM), grid.y);
+          if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1, 2, true, 2>), g2, blk, 0, st, a);
+          else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2, 2, true, 2>), g2, blk, 0, st, a);
+          else hipLaunchKernelGGL((gather_x3_kernel<true, 3, 0, 2, true, 2>), g2, blk, 0, st, a);
+        } else if (f16 && wide) SE_X3_LAUNCH(3, 2, true);
         else if (f16) SE_X3_LAUNCH(3, 1, true);
         else if (terms == 1 && wide) SE_X3_LAUNCH(1, 2, false);
         else if (terms == 1) SE_X3_LAUNCH(1, 1, false);

@@ -210,17 +210,20 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // and split once per 256 output columns instead of once per 128.
 // F16: scaled split-fp16 operands (SE_MATH_F16X3; a.amax_a / a.amax_w give the
 // per-tensor scales of the gathered tensor and the weights).
-template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false>
+// BMX = 2 (with NW = 2): a 256 (n) x 256 (m) tile of 8 waves of 64 (n) x 128 (m),
+// twice the MFMA work per barrier and half the LDS fragment bytes per MFMA.
+template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int BMX = 1>
 __global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
   static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
   static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
   static_assert(NW == 1 || NW == 2, "128 or 256 columns per workgroup");
+  static_assert(BMX == 1 || (BMX == 2 && NW == 2), "256-row tiles need the 8-wave workgroup");
   constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
   constexpr int THR = kThreads * NW;
-  constexpr int BN = kX3BN * NW, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
-  constexpr int AJ = 16 / NW;                     // gathered k per thread per step
+  constexpr int BN = kX3BN * NW, BM = kX3BM * BMX, WM = 2, TN = 64, TM = 64 * BMX, RN = 2, RM = 2 * BMX;
+  constexpr int AJ = 16 * BMX / NW;               // gathered k per thread per step
   constexpr int CPT = AJ / 8;                     // 16-B chunks per plane per thread
   __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * BM * 4];
   __shared__ __attribute__((aligned(16))) u32x4 sW[2][2 * BN * 4];   // [t][plane][128 rows][4]
@@ -351,39 +354,45 @@ gather_x3_kernel(const GatherArgs a) {
 
   const int lh = lane >> 5, lr = lane & 31;
   const int fsw = (lr >> 2) & 3;
+  // BMX = 1: both k-substeps' fragments are read up front; BMX = 2 (twice the
+  // accumulators) reads them per k-substep to stay inside 256 registers
+  constexpr int FS = BMX == 1 ? 2 : 1;           // k-substeps of fragments held at once
   auto compute = [&](int cur) __attribute__((always_inline)) {
-    u32x4 wf[2][RN][PL], af[2][RM][PL];   // [ks][block][plane]
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = (2 * ks + lh) ^ fsw;
+    for (int k0 = 0; k0 < 2; k0 += FS) {
+      u32x4 wf[FS][RN][PL], af[FS][RM][PL];     // [ks][block][plane]
 #pragma unroll
-      for (int i = 0; i < RN; ++i) {
-        const int n = wn * TN + 32 * i;           // block's first column (uniform)
+      for (int kk = 0; kk < FS; ++kk) {
+        const int c = (2 * (k0 + kk) + lh) ^ fsw;
 #pragma unroll
-        for (int p = 0; p < PL; ++p)
-          wf[ks][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+        for (int i = 0; i < RN; ++i) {
+          const int n = wn * TN + 32 * i;         // block's first column (uniform)
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            wf[kk][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+        }
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            af[kk][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
       }
 #pragma unroll
-      for (int j = 0; j < RM; ++j)
+      for (int kk = 0; kk < FS; ++kk)
 #pragma unroll
-        for (int p = 0; p < PL; ++p)
-          af[ks][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
+        for (int t = 0; t < TERMS; ++t)  // terms: hi*hi, hi*lo, lo*hi
+#pragma unroll
+          for (int i = 0; i < RN; ++i)
+#pragma unroll
+            for (int j = 0; j < RM; ++j)
+              acc[i][j] = mfma_32x32x16<F16>(wf[kk][i][t == 2 ? 1 : 0], af[kk][j][t == 1 ? 1 : 0], acc[i][j]);
     }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int t = 0; t < TERMS; ++t)  // terms: hi*hi, hi*lo, lo*hi
-#pragma unroll
-        for (int i = 0; i < RN; ++i)
-#pragma unroll
-          for (int j = 0; j < RM; ++j)
-            acc[i][j] = mfma_32x32x16<F16>(wf[ks][i][t == 2 ? 1 : 0], af[ks][j][t == 1 ? 1 : 0], acc[i][j]);
   };
   auto interleave = [&]() __attribute__((always_inline)) {
 #if SEHIP_IGLP
     __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);                  // first k-substep fragments
 #pragma unroll
-    for (int i = 0; i < 24; ++i) {
+    for (int i = 0; i < 2 * TERMS * RN * RM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
       if (i < AJ + 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
@@ -393,24 +402,47 @@ gather_x3_kernel(const GatherArgs a) {
   };
 
   const int nk = a.Kp / kBK;
-  load_tile(s0, 0);
-  store_tile(s0, 0);
-  if (nk > 1) load_tile(s1, kBK);
-  __syncthreads();
-  int kt = 0;
-  for (; kt + 1 < nk; kt += 2) {
-    load_tile(s0, min(kt + 2, nk - 1) * kBK);
-    compute(0);
-    store_tile(s1, 1);
-    interleave();
-    __syncthreads();
-    load_tile(s1, min(kt + 3, nk - 1) * kBK);
-    compute(1);
+  if constexpr (BMX == 2) {
+    // one register staging set (prefetch distance 1): a K-step is 96 MFMAs per
+    // SIMD here, long enough to cover the next tile's loads
+    load_tile(s0, 0);
     store_tile(s0, 0);
-    interleave();
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+#if SEHIP_GEMM_PROBE == 1   // measurement probe: MFMA + fragment reads + barrier only
+      const bool more = false;
+#elif SEHIP_GEMM_PROBE == 2 // probe: no global loads (the LDS stores stay)
+      const bool more = kt + 1 < nk;
+      if (false) load_tile(s0, (kt + 1) * kBK);
+#else
+      const bool more = kt + 1 < nk;
+      if (more) load_tile(s0, (kt + 1) * kBK);
+#endif
+      compute(kt & 1);
+      if (more) store_tile(s0, (kt + 1) & 1);
+      interleave();
+      __syncthreads();
+    }
+  } else {
+    load_tile(s0, 0);
+    store_tile(s0, 0);
+    if (nk > 1) load_tile(s1, kBK);
+    __syncthreads();
+    int kt = 0;
+    for (; kt + 1 < nk; kt += 2) {
+      load_tile(s0, min(kt + 2, nk - 1) * kBK);
+      compute(0);
+      store_tile(s1, 1);
+      interleave();
+      __syncthreads();
+      load_tile(s1, min(kt + 3, nk - 1) * kBK);
+      compute(1);
+      store_tile(s0, 0);
+      interleave();
+      __syncthreads();
+    }
+    if (kt < nk) compute(0);
   }
-  if (kt < nk) compute(0);
   if constexpr (F16) {   // undo the operand scales (exact)
 #pragma unroll
     for (int i = 0; i < RN; ++i)
