@@ -1108,11 +1108,22 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
   w.Np = round_up(w.N, w.N <= 32 ? 32 : 128);
   const int tiles = (w.c.Kp / 128) * (w.Np / (w.N <= 32 ? 32 : 128));
   int splits = std::max(1, 1024 / std::max(tiles, 1));
+  // At most kWgradMps positions per m-split (SEHIP_WGRAD_MPS overrides; 0 = no
+  // limit): the (k, n) tiles of one split run on one XCD and re-read G and D
+  // through its L2; short splits keep them close enough together for those
+  // re-reads to hit (dec5 weight-grad FETCH 40-48 -> 29-32 GB, 14.3 -> 12.4 ms;
+  // FRCRN step 574 -> 588 utt/s, same box).
+  static const int mps = [] {
+    const char* e = std::getenv("SEHIP_WGRAD_MPS");
+    return e ? std::max(0, std::atoi(e)) : 4096;
+  }();
+  if (mps > 0) splits = std::max(splits, (w.M + mps - 1) / mps);
   const int max_by_m = std::max(1, w.M / 512);
   splits = std::min(splits, max_by_m);
-  // keep the slab <= 256 MB
+  // keep the slab <= 256 MB (1 GB with SEHIP_WGRAD_MPS)
   const size_t per = (size_t)w.c.Kp * w.Np * sizeof(float);
-  splits = (int)std::min<size_t>(splits, std::max<size_t>(1, (256u << 20) / per));
+  const size_t cap = mps > 0 ? (1024ull << 20) : (256ull << 20);
+  splits = (int)std::min<size_t>(splits, std::max<size_t>(1, cap / per));
   w.m_per_split = round_up((w.M + splits - 1) / splits, 64);
   w.splits = (w.M + w.m_per_split - 1) / w.m_per_split;
   return w;
