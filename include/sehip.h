@@ -45,6 +45,12 @@ const char* se_strerror(int code);
 /* Loader self-test: out[i] = 3*i + 1 for i < n (one tiny kernel). */
 int se_probe(int* out, int n, void* stream);
 
+/* A HIP stream on a subset of the CUs (CU i enabled when i % den < num), and
+ * its release. The deferred weight-grad side stream of the Python host uses one
+ * (SEHIP_WGRAD_CUS=num/den). */
+int se_stream_create_cu_subset(int num, int den, void** stream);
+int se_stream_destroy(void* stream);
+
 /* ------------------------------------------------------------------------
  * ConvSTFT / ConviSTFT (models/conv_stft.py:7-116)
  *

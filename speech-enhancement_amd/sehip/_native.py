@@ -46,6 +46,8 @@ _SIGNATURES = {
     "se_abi_version": (c_int, []),
     "se_strerror": (c_char_p, [c_int]),
     "se_probe": (c_int, [_P, c_int, _P]),
+    "se_stream_create_cu_subset": (c_int, [c_int, c_int, _PP]),
+    "se_stream_destroy": (c_int, [_P]),
     "se_stft_num_frames": (c_int, [c_int] * 5),
     "se_stft_fwd": (c_int, [_P, _P, _P] + [c_int] * 7 + [_P, _P, _P]),
     "se_istft_fwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),

@@ -58,6 +58,20 @@ def deferred_weight_grads(enabled: bool = True):
             torch.cuda.current_stream(side.device).wait_stream(side)
 
 
+def _new_side_stream(dev):
+    """The deferred weight-grad stream: a plain torch stream, or with
+    SEHIP_WGRAD_CUS=num/den a HIP stream on that fraction of the CUs
+    (se_stream_create_cu_subset), wrapped as a torch ExternalStream."""
+    spec = os.environ.get("SEHIP_WGRAD_CUS")
+    if not spec:
+        return torch.cuda.Stream(dev)
+    num, den = (int(v) for v in spec.split("/"))
+    h = N.c_void_p()
+    with torch.cuda.device(dev):
+        N.check(N.lib().se_stream_create_cu_subset(num, den, N.ctypes.byref(h)), "se_stream_create_cu_subset")
+    return torch.cuda.ExternalStream(h.value, device=dev)
+
+
 def _wgrad_stream(*inputs):
     """Context for a weight-grad launch: a no-op, or (deferred_weight_grads) the
     device's side stream, after it waited for the current stream; the inputs are
@@ -67,7 +81,7 @@ def _wgrad_stream(*inputs):
     dev = inputs[0].device
     side = _DEFER_STREAMS.get(dev)
     if side is None:
-        side = _DEFER_STREAMS[dev] = torch.cuda.Stream(dev)
+        side = _DEFER_STREAMS[dev] = _new_side_stream(dev)
         SIDE_STREAMS.append(side)
     side.wait_stream(torch.cuda.current_stream(dev))
     for t in inputs:
