@@ -18,49 +18,51 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunk = 8192;     // elements per workgroup iteration of the slot kernels
 
-template <typename T>
+template <typename T, int NT = kThreads>
 __device__ __forceinline__ T block_sum(T v, T* red) {
   v = se::wave_sum(v);
   if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
   __syncthreads();
   T s = 0;
 #pragma unroll
-  for (int w = 0; w < kThreads / 64; ++w) s += red[w];
+  for (int w = 0; w < NT / 64; ++w) s += red[w];
   __syncthreads();
   return s;
 }
+
+constexpr int kItemThreads = 1024;   // one workgroup per utterance: the whole CU
 
 // per-utterance save: [0] mean e, [1] mean t, [2] dot (fp32), [3] |t|^2 (fp32),
 // [4] S, [5] N, [6] sum p, [7] sum (e' - p)  (doubles)
 constexpr int kSave = 8;
 
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kItemThreads)
 sisnr_items_kernel(const float* __restrict__ est, int le, long long est_stride, const float* __restrict__ tgt, int lt,
                    int zero_mean, double* __restrict__ save) {
   const int b = blockIdx.x;
   const float* e = est + (long long)b * est_stride;
   const float* t = tgt + (long long)b * lt;
   const int ne = min(le, lt);                 // estimate samples inside the target length
-  __shared__ double red[kThreads / 64];
+  __shared__ double red[kItemThreads / 64];
   float me = 0.f, mt = 0.f;
   if (zero_mean) {
     double se_ = 0, st = 0;
-    for (int i = threadIdx.x; i < lt; i += kThreads) {
+    for (int i = threadIdx.x; i < lt; i += kItemThreads) {
       se_ += i < ne ? e[i] : 0.f;
       st += t[i];
     }
-    me = (float)(block_sum(se_, red) / lt);
-    mt = (float)(block_sum(st, red) / lt);
+    me = (float)(block_sum<double, kItemThreads>(se_, red) / lt);
+    mt = (float)(block_sum<double, kItemThreads>(st, red) / lt);
   }
   double dot = 0, tt = 0;
-  for (int i = threadIdx.x; i < lt; i += kThreads) {
+  for (int i = threadIdx.x; i < lt; i += kItemThreads) {
     const float ei = (i < ne ? e[i] : 0.f) - me, ti = t[i] - mt;
     dot += (double)ei * ti;
     tt += (double)ti * ti;
   }
-  const float dotf = (float)block_sum(dot, red), ttf = (float)block_sum(tt, red);
+  const float dotf = (float)block_sum<double, kItemThreads>(dot, red), ttf = (float)block_sum<double, kItemThreads>(tt, red);
   double S = 0, Nn = 0, sp = 0, sr = 0;
-  for (int i = threadIdx.x; i < lt; i += kThreads) {
+  for (int i = threadIdx.x; i < lt; i += kItemThreads) {
     const float ei = (i < ne ? e[i] : 0.f) - me, ti = t[i] - mt;
     const float p = dotf * ti / ttf;          // proj = sum(e*t) * t / t_energy
     const float r = ei - p;
@@ -69,10 +71,10 @@ sisnr_items_kernel(const float* __restrict__ est, int le, long long est_stride, 
     sp += p;
     sr += r;
   }
-  S = block_sum(S, red);
-  Nn = block_sum(Nn, red);
-  sp = block_sum(sp, red);
-  sr = block_sum(sr, red);
+  S = block_sum<double, kItemThreads>(S, red);
+  Nn = block_sum<double, kItemThreads>(Nn, red);
+  sp = block_sum<double, kItemThreads>(sp, red);
+  sr = block_sum<double, kItemThreads>(sr, red);
   if (threadIdx.x == 0) {
     double* s = save + (long long)b * kSave;
     s[0] = me; s[1] = mt; s[2] = dotf; s[3] = ttf; s[4] = S; s[5] = Nn; s[6] = sp; s[7] = sr;
@@ -227,7 +229,7 @@ extern "C" int se_sisnr_fwd(const float* est, int le, long long est_stride, cons
                             int zero_mean, float eps, float* loss, void* save, void* stream) {
   if (!est || !target || !loss || !save || B <= 0 || le <= 0 || lt <= 0 || est_stride < le) return SE_E_ARG;
   hipStream_t st = se::as_stream(stream);
-  hipLaunchKernelGGL(sisnr_items_kernel, dim3(B), dim3(kThreads), 0, st, est, le, est_stride, target, lt, zero_mean,
+  hipLaunchKernelGGL(sisnr_items_kernel, dim3(B), dim3(kItemThreads), 0, st, est, le, est_stride, target, lt, zero_mean,
                      (double*)save);
   SE_LAUNCH_CHECK();
   hipLaunchKernelGGL(sisnr_finalize_kernel, dim3(1), dim3(kThreads), 0, st, (const double*)save, B, eps, loss);
