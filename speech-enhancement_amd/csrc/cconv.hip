@@ -436,6 +436,8 @@ struct WgradArgs {
   // elements per plane; m_per_split counts output rows; per-tap input offsets
   long long pk_plane_g, pk_plane_d, pk_plane_d2;
   int toffh[kMaxTaps], toffw[kMaxTaps];
+  // wgrad_x3_kernel: tile space (k-tiles, n-tiles, m-splits) walked by its 1-D grid
+  int vk, vn, vs;
 };
 
 // Small-N weight grad (N <= 8: FRCRN's final_conv 128->2 and the CCBAM spatial
@@ -1439,6 +1441,18 @@ extern "C" int se_conv2d_bwd_data(const se_conv2d_desc* d, const float* dy, cons
 
 namespace {
 
+// 1-D grid of wgrad_x3_kernel over its tile space; SEHIP_WGRAD_WG caps the
+// workgroup count (a persistent grid that leaves CUs to the main stream).
+dim3 x3_wgrad_grid(WgradArgs& a, const WgradPlan& w) {
+  static const int cap = [] {
+    const char* e = std::getenv("SEHIP_WGRAD_WG");
+    return e ? std::max(0, std::atoi(e)) : 0;
+  }();
+  a.vk = w.c.Kp / 128; a.vn = w.Np / 128; a.vs = w.splits;
+  const int tiles = a.vk * a.vn * a.vs;
+  return dim3((unsigned)(cap > 0 ? std::min(tiles, ((cap + 7) / 8) * 8) : tiles));
+}
+
 // Weight-grad pass. jn (transposed convs only): the conv's input x is the
 // decoder skip join, D = s with D2 = jn->x2 on (h2, w2) (se_conv2d_bwd_weight_joined).
 int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, float* dwi,
@@ -1543,17 +1557,17 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
   } else if (f16) {
-    dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
+    const dim3 grid = x3_wgrad_grid(a, w);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true>), grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.math == SE_MATH_BF16X3) {
-    dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
+    const dim3 grid = x3_wgrad_grid(a, w);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
   } else if (split_ok) {   // SE_MATH_BF16
-    dim3 grid(w.c.Kp / 128, w.Np / 128, w.splits);
+    const dim3 grid = x3_wgrad_grid(a, w);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1>), grid, dim3(kThreads), 0, st, a);

@@ -541,10 +541,13 @@ wgrad_x3_kernel(const WgradArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wk = wave / WNn, wnn = wave % WNn;
-  const int nkn = gridDim.x * gridDim.y;
-  const int tile = xcd_remap((blockIdx.z * gridDim.y + blockIdx.y) * gridDim.x + blockIdx.x, nkn * gridDim.z);
+  // tile space (a.vk k-tiles x a.vn n-tiles x a.vs m-splits), walked by a 1-D
+  // grid of at most that many workgroups (a persistent grid when capped)
+  const int nkn = a.vk * a.vn, ntiles = nkn * a.vs;
+  for (int L = blockIdx.x; L < ntiles; L += gridDim.x) {
+  const int tile = xcd_remap(L, ntiles);
   const int split = tile / nkn, kn = tile % nkn;
-  const int k0 = (kn % gridDim.x) * BKO, n0 = (kn / gridDim.x) * BNO;
+  const int k0 = (kn % a.vk) * BKO, n0 = (kn / a.vk) * BNO;
   const int mbeg = split * a.m_per_split;
   const int mend = min(a.M, mbeg + a.m_per_split);
   const long long HiWi = (long long)a.Hi * a.Wi;
@@ -777,6 +780,8 @@ wgrad_x3_kernel(const WgradArgs a) {
         const int n = n0 + wnn * TN + 32 * j + lc;
         out[(long long)k * a.Np + n] = F16 ? __builtin_ldexpf(acc[i][j][r], ush) : acc[i][j][r];
       }
+  __syncthreads();   // the next tile restages sK and sm
+  }
 }
 
 // ---------------------------------------------------------------------------
