@@ -1308,7 +1308,12 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
           a.pk_plane2 = (long long)g.B * a.Cpk2 * jn->h2 * jn->w2;
         }
         const dim3 blk(kPkThreads);
-        if (ldw % 256 == 0) {           // 128 x 256 tiles
+        if (ldw % 256 == 0 && gemm_bm() == 256) {   // 256 x 256 tiles, two stages
+          const dim3 grid(se::ceil_div(M, 256), ldw / 256);
+          if (join_in) hipLaunchKernelGGL((gather_pk_kernel<1, 256, 256, 2>), grid, blk, 0, st, a);
+          else if (join_out) hipLaunchKernelGGL((gather_pk_kernel<2, 256, 256, 2>), grid, blk, 0, st, a);
+          else hipLaunchKernelGGL((gather_pk_kernel<0, 256, 256, 2>), grid, blk, 0, st, a);
+        } else if (ldw % 256 == 0) {    // 128 x 256 tiles
           const dim3 grid(se::ceil_div(M, 128), ldw / 256);
           if (join_in) hipLaunchKernelGGL((gather_pk_kernel<1, 128, 256>), grid, blk, 0, st, a);
           else if (join_out) hipLaunchKernelGGL((gather_pk_kernel<2, 128, 256>), grid, blk, 0, st, a);

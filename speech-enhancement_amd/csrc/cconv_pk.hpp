@@ -80,11 +80,15 @@ typedef __attribute__((address_space(3))) void lds_void;
 
 constexpr int kPkThreads = 512, kPkStages = 3;
 
-template <int JM, int BM, int BN>
+// (BM, BN) = (256, 256), S = 2: 8 waves of 128 (m) x 64 (n), two 64-KB stages,
+// the next stage issued before the current one is computed.
+template <int JM, int BM, int BN, int S = kPkStages>
 __global__ void __launch_bounds__(kPkThreads, 1)
 gather_pk_kernel(const GatherArgs a) {
-  static_assert((BM == 256 && BN == 128) || (BM == 128 && BN == 256), "8 waves of 64 x 64");
-  constexpr int WM = BM / 64, TN = 64, TM = 64, RN = 2, RM = 2, PL = 2;
+  static_assert((BM == 256 && BN == 128) || (BM == 128 && BN == 256) || (BM == 256 && BN == 256 && S == 2),
+                "8 waves of 64 x 64, or of 128 x 64 with two stages");
+  constexpr bool BIG = BM == 256 && BN == 256;
+  constexpr int WM = BIG ? 2 : BM / 64, TN = 64, TM = BM / WM, RN = 2, RM = TM / 32, PL = 2;
   constexpr int A_U4 = BM * 2 * 4, B_U4 = BN * 2 * 4;      // u32x4 per stage image
   constexpr int A_PCS = BM / 64, B_PCS = BN / 64;           // 1-KB LDS-DMA pieces per wave per stage
   constexpr int VM_NEXT = A_PCS + B_PCS;                    // loads of one stage per wave
@@ -93,7 +97,7 @@ gather_pk_kernel(const GatherArgs a) {
   // from scalar arithmetic and the per-tap offsets from the kernel arguments (a table
   // read from global memory or LDS there is waited for with vmcnt(0), which would drain
   // the stage in flight)
-  constexpr int RING = kPkStages * (A_U4 + B_U4);
+  constexpr int RING = S * (A_U4 + B_U4);
   __shared__ __attribute__((aligned(16))) u32x4 smem_all[RING];
   auto stage_base = [&](int buf) __attribute__((always_inline)) { return &smem_all[buf * (A_U4 + B_U4)]; };
 
@@ -198,52 +202,71 @@ gather_pk_kernel(const GatherArgs a) {
 
   const int lh = lane >> 5, lr = lane & 31;
   const int fsw = (lr >> 2) & 3;
+  constexpr int FS = BIG ? 1 : 2;                  // k-substeps of fragments held at once
   auto compute = [&](int cur) __attribute__((always_inline)) {
     const u32x4* sA = stage_base(cur);
     const u32x4* sW = stage_base(cur) + A_U4;
-    u32x4 wf[2][RN][PL], af[2][RM][PL];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
-      const int c = (2 * ks + lh) ^ fsw;
+    for (int k0 = 0; k0 < 2; k0 += FS) {
+      u32x4 wf[FS][RN][PL], af[FS][RM][PL];
 #pragma unroll
-      for (int i = 0; i < RN; ++i) {
-        const int n = wn * TN + 32 * i;           // block's first column (uniform)
+      for (int kk = 0; kk < FS; ++kk) {
+        const int c = (2 * (k0 + kk) + lh) ^ fsw;
 #pragma unroll
-        for (int p = 0; p < PL; ++p)
-          wf[ks][i][p] = sW[(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+        for (int i = 0; i < RN; ++i) {
+          const int n = wn * TN + 32 * i;         // block's first column (uniform)
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            wf[kk][i][p] = sW[(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+        }
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            af[kk][j][p] = sA[(p * BM + wm * TM + 32 * j + lr) * 4 + c];
       }
+      if constexpr (BIG) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-      for (int j = 0; j < RM; ++j)
+      for (int kk = 0; kk < FS; ++kk)
 #pragma unroll
-        for (int p = 0; p < PL; ++p)
-          af[ks][j][p] = sA[(p * BM + wm * TM + 32 * j + lr) * 4 + c];
+        for (int t = 0; t < 3; ++t)  // hi*hi, hi*lo, lo*hi
+#pragma unroll
+          for (int i = 0; i < RN; ++i)
+#pragma unroll
+            for (int j = 0; j < RM; ++j)
+              acc[i][j] = mfma_32x32x16<true>(wf[kk][i][t == 2 ? 1 : 0], af[kk][j][t == 1 ? 1 : 0], acc[i][j]);
+      if constexpr (BIG) __builtin_amdgcn_s_setprio(0);
     }
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-      for (int t = 0; t < 3; ++t)  // hi*hi, hi*lo, lo*hi
-#pragma unroll
-        for (int i = 0; i < RN; ++i)
-#pragma unroll
-          for (int j = 0; j < RM; ++j)
-            acc[i][j] = mfma_32x32x16<true>(wf[ks][i][t == 2 ? 1 : 0], af[ks][j][t == 1 ? 1 : 0], acc[i][j]);
   };
 
-  // prologue: stages 0 and 1 in flight, wait for stage 0
-  stage(0, 0);
-  if (nk > 1) stage(1, kBK);
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(VM_NEXT) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  for (int kt = 0; kt < nk; ++kt) {
-    const bool ahead = kt + 2 < nk;
-    if (ahead) stage((kt + 2) % kPkStages, (kt + 2) * kBK);
-    compute(kt % kPkStages);
-    // retire this wave's loads of stage kt + 1 (the stage kt + 2 ones may stay in flight),
-    // then the barrier hands stage kt + 1 to every wave and frees buffer kt for kt + 3
-    if (ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(VM_NEXT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  if constexpr (S == 2) {
+    // prologue: stage 0; each K-step issues the next stage, computes, then waits for it
+    stage(0, 0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * kBK);
+      compute(kt & 1);
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+  } else {
+    // prologue: stages 0 and 1 in flight, wait for stage 0
+    stage(0, 0);
+    if (nk > 1) stage(1, kBK);
+    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(VM_NEXT) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      const bool ahead = kt + 2 < nk;
+      if (ahead) stage((kt + 2) % S, (kt + 2) * kBK);
+      compute(kt % S);
+      // retire this wave's loads of stage kt + 1 (the stage kt + 2 ones may stay in flight),
+      // then the barrier hands stage kt + 1 to every wave and frees buffer kt for kt + 3
+      if (ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(VM_NEXT) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
   }
 #pragma unroll
   for (int i = 0; i < RN; ++i)
