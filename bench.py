@@ -280,11 +280,22 @@ def main():
 
     default_mode = SF.get_conv_math()
     elapsed, loss_v = timed(args.steps, args.warmup)            # the headline: no instrumentation
-    kern = {}
+    kern, kern_iso = {}, {}
     if not args.no_op_timing:
         timer = SF.OpTimer()
         timed(args.steps, 0, timer)
         kern = timer.summary()
+        # the same kernels with the side streams off (SEHIP_OVERLAP=0): each GEMM's own rate,
+        # without the deferred weight-grads / CCBAM gates taking CU slots beside it
+        prev = os.environ.get("SEHIP_OVERLAP")
+        os.environ["SEHIP_OVERLAP"] = "0"
+        timer = SF.OpTimer()
+        timed(args.steps, 1, timer)
+        kern_iso = timer.summary()
+        if prev is None:
+            del os.environ["SEHIP_OVERLAP"]
+        else:
+            os.environ["SEHIP_OVERLAP"] = prev
 
     # ConvSTFT / iSTFT are ~50 us kernels: per-call events inside the step also catch host
     # launch gaps, so their GB/s use 20 back-to-back calls between one event pair
@@ -351,7 +362,8 @@ def main():
                           "fp32 MFMA peak; 'bf16x3' = hi+lo bf16 (4.5e-6, not fp32-class); 'bf16x6' = "
                           "three-way bf16 split, six terms (5.5e-7); tests/test_gpu_conv_x3.py",
         "timing_note": "value: K steps with no instrumentation; roofline / op_breakdown: a second pass "
-                       "of K steps with HIP events around every C-ABI call",
+                       "of K steps with HIP events around every C-ABI call; roofline_isolated: a third "
+                       "pass with the side streams off",
     }
     if "f32" in compare:
         out["f32_exact"] = compare.pop("f32")
@@ -361,6 +373,17 @@ def main():
         out["roofline"] = _roofline(kern, args.steps)
         out["roofline_side_stream"] = _roofline({k: v for k, v in kern.items() if "wgrad" in k},
                                                 args.steps, side_ok=True)
+        if kern_iso:
+            tag = out["roofline"]["timer_tag"] if out["roofline"] else None
+            iso = _roofline({tag: kern_iso[tag]} if tag in kern_iso else kern_iso, args.steps)
+            if iso:
+                iso["note"] = ("the same kernel in a third pass of K steps with the side streams off "
+                               "(SEHIP_OVERLAP=0): its own rate; `roofline` above is its rate inside the "
+                               "overlapped step, where the deferred weight-grads share the CUs")
+            out["roofline_isolated"] = iso
+            wg = {k: v for k, v in kern_iso.items() if "wgrad" in k}
+            if wg:
+                out["roofline_side_stream_isolated"] = _roofline(wg, args.steps, side_ok=True)
         for name, kname in (("stft_fwd", "stft_fwd_ip_kernel"), ("istft_fwd", "istft_fwd_ip_kernel"),
                             ("istft_bwd", "istft_bwd_ip_kernel")):
             st = kern.get(name)
