@@ -77,8 +77,8 @@ FP32_CLASS = {"f32", "f16x3", "bf16x6"}   # per-conv error at or below the exact
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="utterances per GPU")
     ap.add_argument("--cpu-steps", type=int, default=5)
     ap.add_argument("--cpu-batch", type=int, default=8)
