@@ -58,6 +58,9 @@ constexpr size_t kAmaxBytes = 256;   // SE_MATH_F16X3 max |.| slots, zeroed with
 // non-MFMA instructions are interleaved into the MFMA gaps by
 // sched_group_barrier groups (gather fwd/dgrad +6-9 %, weight-grad +6 % over the
 // fenced schedule; build with -DSEHIP_IGLP=0 for the fenced variant).
+#ifndef SEHIP_WGRAD_OCC     // workgroups per CU the weight-grad GEMM is compiled for (variant builds: 1)
+#define SEHIP_WGRAD_OCC 2
+#endif
 #ifndef SEHIP_GEMM_PROBE   // 1 / 2: measurement probes of gather_x3_kernel<..., BMX = 2> (variant builds only)
 #define SEHIP_GEMM_PROBE 0
 #endif

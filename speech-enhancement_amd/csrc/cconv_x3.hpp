@@ -527,7 +527,7 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // DJ: D is the decoder skip join (WgradArgs::D2, a transposed conv's input).
 // F16: scaled split-fp16 operands (SE_MATH_F16X3; a.amax_g / a.amax_d).
 template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false>
-__global__ void __launch_bounds__(kThreads, 2)
+__global__ void __launch_bounds__(kThreads, SEHIP_WGRAD_OCC)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
