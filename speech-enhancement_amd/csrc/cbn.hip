@@ -75,8 +75,10 @@ __device__ __forceinline__ float act_grad(float y, int act, float slope) {
 // grid (Cc, P). Row r = (b, segment) of channel c; rows strided over P.
 // ext[(c * P + p) * 4 + {0..3}] = max x_r, -min x_r, max x_i, -min x_i
 __global__ void __launch_bounds__(kThreads)
-cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, double* part, float* ext) {
+cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, double* part, float* ext,
+                   float* y_amax) {
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
+  if (y_amax && c == 0 && p == 0 && threadIdx.x == 0) *y_amax = 0.f;   // the finalize blocks atomicMax into it
   const int nseg = (HW + kSeg - 1) / kSeg;
   double v[5] = {0, 0, 0, 0, 0};
   float e[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
@@ -101,22 +103,43 @@ cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, dou
   }
 }
 
-// One block; channel c per thread (strided).
-__global__ void cbn_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
-                                    Ptr5 params, int affine, MPtr5 running, int has_running,
-                                    int64_t* nbt, float* save, int training, float eps,
-                                    float momentum, float* y_amax) {
-  float ybound = 0.f;   // upper bound of max |y| over every channel (training)
+// One wave per channel (kFinWaves channels per block): the lanes add the P
+// partial rows in parallel; lane 0 does the channel's closed-form math. The
+// bound of max |y| goes to *y_amax by atomicMax (zeroed by the moments pass);
+// num_batches_tracked is incremented by the apply pass, after every block has
+// read it here.
+constexpr int kFinWaves = 4;
+__global__ void __launch_bounds__(64 * kFinWaves)
+cbn_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
+                    Ptr5 params, int affine, MPtr5 running, int has_running,
+                    const int64_t* nbt, float* save, int training, float eps,
+                    float momentum, float* y_amax) {
   float factor = 0.f;
   if (training && has_running) {
     factor = momentum >= 0.f ? momentum : (float)(1.0 / (double)(nbt ? (*nbt + 1) : 1));
   }
-  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  if (c >= Cc) return;
+  double s[5] = {0, 0, 0, 0, 0};
+  float xmax_r = -INFINITY, xmin_r = -INFINITY, xmax_i = -INFINITY, xmin_i = -INFINITY;
+  if (training) {
+    for (int p = lane; p < P; p += 64) {
+#pragma unroll
+      for (int k = 0; k < 5; ++k) s[k] += part[((long long)c * P + p) * 5 + k];
+      const float* q = ext + ((long long)c * P + p) * 4;
+      xmax_r = fmaxf(xmax_r, q[0]); xmin_r = fmaxf(xmin_r, q[1]);
+      xmax_i = fmaxf(xmax_i, q[2]); xmin_i = fmaxf(xmin_i, q[3]);
+    }
+#pragma unroll
+    for (int k = 0; k < 5; ++k) s[k] = se::wave_sum(s[k]);
+    xmax_r = se::wave_max(xmax_r); xmin_r = se::wave_max(xmin_r);
+    xmax_i = se::wave_max(xmax_i); xmin_i = se::wave_max(xmin_i);
+  }
+  if (lane != 0) return;
+  {
     double mr, mi, vrr, vri, vii;
     if (training) {
-      double s[5] = {0, 0, 0, 0, 0};
-      for (int p = 0; p < P; ++p)
-        for (int k = 0; k < 5; ++k) s[k] += part[((long long)c * P + p) * 5 + k];
       mr = s[0] / count; mi = s[1] / count;
       vrr = s[2] / count - mr * mr;
       vri = s[3] / count - mr * mi;
@@ -152,32 +175,23 @@ __global__ void cbn_finalize_kernel(const double* part, const float* ext, int P,
     o[S_BR] = (float)br; o[S_BI] = (float)bi; o[S_S] = (float)s; o[S_T] = (float)t;
     float dr = INFINITY, di = INFINITY;   // eval: the batch extrema are unknown
     if (training) {
-      float xmax_r = -INFINITY, xmin_r = -INFINITY, xmax_i = -INFINITY, xmin_i = -INFINITY;
-      for (int p = 0; p < P; ++p) {
-        const float* q = ext + ((long long)c * P + p) * 4;
-        xmax_r = fmaxf(xmax_r, q[0]); xmin_r = fmaxf(xmin_r, q[1]);
-        xmax_i = fmaxf(xmax_i, q[2]); xmin_i = fmaxf(xmin_i, q[3]);
-      }
       // max |x - M| (xmin_* hold -min); rounded up so the bound stays a bound
       dr = fmaxf(xmax_r - (float)mr, xmin_r + (float)mr) * 1.0001f;
       di = fmaxf(xmax_i - (float)mi, xmin_i + (float)mi) * 1.0001f;
       const float yr = fabsf((float)zrr) * dr + fabsf((float)zri) * di + fabsf((float)br);
       const float yi = fabsf((float)zir) * dr + fabsf((float)zii) * di + fabsf((float)bi);
-      ybound = fmaxf(ybound, fmaxf(yr, yi) * 1.0001f);
+      if (y_amax) atomicMax(reinterpret_cast<unsigned*>(y_amax), __float_as_uint(fmaxf(yr, yi) * 1.0001f));
     }
     o[S_DR] = dr; o[S_DI] = di; o[S_PAD0] = o[S_PAD1] = 0.f;
   }
-  ybound = block_max(ybound);
-  if (threadIdx.x == 0 && training && y_amax) *y_amax = ybound;
-  __syncthreads();
-  if (threadIdx.x == 0 && training && has_running && nbt) *nbt += 1;
 }
 
 // grid (ceil(HW / (kThreads*4)), Cc, B)
 __global__ void __launch_bounds__(kThreads)
 cbn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
-                 const float* __restrict__ save, int act, float slope) {
+                 const float* __restrict__ save, int act, float slope, int64_t* nbt) {
   const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  if (nbt && blockIdx.x == 0 && c == 0 && b == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked
   const float* s = save + c * kSave;
   const float mr = s[S_MR], mi = s[S_MI], zrr = s[S_ZRR], zri = s[S_ZRI];
   const float zir = s[S_ZIR], zii = s[S_ZII], br = s[S_BR], bi = s[S_BI];
@@ -205,8 +219,10 @@ template <bool G2>
 __global__ void __launch_bounds__(kThreads)
 cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
                        const float* __restrict__ x, int B, int C, int HW, int P,
-                       const float* __restrict__ save, int act, float slope, double* part, float* ext) {
+                       const float* __restrict__ save, int act, float slope, double* part, float* ext,
+                       float* dx_amax) {
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
+  if (dx_amax && c == 0 && p == 0 && threadIdx.x == 0) *dx_amax = 0.f;   // the finalize blocks atomicMax into it
   const int nseg = (HW + kSeg - 1) / kSeg;
   const float* sv = save + c * kSave;
   float gmr = 0.f, gmi = 0.f;   // max |g_r|, max |g_i| (the dx bound)
@@ -242,15 +258,30 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
 // coef layout per channel (16 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi Br Bi pad
 constexpr int kCoef = 16;
 
-__global__ void cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
-                                        const float* save, Ptr5 params, int affine,
-                                        MPtr5 dparams, int has_dparams, int training,
-                                        float* coef, float* dx_amax) {
-  float dbound = 0.f;   // upper bound of max |dx| over every channel (training)
-  for (int c = threadIdx.x; c < Cc; c += blockDim.x) {
-    double sm[6] = {0, 0, 0, 0, 0, 0};
-    for (int p = 0; p < P; ++p)
-      for (int k = 0; k < 6; ++k) sm[k] += part[((long long)c * P + p) * 6 + k];
+// One wave per channel, as cbn_finalize_kernel; the bound of max |dx| goes to
+// *dx_amax by atomicMax (zeroed by the backward moments pass).
+__global__ void __launch_bounds__(64 * kFinWaves)
+cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
+                        const float* save, Ptr5 params, int affine,
+                        MPtr5 dparams, int has_dparams, int training,
+                        float* coef, float* dx_amax) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  if (c >= Cc) return;
+  double sm[6] = {0, 0, 0, 0, 0, 0};
+  float gmr = 0.f, gmi = 0.f;
+  for (int p = lane; p < P; p += 64) {
+#pragma unroll
+    for (int k = 0; k < 6; ++k) sm[k] += part[((long long)c * P + p) * 6 + k];
+    gmr = fmaxf(gmr, ext[((long long)c * P + p) * 2 + 0]);
+    gmi = fmaxf(gmi, ext[((long long)c * P + p) * 2 + 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < 6; ++k) sm[k] = se::wave_sum(sm[k]);
+  gmr = se::wave_max(gmr);
+  gmi = se::wave_max(gmi);
+  if (lane != 0) return;
+  {
     const float* s = save + (long long)c * kSave;
     const double urr = s[S_URR], uri = s[S_URI], uii = s[S_UII];
     const double vrr = s[S_VRR], vri = s[S_VRI], vii = s[S_VII];
@@ -301,22 +332,15 @@ __global__ void cbn_bwd_finalize_kernel(const double* part, const float* ext, in
     o[6] = (float)grr; o[7] = (float)gri; o[8] = (float)gii;
     o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = s[S_BR]; o[12] = s[S_BI];
     o[13] = o[14] = o[15] = 0.f;
-    if (training) {   // dx = Z^T (g - gb) + Gamma (x - M), bounded term by term
-      float gr = 0.f, gi = 0.f;
-      for (int p = 0; p < P; ++p) {
-        gr = fmaxf(gr, ext[((long long)c * P + p) * 2 + 0]);
-        gi = fmaxf(gi, ext[((long long)c * P + p) * 2 + 1]);
-      }
-      gr += fabsf(o[4]);
-      gi += fabsf(o[5]);
+    if (training && dx_amax) {   // dx = Z^T (g - gb) + Gamma (x - M), bounded term by term
+      const float gr = gmr + fabsf(o[4]);
+      const float gi = gmi + fabsf(o[5]);
       const float dr = s[S_DR], di = s[S_DI];
       const float br = fabsf(o[0]) * gr + fabsf(o[1]) * gi + fabsf(o[6]) * dr + fabsf(o[7]) * di;
       const float bi = fabsf(o[2]) * gr + fabsf(o[3]) * gi + fabsf(o[7]) * dr + fabsf(o[8]) * di;
-      dbound = fmaxf(dbound, fmaxf(br, bi) * 1.0001f);
+      atomicMax(reinterpret_cast<unsigned*>(dx_amax), __float_as_uint(fmaxf(br, bi) * 1.0001f));
     }
   }
-  dbound = block_max(dbound);
-  if (threadIdx.x == 0 && training && dx_amax) *dx_amax = dbound;
 }
 
 template <bool G2>
@@ -384,14 +408,16 @@ extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (running) for (int k = 0; k < 5; ++k) rp.p[k] = running[k];
   if (training) {
-    hipLaunchKernelGGL(cbn_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part, ext);
+    hipLaunchKernelGGL(cbn_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part, ext,
+                       y_amax);
     SE_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(cbn_finalize_kernel, dim3(1), dim3(256), 0, st, part, ext, P, (double)B * HW, Cc,
-                     pp, params ? 1 : 0, rp, running ? 1 : 0, nbt, save, training, eps, momentum, y_amax);
+  hipLaunchKernelGGL(cbn_finalize_kernel, dim3(se::ceil_div(Cc, kFinWaves)), dim3(64 * kFinWaves), 0, st, part,
+                     ext, P, (double)B * HW, Cc, pp, params ? 1 : 0, rp, running ? 1 : 0, (const int64_t*)nbt, save,
+                     training, eps, momentum, training ? y_amax : nullptr);
   SE_LAUNCH_CHECK();
   hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), Cc, B), dim3(kThreads),
-                     0, st, x, y, C, HW, save, act, slope);
+                     0, st, x, y, C, HW, save, act, slope, (training && running) ? nbt : nullptr);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
@@ -416,13 +442,14 @@ int cbn_bwd_impl(const float* gy, const float* gy2, const float* x, float* dx, i
   if (dparams) for (int k = 0; k < 5; ++k) dp.p[k] = dparams[k];
   if (gy2)
     hipLaunchKernelGGL(cbn_bwd_moments_kernel<true>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2, x,
-                       B, C, HW, P, save, act, slope, part, ext);
+                       B, C, HW, P, save, act, slope, part, ext, training ? dx_amax : nullptr);
   else
     hipLaunchKernelGGL(cbn_bwd_moments_kernel<false>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2,
-                       x, B, C, HW, P, save, act, slope, part, ext);
+                       x, B, C, HW, P, save, act, slope, part, ext, training ? dx_amax : nullptr);
   SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cbn_bwd_finalize_kernel, dim3(1), dim3(256), 0, st, part, ext, P, (double)B * HW,
-                     Cc, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, dx_amax);
+  hipLaunchKernelGGL(cbn_bwd_finalize_kernel, dim3(se::ceil_div(Cc, kFinWaves)), dim3(64 * kFinWaves), 0, st,
+                     part, ext, P, (double)B * HW, Cc, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training,
+                     coef, training ? dx_amax : nullptr);
   SE_LAUNCH_CHECK();
   const dim3 grid(se::ceil_div(HW, kThreads * 4), Cc, B);
   if (gy2)

@@ -824,14 +824,33 @@ class _LstmLayer(torch.autograd.Function):
             xs = x.reshape(B * T, I) if shared else x.reshape(L, B * T, I)
             dw_ih = torch.matmul(dgt, xs)
         if ctx.needs_input_grad[2]:
-            # h_{t-1} in processing order (zero at the first step of each direction)
-            hp = torch.zeros_like(h)
-            for l in range(L):
-                if (ctx.rev_mask >> l) & 1:
-                    hp[l, :, :-1] = h[l, :, 1:]
+            # dW_hh[l] = sum_t dgates_t^T h_{t-1} (processing order; h_{-1} = 0), without
+            # materialising the shifted h: on the flattened (b, t) rows the pairs are
+            # (row r, row r - 1) forward / (r, r + 1) reverse, minus the B - 1 pairs that
+            # straddle two sequences
+            hf = h.reshape(L, B * T, H)
+            dw_hh = torch.zeros((L, G, H), device=h.device, dtype=h.dtype)
+            for rev in ((0, 1) if T > 1 else ()):   # T = 1: every h_{t-1} is h_{-1} = 0
+                ls = [l for l in range(L) if ((ctx.rev_mask >> l) & 1) == rev]
+                if not ls:
+                    continue
+                idx = torch.tensor(ls, device=h.device) if len(ls) < L else None
+                dgl = dg if idx is None else dg.index_select(0, idx)
+                hl = hf if idx is None else hf.index_select(0, idx)
+                if rev == 0:
+                    w = torch.bmm(dgl[:, 1:].transpose(1, 2), hl[:, :-1])
+                    if B > 1:   # rows b*T (t = 0) paired with the previous sequence's last h
+                        r = torch.arange(1, B, device=h.device) * T
+                        w -= torch.bmm(dgl[:, r].transpose(1, 2), hl[:, r - 1])
                 else:
-                    hp[l, :, 1:] = h[l, :, :-1]
-            dw_hh = torch.bmm(dgt, hp.reshape(L, B * T, H))
+                    w = torch.bmm(dgl[:, :-1].transpose(1, 2), hl[:, 1:])
+                    if B > 1:   # rows b*T + T-1 (t = T-1) paired with the next sequence's first h
+                        r = torch.arange(1, B, device=h.device) * T
+                        w -= torch.bmm(dgl[:, r - 1].transpose(1, 2), hl[:, r])
+                if idx is None:
+                    dw_hh = w
+                else:
+                    dw_hh.index_copy_(0, idx, w)
         if ctx.has_b[0] and ctx.needs_input_grad[3] or ctx.has_b[1] and ctx.needs_input_grad[4]:
             db = dg.sum(1)
             db_ih = db if ctx.has_b[0] else None
