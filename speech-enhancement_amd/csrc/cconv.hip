@@ -115,6 +115,7 @@ struct GatherArgs {
   // scalars from the kernel arguments
   int ntaps, kblk;
   int toffh[kMaxTaps], toffw[kMaxTaps];
+  int pp_pair;         // ping-pong gather: 0 = waves 4-7 late, 1 = odd waves late
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -1177,6 +1178,16 @@ static int gemm_bm() {
   return bm;
 }
 
+// SEHIP_GEMM_PP=1: the ping-pong schedule of gather_x3_kernel (read once)
+static int gemm_pp_mode() {   // 0 off, 1 waves 4-7 late, 2 odd waves late
+  static const int pp = [] {
+    const char* e = std::getenv("SEHIP_GEMM_PP");
+    return e ? std::atoi(e) : 0;
+  }();
+  return pp;
+}
+static bool gemm_pp() { return gemm_pp_mode() > 0; }
+
 static int gemm_nw() {
   static const int nw = [] {
     const char* e = std::getenv("SEHIP_GEMM_NW");
@@ -1358,6 +1369,11 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
           if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1, 2, true, 2>), g2, blk, 0, st, a);
           else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2, 2, true, 2>), g2, blk, 0, st, a);
           else hipLaunchKernelGGL((gather_x3_kernel<true, 3, 0, 2, true, 2>), g2, blk, 0, st, a);
+        } else if (f16 && wide && gemm_pp() && tu) {   // ping-pong schedule
+          a.pp_pair = gemm_pp_mode() == 2;
+          if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1, 2, true, 1, true>), grid, blk, 0, st, a);
+          else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2, 2, true, 1, true>), grid, blk, 0, st, a);
+          else hipLaunchKernelGGL((gather_x3_kernel<true, 3, 0, 2, true, 1, true>), grid, blk, 0, st, a);
         } else if (f16 && wide) SE_X3_LAUNCH(3, 2, true);
         else if (f16) SE_X3_LAUNCH(3, 1, true);
         else if (terms == 1 && wide) SE_X3_LAUNCH(1, 2, false);

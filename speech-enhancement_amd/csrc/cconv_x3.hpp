@@ -212,7 +212,12 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // per-tensor scales of the gathered tensor and the weights).
 // BMX = 2 (with NW = 2): a 256 (n) x 256 (m) tile of 8 waves of 64 (n) x 128 (m),
 // twice the MFMA work per barrier and half the LDS fragment bytes per MFMA.
-template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int BMX = 1>
+// PP (with NW = 2): ping-pong schedule. Waves 4-7 run one barrier behind waves
+// 0-3 (each SIMD holds one wave of each half), and every K-step is two barrier
+// intervals: a memory part (fragment reads of this step, LDS stores of the
+// next, global loads of the one after) and an MFMA part. In each interval one
+// wave per SIMD issues MFMAs while the other does its memory part.
+template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int BMX = 1, bool PP = false>
 __global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
@@ -225,8 +230,9 @@ gather_x3_kernel(const GatherArgs a) {
   constexpr int BN = kX3BN * NW, BM = kX3BM * BMX, WM = 2, TN = 64, TM = 64 * BMX, RN = 2, RM = 2 * BMX;
   constexpr int AJ = 16 * BMX / NW;               // gathered k per thread per step
   constexpr int CPT = AJ / 8;                     // 16-B chunks per plane per thread
-  __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * BM * 4];
-  __shared__ __attribute__((aligned(16))) u32x4 sW[2][2 * BN * 4];   // [t][plane][128 rows][4]
+  constexpr int NBUF = PP ? 3 : 2;                // LDS stages (ping-pong: a 3-stage ring)
+  __shared__ __attribute__((aligned(16))) u32x4 sA[NBUF][2 * BM * 4];
+  __shared__ __attribute__((aligned(16))) u32x4 sW[NBUF][2 * BN * 4];   // [t][plane][128 rows][4]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
@@ -402,7 +408,69 @@ gather_x3_kernel(const GatherArgs a) {
   };
 
   const int nk = a.Kp / kBK;
-  if constexpr (BMX == 2) {
+  if constexpr (PP) {
+    static_assert(NW == 2 && BMX == 1, "ping-pong needs the two halves of the 8-wave workgroup");
+    // Per K-step: memory part = this step's fragment reads; MFMA part = the 24 MFMAs
+    // with the staging of step + 2 (LDS stores of the tile loaded one step earlier,
+    // then the global loads of step + 3) interleaved into their gaps. A 3-stage LDS
+    // ring keeps the stores of step + 2 off the stage the other half is reading.
+    const bool late = a.pp_pair ? (wave & 1) : (wave >= 4);   // which half runs one barrier behind
+    u32x4 wf[2][RN][PL], af[2][RM][PL];
+    auto read_frags = [&](int cur) __attribute__((always_inline)) {
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        const int c = (2 * ks + lh) ^ fsw;
+#pragma unroll
+        for (int i = 0; i < RN; ++i) {
+          const int n = wn * TN + 32 * i;
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            wf[ks][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+        }
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            af[ks][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
+      }
+    };
+    load_tile(s0, 0);
+    store_tile(s0, 0);
+    if (nk > 1) { load_tile(s0, kBK); store_tile(s0, 1); }
+    if (nk > 2) load_tile(s0, 2 * kBK);
+    __syncthreads();
+    if (late) __builtin_amdgcn_s_barrier();
+    for (int kt = 0; kt < nk; ++kt) {
+      read_frags(kt % 3);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      if (kt + 2 < nk) {
+        store_tile(s0, (kt + 2) % 3);
+        if (kt + 3 < nk) load_tile(s0, (kt + 3) * kBK);
+      }
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int t = 0; t < TERMS; ++t)
+#pragma unroll
+          for (int i = 0; i < RN; ++i)
+#pragma unroll
+            for (int j = 0; j < RM; ++j)
+              acc[i][j] = mfma_32x32x16<F16>(wf[ks][i][t == 2 ? 1 : 0], af[ks][j][t == 1 ? 1 : 0], acc[i][j]);
+#if SEHIP_IGLP
+#pragma unroll
+      for (int i = 0; i < 2 * TERMS * RN * RM; ++i) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
+        if (i < 6) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);       // DS write
+        if (i < AJ + 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // global load
+        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                  // VALU
+      }
+#endif
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+    }
+    if (!late) __builtin_amdgcn_s_barrier();   // every wave has passed the same number of barriers
+  } else if constexpr (BMX == 2) {
     // one register staging set (prefetch distance 1): a K-step is 96 MFMAs per
     // SIMD here, long enough to cover the next tile's loads
     load_tile(s0, 0);
