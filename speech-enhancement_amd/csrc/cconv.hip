@@ -67,6 +67,9 @@ constexpr size_t kAmaxBytes = 256;   // SE_MATH_F16X3 max |.| slots, zeroed with
 #ifndef SEHIP_IGLP
 #define SEHIP_IGLP 1
 #endif
+#ifndef SEHIP_GEMM_M16      // 1: f16x3 gather GEMMs on v_mfma_f32_16x16x32_f16 (16x16 accumulator blocks)
+#define SEHIP_GEMM_M16 0
+#endif
 #ifndef SEHIP_IG_VMEM
 #define SEHIP_IG_VMEM 0x020   // group mask for the global loads (0x020 VMEM read, 0x010 any VMEM)
 #endif

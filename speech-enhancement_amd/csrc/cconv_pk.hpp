@@ -140,7 +140,7 @@ gather_pk_kernel(const GatherArgs a) {
     hb[j] = qh * a.sh;
     wb[j] = qw * a.sw;
     rbase[j] = b - b0;
-    csrc[j] = slot ^ ((r >> 2) & 3);
+    csrc[j] = slot ^ x3_swz(r);
   }
   const long long HW1 = (long long)a.Hi * a.Wi, HW2 = (long long)a.H2 * a.W2;
   const _Float16* X = reinterpret_cast<const _Float16*>(a.X);
@@ -201,7 +201,7 @@ gather_pk_kernel(const GatherArgs a) {
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int lh = lane >> 5, lr = lane & 31;
-  const int fsw = (lr >> 2) & 3;
+  const int fsw = x3_swz(lr);
   constexpr int FS = BIG ? 1 : 2;                  // k-substeps of fragments held at once
   auto compute = [&](int cur) __attribute__((always_inline)) {
     const u32x4* sA = stage_base(cur);

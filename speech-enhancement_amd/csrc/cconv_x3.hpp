@@ -111,10 +111,22 @@ __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, 
 }
 
 // LDS / pre-tiled weight image of one operand tile: [plane (hi, lo)][row][4
-// chunks of 8 bf16 = 16 B], chunk c of row `row` stored at c ^ ((row >> 2) & 3).
-// 64-B rows, XOR swizzle: ds_read_b128 fragment reads (lane -> row r, chunk
-// 2ks + h) are conflict-free in all four 16-lane groups.
-__device__ __forceinline__ int x3_chunk(int row, int c) { return c ^ ((row >> 2) & 3); }
+// chunks of 8 bf16 = 16 B], chunk c of row `row` stored at c ^ x3_swz(row).
+// 64-B rows, XOR swizzle: ds_read_b128 fragment reads are conflict-free in all
+// four 16-lane groups. x3_swz = (row >> 2) & 3 serves the 32x32x16 reads (lane
+// -> row r = l & 31, chunk 2ks + (l >> 5)); with SEHIP_GEMM_M16 the swizzle is
+// the 8-entry table f(g), g = (row >> 2) & 7, f = [0,0,3,3,1,2,2,1], which keeps
+// those reads conflict-free and also the 16x16x32 reads (lane -> row l & 15 of a
+// 16-row block, chunk l >> 4): in every lane group the 16 lanes hit the 16
+// distinct 16-B slots of a 256-B bank row.
+__device__ __forceinline__ int x3_swz(int row) {
+#if SEHIP_GEMM_M16
+  return (0x69F0 >> (((row >> 2) & 7) * 2)) & 3;
+#else
+  return (row >> 2) & 3;
+#endif
+}
+__device__ __forceinline__ int x3_chunk(int row, int c) { return c ^ x3_swz(row); }
 
 constexpr int kX3BN = 128, kX3BM = 128;
 
@@ -230,6 +242,7 @@ gather_x3_kernel(const GatherArgs a) {
   constexpr int BN = kX3BN * NW, BM = kX3BM * BMX, WM = 2, TN = 64, TM = 64 * BMX, RN = 2, RM = 2 * BMX;
   constexpr int AJ = 16 * BMX / NW;               // gathered k per thread per step
   constexpr int CPT = AJ / 8;                     // 16-B chunks per plane per thread
+  constexpr bool M16 = SEHIP_GEMM_M16 && F16 && TERMS == 3 && BMX == 1 && !PP;
   constexpr int NBUF = PP ? 3 : 2;                // LDS stages (ping-pong: a 3-stage ring)
   __shared__ __attribute__((aligned(16))) u32x4 sA[NBUF][2 * BM * 4];
   __shared__ __attribute__((aligned(16))) u32x4 sW[NBUF][2 * BN * 4];   // [t][plane][128 rows][4]
@@ -330,7 +343,7 @@ gather_x3_kernel(const GatherArgs a) {
       st.rw[j] = src[PL == 2 ? e : e + (e >> 9) * 512];
     }
   };
-  const int swz = (am >> 2) & 3;
+  const int swz = x3_swz(am);
   auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
 #pragma unroll
     for (int q = 0; q < CPT; ++q) {
@@ -350,20 +363,52 @@ gather_x3_kernel(const GatherArgs a) {
     for (int j = 0; j < 2 * PL; ++j) sW[buf][tid + THR * j] = st.rw[j];
   };
 
-  f32x16 acc[RN][RM];
+  // M16: 16x16 accumulator blocks (v_mfma_f32_16x16x32_f16, one 32-deep
+  // k-substep per K-step): QN x QM blocks of 4 floats instead of RN x RM of 16
+  constexpr int QN = M16 ? 2 * RN : RN, QM = M16 ? 2 * RM : RM, AR = M16 ? 4 : 16;
+  typedef float accv __attribute__((ext_vector_type(AR)));
+  accv acc[QN][QM];
 #pragma unroll
-  for (int i = 0; i < RN; ++i)
+  for (int i = 0; i < QN; ++i)
 #pragma unroll
-    for (int j = 0; j < RM; ++j)
+    for (int j = 0; j < QM; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < AR; ++r) acc[i][j][r] = 0.f;
 
   const int lh = lane >> 5, lr = lane & 31;
-  const int fsw = (lr >> 2) & 3;
+  const int fsw = x3_swz(lr);
   // BMX = 1: both k-substeps' fragments are read up front; BMX = 2 (twice the
   // accumulators) reads them per k-substep to stay inside 256 registers
   constexpr int FS = BMX == 1 ? 2 : 1;           // k-substeps of fragments held at once
   auto compute = [&](int cur) __attribute__((always_inline)) {
+    if constexpr (M16) {
+      // lane l: row l & 15 of a 16-row block, chunk l >> 4 (k 8(l >> 4) .. +8)
+      const int r16 = lane & 15, q4 = lane >> 4;
+      u32x4 wf[QN][PL], af[QM][PL];
+#pragma unroll
+      for (int i = 0; i < QN; ++i) {
+        const int n = wn * TN + 16 * i, row = (n & 127) + r16;
+        const int c = q4 ^ x3_swz(row);
+#pragma unroll
+        for (int p = 0; p < PL; ++p) wf[i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + row) * 4 + c];
+      }
+#pragma unroll
+      for (int j = 0; j < QM; ++j) {
+        const int row = wm * TM + 16 * j + r16;
+        const int c = q4 ^ x3_swz(row);
+#pragma unroll
+        for (int p = 0; p < PL; ++p) af[j][p] = sA[cur][(p * BM + row) * 4 + c];
+      }
+#pragma unroll
+      for (int t = 0; t < TERMS; ++t)
+#pragma unroll
+        for (int i = 0; i < QN; ++i)
+#pragma unroll
+          for (int j = 0; j < QM; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, wf[i][t == 2 ? 1 : 0]),
+                                                               __builtin_bit_cast(f16x8, af[j][t == 1 ? 1 : 0]),
+                                                               acc[i][j], 0, 0, 0);
+    } else {
 #pragma unroll
     for (int k0 = 0; k0 < 2; k0 += FS) {
       u32x4 wf[FS][RN][PL], af[FS][RM][PL];     // [ks][block][plane]
@@ -393,12 +438,13 @@ gather_x3_kernel(const GatherArgs a) {
             for (int j = 0; j < RM; ++j)
               acc[i][j] = mfma_32x32x16<F16>(wf[kk][i][t == 2 ? 1 : 0], af[kk][j][t == 1 ? 1 : 0], acc[i][j]);
     }
+    }
   };
   auto interleave = [&]() __attribute__((always_inline)) {
 #if SEHIP_IGLP
-    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);                  // first k-substep fragments
+    __builtin_amdgcn_sched_group_barrier(0x100, M16 ? 4 : 8, 0);        // first fragments
 #pragma unroll
-    for (int i = 0; i < 2 * TERMS * RN * RM; ++i) {
+    for (int i = 0; i < (M16 ? TERMS * QN * QM : 2 * TERMS * RN * RM); ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
       if (i < AJ + 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
@@ -513,11 +559,11 @@ gather_x3_kernel(const GatherArgs a) {
   }
   if constexpr (F16) {   // undo the operand scales (exact)
 #pragma unroll
-    for (int i = 0; i < RN; ++i)
+    for (int i = 0; i < QN; ++i)
 #pragma unroll
-      for (int j = 0; j < RM; ++j)
+      for (int j = 0; j < QM; ++j)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], ush);
+        for (int r = 0; r < AR; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], ush);
   }
 
   // --- epilogue (as gather_gemm_kernel) ---
@@ -530,14 +576,19 @@ gather_x3_kernel(const GatherArgs a) {
   __syncthreads();
   const long long HoWo = (long long)a.Ho * a.Wo;
   const bool full_n = n0 + BN <= a.N;
+  // accumulator map: block (i, j) element r2 is column (m) BLK j + lrow and row
+  // (n) BLK i + 4 lq + roff(r2) of the wave tile
+  constexpr int BLK = M16 ? 16 : 32;
+  const int lrow = M16 ? (lane & 15) : lr, lq = M16 ? (lane >> 4) : lh;
+  auto roff = [](int r2) { return M16 ? r2 : (r2 & 3) + 8 * (r2 >> 2); };
 #pragma unroll
-  for (int j = 0; j < RM; ++j) {
-    const int mm = m0 + wm * TM + 32 * j + lr;
+  for (int j = 0; j < QM; ++j) {
+    const int mm = m0 + wm * TM + BLK * j + lrow;
     if (mm >= a.M) continue;
     const int qhw = a.Qh * a.Qw;
     const int b = mm / qhw, r = mm - b * qhw;
     const int qh = r / a.Qw, qw = r - qh * a.Qw;
-    const int nl0 = wn * TN + 4 * lh;
+    const int nl0 = wn * TN + 4 * lq;
     if constexpr (JM == 2) {
       // joined output: a 32-row block of n lies in one join chunk (yjh % 32 == 0);
       // s chunks -> Y over Ho x Wo, x chunks -> Y2 over YH2 x YW2 (rows >= YH2,
@@ -546,27 +597,27 @@ gather_x3_kernel(const GatherArgs a) {
       const long long P2 = (long long)a.YH2 * a.YW2;
       const int cpb = 2 * a.yjh;
 #pragma unroll
-      for (int i = 0; i < RN; ++i) {
-        const int nb = n0 + wn * TN + 32 * i;     // block's first channel (wave-uniform)
+      for (int i = 0; i < QN; ++i) {
+        const int nb = n0 + wn * TN + BLK * i;    // block's first channel (wave-uniform)
         const int q = nb / a.yjh;
-        const int cb = (q >> 1) * a.yjh + (nb - q * a.yjh) + 4 * lh;
+        const int cb = (q >> 1) * a.yjh + (nb - q * a.yjh) + 4 * lq;
         const bool to_x = (q & 1) == 0;
         if (to_x && oh >= a.YH2) continue;
         const long long pl = to_x ? P2 : HoWo;
         float* yp = to_x ? a.Y2 + ((long long)b * cpb + cb) * P2 + (long long)oh * a.YW2 + ow
                          : a.Y + ((long long)b * cpb + cb) * HoWo + (long long)oh * a.Wo + ow;
 #pragma unroll
-        for (int r2 = 0; r2 < 16; ++r2) yp[(long long)((r2 & 3) + 8 * (r2 >> 2)) * pl] = acc[i][j][r2];
+        for (int r2 = 0; r2 < AR; ++r2) yp[(long long)roff(r2) * pl] = acc[i][j][r2];
       }
       continue;
     }
     float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
                 (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
 #pragma unroll
-    for (int i = 0; i < RN; ++i)
+    for (int i = 0; i < QN; ++i)
 #pragma unroll
-      for (int r2 = 0; r2 < 16; ++r2) {
-        const int nl = 32 * i + (r2 & 3) + 8 * (r2 >> 2);
+      for (int r2 = 0; r2 < AR; ++r2) {
+        const int nl = BLK * i + roff(r2);
         if (full_n || n0 + nl0 + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
       }
   }
