@@ -300,17 +300,19 @@ int se_lstm_bwd(const float* dy, const float* w_hh, const float* gates,
                 const float* c, float* dgates, int L, int B, int T, int H,
                 unsigned rev_mask, void* stream);
 
-/* Wide hidden sizes, H in {256, 512} (CARN's nn.LSTM(512), models/
- * _2104_05267_carn.py:132; replaces the MIOpen per-step kernels behind it):
- * same arguments, layouts and results as se_lstm_fwd / se_lstm_bwd (no zero
- * row; any B). W_hh is spread over a group of H/32 workgroups, each holding
- * the gate rows (fwd) / columns (bwd) of 32 hidden units in registers; the
+/* Wide hidden sizes, H in {256, 512, 1024} (CARN's nn.LSTM(512), models/
+ * _2104_05267_carn.py:132; CRN's nn.LSTM(1024), models/_1809_01405_crn.py:90;
+ * replaces the MIOpen per-step kernels behind them): same arguments, layouts
+ * and results as se_lstm_fwd / se_lstm_bwd (no zero row; any B). W_hh is
+ * spread over a group of H/U workgroups (U = 32, 16 at H = 1024), each holding
+ * the gate rows (fwd) / columns (bwd) of U hidden units in registers; the
  * group exchanges h_t / dgates_t through the outputs every step.
  * sync  : device int[se_lstm_wide_sync_ints()] scratch (zeroed by the call)
  * status: device int; set non-zero if a group barrier timed out (the outputs
  *         are then NaN from that step on); never cleared by the library.
- * SE_E_UNSUPPORTED when the groups cannot all be resident on the device at
- * once (L * ceil(B / 8) * H / 32 > number of CUs). */
+ * A batch whose groups cannot all be resident at once runs as consecutive
+ * launches over slices of it; SE_E_UNSUPPORTED only when L LSTMs of 8
+ * sequences do not fit (L * H / U > number of CUs). */
 int se_lstm_wide_supported(int hidden);
 int se_lstm_wide_sync_ints(void);
 int se_lstm_wide_fwd(const float* xproj, long long x_lstm_stride, int x_row_stride,

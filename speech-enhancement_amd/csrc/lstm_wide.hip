@@ -1,16 +1,20 @@
-// Wide-hidden LSTM recurrence (H = 256 / 512): CARN's nn.LSTM(512, 512, 2
-// layers) (models/_2104_05267_carn.py:132; config 5 runs it over 9002 frames)
-// and any ComplexLSTM / nn.LSTM of that width. Same contract and layouts as
+// Wide-hidden LSTM recurrence (H = 256 / 512 / 1024): CARN's nn.LSTM(512, 512,
+// 2 layers) (models/_2104_05267_carn.py:132; config 5 runs it over 9002
+// frames), CRN's nn.LSTM(1024, 1024, 2 layers) (models/_1809_01405_crn.py:90)
+// and any ComplexLSTM / nn.LSTM of those widths. Same contract and layouts as
 // lstm.hip (torch.nn.LSTM math, gate order i, f, g, o, h0 = c0 = 0; xproj and
 // all weight gradients are the caller's GEMMs), different decomposition:
 //
-// W_hh is 4H x H fp32 = 1 MB (H = 256) / 4 MB (H = 512): more than one CU's
-// register file. A GROUP of NWG = H / 32 workgroups runs one block of BS
-// sequences of one LSTM; member m owns hidden units [32 m, 32 m + 32):
-//   fwd: the 4 x 32 gate rows of its units (128 x H weights in VGPRs, thread
-//        = one row x one quarter of the columns), the cell update of its units;
-//   bwd: the 32 columns of its units over all 4H rows (4H x 32 weights, thread
-//        = one column x one 1/16 of the rows), the cell backward of its units.
+// W_hh is 4H x H fp32 = 1 / 4 / 16 MB: more than one CU's register file. A
+// GROUP of NWG = H / U workgroups runs one block of BS sequences of one LSTM;
+// member m owns hidden units [U m, U m + U) (U = 32, or 16 at H = 1024 so that
+// a thread still holds 128 weights):
+//   fwd: the 4U gate rows of its units (4U x H weights in VGPRs, thread = one
+//        row x one 1/QS of the columns, QS = 512 / 4U), the cell update of its
+//        units;
+//   bwd: the U columns of its units over all 4H rows (4H x U weights, thread =
+//        one column x one 1/RBN of the rows, RBN = 512 / U), the cell backward
+//        of its units.
 // Per step the members exchange h_t (fwd, H floats per sequence) or dgates_t
 // (bwd, 4H floats per sequence) through the h / dgates OUTPUTS themselves:
 // agent-scope atomic stores and loads (coherent across XCDs and CUs), and one
@@ -19,16 +23,17 @@
 //
 // Residency: a group's members spin on each other, so all of them must be
 // resident together; the host admits a launch only when every group fits on
-// the device at one workgroup per CU (sync groups are placed on one XCD each:
-// block id % 8 is the XCD under round-robin dispatch, so the exchange stays
-// in one L2 where the placement holds). The spin is bounded: on a timeout the
-// workgroup stops waiting, writes NaN outputs from then on and sets *status.
+// the device at one workgroup per CU, and runs larger batches as consecutive
+// launches over batch slices. Sync groups of up to 32 members are placed on
+// one XCD each (block id % 8 is the XCD under round-robin dispatch, so the
+// exchange stays in one L2 where the placement holds); a 64-member group
+// (H = 1024) spans two XCDs. The spin is bounded: on a timeout the workgroup
+// stops waiting, writes NaN outputs from then on and sets *status.
 #include "common.hpp"
 
 namespace {
 
 constexpr int kWThreads = 512;
-constexpr int kHJ = 32;                    // hidden units per member
 constexpr int kMaxSpins = 1 << 24;         // x s_sleep(1) (64 clk): ~0.4 s
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -62,16 +67,19 @@ struct WideArgs {
   int B, T;
   unsigned rev_mask;
   int ngroups, nbg;     // groups; batch groups per LSTM
+  int b_lo, b_hi;       // the batch slice [b_lo, b_hi) this launch runs
   int* sync;            // [ngroups] step counters (zeroed by the host)
   int* status;
 };
 
-// block -> (group, member): a group's members share block id % 8 (one XCD)
+// block -> (group, member): a group's members share block id % 8 (one XCD),
+// or for NWG > 32 spread over XPG = NWG / 32 consecutive XCD ids
 template <int NWG>
 __device__ __forceinline__ void role_of(int bid, int& gi, int& mem) {
+  constexpr int XPG = NWG > 32 ? NWG / 32 : 1, MPX = NWG / XPG;
   const int xcd = bid & 7, slot = bid >> 3;
-  gi = xcd + 8 * (slot / NWG);
-  mem = slot % NWG;
+  gi = xcd / XPG + (8 / XPG) * (slot / MPX);
+  mem = (xcd % XPG) * MPX + slot % MPX;
 }
 
 // Publish this workgroup's stores of the step, arrive, wait for the group.
@@ -100,23 +108,24 @@ __device__ __forceinline__ bool group_barrier(int* ctr, int target, bool ok, int
   return *s_ok != 0;
 }
 
-template <int H, int BS>
+template <int H, int U, int BS>
 __global__ __launch_bounds__(kWThreads) void lstmw_fwd_kernel(WideArgs a) {
-  constexpr int NWG = H / kHJ, G = 4 * H, R = 4 * kHJ, KQ = H / 4;
+  constexpr int NWG = H / U, G = 4 * H, R = 4 * U, QS = kWThreads / R, KQ = H / QS, RW = R / 64;
+  static_assert(R % 64 == 0 && KQ % 4 == 0 && KQ <= 128, "fwd thread map");
   int gi, mem;
   role_of<NWG>(blockIdx.x, gi, mem);
   if (gi >= a.ngroups) return;                      // whole padding groups leave together
-  const int l = gi / a.nbg, b0 = (gi % a.nbg) * BS;
-  const int j0 = mem * kHJ;
+  const int l = gi / a.nbg, b0 = a.b_lo + (gi % a.nbg) * BS;
+  const int j0 = mem * U;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int row = (wave & 1) * 64 + lane;           // local gate row: gate row / 32, unit row % 32
-  const int q = __builtin_amdgcn_readfirstlane(wave >> 1);   // column quarter
+  const int row = (wave % RW) * 64 + lane;          // local gate row: gate row / U, unit row % U
+  const int q = __builtin_amdgcn_readfirstlane(wave / RW);   // column part
   const bool rev = (a.rev_mask >> l) & 1u;
   const int T = a.T, dir = rev ? -1 : 1, t0 = rev ? T - 1 : 0;
 
   f32x2 w[KQ / 2];
   {
-    const int grow = (row / kHJ) * H + j0 + (row % kHJ);
+    const int grow = (row / U) * H + j0 + (row % U);
     const float4* W = reinterpret_cast<const float4*>(a.w_hh + ((size_t)l * G + grow) * H + q * KQ);
 #pragma unroll
     for (int k = 0; k < KQ / 4; ++k) {
@@ -126,7 +135,7 @@ __global__ __launch_bounds__(kWThreads) void lstmw_fwd_kernel(WideArgs a) {
     }
   }
   __shared__ __attribute__((aligned(16))) float sh[BS][H];   // h_{t-1}
-  __shared__ float sp[4][BS][R];                             // quarter partial sums
+  __shared__ float sp[QS][BS][R];                            // column-part partial sums
   __shared__ float sg[BS][R];                                // activated gates
   __shared__ int s_ok;
   for (int i = tid; i < BS * H; i += kWThreads) (&sh[0][0])[i] = 0.f;
@@ -135,8 +144,8 @@ __global__ __launch_bounds__(kWThreads) void lstmw_fwd_kernel(WideArgs a) {
   constexpr int GU = (BS * R + kWThreads - 1) / kWThreads;
   float xnext[GU];
   auto xrow = [&](int b, int r, int t) __attribute__((always_inline)) {
-    const int bb = min(b0 + b, a.B - 1);
-    return a.xproj + (size_t)l * a.x_lstm + ((size_t)bb * T + t) * a.x_row + (r / kHJ) * H + j0 + (r % kHJ);
+    const int bb = min(b0 + b, a.b_hi - 1);
+    return a.xproj + (size_t)l * a.x_lstm + ((size_t)bb * T + t) * a.x_row + (r / U) * H + j0 + (r % U);
   };
   auto xfetch = [&](int s) __attribute__((always_inline)) {
     const int t = t0 + dir * min(s, T - 1);
@@ -148,7 +157,7 @@ __global__ __launch_bounds__(kWThreads) void lstmw_fwd_kernel(WideArgs a) {
   };
   xfetch(0);
   float cst = 0.f;                                  // cell state of (b, j) = (tid / 32, tid % 32)
-  const int cb = tid / kHJ, cj = tid % kHJ;
+  const int cb = tid / U, cj = tid % U;
   bool ok = true;
   int* ctr = a.sync + gi;
   __syncthreads();
@@ -179,17 +188,20 @@ __global__ __launch_bounds__(kWThreads) void lstmw_fwd_kernel(WideArgs a) {
       const int idx = tid + kWThreads * u;
       if (idx < BS * R) {
         const int b = idx / R, r = idx % R;
-        const float z = xnext[u] + ((sp[0][b][r] + sp[1][b][r]) + (sp[2][b][r] + sp[3][b][r]));
-        const float v = (r / kHJ) == 2 ? tanh_w(z) : sigm(z);
+        float rec = 0.f;
+#pragma unroll
+        for (int p = 0; p < QS; p += 2) rec += sp[p][b][r] + sp[p + 1][b][r];
+        const float z = xnext[u] + rec;
+        const float v = (r / U) == 2 ? tanh_w(z) : sigm(z);
         sg[b][r] = v;
-        if (b0 + b < a.B)
-          a.gates[(((size_t)l * a.B + b0 + b) * T + t) * G + (r / kHJ) * H + j0 + (r % kHJ)] = ok ? v : __int_as_float(0x7fc00000);
+        if (b0 + b < a.b_hi)
+          a.gates[(((size_t)l * a.B + b0 + b) * T + t) * G + (r / U) * H + j0 + (r % U)] = ok ? v : __int_as_float(0x7fc00000);
       }
     }
     xfetch(s + 1);
     __syncthreads();
-    if (tid < BS * kHJ && b0 + cb < a.B) {
-      const float ig = sg[cb][cj], fg = sg[cb][kHJ + cj], gg = sg[cb][2 * kHJ + cj], og = sg[cb][3 * kHJ + cj];
+    if (tid < BS * U && b0 + cb < a.b_hi) {
+      const float ig = sg[cb][cj], fg = sg[cb][U + cj], gg = sg[cb][2 * U + cj], og = sg[cb][3 * U + cj];
       cst = fg * cst + ig * gg;
       const size_t o = (((size_t)l * a.B + b0 + cb) * T + t) * H + j0 + cj;
       const float nan = __int_as_float(0x7fc00000);
@@ -201,23 +213,24 @@ __global__ __launch_bounds__(kWThreads) void lstmw_fwd_kernel(WideArgs a) {
     // h_t of every member -> sh (rows past B read as 0)
     for (int i = tid; i < BS * H; i += kWThreads) {
       const int b = i / H, k = i % H;
-      (&sh[0][0])[i] = b0 + b < a.B ? ld_agent(a.h + (((size_t)l * a.B + b0 + b) * T + t) * H + k) : 0.f;
+      (&sh[0][0])[i] = b0 + b < a.b_hi ? ld_agent(a.h + (((size_t)l * a.B + b0 + b) * T + t) * H + k) : 0.f;
     }
     __syncthreads();
   }
 }
 
-template <int H, int BS>
+template <int H, int U, int BS>
 __global__ __launch_bounds__(kWThreads) void lstmw_bwd_kernel(WideArgs a) {
-  constexpr int NWG = H / kHJ, G = 4 * H, RB = G / 16;
+  constexpr int NWG = H / U, G = 4 * H, RBN = kWThreads / U, RB = G / RBN;
+  static_assert(RB % 4 == 0 && RB <= 128, "bwd thread map");
   int gi, mem;
   role_of<NWG>(blockIdx.x, gi, mem);
   if (gi >= a.ngroups) return;
-  const int l = gi / a.nbg, b0 = (gi % a.nbg) * BS;
-  const int j0 = mem * kHJ;
+  const int l = gi / a.nbg, b0 = a.b_lo + (gi % a.nbg) * BS;
+  const int j0 = mem * U;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int col = lane & 31;                        // unit j0 + col
-  const int rb = wave * 2 + (lane >> 5);            // row block: rows rb*RB .. +RB of all 4H
+  const int col = lane % U;                         // unit j0 + col
+  const int rb = wave * (64 / U) + lane / U;        // row block: rows rb*RB .. +RB of all 4H
   const bool rev = (a.rev_mask >> l) & 1u;
   const int T = a.T, dir = rev ? -1 : 1, t0 = rev ? T - 1 : 0;
 
@@ -228,14 +241,14 @@ __global__ __launch_bounds__(kWThreads) void lstmw_bwd_kernel(WideArgs a) {
     for (int i = 0; i < RB / 2; ++i) w[i] = f32x2{W[(size_t)(2 * i) * H], W[(size_t)(2 * i + 1) * H]};
   }
   __shared__ __attribute__((aligned(16))) float sdg[BS][G];   // dgates_{t+1} of every member
-  __shared__ float sp[16][BS][kHJ];
+  __shared__ float sp[RBN][BS][U];
   __shared__ int s_ok;
   for (int i = tid; i < BS * G; i += kWThreads) (&sdg[0][0])[i] = 0.f;
 
-  // cell threads: (b, j) = (tid / 32, tid % 32), tid < BS * 32
-  const int cb = tid / kHJ, cj = tid % kHJ;
-  const bool cell = tid < BS * kHJ && b0 + cb < a.B;
-  const size_t rowc = ((size_t)l * a.B + min(b0 + cb, a.B - 1)) * T;
+  // cell threads: (b, j) = (tid / U, tid % U), tid < BS * U
+  const int cb = tid / U, cj = tid % U;
+  const bool cell = tid < BS * U && b0 + cb < a.b_hi;
+  const size_t rowc = ((size_t)l * a.B + min(b0 + cb, a.b_hi - 1)) * T;
   struct Pre { float dy, c, cp, g[4]; };
   auto fetch = [&](int s, Pre& p) __attribute__((always_inline)) {
     s = max(s, 0);
@@ -279,7 +292,7 @@ __global__ __launch_bounds__(kWThreads) void lstmw_bwd_kernel(WideArgs a) {
     if (cell) {
       float dh_rec = 0.f;
 #pragma unroll
-      for (int r = 0; r < 16; ++r) dh_rec += sp[r][cb][cj];
+      for (int r = 0; r < RBN; ++r) dh_rec += sp[r][cb][cj];
       const Pre p = pre;
       if (s > 0) fetch(s - 1, pre);
       const float dh = p.dy + dh_rec, ct = p.c, cp = p.cp;
@@ -298,7 +311,7 @@ __global__ __launch_bounds__(kWThreads) void lstmw_bwd_kernel(WideArgs a) {
     ok = group_barrier(ctr, NWG * (T - s), ok, a.status, &s_ok);
     for (int i = tid; i < BS * G; i += kWThreads) {
       const int b = i / G, r = i % G;
-      (&sdg[0][0])[i] = b0 + b < a.B ? ld_agent(a.dgates + (((size_t)l * a.B + b0 + b) * T + t) * G + r) : 0.f;
+      (&sdg[0][0])[i] = b0 + b < a.b_hi ? ld_agent(a.dgates + (((size_t)l * a.B + b0 + b) * T + t) * G + r) : 0.f;
     }
     __syncthreads();
   }
@@ -316,9 +329,13 @@ int cu_count() {
   return n;
 }
 
-// Smallest BS whose groups take at most half the CUs (else all of them).
+constexpr int units_of(int H) { return H > 512 ? 16 : 32; }
+
+// Smallest BS whose groups take at most half the CUs (else all of them), for
+// the batch slice of B sequences
 int plan_of(int L, int B, int H, Plan& p) {
-  const int nwg = H / kHJ, cus = cu_count();
+  const int nwg = H / units_of(H), cus = cu_count();
+  const int gpr = nwg > 32 ? 8 / (nwg / 32) : 8;   // groups per round of 8 XCD ids
   if (cus <= 0) return SE_E_LAUNCH;
   for (int pass = 0; pass < 2; ++pass) {
     const int budget = pass == 0 ? cus / 2 : cus;
@@ -327,7 +344,7 @@ int plan_of(int L, int B, int H, Plan& p) {
       const long long wgs = (long long)L * nbg * nwg;
       if (wgs <= budget) {
         p.bs = bs; p.nbg = nbg; p.ngroups = L * nbg;
-        p.blocks = ((p.ngroups + 7) / 8) * 8 * nwg;
+        p.blocks = ((p.ngroups + gpr - 1) / gpr) * gpr * nwg;
         return SE_OK;
       }
     }
@@ -337,11 +354,12 @@ int plan_of(int L, int B, int H, Plan& p) {
 
 template <int H>
 int launch_wide(bool bwd, WideArgs& a, const Plan& p, hipStream_t st) {
+  constexpr int U = units_of(H);
   const dim3 grid(p.blocks), blk(kWThreads);
 #define SE_WIDE_CASE(BSV)                                                                      \
   case BSV:                                                                                    \
-    if (bwd) hipLaunchKernelGGL((lstmw_bwd_kernel<H, BSV>), grid, blk, 0, st, a);              \
-    else hipLaunchKernelGGL((lstmw_fwd_kernel<H, BSV>), grid, blk, 0, st, a);                  \
+    if (bwd) hipLaunchKernelGGL((lstmw_bwd_kernel<H, U, BSV>), grid, blk, 0, st, a);           \
+    else hipLaunchKernelGGL((lstmw_fwd_kernel<H, U, BSV>), grid, blk, 0, st, a);               \
     break;
   switch (p.bs) {
     SE_WIDE_CASE(1)
@@ -355,21 +373,35 @@ int launch_wide(bool bwd, WideArgs& a, const Plan& p, hipStream_t st) {
   return SE_OK;
 }
 
+// One launch per batch slice: the whole batch when its groups fit on the device
+// at once, else slices of the largest multiple of 8 sequences that do.
 int wide_common(bool bwd, WideArgs& a, int L, int H, int* sync, int* status, hipStream_t st) {
   if (L <= 0 || L > 32 || a.B <= 0 || a.T <= 0 || !sync || !status) return SE_E_ARG;
-  if (H != 256 && H != 512) return SE_E_UNSUPPORTED;
+  if (H != 256 && H != 512 && H != 1024) return SE_E_UNSUPPORTED;
   if ((long long)L * a.B * a.T * 4 * H >= (1ll << 40)) return SE_E_SHAPE;
   Plan p{};
-  int rc = plan_of(L, a.B, H, p);
-  if (rc) return rc;
-  a.ngroups = p.ngroups; a.nbg = p.nbg; a.sync = sync; a.status = status;
-  if (hipMemsetAsync(sync, 0, sizeof(int) * p.ngroups, st) != hipSuccess) return SE_E_LAUNCH;
-  return H == 256 ? launch_wide<256>(bwd, a, p, st) : launch_wide<512>(bwd, a, p, st);
+  int slice = a.B;
+  while (plan_of(L, slice, H, p) != SE_OK) {
+    if (slice <= 8) return SE_E_UNSUPPORTED;
+    slice = ((slice / 2 + 7) / 8) * 8;
+  }
+  for (int lo = 0; lo < a.B; lo += slice) {
+    const int nb = std::min(slice, a.B - lo);
+    int rc = plan_of(L, nb, H, p);
+    if (rc) return rc;
+    a.ngroups = p.ngroups; a.nbg = p.nbg; a.sync = sync; a.status = status;
+    a.b_lo = lo; a.b_hi = lo + nb;
+    if (hipMemsetAsync(sync, 0, sizeof(int) * p.ngroups, st) != hipSuccess) return SE_E_LAUNCH;
+    rc = H == 256 ? launch_wide<256>(bwd, a, p, st)
+                  : H == 512 ? launch_wide<512>(bwd, a, p, st) : launch_wide<1024>(bwd, a, p, st);
+    if (rc) return rc;
+  }
+  return SE_OK;
 }
 
 }  // namespace
 
-extern "C" int se_lstm_wide_supported(int hidden) { return hidden == 256 || hidden == 512; }
+extern "C" int se_lstm_wide_supported(int hidden) { return hidden == 256 || hidden == 512 || hidden == 1024; }
 
 extern "C" int se_lstm_wide_sync_ints(void) { return 4096; }
 

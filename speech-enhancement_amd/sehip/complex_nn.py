@@ -173,8 +173,8 @@ class ComplexLinear(nn.Module):
         return merge_real_imag(x, self.real_linear(re), self.imag_linear(im), dim=-1)
 
 
-# hidden sizes of the HIP recurrence: se_lstm_* (64, 128), se_lstm_wide_* (256, 512)
-HIP_LSTM_HIDDEN = (64, 128, 256, 512)
+# hidden sizes of the HIP recurrence: se_lstm_* (64, 128), se_lstm_wide_* (256, 512, 1024)
+HIP_LSTM_HIDDEN = (64, 128, 256, 512, 1024)
 
 
 def _hip_lstm_ok(m: nn.LSTM) -> bool:
@@ -233,7 +233,7 @@ def stacked_lstms(x, lstms, batch_first=True, with_state=False):
 class LSTM(nn.LSTM):
     """torch.nn.LSTM (same constructor, parameters and state_dict keys) whose
     recurrence runs on the HIP kernels (stacked_lstms) when the configuration
-    is covered: hidden 64 / 128 / 256 / 512, no proj_size, no initial state,
+    is covered: hidden 64 / 128 / 256 / 512 / 1024, no proj_size, no initial state,
     a dense [B, T, I] (batch_first) or [T, B, I] CUDA input. fp16 / bf16
     parameters and inputs (model.half()) compute in fp32 and return the
     caller's dtype. Anything else is nn.LSTM's own forward."""

@@ -701,7 +701,8 @@ def _zero_row(n: int, device) -> torch.Tensor:
 
 def lstm_supported(hidden: int) -> bool:
     """H the HIP recurrence covers: 64 / 128 (se_lstm_*, one workgroup per
-    sequence pair) and 256 / 512 (se_lstm_wide_*, a group of H/32 workgroups)."""
+    sequence pair) and 256 / 512 / 1024 (se_lstm_wide_*, a group of H/32 or
+    H/16 workgroups)."""
     return bool(N.lib().se_lstm_supported(int(hidden))) or bool(N.lib().se_lstm_wide_supported(int(hidden)))
 
 
@@ -727,7 +728,7 @@ def lstm_wide_status(device="cuda") -> int:
 
 
 def _wide(H: int) -> bool:
-    return H in (256, 512)
+    return H in (256, 512, 1024)
 
 
 class _LstmLayer(torch.autograd.Function):

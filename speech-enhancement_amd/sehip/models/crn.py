@@ -2,7 +2,8 @@
 that exercises the mag/phase API of ConvSTFT / ConviSTFT (HIP kernels); its
 real convs run on the real-weight form of the HIP conv GEMMs (real_conv2d),
 BatchNorm2d + ELU as one fused HIP pass each way (norm.bn_act); the 1024-wide
-LSTM stays nn.LSTM (MIOpen): wider than the HIP recurrences (64-512)."""
+two-layer LSTM (:90) on the wide HIP recurrence (se_lstm_wide_*, a group of 64
+workgroups of 16 hidden units)."""
 from __future__ import annotations
 
 import torch

@@ -1,8 +1,9 @@
 """Parity of the wide-hidden HIP LSTM recurrence (csrc/lstm_wide.hip via
-se_lstm_wide_fwd / se_lstm_wide_bwd: H = 256 / 512, a group of H/32
-workgroups per sequence block exchanging h_t / dgates_t every step) with
-torch.nn.LSTM, the op CARN calls (models/_2104_05267_carn.py:132,
-nn.LSTM(512, 512, num_layers=2, batch_first=True)).
+se_lstm_wide_fwd / se_lstm_wide_bwd: H = 256 / 512 / 1024, a group of H/32
+(H/16 at 1024) workgroups per sequence block exchanging h_t / dgates_t every
+step) with torch.nn.LSTM, the op CARN calls (models/_2104_05267_carn.py:132,
+nn.LSTM(512, 512, num_layers=2, batch_first=True)) and CRN calls
+(models/_1809_01405_crn.py:90, nn.LSTM(1024, 1024, num_layers=2)).
 
 Oracle: PyTorch's CPU nn.LSTM in fp32 at small shapes; at config 5's length
 (one 30 s @ 48 kHz utterance = 9002 frames, H = 512, two layers) nn.LSTM on
@@ -37,6 +38,10 @@ def _status(dev):
     (512, 64, 1, 1, False, 1),       # single step, one sequence
     (256, 256, 9, 12, False, 2),     # BS > 1 groups with a partial last block
     (512, 96, 40, 6, False, 1),      # many groups (BS = 8)
+    (1024, 1024, 2, 9, False, 2),    # CRN's LSTM: 64-member groups over two XCD ids
+    (1024, 48, 3, 6, True, 1),       # bidirectional at H = 1024
+    (1024, 32, 20, 4, False, 1),     # three groups of 8 sequences
+    (1024, 32, 40, 3, False, 1),     # more groups than fit at once: two batch-slice launches
 ])
 def test_wide_lstm_matches_nn_lstm(gpu_device, H, I, B, T, bidir, layers):
     from sehip.complex_nn import stacked_lstms

@@ -248,12 +248,13 @@ def test_frcrn_b16_4s_train_forward_vs_oracle(gpu_device):
 
 @pytest.mark.parametrize("i", [3, 5])
 def test_real_conv_models_backward_vs_oracle(i, gpu_device):
-    """CARN / CRN run their real convs on the HIP conv GEMMs (real_conv2d): train-mode
+    """CARN / CRN on the HIP kernels (real convs on the conv GEMMs, BatchNorm2d +
+    PReLU / ELU fused, the 512- / 1024-wide LSTMs on the wide recurrence): train-mode
     forward + backward against the CPU oracle on the golden input (loss = <wav, r>).
-    Their BatchNorm2d / PReLU / ELU / LSTM stay PyTorch ops, whose GPU (MIOpen) backward
-    is itself not CPU-exact (CRN: nn.BatchNorm2d's input gradient at decoder layer 2
-    is 4.5e-4 off the CPU, tools/crn_act_diag.py), so the gradient gate is 3x the
-    error of the oracle's own modules run on the GPU, floored at 1e-3."""
+    The same modules' GPU (MIOpen) backward is itself not CPU-exact (CRN:
+    nn.BatchNorm2d's input gradient at decoder layer 2 is 4.5e-4 off the CPU,
+    tools/crn_act_diag.py), so the gradient gate is 3x the error of the oracle's own
+    modules run on the GPU, floored at 1e-3."""
     from oracle import models as O
     name, ctor = _models()[i]
     octor = {3: lambda: O.CARN(320, 160, 512), 5: lambda: O.CRN(320, 160, 320)}[i]
