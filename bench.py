@@ -197,7 +197,11 @@ def _roofline(kern, steps, side_ok=False):
     g = convs[tag]
     ach = g["flops"] / (g["ms"] * 1e-3) / 1e12
     terms = TERMS_OF.get(tag.rsplit("_", 1)[-1], 0)
-    peak = BF16_MFMA_PEAK_TFLOPS / terms if terms else FP32_MFMA_PEAK_TFLOPS
+    # split forms: the kernel issues `terms` fp16 / bf16 MFMA products per fp32 product, so
+    # its MFMA rate is terms x the fp32-equivalent rate, against the dense fp16 / bf16 peak
+    ach32 = ach
+    ach = ach32 * terms if terms else ach32
+    peak = BF16_MFMA_PEAK_TFLOPS if terms else FP32_MFMA_PEAK_TFLOPS
     kname, per_call, desc = KERNEL_OF.get(tag, (None, 1, tag))
     launches = g["calls"] * per_call
     alg_bytes_launch = g["bytes"] / launches
@@ -205,6 +209,7 @@ def _roofline(kern, steps, side_ok=False):
     traffic = pmc["hbm_bytes_per_launch"] if pmc else None
     out = {"bound": "mfma", "achieved": round(ach, 2), "peak": round(peak, 1), "unit": "TFLOP/s",
            "frac": round(ach / peak, 4), "traffic": traffic,
+           "achieved_fp32_equivalent": round(ach32, 2),
            "kernel": desc, "kernel_instantiation": kname, "timer_tag": tag,
            "calls_per_step": g["calls"] / steps, "launches_per_step": launches / steps,
            "avg_ms_per_launch": round(g["ms"] / launches, 4),
@@ -215,8 +220,9 @@ def _roofline(kern, steps, side_ok=False):
            "traffic_over_algorithmic": round(traffic / alg_bytes_launch, 3) if traffic else None,
            "rocprof_avg_ms_per_launch": _rocprof_avg_ms(kname) if kname else None,
            "flops_convention": "algorithmic fp32 conv FLOPs (torch FlopCounterMode formula)"
-                               + (f"; peak = bf16/f16 dense MFMA peak / {terms} MFMA terms per fp32 product"
-                                  if terms else "; peak = fp32 MFMA dense peak"),
+                               + (f" x {terms} MFMA terms per fp32 product = fp16/bf16 MFMA FLOPs issued; "
+                                  "peak = dense fp16/bf16 MFMA peak (achieved_fp32_equivalent = the fp32 "
+                                  "conv rate)" if terms else "; peak = fp32 MFMA dense peak"),
            "bytes_convention": "algorithmic bytes = one read of each input, one write of each output "
                                "(fp32); traffic = PMC FETCH_SIZE x2 (gfx950) + WRITE_SIZE per launch of "
                                "that instantiation; avg_ms_per_launch = HIP-event span per call / "
