@@ -274,6 +274,33 @@ int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, float* dx,
                 int act, float slope, float* dx_amax, void* ws, size_t ws_bytes,
                 void* stream);
 
+/* Output head fused into the last ComplexBatchNorm2d (frcrn.py:115, 140-144):
+ * FRCRN's final_conv = nn.Conv2d(C, 2, kernel_size=(1, 2), bias=False) applied
+ * to y = act(CBN(x)) of the last decoder block, whose only consumer it is.
+ * se_cbn_head_fwd writes out [B, 2, H, W-1] = final_conv(y) without writing y
+ * (replaces se_cbn_fwd + the real conv's forward: 2 activation-sized passes
+ * fewer); se_cbn_head_bwd takes gout = dL/dout and forms dL/dy inside both
+ * backward passes, writes dx as se_cbn_bwd, and the head's weight gradient
+ * dw_head [2, C, 1, 2] (overwritten) from y recomputed in the moments pass
+ * (replaces the conv's data-grad and weight-grad and se_cbn_bwd's gy reads).
+ * x: [B, C, H, W]; w_head: [2, C, 1, 2] fp32. out_channels must be 2 and
+ * kernel_w 2 (SE_E_UNSUPPORTED otherwise). Other arguments as se_cbn_fwd /
+ * se_cbn_bwd; the workspace is se_cbn_head_workspace_size(B, C, H * W) bytes
+ * for both. */
+size_t se_cbn_head_workspace_size(int B, int C, int HW);
+
+int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, int W,
+                    const float* const* params, float* const* running, int64_t* nbt,
+                    float* save, int training, float eps, float momentum, int act,
+                    float slope, const float* w_head, int out_channels, int kernel_w,
+                    void* ws, size_t ws_bytes, void* stream);
+
+int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int B, int C, int H, int W,
+                    const float* const* params, const float* save, float* const* dparams,
+                    const float* w_head, float* dw_head, int out_channels, int kernel_w,
+                    int training, int act, float slope, float* dx_amax, void* ws,
+                    size_t ws_bytes, void* stream);
+
 /* ------------------------------------------------------------------------
  * LSTM recurrence (torch.nn.LSTM as used by ComplexLSTM, complex_nn.py:115-145)
  *

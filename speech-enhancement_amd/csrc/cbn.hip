@@ -212,15 +212,63 @@ cbn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int 
   }
 }
 
-// Backward moments: g = (gy [+ gy2]) * act'(z), xt = x - M. gy2 (G2) is a second
-// gradient of the same output (a forked output, se_cbn_bwd2): summed on the fly.
+// Output head of FRCRN (frcrn.py:115, 140-144): final_conv = nn.Conv2d(C, 2, (1, 2),
+// bias=False) applied to y = act(CBN(x)) of the last decoder block. Nothing else
+// reads that y, so it is never written: the forward computes the head straight
+// from x (cbn_head_apply_kernel), and the backward forms dL/dy from the head's
+// gradient g [B, 2, H, W-1] on the fly,
+//   gy_c(h, t) = sum_o w[o, c, 0] g_o(h, t) + w[o, c, 1] g_o(h, t - 1)   (zero off the grid),
+// inside both backward passes, while the moments pass also sums the head's
+// weight gradient dw[o, c, k] = sum g_o(h, t) y_c(h, t + k) from y recomputed.
+constexpr int kHeadNO = 2;   // head output channels
+constexpr int kHeadKW = 2;   // head kernel width (time taps)
+constexpr int kHeadNS = 8;   // extra moments per complex channel: 2 parts x NO x KW
+struct HeadArgs {
+  const float* g;   // [B, NO, H, W - 1]
+  const float* w;   // [NO, C, 1, KW]
+  int W;            // input time width
+};
+
+// g_o at (b, row, t) and (b, row, t - 1) for both outputs, zero off the grid
+struct HeadG { float g0[kHeadNO], g1[kHeadNO]; };
+__device__ __forceinline__ HeadG head_g(const HeadArgs& h, int b, int H, int row, int t) {
+  HeadG r;
+  const int W1 = h.W - 1;
+#pragma unroll
+  for (int o = 0; o < kHeadNO; ++o) {
+    const float* go = h.g + (((long long)b * kHeadNO + o) * H + row) * W1;
+    r.g0[o] = t < W1 ? go[t] : 0.f;
+    r.g1[o] = t >= 1 ? go[t - 1] : 0.f;
+  }
+  return r;
+}
+
+// dL/dy of real channel ch from the head gradient (wc: w[o, ch, k] at o * C * KW + k)
+__device__ __forceinline__ float head_gy(const HeadG& g, const float* wc, int C) {
+  float s = 0.f;
+#pragma unroll
+  for (int o = 0; o < kHeadNO; ++o) s += wc[o * C * kHeadKW] * g.g0[o] + wc[o * C * kHeadKW + 1] * g.g1[o];
+  return s;
+}
+
+__device__ __forceinline__ float act_fwd(float z, int act, float slope) {
+  if (act == 1) return z > 0.f ? z : z * slope;
+  if (act == 2) return fmaxf(z, 0.f);
+  return z;
+}
+
+// Backward moments: g = dL/dy * act'(z), xt = x - M, with dL/dy = gy (SRC 0),
+// gy + gy2 (SRC 1: a forked output, se_cbn_bwd2, summed on the fly) or formed
+// from the head gradient (SRC 2, see HeadArgs; then the head's 8 weight-grad
+// sums per complex channel follow the 6 below in part, stride NS).
 // sums: gr, gi, gr*xtr, gr*xti, gi*xtr, gi*xti
-template <bool G2>
+template <int SRC>
 __global__ void __launch_bounds__(kThreads)
 cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
                        const float* __restrict__ x, int B, int C, int HW, int P,
                        const float* __restrict__ save, int act, float slope, double* part, float* ext,
-                       float* dx_amax) {
+                       float* dx_amax, HeadArgs hd) {
+  constexpr int NS = SRC == 2 ? 6 + kHeadNS : 6;
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
   if (dx_amax && c == 0 && p == 0 && threadIdx.x == 0) *dx_amax = 0.f;   // the finalize blocks atomicMax into it
   const int nseg = (HW + kSeg - 1) / kSeg;
@@ -228,23 +276,53 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
   float gmr = 0.f, gmi = 0.f;   // max |g_r|, max |g_i| (the dx bound)
   const float mr = sv[S_MR], mi = sv[S_MI];
   const float zrr = sv[S_ZRR], zri = sv[S_ZRI], zir = sv[S_ZIR], zii = sv[S_ZII], br = sv[S_BR], bi = sv[S_BI];
-  double v[6] = {0, 0, 0, 0, 0, 0};
+  double v[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) v[k] = 0;
+  const int H = SRC == 2 ? HW / hd.W : 1;
+  const float* wcr = SRC == 2 ? hd.w + c * kHeadKW : nullptr;
+  const float* wci = SRC == 2 ? hd.w + (Cc + c) * kHeadKW : nullptr;
   for (int row = p; row < B * nseg; row += P) {
     const int b = row / nseg, sg = row - b * nseg;
     const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
     const int i1 = min(HW, (sg + 1) * kSeg);
-    for (int i = sg * kSeg + threadIdx.x; i < i1; i += kThreads) {
+    int i = sg * kSeg + threadIdx.x;
+    int hr = 0, ht = 0;   // (row, t) of i in the head's grid, stepped with i
+    if (SRC == 2) { hr = i / hd.W; ht = i - hr * hd.W; }
+    for (; i < i1; i += kThreads) {
       const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
       const float zr = zrr * xr + zri * xi + br, zi = zir * xr + zii * xi + bi;   // = forward pre-activation
-      const float gr = (G2 ? gy[offr + i] + gy2[offr + i] : gy[offr + i]) * act_grad(zr, act, slope);
-      const float gi = (G2 ? gy[offi + i] + gy2[offi + i] : gy[offi + i]) * act_grad(zi, act, slope);
+      float dyr, dyi;
+      HeadG hg;
+      if (SRC == 2) {
+        hg = head_g(hd, b, H, hr, ht);
+        dyr = head_gy(hg, wcr, C);
+        dyi = head_gy(hg, wci, C);
+      } else {
+        dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
+        dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
+      }
+      const float gr = dyr * act_grad(zr, act, slope);
+      const float gi = dyi * act_grad(zi, act, slope);
       gmr = fmaxf(gmr, fabsf(gr)); gmi = fmaxf(gmi, fabsf(gi));
       v[0] += gr; v[1] += gi;
       v[2] += (double)gr * xr; v[3] += (double)gr * xi;
       v[4] += (double)gi * xr; v[5] += (double)gi * xi;
+      if (SRC == 2) {
+        const double yr = act_fwd(zr, act, slope), yi = act_fwd(zi, act, slope);
+#pragma unroll
+        for (int o = 0; o < kHeadNO; ++o) {
+          v[6 + 2 * o] += hg.g0[o] * yr;      // dw[o, c_r, 0]: g(t) y(t)
+          v[7 + 2 * o] += hg.g1[o] * yr;      // dw[o, c_r, 1]: g(t - 1) y(t)
+          v[10 + 2 * o] += hg.g0[o] * yi;     // dw[o, c_i, 0]
+          v[11 + 2 * o] += hg.g1[o] * yi;     // dw[o, c_i, 1]
+        }
+        ht += kThreads;
+        while (ht >= hd.W) { ht -= hd.W; ++hr; }
+      }
     }
   }
-  block_reduce_store<6>(v, part + ((long long)c * P + p) * 6);
+  block_reduce_store<NS>(v, part + ((long long)c * P + p) * NS);
   __syncthreads();
   gmr = block_max(gmr);
   __syncthreads();
@@ -260,27 +338,43 @@ constexpr int kCoef = 16;
 
 // One wave per channel, as cbn_finalize_kernel; the bound of max |dx| goes to
 // *dx_amax by atomicMax (zeroed by the backward moments pass).
+// HEAD: part holds the head's 8 weight-grad sums after the 6 moments (stride
+// 6 + kHeadNS); they are added in the same fixed order and written to dwh.
+template <bool HEAD>
 __global__ void __launch_bounds__(64 * kFinWaves)
 cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
                         const float* save, Ptr5 params, int affine,
                         MPtr5 dparams, int has_dparams, int training,
-                        float* coef, float* dx_amax) {
+                        float* coef, float* dx_amax, float* dwh) {
+  constexpr int NS = HEAD ? 6 + kHeadNS : 6;
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
   if (c >= Cc) return;
-  double sm[6] = {0, 0, 0, 0, 0, 0};
+  double sm[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) sm[k] = 0;
   float gmr = 0.f, gmi = 0.f;
   for (int p = lane; p < P; p += 64) {
 #pragma unroll
-    for (int k = 0; k < 6; ++k) sm[k] += part[((long long)c * P + p) * 6 + k];
+    for (int k = 0; k < NS; ++k) sm[k] += part[((long long)c * P + p) * NS + k];
     gmr = fmaxf(gmr, ext[((long long)c * P + p) * 2 + 0]);
     gmi = fmaxf(gmi, ext[((long long)c * P + p) * 2 + 1]);
   }
 #pragma unroll
-  for (int k = 0; k < 6; ++k) sm[k] = se::wave_sum(sm[k]);
+  for (int k = 0; k < NS; ++k) sm[k] = se::wave_sum(sm[k]);
   gmr = se::wave_max(gmr);
   gmi = se::wave_max(gmi);
   if (lane != 0) return;
+  if (HEAD) {   // dw[o, ch, k] at (o * C + ch) * KW + k, C = 2 Cc
+    const int C = 2 * Cc;
+#pragma unroll
+    for (int o = 0; o < kHeadNO; ++o)
+#pragma unroll
+      for (int k = 0; k < kHeadKW; ++k) {
+        dwh[((long long)o * C + c) * kHeadKW + k] = (float)sm[6 + 2 * o + k];
+        dwh[((long long)o * C + Cc + c) * kHeadKW + k] = (float)sm[10 + 2 * o + k];
+      }
+  }
   {
     const float* s = save + (long long)c * kSave;
     const double urr = s[S_URR], uri = s[S_URI], uii = s[S_UII];
@@ -343,16 +437,17 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
   }
 }
 
-template <bool G2>
+template <int SRC>   // dL/dy source as cbn_bwd_moments_kernel
 __global__ void __launch_bounds__(kThreads)
 cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
                      const float* __restrict__ x, float* __restrict__ dx, int C, int HW,
-                     const float* __restrict__ coef, int act, float slope) {
+                     const float* __restrict__ coef, int act, float slope, HeadArgs hd) {
   const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
   const float* k = coef + c * kCoef;
   const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
   const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
   const float br = k[11], bi = k[12];
+  const int H = SRC == 2 ? HW / hd.W : 1;
   // forward Z = [[a00, a10], [a01, a11]] (coef holds Z^T)
   const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
   const int base = blockIdx.x * kThreads * 4 + threadIdx.x;
@@ -362,11 +457,85 @@ cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ gy2
     if (i < HW) {
       const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
       const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
-      const float gr = (G2 ? gy[offr + i] + gy2[offr + i] : gy[offr + i]) * act_grad(zr, act, slope) - gbr;
-      const float gi = (G2 ? gy[offi + i] + gy2[offi + i] : gy[offi + i]) * act_grad(zi, act, slope) - gbi;
+      float dyr, dyi;
+      if (SRC == 2) {
+        const int hr = i / hd.W;
+        const HeadG hg = head_g(hd, b, H, hr, i - hr * hd.W);
+        dyr = head_gy(hg, hd.w + c * kHeadKW, C);
+        dyi = head_gy(hg, hd.w + (Cc + c) * kHeadKW, C);
+      } else {
+        dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
+        dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
+      }
+      const float gr = dyr * act_grad(zr, act, slope) - gbr;
+      const float gi = dyi * act_grad(zi, act, slope) - gbi;
       dx[offr + i] = a00 * gr + a01 * gi + grr * xr + gri * xi;
       dx[offi + i] = a10 * gr + a11 * gi + gri * xr + gii * xi;
     }
+  }
+}
+
+// Forward of the head: out[b, o, h, t] = sum_c sum_k w[o, c, k] y_c(h, t + k),
+// y = act(Z (x - M) + B), t < W - 1. One thread per input position loops over
+// the channels (fp32 sums in channel order, as a direct conv); a wave covers 64
+// consecutive positions of one plane and writes the 63 outputs whose t + 1
+// neighbour is in the wave (waves overlap by one position), taking the k = 1
+// partial sum from lane + 1. grid: ceil(B * ceil(HW / 63) / 4) blocks of 256.
+__global__ void __launch_bounds__(kThreads)
+cbn_head_apply_kernel(const float* __restrict__ x, float* __restrict__ out, int B, int C, int HW, int W,
+                      const float* __restrict__ save, const float* __restrict__ wh, int act, float slope,
+                      int64_t* nbt) {
+  extern __shared__ float sm[];   // Cc x 8 CBN coefficients, then NO x C x KW head weights
+  const int Cc = C / 2;
+  if (nbt && blockIdx.x == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked
+  for (int j = threadIdx.x; j < Cc * 8; j += kThreads) {
+    const int c = j >> 3, f = j & 7;
+    const int src[8] = {S_MR, S_MI, S_ZRR, S_ZRI, S_ZIR, S_ZII, S_BR, S_BI};
+    sm[j] = save[c * kSave + src[f]];
+  }
+  float* sw = sm + Cc * 8;
+  for (int j = threadIdx.x; j < kHeadNO * C * kHeadKW; j += kThreads) sw[j] = wh[j];
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const long long wave = (long long)blockIdx.x * (kThreads / 64) + (threadIdx.x >> 6);
+  const int wpb = (HW + 62) / 63;   // waves per plane
+  if (wave >= (long long)B * wpb) return;
+  const int b = (int)(wave / wpb);
+  const int pos = (int)(wave - (long long)b * wpb) * 63 + lane;
+  const bool in = pos < HW;
+  const float* xb = x + (long long)b * C * HW + (in ? pos : 0);
+  float p[kHeadNO][kHeadKW] = {};
+  constexpr int U = 4;
+  for (int c0 = 0; c0 < Cc; c0 += U) {
+    float vr[U], vi[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = min(c0 + u, Cc - 1);
+      vr[u] = xb[(long long)c * HW];
+      vi[u] = xb[(long long)(Cc + c) * HW];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int c = c0 + u;
+      if (c < Cc) {
+        const float* k = sm + c * 8;
+        const float xr = vr[u] - k[0], xi = vi[u] - k[1];
+        const float yr = act_fwd(k[2] * xr + k[3] * xi + k[6], act, slope);
+        const float yi = act_fwd(k[4] * xr + k[5] * xi + k[7], act, slope);
+#pragma unroll
+        for (int o = 0; o < kHeadNO; ++o)
+#pragma unroll
+          for (int t = 0; t < kHeadKW; ++t)
+            p[o][t] += sw[(o * C + c) * kHeadKW + t] * yr + sw[(o * C + Cc + c) * kHeadKW + t] * yi;
+      }
+    }
+  }
+  const int H = HW / W, row = pos / W, t = pos - row * W;
+#pragma unroll
+  for (int o = 0; o < kHeadNO; ++o) {
+    const float nx = __shfl_down(p[o][1], 1, 64);   // lane + 1's k = 1 partial
+    if (in && lane < 63 && t < W - 1)
+      out[(((long long)b * kHeadNO + o) * H + row) * (W - 1) + t] = p[o][0] + nx;
   }
 }
 
@@ -377,28 +546,36 @@ int pick_P(int B, int Cc, int HW) {
 
 }  // namespace
 
-extern "C" size_t se_cbn_workspace_size(int B, int C, int HW) {
+// workspace: part [Cc][P][ns] doubles, coef [Cc][kCoef], ext [Cc][P][4] floats;
+// ns = 6 (5 forward moments), or 6 + kHeadNS for the head's backward
+static size_t ws_bytes_ns(int B, int C, int HW, int ns) {
   if (B <= 0 || C <= 0 || HW <= 0) return 0;
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
-  return (size_t)Cc * P * 6 * sizeof(double) + (size_t)Cc * kCoef * sizeof(float) +
+  return (size_t)Cc * P * ns * sizeof(double) + (size_t)Cc * kCoef * sizeof(float) +
          (size_t)Cc * P * 4 * sizeof(float) + 512;
 }
 
-// per-(channel, partition) extrema of the moments passes, after part and coef
-static float* ext_of(void* ws, int Cc, int P) {
-  return (float*)((char*)ws + (size_t)Cc * P * 6 * sizeof(double) + (size_t)Cc * kCoef * sizeof(float));
+extern "C" size_t se_cbn_workspace_size(int B, int C, int HW) { return ws_bytes_ns(B, C, HW, 6); }
+
+extern "C" size_t se_cbn_head_workspace_size(int B, int C, int HW) {
+  return ws_bytes_ns(B, C, HW, 6 + kHeadNS);
 }
 
-extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
-                          const float* const* params, float* const* running, int64_t* nbt,
-                          float* save, int training, float eps, float momentum, int act,
-                          float slope, float* y_amax, void* ws, size_t ws_bytes, void* stream) {
-  if (!x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || act < 0 || act > 2)
-    return SE_E_ARG;
-  if (!training && !running) return SE_E_ARG;  // eval needs running statistics
-  if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
-  hipStream_t st = se::as_stream(stream);
+// per-(channel, partition) extrema of the moments passes, after part and coef
+static float* coef_of(void* ws, int Cc, int P, int ns) {
+  return (float*)((char*)ws + (size_t)Cc * P * ns * sizeof(double));
+}
+static float* ext_of(void* ws, int Cc, int P, int ns = 6) {
+  return (float*)((char*)coef_of(ws, Cc, P, ns) + (size_t)Cc * kCoef * sizeof(float));
+}
+
+namespace {
+
+// moments + finalize of the training forward (running update, save, y bound)
+int cbn_stats(const float* x, int B, int C, int HW, const float* const* params, float* const* running,
+              int64_t* nbt, float* save, int training, float eps, float momentum, float* y_amax,
+              void* ws, hipStream_t st) {
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
   double* part = (double*)ws;
@@ -416,50 +593,104 @@ extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
                      ext, P, (double)B * HW, Cc, pp, params ? 1 : 0, rp, running ? 1 : 0, (const int64_t*)nbt, save,
                      training, eps, momentum, training ? y_amax : nullptr);
   SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), Cc, B), dim3(kThreads),
+  return SE_OK;
+}
+
+}  // namespace
+
+extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
+                          const float* const* params, float* const* running, int64_t* nbt,
+                          float* save, int training, float eps, float momentum, int act,
+                          float slope, float* y_amax, void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || act < 0 || act > 2)
+    return SE_E_ARG;
+  if (!training && !running) return SE_E_ARG;  // eval needs running statistics
+  if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
+  hipStream_t st = se::as_stream(stream);
+  const int rc = cbn_stats(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st);
+  if (rc != SE_OK) return rc;
+  hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), C / 2, B), dim3(kThreads),
                      0, st, x, y, C, HW, save, act, slope, (training && running) ? nbt : nullptr);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, int W,
+                               const float* const* params, float* const* running, int64_t* nbt,
+                               float* save, int training, float eps, float momentum, int act,
+                               float slope, const float* w_head, int out_channels, int kernel_w,
+                               void* ws, size_t ws_bytes, void* stream) {
+  if (!x || !out || !save || !w_head || B <= 0 || C <= 0 || (C & 1) || H <= 0 || W < 2 || act < 0 || act > 2)
+    return SE_E_ARG;
+  if (out_channels != kHeadNO || kernel_w != kHeadKW) return SE_E_UNSUPPORTED;
+  if ((long long)H * W >= (1LL << 31)) return SE_E_UNSUPPORTED;
+  if (!training && !running) return SE_E_ARG;
+  const int HW = H * W;
+  if (ws_bytes < se_cbn_head_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
+  hipStream_t st = se::as_stream(stream);
+  const int rc = cbn_stats(x, B, C, HW, params, running, nbt, save, training, eps, momentum, nullptr, ws, st);
+  if (rc != SE_OK) return rc;
+  const long long waves = (long long)B * ((HW + 62) / 63);
+  const size_t lds = ((size_t)(C / 2) * 8 + (size_t)kHeadNO * C * kHeadKW) * sizeof(float);
+  if (lds > 64 * 1024) return SE_E_UNSUPPORTED;
+  hipLaunchKernelGGL(cbn_head_apply_kernel, dim3(se::ceil_div(waves, kThreads / 64)), dim3(kThreads), lds, st,
+                     x, out, B, C, HW, W, save, w_head, act, slope, (training && running) ? nbt : nullptr);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
 
 namespace {
 
-int cbn_bwd_impl(const float* gy, const float* gy2, const float* x, float* dx, int B, int C,
-                 int HW, const float* const* params, const float* save, float* const* dparams,
-                 int training, int act, float slope, float* dx_amax, void* ws, size_t ws_bytes,
+// src 0: gy, 1: gy + gy2, 2: the head gradient (hd)
+int cbn_bwd_impl(int src, const float* gy, const float* gy2, const HeadArgs& hd, const float* x, float* dx,
+                 int B, int C, int HW, const float* const* params, const float* save, float* const* dparams,
+                 int training, int act, float slope, float* dx_amax, float* dwh, void* ws, size_t ws_bytes,
                  void* stream) {
-  if (!gy || !x || !dx || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0) return SE_E_ARG;
-  if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
+  const int ns = src == 2 ? 6 + kHeadNS : 6;
+  if (ws_bytes < ws_bytes_ns(B, C, HW, ns) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
   double* part = (double*)ws;
-  float* coef = (float*)((char*)ws + (size_t)Cc * P * 6 * sizeof(double));
-  float* ext = ext_of(ws, Cc, P);
+  float* coef = coef_of(ws, Cc, P, ns);
+  float* ext = ext_of(ws, Cc, P, ns);
   Ptr5 pp{};
   MPtr5 dp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (dparams) for (int k = 0; k < 5; ++k) dp.p[k] = dparams[k];
-  if (gy2)
-    hipLaunchKernelGGL(cbn_bwd_moments_kernel<true>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2, x,
-                       B, C, HW, P, save, act, slope, part, ext, training ? dx_amax : nullptr);
+  float* xa = training ? dx_amax : nullptr;
+  const dim3 mg(Cc, P), mb(kThreads);
+  if (src == 1)
+    hipLaunchKernelGGL(cbn_bwd_moments_kernel<1>, mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
+                       part, ext, xa, hd);
+  else if (src == 2)
+    hipLaunchKernelGGL(cbn_bwd_moments_kernel<2>, mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
+                       part, ext, xa, hd);
   else
-    hipLaunchKernelGGL(cbn_bwd_moments_kernel<false>, dim3(Cc, P), dim3(kThreads), 0, st, gy, gy2,
-                       x, B, C, HW, P, save, act, slope, part, ext, training ? dx_amax : nullptr);
+    hipLaunchKernelGGL(cbn_bwd_moments_kernel<0>, mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
+                       part, ext, xa, hd);
   SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cbn_bwd_finalize_kernel, dim3(se::ceil_div(Cc, kFinWaves)), dim3(64 * kFinWaves), 0, st,
-                     part, ext, P, (double)B * HW, Cc, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training,
-                     coef, training ? dx_amax : nullptr);
+  const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
+  if (src == 2)
+    hipLaunchKernelGGL(cbn_bwd_finalize_kernel<true>, fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
+                       params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, dwh);
+  else
+    hipLaunchKernelGGL(cbn_bwd_finalize_kernel<false>, fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
+                       params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, nullptr);
   SE_LAUNCH_CHECK();
   const dim3 grid(se::ceil_div(HW, kThreads * 4), Cc, B);
-  if (gy2)
-    hipLaunchKernelGGL(cbn_bwd_apply_kernel<true>, grid, dim3(kThreads), 0, st, gy, gy2, x, dx, C,
-                       HW, coef, act, slope);
+  if (src == 1)
+    hipLaunchKernelGGL(cbn_bwd_apply_kernel<1>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);
+  else if (src == 2)
+    hipLaunchKernelGGL(cbn_bwd_apply_kernel<2>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);
   else
-    hipLaunchKernelGGL(cbn_bwd_apply_kernel<false>, grid, dim3(kThreads), 0, st, gy, gy2, x, dx, C,
-                       HW, coef, act, slope);
+    hipLaunchKernelGGL(cbn_bwd_apply_kernel<0>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);
   SE_LAUNCH_CHECK();
   return SE_OK;
+}
+
+bool bwd_args_ok(const float* x, const float* dx, const float* save, int B, int C, int HW) {
+  return x && dx && save && B > 0 && C > 0 && !(C & 1) && HW > 0;
 }
 
 }  // namespace
@@ -469,8 +700,9 @@ extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float
                           float* const* dparams, int training, int act, float slope,
                           float* dx_amax, void* ws, size_t ws_bytes, void* stream) {
   (void)y;   // not read: act' is recomputed from x (see the file comment); may be NULL
-  return cbn_bwd_impl(gy, nullptr, x, dx, B, C, HW, params, save, dparams, training, act, slope,
-                      dx_amax, ws, ws_bytes, stream);
+  if (!gy || !bwd_args_ok(x, dx, save, B, C, HW)) return SE_E_ARG;
+  return cbn_bwd_impl(0, gy, nullptr, HeadArgs{}, x, dx, B, C, HW, params, save, dparams, training, act, slope,
+                      dx_amax, nullptr, ws, ws_bytes, stream);
 }
 
 // Forked output (the encoder block's y feeds the next conv AND the decoder skip):
@@ -480,7 +712,21 @@ extern "C" int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, fl
                            int C, int HW, const float* const* params, const float* save,
                            float* const* dparams, int training, int act, float slope,
                            float* dx_amax, void* ws, size_t ws_bytes, void* stream) {
-  if (!gy2) return SE_E_ARG;
-  return cbn_bwd_impl(gy, gy2, x, dx, B, C, HW, params, save, dparams, training, act, slope,
-                      dx_amax, ws, ws_bytes, stream);
+  if (!gy || !gy2 || !bwd_args_ok(x, dx, save, B, C, HW)) return SE_E_ARG;
+  return cbn_bwd_impl(1, gy, gy2, HeadArgs{}, x, dx, B, C, HW, params, save, dparams, training, act, slope,
+                      dx_amax, nullptr, ws, ws_bytes, stream);
+}
+
+extern "C" int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int B, int C, int H, int W,
+                               const float* const* params, const float* save, float* const* dparams,
+                               const float* w_head, float* dw_head, int out_channels, int kernel_w,
+                               int training, int act, float slope, float* dx_amax, void* ws,
+                               size_t ws_bytes, void* stream) {
+  if (!gout || !w_head || !dw_head || H <= 0 || W < 2 || act < 0 || act > 2) return SE_E_ARG;
+  if (out_channels != kHeadNO || kernel_w != kHeadKW) return SE_E_UNSUPPORTED;
+  if ((long long)H * W >= (1LL << 31)) return SE_E_UNSUPPORTED;
+  if (!bwd_args_ok(x, dx, save, B, C, H * W)) return SE_E_ARG;
+  const HeadArgs hd{gout, w_head, W};
+  return cbn_bwd_impl(2, nullptr, nullptr, hd, x, dx, B, C, H * W, params, save, dparams, training, act, slope,
+                      dx_amax, dw_head, ws, ws_bytes, stream);
 }

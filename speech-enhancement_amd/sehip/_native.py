@@ -75,6 +75,11 @@ _SIGNATURES = {
                            c_int, c_int, c_float, _P, _P, c_size_t, _P]),
     "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP,
                             c_int, c_int, c_float, _P, _P, c_size_t, _P]),
+    "se_cbn_head_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "se_cbn_head_fwd": (c_int, [_P, _P] + [c_int] * 4 + [_PP, _PP, _P, _P, c_int, c_float, c_float, c_int,
+                                c_float, _P, c_int, c_int, _P, c_size_t, _P]),
+    "se_cbn_head_bwd": (c_int, [_P, _P, _P] + [c_int] * 4 + [_PP, _P, _PP, _P, _P, c_int, c_int, c_int, c_int,
+                                c_float, _P, _P, c_size_t, _P]),
     "se_lstm_supported": (c_int, [c_int]),
     "se_lstm_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P, _P] + [c_int] * 4
                     + [ctypes.c_uint, _P]),

@@ -607,6 +607,72 @@ def complex_batch_norm(x, wrr, wri, wii, br, bi, running, nbt, training, eps, mo
                             act, slope, fork)
 
 
+class _ComplexBNHead(torch.autograd.Function):
+    """final_conv(act(CBN(x))) with final_conv = Conv2d(C, 2, (1, 2), bias=False):
+    se_cbn_head_fwd / se_cbn_head_bwd (the activation y is never written)."""
+
+    @staticmethod
+    def forward(ctx, x, wrr, wri, wii, br, bi, w_head, running, nbt, training, eps, momentum, act, slope):
+        N.require_device(x, wrr, w_head)
+        x = x.contiguous()
+        w_head = w_head.contiguous()
+        b, c, h, w = x.shape
+        out = torch.empty((b, w_head.shape[0], h, w - 1), device=x.device, dtype=x.dtype)
+        save = torch.empty(N.CBN_SAVE_FLOATS * (c // 2), device=x.device, dtype=torch.float32)
+        params = (wrr, wri, wii, br, bi) if wrr is not None else None
+        lib = N.lib()
+        ws = _workspace(lib.se_cbn_head_workspace_size(b, c, h * w), x.device)
+        mom = -1.0 if momentum is None else float(momentum)
+        t0 = _TIMER.begin() if _TIMER else None
+        N.check(lib.se_cbn_head_fwd(x.data_ptr(), out.data_ptr(), b, c, h, w,
+                                    N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
+                                    save.data_ptr(), int(training), float(eps), mom, int(act),
+                                    float(slope), w_head.data_ptr(), w_head.shape[0], w_head.shape[3],
+                                    ws.data_ptr(), ws.numel(), N.stream_of(x)), "se_cbn_head_fwd")
+        if t0 is not None:   # (1 read for the moments in training) + 1 read + the head's write
+            _TIMER.end("cbn_head_fwd", t0, 0.0, 4.0 * (x.numel() * (2 if training else 1) + out.numel()))
+        ctx.save_for_backward(x, save, w_head, *(params or ()))
+        ctx.cfg = (int(training), int(act), float(slope), params is not None)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        x, save, w_head, *params = ctx.saved_tensors
+        training, act, slope, affine = ctx.cfg
+        gout = gout.contiguous()
+        b, c, h, w = x.shape
+        dx = torch.empty_like(x)
+        dw_head = torch.empty_like(w_head)
+        dparams = [torch.empty_like(p) for p in params] if affine else None
+        lib = N.lib()
+        ws = _workspace(lib.se_cbn_head_workspace_size(b, c, h * w), x.device)
+        dxa = new_amax(x.device) if training else None   # bound of max |dx| (the conv's dy)
+        t0 = _TIMER.begin() if _TIMER else None
+        N.check(lib.se_cbn_head_bwd(gout.data_ptr(), x.data_ptr(), dx.data_ptr(), b, c, h, w,
+                                    N.ptr_array(params if affine else None), save.data_ptr(),
+                                    N.ptr_array(dparams), w_head.data_ptr(), dw_head.data_ptr(),
+                                    w_head.shape[0], w_head.shape[3], training, act, slope, N.ptr(dxa),
+                                    ws.data_ptr(), ws.numel(), N.stream_of(gout)), "se_cbn_head_bwd")
+        if dxa is not None:
+            amax_put(dx, dxa)
+        if t0 is not None:   # x read twice, dx written (the head gradient is L2-resident)
+            _TIMER.end("cbn_head_bwd", t0, 0.0, 4.0 * (3 * x.numel() + 2 * gout.numel()))
+        g = dparams or [None] * 5
+        return (dx, *g, dw_head, None, None, None, None, None, None, None)
+
+
+HEAD_SUPPORTED = ((2, 1, 2),)   # (out_channels, kernel_h, kernel_w) of se_cbn_head_*
+
+
+def complex_batch_norm_head(x, wrr, wri, wii, br, bi, w_head, running, nbt, training, eps, momentum,
+                            act=ACT_NONE, slope=0.0):
+    """conv2d(act(ComplexBatchNorm2d(x)), w_head) for a real (1, 2)-kernel, 2-output,
+    bias-free conv without padding (FRCRN's final_conv), fused: the activation is
+    never written. Returns [B, 2, H, W - 1]."""
+    return _ComplexBNHead.apply(x, wrr, wri, wii, br, bi, w_head, running, nbt, training, eps,
+                                momentum, act, slope)
+
+
 # --------------------------------------------------------------------------
 # ConvSTFT / ConviSTFT — se_stft_* / se_istft_* (stft.hip)
 # --------------------------------------------------------------------------

@@ -74,6 +74,33 @@ class _CausalConvBase(nn.Module):
             return self(F.complex_join(x, skip))
         return norm_act(self.norm, self.act, conv.forward_joined(x, skip))
 
+    def forward_joined_head(self, x, skip, head: nn.Conv2d):
+        """head(self(complex_join(x, skip))) for FRCRN's final_conv (frcrn.py:115, 140):
+        the CBN + activation + head run as one fused op (se_cbn_head_*), so the block's
+        output is never written; anything the fused op does not cover runs unfused."""
+        conv = self._conv()
+        act = {nn.LeakyReLU: F.ACT_LEAKY, nn.ReLU: F.ACT_RELU, nn.Identity: F.ACT_NONE}.get(type(self.act))
+        w = head.weight
+        fusable = (os.environ.get("SEHIP_HEAD", "1") != "0" and isinstance(self.norm, ComplexBatchNorm2d)
+                   and act is not None and not self.padding[1] and x.is_cuda
+                   and isinstance(conv, (ComplexConv2d, ComplexConvTranspose2d)) and x.shape[1] == skip.shape[1]
+                   and type(head) is nn.Conv2d and head.bias is None and w.dtype == torch.float32
+                   and x.dtype == torch.float32 and (w.shape[0], w.shape[2], w.shape[3]) in F.HEAD_SUPPORTED
+                   and head.stride == (1, 1) and head.padding == (0, 0) and head.dilation == (1, 1)
+                   and head.groups == 1)
+        if not fusable:
+            return real_conv2d(head, self.forward_joined(x, skip))
+        y = conv.forward_joined(x, skip)
+        if w.shape[1] != y.shape[1]:
+            raise ValueError(f"head takes {w.shape[1]} channels, the block gives {y.shape[1]}")
+        n = self.norm
+        running = (n.RMr, n.RMi, n.RVrr, n.RVri, n.RVii) if n.track_running_stats else None
+        slope = self.act.negative_slope if act == F.ACT_LEAKY else 0.0
+        return F.complex_batch_norm_head(y, n.Wrr, n.Wri, n.Wii, n.Br, n.Bi, w, running,
+                                         n.num_batches_tracked if n.track_running_stats else None,
+                                         n.training or not n.track_running_stats, n.eps, n.momentum,
+                                         act, slope)
+
 
 def _make_block(block, transposed, in_channels, out_channels, kernel_size, padding, norm, act,
                 causal, is_complex, kwargs):
@@ -182,7 +209,9 @@ class Decoder(nn.Module):
                 self.attend_skip(state, skip, i)
         return state
 
-    def forward(self, x, encoder_outputs, attended=None):
+    def forward(self, x, encoder_outputs, attended=None, head=None):
+        """head: a conv applied to the last block's output (FRCRN's final_conv), fused
+        into that block's CBN where the fused op covers it (forward_joined_head)."""
         if attended is not None:   # gated on the side stream (attend_skips)
             gated, ready = (list(reversed(t)) for t in attended)   # popped like encoder_outputs
             main = torch.cuda.current_stream(x.device)
@@ -200,8 +229,10 @@ class Decoder(nn.Module):
             # modes without a joined kernel materialise it in one pass (se_complex_join)
             if x.shape[-1] - skip.shape[-1] not in (0, 1) or skip.shape[-2] - x.shape[-2] not in (0, 1):
                 raise ValueError(f"decoder/skip grids do not align: {tuple(x.shape)} vs {tuple(skip.shape)}")
+            if head is not None and layer is self.layers[-1]:
+                return layer.forward_joined_head(x, skip, head)
             x = layer.forward_joined(x, skip)
-        return x
+        return real_conv2d(head, x) if head is not None else x
 
 
 class FRCRN(nn.Module):
@@ -240,8 +271,9 @@ class FRCRN(nn.Module):
         b, c, f, t = h.shape                                           # :133-137
         h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2))
         h = h.transpose(1, 2).reshape(b, c, f, t)
-        h = self.decoder(h, skips, attended)
-        mask = torch.tanh(TF.pad(real_conv2d(self.final_conv, h), (0, 0, 1, 0)))   # :140-144
+        # decoder + final_conv; the conv is fused into the last block's CBN (se_cbn_head_*)
+        h = self.decoder(h, skips, attended, head=self.final_conv)
+        mask = torch.tanh(TF.pad(h, (0, 0, 1, 0)))                    # :140-144
         est = TF.pad(mask * noisy, (0, 0, 1, 0))                       # :145-146 (DC back as 0)
         est = est.reshape(b, 2 * half, est.shape[-1])                  # cat(re, im) on dim 1 (:149-152)
         wav = self.istft(est)

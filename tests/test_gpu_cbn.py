@@ -138,3 +138,80 @@ def test_cbn_fork_sums_both_gradients(used, gpu_device):
     assert torch.equal(x1.grad, x0.grad)
     for n in ("Wrr", "Wri", "Wii", "Br", "Bi"):
         assert torch.equal(getattr(m1, n).grad, getattr(m0, n).grad), n
+
+
+@pytest.mark.parametrize("shape,act,train", [((3, 128, 19, 41), 1, True), ((2, 128, 5, 2), 1, True),
+                                             ((2, 16, 7, 300), 2, True), ((3, 128, 19, 41), 1, False),
+                                             ((2, 32, 11, 70), 0, True)])
+def test_cbn_head_fused_vs_fp64(shape, act, train, gpu_device):
+    """se_cbn_head_*: final_conv(act(CBN(x))) (frcrn.py:115, 140) with the activation never
+    written, vs the fp64 oracle CBN + activation + conv2d on the CPU: the head output, dx,
+    the 5 CBN parameter gradients, the head's weight gradient and the running statistics."""
+    from sehip import functional as F
+    from sehip.complex_nn import ComplexBatchNorm2d
+    from oracle.complex_nn import ComplexBatchNorm2d as OCBN
+    tf = torch.nn.functional
+    b, c, h, w = shape
+    gen = torch.Generator().manual_seed(21)
+    x = torch.randn(shape, generator=gen) * 1.7 + 0.4
+    x[:, c // 2:] += 0.5 * x[:, :c // 2]
+    wh = torch.randn(2, c, 1, 2, generator=gen) / c ** 0.5
+    gout = torch.randn(b, 2, h, w - 1, generator=gen)
+    acts = {0: lambda t: t, 1: lambda t: tf.leaky_relu(t, 0.2), 2: tf.relu}
+
+    mo = paramfill.fill_(OCBN(c), seed=7).double()
+    mo.train(train)
+    if not train:   # non-trivial running statistics
+        with torch.no_grad():
+            mo.RMr.uniform_(-0.5, 0.5); mo.RMi.uniform_(-0.5, 0.5)
+            mo.RVrr.uniform_(1, 3); mo.RVii.uniform_(1, 3); mo.RVri.uniform_(-0.5, 0.5)
+    m = paramfill.fill_(ComplexBatchNorm2d(c), seed=7).cuda()
+    m.load_state_dict({k: v.float() for k, v in mo.state_dict().items()})
+    m.train(train)
+    xo = x.double().requires_grad_(True)
+    who = wh.double().requires_grad_(True)
+    yo = tf.conv2d(acts[act](mo(xo)), who)
+    yo.backward(gout.double())
+
+    xg = x.cuda().requires_grad_(True)
+    whg = wh.cuda().requires_grad_(True)
+    running = (m.RMr, m.RMi, m.RVrr, m.RVri, m.RVii)
+    y = F.complex_batch_norm_head(xg, m.Wrr, m.Wri, m.Wii, m.Br, m.Bi, whg, running, m.num_batches_tracked,
+                                  train, m.eps, m.momentum, act, 0.2)
+    y.backward(gout.cuda())
+    assert y.shape == yo.shape
+    assert rel_l2(y.detach().cpu().numpy(), yo.detach().numpy()) < 1e-5
+    assert rel_l2(xg.grad.cpu().numpy(), xo.grad.numpy()) < 1e-5
+    assert rel_l2(whg.grad.cpu().numpy(), who.grad.numpy()) < 1e-5
+    for n in ("Wrr", "Wri", "Wii", "Br", "Bi"):
+        assert rel_l2(getattr(m, n).grad.cpu().numpy(), getattr(mo, n).grad.numpy()) < 1e-5, n
+    for n in ("RMr", "RMi", "RVrr", "RVri", "RVii"):
+        np.testing.assert_allclose(getattr(m, n).cpu().numpy(), getattr(mo, n).detach().numpy(),
+                                   rtol=1e-5, atol=1e-6)
+    assert int(m.num_batches_tracked) == int(mo.num_batches_tracked)
+
+
+def test_frcrn_head_fused_matches_unfused(gpu_device, monkeypatch):
+    """FRCRN train step with the head fused (default) vs SEHIP_HEAD=0 (CBN apply + the
+    real final_conv on the conv kernels): same enhanced output and gradients to fp32
+    rounding (different summation orders only)."""
+    from sehip import models as M
+    noisy, _ = paramfill.structured_pair(2, 16000, seed=3)
+    x = torch.from_numpy(noisy).cuda()
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SEHIP_HEAD", flag)
+        m = paramfill.fill_(M.FRCRN(), seed=3).cuda().train()
+        spec, wav = m(x)
+        (spec.square().sum() + wav.sum()).backward()
+        torch.cuda.synchronize()
+        res.append((spec.detach(), wav.detach(), {n: p.grad.clone() for n, p in m.named_parameters()},
+                    {n: b.clone() for n, b in m.named_buffers()}))
+    (s1, w1, g1, b1), (s0, w0, g0, b0) = res
+    assert rel_l2(s1.cpu().numpy(), s0.cpu().numpy()) < 1e-6
+    assert rel_l2(w1.cpu().numpy(), w0.cpu().numpy()) < 1e-6
+    for n in g0:
+        assert rel_l2(g1[n].cpu().numpy(), g0[n].cpu().numpy()) < 1e-4, n
+    for n in b0:
+        if b0[n].is_floating_point():
+            np.testing.assert_allclose(b1[n].cpu().numpy(), b0[n].cpu().numpy(), rtol=1e-5, atol=1e-6)
