@@ -154,6 +154,11 @@ typedef struct se_conv2d_desc {
   const void* x_packed;
   const void* x2_packed;
   const void* dy_packed;
+  /* SE_MATH_F16X3 only, optional: device fp32 [1] holding an upper bound of
+   * max |w| over the real and imaginary weights (se_amax_weights). The forward
+   * and data-grad passes of one conv call share it (the weights do not change
+   * between them); NULL = the pass computes it itself (two reductions). */
+  const float* w_amax;
 } se_conv2d_desc;
 
 enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3,
@@ -169,6 +174,11 @@ int se_pack_cl16(const float* x, int B, int C, int H, int W, const float* amax,
 /* amax[0] = max(amax[0], max_i |x[i]|) over n elements (atomic; zero amax[0]
  * first for a fresh maximum). The scale source of SE_MATH_F16X3. */
 int se_amax(const float* x, long long n, float* amax, void* stream);
+
+/* max(max |wr|, max |wi|) of a conv's weights (wi may be NULL) written to
+ * *amax by one single-workgroup launch (no zeroing, no atomics): the
+ * se_conv2d_desc.w_amax of an SE_MATH_F16X3 conv call. */
+int se_amax_weights(const float* wr, long long n, const float* wi, float* amax, void* stream);
 
 /* Output spatial size (nn.Conv2d / nn.ConvTranspose2d formulas). */
 int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w);

@@ -23,6 +23,7 @@
 #include "common.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace {
 
@@ -210,6 +211,39 @@ cbn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int 
       y[offi + i] = yi;
     }
   }
+}
+
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+
+// cbn_apply_kernel with 16-B accesses (HW % 4 == 0: every plane starts 16-B
+// aligned): one float4 of the real and one of the imaginary plane per thread.
+// grid (ceil(HW / (kThreads*4)), Cc, B)
+__global__ void __launch_bounds__(kThreads)
+cbn_apply4_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
+                  const float* __restrict__ save, int act, float slope, int64_t* nbt) {
+  const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  if (nbt && blockIdx.x == 0 && c == 0 && b == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked
+  const float* s = save + c * kSave;
+  const float mr = s[S_MR], mi = s[S_MI], zrr = s[S_ZRR], zri = s[S_ZRI];
+  const float zir = s[S_ZIR], zii = s[S_ZII], br = s[S_BR], bi = s[S_BI];
+  const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+  const int i = (blockIdx.x * kThreads + threadIdx.x) * 4;
+  if (i >= HW) return;
+  const f32x4v xr4 = *reinterpret_cast<const f32x4v*>(x + offr + i);
+  const f32x4v xi4 = *reinterpret_cast<const f32x4v*>(x + offi + i);
+  f32x4v yr4, yi4;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float xr = xr4[u] - mr, xi = xi4[u] - mi;
+    float yr = zrr * xr + zri * xi + br;
+    float yi = zir * xr + zii * xi + bi;
+    if (act == 1) { yr = yr > 0.f ? yr : yr * slope; yi = yi > 0.f ? yi : yi * slope; }
+    else if (act == 2) { yr = fmaxf(yr, 0.f); yi = fmaxf(yi, 0.f); }
+    yr4[u] = yr;
+    yi4[u] = yi;
+  }
+  *reinterpret_cast<f32x4v*>(y + offr + i) = yr4;
+  *reinterpret_cast<f32x4v*>(y + offi + i) = yi4;
 }
 
 // Output head of FRCRN (frcrn.py:115, 140-144): final_conv = nn.Conv2d(C, 2, (1, 2),
@@ -475,6 +509,43 @@ cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ gy2
   }
 }
 
+// cbn_bwd_apply_kernel<SRC 0 / 1> with 16-B accesses (HW % 4 == 0)
+template <int SRC>
+__global__ void __launch_bounds__(kThreads)
+cbn_bwd_apply4_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
+                      const float* __restrict__ x, float* __restrict__ dx, int C, int HW,
+                      const float* __restrict__ coef, int act, float slope) {
+  static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
+  const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  const float* k = coef + c * kCoef;
+  const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
+  const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
+  const float br = k[11], bi = k[12];
+  const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+  const int i = (blockIdx.x * kThreads + threadIdx.x) * 4;
+  if (i >= HW) return;
+  const f32x4v xr4 = *reinterpret_cast<const f32x4v*>(x + offr + i);
+  const f32x4v xi4 = *reinterpret_cast<const f32x4v*>(x + offi + i);
+  f32x4v gr4 = *reinterpret_cast<const f32x4v*>(gy + offr + i);
+  f32x4v gi4 = *reinterpret_cast<const f32x4v*>(gy + offi + i);
+  if (SRC == 1) {
+    gr4 += *reinterpret_cast<const f32x4v*>(gy2 + offr + i);
+    gi4 += *reinterpret_cast<const f32x4v*>(gy2 + offi + i);
+  }
+  f32x4v dr4, di4;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const float xr = xr4[u] - mr, xi = xi4[u] - mi;
+    const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
+    const float gr = gr4[u] * act_grad(zr, act, slope) - gbr;
+    const float gi = gi4[u] * act_grad(zi, act, slope) - gbi;
+    dr4[u] = a00 * gr + a01 * gi + grr * xr + gri * xi;
+    di4[u] = a10 * gr + a11 * gi + gri * xr + gii * xi;
+  }
+  *reinterpret_cast<f32x4v*>(dx + offr + i) = dr4;
+  *reinterpret_cast<f32x4v*>(dx + offi + i) = di4;
+}
+
 // Forward of the head: out[b, o, h, t] = sum_c sum_k w[o, c, k] y_c(h, t + k),
 // y = act(Z (x - M) + B), t < W - 1. One thread per input position loops over
 // the channels (fp32 sums in channel order, as a direct conv); a wave covers 64
@@ -537,6 +608,15 @@ cbn_head_apply_kernel(const float* __restrict__ x, float* __restrict__ out, int 
     if (in && lane < 63 && t < W - 1)
       out[(((long long)b * kHeadNO + o) * H + row) * (W - 1) + t] = p[o][0] + nx;
   }
+}
+
+// 16-B apply kernels where HW % 4 == 0 (SEHIP_CBN_VEC=0: the scalar kernels; read once)
+bool vec_ok() {
+  static const bool on = [] {
+    const char* e = std::getenv("SEHIP_CBN_VEC");
+    return !(e && e[0] == '0');
+  }();
+  return on;
 }
 
 int pick_P(int B, int Cc, int HW) {
@@ -609,8 +689,12 @@ extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
   hipStream_t st = se::as_stream(stream);
   const int rc = cbn_stats(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st);
   if (rc != SE_OK) return rc;
-  hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), C / 2, B), dim3(kThreads),
-                     0, st, x, y, C, HW, save, act, slope, (training && running) ? nbt : nullptr);
+  if (HW % 4 == 0 && vec_ok())
+    hipLaunchKernelGGL(cbn_apply4_kernel, dim3(se::ceil_div(HW, kThreads * 4), C / 2, B), dim3(kThreads),
+                       0, st, x, y, C, HW, save, act, slope, (training && running) ? nbt : nullptr);
+  else
+    hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), C / 2, B), dim3(kThreads),
+                       0, st, x, y, C, HW, save, act, slope, (training && running) ? nbt : nullptr);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
@@ -679,7 +763,12 @@ int cbn_bwd_impl(int src, const float* gy, const float* gy2, const HeadArgs& hd,
                        params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, nullptr);
   SE_LAUNCH_CHECK();
   const dim3 grid(se::ceil_div(HW, kThreads * 4), Cc, B);
-  if (src == 1)
+  const bool v4 = HW % 4 == 0 && vec_ok();
+  if (src == 1 && v4)
+    hipLaunchKernelGGL(cbn_bwd_apply4_kernel<1>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope);
+  else if (src == 0 && v4)
+    hipLaunchKernelGGL(cbn_bwd_apply4_kernel<0>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope);
+  else if (src == 1)
     hipLaunchKernelGGL(cbn_bwd_apply_kernel<1>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);
   else if (src == 2)
     hipLaunchKernelGGL(cbn_bwd_apply_kernel<2>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);

@@ -998,6 +998,7 @@ struct ConvGeom {
   int math;       // SE_MATH_*
   const float* x_amax;    // SE_MATH_F16X3 scale sources from the caller (or nullptr)
   const float* dy_amax;
+  const float* w_amax;    // bound of max |w| from the caller (or nullptr)
   const void* x_packed;   // SE_MATH_F16X3 CL16 operands from the caller (or nullptr)
   const void* x2_packed;
   const void* dy_packed;
@@ -1014,6 +1015,7 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.math = d->math;
   g.x_amax = d->x_amax;
   g.dy_amax = d->dy_amax;
+  g.w_amax = d->w_amax;
   g.x_packed = d->x_packed;
   g.x2_packed = d->x2_packed;
   g.dy_packed = d->dy_packed;
@@ -1235,10 +1237,13 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const void* pk = pass == kFwd ? g.x_packed : g.dy_packed;
   const void* pk2 = (pass == kFwd && jn && jn->x2) ? g.x2_packed : nullptr;
   const bool packed = f16 && pk && amax_a && (!jn || !jn->x2 || pk2);
+  const float* wamax = g.w_amax ? g.w_amax : amax_slot;   // bound of max |w|
   if (f16) {
     const long long nw = (long long)(g.complex_w ? g.Ci / 2 : g.Ci) * (g.complex_w ? g.Co / 2 : g.Co) * g.kh * g.kw;
-    launch_amax(wr, nw, amax_slot, st);
-    if (g.complex_w) launch_amax(wi, nw, amax_slot, st);
+    if (!g.w_amax) {
+      launch_amax(wr, nw, amax_slot, st);
+      if (g.complex_w) launch_amax(wi, nw, amax_slot, st);
+    }
     if (!amax_a) {
       launch_amax(X, (long long)g.B * (jn && jn->x2 ? 2 * jn->jh : Cg) * Hi * Wi, amax_slot + 1, st);
       if (jn && jn->x2) launch_amax(jn->x2, (long long)g.B * 2 * jn->jh * jn->h2 * jn->w2, amax_slot + 1, st);
@@ -1278,7 +1283,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     else if (f16)
       hipLaunchKernelGGL(prep_class_x3_kernel<true>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, (const float*)amax_slot);
+                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, wamax);
     else if (x3)
       hipLaunchKernelGGL(prep_class_x3_kernel<false>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
@@ -1289,7 +1294,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
                          Wp, ktab);
     GatherArgs a{};
     a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.zero = zero; a.Y = Y;
-    a.amax_a = amax_a; a.amax_w = amax_slot;
+    a.amax_a = amax_a; a.amax_w = wamax;
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
@@ -1415,6 +1420,31 @@ extern "C" int se_pack_cl16(const float* x, int B, int C, int H, int W, const fl
   const int HW = H * W;
   hipLaunchKernelGGL(pack_cl16_kernel, dim3(se::ceil_div(HW, 64), se::ceil_div(C, 64), B), dim3(256), 0,
                      se::as_stream(stream), x, C, HW, amax, (_Float16*)out, (long long)B * C * HW);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+// one workgroup: max |.| over wr (and wi), written straight to *out
+__global__ void __launch_bounds__(1024) amax_weights_kernel(const float* __restrict__ wr, long long n,
+                                                            const float* __restrict__ wi, float* out) {
+  float m = 0.f;
+  for (long long i = threadIdx.x; i < n; i += 1024) {
+    m = fmaxf(m, fabsf(wr[i]));
+    if (wi) m = fmaxf(m, fabsf(wi[i]));
+  }
+  m = se::wave_max(m);
+  __shared__ float red[16];
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    for (int w = 1; w < 16; ++w) m = fmaxf(m, red[w]);
+    *out = m;
+  }
+}
+
+extern "C" int se_amax_weights(const float* wr, long long n, const float* wi, float* amax, void* stream) {
+  if (!wr || !amax || n < 0) return SE_E_ARG;
+  hipLaunchKernelGGL(amax_weights_kernel, dim3(1), dim3(1024), 0, se::as_stream(stream), wr, n, wi, amax);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

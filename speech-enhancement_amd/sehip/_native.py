@@ -36,7 +36,8 @@ class ConvDesc(ctypes.Structure):
         "dil_h", "dil_w", "out_pad_h", "out_pad_w", "transposed",
         "complex_weights", "pad_h_end", "pad_w_end", "math")] + [
         ("x_amax", c_void_p), ("dy_amax", c_void_p),   # SE_MATH_F16X3 scale sources (or NULL)
-        ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p)]   # CL16 operands (or NULL)
+        ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p),   # CL16 operands (or NULL)
+        ("w_amax", c_void_p)]   # SE_MATH_F16X3 bound of max |w| (or NULL)
 
 
 _P = c_void_p
@@ -54,6 +55,7 @@ _SIGNATURES = {
     "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
     "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
     "se_amax": (c_int, [_P, ctypes.c_longlong, _P, _P]),
+    "se_amax_weights": (c_int, [_P, ctypes.c_longlong, _P, _P, _P]),
     "se_pack_cl16_bytes": (c_size_t, [c_int] * 4),
     "se_pack_cl16": (c_int, [_P] + [c_int] * 4 + [_P, _P, _P]),
     "se_mix_snr": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P, _P]),

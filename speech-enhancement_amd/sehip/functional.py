@@ -241,6 +241,22 @@ def new_amax(device) -> torch.Tensor:
     return torch.empty(1, device=device, dtype=torch.float32)
 
 
+def _weight_amax(d, wr, wi):
+    """se_conv2d_desc.w_amax for one conv call: one single-workgroup launch in the
+    forward, shared by the forward and data-grad GEMMs (which otherwise reduce the
+    weights twice each); None where no split-fp16 gather pass reads it, or with
+    SEHIP_WAMAX=0 (the passes then reduce the weights themselves)."""
+    need = ((_pass_math("fwd", d) == F16X3 and d.out_channels > 64)
+            or (_pass_math("data", d) == F16X3 and d.in_channels > 64))
+    if not need or os.environ.get("SEHIP_WAMAX", "1") == "0":
+        return None
+    a = new_amax(wr.device)
+    n = wr.numel()
+    N.check(N.lib().se_amax_weights(wr.data_ptr(), n, N.ptr(wi), a.data_ptr(), N.stream_of(wr)),
+            "se_amax_weights")
+    return a
+
+
 def _f16_operands(d):
     """(x, dy) -> whether a SE_MATH_F16X3 GEMM of this conv reads that operand's
     scale: the split kernels' shape rules of cconv.hip (gather N > 64, weight-grad
@@ -338,6 +354,8 @@ class _Conv2d(torch.autograd.Function):
         ws = _workspace(nbytes, x.device)
         xa = amax_of(x) if _f16_operands(d)[0] else None
         d.x_amax = N.ptr(xa)
+        wa = _weight_amax(d, wr, wi)
+        d.w_amax = N.ptr(wa)
         t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_conv2d_fwd(_with_math(d, "fwd"), x.data_ptr(), wr.data_ptr(), N.ptr(wi),
                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(),
@@ -346,7 +364,7 @@ class _Conv2d(torch.autograd.Function):
             _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
                        4.0 * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
         ctx.save_for_backward(x, wr, wi)
-        ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax = d, nbytes, br is not None, xa
+        ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax, ctx.w_amax = d, nbytes, br is not None, xa, wa
         return y
 
     @staticmethod
@@ -356,7 +374,7 @@ class _Conv2d(torch.autograd.Function):
         d, lib = ctx.desc, N.lib()
         ws = _workspace(ctx.nbytes, gy.device)
         ga = amax_of(gy) if _f16_operands(d)[1] else None
-        d.x_amax, d.dy_amax = N.ptr(ctx.x_amax), N.ptr(ga)
+        d.x_amax, d.dy_amax, d.w_amax = N.ptr(ctx.x_amax), N.ptr(ga), N.ptr(ctx.w_amax)
         dx = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
@@ -432,6 +450,8 @@ class _ConvJoined(torch.autograd.Function):
         # scale source of the joined input: max of the two sources' bounds
         xa = torch.maximum(amax_of(x), amax_of(s)) if _f16_operands(d)[0] else None
         d.x_amax = N.ptr(xa)
+        wa = _weight_amax(d, wr, wi)
+        d.w_amax = N.ptr(wa)
         t0 = _TIMER.begin() if _TIMER else None
         rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
                                       wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(),
@@ -444,7 +464,7 @@ class _ConvJoined(torch.autograd.Function):
             _TIMER.end(_gemm_tag("fwd", d, joined=True), t0, _conv_flops(d),
                        4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
         ctx.save_for_backward(x, s, wr, wi)
-        ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax = d, nbytes, br is not None, xa
+        ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax, ctx.w_amax = d, nbytes, br is not None, xa, wa
         return y
 
     @staticmethod
@@ -459,7 +479,7 @@ class _ConvJoined(torch.autograd.Function):
         xa = ctx.x_amax
         if xa is None and _f16_operands(d)[0]:   # mode changed since forward
             xa = torch.maximum(amax_of(x), amax_of(s))
-        d.x_amax, d.dy_amax = N.ptr(xa), N.ptr(ga)
+        d.x_amax, d.dy_amax, d.w_amax = N.ptr(xa), N.ptr(ga), N.ptr(ctx.w_amax)
         gx = gs = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             gx, gs = torch.empty_like(x), torch.empty_like(s)
