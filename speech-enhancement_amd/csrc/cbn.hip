@@ -88,12 +88,21 @@ cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, dou
     const float* xr = x + ((long long)b * C + c) * HW;
     const float* xi = x + ((long long)b * C + Cc + c) * HW;
     const int i1 = min(HW, (sg + 1) * kSeg);
-    for (int i = sg * kSeg + threadIdx.x; i < i1; i += kThreads) {
-      const float fr = xr[i], fm = xi[i];
+    auto body = [&](float fr, float fm) __attribute__((always_inline)) {
       e[0] = fmaxf(e[0], fr); e[1] = fmaxf(e[1], -fr); e[2] = fmaxf(e[2], fm); e[3] = fmaxf(e[3], -fm);
       const double r = fr, m = fm;
       v[0] += r; v[1] += m; v[2] += r * r; v[3] += r * m; v[4] += m * m;
+    };
+    int i = sg * kSeg + threadIdx.x;
+    constexpr int U = 4;   // loads of four positions in flight; the sums keep their order
+    for (; i + (U - 1) * kThreads < i1; i += U * kThreads) {
+      float fr[U], fm[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) { fr[u] = xr[i + u * kThreads]; fm[u] = xi[i + u * kThreads]; }
+#pragma unroll
+      for (int u = 0; u < U; ++u) body(fr[u], fm[u]);
     }
+    for (; i < i1; i += kThreads) body(xr[i], xi[i]);
   }
   block_reduce_store<5>(v, part + ((long long)c * P + p) * 5);
 #pragma unroll
@@ -323,19 +332,9 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
     int i = sg * kSeg + threadIdx.x;
     int hr = 0, ht = 0;   // (row, t) of i in the head's grid, stepped with i
     if (SRC == 2) { hr = i / hd.W; ht = i - hr * hd.W; }
-    for (; i < i1; i += kThreads) {
-      const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+    auto body = [&](float fxr, float fxi, float dyr, float dyi, const HeadG& hg) __attribute__((always_inline)) {
+      const float xr = fxr - mr, xi = fxi - mi;
       const float zr = zrr * xr + zri * xi + br, zi = zir * xr + zii * xi + bi;   // = forward pre-activation
-      float dyr, dyi;
-      HeadG hg;
-      if (SRC == 2) {
-        hg = head_g(hd, b, H, hr, ht);
-        dyr = head_gy(hg, wcr, C);
-        dyi = head_gy(hg, wci, C);
-      } else {
-        dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
-        dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
-      }
       const float gr = dyr * act_grad(zr, act, slope);
       const float gi = dyi * act_grad(zi, act, slope);
       gmr = fmaxf(gmr, fabsf(gr)); gmi = fmaxf(gmi, fabsf(gi));
@@ -351,8 +350,51 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
           v[10 + 2 * o] += hg.g0[o] * yi;     // dw[o, c_i, 0]
           v[11 + 2 * o] += hg.g1[o] * yi;     // dw[o, c_i, 1]
         }
+      }
+    };
+    if (SRC == 2) {
+      // four positions per iteration, every load issued before the arithmetic
+      constexpr int U = 4;
+      for (; i + (U - 1) * kThreads < i1; i += U * kThreads) {
+        float fr[U], fm[U];
+        HeadG hg[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          fr[u] = x[offr + i + u * kThreads];
+          fm[u] = x[offi + i + u * kThreads];
+          hg[u] = head_g(hd, b, H, hr, ht);
+          ht += kThreads;
+          while (ht >= hd.W) { ht -= hd.W; ++hr; }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) body(fr[u], fm[u], head_gy(hg[u], wcr, C), head_gy(hg[u], wci, C), hg[u]);
+      }
+      for (; i < i1; i += kThreads) {
+        const HeadG hg = head_g(hd, b, H, hr, ht);
+        body(x[offr + i], x[offi + i], head_gy(hg, wcr, C), head_gy(hg, wci, C), hg);
         ht += kThreads;
         while (ht >= hd.W) { ht -= hd.W; ++hr; }
+      }
+    } else {
+      const HeadG none{};
+      constexpr int U = 4;   // loads of four positions in flight; the sums keep their order
+      for (; i + (U - 1) * kThreads < i1; i += U * kThreads) {
+        float fr[U], fm[U], dr[U], dm[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const int j = i + u * kThreads;
+          fr[u] = x[offr + j];
+          fm[u] = x[offi + j];
+          dr[u] = SRC == 1 ? gy[offr + j] + gy2[offr + j] : gy[offr + j];
+          dm[u] = SRC == 1 ? gy[offi + j] + gy2[offi + j] : gy[offi + j];
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) body(fr[u], fm[u], dr[u], dm[u], none);
+      }
+      for (; i < i1; i += kThreads) {
+        const float dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
+        const float dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
+        body(x[offr + i], x[offi + i], dyr, dyi, none);
       }
     }
   }
