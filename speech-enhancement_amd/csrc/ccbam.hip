@@ -120,6 +120,7 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const float* __restrict
   const int Ch = C / 2;
   const float s0 = sa[((size_t)b * 2) * HW + hw], s1 = sa[((size_t)b * 2 + 1) * HW + hw];
   const size_t base = (size_t)b * C * HW + hw;
+#pragma unroll 8
   for (int c = 0; c < C; ++c) out[base + (size_t)c * HW] = x[base + (size_t)c * HW] * sca[c] + (c < Ch ? s0 : s1);
 }
 
@@ -133,8 +134,20 @@ __global__ __launch_bounds__(kThreads) void bwd_sa_kernel(const float* __restric
   const int Ch = C / 2;
   const float* gb = g + (size_t)b * C * HW + hw;
   float s0 = 0.f, s1 = 0.f;
-  for (int c = 0; c < Ch; ++c) s0 += gb[(size_t)c * HW];
-  for (int c = Ch; c < C; ++c) s1 += gb[(size_t)c * HW];
+  // eight loads per half in flight; each half still sums in channel order
+  constexpr int U = 8;
+  int c = 0;
+  for (; c + U <= Ch; c += U) {
+    float v0[U], v1[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      v0[u] = gb[(size_t)(c + u) * HW];
+      v1[u] = gb[(size_t)(Ch + c + u) * HW];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) { s0 += v0[u]; s1 += v1[u]; }
+  }
+  for (; c < Ch; ++c) { s0 += gb[(size_t)c * HW]; s1 += gb[(size_t)(Ch + c) * HW]; }
   dsa[((size_t)b * 2) * HW + hw] = s0;
   dsa[((size_t)b * 2 + 1) * HW + hw] = s1;
 }
@@ -237,6 +250,7 @@ __global__ __launch_bounds__(kThreads) void bwd_dx_kernel(const float* __restric
     pi[h] = idx[((size_t)b * 2 + h) * HW + hw];
   }
   const size_t base = (size_t)b * C * HW + hw;
+#pragma unroll 8
   for (int c = 0; c < C; ++c) {
     const int h = c < Ch ? 0 : 1, cc = c - h * Ch;
     const size_t o = base + (size_t)c * HW;
