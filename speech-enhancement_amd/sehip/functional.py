@@ -909,7 +909,7 @@ class _LstmLayer(torch.autograd.Function):
                 dx = torch.bmm(dg, w_ih).reshape(L, B, T, I)
         if ctx.needs_input_grad[1]:
             xs = x.reshape(B * T, I) if shared else x.reshape(L, B * T, I)
-            dw_ih = torch.matmul(dgt, xs)
+            dw_ih = torch.stack([_tn_splitk(dg[l], xs if shared else xs[l]) for l in range(L)])
         if ctx.needs_input_grad[2]:
             # dW_hh[l] = sum_t dgates_t^T h_{t-1} (processing order; h_{-1} = 0), without
             # materialising the shifted h: on the flattened (b, t) rows the pairs are
@@ -917,32 +917,38 @@ class _LstmLayer(torch.autograd.Function):
             # straddle two sequences
             hf = h.reshape(L, B * T, H)
             dw_hh = torch.zeros((L, G, H), device=h.device, dtype=h.dtype)
-            for rev in ((0, 1) if T > 1 else ()):   # T = 1: every h_{t-1} is h_{-1} = 0
-                ls = [l for l in range(L) if ((ctx.rev_mask >> l) & 1) == rev]
-                if not ls:
-                    continue
-                idx = torch.tensor(ls, device=h.device) if len(ls) < L else None
-                dgl = dg if idx is None else dg.index_select(0, idx)
-                hl = hf if idx is None else hf.index_select(0, idx)
-                if rev == 0:
-                    w = torch.bmm(dgl[:, 1:].transpose(1, 2), hl[:, :-1])
-                    if B > 1:   # rows b*T (t = 0) paired with the previous sequence's last h
-                        r = torch.arange(1, B, device=h.device) * T
-                        w -= torch.bmm(dgl[:, r].transpose(1, 2), hl[:, r - 1])
+            r = torch.arange(1, B, device=h.device) * T if B > 1 else None
+            for l in (range(L) if T > 1 else ()):   # T = 1: every h_{t-1} is h_{-1} = 0
+                if ((ctx.rev_mask >> l) & 1) == 0:
+                    w = _tn_splitk(dg[l, 1:], hf[l, :-1])
+                    if r is not None:   # rows b*T (t = 0) paired with the previous sequence's last h
+                        w -= dg[l, r].t() @ hf[l, r - 1]
                 else:
-                    w = torch.bmm(dgl[:, :-1].transpose(1, 2), hl[:, 1:])
-                    if B > 1:   # rows b*T + T-1 (t = T-1) paired with the next sequence's first h
-                        r = torch.arange(1, B, device=h.device) * T
-                        w -= torch.bmm(dgl[:, r - 1].transpose(1, 2), hl[:, r])
-                if idx is None:
-                    dw_hh = w
-                else:
-                    dw_hh.index_copy_(0, idx, w)
+                    w = _tn_splitk(dg[l, :-1], hf[l, 1:])
+                    if r is not None:   # rows b*T + T-1 (t = T-1) paired with the next sequence's first h
+                        w -= dg[l, r - 1].t() @ hf[l, r]
+                dw_hh[l] = w
         if ctx.has_b[0] and ctx.needs_input_grad[3] or ctx.has_b[1] and ctx.needs_input_grad[4]:
             db = dg.sum(1)
             db_ih = db if ctx.has_b[0] else None
             db_hh = db if ctx.has_b[1] else None
         return dx, dw_ih, dw_hh, db_ih, db_hh, None
+
+
+def _tn_splitk(a, b):
+    """a^T b for row-major [R, G] and [R, I] (contiguous rows) with a long reduction
+    R (the LSTM weight gradients, R = B*T): split-K over S row chunks (one bmm of S
+    [G, I] products, summed in chunk order, plus the leftover rows), so the GEMM runs
+    on S times the workgroups instead of a handful of long-K tiles."""
+    R = a.shape[0]
+    S = next((s for s in (32, 16, 8, 4, 2) if R // s >= 1024), 1)
+    if S == 1 or os.environ.get("SEHIP_LSTM_SPLITK", "1") == "0":
+        return a.t() @ b
+    C = R // S
+    out = torch.bmm(a[:S * C].view(S, C, -1).transpose(1, 2), b[:S * C].view(S, C, -1)).sum(0)
+    if S * C < R:
+        out += a[S * C:].t() @ b[S * C:]
+    return out
 
 
 def lstm_layer(x, w_ih, w_hh, b_ih=None, b_hh=None, rev_mask: int = 0, with_cell: bool = False):
