@@ -661,9 +661,14 @@ bool vec_ok() {
   return on;
 }
 
+// moments workgroups per pass: Cc x P ~ 2048 (SEHIP_CBN_WG overrides; read once)
 int pick_P(int B, int Cc, int HW) {
+  static const int wg = [] {
+    const char* e = std::getenv("SEHIP_CBN_WG");
+    return e ? std::max(64, std::atoi(e)) : 2048;
+  }();
   const int rows = B * ((HW + kSeg - 1) / kSeg);
-  return std::max(1, std::min(rows, std::max(1, 2048 / std::max(Cc, 1))));
+  return std::max(1, std::min(rows, std::max(1, wg / std::max(Cc, 1))));
 }
 
 }  // namespace

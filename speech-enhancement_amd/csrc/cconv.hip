@@ -445,7 +445,25 @@ struct WgradArgs {
   int toffh[kMaxTaps], toffw[kMaxTaps];
   // wgrad_x3_kernel: tile space (k-tiles, n-tiles, m-splits) walked by its 1-D grid
   int vk, vn, vs;
+  // wgrad_x3_kernel with ktab == nullptr: entries computed in the kernel from
+  // (ntaps, toffh, toffw), k = t * Cg + c (as prep_class_kernel)
+  int ntaps;
 };
+
+// ktab[k] of a weight-grad pass (prep_class_kernel's rule) from the tap table
+__device__ __forceinline__ int4 wgrad_ktab(const WgradArgs& a, int k) {
+  int4 e;
+  if (k < a.ntaps * a.Cg) {
+    const int t = k / a.Cg, c = k - t * a.Cg;
+    e.x = (int)((long long)c * a.Hi * a.Wi + (long long)a.toffh[t] * a.Wi + a.toffw[t]);
+    e.y = a.toffh[t];
+    e.z = a.toffw[t];
+  } else {
+    e.x = 0; e.y = kInvalidOff; e.z = 0;
+  }
+  e.w = 0;
+  return e;
+}
 
 // Small-N weight grad (N <= 8: FRCRN's final_conv 128->2 and the CCBAM spatial
 // ComplexConv2d 4->2): an MFMA tile would be >= 75% padding, and the pass is
@@ -776,11 +794,24 @@ wgrad_gemm_kernel(const WgradArgs a) {
 }
 
 // Deterministic split reduction: slab[0][k][n] = sum_s slab[s][k][n] (coalesced).
-__global__ void slab_reduce_kernel(float* slab, int splits, long long per) {
+// In place: row g*gs of each group of gs consecutive split rows gets the group's
+// sum (blockIdx.y = group; rows added in order); with gs = splits, row 0 gets
+// the total. Two passes (groups, then the group rows at stride gs) keep the
+// order fixed and give the few-output / many-split slabs enough workgroups.
+__global__ void slab_reduce_kernel(float* slab, int splits, long long per, int gs) {
+  const int g0 = blockIdx.y * gs, g1 = min(splits, g0 + gs);
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < per;
+       i += (long long)gridDim.x * blockDim.x) {
+    float s = slab[(long long)g0 * per + i];
+    for (int sp = g0 + 1; sp < g1; ++sp) s += slab[(long long)sp * per + i];
+    slab[(long long)g0 * per + i] = s;
+  }
+}
+__global__ void slab_gather_kernel(float* slab, int splits, long long per, int gs) {
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < per;
        i += (long long)gridDim.x * blockDim.x) {
     float s = slab[i];
-    for (int sp = 1; sp < splits; ++sp) s += slab[(long long)sp * per + i];
+    for (int sp = gs; sp < splits; sp += gs) s += slab[(long long)sp * per + i];
     slab[i] = s;
   }
 }
@@ -1539,9 +1570,12 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   p = align256(p + (size_t)w.splits * w.c.Kp * w.Np * sizeof(float));
   int4* ktab = (int4*)p;
 
+  const bool x3_path = g.math == SE_MATH_F16X3 && split_ok && w.N > 32 && w.N > kSmallWgradN && w.Np != 32 &&
+                       !(g.x_packed || g.dy_packed) && w.c.taps.n <= kMaxTaps && !env_flag_off("SEHIP_WGRAD_DKTAB");
   // ktab only (no weights): reuse prep_class_kernel with ldw = 1 writing into slab[0]
-  // would clobber; build it with a one-column pass into a scratch row instead.
-  {
+  // would clobber; build it with a one-column pass into a scratch row instead. The
+  // split-fp16 weight-grad kernel computes its entries itself (no launch).
+  if (!x3_path) {
     WeightView wv{nullptr, nullptr, g.Ci, g.Co, g.kh, g.kw, g.transposed, 0};
     // N = 0 -> every Wp entry is 0 and only ktab matters; Wp scratch = slab start
     hipLaunchKernelGGL(prep_class_kernel, dim3(se::ceil_div(w.c.Kp, 256)), dim3(256), 0, st, wv,
@@ -1550,7 +1584,9 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   WgradArgs a{};
   a.X = g.transposed ? dy : x;
   a.D = g.transposed ? x : dy;
-  a.ktab = ktab; a.slab = slab; a.zero = zero;
+  a.ktab = x3_path ? nullptr : ktab; a.slab = slab; a.zero = zero;
+  a.ntaps = w.c.taps.n;
+  for (int t = 0; t < w.c.taps.n && t < kMaxTaps; ++t) { a.toffh[t] = w.c.taps.offh[t]; a.toffw[t] = w.c.taps.offw[t]; }
   a.Cg = w.Cg; a.Hi = w.Hi; a.Wi = w.Wi;
   a.N = w.N; a.Qh = w.Qh; a.Qw = w.Qw; a.sh = w.c.h.s; a.sw = w.c.w.s;
   a.Kp = w.c.Kp; a.Np = w.Np; a.M = w.M; a.m_per_split = w.m_per_split;
@@ -1637,9 +1673,17 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
 
   const long long per = (long long)w.c.Kp * w.Np;
   if (w.splits > 1) {
-    hipLaunchKernelGGL(slab_reduce_kernel, dim3((unsigned)std::min<long long>((per + 255) / 256, 2048)),
-                       dim3(256), 0, st, slab, w.splits, per);
+    const unsigned bx = (unsigned)std::min<long long>((per + 255) / 256, 2048);
+    // groups of >= 16 splits until ~2048 workgroups (SEHIP_SLAB_2L=0: one pass)
+    int ng = env_flag_off("SEHIP_SLAB_2L") ? 1 : std::max(1, std::min<int>(w.splits / 16, 2048 / (int)bx));
+    const int gs = se::ceil_div(w.splits, ng);
+    ng = se::ceil_div(w.splits, gs);
+    hipLaunchKernelGGL(slab_reduce_kernel, dim3(bx, ng), dim3(256), 0, st, slab, w.splits, per, gs);
     SE_LAUNCH_CHECK();
+    if (ng > 1) {
+      hipLaunchKernelGGL(slab_gather_kernel, dim3(bx), dim3(256), 0, st, slab, w.splits, per, gs);
+      SE_LAUNCH_CHECK();
+    }
   }
   UnpackArgs u{};
   u.slab = slab; u.splits = 1; u.Kp = w.c.Kp; u.Np = w.Np;

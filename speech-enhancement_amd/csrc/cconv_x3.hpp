@@ -674,7 +674,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   const int ml = lane & 31, lr = lane >> 5;
   const int rbase = 32 * wave + RJ * lr;     // this thread's first G row / D row
 
-  for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab[k0 + i];
+  for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
   __syncthreads();
   float sg = 1.f, sd = 1.f;   // F16: operand scales; the slab gets acc * 2^ush
   int ush = 0;
@@ -712,7 +712,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   if constexpr (DJ)
     rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.D2 + (long long)bfirst * dcpb * QQ2), (short)0,
                                                 0x7FFFFFFF, 0x00020000);
-  const int4 tap_e = a.ktab[k0];
+  const int4 tap_e = sK[0];
   const int cbase = k0 % a.Cg;
   const bool one_wrap = a.Qw >= BMR;
   auto advance = [&]() __attribute__((always_inline)) {

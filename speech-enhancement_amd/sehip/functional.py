@@ -929,7 +929,7 @@ class _LstmLayer(torch.autograd.Function):
                         w -= dg[l, r - 1].t() @ hf[l, r]
                 dw_hh[l] = w
         if ctx.has_b[0] and ctx.needs_input_grad[3] or ctx.has_b[1] and ctx.needs_input_grad[4]:
-            db = dg.sum(1)
+            db = _rows_sum(dg)
             db_ih = db if ctx.has_b[0] else None
             db_hh = db if ctx.has_b[1] else None
         return dx, dw_ih, dw_hh, db_ih, db_hh, None
@@ -948,6 +948,21 @@ def _tn_splitk(a, b):
     out = torch.bmm(a[:S * C].view(S, C, -1).transpose(1, 2), b[:S * C].view(S, C, -1)).sum(0)
     if S * C < R:
         out += a[S * C:].t() @ b[S * C:]
+    return out
+
+
+def _rows_sum(a):
+    """a.sum(1) for [L, R, G] with long R (the LSTM bias gradients): the rows in S
+    chunks reduced first (S x more workgroups than ATen's reduction over R), then
+    the S partial rows, in order."""
+    L, R, G = a.shape
+    S = next((s for s in (32, 16, 8, 4, 2) if R // s >= 1024), 1)
+    if S == 1 or os.environ.get("SEHIP_LSTM_SPLITK", "1") == "0":
+        return a.sum(1)
+    C = R // S
+    out = a[:, :S * C].reshape(L, S, C, G).sum(2).sum(1)
+    if S * C < R:
+        out += a[:, S * C:].sum(1)
     return out
 
 
