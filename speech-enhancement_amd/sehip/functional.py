@@ -386,8 +386,12 @@ class _Conv2d(torch.autograd.Function):
                 _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
                            4.0 * (gy.numel() + dx.numel() + wr.numel() * (2 if wi is not None else 1)))
         if any(ctx.needs_input_grad[1:5]):
-            with _wgrad_stream(x, gy, ctx.x_amax, ga):
-                if _DEFER is not None:
+            # a conv without an input gradient (a model's first conv) is the last one in
+            # the backward: its weight-grad runs on the current stream, beside the side
+            # stream's still-queued weight-grads, instead of behind them
+            last = not ctx.needs_input_grad[0] and os.environ.get("SEHIP_LAST_WGRAD_INLINE", "1") != "0"
+            with contextlib.nullcontext() if last else _wgrad_stream(x, gy, ctx.x_amax, ga):
+                if _DEFER is not None and not last:
                     ws = _workspace(ctx.nbytes, gy.device)
                 if ctx.x_amax is None and _f16_operands(d)[0]:   # mode changed since forward
                     d.x_amax = N.ptr(amax_of(x))

@@ -204,8 +204,8 @@ class Decoder(nn.Module):
         """All six gates at once on the side stream (after the encoder): returns
         (gated skips in decoder order, their ready events) or None (see gate_state)."""
         state = self.gate_state(encoder_outputs[0])
-        if state is not None:
-            for i, skip in enumerate(encoder_outputs):
+        if state is not None:   # deepest (smallest, first needed) skip first
+            for i, skip in reversed(list(enumerate(encoder_outputs))):
                 self.attend_skip(state, skip, i)
         return state
 
@@ -265,8 +265,11 @@ class FRCRN(nn.Module):
             skips.append(skip)                                         # as soon as it exists
             if attended is not None and early:
                 self.decoder.attend_skip(attended, skip, i)
-        if attended is not None and not early:                         # all six after the encoder
-            for i, skip in enumerate(skips):
+        if attended is not None and not early:                         # all six after the encoder,
+            order = list(enumerate(skips))                             # in the decoder's order (the
+            if os.environ.get("SEHIP_GATE_ORDER", "dec") == "dec":     # smallest, deepest skip first):
+                order.reverse()                                        # the decoder starts right after
+            for i, skip in order:                                      # the LSTM, beside the big gates
                 self.decoder.attend_skip(attended, skip, i)
         b, c, f, t = h.shape                                           # :133-137
         h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2))
