@@ -23,6 +23,8 @@
 // single L2 round trip (measured: 4.7 -> 2.7 us per forward step at H = 128).
 #include "common.hpp"
 
+#include <cstdlib>
+
 
 namespace {
 
@@ -340,13 +342,222 @@ __global__ __launch_bounds__(4 * H) void lstm_bwd_kernel(LstmArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// LDS-exchange forms (default): the recurrent operand (h_{t-1} forward,
+// dgates_t backward) never leaves the workgroup, so it goes through LDS:
+// written by the cell update, one barrier, then read by every lane as 16-B
+// broadcast loads (all lanes of a wave read the same address: no bank
+// conflict) straight into the packed FMAs. No global round trip and no wait
+// for the step's stores in the recurrence (they are only for the backward /
+// the weight gradients). The products are summed in the same order as the
+// scalar-operand kernels above (even pairs into acc[0], odd into acc[1]), so
+// the results are bit-identical.
+// ---------------------------------------------------------------------------
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <int H, int BS>
+__global__ __launch_bounds__(4 * H) void lstm_fwd_lds_kernel(LstmArgs a) {
+  constexpr int G = 4 * H;
+  const int r = threadIdx.x;
+  const int l = blockIdx.y, b0 = blockIdx.x * BS;
+  const bool rev = (a.rev_mask >> l) & 1u;
+  const int T = a.T;
+
+  f32x2 w[H / 2];
+  {
+    const f32x2* W = reinterpret_cast<const f32x2*>(a.w_hh + ((size_t)l * G + r) * H);
+#pragma unroll
+    for (int q = 0; q < H / 2; ++q) w[q] = W[q];
+  }
+  __shared__ float sg[BS][G];
+  __shared__ __attribute__((aligned(16))) float sh[BS][H];   // h_{t-1}
+  for (int i = r; i < BS * H; i += G) (&sh[0][0])[i] = 0.f;   // h_{-1} = 0
+
+  const float* xp = a.xproj + (size_t)l * a.x_lstm + r;
+  int brow[BS];
+#pragma unroll
+  for (int b = 0; b < BS; ++b) brow[b] = min(b0 + b, a.B - 1);
+  const int gate = __builtin_amdgcn_readfirstlane(r / H);
+  static_assert((4 * H) % (BS * H) == 0, "threads must cover the cells");
+  const int cb = (r % (BS * H)) / H, cj = r % H;
+  const size_t crow = (size_t)l * a.B + brow[cb];
+  float cst = 0.f;
+  const int dir = rev ? -1 : 1, t0 = rev ? T - 1 : 0;
+  auto xload = [&](int sx, float* dst) __attribute__((always_inline)) {
+    const float* q = xp + (size_t)(t0 + dir * min(sx, T - 1)) * a.x_row;
+#pragma unroll
+    for (int b = 0; b < BS; ++b) dst[b] = q[(size_t)brow[b] * T * a.x_row];
+  };
+  float xa[BS], xb[BS];
+  xload(0, xa);
+  xload(1, xb);
+  __syncthreads();
+  auto step = [&](int s, float* xs) __attribute__((always_inline)) {
+    const int t = t0 + dir * s;
+    float z[BS];
+#pragma unroll
+    for (int b = 0; b < BS; ++b) {
+      f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
+      const f32x4* hv = reinterpret_cast<const f32x4*>(&sh[b][0]);
+#pragma unroll
+      for (int c0 = 0; c0 < H / 4; c0 += 8) {   // chunks of 8 loads: bounded live registers
+#pragma unroll
+        for (int q4 = c0; q4 < c0 + 8; ++q4) {
+          const f32x4 v = hv[q4];
+          acc0 = __builtin_elementwise_fma(w[2 * q4], f32x2{v.x, v.y}, acc0);
+          acc1 = __builtin_elementwise_fma(w[2 * q4 + 1], f32x2{v.z, v.w}, acc1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      z[b] = xs[b] + ((acc0.x + acc0.y) + (acc1.x + acc1.y));
+    }
+    float v[BS];
+#pragma unroll
+    for (int b = 0; b < BS; ++b) {
+      const float th = tanh_bf(z[b]), sg_ = sigmoidf(z[b]);
+      v[b] = gate == 2 ? th : sg_;
+      sg[b][r] = v[b];
+    }
+#pragma unroll
+    for (int b = BS - 1; b >= 0; --b) a.gates[(((size_t)l * a.B + brow[b]) * T + t) * G + r] = v[b];
+    __syncthreads();   // gates of the step complete; every read of h_{t-1} done
+    {
+      const float ig = sg[cb][cj], fg = sg[cb][H + cj], gg = sg[cb][2 * H + cj], og = sg[cb][3 * H + cj];
+      cst = fg * cst + ig * gg;
+      const float hv = og * tanh_bf(cst);
+      const size_t o = (crow * T + t) * H + cj;
+      a.c[o] = cst;
+      a.h[o] = hv;
+      sh[cb][cj] = hv;   // duplicate cells store the same value
+    }
+    xload(s + 2, xs);
+    __syncthreads();   // h_t in LDS for the next step
+  };
+  int s = 0;
+  for (; s + 1 < T; s += 2) {
+    step(s, xa);
+    step(s + 1, xb);
+  }
+  if (s < T) step(s, xa);
+}
+
+template <int H, int BS>
+__global__ __launch_bounds__(4 * H) void lstm_bwd_lds_kernel(LstmArgs a) {
+  constexpr int G = 4 * H;
+  const int tid = threadIdx.x;
+  const int k = tid % H;
+  const int rq = __builtin_amdgcn_readfirstlane(tid / H);
+  const int l = blockIdx.y, b0 = blockIdx.x * BS;
+  const bool rev = (a.rev_mask >> l) & 1u;
+  const int T = a.T;
+
+  f32x2 w[H / 2];
+  {
+    const float* W = a.w_hh + ((size_t)l * G + rq * H) * H + k;
+#pragma unroll
+    for (int p = 0; p < H / 2; ++p) w[p] = f32x2{W[(2 * p) * H], W[(2 * p + 1) * H]};
+  }
+  __shared__ float sp[4][BS][H];
+  __shared__ __attribute__((aligned(16))) float sdg[BS][G];   // dgates_t
+
+  static_assert((4 * H) % (BS * H) == 0, "threads must cover the cells");
+  const int cb = (tid % (BS * H)) / H, cj = tid % H;
+  float dc = 0.f, dh_rec = 0.f;
+  const size_t rowc = ((size_t)l * a.B + min(b0 + cb, a.B - 1)) * T;
+  const int dir = rev ? -1 : 1, t0 = rev ? T - 1 : 0;
+
+  struct Pre { float dy, c, cp, g[4]; };
+  auto fetch = [&](int sx, Pre& p) __attribute__((always_inline)) {
+    sx = max(sx, 0);
+    const int t = t0 + dir * sx;
+    const int tp = t0 + dir * max(sx - 1, 0);
+    const size_t o = (rowc + t) * H + cj;
+    p.dy = a.dy[o];
+    p.c = a.c[o];
+    p.cp = a.c[(rowc + tp) * H + cj] * (sx > 0 ? 1.f : 0.f);
+    const float* gp = a.gates + (rowc + t) * G + cj;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) p.g[q] = gp[q * H];
+  };
+  Pre pa, pb;
+  fetch(T - 1, pa);
+  fetch(T - 2, pb);
+
+  auto cell_step = [&](int s, const Pre& pc_) __attribute__((always_inline)) {
+    const int t = t0 + dir * s;
+    const float dh = pc_.dy + dh_rec, ct = pc_.c, cp = pc_.cp;
+    const float ig = pc_.g[0], fg = pc_.g[1], gg = pc_.g[2], og = pc_.g[3];
+    const float tc = tanh_bf(ct);
+    dc += dh * og * (1.f - tc * tc);
+    const float d0 = dc * gg * ig * (1.f - ig);
+    const float d1 = dc * cp * fg * (1.f - fg);
+    const float d2 = dc * ig * (1.f - gg * gg);
+    const float d3 = dh * tc * og * (1.f - og);
+    dc *= fg;
+    float* dg = a.dgates + (rowc + t) * G + cj;
+    dg[0] = d0;
+    dg[H] = d1;
+    dg[2 * H] = d2;
+    dg[3 * H] = d3;
+    sdg[cb][cj] = d0;
+    sdg[cb][H + cj] = d1;
+    sdg[cb][2 * H + cj] = d2;
+    sdg[cb][3 * H + cj] = d3;
+  };
+  auto rec_step = [&](int s, Pre& pc_) __attribute__((always_inline)) {
+    fetch(s - 2, pc_);
+    __syncthreads();   // dgates_t in LDS
+#pragma unroll
+    for (int b = 0; b < BS; ++b) {
+      f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
+      const f32x4* gv = reinterpret_cast<const f32x4*>(&sdg[b][rq * H]);
+#pragma unroll
+      for (int c0 = 0; c0 < H / 4; c0 += 8) {   // chunks of 8 loads: bounded live registers
+#pragma unroll
+        for (int p4 = c0; p4 < c0 + 8; ++p4) {
+          const f32x4 v = gv[p4];
+          acc0 = __builtin_elementwise_fma(w[2 * p4], f32x2{v.x, v.y}, acc0);
+          acc1 = __builtin_elementwise_fma(w[2 * p4 + 1], f32x2{v.z, v.w}, acc1);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      sp[rq][b][k] = (acc0.x + acc0.y) + (acc1.x + acc1.y);
+    }
+    __syncthreads();
+    dh_rec = (sp[0][cb][cj] + sp[1][cb][cj]) + (sp[2][cb][cj] + sp[3][cb][cj]);
+  };
+  int s = T - 1;
+  for (; s >= 2; s -= 2) {
+    cell_step(s, pa);
+    rec_step(s, pa);
+    cell_step(s - 1, pb);
+    rec_step(s - 1, pb);
+  }
+  if (s == 1) {
+    cell_step(1, pa);
+    rec_step(1, pa);
+    cell_step(0, pb);
+  } else {
+    cell_step(0, pa);
+  }
+}
+
 constexpr int kBS = 2;
 
 template <int H>
 int launch(bool bwd, const LstmArgs& a, int L, hipStream_t st) {
   dim3 grid((a.B + kBS - 1) / kBS, L);
-  if (bwd)
+  // SEHIP_LSTM_LDS=0: the scalar-load (global round trip) forms; read once
+  static const bool lds = [] {
+    const char* e = std::getenv("SEHIP_LSTM_LDS");
+    return !(e && e[0] == '0');
+  }();
+  if (bwd && lds)
+    hipLaunchKernelGGL((lstm_bwd_lds_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
+  else if (bwd)
     hipLaunchKernelGGL((lstm_bwd_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
+  else if (lds)
+    hipLaunchKernelGGL((lstm_fwd_lds_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
   else
     hipLaunchKernelGGL((lstm_fwd_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
   SE_LAUNCH_CHECK();
