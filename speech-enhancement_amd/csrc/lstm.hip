@@ -355,6 +355,27 @@ __global__ __launch_bounds__(4 * H) void lstm_bwd_kernel(LstmArgs a) {
 // ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
+// acc0 / acc1 += w[q] * (v[2q], v[2q+1]) for q even / odd, v = the H floats at
+// src (LDS), read as 16-B broadcast loads (every lane the same address).
+// Measured alternatives (FRCRN size, isolated, fwd / bwd per launch): v_readlane
+// into SGPR operands 939 / 837 us; a k-split matvec (4 rows x 32 columns per
+// lane, a quarter of the LDS->VGPR traffic) 696 us fwd; whole cells per wave
+// (gates met by shuffles, one barrier per step) 805 us fwd; this form 733 / 736.
+template <int H>
+__device__ __forceinline__ void matvec_step(const f32x2 (&w)[H / 2], const float* src, f32x2& acc0, f32x2& acc1) {
+  const f32x4* hv = reinterpret_cast<const f32x4*>(src);
+#pragma unroll
+  for (int c0 = 0; c0 < H / 4; c0 += 8) {   // chunks of 8 loads: bounded live registers
+#pragma unroll
+    for (int q4 = c0; q4 < c0 + 8; ++q4) {
+      const f32x4 v = hv[q4];
+      acc0 = __builtin_elementwise_fma(w[2 * q4], f32x2{v.x, v.y}, acc0);
+      acc1 = __builtin_elementwise_fma(w[2 * q4 + 1], f32x2{v.z, v.w}, acc1);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 template <int H, int BS>
 __global__ __launch_bounds__(4 * H) void lstm_fwd_lds_kernel(LstmArgs a) {
   constexpr int G = 4 * H;
@@ -398,17 +419,7 @@ __global__ __launch_bounds__(4 * H) void lstm_fwd_lds_kernel(LstmArgs a) {
 #pragma unroll
     for (int b = 0; b < BS; ++b) {
       f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
-      const f32x4* hv = reinterpret_cast<const f32x4*>(&sh[b][0]);
-#pragma unroll
-      for (int c0 = 0; c0 < H / 4; c0 += 8) {   // chunks of 8 loads: bounded live registers
-#pragma unroll
-        for (int q4 = c0; q4 < c0 + 8; ++q4) {
-          const f32x4 v = hv[q4];
-          acc0 = __builtin_elementwise_fma(w[2 * q4], f32x2{v.x, v.y}, acc0);
-          acc1 = __builtin_elementwise_fma(w[2 * q4 + 1], f32x2{v.z, v.w}, acc1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      matvec_step<H>(w, &sh[b][0], acc0, acc1);
       z[b] = xs[b] + ((acc0.x + acc0.y) + (acc1.x + acc1.y));
     }
     float v[BS];
@@ -510,17 +521,7 @@ __global__ __launch_bounds__(4 * H) void lstm_bwd_lds_kernel(LstmArgs a) {
 #pragma unroll
     for (int b = 0; b < BS; ++b) {
       f32x2 acc0 = f32x2{0.f, 0.f}, acc1 = f32x2{0.f, 0.f};
-      const f32x4* gv = reinterpret_cast<const f32x4*>(&sdg[b][rq * H]);
-#pragma unroll
-      for (int c0 = 0; c0 < H / 4; c0 += 8) {   // chunks of 8 loads: bounded live registers
-#pragma unroll
-        for (int p4 = c0; p4 < c0 + 8; ++p4) {
-          const f32x4 v = gv[p4];
-          acc0 = __builtin_elementwise_fma(w[2 * p4], f32x2{v.x, v.y}, acc0);
-          acc1 = __builtin_elementwise_fma(w[2 * p4 + 1], f32x2{v.z, v.w}, acc1);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      matvec_step<H>(w, &sdg[b][rq * H], acc0, acc1);
       sp[rq][b][k] = (acc0.x + acc0.y) + (acc1.x + acc1.y);
     }
     __syncthreads();
@@ -547,7 +548,9 @@ constexpr int kBS = 2;
 template <int H>
 int launch(bool bwd, const LstmArgs& a, int L, hipStream_t st) {
   dim3 grid((a.B + kBS - 1) / kBS, L);
-  // SEHIP_LSTM_LDS=0: the scalar-load (global round trip) forms; read once
+  // SEHIP_LSTM_LDS=0: the scalar-load (global round trip) forms; read once.
+  // Isolated at FRCRN size (tools/gpu_lstm_modes.sh): fwd / bwd 1060 / 987 us
+  // (scalar loads) vs 733 / 736 us (LDS)
   static const bool lds = [] {
     const char* e = std::getenv("SEHIP_LSTM_LDS");
     return !(e && e[0] == '0');
