@@ -1529,14 +1529,25 @@ extern "C" int se_conv2d_bwd_data(const se_conv2d_desc* d, const float* dy, cons
 
 namespace {
 
+// SEHIP_WGRAD_NB=1 keeps the split-fp16 weight-grad on 128 x 128 tiles where
+// 128 x 256 ones fit (the default, N % 256 == 0).
+int wgrad_nb() {
+  static const int v = [] {
+    const char* e = std::getenv("SEHIP_WGRAD_NB");
+    return e && std::atoi(e) == 1 ? 1 : 2;
+  }();
+  return v;
+}
+
 // 1-D grid of wgrad_x3_kernel over its tile space; SEHIP_WGRAD_WG caps the
 // workgroup count (a persistent grid that leaves CUs to the main stream).
-dim3 x3_wgrad_grid(WgradArgs& a, const WgradPlan& w) {
+// nb: 128-row D blocks per workgroup (wgrad_x3_kernel NB).
+dim3 x3_wgrad_grid(WgradArgs& a, const WgradPlan& w, int nb = 1) {
   static const int cap = [] {
     const char* e = std::getenv("SEHIP_WGRAD_WG");
     return e ? std::max(0, std::atoi(e)) : 0;
   }();
-  a.vk = w.c.Kp / 128; a.vn = w.Np / 128; a.vs = w.splits;
+  a.vk = w.c.Kp / 128; a.vn = w.Np / (128 * nb); a.vs = w.splits;
   const int tiles = a.vk * a.vn * a.vs;
   return dim3((unsigned)(cap > 0 ? std::min(tiles, ((cap + 7) / 8) * 8) : tiles));
 }
@@ -1649,6 +1660,12 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     dim3 grid(w.c.Kp / 128, 1, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
+  } else if (f16 && w.Np % 256 == 0 && wgrad_nb() == 2) {   // 128 x 256 tiles, 8 waves
+    const dim3 grid = x3_wgrad_grid(a, w, 2);
+    const dim3 blk(2 * kThreads);
+    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2>), grid, blk, 0, st, a);
+    else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 2>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true, 2>), grid, blk, 0, st, a);
   } else if (f16) {
     const dim3 grid = x3_wgrad_grid(a, w);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true>), grid, dim3(kThreads), 0, st, a);

@@ -645,16 +645,24 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 
 // DJ: D is the decoder skip join (WgradArgs::D2, a transposed conv's input).
 // F16: scaled split-fp16 operands (SE_MATH_F16X3; a.amax_g / a.amax_d).
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false>
-__global__ void __launch_bounds__(kThreads, SEHIP_WGRAD_OCC)
+// NB: 128-row D blocks per workgroup (tile 128 k x 128 NB n, 4 NB waves of
+// 64 x 64). With NB = 2 the gathered G tile of a step is loaded and split once
+// for 256 output columns (a thread stages 8 G rows and 16 D rows instead of
+// 16 + 16), a quarter fewer loads and splits per MFMA; every output keeps its
+// m-split and its order of positions, so the slabs are bit-identical.
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1>
+__global__ void __launch_bounds__(kThreads * NB, NB == 1 ? SEHIP_WGRAD_OCC : 1)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
+  static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
-  constexpr int BKO = 128, BNO = 128, WNn = 2, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
-  constexpr int RJ = 16;                     // rows per thread per operand
+  constexpr int BKO = 128, BNO = 128 * NB, WNn = 2 * NB, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
+  constexpr int RJ = 16;                     // D rows per thread
+  constexpr int RJG = 16 / NB;               // G rows per thread
   constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
-  __shared__ __attribute__((aligned(16))) unsigned char sm[2][4 * PLANE];   // G hi, G lo, D hi, D lo
+  // G hi, G lo, then per 128-row D block: D hi, D lo
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 + 2 * NB) * PLANE];
   __shared__ int4 sK[BKO];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -672,7 +680,8 @@ wgrad_x3_kernel(const WgradArgs a) {
   const long long HiWi = (long long)a.Hi * a.Wi;
   const long long QQ = (long long)a.Qh * a.Qw;
   const int ml = lane & 31, lr = lane >> 5;
-  const int rbase = 32 * wave + RJ * lr;     // this thread's first G row / D row
+  const int rbase = 32 * wave + RJ * lr;     // this thread's first D row
+  const int rbase_g = (32 / NB) * wave + RJG * lr;   // ... and first G row
 
   for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
   __syncthreads();
@@ -693,7 +702,7 @@ wgrad_x3_kernel(const WgradArgs a) {
     cqh = r / a.Qw;
     cqw = r - cqh * a.Qw;
   }
-  struct Stage { float rg[RJ], rd[RJ]; };
+  struct Stage { float rg[RJG], rd[RJ]; };
   Stage st0, st1;
   auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
     const unsigned long long v = (unsigned long long)p;
@@ -765,19 +774,19 @@ wgrad_x3_kernel(const WgradArgs a) {
     if constexpr (TU) {
       const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
       const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      const int vg = ok ? (int)(((long long)rb * a.Cg * HiWi + (long long)(cbase + RJ * lr) * HiWi +
+      const int vg = ok ? (int)(((long long)rb * a.Cg * HiWi + (long long)(cbase + RJG * lr) * HiWi +
                                  (long long)hi * a.Wi + wi) * 4) : (int)0x80000000;
       const int gs = (int)(HiWi * 4);
 #pragma unroll
-      for (int j = 0; j < RJ; ++j)
+      for (int j = 0; j < RJG; ++j)
         S.rg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-            rg_src, vg, (32 * wave + j) * gs, 0));
+            rg_src, vg, ((32 / NB) * wave + j) * gs, 0));
     } else {
       const int hb = cqh * a.sh, wb = cqw * a.sw;
       const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
 #pragma unroll
-      for (int j = 0; j < RJ; ++j) {
-        const int4 e = sK[rbase + j];
+      for (int j = 0; j < RJG; ++j) {
+        const int4 e = sK[rbase_g + j];
         const int hi = hb + e.y, wi = wb + e.z;
         const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
         S.rg[j] = *(ok ? a.X + xb + e.x : a.zero);
@@ -790,23 +799,27 @@ wgrad_x3_kernel(const WgradArgs a) {
   };
   auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
     unsigned char* base = sm[buf];
+    unsigned char* dbase = base + (2 + 2 * (rbase >> 7)) * PLANE;   // this thread's D block
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       u32x4 GH, GL, DH, DL;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         unsigned h, l;
-        split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
-        GH[e] = h; GL[e] = l;
+        if (q < RJG / 8) {
+          split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
+          GH[e] = h; GL[e] = l;
+        }
         split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
         DH[e] = h; DL[e] = l;
       }
-      const int off = wx3_off(ml, rbase / 8 + q);
-      *reinterpret_cast<u32x4*>(base + 0 * PLANE + off) = GH;
-      *reinterpret_cast<u32x4*>(base + 2 * PLANE + off) = DH;
-      if constexpr (PL == 2) {
-        *reinterpret_cast<u32x4*>(base + 1 * PLANE + off) = GL;
-        *reinterpret_cast<u32x4*>(base + 3 * PLANE + off) = DL;
+      const int offd = wx3_off(ml, (rbase & 127) / 8 + q);
+      *reinterpret_cast<u32x4*>(dbase + offd) = DH;
+      if constexpr (PL == 2) *reinterpret_cast<u32x4*>(dbase + PLANE + offd) = DL;
+      if (q < RJG / 8) {
+        const int offg = wx3_off(ml, rbase_g / 8 + q);
+        *reinterpret_cast<u32x4*>(base + 0 * PLANE + offg) = GH;
+        if constexpr (PL == 2) *reinterpret_cast<u32x4*>(base + 1 * PLANE + offg) = GL;
       }
     }
   };
@@ -843,7 +856,8 @@ wgrad_x3_kernel(const WgradArgs a) {
 #pragma unroll
         for (int i = 0; i < RK; ++i) ga[i][p] = frag(base + p * PLANE, wk * TK + 32 * i, 16 * ks);
 #pragma unroll
-        for (int j = 0; j < RN; ++j) gb[j][p] = frag(base + (2 + p) * PLANE, wnn * TN + 32 * j, 16 * ks);
+        for (int j = 0; j < RN; ++j)
+          gb[j][p] = frag(base + (2 + 2 * (wnn >> 1) + p) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
       }
 #pragma unroll
       for (int t = 0; t < TERMS; ++t)
