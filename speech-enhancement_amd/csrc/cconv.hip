@@ -1668,8 +1668,10 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true, 2>), grid, blk, 0, st, a);
   } else if (f16) {
     const dim3 grid = x3_wgrad_grid(a, w);
+    const bool kpad = (w.c.taps.n * w.Cg) % 128 != 0;   // e.g. a first conv: K = 10 taps x 2
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true>), grid, dim3(kThreads), 0, st, a);
+    else if (kpad) hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true, 1, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true>), grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.math == SE_MATH_BF16X3) {
     const dim3 grid = x3_wgrad_grid(a, w);

@@ -650,7 +650,8 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // for 256 output columns (a thread stages 8 G rows and 16 D rows instead of
 // 16 + 16), a quarter fewer loads and splits per MFMA; every output keeps its
 // m-split and its order of positions, so the slabs are bit-identical.
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1>
+// KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false>
 __global__ void __launch_bounds__(kThreads * NB, NB == 1 ? SEHIP_WGRAD_OCC : 1)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
@@ -680,6 +681,14 @@ wgrad_x3_kernel(const WgradArgs a) {
   const long long HiWi = (long long)a.Hi * a.Wi;
   const long long QQ = (long long)a.Qh * a.Qw;
   const int ml = lane & 31, lr = lane >> 5;
+  // valid k rows of this tile (k < ntaps * Cg; the rest is Kp padding, e.g.
+  // 108 of 128 in a first conv with Cg = 2): a wave skips the loads, splits,
+  // fragment reads and MFMAs of 32-row blocks that hold only padding (their
+  // slab rows stay 0), wave-uniform; only in the KP instantiation (the branches
+  // cost the full tiles their MFMA interleave: 627 vs 629 utt/s when always on)
+  const int kv = KP ? min(BKO, a.ntaps * a.Cg - k0) : BKO;
+  const int kvw = kv - wk * TK;                       // ... of this wave's 64 MFMA rows
+  const bool gact = (32 / NB) * wave < kv;            // this wave stages some valid G row
   const int rbase = 32 * wave + RJ * lr;     // this thread's first D row
   const int rbase_g = (32 / NB) * wave + RJG * lr;   // ... and first G row
 
@@ -771,7 +780,10 @@ wgrad_x3_kernel(const WgradArgs a) {
       vd = dok ? (int)(((long long)rb * a.N * QQ + (long long)(n0 + RJ * lr) * QQ +
                         (long long)cqh * a.Qw + cqw) * 4) : (int)0x80000000;
     }
-    if constexpr (TU) {
+    if (KP && !gact) {
+#pragma unroll
+      for (int j = 0; j < RJG; ++j) S.rg[j] = 0.f;
+    } else if constexpr (TU) {
       const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
       const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
       const int vg = ok ? (int)(((long long)rb * a.Cg * HiWi + (long long)(cbase + RJG * lr) * HiWi +
@@ -816,7 +828,7 @@ wgrad_x3_kernel(const WgradArgs a) {
       const int offd = wx3_off(ml, (rbase & 127) / 8 + q);
       *reinterpret_cast<u32x4*>(dbase + offd) = DH;
       if constexpr (PL == 2) *reinterpret_cast<u32x4*>(dbase + PLANE + offd) = DL;
-      if (q < RJG / 8) {
+      if (q < RJG / 8 && (!KP || gact)) {
         const int offg = wx3_off(ml, rbase_g / 8 + q);
         *reinterpret_cast<u32x4*>(base + 0 * PLANE + offg) = GH;
         if constexpr (PL == 2) *reinterpret_cast<u32x4*>(base + 1 * PLANE + offg) = GL;
@@ -854,7 +866,8 @@ wgrad_x3_kernel(const WgradArgs a) {
 #pragma unroll
       for (int p = 0; p < PL; ++p) {
 #pragma unroll
-        for (int i = 0; i < RK; ++i) ga[i][p] = frag(base + p * PLANE, wk * TK + 32 * i, 16 * ks);
+        for (int i = 0; i < RK; ++i)
+          if (!KP || 32 * i < kvw) ga[i][p] = frag(base + p * PLANE, wk * TK + 32 * i, 16 * ks);
 #pragma unroll
         for (int j = 0; j < RN; ++j)
           gb[j][p] = frag(base + (2 + 2 * (wnn >> 1) + p) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
@@ -863,10 +876,11 @@ wgrad_x3_kernel(const WgradArgs a) {
       for (int t = 0; t < TERMS; ++t)
 #pragma unroll
         for (int i = 0; i < RK; ++i)
+          if (!KP || 32 * i < kvw)
 #pragma unroll
-          for (int j = 0; j < RN; ++j)
-            acc[i][j] = mfma_32x32x16<F16>(__builtin_bit_cast(u32x4, ga[i][t == 2 ? 1 : 0]),
-                                           __builtin_bit_cast(u32x4, gb[j][t == 1 ? 1 : 0]), acc[i][j]);
+            for (int j = 0; j < RN; ++j)
+              acc[i][j] = mfma_32x32x16<F16>(__builtin_bit_cast(u32x4, ga[i][t == 2 ? 1 : 0]),
+                                             __builtin_bit_cast(u32x4, gb[j][t == 1 ? 1 : 0]), acc[i][j]);
     }
   };
   auto interleave = [&]() __attribute__((always_inline)) {
