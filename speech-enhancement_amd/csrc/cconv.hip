@@ -1539,15 +1539,26 @@ int wgrad_nb() {
   return v;
 }
 
+// SEHIP_WGRAD_KB=2 runs the N = 128 split-fp16 weight-grads on 256 x 128 tiles
+// where Kp % 256 == 0 (bit-identical; measured 612.7 / 614.2 vs 617.8 / 614.9
+// utt/s same box, so 128 x 128 stays the default).
+int wgrad_kb() {
+  static const int v = [] {
+    const char* e = std::getenv("SEHIP_WGRAD_KB");
+    return e && std::atoi(e) == 2 ? 2 : 1;
+  }();
+  return v;
+}
+
 // 1-D grid of wgrad_x3_kernel over its tile space; SEHIP_WGRAD_WG caps the
 // workgroup count (a persistent grid that leaves CUs to the main stream).
 // nb: 128-row D blocks per workgroup (wgrad_x3_kernel NB).
-dim3 x3_wgrad_grid(WgradArgs& a, const WgradPlan& w, int nb = 1) {
+dim3 x3_wgrad_grid(WgradArgs& a, const WgradPlan& w, int nb = 1, int kb = 1) {
   static const int cap = [] {
     const char* e = std::getenv("SEHIP_WGRAD_WG");
     return e ? std::max(0, std::atoi(e)) : 0;
   }();
-  a.vk = w.c.Kp / 128; a.vn = w.Np / (128 * nb); a.vs = w.splits;
+  a.vk = w.c.Kp / (128 * kb); a.vn = w.Np / (128 * nb); a.vs = w.splits;
   const int tiles = a.vk * a.vn * a.vs;
   return dim3((unsigned)(cap > 0 ? std::min(tiles, ((cap + 7) / 8) * 8) : tiles));
 }
@@ -1666,6 +1677,9 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2>), grid, blk, 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 2>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true, 2>), grid, blk, 0, st, a);
+  } else if (f16 && !jn && tu && w.Np == 128 && w.c.Kp % 256 == 0 && wgrad_kb() == 2) {   // 256 x 128 tiles
+    const dim3 grid = x3_wgrad_grid(a, w, 1, 2);
+    hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 1, false, 2>), grid, dim3(2 * kThreads), 0, st, a);
   } else if (f16) {
     const dim3 grid = x3_wgrad_grid(a, w);
     const bool kpad = (w.c.taps.n * w.Cg) % 128 != 0;   // e.g. a first conv: K = 10 taps x 2

@@ -650,20 +650,24 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // for 256 output columns (a thread stages 8 G rows and 16 D rows instead of
 // 16 + 16), a quarter fewer loads and splits per MFMA; every output keeps its
 // m-split and its order of positions, so the slabs are bit-identical.
+// KB: the same with two 128-row G blocks (tile 256 k x 128 n, 8 waves): the D
+// tile of a step is staged once for two taps (a thread stages 16 G rows and 8
+// D rows); for N = 128 (the encoder's weight-grads, 10 k-tiles per split).
 // KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false>
-__global__ void __launch_bounds__(kThreads * NB, NB == 1 ? SEHIP_WGRAD_OCC : 1)
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int KB = 1>
+__global__ void __launch_bounds__(kThreads * NB * KB, NB * KB == 1 ? SEHIP_WGRAD_OCC : 1)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
-  static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
+  static_assert(NB * KB <= 2, "one or two 128-row D blocks, or two G blocks");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
-  constexpr int BKO = 128, BNO = 128 * NB, WNn = 2 * NB, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
-  constexpr int RJ = 16;                     // D rows per thread
+  constexpr int BKO = 128 * KB, BNO = 128 * NB, WNn = 2 * NB, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
+  constexpr int RJ = 16 / KB;                // D rows per thread
   constexpr int RJG = 16 / NB;               // G rows per thread
   constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
-  // G hi, G lo, then per 128-row D block: D hi, D lo
-  __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 + 2 * NB) * PLANE];
+  // per 128-row G block: G hi, G lo; then per 128-row D block: D hi, D lo
+  constexpr int DPL = 2 * KB;                // first D plane
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 * KB + 2 * NB) * PLANE];
   __shared__ int4 sK[BKO];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -689,8 +693,9 @@ wgrad_x3_kernel(const WgradArgs a) {
   const int kv = KP ? min(BKO, a.ntaps * a.Cg - k0) : BKO;
   const int kvw = kv - wk * TK;                       // ... of this wave's 64 MFMA rows
   const bool gact = (32 / NB) * wave < kv;            // this wave stages some valid G row
-  const int rbase = 32 * wave + RJ * lr;     // this thread's first D row
-  const int rbase_g = (32 / NB) * wave + RJG * lr;   // ... and first G row
+  const int rbase = (32 / KB) * wave + RJ * lr;     // this thread's first D row
+  const int rbase_g = (32 / NB) * wave + RJG * lr;  // ... and first G row
+  const int gblk = ((32 / NB) * wave) >> 7;         // G block of this wave's rows (wave-uniform)
 
   for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
   __syncthreads();
@@ -730,8 +735,8 @@ wgrad_x3_kernel(const WgradArgs a) {
   if constexpr (DJ)
     rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.D2 + (long long)bfirst * dcpb * QQ2), (short)0,
                                                 0x7FFFFFFF, 0x00020000);
-  const int4 tap_e = sK[0];
-  const int cbase = k0 % a.Cg;
+  const int4 tap_e = sK[128 * gblk];                // TU: one tap per 128-row block
+  const int cbase = (k0 + 128 * gblk) % a.Cg;
   const bool one_wrap = a.Qw >= BMR;
   auto advance = [&]() __attribute__((always_inline)) {
     if (one_wrap) {
@@ -760,12 +765,12 @@ wgrad_x3_kernel(const WgradArgs a) {
     // Np-padded tail; tail rows read 0 through an out-of-range voffset (they
     // must not be read: past the last batch item they leave the allocation).
     const bool dok = mv & (n0 + rbase < a.N);
-    int vd, ds = (int)(QQ * 4), srow = 32 * wave;
+    int vd, ds = (int)(QQ * 4), srow = (32 / KB) * wave;
     __amdgpu_buffer_rsrc_t rdr = rd_src;
     if constexpr (DJ) {
       // joined D: chunks [x_re, s_re, x_im, s_im] of djh rows; a wave's 32 rows
       // lie in one chunk (djh % 32 == 0)
-      const int nb = n0 + 32 * wave;
+      const int nb = n0 + (32 / KB) * wave;
       const int q = nb / a.djh;
       const bool from_x = (q & 1) == 0;
       const int cr = (q >> 1) * a.djh + (nb - q * a.djh) + RJ * lr;   // row in its source
@@ -792,7 +797,7 @@ wgrad_x3_kernel(const WgradArgs a) {
 #pragma unroll
       for (int j = 0; j < RJG; ++j)
         S.rg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-            rg_src, vg, ((32 / NB) * wave + j) * gs, 0));
+            rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs, 0));
     } else {
       const int hb = cqh * a.sh, wb = cqw * a.sw;
       const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
@@ -811,7 +816,8 @@ wgrad_x3_kernel(const WgradArgs a) {
   };
   auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
     unsigned char* base = sm[buf];
-    unsigned char* dbase = base + (2 + 2 * (rbase >> 7)) * PLANE;   // this thread's D block
+    unsigned char* dbase = base + (DPL + 2 * (rbase >> 7)) * PLANE;   // this thread's D block
+    unsigned char* gbase = base + 2 * gblk * PLANE;                    // ... and G block
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       u32x4 GH, GL, DH, DL;
@@ -822,16 +828,20 @@ wgrad_x3_kernel(const WgradArgs a) {
           split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
           GH[e] = h; GL[e] = l;
         }
-        split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
-        DH[e] = h; DL[e] = l;
+        if (q < RJ / 8) {
+          split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
+          DH[e] = h; DL[e] = l;
+        }
       }
-      const int offd = wx3_off(ml, (rbase & 127) / 8 + q);
-      *reinterpret_cast<u32x4*>(dbase + offd) = DH;
-      if constexpr (PL == 2) *reinterpret_cast<u32x4*>(dbase + PLANE + offd) = DL;
+      if (q < RJ / 8) {
+        const int offd = wx3_off(ml, (rbase & 127) / 8 + q);
+        *reinterpret_cast<u32x4*>(dbase + offd) = DH;
+        if constexpr (PL == 2) *reinterpret_cast<u32x4*>(dbase + PLANE + offd) = DL;
+      }
       if (q < RJG / 8 && (!KP || gact)) {
-        const int offg = wx3_off(ml, rbase_g / 8 + q);
-        *reinterpret_cast<u32x4*>(base + 0 * PLANE + offg) = GH;
-        if constexpr (PL == 2) *reinterpret_cast<u32x4*>(base + 1 * PLANE + offg) = GL;
+        const int offg = wx3_off(ml, (rbase_g & 127) / 8 + q);
+        *reinterpret_cast<u32x4*>(gbase + offg) = GH;
+        if constexpr (PL == 2) *reinterpret_cast<u32x4*>(gbase + PLANE + offg) = GL;
       }
     }
   };
@@ -867,10 +877,11 @@ wgrad_x3_kernel(const WgradArgs a) {
       for (int p = 0; p < PL; ++p) {
 #pragma unroll
         for (int i = 0; i < RK; ++i)
-          if (!KP || 32 * i < kvw) ga[i][p] = frag(base + p * PLANE, wk * TK + 32 * i, 16 * ks);
+          if (!KP || 32 * i < kvw)
+            ga[i][p] = frag(base + (2 * (wk >> 1) + p) * PLANE, (wk & 1) * TK + 32 * i, 16 * ks);
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          gb[j][p] = frag(base + (2 + 2 * (wnn >> 1) + p) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
+          gb[j][p] = frag(base + (DPL + 2 * (wnn >> 1) + p) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
       }
 #pragma unroll
       for (int t = 0; t < TERMS; ++t)
