@@ -148,3 +148,20 @@ def test_bf16x3_small_channels_match_golden(i, case, gpu_device):
              kw["stride"], "bf16x3")
     for key in ("y", "dx", "dwr", "dwi"):
         assert rel_l2(r[key].numpy(), g[f"{name}_{key}"]) < 1e-5, (name, key)
+
+
+@pytest.mark.parametrize("n,off,complex_w", [(81920, 0, True), (81920, 0, False), (40963, 0, True),
+                                             (40960, 1, True), (7, 0, True), (1 << 20, 0, True)])
+def test_amax_weights_exact(n, off, complex_w):
+    """se_amax_weights (the f16x3 weight scale source): max |wr|, |wi| exactly,
+    on the 16-B vector path, ragged tails and unaligned pointers."""
+    from sehip import _native as N
+    g = torch.Generator().manual_seed(n + off)
+    wr = (torch.randn(n + off, generator=g) * 3).cuda()[off:]
+    wi = (torch.randn(n + off, generator=g) * 5).cuda()[off:] if complex_w else None
+    wr[n // 2] = -17.5   # the maximum magnitude, negative
+    out = torch.full((1,), -1.0, device="cuda")
+    N.check(N.lib().se_amax_weights(wr.data_ptr(), n, N.ptr(wi), out.data_ptr(), N.stream_of(wr)),
+            "se_amax_weights")
+    ref = wr.abs().max() if wi is None else torch.maximum(wr.abs().max(), wi.abs().max())
+    assert out.item() == ref.item()
