@@ -655,7 +655,7 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // D rows); for N = 128 (the encoder's weight-grads, 10 k-tiles per split).
 // KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
 template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int KB = 1>
-__global__ void __launch_bounds__(kThreads * NB * KB, NB * KB == 1 ? SEHIP_WGRAD_OCC : 1)
+__global__ void __launch_bounds__(kThreads * NB * KB, SEHIP_WGRAD_OCC)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
