@@ -250,11 +250,12 @@ def test_frcrn_b16_4s_train_forward_vs_oracle(gpu_device):
 def test_real_conv_models_backward_vs_oracle(i, gpu_device):
     """CARN / CRN on the HIP kernels (real convs on the conv GEMMs, BatchNorm2d +
     PReLU / ELU fused, the 512- / 1024-wide LSTMs on the wide recurrence): train-mode
-    forward + backward against the CPU oracle on the golden input (loss = <wav, r>).
-    The same modules' GPU (MIOpen) backward is itself not CPU-exact (CRN:
-    nn.BatchNorm2d's input gradient at decoder layer 2 is 4.5e-4 off the CPU,
-    tools/crn_act_diag.py), so the gradient gate is 3x the error of the oracle's own
-    modules run on the GPU, floored at 1e-3."""
+    forward + backward on the golden input (loss = <wav, r>) against an fp64 CPU run of
+    the oracle. The gradient gate is the fp32 CPU oracle's own error vs fp64 (measured:
+    HIP 5.4e-7 / 1.4e-6 vs CPU fp32 8.5e-7 / 2.6e-6, profiles/r2_grad64_real_models.log;
+    torch on the GPU is 1.8e-2 off at CRN, so it no longer sets the bar): all
+    parameters together within 2x of it, and the worst single parameter within 5x of
+    the CPU's worst."""
     from oracle import models as O
     name, ctor = _models()[i]
     octor = {3: lambda: O.CARN(320, 160, 512), 5: lambda: O.CRN(320, 160, 320)}[i]
@@ -262,22 +263,28 @@ def test_real_conv_models_backward_vs_oracle(i, gpu_device):
     x = torch.from_numpy(g["x"])
     r = None
 
-    def grads(m, dev):
+    def grads(m, dev, dtype=torch.float32):
         nonlocal r
-        _, w = m(x.to(dev))
+        m = m.to(dev).to(dtype).train()
+        _, w = m(x.to(dev, dtype))
         if r is None:
             r = torch.randn(w.shape, generator=torch.Generator().manual_seed(3))
-        (w * r.to(dev)).sum().backward()
-        return w.detach().cpu(), {n: p.grad.detach().cpu() for n, p in m.named_parameters()
-                                  if p.grad is not None}
+        (w * r.to(dev, dtype)).sum().backward()
+        return w.detach().double().cpu(), {n: p.grad.detach().double().cpu()
+                                           for n, p in m.named_parameters() if p.grad is not None}
 
-    wo, go = grads(paramfill.fill_(octor(), seed=20 + i).train(), "cpu")
-    _, gt = grads(paramfill.fill_(octor(), seed=20 + i).cuda().train(), "cuda")   # torch on the GPU
-    wh, gh = grads(paramfill.fill_(ctor(), seed=20 + i).cuda().train(), "cuda")   # sehip
+    wo, g64 = grads(paramfill.fill_(octor(), seed=20 + i), "cpu", torch.float64)
+    _, g32 = grads(paramfill.fill_(octor(), seed=20 + i), "cpu")                 # fp32 oracle
+    wh, gh = grads(paramfill.fill_(ctor(), seed=20 + i), "cuda")                 # sehip
     assert rel_l2(wh.numpy(), wo.numpy()) < TOL
-    names = sorted(go)
+    names = sorted(g64)
+    assert sorted(gh) == names
     cat = lambda d: torch.cat([d[n].flatten() for n in names])
-    b = cat(go)
+    b = cat(g64)
     e_hip = ((cat(gh) - b).norm() / b.norm()).item()
-    e_torch = ((cat(gt) - b).norm() / b.norm()).item()
-    assert e_hip < max(3 * e_torch, 1e-3), (name, e_hip, e_torch)
+    e_cpu = ((cat(g32) - b).norm() / b.norm()).item()
+    per = lambda d: max(((d[n] - g64[n]).norm() / (g64[n].norm() + 1e-300)).item() for n in names)
+    p_hip, p_cpu = per(gh), per(g32)
+    print(f"{name}: grads vs fp64 hip {e_hip:.2e} cpu-fp32 {e_cpu:.2e}; worst param {p_hip:.2e} / {p_cpu:.2e}")
+    assert e_hip < 2 * e_cpu and e_hip < 1e-5, (name, e_hip, e_cpu)
+    assert p_hip < 5 * p_cpu and p_hip < 1e-3, (name, p_hip, p_cpu)
