@@ -119,6 +119,9 @@ struct GatherArgs {
   int ntaps, kblk;
   int toffh[kMaxTaps], toffw[kMaxTaps];
   int pp_pair;         // ping-pong gather: 0 = waves 4-7 late, 1 = odd waves late
+  // merged stride-phase classes (merge_h_phases): output columns n' >= mrg_np are
+  // channel n' - mrg_np of output row 1 + Sh * qh (rows >= Ho dropped); 0 = off
+  int mrg_np;
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -851,6 +854,10 @@ struct TapList {
   int n;
   int ti[kMaxTaps], tj[kMaxTaps];     // kernel (i, j) of each tap
   int offh[kMaxTaps], offw[kMaxTaps]; // input offsets
+  // merged stride-phase classes (merge_h_phases): columns [mrg_np, 2 mrg_np) are
+  // phase 1, whose kernel row of tap t is ti2[t]; a row of -1 is a zero weight
+  int mrg_np;
+  int ti2[kMaxTaps];
 };
 
 // Builds Wp[k = t*Cg + c][n] (zero rows/cols up to Kp x ldw) and ktab[k].
@@ -974,6 +981,7 @@ struct Dim1 {   // one spatial dim of one class
   int p, S, Q, s;
   int ntaps;
   int tap[16], off[16];
+  int tap2[16];   // merged classes: phase-1 kernel index per offset (-1: none)
 };
 
 // strided gather: out q in [0, Lout), in = q*stride + i*dil - pad
@@ -1004,6 +1012,7 @@ struct ClassPlan {
   Dim1 h, w;
   TapList taps;
   int K, Kp;
+  int mrg;        // 1: two h phases merged along the columns (merge_h_phases)
 };
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
@@ -1014,6 +1023,7 @@ static void finish_plan(ClassPlan& c, int Cg) {
   for (int a = 0; a < c.h.ntaps; ++a)
     for (int b = 0; b < c.w.ntaps; ++b, ++t) {
       c.taps.ti[t] = c.h.tap[a]; c.taps.tj[t] = c.w.tap[b];
+      c.taps.ti2[t] = c.mrg ? c.h.tap2[a] : -1;
       c.taps.offh[t] = c.h.off[a]; c.taps.offw[t] = c.w.off[b];
     }
   c.K = c.taps.n * Cg;
@@ -1092,6 +1102,59 @@ static std::vector<ClassPlan> plan_pass(const ConvGeom& g, Pass pass) {
       out.push_back(c);
     }
   return out;
+}
+
+// A transposed conv's forward with stride 2 in H and 1 in W has two stride-phase
+// classes (even / odd output rows: FRCRN's decoder, kernel (5, 2): input row
+// offsets {0, -1, -2} and {0, -1}) that gather the same input rows. Merged, they
+// are one class over the union of the offsets with 2 x 128 output columns
+// (phase 0 | phase 1, a zero weight where a phase has no tap at an offset):
+// the gathered activations are loaded and split once for both phases and the
+// GEMM runs on the 256-column (NW = 2) tiles, for 1.2x the MFMA work of the two
+// classes (FRCRN: K = 6 x Cg per column instead of 6 x Cg and 4 x Cg).
+static bool merge_h_phases(const std::vector<ClassPlan>& cls, int Cg, ClassPlan& m) {
+  if (cls.size() != 2) return false;
+  const ClassPlan& c0 = cls[0];
+  const ClassPlan& c1 = cls[1];
+  if (c0.h.S != 2 || c0.h.p != 0 || c1.h.p != 1 || c0.h.s != 1 || c1.h.s != 1) return false;
+  if (c0.w.S != 1 || c1.w.S != 1 || c0.w.p != c1.w.p || c0.w.Q != c1.w.Q || c1.h.Q > c0.h.Q ||
+      c1.h.Q < c0.h.Q - 1)
+    return false;
+  m = ClassPlan{};
+  m.w = c0.w;
+  m.h = c0.h;
+  m.mrg = 1;
+  int n = 0;
+  for (int a = 0; a < c0.h.ntaps; ++a) {
+    m.h.tap[n] = c0.h.tap[a]; m.h.off[n] = c0.h.off[a]; m.h.tap2[n] = -1;
+    for (int b = 0; b < c1.h.ntaps; ++b)
+      if (c1.h.off[b] == c0.h.off[a]) m.h.tap2[n] = c1.h.tap[b];
+    ++n;
+  }
+  for (int b = 0; b < c1.h.ntaps; ++b) {
+    bool seen = false;
+    for (int a = 0; a < c0.h.ntaps; ++a) seen |= c0.h.off[a] == c1.h.off[b];
+    if (seen) continue;
+    if (n >= 16) return false;
+    m.h.tap[n] = -1; m.h.off[n] = c1.h.off[b]; m.h.tap2[n] = c1.h.tap[b];
+    ++n;
+  }
+  m.h.ntaps = n;
+  if (n * m.w.ntaps > kMaxTaps) return false;
+  finish_plan(m, Cg);
+  m.taps.mrg_np = 128;
+  return true;
+}
+
+// SEHIP_FWD_MERGE=1 runs the merged form (merge_h_phases). Off by default: the
+// full GPU suite passes with it (252 tests), but the step measured 616.2 / 617.4
+// vs 624.4 / 622.7 utt/s (same box): the 1.2x MFMA work is not won back.
+static bool fwd_merge_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("SEHIP_FWD_MERGE");
+    return e && std::atoi(e) == 1;
+  }();
+  return v;
 }
 
 static inline int ldw_for(int N) {
@@ -1241,7 +1304,17 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
   const int Ho = (pass == kFwd) ? g.Ho : g.Hi, Wo = (pass == kFwd) ? g.Wo : g.Wi;
   if (ws_bytes < gather_ws_bytes(cls, N)) return SE_E_WORKSPACE;
-  const int ldw = ldw_for(N);
+  int ldw = ldw_for(N);
+  {   // stride-phase classes merged along the columns (split-fp16, 256-column tiles)
+    ClassPlan mp;
+    const bool pk_in = (pass == kFwd ? g.x_packed : g.dy_packed) != nullptr;
+    if (pass == kFwd && g.transposed && g.math == SE_MATH_F16X3 && N > 64 && ldw == 128 && !pk_in &&
+        gemm_nw() == 2 && gemm_bm() != 256 && !gemm_pp() && fwd_merge_on() && merge_h_phases(cls, Cg, mp) &&
+        ws_bytes >= gather_ws_bytes({mp}, 256)) {
+      cls.assign(1, mp);
+      ldw = 256;
+    }
+  }
   WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w};
 
   char* p = align256((char*)ws);
@@ -1329,6 +1402,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
+    a.mrg_np = c.mrg ? c.taps.mrg_np : 0;
     if (jn) {
       a.X2 = jn->x2; a.jh = jn->jh; a.H2 = jn->h2; a.W2 = jn->w2;
       a.Y2 = jn->y2; a.yjh = jn->yjh; a.YH2 = jn->yh2; a.YW2 = jn->yw2;
@@ -1525,6 +1599,11 @@ extern "C" size_t se_conv2d_workspace_size(const se_conv2d_desc* d) {
   ConvGeom g;
   if (geom_of(d, g)) return 0;
   size_t a = gather_ws_bytes(plan_pass(g, kFwd), g.Co);
+  {
+    ClassPlan mp;
+    if (g.transposed && g.Co > 64 && g.Co <= 128 && merge_h_phases(plan_pass(g, kFwd), g.Ci, mp))
+      a = std::max(a, gather_ws_bytes({mp}, 256));
+  }
   size_t b = gather_ws_bytes(plan_pass(g, kData), g.Ci);
   size_t c = wgrad_ws_bytes(plan_wgrad(g));
   return std::max(a, std::max(b, c));

@@ -164,11 +164,15 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
     const int k = (int)(idx % Kp);                    // k fastest: a thread group fills rows
     const int n = (int)(idx / Kp);
     float v = 0.f;
-    if (k < K && n < N) {
+    // merged phases (TapList::mrg_np): column n of phase 1 is channel n - mrg_np
+    const int ph = taps.mrg_np ? n / taps.mrg_np : 0;
+    const int nn = n - ph * taps.mrg_np;
+    if (k < K && nn < N) {
       int t, c;
       split_k(k, Cg, taps.n, kblk, t, c);
-      const int ci = data_grad ? n : c, co = data_grad ? c : n;
-      v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
+      const int ci = data_grad ? nn : c, co = data_grad ? c : nn;
+      const int ti = ph ? taps.ti2[t] : taps.ti[t];
+      if (ti >= 0) v = kernel_value(w, ci, co, ti, taps.tj[t]);
     }
     unsigned short hb, lb;
     if constexpr (F16) {
@@ -570,7 +574,7 @@ gather_x3_kernel(const GatherArgs a) {
   __syncthreads();
   float* sBias = reinterpret_cast<float*>(&sW[0][0]);
   for (int i = tid; i < BN; i += THR) {
-    const int n = n0 + i;
+    const int n = a.mrg_np ? (n0 + i) % a.mrg_np : n0 + i;
     sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   }
   __syncthreads();
@@ -609,6 +613,22 @@ gather_x3_kernel(const GatherArgs a) {
 #pragma unroll
         for (int r2 = 0; r2 < AR; ++r2) yp[(long long)roff(r2) * pl] = acc[i][j][r2];
       }
+      continue;
+    }
+    if (a.mrg_np) {   // merged phases: this wave's 64 columns lie in one phase
+      const int mph = (n0 + wn * TN) / a.mrg_np;
+      const int oh = a.ph + mph + a.Sh * qh;
+      if (oh >= a.Ho) continue;
+      const int nc = n0 + nl0 - mph * a.mrg_np;    // channel of this lane's first column
+      float* yb = a.Y + (long long)b * a.N * HoWo + (long long)oh * a.Wo + (a.pw + a.Sw * qw) +
+                  (long long)nc * HoWo;
+#pragma unroll
+      for (int i = 0; i < QN; ++i)
+#pragma unroll
+        for (int r2 = 0; r2 < AR; ++r2) {
+          const int nl = BLK * i + roff(r2);
+          if (nc + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
+        }
       continue;
     }
     float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
