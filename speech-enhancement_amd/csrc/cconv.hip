@@ -24,6 +24,8 @@
 // contiguous time axis and epilogue stores are 128-B coalesced.
 #include "common.hpp"
 
+#include <mutex>
+
 #include <algorithm>
 #include <cstdlib>
 #include <vector>
@@ -43,7 +45,26 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // selecting after the load: the loaded register then feeds the LDS write
 // directly and the load stays in flight across the MFMA loop.
 constexpr size_t kZeroBytes = 256;
-constexpr size_t kAmaxBytes = 256;   // SE_MATH_F16X3 max |.| slots, zeroed with the zero page
+constexpr size_t kAmaxBytes = 256;   // SE_MATH_F16X3 max |.| slots, zeroed only when a pass fills one
+
+// The zero page lives once per device (allocated and cleared on first use, never
+// written), not in the workspace: a per-call hipMemsetAsync was a fill launch on
+// the caller's stream before every conv pass, and in the backward each such
+// launch waits for a CU slot beside the side-stream weight-grads.
+static const float* zero_page() {
+  static std::mutex mu;
+  static void* pages[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  std::lock_guard<std::mutex> lock(mu);
+  if (!pages[dev]) {
+    void* q = nullptr;
+    if (hipMalloc(&q, kZeroBytes) != hipSuccess) return nullptr;
+    if (hipMemset(q, 0, kZeroBytes) != hipSuccess) { (void)hipFree(q); return nullptr; }
+    pages[dev] = q;
+  }
+  return (const float*)pages[dev];
+}
 
 // ---------------------------------------------------------------------------
 // Gather-GEMM (forward and data-grad)
@@ -950,28 +971,33 @@ __global__ void wgrad_finish_kernel(const UnpackArgs u) {
   }
 }
 
-// Bias grad: db_full[n] = sum over (b, h, w) of dy[b, n, h, w]; then fold.
+// Bias grad: db_full[n] = sum over (b, h, w) of dy[b, n, h, w]; then fold. One
+// block per real channel, or per complex channel pair (n, n + N/2), written
+// directly (no zeroed outputs, no atomics): d(br) = sum(dy_re) + sum(dy_im),
+// d(bi) = -sum(dy_re) + sum(dy_im), the values the two-atomic form produced.
 __global__ void bias_grad_kernel(const float* dy, int B, int N, long long HW, int complex_w,
                                  float* dbr, float* dbi) {
-  const int n = blockIdx.x;  // one block per real output channel (re and im folded below)
+  const int n = blockIdx.x;
   __shared__ float red[kThreads / 64];
-  float s = 0.f;
-  for (int b = 0; b < B; ++b) {
-    const float* p = dy + ((long long)b * N + n) * HW;
-    for (long long i = threadIdx.x; i < HW; i += kThreads) s += p[i];
+  float t[2] = {0.f, 0.f};
+  for (int q = 0; q < (complex_w ? 2 : 1); ++q) {
+    const int ch = n + q * (N / 2);
+    float s = 0.f;
+    for (int b = 0; b < B; ++b) {
+      const float* p = dy + ((long long)b * N + ch) * HW;
+      for (long long i = threadIdx.x; i < HW; i += kThreads) s += p[i];
+    }
+    s = se::wave_sum(s);
+    __syncthreads();   // red is reused by the second channel
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0)
+      for (int i = 0; i < kThreads / 64; ++i) t[q] += red[i];
   }
-  s = se::wave_sum(s);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
-  __syncthreads();
-  if (threadIdx.x == 0) {
-    float t = 0.f;
-    for (int i = 0; i < kThreads / 64; ++i) t += red[i];
-    if (!complex_w) { dbr[n] = t; return; }
-    const int h = N / 2;
-    // d(br) = sum(dy_re) + sum(dy_im); d(bi) = -sum(dy_re) + sum(dy_im)
-    if (n < h) { atomicAdd(&dbr[n], t); atomicAdd(&dbi[n], -t); }
-    else { atomicAdd(&dbr[n - h], t); atomicAdd(&dbi[n - h], t); }
-  }
+  if (threadIdx.x != 0) return;
+  if (!complex_w) { dbr[n] = t[0]; return; }
+  dbr[n] = t[0] + t[1];
+  dbi[n] = -t[0] + t[1];
 }
 
 // ---------------------------------------------------------------------------
@@ -1318,9 +1344,14 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w};
 
   char* p = align256((char*)ws);
-  const float* zero = (const float*)p;
+  const float* zero = zero_page();
+  if (!zero) return SE_E_LAUNCH;
   float* amax_slot = (float*)(p + kZeroBytes);   // [0] weights, [1] gathered tensor
-  (void)hipMemsetAsync(p, 0, kZeroBytes + kAmaxBytes, st);
+  {   // the slots are atomicMax targets of launch_amax: zeroed only if a pass fills one
+    const float* aa = pass == kFwd ? g.x_amax : g.dy_amax;
+    if (g.math == SE_MATH_F16X3 && N > 64 && (!g.w_amax || !aa))
+      (void)hipMemsetAsync(amax_slot, 0, kAmaxBytes, st);
+  }
   p = align256(p + kZeroBytes + kAmaxBytes);
   float* bias_full = nullptr;
   if (pass == kFwd && bias_br) {
@@ -1688,9 +1719,11 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     if (!tu || !split_ok || w.N <= 32 || w.N != 4 * jn->jh) return SE_E_UNSUPPORTED;
   }
   char* p = align256((char*)ws);
-  const float* zero = (const float*)p;
+  const float* zero = zero_page();
+  if (!zero) return SE_E_LAUNCH;
   float* amax_slot = (float*)(p + kZeroBytes);   // [0] x (joined: x and s), [1] dy
-  (void)hipMemsetAsync(p, 0, kZeroBytes + kAmaxBytes, st);
+  if (g.math == SE_MATH_F16X3 && (!g.x_amax || !g.dy_amax))   // launch_amax targets below
+    (void)hipMemsetAsync(amax_slot, 0, kAmaxBytes, st);
   p = align256(p + kZeroBytes + kAmaxBytes);
   float* slab = (float*)p;
   p = align256(p + (size_t)w.splits * w.c.Kp * w.Np * sizeof(float));
@@ -1834,11 +1867,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
 
   if (dbr) {
     const int hco = g.complex_w ? g.Co / 2 : g.Co;
-    if (g.complex_w) {
-      (void)hipMemsetAsync(dbr, 0, sizeof(float) * hco, st);
-      (void)hipMemsetAsync(dbi, 0, sizeof(float) * hco, st);
-    }
-    hipLaunchKernelGGL(bias_grad_kernel, dim3(g.Co), dim3(kThreads), 0, st, dy, g.B, g.Co,
+    hipLaunchKernelGGL(bias_grad_kernel, dim3(hco), dim3(kThreads), 0, st, dy, g.B, g.Co,
                        (long long)g.Ho * g.Wo, g.complex_w, dbr, dbi);
     SE_LAUNCH_CHECK();
   }
