@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 2
+#define SEHIP_ABI_VERSION 3
 
 enum {
   SE_OK = 0,
@@ -159,6 +159,15 @@ typedef struct se_conv2d_desc {
    * and data-grad passes of one conv call share it (the weights do not change
    * between them); NULL = the pass computes it itself (two reductions). */
   const float* w_amax;
+  /* se_conv2d_bwd_data only (ABI 3): 1 = add the input gradient into dx
+   * (dx += dL/dx) instead of overwriting it. For a conv input with a second
+   * consumer whose gradient already sits in dx (FRCRN: an encoder block output
+   * that also feeds a decoder skip): the consumer's CBN backward then reads one
+   * gradient tensor instead of two. Supported on the split GEMM kernels
+   * (SE_MATH_BF16X3 / SE_MATH_BF16 / SE_MATH_F16X3 with more than 64 input
+   * channels, non-joined, fp32 dx); other shapes return SE_E_UNSUPPORTED before
+   * launching anything. */
+  int accumulate_dx;
 } se_conv2d_desc;
 
 enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3,

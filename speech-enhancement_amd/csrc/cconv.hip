@@ -143,6 +143,7 @@ struct GatherArgs {
   // merged stride-phase classes (merge_h_phases): output columns n' >= mrg_np are
   // channel n' - mrg_np of output row 1 + Sh * qh (rows >= Ho dropped); 0 = off
   int mrg_np;
+  int accum;           // data-grad: Y += result (se_conv2d_desc.accumulate_dx)
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -1069,6 +1070,7 @@ struct ConvGeom {
   const void* x_packed;   // SE_MATH_F16X3 CL16 operands from the caller (or nullptr)
   const void* x2_packed;
   const void* dy_packed;
+  int accum;      // se_conv2d_desc.accumulate_dx
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -1086,6 +1088,8 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.x_packed = d->x_packed;
   g.x2_packed = d->x2_packed;
   g.dy_packed = d->dy_packed;
+  g.accum = d->accumulate_dx;
+  if (g.accum != 0 && g.accum != 1) return SE_E_ARG;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16X3) return SE_E_ARG;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
@@ -1330,6 +1334,10 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
   const int Ho = (pass == kFwd) ? g.Ho : g.Hi, Wo = (pass == kFwd) ? g.Wo : g.Wi;
   if (ws_bytes < gather_ws_bytes(cls, N)) return SE_E_WORKSPACE;
+  if (g.accum) {   // dx += result: the split kernels' plain epilogue only (checked before any launch)
+    const bool split = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3) && N > 64;
+    if (pass != kData || jn || !split || g.dy_packed) return SE_E_UNSUPPORTED;
+  }
   int ldw = ldw_for(N);
   {   // stride-phase classes merged along the columns (split-fp16, 256-column tiles)
     ClassPlan mp;
@@ -1434,6 +1442,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
     a.mrg_np = c.mrg ? c.taps.mrg_np : 0;
+    a.accum = g.accum;
     if (jn) {
       a.X2 = jn->x2; a.jh = jn->jh; a.H2 = jn->h2; a.W2 = jn->w2;
       a.Y2 = jn->y2; a.yjh = jn->yjh; a.YH2 = jn->yh2; a.YW2 = jn->yw2;

@@ -638,7 +638,11 @@ gather_x3_kernel(const GatherArgs a) {
 #pragma unroll
       for (int r2 = 0; r2 < AR; ++r2) {
         const int nl = BLK * i + roff(r2);
-        if (full_n || n0 + nl0 + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
+        if (full_n || n0 + nl0 + nl < a.N) {
+          float v = acc[i][j][r2] + sBias[nl0 + nl];
+          if (a.accum) v += yb[(long long)nl * HoWo];   // = the consumer's gy + gy2, same fp32 add
+          yb[(long long)nl * HoWo] = v;
+        }
       }
   }
 }

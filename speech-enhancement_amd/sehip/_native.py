@@ -37,7 +37,8 @@ class ConvDesc(ctypes.Structure):
         "complex_weights", "pad_h_end", "pad_w_end", "math")] + [
         ("x_amax", c_void_p), ("dy_amax", c_void_p),   # SE_MATH_F16X3 scale sources (or NULL)
         ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p),   # CL16 operands (or NULL)
-        ("w_amax", c_void_p)]   # SE_MATH_F16X3 bound of max |w| (or NULL)
+        ("w_amax", c_void_p),   # SE_MATH_F16X3 bound of max |w| (or NULL)
+        ("accumulate_dx", c_int)]   # se_conv2d_bwd_data: dx += dL/dx (ABI 3)
 
 
 _P = c_void_p
