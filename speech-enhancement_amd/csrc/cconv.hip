@@ -1179,12 +1179,9 @@ static bool merge_h_phases(const std::vector<ClassPlan>& cls, int Cg, ClassPlan&
 // SEHIP_FWD_MERGE=1 runs the merged form (merge_h_phases). Off by default: the
 // full GPU suite passes with it (252 tests), but the step measured 616.2 / 617.4
 // vs 624.4 / 622.7 utt/s (same box): the 1.2x MFMA work is not won back.
-static bool fwd_merge_on() {
-  static const bool v = [] {
-    const char* e = std::getenv("SEHIP_FWD_MERGE");
-    return e && std::atoi(e) == 1;
-  }();
-  return v;
+static bool fwd_merge_on() {   // read per call (tests switch it within one process)
+  const char* e = std::getenv("SEHIP_FWD_MERGE");
+  return e && std::atoi(e) == 1;
 }
 
 static inline int ldw_for(int N) {

@@ -165,3 +165,27 @@ def test_amax_weights_exact(n, off, complex_w):
             "se_amax_weights")
     ref = wr.abs().max() if wi is None else torch.maximum(wr.abs().max(), wi.abs().max())
     assert out.item() == ref.item()
+
+
+@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", [l for l in LAYERS if l[1] and l[3] == 128])
+def test_merged_phase_forward_vs_fp64(name, tr, cin, cout, shape, stride, gpu_device, monkeypatch):
+    """SEHIP_FWD_MERGE=1 (opt-in): the two stride-phase classes of the transposed-conv
+    forward run as one class over the union of input-row offsets on 256-column tiles.
+    Its output is bit-identical to the default two-class form (measured) and held to
+    the fp32-class bar against fp64."""
+    from sehip import functional as F
+    m, x, gy, ref = _fp64_ref(name, tr, cin, cout, shape, stride)
+    exact = _hip(F, m, x, gy, tr, stride, "f32")
+    monkeypatch.setenv("SEHIP_FWD_MERGE", "1")
+    merged = _hip(F, m, x, gy, tr, stride, "f16x3")
+    monkeypatch.setenv("SEHIP_FWD_MERGE", "0")
+    plain = _hip(F, m, x, gy, tr, stride, "f16x3")
+    r = ref["y"].numpy()
+    e32, em, ep = (rel_l2(t["y"].numpy(), r) for t in (exact, merged, plain))
+    same = torch.equal(merged["y"], plain["y"])
+    print(f"{name} fwd: f32 {e32:.2e}  f16x3 merged {em:.2e}  two-class {ep:.2e}  bit-identical {same}")
+    assert em < 1e-5 and em <= max(F16_VS_F32 * e32, 1e-7), (name, em, e32)
+    # phase 0 keeps its K order and phase 1 only gains exact zero products: same bits
+    assert same
+    for k in ("dx", "dwr", "dwi"):   # the backward passes do not depend on the knob
+        assert torch.equal(merged[k], plain[k]), k

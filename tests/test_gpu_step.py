@@ -144,3 +144,31 @@ def test_train_step_uses_fused_glue(gpu_device):
     m2 = paramfill.fill_(M.FRCRN(), seed=12).to(gpu_device).train()
     loss = train_step(m2, make_optimizer(m2), x, c)
     assert torch.isfinite(loss)
+
+
+def test_frcrn_fork_gradient_handoff_bit_identical(gpu_device, monkeypatch):
+    """SEHIP_FORK_ACC=1 (opt-in, ABI 3 accumulate_dx): CCBAM's input gradient is handed
+    to the next encoder conv's data-grad, which adds into it in the GEMM epilogue. The
+    FRCRN gradients must equal the default two-tensor form bit for bit (the same fp32
+    add), and the five encoder data-grads must have accumulated."""
+    import paramfill
+    from sehip import functional as F
+    from sehip.losses import SI_SNR_loss
+    from sehip.models import FRCRN
+
+    def grads():
+        m = paramfill.fill_(FRCRN(), seed=9).cuda().train()
+        noisy, clean = (torch.from_numpy(t).cuda() for t in paramfill.structured_pair(2, 16000, seed=60))
+        _, wav = m(noisy)
+        SI_SNR_loss(wav, clean).backward()
+        torch.cuda.synchronize()
+        return {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
+
+    monkeypatch.setenv("SEHIP_FORK_ACC", "0")
+    g0 = grads()
+    monkeypatch.setenv("SEHIP_FORK_ACC", "1")
+    before = F.FORK_ACC_CALLS[0]
+    g1 = grads()
+    assert F.FORK_ACC_CALLS[0] - before == 5
+    bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
+    assert not bad, bad[:6]
