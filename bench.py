@@ -80,11 +80,15 @@ def parse():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch", type=int, default=64, help="utterances per GPU")
-    ap.add_argument("--cpu-steps", type=int, default=5)
+    ap.add_argument("--cpu-steps", type=int, default=20, help="timed oracle steps (BASELINE.md plan: >= 20)")
+    ap.add_argument("--cpu-warmup", type=int, default=5, help="untimed oracle steps first (BASELINE.md plan: 5)")
     ap.add_argument("--cpu-batch", type=int, default=8)
+    ap.add_argument("--cpu-budget-s", type=float, default=330.0,
+                    help="wall-clock cap of the CPU baseline (warm-up + timed); the timed loop stops early "
+                         "past it and the sample says how many steps ran")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-op-timing", action="store_true")
-    ap.add_argument("--compare", default="f32;bf16x3;bf16",
+    ap.add_argument("--compare", default="f32",
                     help="';'-separated conv math modes timed beside the default step: the all-fp32 MFMA "
                          "step (reported as f32_exact, with its own warm-up and roofline) and the coarser "
                          "split-bf16 / one-term bf16 steps; '' for none")
@@ -120,26 +124,59 @@ def _cpu_model():
     return platform.processor() or "unknown"
 
 
-def cpu_baseline(batch, steps):
+def _cpu_threads():
+    """BASELINE.md's plan: len(os.sched_getaffinity(0)) threads, capped by
+    OMP_NUM_THREADS where the job sets it (the GPU box's CPU share is 16 cores
+    while the affinity mask lists the whole machine)."""
+    aff = len(os.sched_getaffinity(0))
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return (min(aff, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else aff), aff
+
+
+def cpu_baseline(batch, steps, warmup, budget_s):
     """Oracle (pure-PyTorch CPU restatement of the reference, pinned by the
-    golden fixtures) timed on this box's host cores: a bounded sample of the
-    same workload (BASELINE.md's CPU-baseline plan: B = 8 train steps)."""
+    golden fixtures) timed on this box's host cores: BASELINE.md's CPU-baseline
+    plan (B = 8 FRCRN train steps, 5 warm-up + 20 timed, fp32), under a wall-clock
+    cap so the default bench stays bounded."""
     sys.path.insert(0, ROOT)
     from oracle import models as O, train as OT
     from sehip.data import synthetic_pairs
-    threads = torch.get_num_threads()
-    noisy, clean = synthetic_pairs(batch, SR * SECONDS, seed=99, device="cpu")
-    m = O.FRCRN().train()
-    opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-2)
-    OT.train_step(m, opt, noisy, clean)                     # warm-up
-    t0 = time.perf_counter()
-    for _ in range(steps):
-        OT.train_step(m, opt, noisy, clean)
-    dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 4), "unit": "utterances/sec", "cores": threads, "kind": "port",
-            "sample": f"{steps} oracle FRCRN train steps (fwd+SI-SNR+bwd+clip+AdamW, fp32, B={batch} x 4 s "
-                      f"@ 16 kHz) after 1 warm-up step, torch CPU, {threads} threads",
-            "cpu_model": _cpu_model(), "seconds": round(dt, 2)}
+    threads, affinity = _cpu_threads()
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    try:
+        noisy, clean = synthetic_pairs(batch, SR * SECONDS, seed=99, device="cpu")
+        m = O.FRCRN().train()
+        opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-2)
+        t_start = time.perf_counter()
+        for _ in range(warmup):
+            OT.train_step(m, opt, noisy, clean)
+        t_warm = time.perf_counter() - t_start
+        per_step = t_warm / max(warmup, 1)
+        t0 = time.perf_counter()
+        done = 0
+        for _ in range(steps):
+            if done and time.perf_counter() - t_start + per_step > budget_s:
+                break
+            OT.train_step(m, opt, noisy, clean)
+            done += 1
+        dt = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    return {"value": round(batch * done / dt, 4), "unit": "utterances/sec", "cores": threads, "kind": "port",
+            "sample": f"{done} timed oracle FRCRN train steps (fwd+SI-SNR+bwd+clip+AdamW, fp32, B={batch} x 4 s "
+                      f"@ 16 kHz) after {warmup} warm-up steps, torch CPU, {threads} threads"
+                      + (f" (stopped at the {budget_s:.0f} s cap; {steps} planned)" if done < steps else ""),
+            "cpu_model": _cpu_model(), "affinity_cpus": affinity, "seconds": round(dt, 2),
+            "warmup_seconds": round(t_warm, 2)}
+
+
+def _rccl_version():
+    try:
+        v = torch.cuda.nccl.version()
+        return ".".join(str(x) for x in v) if isinstance(v, tuple) else str(v)
+    except Exception:   # noqa: BLE001 (reported, not needed)
+        return None
 
 
 def _kernel_key(name):
@@ -241,7 +278,27 @@ def _breakdown(kern, steps):
 
 
 def main():
+    """`--gpus N` is the world size. Under torchrun (WORLD_SIZE set) it must equal
+    WORLD_SIZE. Without torchrun and N > 1, this process spawns the N ranks itself
+    (sehip.train.spawn_ranks: one fresh process per GPU, RCCL) after checking,
+    without initialising the GPU, that N GPUs are visible; it never silently runs
+    fewer ranks than asked."""
     args = parse()
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is None and args.gpus > 1:
+        visible = torch.cuda.device_count()      # counts devices without initialising them
+        if visible < args.gpus:
+            raise SystemExit(f"bench.py --gpus {args.gpus}: only {visible} GPU(s) visible; refusing to run "
+                             f"fewer ranks than asked")
+        from sehip.train import spawn_ranks
+        spawn_ranks(args.gpus, run, (args,))
+        return
+    if env_world is not None and int(env_world) != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but WORLD_SIZE={env_world}")
+    run(args)
+
+
+def run(args):
     from sehip import functional as SF
     from sehip.data import synthetic_pairs
     from sehip.models import FRCRN
@@ -252,6 +309,9 @@ def main():
     rank, world, local, device = setup_distributed()
     if device.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
+    if world != args.gpus:
+        raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} rank(s)")
+    dist_backend = torch.distributed.get_backend() if world > 1 else None
     torch.manual_seed(2023 + rank)
     model = FRCRN().to(device).train()
     model = wrap_ddp(model, device)
@@ -360,6 +420,9 @@ def main():
                    "per_gpu_batch": B, "global_batch": B * world, "seq_len": L,
                    "parallelism": f"dp{world}"},
         "final_loss": round(loss_v, 4),
+        "dist": ({"world": world, "backend": dist_backend, "rccl_version": _rccl_version(),
+                  "launcher": "torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else "bench.py spawn"}
+                 if world > 1 else None),
         "conv_math": default_mode,
         "conv_math_note": "fp32 storage and accumulation everywhere; 'f16x3' scales each operand by a "
                           "per-tensor power of two, splits it into hi+lo fp16 and sums hi*hi+hi*lo+lo*hi "
@@ -410,7 +473,7 @@ def main():
         total_conv = sum(v["flops"] for k, v in kern.items() if k.startswith("conv"))
         out["conv_flops_per_utt"] = total_conv / (B * args.steps)
     if world == 1 and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_steps)
+        out["cpu_baseline"] = cpu_baseline(args.cpu_batch, args.cpu_steps, args.cpu_warmup, args.cpu_budget_s)
     print(json.dumps(out), flush=True)
 
 

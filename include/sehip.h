@@ -509,6 +509,14 @@ int se_crop_pad(const float* src, const long long* off, const int* len,
 int se_pcm16_to_float(const int16_t* in, long long n, float* out, void* stream);
 int se_float_to_pcm16(const float* in, long long n, int16_t* out, void* stream);
 
+/* se_resample: mix_audio.py:71-77 (torchaudio.transforms.Resample(orig, new),
+ * default sinc_interp_hann, lowpass_filter_width 6, rolloff 0.99) as a
+ * polyphase FIR: x [rows, L] -> out [rows, Lout], Lout = ceil(new * L / orig);
+ * orig / nw are the rates divided by their gcd; kern [nw][K] (K = 2 width + orig)
+ * is the windowed-sinc table built by the host (sehip.data.resample_kernel). */
+int se_resample(const float* x, int rows, int L, int orig, int nw, const float* kern, int K, int width,
+                float* out, int Lout, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -88,3 +88,42 @@ def pcm16_to_float(x):
 
 def float_to_pcm16(x):
     return torch.clamp(torch.round(x * 32768.0), -32768, 32767).to(torch.int16)
+
+
+def sinc_resample_kernel(orig_freq, new_freq, lowpass_filter_width=6, rolloff=0.99, dtype=torch.float32):
+    """torchaudio.functional.resample's kernel (sinc_interp_hann, the default of
+    torchaudio.transforms.Resample that mix_audio.py:71-77 uses), restated from
+    torchaudio's published algorithm (torchaudio is absent here; parity unpinned):
+    rates divided by their gcd; cut-off min(orig, new) * rolloff; per output phase a
+    windowed sinc over 2 width + orig input taps. Returns (kernel [new, 1, K], width,
+    orig', new')."""
+    import math
+    g = math.gcd(int(orig_freq), int(new_freq))
+    orig, new = int(orig_freq) // g, int(new_freq) // g
+    base = min(orig, new) * rolloff
+    width = math.ceil(lowpass_filter_width * orig / base)
+    idx = torch.arange(-width, width + orig, dtype=dtype)[None, None] / orig
+    t = torch.arange(0, -new, -1, dtype=dtype)[:, None, None] / new + idx
+    t = (t * base).clamp(-lowpass_filter_width, lowpass_filter_width)
+    window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    t = t * math.pi
+    kern = torch.where(t == 0, torch.tensor(1.0, dtype=dtype), t.sin() / t)
+    kern = kern * window * (base / orig)
+    return kern, width, orig, new
+
+
+def resample(waveform, orig_freq, new_freq):
+    """torchaudio.functional.resample (sinc_interp_hann): pad width / width + orig,
+    strided conv1d with the polyphase kernel, interleave phases, trim to
+    ceil(new * L / orig)."""
+    import math
+    if orig_freq == new_freq:
+        return waveform
+    kern, width, orig, new = sinc_resample_kernel(orig_freq, new_freq, dtype=waveform.dtype)
+    shape = waveform.shape
+    w = waveform.reshape(-1, shape[-1])
+    n, length = w.shape
+    w = F.pad(w, (width, width + orig))
+    out = F.conv1d(w[:, None], kern, stride=orig).transpose(1, 2).reshape(n, -1)
+    out = out[..., :math.ceil(new * length / orig)]
+    return out.reshape(shape[:-1] + out.shape[-1:])

@@ -97,6 +97,30 @@ __global__ void float_to_pcm16_kernel(const float* __restrict__ in, long long n,
   }
 }
 
+// Band-limited resampling by orig/new (both divided by their gcd): the
+// polyphase FIR of torchaudio.transforms.Resample's default sinc_interp_hann,
+// which mix_audio.py:71-77 applies when a file's rate differs from the mix rate.
+// out[r, j] = sum_t xpad[r, (j / nw) * og + t] * kern[j % nw, t], xpad = x with
+// `width` zeros in front (and zeros past the end). One thread per output
+// sample, taps summed in order; kern [nw][K] comes from the host.
+__global__ void __launch_bounds__(kThreads)
+resample_kernel(const float* __restrict__ x, int L, int og, int nw, const float* __restrict__ kern, int K,
+                int width, float* __restrict__ out, int Lout) {
+  const int r = blockIdx.y;
+  const int j = blockIdx.x * kThreads + threadIdx.x;
+  if (j >= Lout) return;
+  const int i = j / nw, p = j - i * nw;
+  const float* xr = x + (long long)r * L;
+  const float* kp = kern + (long long)p * K;
+  const long long u0 = (long long)i * og - width;
+  float acc = 0.f;
+  for (int t = 0; t < K; ++t) {
+    const long long u = u0 + t;
+    if (u >= 0 && u < L) acc = fmaf(xr[u], kp[t], acc);
+  }
+  out[(long long)r * Lout + j] = acc;
+}
+
 inline unsigned grid_of(long long n) {
   const long long g = (n + kThreads - 1) / kThreads;
   return (unsigned)(g < 8192 ? (g > 0 ? g : 1) : 8192);
@@ -141,6 +165,18 @@ extern "C" int se_float_to_pcm16(const float* in, long long n, int16_t* out, voi
   if (!in || !out || n < 0) return SE_E_ARG;
   if (n == 0) return SE_OK;
   hipLaunchKernelGGL(float_to_pcm16_kernel, dim3(grid_of(n)), dim3(kThreads), 0, se::as_stream(stream), in, n, out);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_resample(const float* x, int rows, int L, int orig, int nw, const float* kern, int K, int width,
+                           float* out, int Lout, void* stream) {
+  if (!x || !kern || !out || rows < 0 || L <= 0 || orig <= 0 || nw <= 0 || K <= 0 || width < 0 || Lout < 0)
+    return SE_E_ARG;
+  if ((long long)((L - 1) / orig + 1) * nw < Lout) return SE_E_SHAPE;
+  if (rows == 0 || Lout == 0) return SE_OK;
+  hipLaunchKernelGGL(resample_kernel, dim3(se::ceil_div(Lout, kThreads), rows), dim3(kThreads), 0,
+                     se::as_stream(stream), x, L, orig, nw, kern, K, width, out, Lout);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

@@ -63,6 +63,7 @@ _SIGNATURES = {
     "se_crop_pad": (c_int, [_P, _P, _P, _P, c_int, c_int, _P, _P]),
     "se_pcm16_to_float": (c_int, [_P, ctypes.c_longlong, _P, _P]),
     "se_float_to_pcm16": (c_int, [_P, ctypes.c_longlong, _P, _P]),
+    "se_resample": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int, c_int, _P, c_int, _P]),
     "se_conv2d_workspace_size": (c_size_t, [_P]),
     "se_conv2d_fwd": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),

@@ -82,6 +82,9 @@ class _FusedComplexConv(nn.Module):
     real convs + sub/add/cat."""
 
     transposed = False
+    # set by a model on its first conv, whose input is the raw spectrum (the batch's
+    # whole level spread): its f16x3 GEMMs run exact fp32 (functional._pass_math)
+    exact_fp32 = False
 
     def _geometry(self):
         c = self.real_conv
@@ -104,7 +107,7 @@ class _FusedComplexConv(nn.Module):
                      out_channels=2 * c.out_channels, kernel=c.kernel_size, stride=c.stride,
                      padding=begin, padding_end=end, dilation=c.dilation,
                      output_padding=getattr(c, "output_padding", (0, 0)),
-                     transposed=self.transposed)
+                     transposed=self.transposed, exact=self.exact_fp32)
         return rebuild(y.to(xs.dtype))
 
     def forward_joined(self, x, skip):
@@ -145,7 +148,8 @@ class ComplexConvTranspose2d(_FusedComplexConv):
 def real_conv2d(conv: nn.Module, x, input_pad=None):
     """A plain nn.Conv2d / nn.ConvTranspose2d evaluated by the same HIP GEMM
     (e.g. FRCRN's real final_conv, frcrn.py:115); input_pad as in
-    _FusedComplexConv.forward."""
+    _FusedComplexConv.forward. A conv flagged `sehip_exact_fp32` (a model's first,
+    data-fed conv) runs exact fp32 where the mode is f16x3."""
     tr = isinstance(conv, nn.ConvTranspose2d)
     if conv.groups != 1 or isinstance(conv.padding, str):
         raise NotImplementedError("sehip real conv: groups / string padding")
@@ -153,7 +157,7 @@ def real_conv2d(conv: nn.Module, x, input_pad=None):
     y = F.conv2d(_f32(x), _f32(conv.weight), None, _f32(conv.bias), None, out_channels=conv.out_channels,
                  kernel=conv.kernel_size, stride=conv.stride, padding=begin, padding_end=end,
                  dilation=conv.dilation, output_padding=getattr(conv, "output_padding", (0, 0)),
-                 transposed=tr)
+                 transposed=tr, exact=getattr(conv, "sehip_exact_fp32", False))
     return y.to(x.dtype)
 
 
@@ -378,3 +382,24 @@ class ComplexPReLU(nn.Module):
 
 ComplexReLU = nn.ReLU            # complex_nn.py:359
 ComplexLeakyReLU = nn.LeakyReLU  # complex_nn.py:360
+
+
+def mark_data_fed(block: nn.Module) -> nn.Module:
+    """mark_data_fed_conv on every conv inside `block` (a model's first block)."""
+    for m in block.modules():
+        if isinstance(m, (_FusedComplexConv, nn.Conv2d, nn.ConvTranspose2d)):
+            mark_data_fed_conv(m)
+    return block
+
+
+def mark_data_fed_conv(conv: nn.Module) -> nn.Module:
+    """Flag a model's first conv (its input is the raw spectrum or magnitude, which
+    carries the whole level spread of the batch; every later conv operand is a
+    per-channel normalised activation or a gradient of one): its passes run exact
+    fp32 where the conv math is the per-tensor-scaled f16x3. This conv is HBM-bound
+    (Cin = 2), so exact products cost nothing measurable."""
+    if isinstance(conv, _FusedComplexConv):
+        conv.exact_fp32 = True
+    else:   # (the real_conv / imag_conv holders of a fused conv are flagged too, harmlessly)
+        conv.sehip_exact_fp32 = True
+    return conv

@@ -45,6 +45,7 @@ def synthetic_pairs(batch: int, length: int = 64000, sr: int = 16000, seed: int 
 # made on the host with a `random.Random` in the reference's order, so a seeded
 # run draws what the reference would; the kernels then mix / crop / pad.
 # --------------------------------------------------------------------------
+import os
 import random as _random
 import wave as _wave
 
@@ -93,19 +94,82 @@ def mix_batch(clean: torch.Tensor, noise: torch.Tensor, snr_db, noise_start=None
     return mix, rep, scale
 
 
-def get_noisy_data(clean_audio, noise_audio, noise_repeat=None, k=100, rng=None):
-    """mix_audio.py:20-149 for tensors already in memory (channels x samples or 1-D;
-    no resampling, no wav writing): k mixes of one clean / noise pair at random
-    integer SNRs in [-20, 20], drawn with `rng` (a random.Random, or the module
-    `random` as in the reference) in the reference's order. Mono downmix as
-    :65-69. Returns (clean_amp, noise_amp, outputs) with the reference's keys."""
+def resample_kernel(orig_freq: int, new_freq: int, lowpass_filter_width: int = 6, rolloff: float = 0.99):
+    """Host table of the band-limited resampler that mix_audio.py:71-77 applies
+    (torchaudio.transforms.Resample's default sinc_interp_hann): rates divided by
+    their gcd, cut-off min(orig, new) * rolloff, per output phase a Hann-windowed
+    sinc over K = 2 width + orig input taps. Returns (kern [new, K] fp32, width,
+    orig', new')."""
+    g = math.gcd(int(orig_freq), int(new_freq))
+    orig, new = int(orig_freq) // g, int(new_freq) // g
+    base = min(orig, new) * rolloff
+    width = math.ceil(lowpass_filter_width * orig / base)
+    idx = torch.arange(-width, width + orig, dtype=torch.float32)[None] / orig
+    t = torch.arange(0, -new, -1, dtype=torch.float32)[:, None] / new + idx
+    t = (t * base).clamp(-lowpass_filter_width, lowpass_filter_width)
+    window = torch.cos(t * math.pi / lowpass_filter_width / 2) ** 2
+    t = t * math.pi
+    kern = torch.where(t == 0, torch.tensor(1.0), t.sin() / t) * window * (base / orig)
+    return kern.contiguous(), width, orig, new
+
+
+_RESAMPLE_TABLES: dict = {}
+
+
+def resample(waveform: torch.Tensor, orig_freq: int, new_freq: int) -> torch.Tensor:
+    """[..., L] on the GPU resampled from orig_freq to new_freq (se_resample), with
+    torchaudio.functional.resample's length ceil(new * L / orig)."""
+    if int(orig_freq) == int(new_freq):
+        return waveform
+    N.require_device(waveform)
+    key = (int(orig_freq), int(new_freq), str(waveform.device))
+    if key not in _RESAMPLE_TABLES:
+        kern, width, o, n = resample_kernel(orig_freq, new_freq)
+        _RESAMPLE_TABLES[key] = (kern.to(waveform.device), width, o, n)
+    kern, width, o, n = _RESAMPLE_TABLES[key]
+    x = waveform.reshape(-1, waveform.shape[-1]).contiguous()
+    rows, L = x.shape
+    lout = math.ceil(n * L / o)
+    out = torch.empty(rows, lout, device=x.device, dtype=torch.float32)
+    N.check(N.lib().se_resample(x.data_ptr(), rows, L, o, n, kern.data_ptr(), kern.shape[1], width, out.data_ptr(),
+                                lout, N.stream_of(x)), "se_resample")
+    return out.reshape(waveform.shape[:-1] + (lout,))
+
+
+def _as_audio(src, sample_rate, device):
+    """A path (PCM16 wav, read with its own rate) or a [channels, samples] / [samples]
+    tensor (at `sample_rate`), as a [channels, samples] fp32 tensor on the device."""
+    if isinstance(src, (str, os.PathLike)):
+        return load_wav(src, device=device)
+    t = src[None] if src.dim() == 1 else src
+    return t.to(device=device, dtype=torch.float32), sample_rate
+
+
+def get_noisy_data(clean_audio_path, noise_audio_path, mix_output_path="synth/mix/",
+                   clean_output_path="synth/clean/", noise_output_path="synth/noise/", mix_sample_rate=16000,
+                   clean_sample_rate=None, noise_sample_rate=None, noise_repeat=None, k=100, save=False, *,
+                   rng=None, device="cuda"):
+    """mix_audio.py:20-149 with the per-sample work on the GPU: the same arguments,
+    defaults and return value (clean_amp, noise_amp, outputs), outputs holding the
+    reference's keys 'mixed_output', 'adjusted_noise', 'repeat_noise',
+    'noise_indices', 'snr' (k entries each). Inputs are paths (16-bit PCM wav;
+    torchaudio.load reads more formats) or tensors (channels x samples, or 1-D;
+    their rate is clean/noise_sample_rate, default mix_sample_rate). Stereo is
+    averaged to mono (:65-69), other rates resampled to mix_sample_rate (:71-77,
+    se_resample), then k mixes at random integer SNRs in [-20, 20] are drawn with
+    `rng` (a random.Random, or the module `random` as the reference) in the
+    reference's order and mixed on the device (se_mix_snr). save=True writes
+    <clean>_<noise>_{mix,clean,noise}_<i>.wav as PCM16 into the three output
+    directories (:133-138)."""
     rng = rng or _random
-    c = clean_audio[None] if clean_audio.dim() == 1 else clean_audio
-    n = noise_audio[None] if noise_audio.dim() == 1 else noise_audio
+    c, csr = _as_audio(clean_audio_path, clean_sample_rate or mix_sample_rate, device)
+    n, nsr = _as_audio(noise_audio_path, noise_sample_rate or mix_sample_rate, device)
     if c.shape[0] > 1:
         c = c.mean(dim=0, keepdim=True)
     if n.shape[0] > 1:
         n = n.mean(dim=0, keepdim=True)
+    c = resample(c, csr, mix_sample_rate)
+    n = resample(n, nsr, mix_sample_rate)
     Lc, Ln = c.shape[1], n.shape[1]
     Lnp = min(Ln, Lc)
     starts, snrs, places, indices = [], [], [], []
@@ -119,10 +183,23 @@ def get_noisy_data(clean_audio, noise_audio, noise_repeat=None, k=100, rng=None)
             indices.append([[s, s + Lnp] for s in p])
         else:
             indices.append([[i, i + Lnp] for i in range(0, max_repeat * Lnp, Lnp)])
-    mix, rep, _ = mix_batch(c.expand(k, Lc), n.expand(k, Ln), snrs, starts,
-                            places if noise_repeat is not None else None)
+    if k > 0:
+        mix, rep, _ = mix_batch(c.expand(k, Lc), n.expand(k, Ln), snrs, starts,
+                                places if noise_repeat is not None else None)
+    else:
+        mix = rep = c.new_empty(0, Lc)
     outputs = {"mixed_output": list(mix.unsqueeze(1).unbind(0)), "adjusted_noise": [n] * k,
                "repeat_noise": list(rep.unsqueeze(1).unbind(0)), "noise_indices": indices, "snr": snrs}
+    if save:
+        stem = lambda p: os.path.splitext(os.path.basename(str(p)))[0] if isinstance(p, (str, os.PathLike)) else "audio"
+        name = stem(clean_audio_path) + "_" + stem(noise_audio_path)
+        for d in (mix_output_path, clean_output_path, noise_output_path):
+            os.makedirs(d, exist_ok=True)
+        for i in range(k):
+            save_wav(os.path.join(mix_output_path, f"{name}_mix_{i}.wav"), outputs["mixed_output"][i], mix_sample_rate)
+            save_wav(os.path.join(clean_output_path, f"{name}_clean_{i}.wav"), c, mix_sample_rate)
+            save_wav(os.path.join(noise_output_path, f"{name}_noise_{i}.wav"), outputs["repeat_noise"][i],
+                     mix_sample_rate)
     return c, n, outputs
 
 
@@ -175,6 +252,35 @@ class AudioSpliter:
         nref = len(kept[0][0]["ref"])
         return {"mix": crop([s["mix"] for s, _ in kept]),
                 "ref": [crop([s["ref"][j] for s, _ in kept]) for j in range(nref)]}
+
+
+class AudioDataLoader:
+    """audio_dataloader.py:52-81: a torch DataLoader over `dataset` (items
+    {'mix': [1, L], 'ref': [[1, L], ...]}, as TrainAudioDatasets yields) whose
+    workers only gather the ragged items; each batch is then cropped / padded to
+    chunk_size and stacked on the device (AudioSpliter.collate, se_crop_pad).
+    Items shorter than least_samples are dropped (audio_dataloader.py:32-34).
+    Yields {'mix': [B, 1, chunk], 'ref': [[B, 1, chunk], ...]} on `device`;
+    len() is the dataset length, as the reference's."""
+
+    def __init__(self, dataset, chunk_size=32000, least_samples=16000, device="cuda", rng=None, **kwargs):
+        from torch.utils.data import DataLoader
+        self.dataset = dataset
+        self.batch_size = kwargs["batch_size"]
+        self.device = device
+        self.spliter = AudioSpliter(chunk_size, least_samples, rng=rng)
+        self.data_loader = DataLoader(dataset, collate_fn=list, **kwargs)
+
+    def __iter__(self):
+        for items in self.data_loader:
+            on_dev = [{"mix": it["mix"].to(self.device, non_blocking=True),
+                       "ref": [r.to(self.device, non_blocking=True) for r in it["ref"]]} for it in items]
+            batch = self.spliter.collate(on_dev)
+            if batch:          # every item shorter than least_samples: nothing to yield
+                yield batch
+
+    def __len__(self):
+        return len(self.dataset)
 
 
 def pcm16_to_float(x: torch.Tensor) -> torch.Tensor:

@@ -328,14 +328,23 @@ def _f16_operands(d):
     fwd = _pass_math("fwd", d) == F16X3 and d.out_channels > 64
     data = _pass_math("data", d) == F16X3 and d.in_channels > 64
     n = d.in_channels if d.transposed else d.out_channels
-    wgt = _CONV_MATH["weight"] == F16X3 and n > 32 and n % 16 == 0
+    wgt = _pass_math("weight", d) == F16X3 and n > 32 and n % 16 == 0
     return fwd or wgt, data or wgt
 
 
+SE_MATH_F32 = 0
+
+
 def _pass_math(pass_name, d) -> int:
+    m = _CONV_MATH[pass_name]
     if pass_name == "fwd" and _FWD_DEC[0] is not None and d.transposed and d.in_h >= _FWD_DEC[1]:
-        return _FWD_DEC[0]
-    return _CONV_MATH[pass_name]
+        m = _FWD_DEC[0]
+    # a data-fed conv (exact=True: a model's first conv, whose input is the raw spectrum
+    # and carries the batch's whole level spread) runs exact fp32 where the mode is the
+    # per-tensor-scaled f16x3 (DESIGN.md §3.2 "Dynamic range")
+    if m == F16X3 and getattr(d, "exact", False):
+        return SE_MATH_F32
+    return m
 
 
 def _gemm_tag(pass_name, d, joined=False):
@@ -349,7 +358,7 @@ def _gemm_tag(pass_name, d, joined=False):
     j = "_joined" if joined else ""
     if pass_name == "weight":
         n = d.in_channels if tr else d.out_channels          # channels of the direct operand
-        kind = "smalln" if n <= 8 else (names[_CONV_MATH["weight"]] if n > 32 else "f32")
+        kind = "smalln" if n <= 8 else (names[_pass_math("weight", d)] if n > 32 else "f32")
         kind = "f32" if kind == "bf16x6" else kind
         return f"conv_wgrad{j}_{kind}"
     n = d.out_channels if pass_name == "fwd" else d.in_channels
@@ -386,7 +395,7 @@ def _conv_flops(d) -> float:
 # Complex / real (transposed) conv2d — se_conv2d_* (cconv.hip)
 # --------------------------------------------------------------------------
 def conv_desc(x_shape, out_channels, kernel, stride, padding, dilation, output_padding,
-              transposed, complex_w, padding_end=None) -> N.ConvDesc:
+              transposed, complex_w, padding_end=None, exact=False) -> N.ConvDesc:
     """padding = (top, left) begin padding; padding_end = (bottom, right), or
     None for symmetric padding (nn.Conv2d)."""
     b, cin, h, w = x_shape
@@ -400,7 +409,8 @@ def conv_desc(x_shape, out_channels, kernel, stride, padding, dilation, output_p
     d.out_pad_h, d.out_pad_w = output_padding
     d.transposed, d.complex_weights = int(transposed), int(complex_w)
     d.pad_h_end, d.pad_w_end = (-1, -1) if padding_end is None else padding_end
-    d.math = _CONV_MATH["fwd"]
+    d.exact = bool(exact)   # host-side only (see _pass_math)
+    d.math = _pass_math("fwd", d)
     return d
 
 
@@ -408,11 +418,11 @@ class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wr, wi, br, bi, geom):
         (out_channels, kernel, stride, padding, dilation, output_padding, transposed, complex_w,
-         padding_end) = geom
+         padding_end, exact) = geom
         N.require_device(x, wr, wi, br, bi)
         x = x.contiguous()
         d = conv_desc(tuple(x.shape), out_channels, kernel, stride, padding, dilation,
-                      output_padding, transposed, complex_w, padding_end)
+                      output_padding, transposed, complex_w, padding_end, exact)
         lib = N.lib()
         ho, wo = N.c_int(), N.c_int()
         N.check(lib.se_conv2d_out_shape(N.ctypes.byref(d), N.ctypes.byref(ho), N.ctypes.byref(wo)),
@@ -613,13 +623,14 @@ def conv2d_joined(x, s, wr, wi, br=None, bi=None, *, out_channels, kernel, strid
 
 
 def conv2d(x, wr, wi=None, br=None, bi=None, *, out_channels, kernel, stride=1, padding=0,
-           dilation=1, output_padding=0, transposed=False, padding_end=None):
+           dilation=1, output_padding=0, transposed=False, padding_end=None, exact=False):
     """Fused complex conv (wi given) or real conv (wi None) on the HIP path.
     padding is the (top, left) begin padding; padding_end (bottom, right)
-    defaults to the same (symmetric, as nn.Conv2d)."""
+    defaults to the same (symmetric, as nn.Conv2d). exact=True: a data-fed conv
+    (see _pass_math) whose f16x3 passes run exact fp32 instead."""
     geom = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
             _pair(output_padding), bool(transposed), wi is not None,
-            None if padding_end is None else _pair(padding_end))
+            None if padding_end is None else _pair(padding_end), bool(exact))
     return _Conv2d.apply(x, wr, wi, br, bi, geom)
 
 
@@ -885,12 +896,15 @@ def lstm_supported(hidden: int) -> bool:
 
 
 _WIDE: dict = {}
+_WIDE_PENDING: list = []   # (event, pinned status copy) of launched se_lstm_wide_* calls
 
 
-def _wide_ws(device):
-    """Per-device (sync counters, status word) of se_lstm_wide_*. The status
-    word stays 0 unless a group barrier timed out (lstm_wide_status)."""
-    key = str(device)
+def _wide_ws(device, stream: int):
+    """(sync counters, status word) of se_lstm_wide_* for one (device, stream):
+    a launch memsets its group counters and spins on them, so launches that may
+    overlap (other streams) get their own. The status word stays 0 unless a
+    group barrier timed out (the launch then wrote NaN; lstm_wide_poll raises)."""
+    key = (str(device), int(stream))
     w = _WIDE.get(key)
     if w is None:
         n = int(N.lib().se_lstm_wide_sync_ints())
@@ -899,10 +913,52 @@ def _wide_ws(device):
     return w
 
 
+def _wide_launched(status: torch.Tensor) -> None:
+    """After a wide launch: a non-blocking copy of its status word to pinned host
+    memory, checked by lstm_wide_poll once the launch has finished."""
+    host = torch.empty(1, dtype=torch.int32, pin_memory=True)
+    host.copy_(status, non_blocking=True)
+    ev = torch.cuda.Event()
+    ev.record()
+    _WIDE_PENDING.append((ev, host))
+
+
+class LstmWideTimeout(RuntimeError):
+    """A se_lstm_wide_* group barrier timed out: not every workgroup of a group was
+    resident at once (other work held the CUs), and the outputs are NaN."""
+
+
+def lstm_wide_poll(block: bool = False) -> None:
+    """Raise LstmWideTimeout if a finished se_lstm_wide_* launch reported a barrier
+    timeout. Non-blocking by default (launches still running are checked later);
+    block=True waits for all of them. Called before every wide launch and after
+    every train_step, so a timeout surfaces within one step instead of as NaN."""
+    keep = []
+    for ev, host in _WIDE_PENDING:
+        if block:
+            ev.synchronize()
+        if block or ev.query():
+            if int(host[0]):
+                _WIDE_PENDING.clear()
+                raise LstmWideTimeout("sehip wide LSTM: a group barrier timed out (its workgroups were not all "
+                                      "resident at once); the recurrence outputs are NaN")
+        else:
+            keep.append((ev, host))
+    _WIDE_PENDING[:] = keep
+
+
 def lstm_wide_status(device="cuda") -> int:
-    """0 unless a se_lstm_wide_* group barrier timed out on `device` (then its
-    outputs were written as NaN). Synchronises."""
-    return int(_wide_ws(torch.device(device))[1].item())
+    """0 unless a se_lstm_wide_* group barrier timed out on `device` (on any
+    stream; then its outputs were written as NaN). Synchronises."""
+    dev = str(torch.device(device))
+    return max([int(st.item()) for (d, _), (_, st) in _WIDE.items() if d == dev] or [0])
+
+
+def _wide_check(rc: int, what: str, H: int) -> None:
+    if rc == SE_E_UNSUPPORTED:
+        raise RuntimeError(f"sehip {what}: hidden size {H} needs {H // (32 if H <= 512 else 16)} co-resident "
+                           f"workgroups per group, more than this device's compute units allow")
+    N.check(rc, what)
 
 
 def _wide(H: int) -> bool:
@@ -950,11 +1006,13 @@ class _LstmLayer(torch.autograd.Function):
         gates = torch.empty((L, B, T, G), device=x.device, dtype=x.dtype)
         t0 = _TIMER.begin() if _TIMER else None
         if _wide(H):
-            sync, status = _wide_ws(x.device)
-            N.check(N.lib().se_lstm_wide_fwd(xproj.data_ptr(), x_lstm, x_row, w_hh.data_ptr(), h.data_ptr(),
-                                             c.data_ptr(), gates.data_ptr(), L, B, T, H, int(rev_mask),
-                                             sync.data_ptr(), status.data_ptr(), N.stream_of(x)),
-                    "se_lstm_wide_fwd")
+            lstm_wide_poll()
+            sync, status = _wide_ws(x.device, N.stream_of(x))
+            _wide_check(N.lib().se_lstm_wide_fwd(xproj.data_ptr(), x_lstm, x_row, w_hh.data_ptr(), h.data_ptr(),
+                                                 c.data_ptr(), gates.data_ptr(), L, B, T, H, int(rev_mask),
+                                                 sync.data_ptr(), status.data_ptr(), N.stream_of(x)),
+                        "se_lstm_wide_fwd", H)
+            _wide_launched(status)
         else:
             N.check(N.lib().se_lstm_fwd(xproj.data_ptr(), x_lstm, x_row, w_hh.data_ptr(),
                                         _zero_row(H, x.device).data_ptr(), h.data_ptr(), c.data_ptr(),
@@ -979,11 +1037,13 @@ class _LstmLayer(torch.autograd.Function):
         dgates = torch.empty_like(gates)
         t0 = _TIMER.begin() if _TIMER else None
         if _wide(H):
-            sync, status = _wide_ws(dh.device)
-            N.check(N.lib().se_lstm_wide_bwd(dh.data_ptr(), w_hh.data_ptr(), gates.data_ptr(), c.data_ptr(),
-                                             dgates.data_ptr(), L, B, T, H, ctx.rev_mask, sync.data_ptr(),
-                                             status.data_ptr(), N.stream_of(dh)),
-                    "se_lstm_wide_bwd")
+            lstm_wide_poll()
+            sync, status = _wide_ws(dh.device, N.stream_of(dh))
+            _wide_check(N.lib().se_lstm_wide_bwd(dh.data_ptr(), w_hh.data_ptr(), gates.data_ptr(), c.data_ptr(),
+                                                 dgates.data_ptr(), L, B, T, H, ctx.rev_mask, sync.data_ptr(),
+                                                 status.data_ptr(), N.stream_of(dh)),
+                        "se_lstm_wide_bwd", H)
+            _wide_launched(status)
         else:
             N.check(N.lib().se_lstm_bwd(dh.data_ptr(), w_hh.data_ptr(), gates.data_ptr(), c.data_ptr(),
                                         dgates.data_ptr(), L, B, T, H, ctx.rev_mask, N.stream_of(dh)),

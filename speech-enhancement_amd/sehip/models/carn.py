@@ -13,7 +13,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as TF
 
-from ..complex_nn import LSTM, real_conv2d
+from ..complex_nn import LSTM, mark_data_fed, real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
 from ..norm import bn_act
 
@@ -136,6 +136,7 @@ class CARN(nn.Module):
         self.stft = ConvSTFT(window_size, hop_size, fft_size)
         self.istft = ConviSTFT(window_size, hop_size, fft_size)
         self.encoder = Encoder(in_channels=2, gate=gate)
+        mark_data_fed(self.encoder.layers[0])        # the noisy spectrum enters here
         self.decoder = Decoder(in_channels=128, gate=gate)
         self.lstm = LSTM(input_size=lstm_channels, hidden_size=lstm_channels, num_layers=2, batch_first=True)
         self.linear = nn.Linear(in_features=fft_size, out_features=fft_size + 2)

@@ -10,7 +10,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as TF
 
-from ..complex_nn import LSTM, real_conv2d
+from ..complex_nn import LSTM, mark_data_fed, real_conv2d
 from ..conv_stft import ConvSTFT, ConviSTFT
 from ..norm import bn_act
 
@@ -89,6 +89,7 @@ class CRN(nn.Module):
         self.stft = ConvSTFT(window_size, hop_size, fft_size, return_mag_phase=True)
         self.istft = ConviSTFT(window_size, hop_size, fft_size)
         self.encoder = Encoder()
+        mark_data_fed(self.encoder.layers[0])        # the noisy magnitude enters here
         self.lstm_layers = LSTM(input_size=1024, hidden_size=1024, num_layers=2, batch_first=True)
         self.decoder = Decoder()
 

@@ -6,7 +6,7 @@ import torch.nn as nn
 import torch.nn.functional as TF
 
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLinear,
-                          ComplexLSTM, LSTM, complex_concat, norm_act, real_conv2d)
+                          ComplexLSTM, LSTM, complex_concat, mark_data_fed, norm_act, real_conv2d)
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -127,6 +127,7 @@ class DCCRN(nn.Module):
         self.stft = ConvSTFT(window_size, hop_size, fft_size)
         self.istft = ConviSTFT(window_size, hop_size, fft_size)
         self.encoder = Encoder(enc, in_channels=2, is_complex=is_complex)
+        mark_data_fed(self.encoder.layers[0])        # the noisy spectrum enters here
         self.decoder = Decoder(dec, in_channels=256, is_complex=is_complex)
         self.lstm = LSTMBlock(freq_channels, lstm_channels, linear_channels, num_layers=2, batch_first=True,
                               bidirectional=bidirectional, is_complex=is_complex)

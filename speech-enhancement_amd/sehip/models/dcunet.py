@@ -7,7 +7,7 @@ import torch.nn as nn
 import torch.nn.functional as TF
 
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLeakyReLU,
-                          norm_act, real_conv2d)
+                          mark_data_fed, norm_act, real_conv2d)
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 # name -> per-layer ((complex channels, real channels), kernel, stride, padding)
@@ -133,6 +133,7 @@ class DCUNet(nn.Module):
         self.istft = ConviSTFT(window_size, hop_size, fft_size)
         self.first_conv = ConvBlock(in_channels=mask_channels, out_channels=enc_channels, kernel_size=3,
                                     padding=1, is_complex=is_complex)
+        mark_data_fed(self.first_conv)               # the noisy spectrum enters here
         self.encoder = Encoder(arch, enc_channels, is_complex)
         self.decoder = Decoder(arch, dec_channels, mask_channels, is_complex)
 

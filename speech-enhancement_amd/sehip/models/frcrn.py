@@ -16,7 +16,7 @@ import torch.nn.functional as TF
 
 from ..ccbam import CCBAM
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLSTM,
-                          complex_concat, norm_act, real_conv2d)
+                          complex_concat, mark_data_fed, norm_act, real_conv2d)
 from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
 
@@ -244,6 +244,7 @@ class FRCRN(nn.Module):
         self.stft = ConvSTFT(window_size, hop_size, fft_size)
         self.istft = ConviSTFT(window_size, hop_size, fft_size)
         self.encoder = Encoder(in_channels=2, out_channels=128, is_complex=is_complex)
+        mark_data_fed(self.encoder.layers[0])        # the noisy spectrum enters here
         self.decoder = Decoder(in_channels=128, out_channels=128, is_complex=is_complex,
                                reduction_ratio=reduction_ratio)
         self.lstm = ComplexLSTM(256, lstm_channels, num_layers=2, bidirectional=False, batch_first=True)

@@ -60,15 +60,20 @@ def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=Fals
     norm = torch.empty(1, device=dev, dtype=torch.float32)
     st = N.stream_of(grads[0])
     N.check(N.lib().se_grad_sumsq(table.data_ptr(), n, total, sumsq.data_ptr(), st), "se_grad_sumsq")
-    if error_if_nonfinite and not torch.isfinite(sumsq).item():
-        raise RuntimeError("The total norm for gradients is non-finite")
+    if error_if_nonfinite and not torch.isfinite(sumsq[0]).item():   # [0] = the total (SE_SUMSQ_DOUBLES)
+        raise RuntimeError(f"The total norm of order {float(norm_type)} for gradients from `parameters` "
+                           "is non-finite, so it cannot be clipped")
     N.check(N.lib().se_clip_grads(table.data_ptr(), n, total, sumsq.data_ptr(), float(max_norm), norm.data_ptr(),
                                   st), "se_clip_grads")
     return norm.view(())
 
 
 class AdamW(torch.optim.Optimizer):
-    """torch.optim.AdamW on se_adamw_step: one launch per parameter group."""
+    """torch.optim.AdamW on se_adamw_step: one launch per (parameter group, step
+    count). Parameters of a group normally share their step count; one that
+    missed steps (no gradient on some iterations, or a loaded state_dict with
+    per-parameter steps) is updated by its own launch with its own bias
+    corrections, as torch tracks the step per parameter."""
 
     def __init__(self, params, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, amsgrad=False,
                  *, maximize=False, foreach=None, capturable=False, differentiable=False, fused=None):
@@ -85,7 +90,7 @@ class AdamW(torch.optim.Optimizer):
             with torch.enable_grad():
                 loss = closure()
         for group in self.param_groups:
-            rows, step_val = [], None
+            by_step: dict = {}
             for p in group["params"]:
                 if p.grad is None:
                     continue
@@ -97,18 +102,13 @@ class AdamW(torch.optim.Optimizer):
                     st["exp_avg"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                     st["exp_avg_sq"] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st["step"] += 1
-                s = int(st["step"].item())
-                if step_val is None:
-                    step_val = s
-                elif s != step_val:   # one launch per group needs one step count
-                    raise RuntimeError("sehip AdamW: parameters of a group at different step counts")
-                rows.append((p, p.grad, st["exp_avg"], st["exp_avg_sq"]))
-            if not rows:
-                continue
-            _check([t for r in rows for t in r])
+                s = int(st["step"].item())   # a CPU tensor, as torch's non-capturable AdamW
+                by_step.setdefault(s, []).append((p, p.grad, st["exp_avg"], st["exp_avg_sq"]))
             b1, b2 = group["betas"]
-            table, n, total = _slot_table(rows, rows[0][0].device)
-            N.check(N.lib().se_adamw_step(table.data_ptr(), n, total, float(group["lr"]), float(b1), float(b2),
-                                          float(group["eps"]), float(group["weight_decay"]), step_val,
-                                          N.stream_of(rows[0][0])), "se_adamw_step")
+            for step_val, rows in sorted(by_step.items()):
+                _check([t for r in rows for t in r])
+                table, n, total = _slot_table(rows, rows[0][0].device)
+                N.check(N.lib().se_adamw_step(table.data_ptr(), n, total, float(group["lr"]), float(b1),
+                                              float(b2), float(group["eps"]), float(group["weight_decay"]),
+                                              step_val, N.stream_of(rows[0][0])), "se_adamw_step")
         return loss

@@ -29,7 +29,7 @@ def make_optimizer(model, **overrides):
     kw = dict(ADAMW)
     kw.update(overrides)
     params = list(model.parameters())
-    if params and all(p.is_cuda and p.dtype == torch.float32 for p in params):
+    if params and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() for p in params):
         return _optim.AdamW(params, **kw)
     return torch.optim.AdamW(params, **kw)
 
@@ -86,6 +86,7 @@ def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
 
 
 def _train_step(model, optimizer, noisy, clean, clip_norm):
+    from . import functional as F
     from .functional import deferred_weight_grads
     _, wav = model(noisy)
     loss = si_snr_loss_aligned(wav, clean)     # mono reshape + pad / truncate + SI-SNR
@@ -96,16 +97,23 @@ def _train_step(model, optimizer, noisy, clean, clip_norm):
         _clip(model, clip_norm)
     optimizer.step()
     optimizer.zero_grad(set_to_none=True)
+    F.lstm_wide_poll()      # a wide-LSTM barrier timeout raises here, not as a NaN loss later
     return loss.detach()
 
 
 def setup_distributed(backend: str | None = None):
-    """Initialise torch.distributed from torchrun's env. Returns
-    (rank, world_size, local_rank, device)."""
+    """Initialise torch.distributed from torchrun's env (or spawn_ranks'). Returns
+    (rank, world_size, local_rank, device). With the GPU backend every local rank
+    needs its own device: a rank whose LOCAL_RANK has no GPU raises instead of
+    sharing another rank's."""
     import torch.distributed as dist
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # gloo rehearsals (tests, tools/gpu_ddp_rehearsal.sh) may put several ranks on one GPU
+    shared_ok = (backend or os.environ.get("SEHIP_DIST_BACKEND")) == "gloo"
+    if torch.cuda.is_available() and not shared_ok and local >= torch.cuda.device_count():
+        raise RuntimeError(f"sehip: LOCAL_RANK {local} but only {torch.cuda.device_count()} visible GPU(s)")
     if torch.cuda.is_available():
         torch.cuda.set_device(local)
         device = torch.device("cuda", local)
@@ -119,6 +127,32 @@ def setup_distributed(backend: str | None = None):
             kw["device_id"] = device
         dist.init_process_group(**kw)
     return rank, world, local, device
+
+
+def free_port() -> int:
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _rank_entry(rank, world, port, target, args):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+    target(*args)
+
+
+def spawn_ranks(nprocs: int, target, args=(), port: int | None = None) -> None:
+    """One fresh process per rank (torch.multiprocessing "spawn": a new
+    interpreter each, so nothing the parent holds is inherited), with torchrun's
+    environment (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_ADDR=127.0.0.1 /
+    MASTER_PORT) set before ``target(*args)`` runs; ``setup_distributed`` in the
+    target then binds cuda:LOCAL_RANK and joins the process group. The caller
+    must not have initialised the GPU (device_count() does not). Raises if any
+    rank fails (torch.multiprocessing.ProcessRaisedException / ProcessExitedException)."""
+    import torch.multiprocessing as mp
+    mp.start_processes(_rank_entry, args=(nprocs, port or free_port(), target, tuple(args)), nprocs=nprocs,
+                       join=True, start_method="spawn")
 
 
 class FlatDataParallel(torch.nn.Module):

@@ -69,3 +69,33 @@ def test_carn_chunked_longform_vs_oracle(dtype, gpu_device):
         drift = rel_l2(ref16.float().numpy(), ref32.numpy())
         print(f"chunked fp16: ours {e:.2e}, oracle fp16 drift {drift:.2e}")
         assert e < max(3 * drift, 1e-3), (e, drift)
+
+
+@pytest.mark.timeout(600)
+def test_carn_config5_full_length_vs_oracle(gpu_device):
+    """BASELINE config 5 at its full size: one 30 s @ 48 kHz utterance
+    ([1, 1,440,000]) through CARN in 4 s chunks overlapping 50 ms (8 chunks, one
+    batch; tools/bench_configs.py's plan). fp32 against oracle/longform.py at the
+    north-star 1e-4; fp16 storage (model.half()) against the same fp32 oracle
+    within 3x the oracle's own fp16 drift, measured on the first two chunks (the
+    CPU's fp16 convolutions take ~15 s per chunk)."""
+    from sehip import models as M, longform as L
+    from oracle import models as O, longform as OL
+    sr, chunk, overlap = 48000, 4 * 48000, 48000 // 20
+    noisy, _ = paramfill.structured_pair(1, 30 * sr, sr=sr, seed=35)
+    x = torch.from_numpy(noisy)[0]
+    mo = paramfill.fill_(O.CARN(320, 160, 512), seed=36).eval()
+    ref32 = OL.enhance_chunked(mo, x, chunk, overlap)
+    m = paramfill.fill_(M.CARN(320, 160, 512), seed=36).cuda().eval()
+    got = L.enhance_chunked(m, x.cuda(), chunk, overlap)
+    assert got.shape == (1, 30 * sr)
+    e32 = rel_l2(got.cpu().numpy(), ref32.numpy())
+    got16 = L.enhance_chunked(m.half(), x.cuda().half(), chunk, overlap)
+    e16 = rel_l2(got16.float().cpu().numpy(), ref32.numpy())
+    head = 2 * chunk - overlap                   # the first two chunks' span
+    ref_head32 = OL.enhance_chunked(mo, x[:head], chunk, overlap)
+    ref_head16 = OL.enhance_chunked(mo.half(), x[:head].half(), chunk, overlap)
+    drift = rel_l2(ref_head16.float().numpy(), ref_head32.numpy())
+    print(f"config 5, 30 s @ 48 kHz chunked: fp32 {e32:.2e}; fp16 {e16:.2e} (oracle fp16 drift {drift:.2e})")
+    assert e32 < TOL, e32
+    assert e16 < max(3 * drift, 1e-3), (e16, drift)

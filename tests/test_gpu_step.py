@@ -172,3 +172,40 @@ def test_frcrn_fork_gradient_handoff_bit_identical(gpu_device, monkeypatch):
     assert F.FORK_ACC_CALLS[0] - before == 5
     bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
     assert not bad, bad[:6]
+
+
+def test_clip_grad_norm_error_if_nonfinite(gpu_device):
+    """error_if_nonfinite=True: finite gradients clip as usual, a non-finite one raises
+    (as torch.nn.utils.clip_grad_norm_)."""
+    from sehip.optim import clip_grad_norm_
+    a, b = _params(gpu_device, 5), _params(gpu_device, 5)
+    ta = torch.nn.utils.clip_grad_norm_(a, 0.5, error_if_nonfinite=True)
+    tb = clip_grad_norm_(b, 0.5, error_if_nonfinite=True)
+    assert abs(ta.item() - tb.item()) <= 1e-6 * ta.item()
+    b[1].grad[3] = float("inf")
+    with pytest.raises(RuntimeError, match="non-finite"):
+        clip_grad_norm_(b, 0.5, error_if_nonfinite=True)
+
+
+def test_adamw_parameters_at_different_steps_match_torch(gpu_device):
+    """A parameter without a gradient on some steps falls behind the others' step
+    count; torch keeps a step per parameter, and so does sehip AdamW (one launch per
+    distinct step count): both agree after every step."""
+    from sehip.optim import AdamW
+    a, b = _params(gpu_device, 6), _params(gpu_device, 6)
+    oa = torch.optim.AdamW(a, lr=1e-3, weight_decay=1e-2)
+    ob = AdamW(b, lr=1e-3, weight_decay=1e-2)
+    g = torch.Generator().manual_seed(8)
+    for step in range(5):
+        for i, (pa, pb) in enumerate(zip(a, b)):
+            if i == 1 and step in (0, 2):     # parameter 1 has no gradient on steps 0 and 2
+                pa.grad = pb.grad = None
+            else:
+                ng = (torch.randn(pa.shape, generator=g) * 0.05).to(gpu_device)
+                pa.grad, pb.grad = ng.clone(), ng.clone()
+        oa.step()
+        ob.step()
+        for pa, pb in zip(a, b):
+            d = (pa - pb).abs().max().item()
+            assert d <= 1e-6 * max(pa.abs().max().item(), 1.0), (step, d)
+    assert int(ob.state[b[1]]["step"]) == 3 and int(ob.state[b[0]]["step"]) == 5
