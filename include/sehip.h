@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 3
+#define SEHIP_ABI_VERSION 4   /* 4: SE_DTYPE storage types (CBN), first-block fused backward, se_resample */
 
 enum {
   SE_OK = 0,
@@ -69,22 +69,24 @@ int se_stft_num_frames(int L, int win, int hop, int nfft, int center);
 /* ConvSTFT.forward (conv_stft.py:48-66).
  * x: [B, L]. center=1 reflect-pads nfft/2 on both sides (requires L > nfft/2).
  * mag_phase=0: out0 = spec [B, nfft+2, T] (rows 0..nfft/2 real, rest imag).
- * mag_phase=1: out0 = mags [B, nfft/2+1, T], out1 = phase (atan2(im, re)). */
-int se_stft_fwd(const float* x, float* out0, float* out1, int B, int L, int win,
+ * mag_phase=1: out0 = mags [B, nfft/2+1, T], out1 = phase (atan2(im, re)).
+ * dtype (SE_DTYPE_*): storage type of x and the outputs (fp32 arithmetic);
+ * window / twiddle stay fp32 (the module's kernel tables). */
+int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, int win,
                 int hop, int nfft, int center, int mag_phase,
-                const float* window, const float* twiddle, void* stream);
+                const float* window, const float* twiddle, int dtype, void* stream);
 
 /* ConviSTFT.forward (conv_stft.py:89-116) for a complex spec [B, nfft+2, T]:
  * overlap-add of the pinv-basis frames divided by (OLA(window^2) + 1e-8),
  * out[b, s] = full[b, s + offset] for 0 <= s < out_len. */
-int se_istft_fwd(const float* spec, float* out, int B, int T, int win, int hop,
+int se_istft_fwd(const void* spec, void* out, int B, int T, int win, int hop,
                  int nfft, int offset, int out_len, const float* window,
-                 const float* twiddle, void* stream);
+                 const float* twiddle, int dtype, void* stream);
 
 /* Adjoint of se_istft_fwd: gspec = d(out)/d(spec)^T gout. */
-int se_istft_bwd(const float* gout, float* gspec, int B, int T, int win,
+int se_istft_bwd(const void* gout, void* gspec, int B, int T, int win,
                  int hop, int nfft, int offset, int out_len,
-                 const float* window, const float* twiddle, void* stream);
+                 const float* window, const float* twiddle, int dtype, void* stream);
 
 /* ------------------------------------------------------------------------
  * Complex (transposed) 2-D convolution as ONE fused implicit GEMM
@@ -168,10 +170,26 @@ typedef struct se_conv2d_desc {
    * channels, non-joined, fp32 dx); other shapes return SE_E_UNSUPPORTED before
    * launching anything. */
   int accumulate_dx;
+  /* ABI 4: SE_DTYPE_* storage of x, y, dy, dx, the weights, the biases and their
+   * gradients. 16-bit storage (the reference's model.to(bfloat16) / .half()
+   * runs) reads and writes those tensors as they are and computes with the
+   * one-term MFMA of its own format, whose operands are then exact: bf16 needs
+   * math SE_MATH_BF16, fp16 needs SE_MATH_F16 (SE_E_UNSUPPORTED otherwise, and for
+   * the joined / CL16 forms and the fp32-only small weight-grad shapes, before any
+   * launch). fp32 storage takes any math. */
+  int dtype;
 } se_conv2d_desc;
 
+/* SE_MATH_F16 (5): operands rounded to fp16 (exact for fp16 storage), one MFMA
+ * term on v_mfma_f32_32x32x16_f16, fp32 accumulate, no scaling (the reference's
+ * model.half() conv). */
 enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3,
-       SE_MATH_F16X3 = 4 };
+       SE_MATH_F16X3 = 4, SE_MATH_F16 = 5 };
+
+/* Storage types of the activation tensors an entry point reads and writes
+ * (the reference's model.to(bfloat16) / model.half() runs, BASELINE configs
+ * 2, 3, 5). Entry points without a dtype argument take fp32. */
+enum { SE_DTYPE_F32 = 0, SE_DTYPE_BF16 = 1, SE_DTYPE_F16 = 2 };
 
 /* CL16: x [B, C, H, W] fp32 -> two channels-last fp16 planes [2][B][H][W][C],
  * hi = fp16(x s), lo = fp16(x s - hi), s = 2^(14 - e) with max|x| <= *amax < 2^e
@@ -258,15 +276,23 @@ int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float* x, int x_h
  * y_amax : device fp32 [1] or NULL. Training only: receives an upper bound of
  *          max |y| (from the moments pass's per-channel extrema, no extra
  *          pass), the se_conv2d_desc.x_amax of a SE_MATH_F16X3 consumer.
+ * prelu_w: NULL, or (with act = 1) the device weight of an nn.PReLU() with one
+ *          parameter applied after the norm (DCCRN, dccrn.py:21,45): LeakyReLU
+ *          with the slope read on the device. The backward writes its gradient
+ *          to dprelu_w (one element, overwritten).
+ * dtype  : SE_DTYPE_F32 / BF16 / F16, the storage type of x, y, gy, gy2, dx AND
+ *          of params / dparams / running / prelu_w (a model.to(bfloat16) /
+ *          .half() module keeps all of them in its dtype). Arithmetic is fp32
+ *          (moments fp64); stores round to nearest even. save stays fp32.
  * ------------------------------------------------------------------------ */
 #define SE_CBN_SAVE_FLOATS 20
 size_t se_cbn_workspace_size(int B, int C, int HW);
 
-int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
-               const float* const* params, float* const* running,
+int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
+               const void* const* params, void* const* running,
                int64_t* nbt, float* save, int training, float eps,
-               float momentum, int act, float slope, float* y_amax, void* ws,
-               size_t ws_bytes, void* stream);
+               float momentum, int act, float slope, float* y_amax,
+               const void* prelu_w, int dtype, void* ws, size_t ws_bytes, void* stream);
 
 /* Backward. gy = dL/dy (after the activation), x = forward input. y (the
  * forward output) is NOT read and may be NULL: the activation derivative is
@@ -275,11 +301,11 @@ int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
  * dWii, dBr, dBi (overwritten), or NULL. dx_amax: device fp32 [1] or NULL;
  * training only: an upper bound of max |dx| (the se_conv2d_desc.dy_amax of the
  * producing conv's SE_MATH_F16X3 backward). */
-int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
-               int B, int C, int HW, const float* const* params,
-               const float* save, float* const* dparams, int training,
-               int act, float slope, float* dx_amax, void* ws, size_t ws_bytes,
-               void* stream);
+int se_cbn_bwd(const void* gy, const void* y, const void* x, void* dx,
+               int B, int C, int HW, const void* const* params,
+               const float* save, void* const* dparams, int training,
+               int act, float slope, float* dx_amax, const void* prelu_w, void* dprelu_w,
+               int dtype, void* ws, size_t ws_bytes, void* stream);
 
 /* Backward of a forked output: y feeds two consumers (FRCRN's encoder block
  * output is the next encoder conv's input and the decoder skip, frcrn.py:70-75,
@@ -287,11 +313,11 @@ int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx,
  * autograd's separate gradient-accumulation add (2 reads + 1 write of an
  * activation-sized tensor) is never run. gy2 must not be NULL. Otherwise as
  * se_cbn_bwd. */
-int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, float* dx,
-                int B, int C, int HW, const float* const* params,
-                const float* save, float* const* dparams, int training,
-                int act, float slope, float* dx_amax, void* ws, size_t ws_bytes,
-                void* stream);
+int se_cbn_bwd2(const void* gy, const void* gy2, const void* x, void* dx,
+                int B, int C, int HW, const void* const* params,
+                const float* save, void* const* dparams, int training,
+                int act, float slope, float* dx_amax, const void* prelu_w, void* dprelu_w,
+                int dtype, void* ws, size_t ws_bytes, void* stream);
 
 /* Output head fused into the last ComplexBatchNorm2d (frcrn.py:115, 140-144):
  * FRCRN's final_conv = nn.Conv2d(C, 2, kernel_size=(1, 2), bias=False) applied
@@ -319,6 +345,32 @@ int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int B, int C, 
                     const float* w_head, float* dw_head, int out_channels, int kernel_w,
                     int training, int act, float slope, float* dx_amax, void* ws,
                     size_t ws_bytes, void* stream);
+
+/* First block (conv -> ComplexBatchNorm2d [+ act]) whose conv input x0 needs no
+ * gradient: a model's first, data-fed conv (FRCRN's encoder layer 0,
+ * frcrn.py:28-34, 62-76). se_cbn_bwd_first_conv is se_cbn_bwd / se_cbn_bwd2
+ * (gy2 may be NULL) with the conv's weight gradient accumulated inside the apply
+ * pass from the dL/dy0 it computes, in exact fp32 products: dL/dy0 (the conv's
+ * dy, an activation-sized tensor) is never written, and the conv's separate
+ * weight-grad pass (which reads it back) is replaced. Replaces the conv's
+ * se_conv2d_bwd_weight and the CBN's dx write. The conv is complex, bias-free,
+ * with cin = in_channels / 2 complex input channels; supported: cin = 1, kernel
+ * (5, 2) (SE_E_UNSUPPORTED otherwise). Paddings are the begin paddings (an
+ * asymmetric pad is folded in as se_conv2d_desc). x: [B, C, H, W] (the conv
+ * output = CBN input); dwr / dwi: [C/2, cin, kh, kw] (overwritten). Workspace:
+ * se_cbn_first_conv_workspace_size bytes. */
+typedef struct {
+  const float* x0;        /* conv input [B, 2*cin, in_h, in_w] */
+  int cin, in_h, in_w;
+  int kernel_h, kernel_w, stride_h, stride_w, pad_h, pad_w, dil_h, dil_w;
+  float* dwr;
+  float* dwi;
+} se_first_conv;
+size_t se_cbn_first_conv_workspace_size(int B, int C, int HW, int cin, int kh, int kw);
+int se_cbn_bwd_first_conv(const float* gy, const float* gy2, const float* x, int B, int C, int H, int W,
+                          const float* const* params, const float* save, float* const* dparams,
+                          int training, int act, float slope, const se_first_conv* fc, void* ws,
+                          size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * LSTM recurrence (torch.nn.LSTM as used by ComplexLSTM, complex_nn.py:115-145)
@@ -380,17 +432,19 @@ int se_lstm_wide_bwd(const float* dy, const float* w_hh, const float* gates,
  * act   : 0 none, 1 PReLU (act_param [1] or [C] when act_per_channel),
  *         2 ELU(elu_alpha); dact_param: the PReLU weight gradient
  * save  : device fp32 [2C] = {mean, invstd} used, written by se_bn_fwd
+ * dtype : SE_DTYPE_* of x, y, gy, dx AND weight, bias, running stats, act_param and
+ *         their gradients (a model.half() / .to(bfloat16) module); fp32 arithmetic
  * ws    : se_bn_workspace_size(B, C) bytes (training fwd and every bwd)
  * ------------------------------------------------------------------------ */
 size_t se_bn_workspace_size(int B, int C);
-int se_bn_fwd(const float* x, long long x_plane_stride, int B, int C, int HW, const float* weight,
-              const float* bias, float* running_mean, float* running_var, int training, float momentum,
-              float eps, int act, const float* act_param, int act_per_channel, float elu_alpha, float* y,
-              float* save, void* ws, size_t ws_bytes, void* stream);
-int se_bn_bwd(const float* gy, const float* x, long long x_plane_stride, int B, int C, int HW,
-              const float* weight, const float* bias, const float* save, int training, int act,
-              const float* act_param, int act_per_channel, float elu_alpha, float* dx, float* dweight,
-              float* dbias, float* dact_param, void* ws, size_t ws_bytes, void* stream);
+int se_bn_fwd(const void* x, long long x_plane_stride, int B, int C, int HW, const void* weight,
+              const void* bias, void* running_mean, void* running_var, int training, float momentum,
+              float eps, int act, const void* act_param, int act_per_channel, float elu_alpha, void* y,
+              float* save, int dtype, void* ws, size_t ws_bytes, void* stream);
+int se_bn_bwd(const void* gy, const void* x, long long x_plane_stride, int B, int C, int HW,
+              const void* weight, const void* bias, const float* save, int training, int act,
+              const void* act_param, int act_per_channel, float elu_alpha, void* dx, void* dweight,
+              void* dbias, void* dact_param, int dtype, void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------
  * Train-step glue (trainer.py:99-124, :210-221)
@@ -420,6 +474,16 @@ typedef struct se_tensor_slot {
   long long numel;
   long long offset;
 } se_tensor_slot;
+
+/* FRCRN's complex-ratio mask (frcrn.py:140-152): h = final_conv output
+ * [B, 2, half - 2, T] (half = nfft/2 + 1), spec = ConvSTFT output [B, 2*half, T];
+ * est [B, 2*half, T] = pad(tanh(pad(h, top 1)) * spec[:, :, 1:], top 1), i.e.
+ * est[b, c*half + k, t] = k < 2 ? 0 : tanh(h[b, c, k-2, t]) * spec[b, c*half + k, t].
+ * se_mask_bwd: gh = gest * spec * (1 - tanh(h)^2) on rows k >= 2 (spec takes no
+ * gradient). Replaces the pad / tanh / mul / pad / cat kernels of the reference. */
+int se_mask_fwd(const float* h, const float* spec, int B, int half, int T, float* est, void* stream);
+int se_mask_bwd(const float* gest, const float* h, const float* spec, int B, int half, int T, float* gh,
+                void* stream);
 
 size_t se_sisnr_save_bytes(int B);
 int se_sisnr_fwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,

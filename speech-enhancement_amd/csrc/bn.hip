@@ -8,6 +8,9 @@
 // One workgroup per (b, c) plane for the reductions (fp64 partial sums, no
 // atomics), a per-channel finalize that adds the B partials in order, and one
 // elementwise apply pass: fwd 2 reads + 1 write of the activation, bwd 2 + 3.
+// Storage type T (SE_DTYPE_*): fp32, or bf16 / fp16 for a model.to(bfloat16) /
+// .half() module (BASELINE config 5: CARN fp16) -- activations, parameters, running
+// statistics and the PReLU weight in T, fp32 / fp64 arithmetic; save stays fp32.
 #include "common.hpp"
 
 #include <cmath>
@@ -31,19 +34,27 @@ __device__ __forceinline__ T block_sum(T v, T* red) {
 }
 
 struct BnArgs {
-  const float* x;
+  const void* x;
   long long plane;      // x plane stride (elements)
   int B, C, HW;
-  const float* weight;  // [C] or null (affine=False)
-  const float* bias;
-  const float* act_param;   // PReLU weight: [1] or [C]
+  const void* weight;   // [C] or null (affine=False)
+  const void* bias;
+  const void* act_param;    // PReLU weight: [1] or [C]
   int act, act_per_channel;
   float elu_alpha;
 };
 
+template <typename T> __device__ __forceinline__ float ldp(const void* p, long long i, float dflt = 0.f) {
+  return p ? (float)static_cast<const T*>(p)[i] : dflt;
+}
+template <typename T> __device__ __forceinline__ void stp(void* p, long long i, float v) {
+  static_cast<T*>(p)[i] = (T)v;
+}
+
+template <typename T>
 __device__ __forceinline__ float act_fwd(const BnArgs& a, int c, float z) {
   if (a.act == kPReLU) {
-    const float w = a.act_param[a.act_per_channel ? c : 0];
+    const float w = ldp<T>(a.act_param, a.act_per_channel ? c : 0);
     return z >= 0.f ? z : w * z;                         // torch prelu: x > 0 ? x : w x (0 maps to 0 either way)
   }
   if (a.act == kELU) return z > 0.f ? z : a.elu_alpha * (expf(z) - 1.f);
@@ -51,20 +62,22 @@ __device__ __forceinline__ float act_fwd(const BnArgs& a, int c, float z) {
 }
 
 // d act / dz (as torch's backward formulas: prelu x > 0 ? 1 : w; elu x > 0 ? 1 : y + alpha)
+template <typename T>
 __device__ __forceinline__ float act_grad(const BnArgs& a, int c, float z) {
-  if (a.act == kPReLU) return z > 0.f ? 1.f : a.act_param[a.act_per_channel ? c : 0];
+  if (a.act == kPReLU) return z > 0.f ? 1.f : ldp<T>(a.act_param, a.act_per_channel ? c : 0);
   if (a.act == kELU) return z > 0.f ? 1.f : a.elu_alpha * expf(z);
   return 1.f;
 }
 
 // grid (B, C): sum x, sum x^2 of one plane -> part[(c * B + b) * 2 + {0, 1}]
+template <typename T>
 __global__ void __launch_bounds__(kThreads) bn_moments_kernel(BnArgs a, double* __restrict__ part) {
   const int b = blockIdx.x, c = blockIdx.y;
-  const float* x = a.x + ((long long)b * a.C + c) * a.plane;
+  const T* x = static_cast<const T*>(a.x) + ((long long)b * a.C + c) * a.plane;
   __shared__ double red[kThreads / 64];
   double s = 0, ss = 0;
   for (int i = threadIdx.x; i < a.HW; i += kThreads) {
-    const double v = x[i];
+    const double v = (float)x[i];
     s += v;
     ss += v * v;
   }
@@ -78,8 +91,9 @@ __global__ void __launch_bounds__(kThreads) bn_moments_kernel(BnArgs a, double* 
 
 // one thread per channel: mean, biased var -> save = {mean, invstd}; running
 // stats as torch: r = (1 - m) r + m * stat (running_var with the unbiased var)
+template <typename T>
 __global__ void bn_finalize_kernel(const double* __restrict__ part, int B, int C, long long n, float eps,
-                                   float momentum, float* __restrict__ rmean, float* __restrict__ rvar,
+                                   float momentum, void* __restrict__ rmean, void* __restrict__ rvar,
                                    float* __restrict__ save) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -93,55 +107,59 @@ __global__ void bn_finalize_kernel(const double* __restrict__ part, int B, int C
   save[c] = (float)mean;
   save[C + c] = (float)(1.0 / sqrt(var + (double)eps));
   if (rmean) {
-    rmean[c] = (1.f - momentum) * rmean[c] + momentum * (float)mean;
+    stp<T>(rmean, c, (1.f - momentum) * ldp<T>(rmean, c) + momentum * (float)mean);
     const double unbiased = n > 1 ? var * n / (n - 1) : var;
-    rvar[c] = (1.f - momentum) * rvar[c] + momentum * (float)unbiased;
+    stp<T>(rvar, c, (1.f - momentum) * ldp<T>(rvar, c) + momentum * (float)unbiased);
   }
 }
 
 // eval: save = {running mean, 1 / sqrt(running var + eps)}
-__global__ void bn_eval_stats_kernel(const float* __restrict__ rmean, const float* __restrict__ rvar, int C,
+template <typename T>
+__global__ void bn_eval_stats_kernel(const void* __restrict__ rmean, const void* __restrict__ rvar, int C,
                                      float eps, float* __restrict__ save) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
-  save[c] = rmean[c];
-  save[C + c] = 1.f / sqrtf(rvar[c] + eps);
+  save[c] = ldp<T>(rmean, c);
+  save[C + c] = 1.f / sqrtf(ldp<T>(rvar, c) + eps);
 }
 
 // grid (ceil(HW / (4 kThreads)), B * C): y = act((x - mean) * invstd * w + b)
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-bn_apply_kernel(BnArgs a, const float* __restrict__ save, float* __restrict__ y) {
+bn_apply_kernel(BnArgs a, const float* __restrict__ save, T* __restrict__ y) {
   const int bc = blockIdx.y, c = bc % a.C;
   const float mean = save[c], inv = save[a.C + c];
-  const float w = a.weight ? a.weight[c] : 1.f, bb = a.bias ? a.bias[c] : 0.f;
-  const float* x = a.x + (long long)bc * a.plane;
-  float* yo = y + (long long)bc * a.HW;
+  const float w = ldp<T>(a.weight, c, 1.f), bb = ldp<T>(a.bias, c, 0.f);
+  const T* x = static_cast<const T*>(a.x) + (long long)bc * a.plane;
+  T* yo = y + (long long)bc * a.HW;
   for (int u = 0; u < 4; ++u) {
     const int i = (blockIdx.x * 4 + u) * kThreads + threadIdx.x;
     if (i >= a.HW) return;
-    yo[i] = act_fwd(a, c, (x[i] - mean) * inv * w + bb);
+    yo[i] = (T)act_fwd<T>(a, c, ((float)x[i] - mean) * inv * w + bb);
   }
 }
 
 // grid (B, C): per plane sum g, sum g * xhat, and the PReLU weight partial
 // sum gy * z [z <= 0] (g = gy * act'(z), z recomputed from x)
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-bn_bwd_moments_kernel(BnArgs a, const float* __restrict__ gy, const float* __restrict__ save,
+bn_bwd_moments_kernel(BnArgs a, const T* __restrict__ gy, const float* __restrict__ save,
                       double* __restrict__ part) {
   const int b = blockIdx.x, c = blockIdx.y;
   const float mean = save[c], inv = save[a.C + c];
-  const float w = a.weight ? a.weight[c] : 1.f, bb = a.bias ? a.bias[c] : 0.f;
-  const float* x = a.x + ((long long)b * a.C + c) * a.plane;
-  const float* g = gy + ((long long)b * a.C + c) * a.HW;
+  const float w = ldp<T>(a.weight, c, 1.f), bb = ldp<T>(a.bias, c, 0.f);
+  const T* x = static_cast<const T*>(a.x) + ((long long)b * a.C + c) * a.plane;
+  const T* g = gy + ((long long)b * a.C + c) * a.HW;
   __shared__ double red[kThreads / 64];
   double sg = 0, sgx = 0, sa = 0;
   for (int i = threadIdx.x; i < a.HW; i += kThreads) {
-    const float xh = (x[i] - mean) * inv;
+    const float xh = ((float)x[i] - mean) * inv;
     const float z = xh * w + bb;
-    const float gz = g[i] * act_grad(a, c, z);
+    const float gi = (float)g[i];
+    const float gz = gi * act_grad<T>(a, c, z);
     sg += gz;
     sgx += (double)gz * xh;
-    if (a.act == kPReLU && !(z > 0.f)) sa += (double)g[i] * z;
+    if (a.act == kPReLU && !(z > 0.f)) sa += (double)gi * z;
   }
   sg = block_sum(sg, red);
   sgx = block_sum(sgx, red);
@@ -156,9 +174,10 @@ bn_bwd_moments_kernel(BnArgs a, const float* __restrict__ gy, const float* __res
 // per-channel means the dx pass needs -> red[c] = {sum g / n, sum g xhat / n};
 // PReLU: per-channel weight grads, or (shared weight) channel partials summed
 // by bn_act_param_kernel
+template <typename T>
 __global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int B, int C, long long n, int act,
-                                       int act_per_channel, float* __restrict__ dweight, float* __restrict__ dbias,
-                                       float* __restrict__ dact, double* __restrict__ act_part,
+                                       int act_per_channel, void* __restrict__ dweight, void* __restrict__ dbias,
+                                       void* __restrict__ dact, double* __restrict__ act_part,
                                        float* __restrict__ red) {
   const int c = blockIdx.x * blockDim.x + threadIdx.x;
   if (c >= C) return;
@@ -169,41 +188,43 @@ __global__ void bn_bwd_finalize_kernel(const double* __restrict__ part, int B, i
     sgx += p[1];
     sa += p[2];
   }
-  if (dweight) dweight[c] = (float)sgx;
-  if (dbias) dbias[c] = (float)sg;
+  if (dweight) stp<T>(dweight, c, (float)sgx);
+  if (dbias) stp<T>(dbias, c, (float)sg);
   red[c] = (float)(sg / n);
   red[C + c] = (float)(sgx / n);
   if (act == kPReLU) {
-    if (act_per_channel) dact[c] = (float)sa;
+    if (act_per_channel) stp<T>(dact, c, (float)sa);
     else act_part[c] = sa;
   }
 }
 
-__global__ void bn_act_param_kernel(const double* __restrict__ act_part, int C, float* __restrict__ dact) {
+template <typename T>
+__global__ void bn_act_param_kernel(const double* __restrict__ act_part, int C, void* __restrict__ dact) {
   __shared__ double r[kThreads / 64];
   double s = 0;
   for (int c = threadIdx.x; c < C; c += kThreads) s += act_part[c];
   s = block_sum(s, r);
-  if (threadIdx.x == 0) dact[0] = (float)s;
+  if (threadIdx.x == 0) stp<T>(dact, 0, (float)s);
 }
 
 // grid (ceil(HW / (4 kThreads)), B * C): train dx = w inv (g - mean g - xhat mean(g xhat)); eval dx = w inv g
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-bn_bwd_apply_kernel(BnArgs a, const float* __restrict__ gy, const float* __restrict__ save,
-                    const float* __restrict__ red, int training, float* __restrict__ dx) {
+bn_bwd_apply_kernel(BnArgs a, const T* __restrict__ gy, const float* __restrict__ save,
+                    const float* __restrict__ red, int training, T* __restrict__ dx) {
   const int bc = blockIdx.y, c = bc % a.C;
   const float mean = save[c], inv = save[a.C + c];
-  const float w = a.weight ? a.weight[c] : 1.f, bb = a.bias ? a.bias[c] : 0.f;
+  const float w = ldp<T>(a.weight, c, 1.f), bb = ldp<T>(a.bias, c, 0.f);
   const float mg = training ? red[c] : 0.f, mgx = training ? red[a.C + c] : 0.f;
-  const float* x = a.x + (long long)bc * a.plane;
-  const float* g = gy + (long long)bc * a.HW;
-  float* d = dx + (long long)bc * a.HW;
+  const T* x = static_cast<const T*>(a.x) + (long long)bc * a.plane;
+  const T* g = gy + (long long)bc * a.HW;
+  T* d = dx + (long long)bc * a.HW;
   for (int u = 0; u < 4; ++u) {
     const int i = (blockIdx.x * 4 + u) * kThreads + threadIdx.x;
     if (i >= a.HW) return;
-    const float xh = (x[i] - mean) * inv;
-    const float gz = g[i] * act_grad(a, c, xh * w + bb);
-    d[i] = w * inv * (gz - mg - xh * mgx);
+    const float xh = ((float)x[i] - mean) * inv;
+    const float gz = (float)g[i] * act_grad<T>(a, c, xh * w + bb);
+    d[i] = (T)(w * inv * (gz - mg - xh * mgx));
   }
 }
 
@@ -220,58 +241,96 @@ extern "C" size_t se_bn_workspace_size(int B, int C) {
                           : 0;
 }
 
-extern "C" int se_bn_fwd(const float* x, long long x_plane_stride, int B, int C, int HW, const float* weight,
-                         const float* bias, float* running_mean, float* running_var, int training, float momentum,
-                         float eps, int act, const float* act_param, int act_per_channel, float elu_alpha, float* y,
-                         float* save, void* ws, size_t ws_bytes, void* stream) {
-  BnArgs a{x, x_plane_stride, B, C, HW, weight, bias, act_param, act, act_per_channel, elu_alpha};
-  int rc = check(a);
-  if (rc) return rc;
-  if (!y || !save || (!training && (!running_mean || !running_var)) || (!running_mean != !running_var))
-    return SE_E_ARG;
-  hipStream_t st = se::as_stream(stream);
+namespace {
+
+template <typename T>
+int bn_fwd_t(const BnArgs& a, void* running_mean, void* running_var, int training, float momentum, float eps, T* y,
+             float* save, void* ws, hipStream_t st) {
+  const int B = a.B, C = a.C, HW = a.HW;
   if (training) {
-    if (!ws || ws_bytes < se_bn_workspace_size(B, C)) return SE_E_WORKSPACE;
     double* part = (double*)ws;
-    hipLaunchKernelGGL(bn_moments_kernel, dim3(B, C), dim3(kThreads), 0, st, a, part);
+    hipLaunchKernelGGL(bn_moments_kernel<T>, dim3(B, C), dim3(kThreads), 0, st, a, part);
     SE_LAUNCH_CHECK();
-    hipLaunchKernelGGL(bn_finalize_kernel, dim3(se::ceil_div(C, 64)), dim3(64), 0, st, part, B, C,
+    hipLaunchKernelGGL(bn_finalize_kernel<T>, dim3(se::ceil_div(C, 64)), dim3(64), 0, st, part, B, C,
                        (long long)B * HW, eps, momentum, running_mean, running_var, save);
   } else {
-    hipLaunchKernelGGL(bn_eval_stats_kernel, dim3(se::ceil_div(C, 64)), dim3(64), 0, st, running_mean, running_var,
-                       C, eps, save);
+    hipLaunchKernelGGL(bn_eval_stats_kernel<T>, dim3(se::ceil_div(C, 64)), dim3(64), 0, st,
+                       (const void*)running_mean, (const void*)running_var, C, eps, save);
   }
   SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(se::ceil_div(HW, 4 * kThreads), B * C), dim3(kThreads), 0, st, a,
+  hipLaunchKernelGGL(bn_apply_kernel<T>, dim3(se::ceil_div(HW, 4 * kThreads), B * C), dim3(kThreads), 0, st, a,
                      (const float*)save, y);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
 
-extern "C" int se_bn_bwd(const float* gy, const float* x, long long x_plane_stride, int B, int C, int HW,
-                         const float* weight, const float* bias, const float* save, int training, int act,
-                         const float* act_param, int act_per_channel, float elu_alpha, float* dx, float* dweight,
-                         float* dbias, float* dact_param, void* ws, size_t ws_bytes, void* stream) {
+template <typename T>
+int bn_bwd_t(const BnArgs& a, const T* gy, const float* save, int training, T* dx, void* dweight, void* dbias,
+             void* dact_param, void* ws, hipStream_t st) {
+  const int B = a.B, C = a.C, HW = a.HW;
+  double* part = (double*)ws;
+  double* act_part = part + (size_t)B * C * 3;
+  float* red = (float*)(act_part + C);
+  hipLaunchKernelGGL(bn_bwd_moments_kernel<T>, dim3(B, C), dim3(kThreads), 0, st, a, gy, save, part);
+  SE_LAUNCH_CHECK();
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<T>, dim3(se::ceil_div(C, 64)), dim3(64), 0, st, (const double*)part, B,
+                     C, (long long)B * HW, a.act, a.act_per_channel, dweight, dbias, dact_param, act_part, red);
+  SE_LAUNCH_CHECK();
+  if (a.act == kPReLU && !a.act_per_channel) {
+    hipLaunchKernelGGL(bn_act_param_kernel<T>, dim3(1), dim3(kThreads), 0, st, (const double*)act_part, C,
+                       dact_param);
+    SE_LAUNCH_CHECK();
+  }
+  hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(se::ceil_div(HW, 4 * kThreads), B * C), dim3(kThreads), 0, st,
+                     a, gy, save, (const float*)red, training, dx);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+}  // namespace
+
+extern "C" int se_bn_fwd(const void* x, long long x_plane_stride, int B, int C, int HW, const void* weight,
+                         const void* bias, void* running_mean, void* running_var, int training, float momentum,
+                         float eps, int act, const void* act_param, int act_per_channel, float elu_alpha, void* y,
+                         float* save, int dtype, void* ws, size_t ws_bytes, void* stream) {
+  BnArgs a{x, x_plane_stride, B, C, HW, weight, bias, act_param, act, act_per_channel, elu_alpha};
+  int rc = check(a);
+  if (rc) return rc;
+  if (!y || !save || (!training && (!running_mean || !running_var)) || (!running_mean != !running_var))
+    return SE_E_ARG;
+  if (training && (!ws || ws_bytes < se_bn_workspace_size(B, C))) return SE_E_WORKSPACE;
+  hipStream_t st = se::as_stream(stream);
+  switch (dtype) {
+    case SE_DTYPE_F32:
+      return bn_fwd_t<float>(a, running_mean, running_var, training, momentum, eps, (float*)y, save, ws, st);
+    case SE_DTYPE_BF16:
+      return bn_fwd_t<__bf16>(a, running_mean, running_var, training, momentum, eps, (__bf16*)y, save, ws, st);
+    case SE_DTYPE_F16:
+      return bn_fwd_t<_Float16>(a, running_mean, running_var, training, momentum, eps, (_Float16*)y, save, ws, st);
+    default:
+      return SE_E_ARG;
+  }
+}
+
+extern "C" int se_bn_bwd(const void* gy, const void* x, long long x_plane_stride, int B, int C, int HW,
+                         const void* weight, const void* bias, const float* save, int training, int act,
+                         const void* act_param, int act_per_channel, float elu_alpha, void* dx, void* dweight,
+                         void* dbias, void* dact_param, int dtype, void* ws, size_t ws_bytes, void* stream) {
   BnArgs a{x, x_plane_stride, B, C, HW, weight, bias, act_param, act, act_per_channel, elu_alpha};
   int rc = check(a);
   if (rc) return rc;
   if (!gy || !save || !dx || (act == kPReLU && !dact_param)) return SE_E_ARG;
   if (!ws || ws_bytes < se_bn_workspace_size(B, C)) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
-  double* part = (double*)ws;
-  double* act_part = part + (size_t)B * C * 3;
-  float* red = (float*)(act_part + C);
-  hipLaunchKernelGGL(bn_bwd_moments_kernel, dim3(B, C), dim3(kThreads), 0, st, a, gy, save, part);
-  SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(se::ceil_div(C, 64)), dim3(64), 0, st, (const double*)part, B, C,
-                     (long long)B * HW, act, act_per_channel, dweight, dbias, dact_param, act_part, red);
-  SE_LAUNCH_CHECK();
-  if (act == kPReLU && !act_per_channel) {
-    hipLaunchKernelGGL(bn_act_param_kernel, dim3(1), dim3(kThreads), 0, st, (const double*)act_part, C, dact_param);
-    SE_LAUNCH_CHECK();
+  switch (dtype) {
+    case SE_DTYPE_F32:
+      return bn_bwd_t<float>(a, (const float*)gy, save, training, (float*)dx, dweight, dbias, dact_param, ws, st);
+    case SE_DTYPE_BF16:
+      return bn_bwd_t<__bf16>(a, (const __bf16*)gy, save, training, (__bf16*)dx, dweight, dbias, dact_param, ws, st);
+    case SE_DTYPE_F16:
+      return bn_bwd_t<_Float16>(a, (const _Float16*)gy, save, training, (_Float16*)dx, dweight, dbias, dact_param,
+                                ws, st);
+    default:
+      return SE_E_ARG;
   }
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(se::ceil_div(HW, 4 * kThreads), B * C), dim3(kThreads), 0, st, a,
-                     gy, save, (const float*)red, training, dx);
-  SE_LAUNCH_CHECK();
-  return SE_OK;
 }

@@ -47,8 +47,28 @@ __device__ __forceinline__ float block_max(float v) {
   return v;
 }
 
-struct Ptr5 { const float* p[5]; };
-struct MPtr5 { float* p[5]; };
+// Storage types (SE_DTYPE_*): the activations, and in a bf16 / fp16 model (the
+// reference's model.to(bfloat16) / .half()) the module's parameters and running
+// statistics too, are T in memory; all arithmetic is fp32 / fp64, loads convert up
+// and stores round to nearest even. The per-channel state (save, coef) stays fp32.
+struct Ptr5 { const void* p[5]; };
+struct MPtr5 { void* p[5]; };
+template <typename T> __device__ __forceinline__ float ldv(const void* p, long long i) {
+  return (float)static_cast<const T*>(p)[i];
+}
+template <typename T> __device__ __forceinline__ void stv(void* p, long long i, float v) {
+  static_cast<T*>(p)[i] = (T)v;
+}
+// 4 consecutive elements <-> f32x4 (16-B fp32 / 8-B bf16, fp16 accesses)
+typedef float f32x4v __attribute__((ext_vector_type(4)));
+template <typename T> __device__ __forceinline__ f32x4v ld4(const T* p) {
+  typedef T T4 __attribute__((ext_vector_type(4)));
+  return __builtin_convertvector(*reinterpret_cast<const T4*>(p), f32x4v);
+}
+template <typename T> __device__ __forceinline__ void st4(T* p, f32x4v v) {
+  typedef T T4 __attribute__((ext_vector_type(4)));
+  *reinterpret_cast<T4*>(p) = __builtin_convertvector(v, T4);
+}
 
 template <int NS>
 __device__ __forceinline__ void block_reduce_store(double (&v)[NS], double* out) {
@@ -75,8 +95,9 @@ __device__ __forceinline__ float act_grad(float y, int act, float slope) {
 
 // grid (Cc, P). Row r = (b, segment) of channel c; rows strided over P.
 // ext[(c * P + p) * 4 + {0..3}] = max x_r, -min x_r, max x_i, -min x_i
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, double* part, float* ext,
+cbn_moments_kernel(const T* __restrict__ x, int B, int C, int HW, int P, double* part, float* ext,
                    float* y_amax) {
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
   if (y_amax && c == 0 && p == 0 && threadIdx.x == 0) *y_amax = 0.f;   // the finalize blocks atomicMax into it
@@ -85,8 +106,8 @@ cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, dou
   float e[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
   for (int row = p; row < B * nseg; row += P) {
     const int b = row / nseg, sg = row - b * nseg;
-    const float* xr = x + ((long long)b * C + c) * HW;
-    const float* xi = x + ((long long)b * C + Cc + c) * HW;
+    const T* xr = x + ((long long)b * C + c) * HW;
+    const T* xi = x + ((long long)b * C + Cc + c) * HW;
     const int i1 = min(HW, (sg + 1) * kSeg);
     auto body = [&](float fr, float fm) __attribute__((always_inline)) {
       e[0] = fmaxf(e[0], fr); e[1] = fmaxf(e[1], -fr); e[2] = fmaxf(e[2], fm); e[3] = fmaxf(e[3], -fm);
@@ -98,11 +119,11 @@ cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, dou
     for (; i + (U - 1) * kThreads < i1; i += U * kThreads) {
       float fr[U], fm[U];
 #pragma unroll
-      for (int u = 0; u < U; ++u) { fr[u] = xr[i + u * kThreads]; fm[u] = xi[i + u * kThreads]; }
+      for (int u = 0; u < U; ++u) { fr[u] = (float)xr[i + u * kThreads]; fm[u] = (float)xi[i + u * kThreads]; }
 #pragma unroll
       for (int u = 0; u < U; ++u) body(fr[u], fm[u]);
     }
-    for (; i < i1; i += kThreads) body(xr[i], xi[i]);
+    for (; i < i1; i += kThreads) body((float)xr[i], (float)xi[i]);
   }
   block_reduce_store<5>(v, part + ((long long)c * P + p) * 5);
 #pragma unroll
@@ -119,6 +140,7 @@ cbn_moments_kernel(const float* __restrict__ x, int B, int C, int HW, int P, dou
 // num_batches_tracked is incremented by the apply pass, after every block has
 // read it here.
 constexpr int kFinWaves = 4;
+template <typename T>
 __global__ void __launch_bounds__(64 * kFinWaves)
 cbn_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
                     Ptr5 params, int affine, MPtr5 running, int has_running,
@@ -155,13 +177,15 @@ cbn_finalize_kernel(const double* part, const float* ext, int P, double count, i
       vri = s[3] / count - mr * mi;
       vii = s[4] / count - mi * mi;
       if (has_running) {  // lerp_ in fp32 like the reference (:250-251, :272-274)
-        float* rm[5] = {running.p[0], running.p[1], running.p[2], running.p[3], running.p[4]};
         const float nv[5] = {(float)mr, (float)mi, (float)vrr, (float)vri, (float)vii};
-        for (int k = 0; k < 5; ++k) rm[k][c] = rm[k][c] + factor * (nv[k] - rm[k][c]);
+        for (int k = 0; k < 5; ++k) {
+          const float r = ldv<T>(running.p[k], c);
+          stv<T>(running.p[k], c, r + factor * (nv[k] - r));
+        }
       }
     } else {
-      mr = running.p[0][c]; mi = running.p[1][c];
-      vrr = running.p[2][c]; vri = running.p[3][c]; vii = running.p[4][c];
+      mr = ldv<T>(running.p[0], c); mi = ldv<T>(running.p[1], c);
+      vrr = ldv<T>(running.p[2], c); vri = ldv<T>(running.p[3], c); vii = ldv<T>(running.p[4], c);
     }
     vrr += eps; vii += eps;
     const double s = sqrt(vrr * vii - vri * vri);
@@ -170,12 +194,12 @@ cbn_finalize_kernel(const double* part, const float* ext, int P, double count, i
     const double urr = (s + vii) * r, uii = (s + vrr) * r, uri = -vri * r;
     double zrr = urr, zri = uri, zir = uri, zii = uii, br = 0, bi = 0;
     if (affine) {
-      const double wrr = params.p[0][c], wri = params.p[1][c], wii = params.p[2][c];
+      const double wrr = ldv<T>(params.p[0], c), wri = ldv<T>(params.p[1], c), wii = ldv<T>(params.p[2], c);
       zrr = wrr * urr + wri * uri;
       zri = wrr * uri + wri * uii;
       zir = wri * urr + wii * uri;
       zii = wri * uri + wii * uii;
-      br = params.p[3][c]; bi = params.p[4][c];
+      br = ldv<T>(params.p[3], c); bi = ldv<T>(params.p[4], c);
     }
     float* o = save + (long long)c * kSave;
     o[S_MR] = (float)mr; o[S_MI] = (float)mi;
@@ -196,11 +220,14 @@ cbn_finalize_kernel(const double* part, const float* ext, int P, double count, i
   }
 }
 
-// grid (ceil(HW / (kThreads*4)), Cc, B)
+// grid (ceil(HW / (kThreads*4)), Cc, B). pw != NULL: nn.PReLU() (one weight,
+// dccrn.py:21,45) as LeakyReLU with the slope read from the device parameter.
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-cbn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
-                 const float* __restrict__ save, int act, float slope, int64_t* nbt) {
+cbn_apply_kernel(const T* __restrict__ x, T* __restrict__ y, int C, int HW,
+                 const float* __restrict__ save, int act, float slope, int64_t* nbt, const T* pw) {
   const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  if (pw) slope = (float)pw[0];
   if (nbt && blockIdx.x == 0 && c == 0 && b == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked
   const float* s = save + c * kSave;
   const float mr = s[S_MR], mi = s[S_MI], zrr = s[S_ZRR], zri = s[S_ZRI];
@@ -211,26 +238,26 @@ cbn_apply_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int 
   for (int u = 0; u < 4; ++u) {
     const int i = base + u * kThreads;
     if (i < HW) {
-      const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+      const float xr = (float)x[offr + i] - mr, xi = (float)x[offi + i] - mi;
       float yr = zrr * xr + zri * xi + br;
       float yi = zir * xr + zii * xi + bi;
       if (act == 1) { yr = yr > 0.f ? yr : yr * slope; yi = yi > 0.f ? yi : yi * slope; }
       else if (act == 2) { yr = fmaxf(yr, 0.f); yi = fmaxf(yi, 0.f); }
-      y[offr + i] = yr;
-      y[offi + i] = yi;
+      y[offr + i] = (T)yr;
+      y[offi + i] = (T)yi;
     }
   }
 }
 
-typedef float f32x4v __attribute__((ext_vector_type(4)));
-
 // cbn_apply_kernel with 16-B accesses (HW % 4 == 0: every plane starts 16-B
 // aligned): one float4 of the real and one of the imaginary plane per thread.
 // grid (ceil(HW / (kThreads*4)), Cc, B)
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-cbn_apply4_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
-                  const float* __restrict__ save, int act, float slope, int64_t* nbt) {
+cbn_apply4_kernel(const T* __restrict__ x, T* __restrict__ y, int C, int HW,
+                  const float* __restrict__ save, int act, float slope, int64_t* nbt, const T* pw) {
   const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  if (pw) slope = (float)pw[0];
   if (nbt && blockIdx.x == 0 && c == 0 && b == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked
   const float* s = save + c * kSave;
   const float mr = s[S_MR], mi = s[S_MI], zrr = s[S_ZRR], zri = s[S_ZRI];
@@ -238,8 +265,8 @@ cbn_apply4_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int
   const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
   const int i = (blockIdx.x * kThreads + threadIdx.x) * 4;
   if (i >= HW) return;
-  const f32x4v xr4 = *reinterpret_cast<const f32x4v*>(x + offr + i);
-  const f32x4v xi4 = *reinterpret_cast<const f32x4v*>(x + offi + i);
+  const f32x4v xr4 = ld4(x + offr + i);
+  const f32x4v xi4 = ld4(x + offi + i);
   f32x4v yr4, yi4;
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
@@ -251,8 +278,8 @@ cbn_apply4_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int
     yr4[u] = yr;
     yi4[u] = yi;
   }
-  *reinterpret_cast<f32x4v*>(y + offr + i) = yr4;
-  *reinterpret_cast<f32x4v*>(y + offi + i) = yi4;
+  st4(y + offr + i, yr4);
+  st4(y + offi + i, yi4);
 }
 
 // Output head of FRCRN (frcrn.py:115, 140-144): final_conv = nn.Conv2d(C, 2, (1, 2),
@@ -304,14 +331,18 @@ __device__ __forceinline__ float act_fwd(float z, int act, float slope) {
 // gy + gy2 (SRC 1: a forked output, se_cbn_bwd2, summed on the fly) or formed
 // from the head gradient (SRC 2, see HeadArgs; then the head's 8 weight-grad
 // sums per complex channel follow the 6 below in part, stride NS).
-// sums: gr, gi, gr*xtr, gr*xti, gi*xtr, gi*xti
-template <int SRC>
+// sums: gr, gi, gr*xtr, gr*xti, gi*xtr, gi*xti; PR (nn.PReLU, slope from pw): a 7th,
+// sum dL/dy * z [z <= 0] over both planes (the PReLU weight's gradient)
+template <int SRC, typename T = float, bool PR = false>
 __global__ void __launch_bounds__(kThreads)
-cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
-                       const float* __restrict__ x, int B, int C, int HW, int P,
+cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
+                       const T* __restrict__ x, int B, int C, int HW, int P,
                        const float* __restrict__ save, int act, float slope, double* part, float* ext,
-                       float* dx_amax, HeadArgs hd) {
-  constexpr int NS = SRC == 2 ? 6 + kHeadNS : 6;
+                       float* dx_amax, HeadArgs hd, const T* pw) {
+  static_assert(!PR || SRC != 2, "no PReLU on the head path");
+  static_assert(SRC != 2 || sizeof(T) == 4, "the head path is fp32");
+  constexpr int NS = SRC == 2 ? 6 + kHeadNS : (PR ? 7 : 6);
+  if (PR) slope = (float)pw[0];
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
   if (dx_amax && c == 0 && p == 0 && threadIdx.x == 0) *dx_amax = 0.f;   // the finalize blocks atomicMax into it
   const int nseg = (HW + kSeg - 1) / kSeg;
@@ -341,6 +372,7 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
       v[0] += gr; v[1] += gi;
       v[2] += (double)gr * xr; v[3] += (double)gr * xi;
       v[4] += (double)gi * xr; v[5] += (double)gi * xi;
+      if constexpr (PR) v[NS - 1] += (zr <= 0.f ? (double)dyr * zr : 0.0) + (zi <= 0.f ? (double)dyi * zi : 0.0);
       if (SRC == 2) {
         const double yr = act_fwd(zr, act, slope), yi = act_fwd(zi, act, slope);
 #pragma unroll
@@ -360,8 +392,8 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
         HeadG hg[U];
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          fr[u] = x[offr + i + u * kThreads];
-          fm[u] = x[offi + i + u * kThreads];
+          fr[u] = (float)x[offr + i + u * kThreads];
+          fm[u] = (float)x[offi + i + u * kThreads];
           hg[u] = head_g(hd, b, H, hr, ht);
           ht += kThreads;
           while (ht >= hd.W) { ht -= hd.W; ++hr; }
@@ -371,7 +403,7 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
       }
       for (; i < i1; i += kThreads) {
         const HeadG hg = head_g(hd, b, H, hr, ht);
-        body(x[offr + i], x[offi + i], head_gy(hg, wcr, C), head_gy(hg, wci, C), hg);
+        body((float)x[offr + i], (float)x[offi + i], head_gy(hg, wcr, C), head_gy(hg, wci, C), hg);
         ht += kThreads;
         while (ht >= hd.W) { ht -= hd.W; ++hr; }
       }
@@ -383,18 +415,18 @@ cbn_bwd_moments_kernel(const float* __restrict__ gy, const float* __restrict__ g
 #pragma unroll
         for (int u = 0; u < U; ++u) {
           const int j = i + u * kThreads;
-          fr[u] = x[offr + j];
-          fm[u] = x[offi + j];
-          dr[u] = SRC == 1 ? gy[offr + j] + gy2[offr + j] : gy[offr + j];
-          dm[u] = SRC == 1 ? gy[offi + j] + gy2[offi + j] : gy[offi + j];
+          fr[u] = (float)x[offr + j];
+          fm[u] = (float)x[offi + j];
+          dr[u] = SRC == 1 ? (float)gy[offr + j] + (float)gy2[offr + j] : (float)gy[offr + j];
+          dm[u] = SRC == 1 ? (float)gy[offi + j] + (float)gy2[offi + j] : (float)gy[offi + j];
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) body(fr[u], fm[u], dr[u], dm[u], none);
       }
       for (; i < i1; i += kThreads) {
-        const float dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
-        const float dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
-        body(x[offr + i], x[offi + i], dyr, dyi, none);
+        const float dyr = SRC == 1 ? (float)gy[offr + i] + (float)gy2[offr + i] : (float)gy[offr + i];
+        const float dyi = SRC == 1 ? (float)gy[offi + i] + (float)gy2[offi + i] : (float)gy[offi + i];
+        body((float)x[offr + i], (float)x[offi + i], dyr, dyi, none);
       }
     }
   }
@@ -416,13 +448,14 @@ constexpr int kCoef = 16;
 // *dx_amax by atomicMax (zeroed by the backward moments pass).
 // HEAD: part holds the head's 8 weight-grad sums after the 6 moments (stride
 // 6 + kHeadNS); they are added in the same fixed order and written to dwh.
-template <bool HEAD>
+// PR: the 7th sum (the PReLU weight's gradient, per channel) goes to pw_part[c]
+template <bool HEAD, typename T = float, bool PR = false>
 __global__ void __launch_bounds__(64 * kFinWaves)
 cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
                         const float* save, Ptr5 params, int affine,
                         MPtr5 dparams, int has_dparams, int training,
-                        float* coef, float* dx_amax, float* dwh) {
-  constexpr int NS = HEAD ? 6 + kHeadNS : 6;
+                        float* coef, float* dx_amax, float* dwh, double* pw_part) {
+  constexpr int NS = HEAD ? 6 + kHeadNS : (PR ? 7 : 6);
   const int lane = threadIdx.x & 63;
   const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
   if (c >= Cc) return;
@@ -441,6 +474,7 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
   gmr = se::wave_max(gmr);
   gmi = se::wave_max(gmi);
   if (lane != 0) return;
+  if constexpr (PR) pw_part[c] = sm[NS - 1];
   if (HEAD) {   // dw[o, ch, k] at (o * C + ch) * KW + k, C = 2 Cc
     const int C = 2 * Cc;
 #pragma unroll
@@ -459,18 +493,18 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
     // dZ = sum g xt^T
     const double dz00 = sm[2], dz01 = sm[3], dz10 = sm[4], dz11 = sm[5];
     double wrr = 1, wri = 0, wii = 1;
-    if (affine) { wrr = params.p[0][c]; wri = params.p[1][c]; wii = params.p[2][c]; }
+    if (affine) { wrr = ldv<T>(params.p[0], c); wri = ldv<T>(params.p[1], c); wii = ldv<T>(params.p[2], c); }
     double gurr, guri, guii;
     if (affine) {
       // dW = dZ U (U symmetric); W symmetric -> Wri collects both off-diagonals
       const double dw00 = dz00 * urr + dz01 * uri, dw01 = dz00 * uri + dz01 * uii;
       const double dw10 = dz10 * urr + dz11 * uri, dw11 = dz10 * uri + dz11 * uii;
       if (has_dparams) {
-        dparams.p[0][c] = (float)dw00;
-        dparams.p[1][c] = (float)(dw01 + dw10);
-        dparams.p[2][c] = (float)dw11;
-        dparams.p[3][c] = (float)sm[0];
-        dparams.p[4][c] = (float)sm[1];
+        stv<T>(dparams.p[0], c, (float)dw00);
+        stv<T>(dparams.p[1], c, (float)(dw01 + dw10));
+        stv<T>(dparams.p[2], c, (float)dw11);
+        stv<T>(dparams.p[3], c, (float)sm[0]);
+        stv<T>(dparams.p[4], c, (float)sm[1]);
       }
       // dU = W^T dZ = W dZ
       gurr = wrr * dz00 + wri * dz10;
@@ -513,12 +547,13 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
   }
 }
 
-template <int SRC>   // dL/dy source as cbn_bwd_moments_kernel
+template <int SRC, typename T = float>   // dL/dy source as cbn_bwd_moments_kernel
 __global__ void __launch_bounds__(kThreads)
-cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
-                     const float* __restrict__ x, float* __restrict__ dx, int C, int HW,
-                     const float* __restrict__ coef, int act, float slope, HeadArgs hd) {
+cbn_bwd_apply_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
+                     const T* __restrict__ x, T* __restrict__ dx, int C, int HW,
+                     const float* __restrict__ coef, int act, float slope, HeadArgs hd, const T* pw) {
   const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  if (pw) slope = (float)pw[0];
   const float* k = coef + c * kCoef;
   const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
   const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
@@ -531,7 +566,7 @@ cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ gy2
   for (int u = 0; u < 4; ++u) {
     const int i = base + u * kThreads;
     if (i < HW) {
-      const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+      const float xr = (float)x[offr + i] - mr, xi = (float)x[offi + i] - mi;
       const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
       float dyr, dyi;
       if (SRC == 2) {
@@ -540,25 +575,26 @@ cbn_bwd_apply_kernel(const float* __restrict__ gy, const float* __restrict__ gy2
         dyr = head_gy(hg, hd.w + c * kHeadKW, C);
         dyi = head_gy(hg, hd.w + (Cc + c) * kHeadKW, C);
       } else {
-        dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
-        dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
+        dyr = SRC == 1 ? (float)gy[offr + i] + (float)gy2[offr + i] : (float)gy[offr + i];
+        dyi = SRC == 1 ? (float)gy[offi + i] + (float)gy2[offi + i] : (float)gy[offi + i];
       }
       const float gr = dyr * act_grad(zr, act, slope) - gbr;
       const float gi = dyi * act_grad(zi, act, slope) - gbi;
-      dx[offr + i] = a00 * gr + a01 * gi + grr * xr + gri * xi;
-      dx[offi + i] = a10 * gr + a11 * gi + gri * xr + gii * xi;
+      dx[offr + i] = (T)(a00 * gr + a01 * gi + grr * xr + gri * xi);
+      dx[offi + i] = (T)(a10 * gr + a11 * gi + gri * xr + gii * xi);
     }
   }
 }
 
 // cbn_bwd_apply_kernel<SRC 0 / 1> with 16-B accesses (HW % 4 == 0)
-template <int SRC>
+template <int SRC, typename T = float>
 __global__ void __launch_bounds__(kThreads)
-cbn_bwd_apply4_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
-                      const float* __restrict__ x, float* __restrict__ dx, int C, int HW,
-                      const float* __restrict__ coef, int act, float slope) {
+cbn_bwd_apply4_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
+                      const T* __restrict__ x, T* __restrict__ dx, int C, int HW,
+                      const float* __restrict__ coef, int act, float slope, const T* pw) {
   static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
   const int Cc = C / 2, c = blockIdx.y, b = blockIdx.z;
+  if (pw) slope = (float)pw[0];
   const float* k = coef + c * kCoef;
   const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
   const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
@@ -566,13 +602,13 @@ cbn_bwd_apply4_kernel(const float* __restrict__ gy, const float* __restrict__ gy
   const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
   const int i = (blockIdx.x * kThreads + threadIdx.x) * 4;
   if (i >= HW) return;
-  const f32x4v xr4 = *reinterpret_cast<const f32x4v*>(x + offr + i);
-  const f32x4v xi4 = *reinterpret_cast<const f32x4v*>(x + offi + i);
-  f32x4v gr4 = *reinterpret_cast<const f32x4v*>(gy + offr + i);
-  f32x4v gi4 = *reinterpret_cast<const f32x4v*>(gy + offi + i);
+  const f32x4v xr4 = ld4(x + offr + i);
+  const f32x4v xi4 = ld4(x + offi + i);
+  f32x4v gr4 = ld4(gy + offr + i);
+  f32x4v gi4 = ld4(gy + offi + i);
   if (SRC == 1) {
-    gr4 += *reinterpret_cast<const f32x4v*>(gy2 + offr + i);
-    gi4 += *reinterpret_cast<const f32x4v*>(gy2 + offi + i);
+    gr4 += ld4(gy2 + offr + i);
+    gi4 += ld4(gy2 + offi + i);
   }
   f32x4v dr4, di4;
 #pragma unroll
@@ -584,8 +620,111 @@ cbn_bwd_apply4_kernel(const float* __restrict__ gy, const float* __restrict__ gy
     dr4[u] = a00 * gr + a01 * gi + grr * xr + gri * xi;
     di4[u] = a10 * gr + a11 * gi + gri * xr + gii * xi;
   }
-  *reinterpret_cast<f32x4v*>(dx + offr + i) = dr4;
-  *reinterpret_cast<f32x4v*>(dx + offi + i) = di4;
+  st4(dx + offr + i, dr4);
+  st4(dx + offi + i, di4);
+}
+
+// sum over the channels (fixed order, fp64) of the per-channel PReLU weight-grad sums
+template <typename T>
+__global__ void prelu_grad_finish_kernel(const double* pw_part, int Cc, T* dpw) {
+  if (threadIdx.x != 0) return;
+  double s = 0.0;
+  for (int c = 0; c < Cc; ++c) s += pw_part[c];
+  dpw[0] = (T)(float)s;
+}
+
+// First block's conv weight gradient fused into the backward apply (se_cbn_bwd_first_conv).
+// The block is conv -> CBN (+ act) with a conv input x0 that needs no gradient (a
+// model's first, data-fed conv: FRCRN's encoder layer 0, frcrn.py:28-34). The apply
+// pass computes dL/dy0 = dx at each position anyway; instead of writing it (the
+// conv's dy, one activation-sized tensor) for a separate weight-grad GEMM to read
+// back, each thread multiplies it into the conv's gathered input taps right away:
+//   dWr[c, ci, t] += gr * xr + gi * xi,   dWi[c, ci, t] += gi * xr - gr * xi
+// (complex_nn.py:52-65: re = Wr*xr - Wi*xi, im = Wi*xr + Wr*xi), xr / xi the real /
+// imaginary input channel ci at tap t of the position (zero outside the grid).
+// Exact fp32 products, per-thread sums in position order, a fixed-order block
+// reduction; per (channel, batch item) partials summed over the items in fp64 by
+// cbn_first_conv_finish_kernel. grid (Cc, B), one workgroup per (channel, item) plane.
+struct FirstConv {
+  const float* x0;    // [B, 2 cin, Hi, Wi]
+  int Hi, Wi, sh, sw, ph, pw, dh, dw;
+  float* dwr;         // [Cc, cin, KH, KW]
+  float* dwi;
+};
+
+template <int SRC, int CIN, int KH, int KW>
+__global__ void __launch_bounds__(kThreads)
+cbn_bwd_apply_fc_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
+                        const float* __restrict__ x, int C, int HW, int W, const float* __restrict__ coef,
+                        int act, float slope, FirstConv fc, float* __restrict__ wpart) {
+  static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
+  constexpr int NT = CIN * KH * KW, NE = 2 * NT;
+  const int Cc = C / 2, c = blockIdx.x, b = blockIdx.y, B = gridDim.y;
+  const float* k = coef + c * kCoef;
+  const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
+  const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
+  const float br = k[11], bi = k[12];
+  const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+  const long long HiWi = (long long)fc.Hi * fc.Wi;
+  const float* x0r = fc.x0 + (long long)b * 2 * CIN * HiWi;
+  const float* x0i = x0r + CIN * HiWi;
+  float acc[NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) acc[e] = 0.f;
+  for (int i = threadIdx.x; i < HW; i += kThreads) {
+    const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+    const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
+    const float dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
+    const float dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
+    const float g1 = dyr * act_grad(zr, act, slope) - gbr;
+    const float g2 = dyi * act_grad(zi, act, slope) - gbi;
+    const float gr = a00 * g1 + a01 * g2 + grr * xr + gri * xi;   // dL/dy0 (the conv's dy), never stored
+    const float gi = a10 * g1 + a11 * g2 + gri * xr + gii * xi;
+    const int qh = i / W, qw = i - qh * W;
+#pragma unroll
+    for (int th = 0; th < KH; ++th) {
+      const int h = qh * fc.sh + th * fc.dh - fc.ph;
+      const bool hok = (unsigned)h < (unsigned)fc.Hi;
+#pragma unroll
+      for (int tw = 0; tw < KW; ++tw) {
+        const int w = qw * fc.sw + tw * fc.dw - fc.pw;
+        const bool ok = hok & ((unsigned)w < (unsigned)fc.Wi);
+        const long long o = ok ? (long long)h * fc.Wi + w : 0;
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) {
+          const float vr = ok ? x0r[ci * HiWi + o] : 0.f;
+          const float vi = ok ? x0i[ci * HiWi + o] : 0.f;
+          const int e = 2 * ((ci * KH + th) * KW + tw);
+          acc[e] = fmaf(gr, vr, fmaf(gi, vi, acc[e]));
+          acc[e + 1] = fmaf(gi, vr, fmaf(-gr, vi, acc[e + 1]));
+        }
+      }
+    }
+  }
+  __shared__ float red[kThreads / 64][NE];
+#pragma unroll
+  for (int e = 0; e < NE; ++e) {
+    const float v = se::wave_sum(acc[e]);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][e] = v;
+  }
+  __syncthreads();
+  if (threadIdx.x < NE) {
+    float s = 0.f;
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) s += red[w][threadIdx.x];
+    wpart[((long long)c * B + b) * NE + threadIdx.x] = s;
+  }
+}
+
+// dWr / dWi[c, ci, t] = sum over the B items (fixed order, fp64) of the partials.
+// grid (Cc), block NE threads
+__global__ void cbn_first_conv_finish_kernel(const float* __restrict__ wpart, int B, int NE, float* dwr, float* dwi) {
+  const int c = blockIdx.x, e = threadIdx.x;
+  if (e >= NE) return;
+  double s = 0.0;
+  for (int b = 0; b < B; ++b) s += wpart[((long long)c * B + b) * NE + e];
+  const int NT = NE / 2;
+  (e & 1 ? dwi : dwr)[(long long)c * NT + (e >> 1)] = (float)s;
 }
 
 // Forward of the head: out[b, o, h, t] = sum_c sum_k w[o, c, k] y_c(h, t + k),
@@ -673,77 +812,109 @@ int pick_P(int B, int Cc, int HW) {
 
 }  // namespace
 
-// workspace: part [Cc][P][ns] doubles, coef [Cc][kCoef], ext [Cc][P][4] floats;
-// ns = 6 (5 forward moments), or 6 + kHeadNS for the head's backward
+// workspace: part [Cc][P][ns] doubles, coef [Cc][kCoef], ext [Cc][P][4] floats, then
+// pw_part [Cc] doubles; ns = 7 (5 forward moments, 6 backward (+1 PReLU)), or 6 +
+// kHeadNS for the head's backward
 static size_t ws_bytes_ns(int B, int C, int HW, int ns) {
   if (B <= 0 || C <= 0 || HW <= 0) return 0;
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
   return (size_t)Cc * P * ns * sizeof(double) + (size_t)Cc * kCoef * sizeof(float) +
-         (size_t)Cc * P * 4 * sizeof(float) + 512;
+         (size_t)Cc * P * 4 * sizeof(float) + (size_t)Cc * sizeof(double) + 512;
 }
 
-extern "C" size_t se_cbn_workspace_size(int B, int C, int HW) { return ws_bytes_ns(B, C, HW, 6); }
+extern "C" size_t se_cbn_workspace_size(int B, int C, int HW) { return ws_bytes_ns(B, C, HW, 7); }
 
 extern "C" size_t se_cbn_head_workspace_size(int B, int C, int HW) {
   return ws_bytes_ns(B, C, HW, 6 + kHeadNS);
+}
+
+// the backward's workspace, then the first conv's [Cc][B][2 cin kh kw] partials
+extern "C" size_t se_cbn_first_conv_workspace_size(int B, int C, int HW, int cin, int kh, int kw) {
+  if (B <= 0 || C <= 0 || HW <= 0 || cin <= 0 || kh <= 0 || kw <= 0) return 0;
+  return ws_bytes_ns(B, C, HW, 7) + 256 + (size_t)(C / 2) * B * 2 * cin * kh * kw * sizeof(float);
 }
 
 // per-(channel, partition) extrema of the moments passes, after part and coef
 static float* coef_of(void* ws, int Cc, int P, int ns) {
   return (float*)((char*)ws + (size_t)Cc * P * ns * sizeof(double));
 }
-static float* ext_of(void* ws, int Cc, int P, int ns = 6) {
+static float* ext_of(void* ws, int Cc, int P, int ns) {
   return (float*)((char*)coef_of(ws, Cc, P, ns) + (size_t)Cc * kCoef * sizeof(float));
+}
+static double* pwpart_of(void* ws, int Cc, int P, int ns) {
+  return (double*)(((uintptr_t)(ext_of(ws, Cc, P, ns) + (size_t)Cc * P * 4) + 7) & ~(uintptr_t)7);
 }
 
 namespace {
 
 // moments + finalize of the training forward (running update, save, y bound)
-int cbn_stats(const float* x, int B, int C, int HW, const float* const* params, float* const* running,
+template <typename T>
+int cbn_stats(const T* x, int B, int C, int HW, const void* const* params, void* const* running,
               int64_t* nbt, float* save, int training, float eps, float momentum, float* y_amax,
               void* ws, hipStream_t st) {
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
   double* part = (double*)ws;
-  float* ext = ext_of(ws, Cc, P);
+  float* ext = ext_of(ws, Cc, P, 7);
   Ptr5 pp{};
   MPtr5 rp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (running) for (int k = 0; k < 5; ++k) rp.p[k] = running[k];
   if (training) {
-    hipLaunchKernelGGL(cbn_moments_kernel, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part, ext,
+    hipLaunchKernelGGL(cbn_moments_kernel<T>, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part, ext,
                        y_amax);
     SE_LAUNCH_CHECK();
   }
-  hipLaunchKernelGGL(cbn_finalize_kernel, dim3(se::ceil_div(Cc, kFinWaves)), dim3(64 * kFinWaves), 0, st, part,
+  hipLaunchKernelGGL(cbn_finalize_kernel<T>, dim3(se::ceil_div(Cc, kFinWaves)), dim3(64 * kFinWaves), 0, st, part,
                      ext, P, (double)B * HW, Cc, pp, params ? 1 : 0, rp, running ? 1 : 0, (const int64_t*)nbt, save,
                      training, eps, momentum, training ? y_amax : nullptr);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
 
+template <typename T>
+int cbn_fwd_t(const T* x, T* y, int B, int C, int HW, const void* const* params, void* const* running,
+              int64_t* nbt, float* save, int training, float eps, float momentum, int act, float slope,
+              float* y_amax, const T* pw, void* ws, hipStream_t st) {
+  const int rc = cbn_stats<T>(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st);
+  if (rc != SE_OK) return rc;
+  int64_t* nb = (training && running) ? nbt : nullptr;
+  const dim3 grid(se::ceil_div(HW, kThreads * 4), C / 2, B);
+  if (HW % 4 == 0 && vec_ok())
+    hipLaunchKernelGGL(cbn_apply4_kernel<T>, grid, dim3(kThreads), 0, st, x, y, C, HW, save, act, slope, nb, pw);
+  else
+    hipLaunchKernelGGL(cbn_apply_kernel<T>, grid, dim3(kThreads), 0, st, x, y, C, HW, save, act, slope, nb, pw);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+bool act_ok(int act, const void* prelu_w) { return act >= 0 && act <= 2 && (!prelu_w || act == 1); }
+
 }  // namespace
 
-extern "C" int se_cbn_fwd(const float* x, float* y, int B, int C, int HW,
-                          const float* const* params, float* const* running, int64_t* nbt,
+extern "C" int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
+                          const void* const* params, void* const* running, int64_t* nbt,
                           float* save, int training, float eps, float momentum, int act,
-                          float slope, float* y_amax, void* ws, size_t ws_bytes, void* stream) {
-  if (!x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || act < 0 || act > 2)
-    return SE_E_ARG;
+                          float slope, float* y_amax, const void* prelu_w, int dtype, void* ws, size_t ws_bytes,
+                          void* stream) {
+  if (!x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || !act_ok(act, prelu_w)) return SE_E_ARG;
   if (!training && !running) return SE_E_ARG;  // eval needs running statistics
   if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
-  const int rc = cbn_stats(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st);
-  if (rc != SE_OK) return rc;
-  if (HW % 4 == 0 && vec_ok())
-    hipLaunchKernelGGL(cbn_apply4_kernel, dim3(se::ceil_div(HW, kThreads * 4), C / 2, B), dim3(kThreads),
-                       0, st, x, y, C, HW, save, act, slope, (training && running) ? nbt : nullptr);
-  else
-    hipLaunchKernelGGL(cbn_apply_kernel, dim3(se::ceil_div(HW, kThreads * 4), C / 2, B), dim3(kThreads),
-                       0, st, x, y, C, HW, save, act, slope, (training && running) ? nbt : nullptr);
-  SE_LAUNCH_CHECK();
-  return SE_OK;
+  switch (dtype) {
+    case SE_DTYPE_F32:
+      return cbn_fwd_t<float>((const float*)x, (float*)y, B, C, HW, params, running, nbt, save, training, eps,
+                              momentum, act, slope, y_amax, (const float*)prelu_w, ws, st);
+    case SE_DTYPE_BF16:
+      return cbn_fwd_t<__bf16>((const __bf16*)x, (__bf16*)y, B, C, HW, params, running, nbt, save, training, eps,
+                               momentum, act, slope, y_amax, (const __bf16*)prelu_w, ws, st);
+    case SE_DTYPE_F16:
+      return cbn_fwd_t<_Float16>((const _Float16*)x, (_Float16*)y, B, C, HW, params, running, nbt, save, training,
+                                 eps, momentum, act, slope, y_amax, (const _Float16*)prelu_w, ws, st);
+    default:
+      return SE_E_ARG;
+  }
 }
 
 extern "C" int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, int W,
@@ -759,7 +930,8 @@ extern "C" int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, 
   const int HW = H * W;
   if (ws_bytes < se_cbn_head_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
-  const int rc = cbn_stats(x, B, C, HW, params, running, nbt, save, training, eps, momentum, nullptr, ws, st);
+  const int rc = cbn_stats<float>(x, B, C, HW, (const void* const*)params, (void* const*)running, nbt, save,
+                                  training, eps, momentum, nullptr, ws, st);
   if (rc != SE_OK) return rc;
   const long long waves = (long long)B * ((HW + 62) / 63);
   const size_t lds = ((size_t)(C / 2) * 8 + (size_t)kHeadNO * C * kHeadKW) * sizeof(float);
@@ -772,85 +944,151 @@ extern "C" int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, 
 
 namespace {
 
-// src 0: gy, 1: gy + gy2, 2: the head gradient (hd)
-int cbn_bwd_impl(int src, const float* gy, const float* gy2, const HeadArgs& hd, const float* x, float* dx,
-                 int B, int C, int HW, const float* const* params, const float* save, float* const* dparams,
+// src 0: gy, 1: gy + gy2, 2: the head gradient (hd). fc != NULL: the first block's
+// conv weight gradient replaces the dx write (cbn_bwd_apply_fc_kernel; dx unused).
+// pw / dpw: nn.PReLU's weight and its gradient (act 1 with the slope read from pw).
+template <typename T>
+int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T* x, T* dx,
+                 int B, int C, int HW, const void* const* params, const float* save, void* const* dparams,
                  int training, int act, float slope, float* dx_amax, float* dwh, void* ws, size_t ws_bytes,
-                 void* stream) {
-  const int ns = src == 2 ? 6 + kHeadNS : 6;
+                 void* stream, const FirstConv* fc = nullptr, int fc_w = 0, const T* pw = nullptr,
+                 T* dpw = nullptr) {
+  const int ns = src == 2 ? 6 + kHeadNS : 7;
   if (ws_bytes < ws_bytes_ns(B, C, HW, ns) || !ws) return SE_E_WORKSPACE;
+  if (pw && (src == 2 || fc || !dpw)) return SE_E_ARG;
   hipStream_t st = se::as_stream(stream);
   const int Cc = C / 2;
   const int P = pick_P(B, Cc, HW);
   double* part = (double*)ws;
   float* coef = coef_of(ws, Cc, P, ns);
   float* ext = ext_of(ws, Cc, P, ns);
+  double* pwp = pwpart_of(ws, Cc, P, ns);
   Ptr5 pp{};
   MPtr5 dp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (dparams) for (int k = 0; k < 5; ++k) dp.p[k] = dparams[k];
   float* xa = training ? dx_amax : nullptr;
   const dim3 mg(Cc, P), mb(kThreads);
-  if (src == 1)
-    hipLaunchKernelGGL(cbn_bwd_moments_kernel<1>, mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd);
-  else if (src == 2)
-    hipLaunchKernelGGL(cbn_bwd_moments_kernel<2>, mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd);
-  else
-    hipLaunchKernelGGL(cbn_bwd_moments_kernel<0>, mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd);
+  const bool pr = pw != nullptr;
+  if constexpr (sizeof(T) == 4) {
+    if (src == 2)
+      hipLaunchKernelGGL((cbn_bwd_moments_kernel<2, float>), mg, mb, 0, st, (const float*)gy, (const float*)gy2,
+                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr);
+  }
+  if (src == 1 && pr)
+    hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
+                       slope, part, ext, xa, hd, pw);
+  else if (src == 1)
+    hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
+                       part, ext, xa, hd, pw);
+  else if (src == 0 && pr)
+    hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
+                       slope, part, ext, xa, hd, pw);
+  else if (src == 0)
+    hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
+                       part, ext, xa, hd, pw);
   SE_LAUNCH_CHECK();
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
   if (src == 2)
-    hipLaunchKernelGGL(cbn_bwd_finalize_kernel<true>, fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
-                       params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, dwh);
+    hipLaunchKernelGGL((cbn_bwd_finalize_kernel<true, T>), fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
+                       params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, dwh, pwp);
+  else if (pr)
+    hipLaunchKernelGGL((cbn_bwd_finalize_kernel<false, T, true>), fg, fb, 0, st, part, ext, P, (double)B * HW, Cc,
+                       save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, nullptr, pwp);
   else
-    hipLaunchKernelGGL(cbn_bwd_finalize_kernel<false>, fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
-                       params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, nullptr);
+    hipLaunchKernelGGL((cbn_bwd_finalize_kernel<false, T>), fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save,
+                       pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, nullptr, pwp);
   SE_LAUNCH_CHECK();
+  if (pr) {
+    hipLaunchKernelGGL(prelu_grad_finish_kernel<T>, dim3(1), dim3(64), 0, st, pwp, Cc, dpw);
+    SE_LAUNCH_CHECK();
+  }
+  if (fc) {   // (checked by the entry point: FRCRN's first conv, cin 1, kernel (5, 2); fp32)
+    if constexpr (sizeof(T) == 4) {
+      float* wpart = (float*)(((uintptr_t)ws + ws_bytes_ns(B, C, HW, 7) + 255) & ~(uintptr_t)255);
+      if (src == 1)
+        hipLaunchKernelGGL((cbn_bwd_apply_fc_kernel<1, 1, 5, 2>), dim3(Cc, B), mb, 0, st, (const float*)gy,
+                           (const float*)gy2, (const float*)x, C, HW, fc_w, coef, act, slope, *fc, wpart);
+      else
+        hipLaunchKernelGGL((cbn_bwd_apply_fc_kernel<0, 1, 5, 2>), dim3(Cc, B), mb, 0, st, (const float*)gy,
+                           (const float*)gy2, (const float*)x, C, HW, fc_w, coef, act, slope, *fc, wpart);
+      SE_LAUNCH_CHECK();
+      hipLaunchKernelGGL(cbn_first_conv_finish_kernel, dim3(Cc), dim3(64), 0, st, wpart, B, 20, fc->dwr, fc->dwi);
+      SE_LAUNCH_CHECK();
+      return SE_OK;
+    }
+    return SE_E_UNSUPPORTED;
+  }
   const dim3 grid(se::ceil_div(HW, kThreads * 4), Cc, B);
   const bool v4 = HW % 4 == 0 && vec_ok();
   if (src == 1 && v4)
-    hipLaunchKernelGGL(cbn_bwd_apply4_kernel<1>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope);
+    hipLaunchKernelGGL((cbn_bwd_apply4_kernel<1, T>), grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, pw);
   else if (src == 0 && v4)
-    hipLaunchKernelGGL(cbn_bwd_apply4_kernel<0>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope);
+    hipLaunchKernelGGL((cbn_bwd_apply4_kernel<0, T>), grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, pw);
   else if (src == 1)
-    hipLaunchKernelGGL(cbn_bwd_apply_kernel<1>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);
-  else if (src == 2)
-    hipLaunchKernelGGL(cbn_bwd_apply_kernel<2>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);
-  else
-    hipLaunchKernelGGL(cbn_bwd_apply_kernel<0>, grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd);
+    hipLaunchKernelGGL((cbn_bwd_apply_kernel<1, T>), grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd,
+                       pw);
+  else if (src == 2) {
+    if constexpr (sizeof(T) == 4)
+      hipLaunchKernelGGL((cbn_bwd_apply_kernel<2, float>), grid, mb, 0, st, (const float*)gy, (const float*)gy2,
+                         (const float*)x, (float*)dx, C, HW, coef, act, slope, hd, (const float*)nullptr);
+  } else
+    hipLaunchKernelGGL((cbn_bwd_apply_kernel<0, T>), grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, hd,
+                       pw);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
 
-bool bwd_args_ok(const float* x, const float* dx, const float* save, int B, int C, int HW) {
+bool bwd_args_ok(const void* x, const void* dx, const float* save, int B, int C, int HW) {
   return x && dx && save && B > 0 && C > 0 && !(C & 1) && HW > 0;
+}
+
+int cbn_bwd_dtype(int src, const void* gy, const void* gy2, const void* x, void* dx, int B, int C, int HW,
+                  const void* const* params, const float* save, void* const* dparams, int training, int act,
+                  float slope, float* dx_amax, const void* pw, void* dpw, int dtype, void* ws, size_t ws_bytes,
+                  void* stream) {
+  switch (dtype) {
+    case SE_DTYPE_F32:
+      return cbn_bwd_impl<float>(src, (const float*)gy, (const float*)gy2, HeadArgs{}, (const float*)x, (float*)dx,
+                                 B, C, HW, params, save, dparams, training, act, slope, dx_amax, nullptr, ws,
+                                 ws_bytes, stream, nullptr, 0, (const float*)pw, (float*)dpw);
+    case SE_DTYPE_BF16:
+      return cbn_bwd_impl<__bf16>(src, (const __bf16*)gy, (const __bf16*)gy2, HeadArgs{}, (const __bf16*)x,
+                                  (__bf16*)dx, B, C, HW, params, save, dparams, training, act, slope, dx_amax,
+                                  nullptr, ws, ws_bytes, stream, nullptr, 0, (const __bf16*)pw, (__bf16*)dpw);
+    case SE_DTYPE_F16:
+      return cbn_bwd_impl<_Float16>(src, (const _Float16*)gy, (const _Float16*)gy2, HeadArgs{}, (const _Float16*)x,
+                                    (_Float16*)dx, B, C, HW, params, save, dparams, training, act, slope, dx_amax,
+                                    nullptr, ws, ws_bytes, stream, nullptr, 0, (const _Float16*)pw, (_Float16*)dpw);
+    default:
+      return SE_E_ARG;
+  }
 }
 
 }  // namespace
 
-extern "C" int se_cbn_bwd(const float* gy, const float* y, const float* x, float* dx, int B,
-                          int C, int HW, const float* const* params, const float* save,
-                          float* const* dparams, int training, int act, float slope,
-                          float* dx_amax, void* ws, size_t ws_bytes, void* stream) {
+extern "C" int se_cbn_bwd(const void* gy, const void* y, const void* x, void* dx, int B,
+                          int C, int HW, const void* const* params, const float* save,
+                          void* const* dparams, int training, int act, float slope,
+                          float* dx_amax, const void* prelu_w, void* dprelu_w, int dtype, void* ws, size_t ws_bytes,
+                          void* stream) {
   (void)y;   // not read: act' is recomputed from x (see the file comment); may be NULL
-  if (!gy || !bwd_args_ok(x, dx, save, B, C, HW)) return SE_E_ARG;
-  return cbn_bwd_impl(0, gy, nullptr, HeadArgs{}, x, dx, B, C, HW, params, save, dparams, training, act, slope,
-                      dx_amax, nullptr, ws, ws_bytes, stream);
+  if (!gy || !bwd_args_ok(x, dx, save, B, C, HW) || !act_ok(act, prelu_w)) return SE_E_ARG;
+  return cbn_bwd_dtype(0, gy, nullptr, x, dx, B, C, HW, params, save, dparams, training, act, slope, dx_amax,
+                       prelu_w, dprelu_w, dtype, ws, ws_bytes, stream);
 }
 
 // Forked output (the encoder block's y feeds the next conv AND the decoder skip):
 // gy + gy2 is summed inside both passes instead of by a separate add of two
 // activation-sized tensors (3 passes) before the backward.
-extern "C" int se_cbn_bwd2(const float* gy, const float* gy2, const float* x, float* dx, int B,
-                           int C, int HW, const float* const* params, const float* save,
-                           float* const* dparams, int training, int act, float slope,
-                           float* dx_amax, void* ws, size_t ws_bytes, void* stream) {
-  if (!gy || !gy2 || !bwd_args_ok(x, dx, save, B, C, HW)) return SE_E_ARG;
-  return cbn_bwd_impl(1, gy, gy2, HeadArgs{}, x, dx, B, C, HW, params, save, dparams, training, act, slope,
-                      dx_amax, nullptr, ws, ws_bytes, stream);
+extern "C" int se_cbn_bwd2(const void* gy, const void* gy2, const void* x, void* dx, int B,
+                           int C, int HW, const void* const* params, const float* save,
+                           void* const* dparams, int training, int act, float slope,
+                           float* dx_amax, const void* prelu_w, void* dprelu_w, int dtype, void* ws,
+                           size_t ws_bytes, void* stream) {
+  if (!gy || !gy2 || !bwd_args_ok(x, dx, save, B, C, HW) || !act_ok(act, prelu_w)) return SE_E_ARG;
+  return cbn_bwd_dtype(1, gy, gy2, x, dx, B, C, HW, params, save, dparams, training, act, slope, dx_amax,
+                       prelu_w, dprelu_w, dtype, ws, ws_bytes, stream);
 }
 
 extern "C" int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int B, int C, int H, int W,
@@ -863,6 +1101,28 @@ extern "C" int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int
   if ((long long)H * W >= (1LL << 31)) return SE_E_UNSUPPORTED;
   if (!bwd_args_ok(x, dx, save, B, C, H * W)) return SE_E_ARG;
   const HeadArgs hd{gout, w_head, W};
-  return cbn_bwd_impl(2, nullptr, nullptr, hd, x, dx, B, C, H * W, params, save, dparams, training, act, slope,
-                      dx_amax, dw_head, ws, ws_bytes, stream);
+  return cbn_bwd_impl<float>(2, nullptr, nullptr, hd, x, dx, B, C, H * W, (const void* const*)params, save,
+                             (void* const*)dparams, training, act, slope, dx_amax, dw_head, ws, ws_bytes, stream);
+}
+
+// First block (conv -> ComplexBatchNorm2d + act) with a conv input that needs no
+// gradient: the CBN backward with the conv's weight gradient accumulated in the
+// apply pass instead of writing dL/dy0 (see cbn_bwd_apply_fc_kernel).
+extern "C" int se_cbn_bwd_first_conv(const float* gy, const float* gy2, const float* x, int B, int C, int H, int W,
+                                     const float* const* params, const float* save, float* const* dparams,
+                                     int training, int act, float slope, const se_first_conv* fc, void* ws,
+                                     size_t ws_bytes, void* stream) {
+  if (!gy || !fc || !fc->x0 || !fc->dwr || !fc->dwi || H <= 0 || W <= 0 || act < 0 || act > 2) return SE_E_ARG;
+  if (!bwd_args_ok(x, x, save, B, C, H * W)) return SE_E_ARG;
+  if (fc->cin != 1 || fc->kernel_h != 5 || fc->kernel_w != 2) return SE_E_UNSUPPORTED;
+  if (fc->in_h <= 0 || fc->in_w <= 0 || fc->stride_h <= 0 || fc->stride_w <= 0 || fc->dil_h <= 0 || fc->dil_w <= 0)
+    return SE_E_ARG;
+  if ((long long)fc->in_h * fc->in_w * 2 >= (1LL << 31) || (long long)H * W >= (1LL << 31)) return SE_E_UNSUPPORTED;
+  if (ws_bytes < se_cbn_first_conv_workspace_size(B, C, H * W, fc->cin, fc->kernel_h, fc->kernel_w) || !ws)
+    return SE_E_WORKSPACE;
+  const FirstConv f{fc->x0, fc->in_h, fc->in_w, fc->stride_h, fc->stride_w, fc->pad_h, fc->pad_w, fc->dil_h,
+                    fc->dil_w, fc->dwr, fc->dwi};
+  return cbn_bwd_impl<float>(gy2 ? 1 : 0, gy, gy2, HeadArgs{}, x, nullptr, B, C, H * W, (const void* const*)params,
+                             save, (void* const*)dparams, training, act, slope, nullptr, nullptr, ws, ws_bytes, stream,
+                             &f, W);
 }

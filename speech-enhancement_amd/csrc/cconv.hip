@@ -105,8 +105,37 @@ __device__ __forceinline__ int xcd_remap(int L, int total) {
   return xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
 }
 
+// Storage types of the conv tensors (se_conv2d_desc.dtype, SE_DTYPE_*): element
+// type, a load as float and a round-to-nearest-even store at an element index,
+// and a raw buffer load of one element at byte offsets (as float).
+template <int SD> struct Stor { typedef float T; };
+template <> struct Stor<1> { typedef __bf16 T; };
+template <> struct Stor<2> { typedef _Float16 T; };
+template <int SD> __device__ __forceinline__ float ld_s(const void* p, long long i) {
+  return (float)static_cast<const typename Stor<SD>::T*>(p)[i];
+}
+template <int SD> __device__ __forceinline__ void st_s(void* p, long long i, float v) {
+  static_cast<typename Stor<SD>::T*>(p)[i] = (typename Stor<SD>::T)v;
+}
+template <int SD> __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  if constexpr (SD == 0) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, so, 0));
+  } else {
+    const unsigned short v = __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0);
+    if constexpr (SD == 1) return __builtin_bit_cast(float, (unsigned)v << 16);
+    else return (float)__builtin_bit_cast(_Float16, v);
+  }
+}
+// a load of element i of a tensor of runtime storage type sd (small prologue kernels)
+__device__ __forceinline__ float ld_any(const void* p, long long i, int sd) {
+  return sd == 1 ? ld_s<1>(p, i) : (sd == 2 ? ld_s<2>(p, i) : ld_s<0>(p, i));
+}
+__device__ __forceinline__ void st_any(void* p, long long i, float v, int sd) {
+  if (sd == 1) st_s<1>(p, i, v); else if (sd == 2) st_s<2>(p, i, v); else st_s<0>(p, i, v);
+}
+
 struct GatherArgs {
-  const float* X;      // gathered tensor [B, Cg, Hi, Wi]
+  const float* X;      // gathered tensor [B, Cg, Hi, Wi] (fp32, or 16-bit: see SD)
   const int4* ktab;    // [Kp] {c*Hi*Wi + offh*Wi + offw, offh, offw, 0}
   const float* Wp;     // [Kp, ldw]
   const float* bias;   // [N] or nullptr
@@ -404,7 +433,7 @@ gather_gemm_kernel(const GatherArgs a) {
 
 // Small-N variant (N <= 16: final_conv 128->2, the CCBAM k7 conv 4->2 and its
 // data-grad): HBM-bound, one output position per thread, weights in LDS.
-template <int NOUT>
+template <int NOUT, int SD = 0>
 __global__ void __launch_bounds__(kThreads)
 gather_smalln_kernel(const GatherArgs a) {
   extern __shared__ __attribute__((aligned(16))) float sWs[];  // [Kp][NOUT]
@@ -429,7 +458,7 @@ gather_smalln_kernel(const GatherArgs a) {
     const int4 e = a.ktab[k];
     const int hi = hb + e.y, wi = wb + e.z;
     const bool ok = (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
-    const float xv = a.X[ok ? xbase + e.x : 0];
+    const float xv = ld_s<SD>(a.X, ok ? xbase + e.x : 0);
     const float x = ok ? xv : 0.f;
 #pragma unroll
     for (int n = 0; n < NOUT; ++n) acc[n] = fmaf(x, sWs[k * NOUT + n], acc[n]);
@@ -439,7 +468,7 @@ gather_smalln_kernel(const GatherArgs a) {
                           (a.pw + a.Sw * qw);
 #pragma unroll
   for (int n = 0; n < NOUT; ++n)
-    if (n < a.N) a.Y[ybase + n * HoWo] = acc[n] + (a.bias ? a.bias[n] : 0.f);
+    if (n < a.N) st_s<SD>(a.Y, ybase + n * HoWo, acc[n] + (a.bias ? a.bias[n] : 0.f));
 }
 
 // ---------------------------------------------------------------------------
@@ -853,21 +882,22 @@ struct WeightView {
   const float* wi;
   int Ci, Co, kh, kw;
   int transposed, complex_w;
+  int sd;          // SE_DTYPE_* of wr / wi
 };
 
 __device__ __forceinline__ float kernel_value(const WeightView& w, int ci, int co, int i, int j) {
   if (!w.complex_w) {
     const long long idx = w.transposed ? (((long long)ci * w.Co + co) * w.kh + i) * w.kw + j
                                        : (((long long)co * w.Ci + ci) * w.kh + i) * w.kw + j;
-    return w.wr[idx];
+    return ld_any(w.wr, idx, w.sd);
   }
   const int hci = w.Ci / 2, hco = w.Co / 2;
   const bool ci_im = ci >= hci, co_im = co >= hco;
   const int a = ci_im ? ci - hci : ci, b = co_im ? co - hco : co;
   const long long idx = w.transposed ? (((long long)a * hco + b) * w.kh + i) * w.kw + j
                                      : (((long long)b * hci + a) * w.kh + i) * w.kw + j;
-  if (ci_im == co_im) return w.wr[idx];
-  return co_im ? w.wi[idx] : -w.wi[idx];
+  if (ci_im == co_im) return ld_any(w.wr, idx, w.sd);
+  return co_im ? ld_any(w.wi, idx, w.sd) : -ld_any(w.wi, idx, w.sd);
 }
 
 __device__ __forceinline__ int ilv64_host_dev(int c) { return (c & ~63) | ((c & 31) << 1) | ((c >> 5) & 1); }
@@ -918,12 +948,12 @@ __global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int
 #include "cconv_pk.hpp"
 
 // bias_full[n] for the fused complex conv: re = br - bi, im = bi + br.
-__global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out) {
+__global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out, int sd) {
   const int n = blockIdx.x * blockDim.x + threadIdx.x;
   if (n >= N) return;
-  if (!complex_w) { out[n] = br[n]; return; }
+  if (!complex_w) { out[n] = ld_any(br, n, sd); return; }
   const int h = N / 2;
-  out[n] = n < h ? br[n] - bi[n] : bi[n - h] + br[n - h];
+  out[n] = n < h ? ld_any(br, n, sd) - ld_any(bi, n, sd) : ld_any(bi, n - h, sd) + ld_any(br, n - h, sd);
 }
 
 // Sums the wgrad slabs and scatters the real-equivalent gradient dK back onto
@@ -936,6 +966,7 @@ struct UnpackArgs {
   int Ci, Co, kh, kw, transposed, complex_w;
   int Cg;                                  // gather channels of the wgrad pass
   int tap_of[kMaxTaps];                    // (i*kw + j) -> tap index t
+  int sd;                                  // SE_DTYPE_* of dwr / dwi
 };
 
 __device__ __forceinline__ float dk_sum(const UnpackArgs& u, int ci, int co, int t) {
@@ -962,13 +993,13 @@ __global__ void wgrad_finish_kernel(const UnpackArgs u) {
     const int ci = u.transposed ? a0 : b0, co = u.transposed ? b0 : a0;
     const int t = u.tap_of[i * u.kw + j];
     if (!u.complex_w) {
-      u.dwr[idx] = dk_sum(u, ci, co, t);
+      st_any(u.dwr, idx, dk_sum(u, ci, co, t), u.sd);
       continue;
     }
     const float rr = dk_sum(u, ci, co, t), ii = dk_sum(u, ci + hci, co + hco, t);
     const float ri = dk_sum(u, ci, co + hco, t), ir = dk_sum(u, ci + hci, co, t);
-    u.dwr[idx] = rr + ii;
-    u.dwi[idx] = ri - ir;
+    st_any(u.dwr, idx, rr + ii, u.sd);
+    st_any(u.dwi, idx, ri - ir, u.sd);
   }
 }
 
@@ -976,6 +1007,7 @@ __global__ void wgrad_finish_kernel(const UnpackArgs u) {
 // block per real channel, or per complex channel pair (n, n + N/2), written
 // directly (no zeroed outputs, no atomics): d(br) = sum(dy_re) + sum(dy_im),
 // d(bi) = -sum(dy_re) + sum(dy_im), the values the two-atomic form produced.
+template <int SD = 0>
 __global__ void bias_grad_kernel(const float* dy, int B, int N, long long HW, int complex_w,
                                  float* dbr, float* dbi) {
   const int n = blockIdx.x;
@@ -985,8 +1017,8 @@ __global__ void bias_grad_kernel(const float* dy, int B, int N, long long HW, in
     const int ch = n + q * (N / 2);
     float s = 0.f;
     for (int b = 0; b < B; ++b) {
-      const float* p = dy + ((long long)b * N + ch) * HW;
-      for (long long i = threadIdx.x; i < HW; i += kThreads) s += p[i];
+      const long long p = ((long long)b * N + ch) * HW;
+      for (long long i = threadIdx.x; i < HW; i += kThreads) s += ld_s<SD>(dy, p + i);
     }
     s = se::wave_sum(s);
     __syncthreads();   // red is reused by the second channel
@@ -996,9 +1028,9 @@ __global__ void bias_grad_kernel(const float* dy, int B, int N, long long HW, in
       for (int i = 0; i < kThreads / 64; ++i) t[q] += red[i];
   }
   if (threadIdx.x != 0) return;
-  if (!complex_w) { dbr[n] = t[0]; return; }
-  dbr[n] = t[0] + t[1];
-  dbi[n] = -t[0] + t[1];
+  if (!complex_w) { st_s<SD>(dbr, n, t[0]); return; }
+  st_s<SD>(dbr, n, t[0] + t[1]);
+  st_s<SD>(dbi, n, -t[0] + t[1]);
 }
 
 // ---------------------------------------------------------------------------
@@ -1071,6 +1103,7 @@ struct ConvGeom {
   const void* x2_packed;
   const void* dy_packed;
   int accum;      // se_conv2d_desc.accumulate_dx
+  int sd;         // se_conv2d_desc.dtype (SE_DTYPE_*)
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -1089,8 +1122,13 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.x2_packed = d->x2_packed;
   g.dy_packed = d->dy_packed;
   g.accum = d->accumulate_dx;
+  g.sd = d->dtype;
   if (g.accum != 0 && g.accum != 1) return SE_E_ARG;
-  if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16X3) return SE_E_ARG;
+  if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16) return SE_E_ARG;
+  if (g.sd < SE_DTYPE_F32 || g.sd > SE_DTYPE_F16) return SE_E_ARG;
+  // 16-bit storage runs the one-term MFMA of its own format (operands exact)
+  if (g.sd == SE_DTYPE_BF16 && g.math != SE_MATH_BF16) return SE_E_UNSUPPORTED;
+  if (g.sd == SE_DTYPE_F16 && g.math != SE_MATH_F16) return SE_E_UNSUPPORTED;
   if (g.B <= 0 || g.Ci <= 0 || g.Co <= 0 || g.Hi <= 0 || g.Wi <= 0 || g.kh <= 0 || g.kw <= 0 ||
       g.sh <= 0 || g.sw <= 0 || g.dh <= 0 || g.dw <= 0 || g.ph < 0 || g.pw < 0)
     return SE_E_ARG;
@@ -1184,8 +1222,15 @@ static bool fwd_merge_on() {   // read per call (tests switch it within one proc
   return e && std::atoi(e) == 1;
 }
 
-static inline int ldw_for(int N) {
+// One-term bf16 (SE_MATH_BF16, the low-precision configs' arithmetic) runs the
+// 128-column MFMA tiles down to N = 17: even with 2-4x zero columns a bf16 MFMA tile
+// beats the fp32-MFMA tiles (1/16 of the bf16 rate) that the fp32-class modes keep
+// for N <= 64 (DCCRN / DCUNet's 32- and 64-channel layers).
+static inline bool bf16_tiles(int N, int math) { return (math == SE_MATH_BF16 || math == SE_MATH_F16) && N > 16; }
+
+static inline int ldw_for(int N, int math = SE_MATH_F32) {
   if (N <= 16) return N <= 4 ? 4 : (N <= 8 ? 8 : 16);  // = the small-N kernel's NOUT
+  if (bf16_tiles(N, math)) return round_up(N, 128);
   return round_up(N, N <= 64 ? 64 : 128);
 }
 
@@ -1193,9 +1238,10 @@ static inline int ldw_for(int N) {
 // (4) or the three-way split (6)
 constexpr size_t kWpBytesPerElem = 6;
 
-static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N) {
+static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N, int math = SE_MATH_F32) {
   size_t bytes = 0;
-  const int ldw = ldw_for(N);
+  (void)math;   // sized for the wider of the fp32 and bf16 tilings: a conv's passes may differ in math
+  const int ldw = std::max(ldw_for(N, SE_MATH_F32), ldw_for(N, SE_MATH_BF16));
   for (const auto& c : cls) {
     bytes += (size_t)c.Kp * ldw * kWpBytesPerElem;
     bytes += (size_t)c.Kp * sizeof(int4);
@@ -1237,8 +1283,10 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
     w.splits = (w.M + w.m_per_split - 1) / w.m_per_split;
     return w;
   }
-  w.Np = round_up(w.N, w.N <= 32 ? 32 : 128);
-  const int tiles = (w.c.Kp / 128) * (w.Np / (w.N <= 32 ? 32 : 128));
+  // one-term SE_MATH_BF16 / SE_MATH_F16 with N % 16 == 0: the 128-column tiles (see bf16_tiles)
+  const bool n32 = w.N <= 32 && !((g.math == SE_MATH_BF16 || g.math == SE_MATH_F16) && w.N % 16 == 0);
+  w.Np = round_up(w.N, n32 ? 32 : 128);
+  const int tiles = (w.c.Kp / 128) * (w.Np / (n32 ? 32 : 128));
   int splits = std::max(1, 1024 / std::max(tiles, 1));
   // At most kWgradMps positions per m-split (SEHIP_WGRAD_MPS overrides; 0 = no
   // limit): the (k, n) tiles of one split run on one XCD and re-read G and D
@@ -1322,6 +1370,11 @@ static int gemm_nw() {
   return nw;
 }
 
+// a pass that would read a caller's CL16 operand (fp32 storage only)
+static bool pk_pass_any(const ConvGeom& g, Pass pass) {
+  return (pass == kFwd ? g.x_packed : g.dy_packed) != nullptr;
+}
+
 static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const float* wr,
                          const float* wi, const float* bias_br, const float* bias_bi, float* Y,
                          void* ws, size_t ws_bytes, hipStream_t st, const JoinIO* jn = nullptr) {
@@ -1330,12 +1383,12 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const int Cg = (pass == kFwd) ? g.Ci : g.Co;
   const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
   const int Ho = (pass == kFwd) ? g.Ho : g.Hi, Wo = (pass == kFwd) ? g.Wo : g.Wi;
-  if (ws_bytes < gather_ws_bytes(cls, N)) return SE_E_WORKSPACE;
+  if (ws_bytes < gather_ws_bytes(cls, N, g.math)) return SE_E_WORKSPACE;
   if (g.accum) {   // dx += result: the split kernels' plain epilogue only (checked before any launch)
     const bool split = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3) && N > 64;
     if (pass != kData || jn || !split || g.dy_packed) return SE_E_UNSUPPORTED;
   }
-  int ldw = ldw_for(N);
+  int ldw = ldw_for(N, g.math);
   {   // stride-phase classes merged along the columns (split-fp16, 256-column tiles)
     ClassPlan mp;
     const bool pk_in = (pass == kFwd ? g.x_packed : g.dy_packed) != nullptr;
@@ -1346,7 +1399,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       ldw = 256;
     }
   }
-  WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w};
+  WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w, g.sd};
+  if (g.sd != SE_DTYPE_F32 && (jn || pk_pass_any(g, pass))) return SE_E_UNSUPPORTED;   // fp32-only forms
 
   char* p = align256((char*)ws);
   const float* zero = zero_page();
@@ -1363,13 +1417,14 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     bias_full = (float*)p;
     p = align256(p + round_up(N, 128) * sizeof(float));
     hipLaunchKernelGGL(prep_bias_kernel, dim3(se::ceil_div(N, 256)), dim3(256), 0, st,
-                       bias_br, bias_bi, N, g.complex_w, bias_full);
+                       bias_br, bias_bi, N, g.complex_w, bias_full, g.sd);
   }
   // split-bf16 / bf16 / split-fp16 GEMM for the 128-column tiles (N > 64); other
   // shapes stay fp32
-  const bool bf1 = g.math == SE_MATH_BF16 && N > 64;             // one term: hi*hi
+  const bool bf1 = g.math == SE_MATH_BF16 && bf16_tiles(N, g.math);   // one term: hi*hi (bf16)
+  const bool h1 = g.math == SE_MATH_F16 && bf16_tiles(N, g.math);     // one term, fp16, unscaled
   const bool f16 = g.math == SE_MATH_F16X3 && N > 64;            // scaled split-fp16
-  const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1 || f16;   // prep / tiles shared
+  const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1 || h1 || f16;   // prep / tiles shared
   const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
   const float* amax_a = pass == kFwd ? g.x_amax : g.dy_amax;
   // CL16 operands from the caller: the LDS-DMA kernel (gather_pk_kernel) on
@@ -1420,10 +1475,10 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       hipLaunchKernelGGL(prep_class_x6_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
                          pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab);
-    else if (f16)
+    else if (f16 || h1)   // h1: fp16 planes, unscaled (no weight bound)
       hipLaunchKernelGGL(prep_class_x3_kernel<true>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, wamax);
+                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, f16 ? wamax : nullptr);
     else if (x3)
       hipLaunchKernelGGL(prep_class_x3_kernel<false>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
                          dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
@@ -1451,9 +1506,16 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       const size_t sh = (size_t)c.Kp * ldw * sizeof(float);
       if (sh > 64 * 1024) return SE_E_UNSUPPORTED;
       dim3 grid(se::ceil_div(M, kThreads));
-      if (ldw <= 4) hipLaunchKernelGGL(gather_smalln_kernel<4>, grid, dim3(kThreads), sh, st, a);
-      else if (ldw <= 8) hipLaunchKernelGGL(gather_smalln_kernel<8>, grid, dim3(kThreads), sh, st, a);
-      else hipLaunchKernelGGL(gather_smalln_kernel<16>, grid, dim3(kThreads), sh, st, a);
+#define SE_SMALLN(SDV)                                                                                    \
+  do {                                                                                                    \
+    if (ldw <= 4) hipLaunchKernelGGL((gather_smalln_kernel<4, SDV>), grid, dim3(kThreads), sh, st, a);    \
+    else if (ldw <= 8) hipLaunchKernelGGL((gather_smalln_kernel<8, SDV>), grid, dim3(kThreads), sh, st, a); \
+    else hipLaunchKernelGGL((gather_smalln_kernel<16, SDV>), grid, dim3(kThreads), sh, st, a);            \
+  } while (0)
+      if (g.sd == SE_DTYPE_BF16) SE_SMALLN(1);
+      else if (g.sd == SE_DTYPE_F16) SE_SMALLN(2);
+      else SE_SMALLN(0);
+#undef SE_SMALLN
     } else {
       const bool tu = tu_of(c);
       if (packed && tu && ldw % 128 == 0) {
@@ -1514,7 +1576,20 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, T, 0, NWV, F>), grid, blk, 0, st, a);         \
     else hipLaunchKernelGGL((gather_x3_kernel<false, T, 0, NWV, F>), grid, blk, 0, st, a);                \
   } while (0)
-        if (f16 && wide && gemm_bm() == 256 && tu) {   // 256 x 256 tiles (BMX = 2)
+        if (g.sd != SE_DTYPE_F32) {   // 16-bit storage: the one-term tiles of its format
+#define SE_X3_SD(NWV, F, SDV)                                                                              \
+  do {                                                                                                    \
+    if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 0, NWV, F, 1, false, SDV>), grid, blk, 0, st, a); \
+    else hipLaunchKernelGGL((gather_x3_kernel<false, 1, 0, NWV, F, 1, false, SDV>), grid, blk, 0, st, a);   \
+  } while (0)
+          if (g.sd == SE_DTYPE_BF16 && wide) SE_X3_SD(2, false, 1);
+          else if (g.sd == SE_DTYPE_BF16) SE_X3_SD(1, false, 1);
+          else if (wide) SE_X3_SD(2, true, 2);
+          else SE_X3_SD(1, true, 2);
+#undef SE_X3_SD
+        } else if (h1 && wide) SE_X3_LAUNCH(1, 2, true);
+        else if (h1) SE_X3_LAUNCH(1, 1, true);
+        else if (f16 && wide && gemm_bm() == 256 && tu) {   // 256 x 256 tiles (BMX = 2)
           const dim3 g2(se::ceil_div(M, 2 * kX3BM), grid.y);
           if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1, 2, true, 2>), g2, blk, 0, st, a);
           else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2, 2, true, 2>), g2, blk, 0, st, a);
@@ -1635,14 +1710,19 @@ extern "C" int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out
 extern "C" size_t se_conv2d_workspace_size(const se_conv2d_desc* d) {
   ConvGeom g;
   if (geom_of(d, g)) return 0;
-  size_t a = gather_ws_bytes(plan_pass(g, kFwd), g.Co);
+  size_t a = gather_ws_bytes(plan_pass(g, kFwd), g.Co, g.math);
   {
     ClassPlan mp;
     if (g.transposed && g.Co > 64 && g.Co <= 128 && merge_h_phases(plan_pass(g, kFwd), g.Ci, mp))
       a = std::max(a, gather_ws_bytes({mp}, 256));
   }
-  size_t b = gather_ws_bytes(plan_pass(g, kData), g.Ci);
+  size_t b = gather_ws_bytes(plan_pass(g, kData), g.Ci, g.math);
   size_t c = wgrad_ws_bytes(plan_wgrad(g));
+  {   // the weight-grad pass may run in another math than the forward (per-pass modes)
+    ConvGeom g2 = g;
+    g2.math = g.math == SE_MATH_BF16 ? SE_MATH_F32 : SE_MATH_BF16;
+    c = std::max(c, wgrad_ws_bytes(plan_wgrad(g2)));
+  }
   return std::max(a, std::max(b, c));
 }
 
@@ -1714,8 +1794,11 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   const long long QQw = (long long)w.Qh * w.Qw;
   const long long span_w = (w.m_per_split + QQw - 1) / QQw + 1;
   // the split-bf16 / bf16 tile reads D rows in blocks of 16 (N % 16 == 0)
-  const bool split_ok = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3) &&
-                        w.N % 16 == 0;
+  const bool split_ok = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3 ||
+                         g.math == SE_MATH_F16) && w.N % 16 == 0;
+  // 16-bit storage: the one-term split tiles only (the fp32 kernels read fp32)
+  if (g.sd != SE_DTYPE_F32 && (jn || !split_ok || w.N <= kSmallWgradN || w.Np == 32 || g.x_packed || g.dy_packed))
+    return SE_E_UNSUPPORTED;
   if (jn) {
     const int dcpb = 2 * jn->jh;
     const bool tu = g.transposed && (w.Cg % 128 == 0) &&
@@ -1835,6 +1918,16 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
+  } else if (split_ok && g.sd != SE_DTYPE_F32) {   // 16-bit storage, one term of its format
+    const dim3 grid = x3_wgrad_grid(a, w);
+    if (g.sd == SE_DTYPE_BF16 && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 1, false, 1, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, false, 1, false, 1, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true, 1, false, 1, 2>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, true, 1, false, 1, 2>), grid, dim3(kThreads), 0, st, a);
+  } else if (split_ok && g.math == SE_MATH_F16) {   // one-term fp16 on fp32 storage
+    const dim3 grid = x3_wgrad_grid(a, w);
+    if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, true>), grid, dim3(kThreads), 0, st, a);
   } else if (split_ok) {   // SE_MATH_BF16
     const dim3 grid = x3_wgrad_grid(a, w);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true>), grid, dim3(kThreads), 0, st, a);
@@ -1864,7 +1957,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   UnpackArgs u{};
   u.slab = slab; u.splits = 1; u.Kp = w.c.Kp; u.Np = w.Np;
   u.dwr = dwr; u.dwi = dwi; u.Ci = g.Ci; u.Co = g.Co; u.kh = g.kh; u.kw = g.kw;
-  u.transposed = g.transposed; u.complex_w = g.complex_w; u.Cg = w.Cg;
+  u.transposed = g.transposed; u.complex_w = g.complex_w; u.Cg = w.Cg; u.sd = g.sd;
   for (int t = 0; t < w.c.taps.n; ++t) u.tap_of[w.c.taps.ti[t] * g.kw + w.c.taps.tj[t]] = t;
   const long long nw = (long long)(g.complex_w ? g.Ci / 2 : g.Ci) * (g.complex_w ? g.Co / 2 : g.Co) * g.kh * g.kw;
   hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)std::min<long long>((nw + 255) / 256, 4096)),
@@ -1873,8 +1966,15 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
 
   if (dbr) {
     const int hco = g.complex_w ? g.Co / 2 : g.Co;
-    hipLaunchKernelGGL(bias_grad_kernel, dim3(hco), dim3(kThreads), 0, st, dy, g.B, g.Co,
-                       (long long)g.Ho * g.Wo, g.complex_w, dbr, dbi);
+    if (g.sd == SE_DTYPE_BF16)
+      hipLaunchKernelGGL(bias_grad_kernel<1>, dim3(hco), dim3(kThreads), 0, st, dy, g.B, g.Co,
+                         (long long)g.Ho * g.Wo, g.complex_w, dbr, dbi);
+    else if (g.sd == SE_DTYPE_F16)
+      hipLaunchKernelGGL(bias_grad_kernel<2>, dim3(hco), dim3(kThreads), 0, st, dy, g.B, g.Co,
+                         (long long)g.Ho * g.Wo, g.complex_w, dbr, dbi);
+    else
+      hipLaunchKernelGGL(bias_grad_kernel<0>, dim3(hco), dim3(kThreads), 0, st, dy, g.B, g.Co,
+                         (long long)g.Ho * g.Wo, g.complex_w, dbr, dbi);
     SE_LAUNCH_CHECK();
   }
   return SE_OK;

@@ -157,7 +157,7 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
                                      int Hi, int Wi, int data_grad, int kblk, unsigned short* Wt,
                                      int4* ktab, const float* amax_w) {
   const int K = taps.n * Cg;
-  const float sw = F16 ? pow2f(kF16Top - amax_exp(amax_w)) : 1.f;
+  const float sw = (F16 && amax_w) ? pow2f(kF16Top - amax_exp(amax_w)) : 1.f;   // no bound: unscaled (SE_MATH_F16)
   const long long total = (long long)Kp * NT * 128;   // one thread per (k, n)
   for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
        idx += (long long)gridDim.x * blockDim.x) {
@@ -233,12 +233,17 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // intervals: a memory part (fragment reads of this step, LDS stores of the
 // next, global loads of the one after) and an MFMA part. In each interval one
 // wave per SIMD issues MFMAs while the other does its memory part.
-template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int BMX = 1, bool PP = false>
+// SD: storage type of X and Y (se_conv2d_desc.dtype): 0 fp32; 1 bf16 / 2 fp16 with
+// the one-term MFMA of that format (TERMS = 1; F16 = fp16 MFMA, unscaled: the
+// operands are exactly representable), the 16-bit tensors loaded and stored as they are.
+template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int BMX = 1, bool PP = false,
+          int SD = 0>
 __global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
-  static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
+  static_assert(SD == 0 || (TERMS == 1 && JM == 0 && BMX == 1 && !PP), "16-bit storage: one-term, plain tiles");
   static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
+  constexpr int ES = SD ? 2 : 4;                  // bytes per element of X / Y
   static_assert(NW == 1 || NW == 2, "128 or 256 columns per workgroup");
   static_assert(BMX == 1 || (BMX == 2 && NW == 2), "256-row tiles need the 8-wave workgroup");
   constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
@@ -273,9 +278,9 @@ gather_x3_kernel(const GatherArgs a) {
     wb = qw * a.sw;
     xbase = (long long)b * a.Cg * HiWi + (long long)hb * a.Wi + wb;
   }
-  float sa = 1.f;   // F16: activation scale; the epilogue multiplies by 2^ush
+  float sa = 1.f;   // F16 (three terms): activation scale; the epilogue multiplies by 2^ush
   int ush = 0;
-  if constexpr (F16) {
+  if constexpr (F16 && TERMS == 3) {
     const int ea = amax_exp(a.amax_a);
     sa = pow2f(kF16Top - ea);
     ush = ea + amax_exp(a.amax_w) - 2 * kF16Top;
@@ -292,7 +297,7 @@ gather_x3_kernel(const GatherArgs a) {
   const int cpb = JM == 1 ? 2 * a.jh : a.Cg;      // channels per batch item of X
   const long long H2W2 = (long long)a.H2 * a.W2;
   __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(a.X + (long long)b0 * cpb * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+      uniform_ptr((const char*)a.X + (long long)b0 * cpb * HiWi * ES), (short)0, 0x7FFFFFFF, 0x00020000);
   __amdgpu_buffer_rsrc_t rx2 = rx;
   if constexpr (JM == 1)
     rx2 = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.X2 + (long long)b0 * cpb * H2W2), (short)0,
@@ -305,7 +310,7 @@ gather_x3_kernel(const GatherArgs a) {
   if constexpr (TU) {
     if (mval) {
       const int b = m / (a.Qh * a.Qw);
-      xoff = (int)(((long long)(b - b0) * cpb * HiWi + (long long)hb * a.Wi + wb) * 4);
+      xoff = (int)(((long long)(b - b0) * cpb * HiWi + (long long)hb * a.Wi + wb) * ES);
       if constexpr (JM == 1) xoff2 = (int)(((long long)(b - b0) * cpb * H2W2 + (long long)hb * a.W2 + wb) * 4);
     }
   }
@@ -315,7 +320,7 @@ gather_x3_kernel(const GatherArgs a) {
       int c0 = e0.w;
       const int hi = hb + e0.y, wi = wb + e0.z;
       bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      int vo = xoff + (e0.y * a.Wi + e0.z) * 4, cs = (int)(HiWi * 4);
+      int vo = xoff + (e0.y * a.Wi + e0.z) * ES, cs = (int)(HiWi * ES);
       __amdgpu_buffer_rsrc_t r = rx;
       if constexpr (JM == 1) {                    // a K-step lies in one join chunk
         const int q = c0 / a.jh;
@@ -329,15 +334,14 @@ gather_x3_kernel(const GatherArgs a) {
       vo = ok ? vo : (int)0x80000000;
       c0 += AJ * akr;
 #pragma unroll
-      for (int j = 0; j < AJ; ++j)
-        st.ra[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, vo, (c0 + j) * cs, 0));
+      for (int j = 0; j < AJ; ++j) st.ra[j] = bload<SD>(r, vo, (c0 + j) * cs);
     } else {
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {
         const int4 e = a.ktab[k0 + AJ * akr + j];   // uniform index -> s_load
         const int hi = hb + e.y, wi = wb + e.z;
         const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-        st.ra[j] = *(ok ? a.X + xbase + e.x : a.zero);
+        st.ra[j] = ld_s<SD>(ok ? (const void*)a.X : (const void*)a.zero, ok ? xbase + e.x : 0);
       }
     }
     const u32x4* src = wt + (long long)(k0 >> 5) * NT * NW * kX3TileU4;
@@ -561,7 +565,7 @@ gather_x3_kernel(const GatherArgs a) {
     }
     if (kt < nk) compute(0);
   }
-  if constexpr (F16) {   // undo the operand scales (exact)
+  if constexpr (F16 && TERMS == 3) {   // undo the operand scales (exact)
 #pragma unroll
     for (int i = 0; i < QN; ++i)
 #pragma unroll
@@ -620,19 +624,19 @@ gather_x3_kernel(const GatherArgs a) {
       const int oh = a.ph + mph + a.Sh * qh;
       if (oh >= a.Ho) continue;
       const int nc = n0 + nl0 - mph * a.mrg_np;    // channel of this lane's first column
-      float* yb = a.Y + (long long)b * a.N * HoWo + (long long)oh * a.Wo + (a.pw + a.Sw * qw) +
-                  (long long)nc * HoWo;
+      const long long yb = (long long)b * a.N * HoWo + (long long)oh * a.Wo + (a.pw + a.Sw * qw) +
+                           (long long)nc * HoWo;
 #pragma unroll
       for (int i = 0; i < QN; ++i)
 #pragma unroll
         for (int r2 = 0; r2 < AR; ++r2) {
           const int nl = BLK * i + roff(r2);
-          if (nc + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
+          if (nc + nl < a.N) st_s<SD>(a.Y, yb + (long long)nl * HoWo, acc[i][j][r2] + sBias[nl0 + nl]);
         }
       continue;
     }
-    float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
-                (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
+    const long long yb = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
+                         (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
 #pragma unroll
     for (int i = 0; i < QN; ++i)
 #pragma unroll
@@ -640,8 +644,8 @@ gather_x3_kernel(const GatherArgs a) {
         const int nl = BLK * i + roff(r2);
         if (full_n || n0 + nl0 + nl < a.N) {
           float v = acc[i][j][r2] + sBias[nl0 + nl];
-          if (a.accum) v += yb[(long long)nl * HoWo];   // = the consumer's gy + gy2, same fp32 add
-          yb[(long long)nl * HoWo] = v;
+          if (a.accum) v += ld_s<SD>(a.Y, yb + (long long)nl * HoWo);   // = the consumer's gy + gy2, same fp32 add
+          st_s<SD>(a.Y, yb + (long long)nl * HoWo, v);
         }
       }
   }
@@ -678,11 +682,14 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // tile of a step is staged once for two taps (a thread stages 16 G rows and 8
 // D rows); for N = 128 (the encoder's weight-grads, 10 k-tiles per split).
 // KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int KB = 1>
+// SD: storage type of X / D (as gather_x3_kernel; 16-bit with the one-term MFMA)
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int KB = 1,
+          int SD = 0>
 __global__ void __launch_bounds__(kThreads * NB * KB, SEHIP_WGRAD_OCC)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
-  static_assert(!F16 || TERMS == 3, "split-fp16 is the three-term form");
+  static_assert(SD == 0 || (TERMS == 1 && !DJ), "16-bit storage: one-term, no join");
+  constexpr int ES = SD ? 2 : 4;             // bytes per element of X / D
   static_assert(NB * KB <= 2, "one or two 128-row D blocks, or two G blocks");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
   constexpr int BKO = 128 * KB, BNO = 128 * NB, WNn = 2 * NB, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
@@ -723,9 +730,9 @@ wgrad_x3_kernel(const WgradArgs a) {
 
   for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
   __syncthreads();
-  float sg = 1.f, sd = 1.f;   // F16: operand scales; the slab gets acc * 2^ush
+  float sg = 1.f, sd = 1.f;   // F16 (three terms): operand scales; the slab gets acc * 2^ush
   int ush = 0;
-  if constexpr (F16) {
+  if constexpr (F16 && TERMS == 3) {
     const int eg = amax_exp(a.amax_g), ed = amax_exp(a.amax_d);
     sg = pow2f(kF16Top - eg);
     sd = pow2f(kF16Top - ed);
@@ -750,11 +757,11 @@ wgrad_x3_kernel(const WgradArgs a) {
   };
   const int bfirst = (int)(mbeg / QQ);
   __amdgpu_buffer_rsrc_t rg_src = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(a.X + (long long)bfirst * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
+      uniform_ptr((const char*)a.X + (long long)bfirst * a.Cg * HiWi * ES), (short)0, 0x7FFFFFFF, 0x00020000);
   const int dcpb = DJ ? 2 * a.djh : a.N;         // channels per batch item of D
   const long long QQ2 = (long long)a.DH2 * a.DW2;
   __amdgpu_buffer_rsrc_t rd_src = __builtin_amdgcn_make_buffer_rsrc(
-      uniform_ptr(a.D + (long long)bfirst * dcpb * QQ), (short)0, 0x7FFFFFFF, 0x00020000);
+      uniform_ptr((const char*)a.D + (long long)bfirst * dcpb * QQ * ES), (short)0, 0x7FFFFFFF, 0x00020000);
   __amdgpu_buffer_rsrc_t rd2_src = rd_src;
   if constexpr (DJ)
     rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.D2 + (long long)bfirst * dcpb * QQ2), (short)0,
@@ -789,7 +796,7 @@ wgrad_x3_kernel(const WgradArgs a) {
     // Np-padded tail; tail rows read 0 through an out-of-range voffset (they
     // must not be read: past the last batch item they leave the allocation).
     const bool dok = mv & (n0 + rbase < a.N);
-    int vd, ds = (int)(QQ * 4), srow = (32 / KB) * wave;
+    int vd, ds = (int)(QQ * ES), srow = (32 / KB) * wave;
     __amdgpu_buffer_rsrc_t rdr = rd_src;
     if constexpr (DJ) {
       // joined D: chunks [x_re, s_re, x_im, s_im] of djh rows; a wave's 32 rows
@@ -807,7 +814,7 @@ wgrad_x3_kernel(const WgradArgs a) {
       srow = 0;
     } else {
       vd = dok ? (int)(((long long)rb * a.N * QQ + (long long)(n0 + RJ * lr) * QQ +
-                        (long long)cqh * a.Qw + cqw) * 4) : (int)0x80000000;
+                        (long long)cqh * a.Qw + cqw) * ES) : (int)0x80000000;
     }
     if (KP && !gact) {
 #pragma unroll
@@ -816,12 +823,10 @@ wgrad_x3_kernel(const WgradArgs a) {
       const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
       const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
       const int vg = ok ? (int)(((long long)rb * a.Cg * HiWi + (long long)(cbase + RJG * lr) * HiWi +
-                                 (long long)hi * a.Wi + wi) * 4) : (int)0x80000000;
-      const int gs = (int)(HiWi * 4);
+                                 (long long)hi * a.Wi + wi) * ES) : (int)0x80000000;
+      const int gs = (int)(HiWi * ES);
 #pragma unroll
-      for (int j = 0; j < RJG; ++j)
-        S.rg[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-            rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs, 0));
+      for (int j = 0; j < RJG; ++j) S.rg[j] = bload<SD>(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
     } else {
       const int hb = cqh * a.sh, wb = cqw * a.sw;
       const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
@@ -830,12 +835,11 @@ wgrad_x3_kernel(const WgradArgs a) {
         const int4 e = sK[rbase_g + j];
         const int hi = hb + e.y, wi = wb + e.z;
         const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-        S.rg[j] = *(ok ? a.X + xb + e.x : a.zero);
+        S.rg[j] = ld_s<SD>(ok ? (const void*)a.X : (const void*)a.zero, ok ? xb + e.x : 0);
       }
     }
 #pragma unroll
-    for (int j = 0; j < RJ; ++j)
-      S.rd[j] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(rdr, vd, (srow + j) * ds, 0));
+    for (int j = 0; j < RJ; ++j) S.rd[j] = bload<SD>(rdr, vd, (srow + j) * ds);
     advance();
   };
   auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {

@@ -286,3 +286,63 @@ extern "C" int se_adamw_step(const se_tensor_slot* slots, int nslots, long long 
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
+
+// ------------------------------------------------------------------ FRCRN mask
+// frcrn.py:140-152: mask = tanh(pad(h, top 1 row)); est = pad(mask * noisy, top 1)
+// with noisy = the spectrum without its DC row, re-stacked as [B, 2*half, T]. So
+//   est[b, c*half + k, t] = k < 2 ? 0 : tanh(h[b, c, k - 2, t]) * spec[b, c*half + k, t]
+// (row 0: the DC re-padded as 0; row 1: tanh(0) = 0 from the mask pad). One pass
+// instead of pad / tanh / mul / pad / reshape; the backward is one pass too:
+//   dh[b, c, k - 2, t] = dest * spec * (1 - tanh^2)   (the spectrum takes no gradient).
+// grid (ceil(half * T / (4 kThreads)), 2 B)
+__global__ void __launch_bounds__(kThreads)
+mask_fwd_kernel(const float* __restrict__ h, const float* __restrict__ spec, int half, int T,
+                float* __restrict__ est) {
+  const int bc = blockIdx.y;                     // b * 2 + c
+  const long long HT = (long long)half * T;
+  const float* hp = h + (long long)bc * (half - 2) * T;
+  const float* sp = spec + (long long)bc * HT;
+  float* ep = est + (long long)bc * HT;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long long i = ((long long)blockIdx.x * 4 + u) * kThreads + threadIdx.x;
+    if (i >= HT) return;
+    const long long k = i / T;
+    ep[i] = k < 2 ? 0.f : tanhf(hp[i - 2 * T]) * sp[i];
+  }
+}
+
+__global__ void __launch_bounds__(kThreads)
+mask_bwd_kernel(const float* __restrict__ gest, const float* __restrict__ h, const float* __restrict__ spec,
+                int half, int T, float* __restrict__ gh) {
+  const int bc = blockIdx.y;
+  const long long HT = (long long)half * T, HT2 = (long long)(half - 2) * T;
+  const float* hp = h + (long long)bc * HT2;
+  const float* sp = spec + (long long)bc * HT + 2 * T;
+  const float* gp = gest + (long long)bc * HT + 2 * T;
+  float* op = gh + (long long)bc * HT2;
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const long long i = ((long long)blockIdx.x * 4 + u) * kThreads + threadIdx.x;
+    if (i >= HT2) return;
+    const float m = tanhf(hp[i]);
+    op[i] = gp[i] * sp[i] * (1.f - m * m);
+  }
+}
+
+extern "C" int se_mask_fwd(const float* h, const float* spec, int B, int half, int T, float* est, void* stream) {
+  if (!h || !spec || !est || B <= 0 || half < 3 || T <= 0) return SE_E_ARG;
+  hipLaunchKernelGGL(mask_fwd_kernel, dim3(se::ceil_div((long long)half * T, 4 * kThreads), 2 * B), dim3(kThreads), 0,
+                     se::as_stream(stream), h, spec, half, T, est);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_mask_bwd(const float* gest, const float* h, const float* spec, int B, int half, int T, float* gh,
+                           void* stream) {
+  if (!gest || !h || !spec || !gh || B <= 0 || half < 3 || T <= 0) return SE_E_ARG;
+  hipLaunchKernelGGL(mask_bwd_kernel, dim3(se::ceil_div((long long)(half - 2) * T, 4 * kThreads), 2 * B),
+                     dim3(kThreads), 0, se::as_stream(stream), gest, h, spec, half, T, gh);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}

@@ -312,6 +312,21 @@ __device__ __forceinline__ void xcd_frame_block(int& tb, int& b) {
   tb = t - b * gridDim.x;
 }
 
+// Storage type of the signal / spectrum tensors (SE_DTYPE_*). LP = false: fp32 (the
+// kernels as they were); LP = true: bf16 or fp16 by the launch's dt (a uniform
+// branch per access), converted to fp32 on load and rounded to nearest even on store.
+template <bool LP>
+__device__ __forceinline__ float ldx(const void* p, long long i, int dt) {
+  if constexpr (!LP) return static_cast<const float*>(p)[i];
+  else return dt == SE_DTYPE_BF16 ? (float)static_cast<const __bf16*>(p)[i] : (float)static_cast<const _Float16*>(p)[i];
+}
+template <bool LP>
+__device__ __forceinline__ void stx(void* p, long long i, float v, int dt) {
+  if constexpr (!LP) static_cast<float*>(p)[i] = v;
+  else if (dt == SE_DTYPE_BF16) static_cast<__bf16*>(p)[i] = (__bf16)v;
+  else static_cast<_Float16*>(p)[i] = (_Float16)v;
+}
+
 __device__ __forceinline__ int reflect_index(int i, int L) {
   if (i < 0) i = -i;
   if (i >= L) i = 2 * (L - 1) - i;
@@ -323,9 +338,9 @@ __device__ __forceinline__ int ceil_div_i(int a, int b) { return -floor_div(-a, 
 
 // Unpack two packed real-FFT results (pair j) and store rows k = 0..N/2 of frames
 // t0 + 2j, t0 + 2j + 1. out layout [B, N+2, T] or mags/phase [B, N/2+1, T].
-template <int CN, int CP>
+template <int CN, int CP, bool LP = false>
 __device__ void unpack_store(const float2* Z, int Pr, int Nr, int t0, int T, int b,
-                             float* out0, float* out1, int mag_phase) {
+                             void* out0, void* out1, int mag_phase, int dt) {
   const int N = CN ? CN : Nr, P = CP ? CP : Pr;
   const int half = N / 2 + 1;
   const int FT = 2 * P;
@@ -346,19 +361,20 @@ __device__ void unpack_store(const float2* Z, int Pr, int Nr, int t0, int T, int
     }
     im += 0.f;   // -0 -> +0: DC / Nyquist imag parts are exact zeros (atan2 branch cut)
     if (!mag_phase) {
-      out0[((long long)b * (2 * half) + k) * T + t] = re;
-      out0[((long long)b * (2 * half) + half + k) * T + t] = im;
+      stx<LP>(out0, ((long long)b * (2 * half) + k) * T + t, re, dt);
+      stx<LP>(out0, ((long long)b * (2 * half) + half + k) * T + t, im, dt);
     } else {
-      out0[((long long)b * half + k) * T + t] = sqrtf(re * re + im * im);
-      out1[((long long)b * half + k) * T + t] = atan2f(im, re);
+      stx<LP>(out0, ((long long)b * half + k) * T + t, sqrtf(re * re + im * im), dt);
+      stx<LP>(out1, ((long long)b * half + k) * T + t, atan2f(im, re), dt);
     }
   }
 }
 
 struct StftArgs {
-  const float* x;      // [B, L]
-  float* out0;
-  float* out1;
+  const void* x;       // [B, L]
+  void* out0;
+  void* out1;
+  int dt;              // SE_DTYPE_* of x / out0 / out1
   const float* window; // [win]
   const float2* tw;    // [N]
   int L, win, hop, T, pad, mag_phase, P;
@@ -366,28 +382,28 @@ struct StftArgs {
 };
 
 // grid (ceil(T / 2P), B)
-template <int CN, int CP>
+template <int CN, int CP, bool LP = false>
 __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   const int N = CN ? CN : a.pl.N, P = CP ? CP : a.P;
   float2* A = lds;
   float2* Bf = lds + P * N;
   const int b = blockIdx.y, t0 = blockIdx.x * 2 * P;
-  const float* x = a.x + (long long)b * a.L;
+  const long long xo = (long long)b * a.L;
   for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) {
     const int j = idx / N, n = idx - j * N;
     const int ta = t0 + 2 * j, tb = ta + 1;
     float ya = 0.f, yb = 0.f;
     if (n < a.win) {
       const float w = a.window[n];
-      if (ta < a.T) ya = w * x[reflect_index(ta * a.hop + n - a.pad, a.L)];
-      if (tb < a.T) yb = w * x[reflect_index(tb * a.hop + n - a.pad, a.L)];
+      if (ta < a.T) ya = w * ldx<LP>(a.x, xo + reflect_index(ta * a.hop + n - a.pad, a.L), a.dt);
+      if (tb < a.T) yb = w * ldx<LP>(a.x, xo + reflect_index(tb * a.hop + n - a.pad, a.L), a.dt);
     }
     A[idx] = make_float2(ya, yb);
   }
   __syncthreads();
   const float2* Z = fft_any<CN, CP>(A, Bf, P, a.pl, a.tw);
-  unpack_store<CN, CP>(Z, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase);
+  unpack_store<CN, CP, LP>(Z, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
 }
 
 // ConvSTFT with the in-place FFT: kPairsIP frame pairs per block in one LDS
@@ -397,7 +413,7 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
 // (tools/stft_micro.py; the XCD-aware block order merges the 32-B row segments
 // of neighbouring blocks in one L2)
 constexpr int kPairsIP = 4;
-template <int CN, int P = kPairsIP>
+template <int CN, int P = kPairsIP, bool LP = false>
 __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a) {
   constexpr int N = CN;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
@@ -405,7 +421,7 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   int tb, b;
   xcd_frame_block(tb, b);
   const int t0 = tb * 2 * P;
-  const float* x = a.x + (long long)b * a.L;
+  const long long xo = (long long)b * a.L;
   for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
   // frame gather: all of a thread's loads are issued before any is used
   // (compile-time trip count; branch-free clamped addresses and zero weights),
@@ -420,8 +436,8 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
     const bool ok = idx < P * N && n < a.win;
     const int nn = ok ? n : 0;
     const float w = ok ? a.window[nn] : 0.f;
-    const float xa = x[reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L)];
-    const float xb = x[reflect_index(min(tb, a.T - 1) * a.hop + nn - a.pad, a.L)];
+    const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+    const float xb = ldx<LP>(a.x, xo + reflect_index(min(tb, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
     ya[it] = ta < a.T ? w * xa : 0.f;
     yb[it] = tb < a.T ? w * xb : 0.f;
   }
@@ -432,12 +448,13 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   }
   __syncthreads();
   fft_pass_ip<N, P, 0, 1>(A, stw);
-  unpack_store<CN, P>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase);
+  unpack_store<CN, P, LP>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
 }
 
 struct IstftArgs {
-  const float* in;     // fwd: spec [B, N+2, T]; bwd: gout [B, out_len]
-  float* out;          // fwd: out [B, out_len]; bwd: gspec [B, N+2, T]
+  const void* in;      // fwd: spec [B, N+2, T]; bwd: gout [B, out_len]
+  void* out;           // fwd: out [B, out_len]; bwd: gspec [B, N+2, T]
+  int dt;              // SE_DTYPE_* of in / out
   const float* window;
   const float2* tw;
   int T, win, hop, offset, out_len, P, FT;
@@ -470,7 +487,7 @@ __device__ __forceinline__ float apply_g(float v, int n, float se_, float so_, f
 }
 
 // ConviSTFT forward. grid (ceil(out_len / (FT*hop)), B)
-template <int CN, int CP>
+template <int CN, int CP, bool LP = false>
 __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   __shared__ float sums[64];
@@ -483,15 +500,17 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
   const int s1 = min(s0 + a.FT * a.hop, a.offset + a.out_len);
   const int t_lo = max(0, ceil_div_i(s0 - a.win + 1, a.hop));
   const int t_hi = min(a.T - 1, floor_div(s1 - 1, a.hop));
-  const float* spec = a.in + (long long)b * 2 * half * a.T;
+  const long long so = (long long)b * 2 * half * a.T;
 
   // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
   for (int idx = threadIdx.x; idx < half * P; idx += blockDim.x) {
     const int k = idx / P, j = idx - k * P;
     const int ta = t_lo + 2 * j, tb = ta + 1;
     float2 xa = make_float2(0.f, 0.f), xb = xa;
-    if (ta <= t_hi) xa = make_float2(spec[(long long)k * a.T + ta], spec[(long long)(half + k) * a.T + ta]);
-    if (tb <= t_hi) xb = make_float2(spec[(long long)k * a.T + tb], spec[(long long)(half + k) * a.T + tb]);
+    if (ta <= t_hi) xa = make_float2(ldx<LP>(a.in, so + (long long)k * a.T + ta, a.dt),
+                                     ldx<LP>(a.in, so + (long long)(half + k) * a.T + ta, a.dt));
+    if (tb <= t_hi) xb = make_float2(ldx<LP>(a.in, so + (long long)k * a.T + tb, a.dt),
+                                     ldx<LP>(a.in, so + (long long)(half + k) * a.T + tb, a.dt));
     float2* c = A + j * N;
     if (k == 0 || k == N / 2) {
       // E[k] = Re X[k]; C = Re Xa + i Re Xb; store conj
@@ -518,7 +537,7 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
     fr[idx] = a.window[n] * apply_g(v, n, sums[2 * f], sums[2 * f + 1], inv_a, ce, co);
   }
   __syncthreads();
-  float* out = a.out + (long long)b * a.out_len;
+  const long long oo = (long long)b * a.out_len;
   for (int s = s0 + threadIdx.x; s < s1; s += blockDim.x) {
     const int tb0 = max(t_lo, ceil_div_i(s - a.win + 1, a.hop));
     const int tb1 = min(t_hi, floor_div(s, a.hop));
@@ -529,7 +548,7 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
       acc += fr[(t - t_lo) * a.win + n];
       cf += w * w;
     }
-    out[s - a.offset] = acc / (cf + 1e-8f);
+    stx<LP>(a.out, oo + s - a.offset, acc / (cf + 1e-8f), a.dt);
   }
 }
 
@@ -537,7 +556,7 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_kernel(const IstftArgs a) 
 // buffer holds the packed spectra, their FFT and then the windowed synthesis
 // frames (written over it through registers), so a block needs ~half the LDS of
 // istft_fwd_kernel and twice as many blocks share a CU. grid (ceil(out_len / (FT*hop)), B)
-template <int CN, int P>
+template <int CN, int P, bool LP = false>
 __global__ void __launch_bounds__(kThreads) istft_fwd_ip_kernel(const IstftArgs a) {
   constexpr int N = CN, half = N / 2 + 1;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
@@ -549,7 +568,7 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_ip_kernel(const IstftArgs 
   const int s1 = min(s0 + a.FT * a.hop, a.offset + a.out_len);
   const int t_lo = max(0, ceil_div_i(s0 - a.win + 1, a.hop));
   const int t_hi = min(a.T - 1, floor_div(s1 - 1, a.hop));
-  const float* spec = a.in + (long long)b * 2 * half * a.T;
+  const long long so = (long long)b * 2 * half * a.T;
   for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
   // spectrum gather: all of a thread's loads are issued before any is used
   // (compile-time trip count, clamped addresses, zeroed after the load)
@@ -560,10 +579,9 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_ip_kernel(const IstftArgs 
     const int idx = threadIdx.x + it * kThreads;
     const int k = min(idx / P, half - 1), j = idx % P;
     const int ta = min(t_lo + 2 * j, t_hi), tb = min(t_lo + 2 * j + 1, t_hi);
-    const float* re = spec + (long long)k * a.T;
-    const float* im = spec + (long long)(half + k) * a.T;
-    ga[it] = make_float2(re[ta], im[ta]);
-    gb[it] = make_float2(re[tb], im[tb]);
+    const long long re = so + (long long)k * a.T, im = so + (long long)(half + k) * a.T;
+    ga[it] = make_float2(ldx<LP>(a.in, re + ta, a.dt), ldx<LP>(a.in, im + ta, a.dt));
+    gb[it] = make_float2(ldx<LP>(a.in, re + tb, a.dt), ldx<LP>(a.in, im + tb, a.dt));
   }
   // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
 #pragma unroll
@@ -610,7 +628,7 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_ip_kernel(const IstftArgs 
     if (idx < 2 * P * N && n < a.win) fr[f * a.win + n] = v[it];
   }
   __syncthreads();
-  float* out = a.out + (long long)b * a.out_len;
+  const long long oo = (long long)b * a.out_len;
   for (int s = s0 + threadIdx.x; s < s1; s += kThreads) {
     const int tb0 = max(t_lo, ceil_div_i(s - a.win + 1, a.hop));
     const int tb1 = min(t_hi, floor_div(s, a.hop));
@@ -621,12 +639,12 @@ __global__ void __launch_bounds__(kThreads) istft_fwd_ip_kernel(const IstftArgs 
       acc += fr[(t - t_lo) * a.win + n];
       cf += w * w;
     }
-    out[s - a.offset] = acc / (cf + 1e-8f);
+    stx<LP>(a.out, oo + s - a.offset, acc / (cf + 1e-8f), a.dt);
   }
 }
 
 // Adjoint of istft_fwd. grid (ceil(T / 2P), B)
-template <int CN, int CP>
+template <int CN, int CP, bool LP = false>
 __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) {
   extern __shared__ __attribute__((aligned(16))) float2 lds[];
   __shared__ float sums[64];
@@ -636,7 +654,7 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) 
   int tb, b;
   xcd_frame_block(tb, b);
   const int t0 = tb * 2 * P;
-  const float* g = a.in + (long long)b * a.out_len;
+  const long long go = (long long)b * a.out_len;
   for (int idx = threadIdx.x; idx < P * N; idx += blockDim.x) {
     const int j = idx / N, n = idx - j * N;
     float va = 0.f, vb = 0.f;
@@ -656,7 +674,7 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) 
           const float ww = a.window[u - tt * a.hop];
           cf += ww * ww;
         }
-        const float v = w * g[u - a.offset] / (cf + 1e-8f);
+        const float v = w * ldx<LP>(a.in, go + u - a.offset, a.dt) / (cf + 1e-8f);
         if (h == 0) va = v; else vb = v;
       }
     }
@@ -676,12 +694,12 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_kernel(const IstftArgs a) 
   }
   __syncthreads();
   const float2* Z = fft_any<CN, CP>(A, Bf, P, a.pl, a.tw);
-  unpack_store<CN, CP>(Z, P, N, t0, a.T, b, a.out, nullptr, 0);
+  unpack_store<CN, CP, LP>(Z, P, N, t0, a.T, b, a.out, nullptr, 0, a.dt);
 }
 
 // istft_bwd on the in-place FFT (compiled plans): one P*N float2 LDS buffer,
 // static LDS, twice the resident blocks of the ping-pong form. grid (ceil(T / 2P), B)
-template <int CN, int P>
+template <int CN, int P, bool LP = false>
 __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs a) {
   constexpr int N = CN;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
@@ -691,7 +709,7 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
   int tb, b;
   xcd_frame_block(tb, b);
   const int t0 = tb * 2 * P;
-  const float* g = a.in + (long long)b * a.out_len;
+  const long long go = (long long)b * a.out_len;
   for (int i = threadIdx.x; i < N; i += kThreads) {
     stw[i] = a.tw[i];
     swin[i] = i < a.win ? a.window[i] : 0.f;
@@ -707,7 +725,7 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       const int u = (t0 + 2 * j + h) * a.hop + n;
-      ga[it][h] = a.out_len > 0 ? g[min(max(u - a.offset, 0), a.out_len - 1)] : 0.f;
+      ga[it][h] = a.out_len > 0 ? ldx<LP>(a.in, go + min(max(u - a.offset, 0), a.out_len - 1), a.dt) : 0.f;
     }
   }
   __syncthreads();
@@ -753,7 +771,7 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
   }
   __syncthreads();
   fft_pass_ip<N, P, 0, 1>(A, stw);
-  unpack_store<N, P>(A, P, N, t0, a.T, b, a.out, nullptr, 0);
+  unpack_store<N, P, LP>(A, P, N, t0, a.T, b, a.out, nullptr, 0, a.dt);
 }
 
 // ---------------------------------------------------------------------------
@@ -788,19 +806,27 @@ static int pick_pairs(int N) {
   return std::max(1, std::min(kPairs, p));   // sums[] holds 2 floats for 32 frames
 }
 
-// Launch K<CN, CP> for the compiled plans (CP = kPairs), else K<0, 0>.
+// Launch K<CN, CP, LP> for the compiled plans (CP = kPairs), else K<0, 0, LP>;
+// LP = the tensors are bf16 / fp16 (a.dt != SE_DTYPE_F32).
+#define SE_COMMA ,
+#define SE_LP_LAUNCH(K, grid, shm, st, a)                                                           \
+  do {                                                                                             \
+    if ((a).dt != SE_DTYPE_F32) hipLaunchKernelGGL((K, true>), grid, dim3(kThreads), shm, st, a);  \
+    else hipLaunchKernelGGL((K, false>), grid, dim3(kThreads), shm, st, a);                        \
+  } while (0)
 #define SE_STFT_DISPATCH(K, nfft, P, grid, shm, st, a)                                              \
   do {                                                                                             \
     const bool cp_ = (P) == kPairs;                                                                \
     switch (cp_ ? (nfft) : 0) {                                                                    \
-      case 640: hipLaunchKernelGGL((K<640, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
-      case 512: hipLaunchKernelGGL((K<512, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
-      case 400: hipLaunchKernelGGL((K<400, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
-      case 320: hipLaunchKernelGGL((K<320, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
-      case 256: hipLaunchKernelGGL((K<256, kPairs>), grid, dim3(kThreads), shm, st, a); break;     \
-      default: hipLaunchKernelGGL((K<0, 0>), grid, dim3(kThreads), shm, st, a); break;             \
+      case 640: SE_LP_LAUNCH(K<640 SE_COMMA kPairs, grid, shm, st, a); break;                      \
+      case 512: SE_LP_LAUNCH(K<512 SE_COMMA kPairs, grid, shm, st, a); break;                      \
+      case 400: SE_LP_LAUNCH(K<400 SE_COMMA kPairs, grid, shm, st, a); break;                      \
+      case 320: SE_LP_LAUNCH(K<320 SE_COMMA kPairs, grid, shm, st, a); break;                      \
+      case 256: SE_LP_LAUNCH(K<256 SE_COMMA kPairs, grid, shm, st, a); break;                      \
+      default: SE_LP_LAUNCH(K<0 SE_COMMA 0, grid, shm, st, a); break;                              \
     }                                                                                              \
   } while (0)
+static int dtype_ok(int dt) { return dt == SE_DTYPE_F32 || dt == SE_DTYPE_BF16 || dt == SE_DTYPE_F16; }
 
 static int check_common(int win, int hop, int nfft, FftPlan& pl) {
   if (win <= 0 || hop <= 0 || nfft <= 0 || win > nfft) return SE_E_ARG;
@@ -819,19 +845,20 @@ extern "C" int se_stft_num_frames(int L, int win, int hop, int nfft, int center)
   return (Lp - win) / hop + 1;
 }
 
-extern "C" int se_stft_fwd(const float* x, float* out0, float* out1, int B, int L, int win,
+extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, int win,
                            int hop, int nfft, int center, int mag_phase, const float* window,
-                           const float* twiddle, void* stream) {
+                           const float* twiddle, int dtype, void* stream) {
   FftPlan pl;
   int rc = check_common(win, hop, nfft, pl);
   if (rc) return rc;
-  if (!x || !out0 || !window || !twiddle || B <= 0 || L <= 0 || (mag_phase && !out1)) return SE_E_ARG;
+  if (!x || !out0 || !window || !twiddle || B <= 0 || L <= 0 || (mag_phase && !out1) || !dtype_ok(dtype))
+    return SE_E_ARG;
   const int pad = center ? nfft / 2 : 0;
   if (center && L <= pad) return SE_E_SHAPE;   // reflect pad needs L > pad (F.pad reflect)
   const int T = se_stft_num_frames(L, win, hop, nfft, center);
   if (T <= 0) return SE_E_SHAPE;
   StftArgs a{};
-  a.x = x; a.out0 = out0; a.out1 = out1; a.window = window; a.tw = (const float2*)twiddle;
+  a.x = x; a.out0 = out0; a.out1 = out1; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
   a.L = L; a.win = win; a.hop = hop; a.T = T; a.pad = pad; a.mag_phase = mag_phase;
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
@@ -848,10 +875,10 @@ extern "C" int se_stft_fwd(const float* x, float* out0, float* out1, int B, int 
     hipStream_t st = se::as_stream(stream);
 #define SE_STFT_IP(NF)                                                                              \
   do {                                                                                              \
-    if (P == 2) hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 2>), grid, dim3(kThreads), 0, st, a);    \
-    else if (P == 4) hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 4>), grid, dim3(kThreads), 0, st, a); \
-    else if (P == 16) hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 16>), grid, dim3(kThreads), 0, st, a); \
-    else hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 8>), grid, dim3(kThreads), 0, st, a);           \
+    if (P == 2) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 2, grid, 0, st, a);                     \
+    else if (P == 4) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 4, grid, 0, st, a);                \
+    else if (P == 16) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 16, grid, 0, st, a);              \
+    else SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 8, grid, 0, st, a);                            \
   } while (0)
     switch (nfft) {
       case 640: SE_STFT_IP(640); break;
@@ -885,15 +912,15 @@ static int istft_setup(int B, int T, int win, int hop, int nfft, int offset, int
   return SE_OK;
 }
 
-extern "C" int se_istft_fwd(const float* spec, float* out, int B, int T, int win, int hop,
+extern "C" int se_istft_fwd(const void* spec, void* out, int B, int T, int win, int hop,
                             int nfft, int offset, int out_len, const float* window,
-                            const float* twiddle, void* stream) {
+                            const float* twiddle, int dtype, void* stream) {
   IstftArgs a{};
   int rc = istft_setup(B, T, win, hop, nfft, offset, out_len, a);
   if (rc) return rc;
-  if (!spec || !out || !window || !twiddle) return SE_E_ARG;
+  if (!spec || !out || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
   if (out_len == 0) return SE_OK;
-  a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle;
+  a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
   if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
     // in-place FFT, SEHIP_ISTFT_IP_PAIRS = 4 / 8 frame pairs per block (A/B knob)
     static const int ip_pairs = [] {
@@ -909,8 +936,8 @@ extern "C" int se_istft_fwd(const float* spec, float* out, int B, int T, int win
       hipStream_t st = se::as_stream(stream);
 #define SE_ISTFT_IP(NF)                                                                             \
   do {                                                                                              \
-    if (P == 8) hipLaunchKernelGGL((istft_fwd_ip_kernel<NF, 8>), grid, dim3(kThreads), 0, st, a);   \
-    else hipLaunchKernelGGL((istft_fwd_ip_kernel<NF, 4>), grid, dim3(kThreads), 0, st, a);          \
+    if (P == 8) SE_LP_LAUNCH(istft_fwd_ip_kernel<NF SE_COMMA 8, grid, 0, st, a);                    \
+    else SE_LP_LAUNCH(istft_fwd_ip_kernel<NF SE_COMMA 4, grid, 0, st, a);                           \
   } while (0)
       switch (nfft) {
         case 640: SE_ISTFT_IP(640); break;
@@ -933,14 +960,14 @@ extern "C" int se_istft_fwd(const float* spec, float* out, int B, int T, int win
   return SE_OK;
 }
 
-extern "C" int se_istft_bwd(const float* gout, float* gspec, int B, int T, int win, int hop,
+extern "C" int se_istft_bwd(const void* gout, void* gspec, int B, int T, int win, int hop,
                             int nfft, int offset, int out_len, const float* window,
-                            const float* twiddle, void* stream) {
+                            const float* twiddle, int dtype, void* stream) {
   IstftArgs a{};
   int rc = istft_setup(B, T, win, hop, nfft, offset, out_len, a);
   if (rc) return rc;
-  if (!gout || !gspec || !window || !twiddle) return SE_E_ARG;
-  a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle;
+  if (!gout || !gspec || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
+  a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
   if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
     // in-place FFT, SEHIP_ISTFT_IP_PAIRS = 4 / 8 frame pairs per block (A/B knob)
     static const int ip_pairs = [] {
@@ -953,8 +980,8 @@ extern "C" int se_istft_bwd(const float* gout, float* gspec, int B, int T, int w
     hipStream_t st = se::as_stream(stream);
 #define SE_ISTFT_BWD_IP(NF)                                                                         \
   do {                                                                                              \
-    if (P == 8) hipLaunchKernelGGL((istft_bwd_ip_kernel<NF, 8>), grid, dim3(kThreads), 0, st, a);   \
-    else hipLaunchKernelGGL((istft_bwd_ip_kernel<NF, 4>), grid, dim3(kThreads), 0, st, a);          \
+    if (P == 8) SE_LP_LAUNCH(istft_bwd_ip_kernel<NF SE_COMMA 8, grid, 0, st, a);                    \
+    else SE_LP_LAUNCH(istft_bwd_ip_kernel<NF SE_COMMA 4, grid, 0, st, a);                           \
   } while (0)
     switch (nfft) {
       case 640: SE_ISTFT_BWD_IP(640); break;

@@ -38,7 +38,16 @@ class ConvDesc(ctypes.Structure):
         ("x_amax", c_void_p), ("dy_amax", c_void_p),   # SE_MATH_F16X3 scale sources (or NULL)
         ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p),   # CL16 operands (or NULL)
         ("w_amax", c_void_p),   # SE_MATH_F16X3 bound of max |w| (or NULL)
-        ("accumulate_dx", c_int)]   # se_conv2d_bwd_data: dx += dL/dx (ABI 3)
+        ("accumulate_dx", c_int),   # se_conv2d_bwd_data: dx += dL/dx (ABI 3)
+        ("dtype", c_int)]           # SE_DTYPE_* storage of the conv's tensors (ABI 4)
+
+
+class FirstConvDesc(ctypes.Structure):
+    """Mirror of se_first_conv (include/sehip.h)."""
+
+    _fields_ = [("x0", c_void_p)] + [(n, c_int) for n in (
+        "cin", "in_h", "in_w", "kernel_h", "kernel_w", "stride_h", "stride_w", "pad_h", "pad_w",
+        "dil_h", "dil_w")] + [("dwr", c_void_p), ("dwi", c_void_p)]
 
 
 _P = c_void_p
@@ -51,9 +60,9 @@ _SIGNATURES = {
     "se_stream_create_cu_subset": (c_int, [c_int, c_int, _PP]),
     "se_stream_destroy": (c_int, [_P]),
     "se_stft_num_frames": (c_int, [c_int] * 5),
-    "se_stft_fwd": (c_int, [_P, _P, _P] + [c_int] * 7 + [_P, _P, _P]),
-    "se_istft_fwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
-    "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, _P]),
+    "se_stft_fwd": (c_int, [_P, _P, _P] + [c_int] * 7 + [_P, _P, c_int, _P]),
+    "se_istft_fwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, c_int, _P]),
+    "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, c_int, _P]),
     "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
     "se_amax": (c_int, [_P, ctypes.c_longlong, _P, _P]),
     "se_amax_weights": (c_int, [_P, ctypes.c_longlong, _P, _P, _P]),
@@ -72,14 +81,16 @@ _SIGNATURES = {
     "se_conv2d_bwd_data_joined": (c_int, [_P] * 5 + [c_int, c_int, _P, _P, c_size_t, _P]),
     "se_conv2d_bwd_weight_joined": (c_int, [_P, _P, c_int, c_int] + [_P] * 6 + [_P, c_size_t, _P]),
     "se_cbn_workspace_size": (c_size_t, [c_int, c_int, c_int]),
-    "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P,
-                           c_int, c_float, c_float, c_int, c_float, _P, _P,
-                           c_size_t, _P]),
-    "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP,
-                           c_int, c_int, c_float, _P, _P, c_size_t, _P]),
-    "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP,
-                            c_int, c_int, c_float, _P, _P, c_size_t, _P]),
+    "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P, c_int, c_float, c_float, c_int,
+                           c_float, _P, _P, c_int, _P, c_size_t, _P]),
+    "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
+                           c_int, _P, c_size_t, _P]),
+    "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
+                            c_int, _P, c_size_t, _P]),
     "se_cbn_head_workspace_size": (c_size_t, [c_int, c_int, c_int]),
+    "se_cbn_first_conv_workspace_size": (c_size_t, [c_int] * 6),
+    "se_cbn_bwd_first_conv": (c_int, [_P, _P, _P] + [c_int] * 4 + [_PP, _P, _PP, c_int, c_int, c_float, _P, _P,
+                                                                  c_size_t, _P]),
     "se_cbn_head_fwd": (c_int, [_P, _P] + [c_int] * 4 + [_PP, _PP, _P, _P, c_int, c_float, c_float, c_int,
                                 c_float, _P, c_int, c_int, _P, c_size_t, _P]),
     "se_cbn_head_bwd": (c_int, [_P, _P, _P] + [c_int] * 4 + [_PP, _P, _PP, _P, _P, c_int, c_int, c_int, c_int,
@@ -90,10 +101,12 @@ _SIGNATURES = {
     "se_lstm_bwd": (c_int, [_P] * 5 + [c_int] * 4 + [ctypes.c_uint, _P]),
     "se_bn_workspace_size": (c_size_t, [c_int, c_int]),
     "se_bn_fwd": (c_int, [_P, ctypes.c_longlong, c_int, c_int, c_int, _P, _P, _P, _P, c_int, c_float, c_float,
-                          c_int, _P, c_int, c_float, _P, _P, _P, c_size_t, _P]),
+                          c_int, _P, c_int, c_float, _P, _P, c_int, _P, c_size_t, _P]),
     "se_bn_bwd": (c_int, [_P, _P, ctypes.c_longlong, c_int, c_int, c_int, _P, _P, _P, c_int, c_int, _P, c_int,
-                          c_float, _P, _P, _P, _P, _P, c_size_t, _P]),
+                          c_float, _P, _P, _P, _P, c_int, _P, c_size_t, _P]),
     "se_sisnr_save_bytes": (c_size_t, [c_int]),
+    "se_mask_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P]),
+    "se_mask_bwd": (c_int, [_P, _P, _P, c_int, c_int, c_int, _P, _P]),
     "se_sisnr_fwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P]),
     "se_sisnr_bwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P,
                              ctypes.c_longlong, _P]),
@@ -173,6 +186,17 @@ def require_device(*ts: torch.Tensor, dtype=torch.float32) -> None:
                                "there is no CPU fallback in the product path")
         if t.dtype != dtype:
             raise RuntimeError(f"sehip ops take {dtype} tensors (got {t.dtype})")
+
+
+# SE_DTYPE_* (include/sehip.h): storage types of the dtype-aware entry points
+DTYPES = {torch.float32: 0, torch.bfloat16: 1, torch.float16: 2}
+
+
+def dtype_code(t: torch.Tensor) -> int:
+    try:
+        return DTYPES[t.dtype]
+    except KeyError:
+        raise RuntimeError(f"sehip: unsupported storage type {t.dtype} (fp32, bf16, fp16)") from None
 
 
 def ptr_array(ts):

@@ -103,12 +103,12 @@ class _FusedComplexConv(nn.Module):
         xs, rebuild = _stacked(x)
         c = self._geometry()
         begin, end = _fold_pad(c.padding, input_pad, self.transposed)
-        y = F.conv2d(_f32(xs), _f32(c.weight), _f32(self.imag_conv.weight), _f32(c.bias), _f32(self.imag_conv.bias),
+        y = F.conv2d(xs, c.weight, self.imag_conv.weight, c.bias, self.imag_conv.bias,
                      out_channels=2 * c.out_channels, kernel=c.kernel_size, stride=c.stride,
                      padding=begin, padding_end=end, dilation=c.dilation,
                      output_padding=getattr(c, "output_padding", (0, 0)),
                      transposed=self.transposed, exact=self.exact_fp32)
-        return rebuild(y.to(xs.dtype))
+        return rebuild(y)
 
     def forward_joined(self, x, skip):
         """self(complex_concat([align(x), skip])) with the FRCRN decoder's
@@ -154,11 +154,10 @@ def real_conv2d(conv: nn.Module, x, input_pad=None):
     if conv.groups != 1 or isinstance(conv.padding, str):
         raise NotImplementedError("sehip real conv: groups / string padding")
     begin, end = _fold_pad(conv.padding, input_pad, tr)
-    y = F.conv2d(_f32(x), _f32(conv.weight), None, _f32(conv.bias), None, out_channels=conv.out_channels,
-                 kernel=conv.kernel_size, stride=conv.stride, padding=begin, padding_end=end,
-                 dilation=conv.dilation, output_padding=getattr(conv, "output_padding", (0, 0)),
-                 transposed=tr, exact=getattr(conv, "sehip_exact_fp32", False))
-    return y.to(x.dtype)
+    return F.conv2d(x, conv.weight, None, conv.bias, None, out_channels=conv.out_channels,
+                    kernel=conv.kernel_size, stride=conv.stride, padding=begin, padding_end=end,
+                    dilation=conv.dilation, output_padding=getattr(conv, "output_padding", (0, 0)),
+                    transposed=tr, exact=getattr(conv, "sehip_exact_fp32", False))
 
 
 # ------------------------------------------------------------- linear / LSTM
@@ -331,15 +330,17 @@ class ComplexBatchNorm2d(nn.Module):
                 self.Wrr.fill_(1); self.Wii.fill_(1)
                 self.Wri.uniform_(-.9, +.9)
 
-    def forward_act(self, x, act=F.ACT_NONE, slope=0.0, fork=False):
-        """BN followed by a fused activation (LeakyReLU / ReLU). fork=True returns
-        (y, alias of y) for two consumers (see functional.complex_batch_norm)."""
+    def forward_act(self, x, act=F.ACT_NONE, slope=0.0, fork=False, prelu=None):
+        """BN followed by a fused activation (LeakyReLU / ReLU, or the weight of a
+        one-parameter nn.PReLU). fork=True returns (y, alias of y) for two consumers
+        (see functional.complex_batch_norm). x may be fp32, bf16 or fp16 storage, with
+        the module in the same dtype (model.to(bfloat16) / .half())."""
         running = (self.RMr, self.RMi, self.RVrr, self.RVri, self.RVii) if self.track_running_stats else None
         training = self.training or not self.track_running_stats    # complex_nn.py:234
         return F.complex_batch_norm(
             x, self.Wrr, self.Wri, self.Wii, self.Br, self.Bi, running,
             self.num_batches_tracked if self.track_running_stats else None,
-            training, self.eps, self.momentum, act, slope, fork)
+            training, self.eps, self.momentum, act, slope, fork, prelu)
 
     def forward(self, inputs):
         return self.forward_act(inputs)
@@ -349,18 +350,27 @@ class ComplexBatchNorm2d(nn.Module):
                 "track_running_stats={track_running_stats}".format(**self.__dict__))
 
 
+def _module_dtype(m: nn.Module, default):
+    for t in list(m.parameters(recurse=False)) + list(m.buffers(recurse=False)):
+        if t is not None and t.is_floating_point():
+            return t.dtype
+    return default
+
+
 def norm_act(norm: nn.Module, act: nn.Module, x, fork: bool = False):
     """act(norm(x)) with the activation fused into the CBN kernel when both are
     the kinds the kernel knows; otherwise the two modules are applied in turn.
     fork=True returns (y, y2) for two consumers of y: with the CBN kernel y2 is an
     alias whose gradient the CBN backward sums itself; otherwise y2 is y."""
-    if isinstance(norm, ComplexBatchNorm2d):
+    if isinstance(norm, ComplexBatchNorm2d) and _module_dtype(norm, x.dtype) == x.dtype:
         if isinstance(act, nn.LeakyReLU):
             return norm.forward_act(x, F.ACT_LEAKY, act.negative_slope, fork)
         if isinstance(act, nn.ReLU):
             return norm.forward_act(x, F.ACT_RELU, 0.0, fork)
         if isinstance(act, nn.Identity):
             return norm.forward_act(x, fork=fork)
+        if isinstance(act, nn.PReLU) and act.weight.numel() == 1 and act.weight.dtype == x.dtype:
+            return norm.forward_act(x, fork=fork, prelu=act.weight)   # DCCRN, dccrn.py:21,45
     y = act(norm(x))
     return (y, y) if fork else y
 

@@ -41,8 +41,8 @@ class _KernelTables(nn.Module):
     """Keeps the kernels' private fp32 tables (window, twiddles) in fp32 when the
     module is cast (model.half() / .to(bfloat16), as the reference's low-precision
     configs do): the state_dict buffers follow the cast like the reference's, the
-    tables the kernels read do not. Inputs of another float dtype are computed on
-    the fp32 kernels and returned in the caller's dtype."""
+    tables the kernels read do not. bf16 / fp16 signals and spectra are read and
+    written in their own dtype by the kernels (SE_DTYPE_*), fp32 arithmetic."""
 
     _tables = ("_win", "_tw")
 
@@ -81,11 +81,8 @@ class ConvSTFT(_KernelTables):
             raise RuntimeError(f"ConvSTFT expects [L], [B, L] or [B, 1, L], got {tuple(inputs.shape)}")
         if self.center and x.shape[-1] <= self.pad:
             raise RuntimeError(f"reflect padding {self.pad} needs an input longer than {self.pad}")
-        out = F.stft(x.float(), self._win, self._tw, self.window_size, self.hop_size, self.fft_size,
-                     self.center, self.return_mag_phase)
-        if x.dtype == torch.float32:
-            return out
-        return tuple(o.to(x.dtype) for o in out) if self.return_mag_phase else out.to(x.dtype)
+        return F.stft(x, self._win, self._tw, self.window_size, self.hop_size, self.fft_size,
+                      self.center, self.return_mag_phase)
 
 
 class ConviSTFT(_KernelTables):
@@ -114,6 +111,5 @@ class ConviSTFT(_KernelTables):
         else:
             offset = 0
             n = full if output_length is None else min(output_length, full)
-        out = F.istft(inputs.float(), self._win, self._tw, self.window_size, self.hop_size,
-                      self.fft_size, offset, max(n, 0))
-        return out if inputs.dtype == torch.float32 else out.to(inputs.dtype)
+        return F.istft(inputs, self._win, self._tw, self.window_size, self.hop_size,
+                       self.fft_size, offset, max(n, 0))

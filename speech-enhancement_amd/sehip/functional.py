@@ -139,7 +139,9 @@ _TIMER: OpTimer | None = None
 # path's error against fp64) at the MFMA cost of bf16x3.
 # Initial value from SEHIP_CONV_MATH ("f32", "bf16x3", or per pass as
 # "fwd=bf16x3,data=f32,weight=bf16x3"); set_conv_math() changes it.
-_MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2, "bf16": 3, "f16x3": 4}
+_MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2, "bf16": 3, "f16x3": 4, "f16": 5}
+# storage dtype -> the one-term MFMA math 16-bit storage runs (se_conv2d_desc.dtype)
+_STORAGE_MATH = {torch.bfloat16: 3, torch.float16: 5}
 _PASSES = ("fwd", "data", "weight")
 _CONV_MATH = {p: 0 for p in _PASSES}
 # Optional override for the forward passes of transposed convs (the decoder) whose
@@ -336,6 +338,9 @@ SE_MATH_F32 = 0
 
 
 def _pass_math(pass_name, d) -> int:
+    fm = getattr(d, "force_math", None)
+    if fm is not None:   # 16-bit storage: the one-term MFMA of its format on every pass
+        return fm
     m = _CONV_MATH[pass_name]
     if pass_name == "fwd" and _FWD_DEC[0] is not None and d.transposed and d.in_h >= _FWD_DEC[1]:
         m = _FWD_DEC[0]
@@ -418,11 +423,14 @@ class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wr, wi, br, bi, geom):
         (out_channels, kernel, stride, padding, dilation, output_padding, transposed, complex_w,
-         padding_end, exact) = geom
-        N.require_device(x, wr, wi, br, bi)
+         padding_end, exact, force_math) = geom
+        N.require_device(x, wr, wi, br, bi, dtype=x.dtype)
         x = x.contiguous()
         d = conv_desc(tuple(x.shape), out_channels, kernel, stride, padding, dilation,
                       output_padding, transposed, complex_w, padding_end, exact)
+        d.force_math = force_math
+        d.dtype = N.dtype_code(x)
+        d.math = _pass_math("fwd", d)
         lib = N.lib()
         ho, wo = N.c_int(), N.c_int()
         N.check(lib.se_conv2d_out_shape(N.ctypes.byref(d), N.ctypes.byref(ho), N.ctypes.byref(wo)),
@@ -440,7 +448,7 @@ class _Conv2d(torch.autograd.Function):
                                   N.stream_of(x)), "se_conv2d_fwd")
         if t0 is not None:   # bytes: x read + y written + the weights, once
             _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
-                       4.0 * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
+                       x.element_size() * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
         ctx.save_for_backward(x, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax, ctx.w_amax = d, nbytes, br is not None, xa, wa
         return y
@@ -614,12 +622,34 @@ class _ConvJoined(torch.autograd.Function):
 def conv2d_joined(x, s, wr, wi, br=None, bi=None, *, out_channels, kernel, stride=1, padding=0,
                   dilation=1, output_padding=0, transposed=False):
     """conv2d(complex_join(x, s), ...) with the join folded into the GEMMs.
-    x: [B, C, Fx, Tx] decoder state, s: [B, C, F, T] skip, Fx <= F, Tx >= T."""
+    x: [B, C, Fx, Tx] decoder state, s: [B, C, F, T] skip, Fx <= F, Tx >= T.
+    (fp32; other storage types run on fp32 copies.)"""
     if x.shape[1] != s.shape[1] or x.shape[2] > s.shape[2] or x.shape[3] < s.shape[3]:
         raise ValueError(f"sehip conv2d_joined: cannot align {tuple(x.shape)} to {tuple(s.shape)}")
+    if x.dtype != torch.float32:
+        f32 = lambda t: None if t is None else t.float()
+        return conv2d_joined(x.float(), s.float(), f32(wr), f32(wi), f32(br), f32(bi), out_channels=out_channels,
+                             kernel=kernel, stride=stride, padding=padding, dilation=dilation,
+                             output_padding=output_padding, transposed=transposed).to(x.dtype)
     geom = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
             _pair(output_padding), bool(transposed))
     return _ConvJoined.apply(x, s, wr, wi, br, bi, geom)
+
+
+NATIVE16_CALLS = [0]   # convs run on 16-bit storage natively (diagnostics / tests)
+
+
+def _native16_ok(x, wr, wi, br, bi, out_channels, transposed) -> bool:
+    """Whether every pass of a 16-bit-storage conv runs natively (se_conv2d_desc.dtype):
+    the weight-grad's direct operand channels N (out for a conv, in for a convT) on the
+    one-term split tiles (N % 16 == 0, N > 8) when the weights take a gradient."""
+    ts = [t for t in (wr, wi, br, bi) if t is not None]
+    if any(t.dtype != x.dtype for t in ts) or os.environ.get("SEHIP_NATIVE16", "1") == "0":
+        return False
+    if not any(t.requires_grad for t in ts) or not torch.is_grad_enabled():
+        return True
+    n = x.shape[1] if transposed else out_channels
+    return n % 16 == 0 and n > 8
 
 
 def conv2d(x, wr, wi=None, br=None, bi=None, *, out_channels, kernel, stride=1, padding=0,
@@ -627,11 +657,23 @@ def conv2d(x, wr, wi=None, br=None, bi=None, *, out_channels, kernel, stride=1, 
     """Fused complex conv (wi given) or real conv (wi None) on the HIP path.
     padding is the (top, left) begin padding; padding_end (bottom, right)
     defaults to the same (symmetric, as nn.Conv2d). exact=True: a data-fed conv
-    (see _pass_math) whose f16x3 passes run exact fp32 instead."""
-    geom = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
+    (see _pass_math) whose f16x3 passes run exact fp32 instead.
+    bf16 / fp16 tensors (model.to(bfloat16) / .half()) are read and written in their
+    own dtype by the one-term MFMA of that format on every pass; shapes those kernels
+    do not cover compute the same one-term arithmetic on fp32 copies."""
+    base = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
             _pair(output_padding), bool(transposed), wi is not None,
             None if padding_end is None else _pair(padding_end), bool(exact))
-    return _Conv2d.apply(x, wr, wi, br, bi, geom)
+    if x.dtype == torch.float32:
+        return _Conv2d.apply(x, wr, wi, br, bi, base + (None,))
+    if x.dtype not in _STORAGE_MATH:
+        raise RuntimeError(f"sehip conv2d: unsupported storage type {x.dtype}")
+    fm = _STORAGE_MATH[x.dtype]
+    if _native16_ok(x, wr, wi, br, bi, out_channels, transposed):
+        NATIVE16_CALLS[0] += 1
+        return _Conv2d.apply(x, wr, wi, br, bi, base + (fm,))
+    f32 = lambda t: None if t is None else t.float()
+    return _Conv2d.apply(x.float(), f32(wr), f32(wi), f32(br), f32(bi), base + (fm,)).to(x.dtype)
 
 
 # --------------------------------------------------------------------------
@@ -641,10 +683,17 @@ ACT_NONE, ACT_LEAKY, ACT_RELU = 0, 1, 2
 
 
 class _ComplexBN(torch.autograd.Function):
+    """ComplexBatchNorm2d (+ fused LeakyReLU / ReLU, or a one-weight nn.PReLU as
+    `prelu`) on se_cbn_*. x, the parameters, running statistics and prelu share the
+    storage type (fp32, or bf16 / fp16 for model.to(bfloat16) / .half()): the kernels
+    read and write that type directly, with fp32 arithmetic and fp64 moments."""
+
     @staticmethod
     def forward(ctx, x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum, act, slope,
-                fork=False):
-        N.require_device(x, wrr)
+                fork=False, prelu=None):
+        N.require_device(x, dtype=x.dtype)
+        N.require_device(wrr, wri, wii, br, bi, prelu, *(running or ()), dtype=x.dtype)
+        dt = N.dtype_code(x)
         x = x.contiguous()
         b, c = x.shape[:2]
         hw = x[0, 0].numel()
@@ -654,18 +703,22 @@ class _ComplexBN(torch.autograd.Function):
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
         mom = -1.0 if momentum is None else float(momentum)
-        ya = new_amax(x.device) if training else None   # bound of max |y| (F16X3 consumers)
+        if prelu is not None:
+            act, slope = ACT_LEAKY, 0.0
+        # bound of max |y| for an f16x3 consumer (fp32 storage only)
+        ya = new_amax(x.device) if training and dt == 0 else None
         t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
                                N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
                                save.data_ptr(), int(training), float(eps), mom, int(act),
-                               float(slope), N.ptr(ya), ws.data_ptr(), ws.numel(), N.stream_of(x)),
+                               float(slope), N.ptr(ya), N.ptr(prelu), dt, ws.data_ptr(), ws.numel(),
+                               N.stream_of(x)),
                 "se_cbn_fwd")
         if ya is not None:
             amax_put(y, ya)
         if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write
-            _TIMER.end("cbn_fwd", t0, 0.0, 4.0 * x.numel() * (3 if training else 2))
-        ctx.save_for_backward(x, save, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
+            _TIMER.end("cbn_fwd", t0, 0.0, x.element_size() * x.numel() * (3 if training else 2))
+        ctx.save_for_backward(x, save, prelu, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         if fork:   # (y, alias of y): two consumers, two gradients summed inside se_cbn_bwd2
             ctx.set_materialize_grads(False)
@@ -676,7 +729,7 @@ class _ComplexBN(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, gy, gy2=None):
-        x, save, *params = ctx.saved_tensors
+        x, save, prelu, *params = ctx.saved_tensors
         training, act, slope, affine = ctx.cfg
         if ctx.fork is not None:   # a gradient handed over but not accumulated by a conv
             g3 = fork_take(ctx.fork)
@@ -691,43 +744,146 @@ class _ComplexBN(torch.autograd.Function):
         if gy is None:
             gy, gy2 = gy2, None
         if gy is None:
-            return (None,) * 14
+            return (None,) * 15
         gy = gy.contiguous()
         gy2 = gy2.contiguous() if gy2 is not None else None
+        dt = N.dtype_code(x)
         b, c = x.shape[:2]
         hw = x[0, 0].numel()
         dx = torch.empty_like(x)
         dparams = [torch.empty_like(p) for p in params] if affine else None
+        dprelu = torch.empty_like(prelu) if prelu is not None else None
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
-        dxa = new_amax(x.device) if training else None   # bound of max |dx| (the conv's dy)
+        dxa = new_amax(x.device) if training and dt == 0 else None   # bound of max |dx| (the conv's dy)
         t0 = _TIMER.begin() if _TIMER else None
         if gy2 is None:
             N.check(lib.se_cbn_bwd(gy.data_ptr(), None, x.data_ptr(), dx.data_ptr(), b, c, hw,
                                    N.ptr_array(params if affine else None), save.data_ptr(),
-                                   N.ptr_array(dparams), training, act, slope, N.ptr(dxa),
-                                   ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
+                                   N.ptr_array(dparams), training, act, slope, N.ptr(dxa), N.ptr(prelu),
+                                   N.ptr(dprelu), dt, ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd")
         else:
             N.check(lib.se_cbn_bwd2(gy.data_ptr(), gy2.data_ptr(), x.data_ptr(), dx.data_ptr(), b,
                                     c, hw, N.ptr_array(params if affine else None),
                                     save.data_ptr(), N.ptr_array(dparams), training, act, slope,
-                                    N.ptr(dxa), ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd2")
+                                    N.ptr(dxa), N.ptr(prelu), N.ptr(dprelu), dt, ws.data_ptr(), ws.numel(),
+                                    N.stream_of(gy)), "se_cbn_bwd2")
         if dxa is not None:
             amax_put(dx, dxa)
         if t0 is not None:   # (gy [, gy2], x) read twice + dx written
-            _TIMER.end("cbn_bwd", t0, 0.0, 4.0 * x.numel() * (5 if gy2 is None else 7))
+            _TIMER.end("cbn_bwd", t0, 0.0, x.element_size() * x.numel() * (5 if gy2 is None else 7))
         g = dparams or [None] * 5
-        return (dx, *g, None, None, None, None, None, None, None, None)
+        return (dx, *g, None, None, None, None, None, None, None, None, dprelu)
 
 
 def complex_batch_norm(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
-                       act=ACT_NONE, slope=0.0, fork=False):
+                       act=ACT_NONE, slope=0.0, fork=False, prelu=None):
     """ComplexBatchNorm2d forward (+ optional fused activation) on the HIP path.
     running: (RMr, RMi, RVrr, RVri, RVii) or None; nbt: int64 tensor or None.
+    prelu: the weight of a one-parameter nn.PReLU applied after the norm (fused).
     fork=True returns (y, alias of y) for two consumers: their two gradients are summed inside
     the backward kernels (se_cbn_bwd2) instead of by autograd's accumulation add."""
     return _ComplexBN.apply(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
-                            act, slope, fork)
+                            act, slope, fork, prelu)
+
+
+class _FirstBlock(torch.autograd.Function):
+    """A model's first block, conv -> ComplexBatchNorm2d + act, in training, with a
+    conv input that needs no gradient (the noisy spectrum; FRCRN's encoder layer 0,
+    frcrn.py:28-34, 62-76). Forward: the conv (exact fp32: the data-fed conv, see
+    _pass_math) and the CBN forward. Backward: se_cbn_bwd_first_conv, the CBN
+    backward with the conv's weight gradient accumulated in its apply pass (exact
+    fp32 products), so the conv's dy is never written and no weight-grad GEMM reads
+    it back. fork=True returns (y, alias of y) as complex_batch_norm."""
+
+    @staticmethod
+    def forward(ctx, x0, wr, wi, wrr, wri, wii, br, bi, running, nbt, eps, momentum, act, slope, cgeom, fork):
+        kernel, stride, padding, padding_end, dilation = cgeom
+        N.require_device(x0, wr, wi, wrr)
+        x0 = x0.contiguous()
+        lib = N.lib()
+        out_channels = 2 * wr.shape[0]
+        d = conv_desc(tuple(x0.shape), out_channels, kernel, stride, padding, dilation, (0, 0), False, True,
+                      padding_end, exact=True)
+        ho, wo = N.c_int(), N.c_int()
+        N.check(lib.se_conv2d_out_shape(N.ctypes.byref(d), N.ctypes.byref(ho), N.ctypes.byref(wo)),
+                "se_conv2d_out_shape")
+        y0 = torch.empty((x0.shape[0], out_channels, ho.value, wo.value), device=x0.device, dtype=x0.dtype)
+        ws = _workspace(lib.se_conv2d_workspace_size(N.ctypes.byref(d)), x0.device)
+        t0 = _TIMER.begin() if _TIMER else None
+        N.check(lib.se_conv2d_fwd(_with_math(d, "fwd"), x0.data_ptr(), wr.data_ptr(), wi.data_ptr(), None, None,
+                                  y0.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(x0)), "se_conv2d_fwd")
+        if t0 is not None:
+            _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d), 4.0 * (x0.numel() + y0.numel() + 2 * wr.numel()))
+        b, c = y0.shape[:2]
+        hw = y0[0, 0].numel()
+        y = torch.empty_like(y0)
+        save = torch.empty(N.CBN_SAVE_FLOATS * (c // 2), device=x0.device, dtype=torch.float32)
+        params = (wrr, wri, wii, br, bi)
+        ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x0.device)
+        ya = new_amax(x0.device)
+        mom = -1.0 if momentum is None else float(momentum)
+        t0 = _TIMER.begin() if _TIMER else None
+        N.check(lib.se_cbn_fwd(y0.data_ptr(), y.data_ptr(), b, c, hw, N.ptr_array(params), N.ptr_array(running),
+                               N.ptr(nbt), save.data_ptr(), 1, float(eps), mom, int(act), float(slope), ya.data_ptr(),
+                               None, 0, ws.data_ptr(), ws.numel(), N.stream_of(x0)), "se_cbn_fwd")
+        if t0 is not None:
+            _TIMER.end("cbn_fwd", t0, 0.0, 4.0 * y0.numel() * 3)
+        amax_put(y, ya)
+        ctx.save_for_backward(x0, y0, save, wr, *params)
+        ctx.cfg = (int(act), float(slope), d)
+        if fork:
+            ctx.set_materialize_grads(False)
+            return y, y.view(y.shape)
+        return y
+
+    @staticmethod
+    def backward(ctx, gy, gy2=None):
+        x0, y0, save, wr, *params = ctx.saved_tensors
+        act, slope, d = ctx.cfg
+        if gy is None:
+            gy, gy2 = gy2, None
+        if gy is None:
+            return (None,) * 16
+        gy = gy.contiguous()
+        gy2 = gy2.contiguous() if gy2 is not None else None
+        b, c, h, w = y0.shape
+        lib = N.lib()
+        dwr, dwi = torch.empty_like(wr), torch.empty_like(wr)
+        dparams = [torch.empty_like(p) for p in params]
+        fc = N.FirstConvDesc()
+        fc.x0, fc.cin, fc.in_h, fc.in_w = x0.data_ptr(), x0.shape[1] // 2, x0.shape[2], x0.shape[3]
+        fc.kernel_h, fc.kernel_w, fc.stride_h, fc.stride_w = d.kernel_h, d.kernel_w, d.stride_h, d.stride_w
+        fc.pad_h, fc.pad_w, fc.dil_h, fc.dil_w = d.pad_h, d.pad_w, d.dil_h, d.dil_w
+        fc.dwr, fc.dwi = dwr.data_ptr(), dwi.data_ptr()
+        ws = _workspace(lib.se_cbn_first_conv_workspace_size(b, c, h * w, fc.cin, fc.kernel_h, fc.kernel_w),
+                        gy.device)
+        t0 = _TIMER.begin() if _TIMER else None
+        N.check(lib.se_cbn_bwd_first_conv(gy.data_ptr(), N.ptr(gy2), y0.data_ptr(), b, c, h, w,
+                                          N.ptr_array(params), save.data_ptr(), N.ptr_array(dparams), 1, act, slope,
+                                          N.ctypes.byref(fc), ws.data_ptr(), ws.numel(), N.stream_of(gy)),
+                "se_cbn_bwd_first_conv")
+        if t0 is not None:   # (gy [, gy2], y0) read twice, x0 taps from L2; no dx written
+            _TIMER.end("cbn_bwd_first_conv", t0, _conv_flops(d), 4.0 * y0.numel() * (4 if gy2 is None else 6))
+        return (None, dwr, dwi, *dparams, None, None, None, None, None, None, None, None)
+
+
+def first_block_supported(x0, conv_w, bias, norm_training, kernel) -> bool:
+    """The shapes se_cbn_bwd_first_conv covers: a training-mode first block on fp32
+    CUDA tensors whose input carries no gradient, complex conv with one complex input
+    channel, kernel (5, 2), no conv bias (SEHIP_FIRST_FUSED=0 turns it off)."""
+    return (os.environ.get("SEHIP_FIRST_FUSED", "1") != "0" and norm_training and torch.is_grad_enabled()
+            and x0.is_cuda and x0.dtype == torch.float32 and conv_w.dtype == torch.float32
+            and not x0.requires_grad and bias is None and x0.shape[1] == 2 and tuple(kernel) == (5, 2))
+
+
+def first_block(x0, wr, wi, wrr, wri, wii, br, bi, running, nbt, eps, momentum, act, slope, *, kernel, stride,
+                padding, padding_end, dilation, fork=False):
+    """act(CBN(conv(x0))) for a model's first block in training (see _FirstBlock)."""
+    cgeom = (_pair(kernel), _pair(stride), _pair(padding), None if padding_end is None else _pair(padding_end),
+             _pair(dilation))
+    return _FirstBlock.apply(x0, wr, wi, wrr, wri, wii, br, bi, running, nbt, eps, momentum, act, slope, cgeom,
+                             fork)
 
 
 class _ComplexBNHead(torch.autograd.Function):
@@ -802,7 +958,9 @@ def complex_batch_norm_head(x, wrr, wri, wii, br, bi, w_head, running, nbt, trai
 class _Stft(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, window, twiddle, win, hop, nfft, center, mag_phase):
-        N.require_device(x, window, twiddle)
+        N.require_device(window, twiddle)
+        N.require_device(x, dtype=x.dtype)
+        dt = N.dtype_code(x)
         x = x.contiguous()
         b, length = x.shape
         lib = N.lib()
@@ -818,10 +976,11 @@ class _Stft(torch.autograd.Function):
             out1 = None
         t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_stft_fwd(x.data_ptr(), out0.data_ptr(), N.ptr(out1), b, length, win, hop, nfft,
-                                int(center), int(mag_phase), window.data_ptr(), twiddle.data_ptr(),
+                                int(center), int(mag_phase), window.data_ptr(), twiddle.data_ptr(), dt,
                                 N.stream_of(x)), "se_stft_fwd")
         if t0 is not None:   # algorithmic bytes: read the wav once, write the spectrum once
-            _TIMER.end("stft_fwd", t0, 0.0, 4.0 * (x.numel() + out0.numel() + (out1.numel() if mag_phase else 0)))
+            _TIMER.end("stft_fwd", t0, 0.0, x.element_size() * (x.numel() + out0.numel()
+                                                                 + (out1.numel() if mag_phase else 0)))
         return (out0, out1) if mag_phase else out0
 
     @staticmethod
@@ -838,7 +997,9 @@ def stft(x, window, twiddle, win, hop, nfft, center=True, mag_phase=False):
 class _Istft(torch.autograd.Function):
     @staticmethod
     def forward(ctx, spec, window, twiddle, win, hop, nfft, offset, out_len):
-        N.require_device(spec, window, twiddle)
+        N.require_device(window, twiddle)
+        N.require_device(spec, dtype=spec.dtype)
+        dt = N.dtype_code(spec)
         spec = spec.contiguous()
         b, rows, t = spec.shape
         if rows != nfft + 2:
@@ -846,10 +1007,10 @@ class _Istft(torch.autograd.Function):
         out = torch.empty((b, out_len), device=spec.device, dtype=spec.dtype)
         t0 = _TIMER.begin() if _TIMER else None
         N.check(N.lib().se_istft_fwd(spec.data_ptr(), out.data_ptr(), b, t, win, hop, nfft, offset,
-                                     out_len, window.data_ptr(), twiddle.data_ptr(),
+                                     out_len, window.data_ptr(), twiddle.data_ptr(), dt,
                                      N.stream_of(spec)), "se_istft_fwd")
         if t0 is not None:
-            _TIMER.end("istft_fwd", t0, 0.0, 4.0 * (spec.numel() + out.numel()))
+            _TIMER.end("istft_fwd", t0, 0.0, spec.element_size() * (spec.numel() + out.numel()))
         ctx.save_for_backward(window, twiddle)
         ctx.cfg = (b, t, win, hop, nfft, offset, out_len)
         return out
@@ -862,16 +1023,50 @@ class _Istft(torch.autograd.Function):
         gspec = torch.empty((b, nfft + 2, t), device=gout.device, dtype=gout.dtype)
         t0 = _TIMER.begin() if _TIMER else None
         N.check(N.lib().se_istft_bwd(gout.data_ptr(), gspec.data_ptr(), b, t, win, hop, nfft,
-                                     offset, out_len, window.data_ptr(), twiddle.data_ptr(),
+                                     offset, out_len, window.data_ptr(), twiddle.data_ptr(), N.dtype_code(gout),
                                      N.stream_of(gout)), "se_istft_bwd")
         if t0 is not None:
-            _TIMER.end("istft_bwd", t0, 0.0, 4.0 * (gout.numel() + gspec.numel()))
+            _TIMER.end("istft_bwd", t0, 0.0, gout.element_size() * (gout.numel() + gspec.numel()))
         return gspec, None, None, None, None, None, None, None
 
 
 def istft(spec, window, twiddle, win, hop, nfft, offset, out_len):
     """spec [B, nfft+2, T] -> wav [B, out_len] = full OLA signal[offset:offset+out_len]."""
     return _Istft.apply(spec, window, twiddle, win, hop, nfft, offset, out_len)
+
+
+class _Mask(torch.autograd.Function):
+    """FRCRN's mask (frcrn.py:140-152) as one pass each way (se_mask_fwd / _bwd):
+    est = pad(tanh(pad(h, top 1)) * spec[:, :, 1:], top 1) re-stacked [B, 2 half, T]."""
+
+    @staticmethod
+    def forward(ctx, h, spec, half):
+        N.require_device(h, spec)
+        h, spec = h.contiguous(), spec.contiguous()
+        B, T = spec.shape[0], spec.shape[-1]
+        if tuple(h.shape) != (B, 2, half - 2, T) or tuple(spec.shape) != (B, 2 * half, T):
+            raise ValueError(f"sehip mask: h {tuple(h.shape)} / spec {tuple(spec.shape)} do not match half={half}")
+        est = torch.empty_like(spec)
+        N.check(N.lib().se_mask_fwd(h.data_ptr(), spec.data_ptr(), B, half, T, est.data_ptr(), N.stream_of(h)),
+                "se_mask_fwd")
+        ctx.save_for_backward(h, spec)
+        ctx.half = half
+        return est
+
+    @staticmethod
+    def backward(ctx, gest):
+        h, spec = ctx.saved_tensors
+        gest = gest.contiguous()
+        gh = torch.empty_like(h)
+        N.check(N.lib().se_mask_bwd(gest.data_ptr(), h.data_ptr(), spec.data_ptr(), spec.shape[0], ctx.half,
+                                    spec.shape[-1], gh.data_ptr(), N.stream_of(gest)), "se_mask_bwd")
+        return gh, None, None
+
+
+def complex_mask(h, spec, half):
+    """FRCRN's est spectrum from the final_conv output h [B, 2, half-2, T] and the
+    ConvSTFT output spec [B, 2 half, T] (no gradient into spec)."""
+    return _Mask.apply(h, spec.detach(), half)
 
 
 # --------------------------------------------------------------------------

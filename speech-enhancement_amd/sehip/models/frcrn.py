@@ -55,6 +55,9 @@ class _CausalConvBase(nn.Module):
         lp = self.padding[1]
         pad = (lp, 0 if self.causal else lp, 0, 0)
         conv = self._conv()
+        fused = self._first_block(x, conv, pad if lp else None, fork)
+        if fused is not None:
+            return fused
         plain = isinstance(conv, (nn.Conv2d, nn.ConvTranspose2d))
         transposed = isinstance(conv, (nn.ConvTranspose2d, ComplexConvTranspose2d))
         if lp and transposed:                      # zero input columns of a convT: materialise
@@ -64,6 +67,28 @@ class _CausalConvBase(nn.Module):
         # the time pad of a plain conv is folded into its (asymmetric) padding
         y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
         return norm_act(self.norm, self.act, y, fork)
+
+    def _first_block(self, x, conv, input_pad, fork):
+        """The model's first block in training (its conv flagged data-fed): conv + CBN +
+        act as functional.first_block, whose backward computes the conv's weight
+        gradient inside the CBN backward (no dy tensor, no weight-grad GEMM). None where
+        that path does not apply."""
+        n = self.norm
+        if not (isinstance(conv, ComplexConv2d) and conv.exact_fp32 and isinstance(n, ComplexBatchNorm2d)
+                and n.affine and n.track_running_stats and n.training):
+            return None
+        act = {nn.LeakyReLU: F.ACT_LEAKY, nn.ReLU: F.ACT_RELU, nn.Identity: F.ACT_NONE}.get(type(self.act))
+        c = conv.real_conv
+        if act is None or c.groups != 1 or c.padding_mode != "zeros" or isinstance(c.padding, str) or \
+                not F.first_block_supported(x, c.weight, c.bias, True, c.kernel_size):
+            return None
+        from ..complex_nn import _fold_pad
+        begin, end = _fold_pad(c.padding, input_pad, False)
+        slope = self.act.negative_slope if act == F.ACT_LEAKY else 0.0
+        return F.first_block(x, c.weight, conv.imag_conv.weight, n.Wrr, n.Wri, n.Wii, n.Br, n.Bi,
+                             (n.RMr, n.RMi, n.RVrr, n.RVri, n.RVii), n.num_batches_tracked, n.eps, n.momentum, act,
+                             slope, kernel=c.kernel_size, stride=c.stride, padding=begin, padding_end=end,
+                             dilation=c.dilation, fork=fork)
 
     def forward_joined(self, x, skip):
         """self(complex_join(x, skip)) (frcrn.py:95-101) without writing the
@@ -277,8 +302,11 @@ class FRCRN(nn.Module):
         h = h.transpose(1, 2).reshape(b, c, f, t)
         # decoder + final_conv; the conv is fused into the last block's CBN (se_cbn_head_*)
         h = self.decoder(h, skips, attended, head=self.final_conv)
-        mask = torch.tanh(TF.pad(h, (0, 0, 1, 0)))                    # :140-144
-        est = TF.pad(mask * noisy, (0, 0, 1, 0))                       # :145-146 (DC back as 0)
-        est = est.reshape(b, 2 * half, est.shape[-1])                  # cat(re, im) on dim 1 (:149-152)
+        if h.is_cuda and h.dtype == torch.float32 and tuple(h.shape[1:]) == (2, half - 2, spec.shape[-1]):
+            est = F.complex_mask(h, spec, half)                        # :140-152 in one pass each way
+        else:
+            mask = torch.tanh(TF.pad(h, (0, 0, 1, 0)))                 # :140-144
+            est = TF.pad(mask * noisy, (0, 0, 1, 0))                   # :145-146 (DC back as 0)
+            est = est.reshape(b, 2 * half, est.shape[-1])              # cat(re, im) on dim 1 (:149-152)
         wav = self.istft(est)
         return est, torch.clamp_(wav, -1, 1)                           # :153-155

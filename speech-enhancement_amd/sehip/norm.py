@@ -30,18 +30,21 @@ def _plane_stride(x):
 class _BnAct(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, act_param, rmean, rvar, training, momentum, eps, act, per_channel, alpha):
-        N.require_device(x, weight, bias, act_param, rmean, rvar)
+        # fp32, or bf16 / fp16 storage throughout (model.half() / .to(bfloat16)): read and
+        # written in that dtype by the kernels, fp32 arithmetic
+        N.require_device(x, weight, bias, act_param, rmean, rvar, dtype=x.dtype)
+        dt = N.dtype_code(x)
         ps = _plane_stride(x)
         if ps is None:
             x = x.contiguous()
             ps = x.stride(1)
         B, C, H, W = x.shape
-        y = torch.empty((B, C, H, W), device=x.device, dtype=torch.float32)
+        y = torch.empty((B, C, H, W), device=x.device, dtype=x.dtype)
         save = torch.empty(2 * C, device=x.device, dtype=torch.float32)
         ws = torch.empty(int(N.lib().se_bn_workspace_size(B, C)), device=x.device, dtype=torch.uint8)
         N.check(N.lib().se_bn_fwd(x.data_ptr(), ps, B, C, H * W, N.ptr(weight), N.ptr(bias), N.ptr(rmean),
                                   N.ptr(rvar), int(training), float(momentum), float(eps), act, N.ptr(act_param),
-                                  int(per_channel), float(alpha), y.data_ptr(), save.data_ptr(), ws.data_ptr(),
+                                  int(per_channel), float(alpha), y.data_ptr(), save.data_ptr(), dt, ws.data_ptr(),
                                   ws.numel(), N.stream_of(x)), "se_bn_fwd")
         ctx.save_for_backward(x, weight, bias, act_param, save)
         ctx.cfg = (ps, int(training), act, int(per_channel), float(alpha))
@@ -52,21 +55,17 @@ class _BnAct(torch.autograd.Function):
         x, weight, bias, act_param, save = ctx.saved_tensors
         ps, training, act, per_channel, alpha = ctx.cfg
         B, C, H, W = x.shape
-        gy = gy.contiguous().float()
-        dx = torch.empty((B, C, H, W), device=x.device, dtype=torch.float32)
-        dw = torch.empty(C, device=x.device, dtype=torch.float32) if weight is not None else None
-        db = torch.empty(C, device=x.device, dtype=torch.float32) if bias is not None else None
+        gy = gy.contiguous().to(x.dtype)
+        dx = torch.empty((B, C, H, W), device=x.device, dtype=x.dtype)
+        dw = torch.empty(C, device=x.device, dtype=x.dtype) if weight is not None else None
+        db = torch.empty(C, device=x.device, dtype=x.dtype) if bias is not None else None
         da = torch.empty_like(act_param) if act_param is not None else None
         ws = torch.empty(int(N.lib().se_bn_workspace_size(B, C)), device=x.device, dtype=torch.uint8)
         N.check(N.lib().se_bn_bwd(gy.data_ptr(), x.data_ptr(), ps, B, C, H * W, N.ptr(weight), N.ptr(bias),
                                   save.data_ptr(), training, act, N.ptr(act_param), per_channel, alpha,
-                                  dx.data_ptr(), N.ptr(dw), N.ptr(db), N.ptr(da), ws.data_ptr(), ws.numel(),
-                                  N.stream_of(gy)), "se_bn_bwd")
+                                  dx.data_ptr(), N.ptr(dw), N.ptr(db), N.ptr(da), N.dtype_code(x), ws.data_ptr(),
+                                  ws.numel(), N.stream_of(gy)), "se_bn_bwd")
         return dx, dw, db, da, None, None, None, None, None, None, None, None
-
-
-def _f32(t):
-    return t if t is None or t.dtype == torch.float32 else t.float()
 
 
 def bn_act(norm: nn.Module, act: nn.Module, x: torch.Tensor) -> torch.Tensor:
@@ -90,13 +89,10 @@ def bn_act(norm: nn.Module, act: nn.Module, x: torch.Tensor) -> torch.Tensor:
     track = norm.training and norm.track_running_stats
     rmean = norm.running_mean if (track or not use_batch) else None
     rvar = norm.running_var if (track or not use_batch) else None
-    if rmean is not None and rmean.dtype != torch.float32:
-        if track:
-            return act(norm(x))     # half-precision running stats updated in place: the modules' own kernels
-        rmean, rvar = rmean.float(), rvar.float()   # eval (model.half() inference): fp32 copies
+    if x.dtype not in N.DTYPES or any(t is not None and t.dtype != x.dtype
+                                      for t in (norm.weight, norm.bias, param, rmean, rvar)):
+        return act(norm(x))     # mixed dtypes: the modules themselves
     if track:
         norm.num_batches_tracked.add_(1)
-    dt = x.dtype
-    y = _BnAct.apply(_f32(x), _f32(norm.weight), _f32(norm.bias), _f32(param), rmean, rvar, use_batch,
-                     norm.momentum or 0.0, norm.eps, code, param is not None and param.numel() > 1, alpha)
-    return y if dt == torch.float32 else y.to(dt)
+    return _BnAct.apply(x, norm.weight, norm.bias, param, rmean, rvar, use_batch, norm.momentum or 0.0, norm.eps,
+                        code, param is not None and param.numel() > 1, alpha)

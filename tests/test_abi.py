@@ -17,7 +17,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), f"libsehip.so does not export {s}"
     assert N.MISSING == []
-    assert lib.se_abi_version() == 3
+    assert lib.se_abi_version() == 4
 
 
 def test_strerror():
@@ -81,10 +81,10 @@ def test_stft_num_frames_matches_conv1d(L, win, hop, nfft, center):
 def test_stft_validation_needs_no_gpu():
     lib = N.lib()
     # nfft with a factor 7 is not supported by the radix-2/3/4/5 FFT
-    assert lib.se_stft_fwd(None, None, None, 1, 4000, 320, 160, 7 * 64, 1, 0, None, None, None) == -3
-    assert lib.se_stft_fwd(None, None, None, 1, 4000, 320, 160, 642, 1, 0, None, None, None) == -3
-    assert lib.se_stft_fwd(None, None, None, 1, 4000, 700, 160, 640, 1, 0, None, None, None) == -1
-    assert lib.se_istft_fwd(None, None, 1, 10, 320, 160, 640, 0, 10 ** 6, None, None, None) == -2
+    assert lib.se_stft_fwd(None, None, None, 1, 4000, 320, 160, 7 * 64, 1, 0, None, None, 0, None) == -3
+    assert lib.se_stft_fwd(None, None, None, 1, 4000, 320, 160, 642, 1, 0, None, None, 0, None) == -3
+    assert lib.se_stft_fwd(None, None, None, 1, 4000, 700, 160, 640, 1, 0, None, None, 0, None) == -1
+    assert lib.se_istft_fwd(None, None, 1, 10, 320, 160, 640, 0, 10 ** 6, None, None, 0, None) == -2
 
 
 def test_cbn_workspace():

@@ -215,3 +215,153 @@ def test_frcrn_head_fused_matches_unfused(gpu_device, monkeypatch):
     for n in b0:
         if b0[n].is_floating_point():
             np.testing.assert_allclose(b1[n].cpu().numpy(), b0[n].cpu().numpy(), rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("fork", [False, True])
+@pytest.mark.parametrize("shape", [(3, 2, 40, 37), (2, 2, 320, 101)])
+def test_first_block_fused_vs_fp64(shape, fork, gpu_device):
+    """se_cbn_bwd_first_conv: FRCRN's first block (causal pad (1, 0) + ComplexConv2d(2, 128,
+    (5, 2), stride (2, 1), no bias) + ComplexBatchNorm2d + LeakyReLU, frcrn.py:11-34) with
+    the conv's weight gradient accumulated inside the CBN backward apply (no dy tensor),
+    against the fp64 oracle modules on the CPU: the output, the conv's dWr / dWi, the 5
+    CBN parameter gradients and the running statistics; fork=True sums two consumers'
+    gradients (the encoder output feeds the next block and the decoder skip)."""
+    from sehip import functional as F
+    from sehip.complex_nn import ComplexBatchNorm2d, ComplexConv2d
+    from oracle.complex_nn import ComplexBatchNorm2d as OCBN, ComplexConv2d as OConv
+    tf = torch.nn.functional
+    gen = torch.Generator().manual_seed(31)
+    x = torch.randn(shape, generator=gen) * 0.8
+    co = paramfill.fill_(OConv(2, 128, (5, 2), stride=(2, 1), bias=False), seed=5).double()
+    no = paramfill.fill_(OCBN(128), seed=6).double().train()
+    yo = tf.leaky_relu(no(co(tf.pad(x.double(), (1, 0, 0, 0)))), 0.2)
+    g1 = torch.randn(yo.shape, generator=gen, dtype=torch.float64)
+    g2 = torch.randn(yo.shape, generator=gen, dtype=torch.float64)
+    (yo * g1 + (yo * g2 if fork else 0)).sum().backward()
+
+    c = ComplexConv2d(2, 128, (5, 2), stride=(2, 1), bias=False).cuda()
+    c.load_state_dict({k: v.float() for k, v in co.state_dict().items()})
+    n = ComplexBatchNorm2d(128).cuda()
+    n.load_state_dict({k: v.float() for k, v in no.state_dict().items()})
+    xg = x.cuda()
+    assert F.first_block_supported(xg, c.real_conv.weight, None, True, (5, 2))
+    out = F.first_block(xg, c.real_conv.weight, c.imag_conv.weight, n.Wrr, n.Wri, n.Wii, n.Br, n.Bi,
+                        (n.RMr, n.RMi, n.RVrr, n.RVri, n.RVii), n.num_batches_tracked, n.eps, n.momentum,
+                        F.ACT_LEAKY, 0.2, kernel=(5, 2), stride=(2, 1), padding=(0, 1), padding_end=(0, 0),
+                        dilation=(1, 1), fork=fork)
+    if fork:
+        y, y2 = out
+        (y * g1.float().cuda() + y2 * g2.float().cuda()).sum().backward()
+    else:
+        y = out
+        (y * g1.float().cuda()).sum().backward()
+    assert rel_l2(y.detach().cpu().numpy(), yo.detach().numpy()) < 1e-5
+    for name, a, b in (("dWr", c.real_conv.weight, co.real_conv.weight), ("dWi", c.imag_conv.weight, co.imag_conv.weight)):
+        e = rel_l2(a.grad.cpu().numpy(), b.grad.numpy())
+        print(f"{shape} fork={fork} {name}: {e:.2e}")
+        assert e < 1e-5, (name, e)
+    for k in ("Wrr", "Wri", "Wii", "Br", "Bi"):
+        assert rel_l2(getattr(n, k).grad.cpu().numpy(), getattr(no, k).grad.numpy()) < 1e-5, k
+    for k in ("RMr", "RMi", "RVrr", "RVri", "RVii"):
+        np.testing.assert_allclose(getattr(n, k).cpu().numpy(), getattr(no, k).detach().numpy(), rtol=1e-5, atol=1e-6)
+
+
+def test_frcrn_first_block_fused_matches_unfused(gpu_device, monkeypatch):
+    """FRCRN train-mode forward + backward with the fused first block (default) vs
+    SEHIP_FIRST_FUSED=0 (conv weight-grad GEMM on a written dy): same output, gradients
+    to fp32 rounding for the first conv's weights (summed in another order, exact fp32
+    products either way), bit-identical for every other parameter."""
+    from sehip import models as M
+    from sehip.losses import SI_SNR_loss
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=13)
+    x, cl = torch.from_numpy(noisy).cuda(), torch.from_numpy(clean).cuda()
+    res = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SEHIP_FIRST_FUSED", flag)
+        m = paramfill.fill_(M.FRCRN(), seed=14).cuda().train()
+        _, wav = m(x)
+        SI_SNR_loss(wav, cl).backward()
+        torch.cuda.synchronize()
+        res.append((wav.detach(), {k: p.grad.detach() for k, p in m.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for k in res[0][1]:   # only the first conv's weight gradient is computed differently
+        assert k.startswith("encoder.layers.0.conv") or torch.equal(res[0][1][k], res[1][1][k]), k
+    e0 = [((res[0][1][k] - res[1][1][k]).norm() / res[1][1][k].norm()).item()
+          for k in res[0][1] if k.startswith("encoder.layers.0.conv")]
+    print("encoder.layers.0.conv weight grads fused vs unfused:", e0)
+    assert max(e0) < 1e-5
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 1.5e-2), (torch.float16, 2e-3)])
+@pytest.mark.parametrize("train", [True, False])
+def test_cbn_low_precision_storage(dtype, tol, train, gpu_device):
+    """model.to(bfloat16) / .half() (BASELINE configs 2 / 3 / 5): the CBN kernels read
+    and write bf16 / fp16 activations, parameters and running statistics directly
+    (fp32 arithmetic, fp64 moments, no cast passes). Against the fp64 oracle on the
+    same rounded inputs: output, dx, parameter gradients within the storage's rounding;
+    every result in the storage dtype."""
+    from sehip.complex_nn import ComplexBatchNorm2d
+    from oracle.complex_nn import ComplexBatchNorm2d as OCBN
+    tf = torch.nn.functional
+    gen = torch.Generator().manual_seed(41)
+    b, c, h, w = 4, 16, 9, 44
+    x = (torch.randn(b, c, h, w, generator=gen) * 1.3 + 0.2).to(dtype)
+    gy = torch.randn(b, c, h, w, generator=gen).to(dtype)
+    mo = paramfill.fill_(OCBN(c), seed=9).to(dtype).double().train(train)
+    if not train:
+        with torch.no_grad():
+            mo.RVrr.fill_(1.5); mo.RVii.fill_(0.7); mo.RMr.fill_(0.1)
+    m = ComplexBatchNorm2d(c).cuda()
+    m.load_state_dict({k: v.to(dtype) if v.is_floating_point() else v for k, v in mo.state_dict().items()})
+    m = m.to(dtype).train(train)
+    xo = x.double().requires_grad_(True)
+    yo = tf.leaky_relu(mo(xo), 0.2)
+    yo.backward(gy.double())
+    xg = x.cuda().requires_grad_(True)
+    from sehip import functional as F
+    y = m.forward_act(xg, F.ACT_LEAKY, 0.2)
+    y.backward(gy.cuda())
+    assert y.dtype == dtype and xg.grad.dtype == dtype and m.Wrr.grad.dtype == dtype
+    assert rel_l2(y.detach().float().cpu().numpy(), yo.detach().numpy()) < tol
+    assert rel_l2(xg.grad.float().cpu().numpy(), xo.grad.numpy()) < tol
+    for k in ("Wrr", "Wri", "Wii", "Br", "Bi"):
+        assert rel_l2(getattr(m, k).grad.float().cpu().numpy(), getattr(mo, k).grad.numpy()) < tol, k
+    if train:
+        for k in ("RMr", "RVrr", "RVri"):
+            assert getattr(m, k).dtype == dtype
+            np.testing.assert_allclose(getattr(m, k).float().cpu().numpy(), getattr(mo, k).detach().numpy(),
+                                       rtol=2 * tol, atol=2 * tol)
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 1e-5), (torch.bfloat16, 1.5e-2)])
+def test_cbn_prelu_fused(dtype, tol, gpu_device):
+    """DCCRN's block ends in CBN -> nn.PReLU() (one weight, dccrn.py:21,45): the PReLU runs
+    inside the CBN kernels with its slope read on the device, and its weight gradient is a
+    7th sum of the backward moments pass. Against fp64 CBN + PReLU on the CPU."""
+    from sehip.complex_nn import ComplexBatchNorm2d, norm_act
+    from oracle.complex_nn import ComplexBatchNorm2d as OCBN
+    gen = torch.Generator().manual_seed(43)
+    b, c, h, w = 3, 32, 17, 40
+    x = (torch.randn(b, c, h, w, generator=gen) * 0.9).to(dtype)
+    gy = torch.randn(b, c, h, w, generator=gen).to(dtype)
+    mo = paramfill.fill_(OCBN(c), seed=10).to(dtype).double().train()
+    po = torch.nn.PReLU().double()
+    with torch.no_grad():
+        po.weight.fill_(0.3)
+    xo = x.double().requires_grad_(True)
+    yo = po(mo(xo))
+    yo.backward(gy.double())
+    m = ComplexBatchNorm2d(c)
+    m.load_state_dict({k: v.to(dtype) if v.is_floating_point() else v for k, v in mo.state_dict().items()})
+    m = m.cuda().to(dtype).train()
+    p = torch.nn.PReLU().cuda().to(dtype)
+    with torch.no_grad():
+        p.weight.fill_(0.3)
+    xg = x.cuda().requires_grad_(True)
+    y = norm_act(m, p, xg)
+    y.backward(gy.cuda())
+    assert rel_l2(y.detach().float().cpu().numpy(), yo.detach().numpy()) < tol
+    assert rel_l2(xg.grad.float().cpu().numpy(), xo.grad.numpy()) < tol
+    assert rel_l2(p.weight.grad.float().cpu().numpy(), po.weight.grad.numpy()) < tol
+    for k in ("Wrr", "Wri", "Br"):
+        assert rel_l2(getattr(m, k).grad.float().cpu().numpy(), getattr(mo, k).grad.numpy()) < tol, k

@@ -189,3 +189,56 @@ def test_merged_phase_forward_vs_fp64(name, tr, cin, cout, shape, stride, gpu_de
     assert same
     for k in ("dx", "dwr", "dwi"):   # the backward passes do not depend on the knob
         assert torch.equal(merged[k], plain[k]), k
+
+
+CONV16_CASES = LAYERS[:4] + [
+    ("n32", False, 32, 64, (2, 32, 65, 37), (2, 1)),     # DCCRN enc1-like: 32 -> 64 channels (128-col tiles)
+    ("t64", True, 128, 64, (2, 128, 17, 30), (2, 1)),    # convT 128 -> 64 (DCCRN decoder-like)
+    ("n16", False, 64, 16, (2, 64, 33, 21), (1, 1)),     # N = 16: the small-N gather, 16-wide weight-grad tile
+]
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 6e-3), (torch.float16, 1e-3)])
+@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", CONV16_CASES)
+def test_conv_16bit_storage(name, tr, cin, cout, shape, stride, dtype, tol, gpu_device, monkeypatch):
+    """bf16 / fp16 storage (model.to(bfloat16) / .half(); BASELINE configs 2 / 3 / 5): every
+    pass reads and writes the 16-bit tensors directly (se_conv2d_desc.dtype) with the
+    one-term MFMA of that format, whose products of the 16-bit operands are exact. So each
+    result equals, bit for bit, the same one-term arithmetic on fp32 copies rounded once
+    at the end (SEHIP_NATIVE16=0), and is within the 16-bit output rounding of fp64."""
+    from sehip import functional as F
+    cls = O_cnn.ComplexConvTranspose2d if tr else O_cnn.ComplexConv2d
+    m = paramfill.fill_(cls(cin, cout, (5, 2), stride=stride, bias=False), seed=7)
+    gen = torch.Generator().manual_seed(13)
+    x = torch.randn(*shape, generator=gen).to(dtype)
+    wr16, wi16 = m.real_conv.weight.detach().to(dtype), m.imag_conv.weight.detach().to(dtype)
+    md = m.double()
+    with torch.no_grad():
+        md.real_conv.weight.copy_(wr16.double()); md.imag_conv.weight.copy_(wi16.double())
+    xo = x.double().requires_grad_(True)
+    yo = md(xo)
+    gy = torch.randn(yo.shape, generator=gen).to(dtype)
+    yo.backward(gy.double())
+    ref = dict(y=yo.detach(), dx=xo.grad, dwr=md.real_conv.weight.grad, dwi=md.imag_conv.weight.grad)
+
+    def run(native):
+        monkeypatch.setenv("SEHIP_NATIVE16", "1" if native else "0")
+        wr = wr16.cuda().requires_grad_(True)
+        wi = wi16.cuda().requires_grad_(True)
+        xg = x.cuda().requires_grad_(True)
+        before = F.NATIVE16_CALLS[0]
+        y = F.conv2d(xg, wr, wi, out_channels=2 * m.real_conv.out_channels, kernel=(5, 2), stride=stride,
+                     transposed=tr)
+        assert (F.NATIVE16_CALLS[0] - before) == (1 if native else 0)
+        y.backward(gy.cuda())
+        torch.cuda.synchronize()
+        assert y.dtype == dtype and xg.grad.dtype == dtype and wr.grad.dtype == dtype
+        return dict(y=y.detach().cpu(), dx=xg.grad.cpu(), dwr=wr.grad.cpu(), dwi=wi.grad.cpu())
+
+    nat, cast = run(True), run(False)
+    for k, r in ref.items():
+        e = rel_l2(nat[k].float().numpy(), r.numpy())
+        print(f"{name} {dtype} {k}: native vs fp64 {e:.2e}, bit-identical to the cast path: "
+              f"{torch.equal(nat[k], cast[k])}")
+        assert torch.equal(nat[k], cast[k]), (name, k)
+        assert e < tol, (name, k, e)

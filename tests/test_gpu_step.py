@@ -209,3 +209,27 @@ def test_adamw_parameters_at_different_steps_match_torch(gpu_device):
             d = (pa - pb).abs().max().item()
             assert d <= 1e-6 * max(pa.abs().max().item(), 1.0), (step, d)
     assert int(ob.state[b[1]]["step"]) == 3 and int(ob.state[b[0]]["step"]) == 5
+
+
+def test_frcrn_mask_fused_vs_torch(gpu_device):
+    """se_mask_fwd / _bwd (FRCRN's tanh mask x noisy, frcrn.py:140-152) against the
+    reference's pad / tanh / mul / pad / reshape in torch on the same device: est equal
+    to fp32 rounding (the same ops, tanhf vs torch's tanh), the gradient into h likewise,
+    rows 0 and 1 of est exactly 0."""
+    from sehip import functional as F
+    tf = torch.nn.functional
+    g = torch.Generator().manual_seed(5)
+    B, half, T = 3, 321, 77
+    h = torch.randn(B, 2, half - 2, T, generator=g).cuda().requires_grad_(True)
+    spec = torch.randn(B, 2 * half, T, generator=g).cuda()
+    est = F.complex_mask(h, spec, half)
+    noisy = spec.view(B, 2, half, T)[:, :, 1:]
+    h2 = h.detach().clone().requires_grad_(True)
+    ref = tf.pad(torch.tanh(tf.pad(h2, (0, 0, 1, 0))) * noisy, (0, 0, 1, 0)).reshape(B, 2 * half, T)
+    assert (est - ref).abs().max().item() <= 1e-6 * ref.abs().max().item()
+    v = est.view(B, 2, half, T)
+    assert torch.all(v[:, :, :2] == 0)
+    gest = torch.randn(B, 2 * half, T, generator=g).cuda()
+    est.backward(gest)
+    ref.backward(gest)
+    assert ((h.grad - h2.grad).norm() / h2.grad.norm()).item() < 1e-6

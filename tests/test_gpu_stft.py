@@ -82,3 +82,31 @@ def test_stft_istft_vs_oracle_more_plans(win, hop, nfft, gpu_device):
     s = torch.randn_like(ref)
     assert rel_l2(ConviSTFT(win, hop, nfft).cuda()(s.cuda()).cpu().numpy(),
                   O.ConviSTFT(win, hop, nfft)(s).numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.bfloat16, 1e-2), (torch.float16, 1.5e-3)])
+@pytest.mark.parametrize("cfg", [(320, 160, 640), (400, 100, 512), (512, 128, 512)])
+def test_stft_istft_low_precision_storage(cfg, dtype, tol, gpu_device):
+    """bf16 / fp16 signals and spectra (model.to(bfloat16) / .half(), BASELINE configs 2, 3,
+    5): the kernels read and write the storage type directly (fp32 arithmetic, fp32
+    window / twiddle tables). Against the fp32 goldens on the rounded input, within the
+    storage's rounding; the outputs are in the storage dtype."""
+    from sehip.conv_stft import ConvSTFT, ConviSTFT
+    g = golden("stft")
+    win, hop, nfft = cfg
+    tag = f"{win}_{hop}_{nfft}"
+    st = ConvSTFT(win, hop, nfft).cuda().to(dtype)
+    ist = ConviSTFT(win, hop, nfft).cuda().to(dtype)
+    x = torch.from_numpy(g[f"x_{tag}"]).cuda().to(dtype)
+    spec = st(x)
+    assert spec.dtype == dtype
+    ref = ConvSTFT(win, hop, nfft).cuda()(x.float())
+    assert rel_l2(spec.float().cpu().numpy(), ref.cpu().numpy()) < tol
+    assert rel_l2(spec.float().cpu().numpy(), g[f"spec_{tag}"]) < 2 * tol
+    s = torch.from_numpy(g[f"srand_{tag}"]).cuda().to(dtype).requires_grad_(True)
+    out = ist(s)
+    assert out.dtype == dtype
+    assert rel_l2(out.detach().float().cpu().numpy(), g[f"irand_{tag}"]) < 2 * tol
+    (out * torch.from_numpy(g[f"igout_{tag}"]).cuda().to(dtype)).sum().backward()
+    assert s.grad.dtype == dtype
+    assert rel_l2(s.grad.float().cpu().numpy(), g[f"igspec_{tag}"]) < 2 * tol

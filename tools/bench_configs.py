@@ -7,7 +7,14 @@ is config 4, the headline). Synthetic inputs, random-init weights.
      in 4 s chunks overlapping 50 ms (sehip/longform.py), and the same in fp32 and
      as one unchunked sequence (T = 9002 frames)
 
-Usage: python tools/bench_configs.py [--configs 2,3,5] [--iters 5]"""
+Configs 2 and 3 run twice: fp32 storage with bf16 GEMM operands, and as the
+reference's bf16 run, model.to(torch.bfloat16) with bf16 activations end to end
+(the CBN / STFT / BN kernels read and write bf16). Each line carries a roofline:
+algorithmic conv FLOPs per utterance (DCUNet-16 36.8 GFLOP forward,
+DCCRN-CL 199 GFLOP forward + backward) x utterances/s against the 2.5 PFLOP/s dense
+bf16 MFMA peak.
+
+Usage: python tools/bench_configs.py [--configs 2,3,5] [--iters 5] [--storage fp32,bf16]"""
 import argparse, json, os, sys, time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "speech-enhancement_amd"))
@@ -29,30 +36,45 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--configs", default="2,3,5")
     ap.add_argument("--iters", type=int, default=5)
+    ap.add_argument("--storage", default="fp32,bf16")
     a = ap.parse_args()
+    storages = a.storage.split(",")
+    BF16_PEAK = 2500.0
+    FLOPS = {2: 36.8e9, 3: 199e9}   # per utterance (torch FlopCounterMode)
+
+    def roof(cfg, ups):
+        tf = ups * FLOPS[cfg] / 1e12
+        return {"bound": "mfma", "achieved": round(tf, 1), "peak": BF16_PEAK, "unit": "TFLOP/s",
+                "frac": round(tf / BF16_PEAK, 4), "flops_per_utt": FLOPS[cfg]}
     from sehip import functional as F, models as M, longform as L
     from sehip.data import synthetic_pairs
     from sehip.train import make_optimizer, train_step
     dev = torch.device("cuda")
     cfgs = a.configs.split(",")
-    if "2" in cfgs:
-        F.set_conv_math("bf16")
-        m = M.DCUNet("dcunet16", 512, 128, 512).to(dev).eval()
-        x, _ = synthetic_pairs(16, 64000, seed=5, device=dev)
-        with torch.no_grad():
-            dt = timeit(lambda: m(x), a.iters)
-        print(json.dumps({"config": 2, "workload": "DCUNet-16 inference 4 s @ 16 kHz, batch 16", "conv_math": "bf16",
-                          "value": round(16 / dt, 2), "unit": "utterances/sec", "ms_per_batch": round(dt * 1e3, 3)}),
-              flush=True)
-    if "3" in cfgs:
-        F.set_conv_math("bf16")
-        m = M.DCCRN("dccrn-CL", 400, 100, 512).to(dev).train()
-        opt = make_optimizer(m)
-        x, c = synthetic_pairs(64, 64000, seed=6, device=dev)
-        dt = timeit(lambda: train_step(m, opt, x, c), a.iters)
-        print(json.dumps({"config": 3, "workload": "DCCRN-CL train step 4 s @ 16 kHz, batch 64", "conv_math": "bf16",
-                          "value": round(64 / dt, 2), "unit": "utterances/sec", "ms_per_step": round(dt * 1e3, 3)}),
-              flush=True)
+    for storage in storages:
+        sdt = torch.bfloat16 if storage == "bf16" else torch.float32
+        if "2" in cfgs:
+            F.set_conv_math("bf16")
+            m = M.DCUNet("dcunet16", 512, 128, 512).to(dev).eval().to(sdt)
+            x, _ = synthetic_pairs(16, 64000, seed=5, device=dev)
+            x = x.to(sdt)
+            with torch.no_grad():
+                dt = timeit(lambda: m(x), a.iters)
+            print(json.dumps({"config": 2, "workload": "DCUNet-16 inference 4 s @ 16 kHz, batch 16",
+                              "conv_math": "bf16", "storage": storage, "value": round(16 / dt, 2),
+                              "unit": "utterances/sec", "ms_per_batch": round(dt * 1e3, 3),
+                              "roofline": roof(2, 16 / dt)}), flush=True)
+        if "3" in cfgs:
+            F.set_conv_math("bf16")
+            m = M.DCCRN("dccrn-CL", 400, 100, 512).to(dev).train().to(sdt)
+            opt = make_optimizer(m)
+            x, c = synthetic_pairs(64, 64000, seed=6, device=dev)
+            x, c = x.to(sdt), c.to(sdt)
+            dt = timeit(lambda: train_step(m, opt, x, c), a.iters)
+            print(json.dumps({"config": 3, "workload": "DCCRN-CL train step 4 s @ 16 kHz, batch 64",
+                              "conv_math": "bf16", "storage": storage, "value": round(64 / dt, 2),
+                              "unit": "utterances/sec", "ms_per_step": round(dt * 1e3, 3),
+                              "roofline": roof(3, 64 / dt)}), flush=True)
     if "5" in cfgs:
         F.set_conv_math(F.DEFAULT_CONV_MATH)
         sr, secs = 48000, 30
