@@ -80,6 +80,10 @@ def _oracle_grads(noisy, clean, dtype, perturb=0.0, seed=1234):
         gen = torch.Generator().manual_seed(seed)
         x = x * (1 + perturb * torch.randn(x.shape, generator=gen, dtype=dtype))
     m = paramfill.fill_(O.FRCRN(), seed=47).to(dtype).train()
+    if perturb:   # the weights re-rounded too: a stand-in for the rounding inside every layer
+        with torch.no_grad():
+            for p in m.parameters():
+                p.mul_(1 + perturb * torch.randn(p.shape, generator=gen, dtype=dtype))
     _, w = m(x[:, None])
     OT.si_snr_loss(OT.pad_or_truncate_wav(w, c), c).backward()
     return {n: p.grad.double() for n, p in m.named_parameters()}
@@ -91,12 +95,15 @@ def test_frcrn_level_spread_train_step_grads_vs_fp64(gpu_device):
     items included): SI-SNR makes each utterance's gradient scale as 1/level,
     so the backward's operands spread as widely as the forward's. Gate as
     test_frcrn_train_step_golden: every parameter gradient within
-    max(3x the fp32 oracle's error, 3x its 2-ulp input sensitivity, 1e-3) of
-    fp64, the median within 3x the fp32 oracle's median. The sensitivity is the
-    largest move of the fp32 oracle over three 2-ulp input perturbations: a few
-    CCBAM spatial-attention gradients route through channel max-pools whose
-    argmax flips under any re-rounding (measured: one perturbation moves
-    spatial...norm.Wri by 1.2e-2 against 4.9e-3 for the plain fp32 run)."""
+    max(3x the fp32 oracle's error, 3x its 2-ulp sensitivity, 1e-3) of fp64, the
+    median within 3x the fp32 oracle's median. The sensitivity is the largest move
+    of the fp32 oracle over four perturbations of the input and the weights at
+    2^-21 relative, the HIP convs' own per-layer rounding (4.0e-7 rel-L2 f16x3,
+    6.4e-7 exact fp32 MFMA, vs fp64): a few CCBAM spatial-attention gradients route
+    through channel max-pools whose argmax flips under any re-rounding. Measured on
+    the CPU oracle for skip layer 3's spatial...norm.Wri (fp32 vs fp64: 6.2e-3):
+    perturbations at 2^-22 move it up to 1.0e-2, at 2^-20 up to 5.7e-2, at 2^-18
+    up to 1.1 (a chaotic gradient, not a precision signal)."""
     from sehip import models as M
     from sehip.losses import SI_SNR_loss, pad_or_truncate_wav
     noisy, clean, gains = level_spread_batch(4, 64000, seed=51)
@@ -107,7 +114,7 @@ def test_frcrn_level_spread_train_step_grads_vs_fp64(gpu_device):
     torch.cuda.synchronize()
     g64 = _oracle_grads(noisy, clean, torch.float64)
     g32 = _oracle_grads(noisy, clean, torch.float32)
-    g32ps = [_oracle_grads(noisy, clean, torch.float32, perturb=2.0 ** -22, seed=1234 + i) for i in range(3)]
+    g32ps = [_oracle_grads(noisy, clean, torch.float32, perturb=2.0 ** -21, seed=1234 + i) for i in range(4)]
     errs = []
     for n, p in m.named_parameters():
         d = g64[n].norm().item() + 1e-300
@@ -247,5 +254,8 @@ def test_first_conv_runs_exact_fp32(gpu_device):
     finally:
         F.set_op_timer(None)
     tags = [r[0] for r in timer.records if r[0].startswith("conv_")]
-    assert tags.count("conv_fwd_f32") == 1 and tags.count("conv_wgrad_f32") == 1, tags
+    # the first conv's weight-grad: exact fp32 products inside the fused first block's CBN
+    # backward (se_cbn_bwd_first_conv), or the fp32 weight-grad GEMM (SEHIP_FIRST_FUSED=0)
+    fused = sum(r[0] == "cbn_bwd_first_conv" for r in timer.records)
+    assert tags.count("conv_fwd_f32") == 1 and tags.count("conv_wgrad_f32") + fused == 1, tags
     assert tags.count("conv_fwd_f16x3") == 5 and "conv_data_f32" not in tags, tags

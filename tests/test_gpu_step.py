@@ -10,6 +10,8 @@ torch.optim.AdamW (fp32, the ops the reference calls) on the same GPU for the
 update. Tolerances: loss |d| <= 1e-5 |loss| + 1e-5 (fp64 sums vs fp32
 rounding of the reference formula), gradients rel-L2 <= 1e-5; clip and AdamW
 per element <= 1e-6 relative (same fp32 formulas, fp64 norm)."""
+import os
+
 import pytest
 import torch
 
@@ -169,7 +171,10 @@ def test_frcrn_fork_gradient_handoff_bit_identical(gpu_device, monkeypatch):
     monkeypatch.setenv("SEHIP_FORK_ACC", "1")
     before = F.FORK_ACC_CALLS[0]
     g1 = grads()
-    assert F.FORK_ACC_CALLS[0] - before == 5
+    # encoder blocks 1-4 accumulate; block 0's fork with the fused first block
+    # (se_cbn_bwd_first_conv) sums its two gradients in the CBN kernels instead
+    first_fused = os.environ.get("SEHIP_FIRST_FUSED", "1") != "0"
+    assert F.FORK_ACC_CALLS[0] - before == (4 if first_fused else 5)
     bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
     assert not bad, bad[:6]
 
