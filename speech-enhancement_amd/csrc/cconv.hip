@@ -126,6 +126,19 @@ template <int SD> __device__ __forceinline__ float bload(__amdgpu_buffer_rsrc_t 
     else return (float)__builtin_bit_cast(_Float16, v);
   }
 }
+// Raw bits of one 16-bit storage element (zero-extended), for the one-term split kernels
+// whose MFMA format is the storage format (bf16 storage + SE_MATH_BF16, fp16 + SE_MATH_F16):
+// the element is already its own hi operand, so it is staged as loaded and packed pairwise
+// into LDS, with no convert in between (a convert right behind each load made the compiler
+// wait for every load in turn: 2-2.5x slower gathers than the fp32-storage form).
+template <int SD> struct StageT { typedef unsigned T; };
+template <> struct StageT<0> { typedef float T; };
+__device__ __forceinline__ unsigned bload_raw16(__amdgpu_buffer_rsrc_t r, int vo, int so) {
+  return __builtin_amdgcn_raw_buffer_load_b16(r, vo, so, 0);
+}
+__device__ __forceinline__ unsigned ld_raw16(const void* p, long long i) {
+  return static_cast<const unsigned short*>(p)[i];
+}
 // a load of element i of a tensor of runtime storage type sd (small prologue kernels)
 __device__ __forceinline__ float ld_any(const void* p, long long i, int sd) {
   return sd == 1 ? ld_s<1>(p, i) : (sd == 2 ? ld_s<2>(p, i) : ld_s<0>(p, i));

@@ -242,6 +242,7 @@ __global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
   static_assert(SD == 0 || (TERMS == 1 && JM == 0 && BMX == 1 && !PP), "16-bit storage: one-term, plain tiles");
+  static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
   constexpr int ES = SD ? 2 : 4;                  // bytes per element of X / Y
   static_assert(NW == 1 || NW == 2, "128 or 256 columns per workgroup");
@@ -285,7 +286,7 @@ gather_x3_kernel(const GatherArgs a) {
     sa = pow2f(kF16Top - ea);
     ush = ea + amax_exp(a.amax_w) - 2 * kF16Top;
   }
-  struct Stage { float ra[AJ]; u32x4 rw[4]; };
+  struct Stage { typename StageT<SD>::T ra[AJ]; u32x4 rw[4]; };   // 16-bit storage: raw bits
   Stage s0, s1;
   auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
     const unsigned long long v = (unsigned long long)p;
@@ -334,14 +335,19 @@ gather_x3_kernel(const GatherArgs a) {
       vo = ok ? vo : (int)0x80000000;
       c0 += AJ * akr;
 #pragma unroll
-      for (int j = 0; j < AJ; ++j) st.ra[j] = bload<SD>(r, vo, (c0 + j) * cs);
+      for (int j = 0; j < AJ; ++j) {
+        if constexpr (SD != 0) st.ra[j] = bload_raw16(r, vo, (c0 + j) * cs);
+        else st.ra[j] = bload<0>(r, vo, (c0 + j) * cs);
+      }
     } else {
 #pragma unroll
       for (int j = 0; j < AJ; ++j) {
         const int4 e = a.ktab[k0 + AJ * akr + j];   // uniform index -> s_load
         const int hi = hb + e.y, wi = wb + e.z;
         const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-        st.ra[j] = ld_s<SD>(ok ? (const void*)a.X : (const void*)a.zero, ok ? xbase + e.x : 0);
+        const void* src = ok ? (const void*)a.X : (const void*)a.zero;
+        if constexpr (SD != 0) st.ra[j] = ld_raw16(src, ok ? xbase + e.x : 0);
+        else st.ra[j] = ld_s<0>(src, ok ? xbase + e.x : 0);
       }
     }
     const u32x4* src = wt + (long long)(k0 >> 5) * NT * NW * kX3TileU4;
@@ -358,8 +364,9 @@ gather_x3_kernel(const GatherArgs a) {
       u32x4 H, L;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        unsigned h, l;
-        split2<F16>(st.ra[8 * q + 2 * e], st.ra[8 * q + 2 * e + 1], sa, h, l);
+        unsigned h, l = 0;
+        if constexpr (SD != 0) h = st.ra[8 * q + 2 * e] | (st.ra[8 * q + 2 * e + 1] << 16);   // = split2's hi, sa = 1
+        else split2<F16>(st.ra[8 * q + 2 * e], st.ra[8 * q + 2 * e + 1], sa, h, l);
         H[e] = h;
         L[e] = l;
       }
@@ -689,6 +696,7 @@ __global__ void __launch_bounds__(kThreads * NB * KB, SEHIP_WGRAD_OCC)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(SD == 0 || (TERMS == 1 && !DJ), "16-bit storage: one-term, no join");
+  static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   constexpr int ES = SD ? 2 : 4;             // bytes per element of X / D
   static_assert(NB * KB <= 2, "one or two 128-row D blocks, or two G blocks");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
@@ -747,7 +755,7 @@ wgrad_x3_kernel(const WgradArgs a) {
     cqh = r / a.Qw;
     cqw = r - cqh * a.Qw;
   }
-  struct Stage { float rg[RJG], rd[RJ]; };
+  struct Stage { typename StageT<SD>::T rg[RJG], rd[RJ]; };   // 16-bit storage: raw bits
   Stage st0, st1;
   auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
     const unsigned long long v = (unsigned long long)p;
@@ -826,7 +834,10 @@ wgrad_x3_kernel(const WgradArgs a) {
                                  (long long)hi * a.Wi + wi) * ES) : (int)0x80000000;
       const int gs = (int)(HiWi * ES);
 #pragma unroll
-      for (int j = 0; j < RJG; ++j) S.rg[j] = bload<SD>(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
+      for (int j = 0; j < RJG; ++j) {
+        if constexpr (SD != 0) S.rg[j] = bload_raw16(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
+        else S.rg[j] = bload<0>(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
+      }
     } else {
       const int hb = cqh * a.sh, wb = cqw * a.sw;
       const long long xb = (long long)cb * a.Cg * HiWi + (long long)hb * a.Wi + wb;
@@ -835,11 +846,16 @@ wgrad_x3_kernel(const WgradArgs a) {
         const int4 e = sK[rbase_g + j];
         const int hi = hb + e.y, wi = wb + e.z;
         const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-        S.rg[j] = ld_s<SD>(ok ? (const void*)a.X : (const void*)a.zero, ok ? xb + e.x : 0);
+        const void* src = ok ? (const void*)a.X : (const void*)a.zero;
+        if constexpr (SD != 0) S.rg[j] = ld_raw16(src, ok ? xb + e.x : 0);
+        else S.rg[j] = ld_s<0>(src, ok ? xb + e.x : 0);
       }
     }
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) S.rd[j] = bload<SD>(rdr, vd, (srow + j) * ds);
+    for (int j = 0; j < RJ; ++j) {
+      if constexpr (SD != 0) S.rd[j] = bload_raw16(rdr, vd, (srow + j) * ds);
+      else S.rd[j] = bload<0>(rdr, vd, (srow + j) * ds);
+    }
     advance();
   };
   auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
@@ -851,13 +867,15 @@ wgrad_x3_kernel(const WgradArgs a) {
       u32x4 GH, GL, DH, DL;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        unsigned h, l;
+        unsigned h, l = 0;
         if (q < RJG / 8) {
-          split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
+          if constexpr (SD != 0) h = S.rg[8 * q + 2 * e] | (S.rg[8 * q + 2 * e + 1] << 16);   // split2's hi, sg = 1
+          else split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
           GH[e] = h; GL[e] = l;
         }
         if (q < RJ / 8) {
-          split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
+          if constexpr (SD != 0) h = S.rd[8 * q + 2 * e] | (S.rd[8 * q + 2 * e + 1] << 16);
+          else split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
           DH[e] = h; DL[e] = l;
         }
       }

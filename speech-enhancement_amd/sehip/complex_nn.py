@@ -195,8 +195,9 @@ def stacked_lstms(x, lstms, batch_first=True, with_state=False):
     m0 = lstms[0]
     nd = 2 if m0.bidirectional else 1
     H = m0.hidden_size
+    dt = x.dtype                                  # bf16 / fp16 models: fp32 recurrence, caller's dtype out
     xb = x if batch_first else x.transpose(0, 1)
-    inp = xb.contiguous()                         # layer 0: [B, T, I] shared by every LSTM
+    inp = _f32(xb).contiguous()                   # layer 0: [B, T, I] shared by every LSTM
     rev_mask = sum(1 << (i * nd + 1) for i in range(len(lstms))) if nd == 2 else 0
     out = None
     h_last, c_last = [], []
@@ -221,7 +222,7 @@ def stacked_lstms(x, lstms, batch_first=True, with_state=False):
             if m0.dropout > 0 and m0.training:
                 out = torch.nn.functional.dropout(out, m0.dropout, True)
             inp = out.repeat_interleave(nd, dim=0) if nd == 2 else out
-    outs = list(out.unbind(0))
+    outs = [o.to(dt) for o in out.unbind(0)]
     outs = outs if batch_first else [o.transpose(0, 1) for o in outs]
     if not with_state:
         return outs

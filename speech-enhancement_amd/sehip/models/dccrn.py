@@ -29,12 +29,30 @@ class _Block(nn.Module):
         self.norm = norm_cls(out_channels) if norm else nn.Identity()
         self.act = nn.PReLU() if act else nn.Identity()
 
-    def forward(self, x):
+    def forward(self, x, fork: bool = False):
+        """fork=True: (y, y2) for the two consumers of an encoder output (the next block
+        and the decoder skip, dccrn.py:98-101), summed inside the CBN backward."""
         lp = self.padding[1]
-        x = TF.pad(x, (lp, 0 if self.causal else lp, 0, 0))
+        pad = (lp, 0 if self.causal else lp, 0, 0)
         conv = getattr(self, self._attr)
-        y = real_conv2d(conv, x) if isinstance(conv, (nn.Conv2d, nn.ConvTranspose2d)) else conv(x)
-        return norm_act(self.norm, self.act, y)
+        plain = isinstance(conv, (nn.Conv2d, nn.ConvTranspose2d))
+        transposed = isinstance(conv, (nn.ConvTranspose2d, ComplexConvTranspose2d))
+        if lp and transposed:          # zero input columns of a convT: materialised
+            x, pad = TF.pad(x, pad), None
+        elif not lp:
+            pad = None
+        # a conv's causal time pad is folded into its (asymmetric) padding, not materialised
+        y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
+        return norm_act(self.norm, self.act, y, fork)
+
+    def forward_joined(self, x, skip):
+        """self(complex_concat([x[..., :T], skip])) (dccrn.py:116-120) with the concat folded
+        into the convT's GEMMs (se_conv2d_*_joined); None where that path does not apply."""
+        conv = getattr(self, self._attr)
+        if (self.padding[1] or not isinstance(conv, ComplexConvTranspose2d) or x.dtype != torch.float32
+                or skip.dtype != torch.float32 or x.shape[2] != skip.shape[2] or x.shape[1] != skip.shape[1]):
+            return None
+        return norm_act(self.norm, self.act, conv.forward_joined(x, skip))
 
 
 class ConvBlock(_Block):
@@ -86,9 +104,9 @@ class Encoder(nn.Module):
 
     def forward(self, x):
         outs = []
-        for layer in self.layers:
-            x = layer(x)
-            outs.append(x)
+        for layer in self.layers:   # each output feeds the next block (or the LSTM) and a decoder skip
+            x, skip = layer(x, fork=True)
+            outs.append(skip)
         return x, outs
 
 
@@ -106,9 +124,14 @@ class Decoder(nn.Module):
     def forward(self, x, encoder_outputs):
         for layer in self.layers:
             skip = encoder_outputs.pop()
-            if x.shape[-1] > skip.shape[-1]:
-                x = x[..., :-1]
-            x = layer(complex_concat([x, skip], dim=1))
+            # the reference trims one trailing frame of x (dccrn.py:116-117); the joined GEMMs
+            # read the first T frames of x directly
+            y = layer.forward_joined(x, skip) if x.shape[-1] - skip.shape[-1] in (0, 1) else None
+            if y is None:
+                if x.shape[-1] > skip.shape[-1]:
+                    x = x[..., :-1]
+                y = layer(complex_concat([x, skip], dim=1))
+            x = y
         return x
 
 
