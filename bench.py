@@ -113,6 +113,12 @@ def _dtype_label(mode):
     return "mixed (" + "+".join(sorted(modes)) + "; not fp32-class)"
 
 
+def _note(msg):
+    """Progress on stderr (the JSON line stays alone on stdout): a long phase such as the
+    CPU baseline must not look like a hung command to a watchdog."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -149,8 +155,9 @@ def cpu_baseline(batch, steps, warmup, budget_s):
         m = O.FRCRN().train()
         opt = torch.optim.AdamW(m.parameters(), lr=1e-3, weight_decay=1e-2)
         t_start = time.perf_counter()
-        for _ in range(warmup):
+        for i in range(warmup):
             OT.train_step(m, opt, noisy, clean)
+            _note(f"cpu baseline warm-up step {i + 1}/{warmup}")
         t_warm = time.perf_counter() - t_start
         per_step = t_warm / max(warmup, 1)
         t0 = time.perf_counter()
@@ -160,6 +167,7 @@ def cpu_baseline(batch, steps, warmup, budget_s):
                 break
             OT.train_step(m, opt, noisy, clean)
             done += 1
+            _note(f"cpu baseline step {done}/{steps}")
         dt = time.perf_counter() - t0
     finally:
         torch.set_num_threads(prev)
@@ -345,7 +353,9 @@ def run(args):
         return elapsed, float(loss)
 
     default_mode = SF.get_conv_math()
+    _note(f"rank {rank}: {args.warmup} warm-up + {args.steps} timed steps")
     elapsed, loss_v = timed(args.steps, args.warmup)            # the headline: no instrumentation
+    _note(f"rank {rank}: {world * B * args.steps / elapsed:.1f} utt/s")
     kern, kern_iso = {}, {}
     if not args.no_op_timing:
         timer = SF.OpTimer()
@@ -358,6 +368,7 @@ def run(args):
         timer = SF.OpTimer()
         timed(args.steps, 1, timer)
         kern_iso = timer.summary()
+        _note(f"rank {rank}: op timing done")
         if prev is None:
             del os.environ["SEHIP_OVERLAP"]
         else:
@@ -397,6 +408,7 @@ def run(args):
         SF.set_conv_math(mode)
         wu = max(args.warmup, 1) if mode == "f32" else 1
         e2, lc = timed(args.steps, wu)
+        _note(f"rank {rank}: {mode} leg {world * B * args.steps / e2:.1f} utt/s")
         entry = {"conv_math": mode, "dtype": _dtype_label(mode), "value": round(world * B * args.steps / e2, 3),
                  "ms_per_step": round(1e3 * e2 / args.steps, 3), "warmup": wu, "final_loss": round(lc, 4)}
         if mode == "f32" and not args.no_op_timing:

@@ -532,6 +532,23 @@ int se_ccbam_bwd_dx(const float* gout, const float* dpooled, const short* idx,
                     const int* amax, float* dx, int B, int C, int HW,
                     void* stream);
 
+/* Channel-attention MLP (ccbam.py:28-63, ComplexLinear complex_nn.py:93-113):
+ * ca [B, C] = sigmoid(f(mean) + f(max)), f = ComplexLinear(C, Hd, bias=False) ->
+ * ReLU -> ComplexLinear(Hd, C, bias=False), each ComplexLinear a real_linear on the
+ * first half of the features and an imag_linear on the second (no cross terms).
+ * w1r / w1i: [Hd/2][C/2], w2r / w2i: [C/2][Hd/2] (the nn.Linear weights). hsave
+ * [2B, Hd] (the ReLU outputs, avg rows then max rows) is written for the backward.
+ * se_ccbam_mlp_bwd: from dca, dmean / dmax [B, C] and the four weight gradients
+ * (overwritten; fp64 sums over the 2B rows). One workgroup each; needs
+ * (B*C + 2*B*Hd) floats of LDS <= 64 KB (SE_E_UNSUPPORTED otherwise). */
+int se_ccbam_mlp_fwd(const float* mean, const float* mx, const float* w1r, const float* w1i,
+                     const float* w2r, const float* w2i, int B, int C, int Hd, float* ca,
+                     float* hsave, void* stream);
+int se_ccbam_mlp_bwd(const float* dca, const float* ca, const float* mean, const float* mx,
+                     const float* hsave, const float* w1r, const float* w1i, const float* w2r,
+                     const float* w2i, int B, int C, int Hd, float* dmean, float* dmx,
+                     float* dw1r, float* dw1i, float* dw2r, float* dw2i, void* stream);
+
 /* ------------------------------------------------------------------------
  * Decoder skip join (models/_2206_07293_frcrn.py:93-100 + complex_concat,
  * complex_nn.py:4-16): out = [x_re, s_re, x_im, s_im] on channels, with x

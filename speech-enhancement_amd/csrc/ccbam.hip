@@ -271,6 +271,140 @@ int dca_tiles(int HW) { return (HW + kPos * kThreads - 1) / (kPos * kThreads); }
 
 }  // namespace
 
+namespace {
+
+// ---------------------------------------------------------------------------
+// Channel-attention MLP (ccbam.py:28-63): the avg- and max-pooled descriptors p
+// ([2B, C]: rows b < B = mean, rows B + b = max) through the shared
+//   ComplexLinear(C, Hd, bias=False) -> ReLU -> ComplexLinear(Hd, C, bias=False)
+// (complex_nn.py:93-113: the real half of a row through real_linear, the imaginary
+// half through imag_linear, no cross terms), then ca = sigmoid(o_avg + o_max).
+// One workgroup: the whole MLP is ~2B * C * Hd * 2 FMAs (FRCRN: 262 K), a few us,
+// in place of ~10 ATen / rocBLAS launches forward and ~20 backward. Sums run in
+// index order in fp32 (fp64 for the weight gradients over the 2B rows).
+// w1r / w1i: [Hd/2][C/2], w2r / w2i: [C/2][Hd/2] (nn.Linear [out][in]).
+constexpr int kMlpThreads = 256;
+__device__ __forceinline__ float mlp_p(const float* mean, const float* mx, int B, int C, int r, int c) {
+  return r < B ? mean[(long long)r * C + c] : mx[(long long)(r - B) * C + c];
+}
+
+__global__ void __launch_bounds__(kMlpThreads)
+mlp_fwd_kernel(const float* __restrict__ mean, const float* __restrict__ mx, const float* __restrict__ w1r,
+               const float* __restrict__ w1i, const float* __restrict__ w2r, const float* __restrict__ w2i,
+               int B, int C, int Hd, float* __restrict__ ca, float* __restrict__ hsave) {
+  extern __shared__ float sh[];   // h [2B][Hd]
+  const int C2 = C / 2, H2 = Hd / 2;
+  for (int idx = threadIdx.x; idx < 2 * B * Hd; idx += kMlpThreads) {
+    const int r = idx / Hd, j = idx - r * Hd;
+    const int half = j >= H2, jj = j - half * H2;
+    const float* w = (half ? w1i : w1r) + (long long)jj * C2;
+    float s = 0.f;
+    for (int c = 0; c < C2; ++c) s = fmaf(w[c], mlp_p(mean, mx, B, C, r, half * C2 + c), s);
+    s = fmaxf(s, 0.f);
+    sh[idx] = s;
+    hsave[idx] = s;
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < B * C; idx += kMlpThreads) {
+    const int b = idx / C, c = idx - b * C;
+    const int half = c >= C2, cc = c - half * C2;
+    const float* w = (half ? w2i : w2r) + (long long)cc * H2;
+    const float* ha = sh + (long long)b * Hd + half * H2;
+    const float* hm = sh + (long long)(B + b) * Hd + half * H2;
+    float oa = 0.f, om = 0.f;
+    for (int j = 0; j < H2; ++j) { oa = fmaf(w[j], ha[j], oa); om = fmaf(w[j], hm[j], om); }
+    ca[idx] = 1.f / (1.f + expf(-(oa + om)));
+  }
+}
+
+// Backward from dca [B, C]: dmean, dmax [B, C] and the four weight gradients.
+__global__ void __launch_bounds__(kMlpThreads)
+mlp_bwd_kernel(const float* __restrict__ dca, const float* __restrict__ ca, const float* __restrict__ mean,
+               const float* __restrict__ mx, const float* __restrict__ hsave, const float* __restrict__ w1r,
+               const float* __restrict__ w1i, const float* __restrict__ w2r, const float* __restrict__ w2i,
+               int B, int C, int Hd, float* __restrict__ dmean, float* __restrict__ dmx, float* __restrict__ dw1r,
+               float* __restrict__ dw1i, float* __restrict__ dw2r, float* __restrict__ dw2i) {
+  extern __shared__ float sh[];   // g [B][C] (= dL/do of both the avg and the max row), dh [2B][Hd]
+  float* g = sh;
+  float* dh = sh + (long long)B * C;
+  const int C2 = C / 2, H2 = Hd / 2;
+  for (int idx = threadIdx.x; idx < B * C; idx += kMlpThreads) {
+    const float a = ca[idx];
+    g[idx] = dca[idx] * a * (1.f - a);
+  }
+  __syncthreads();
+  for (int idx = threadIdx.x; idx < 2 * B * Hd; idx += kMlpThreads) {
+    const int r = idx / Hd, j = idx - r * Hd;
+    const int half = j >= H2, jj = j - half * H2;
+    const float* w = half ? w2i : w2r;
+    const float* gr = g + (long long)(r % B) * C + half * C2;
+    float s = 0.f;
+    for (int cc = 0; cc < C2; ++cc) s = fmaf(w[(long long)cc * H2 + jj], gr[cc], s);
+    dh[idx] = hsave[idx] > 0.f ? s : 0.f;
+  }
+  __syncthreads();
+  // dW2[c][j] = sum_r g[r mod B][c] h[r][j]
+  for (int idx = threadIdx.x; idx < C * H2; idx += kMlpThreads) {
+    const int c = idx / H2, jj = idx - c * H2;
+    const int half = c >= C2, cc = c - half * C2;
+    double s = 0.0;
+    for (int r = 0; r < 2 * B; ++r) s += (double)g[(long long)(r % B) * C + c] * hsave[(long long)r * Hd + half * H2 + jj];
+    (half ? dw2i : dw2r)[(long long)cc * H2 + jj] = (float)s;
+  }
+  // dW1[j][c] = sum_r dh[r][j] p[r][c]
+  for (int idx = threadIdx.x; idx < Hd * C2; idx += kMlpThreads) {
+    const int j = idx / C2, cc = idx - j * C2;
+    const int half = j >= H2, jj = j - half * H2;
+    double s = 0.0;
+    for (int r = 0; r < 2 * B; ++r) s += (double)dh[(long long)r * Hd + j] * mlp_p(mean, mx, B, C, r, half * C2 + cc);
+    (half ? dw1i : dw1r)[(long long)jj * C2 + cc] = (float)s;
+  }
+  // dp[r][c] = sum_j w1[j][c] dh[r][j]
+  for (int idx = threadIdx.x; idx < 2 * B * C; idx += kMlpThreads) {
+    const int r = idx / C, c = idx - r * C;
+    const int half = c >= C2, cc = c - half * C2;
+    const float* w = half ? w1i : w1r;
+    const float* d = dh + (long long)r * Hd + half * H2;
+    float s = 0.f;
+    for (int jj = 0; jj < H2; ++jj) s = fmaf(w[(long long)jj * C2 + cc], d[jj], s);
+    (r < B ? dmean : dmx)[(long long)(r % B) * C + c] = s;
+  }
+}
+
+}  // namespace
+
+static int mlp_check(int B, int C, int Hd) {
+  if (B <= 0 || C <= 0 || Hd <= 0 || (C & 1) || (Hd & 1)) return SE_E_ARG;
+  const size_t lds = ((size_t)B * C + 2 * (size_t)B * Hd) * sizeof(float);
+  return lds <= 64 * 1024 ? SE_OK : SE_E_UNSUPPORTED;   // one workgroup's LDS
+}
+
+extern "C" int se_ccbam_mlp_fwd(const float* mean, const float* mx, const float* w1r, const float* w1i,
+                                const float* w2r, const float* w2i, int B, int C, int Hd, float* ca, float* hsave,
+                                void* stream) {
+  if (int rc = mlp_check(B, C, Hd)) return rc;
+  if (!mean || !mx || !w1r || !w1i || !w2r || !w2i || !ca || !hsave) return SE_E_ARG;
+  hipLaunchKernelGGL(mlp_fwd_kernel, dim3(1), dim3(kMlpThreads), 2 * (size_t)B * Hd * sizeof(float),
+                     se::as_stream(stream), mean, mx, w1r, w1i, w2r, w2i, B, C, Hd, ca, hsave);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_ccbam_mlp_bwd(const float* dca, const float* ca, const float* mean, const float* mx,
+                                const float* hsave, const float* w1r, const float* w1i, const float* w2r,
+                                const float* w2i, int B, int C, int Hd, float* dmean, float* dmx, float* dw1r,
+                                float* dw1i, float* dw2r, float* dw2i, void* stream) {
+  if (int rc = mlp_check(B, C, Hd)) return rc;
+  if (!dca || !ca || !mean || !mx || !hsave || !w1r || !w1i || !w2r || !w2i || !dmean || !dmx || !dw1r || !dw1i ||
+      !dw2r || !dw2i)
+    return SE_E_ARG;
+  hipLaunchKernelGGL(mlp_bwd_kernel, dim3(1), dim3(kMlpThreads), ((size_t)B * C + 2 * (size_t)B * Hd) * sizeof(float),
+                     se::as_stream(stream), dca, ca, mean, mx, hsave, w1r, w1i, w2r, w2i, B, C, Hd, dmean, dmx, dw1r,
+                     dw1i, dw2r, dw2i);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
 extern "C" size_t se_ccbam_workspace_size(int B, int C, int HW) {
   if (check(B, C, HW)) return 0;
   return (size_t)B * dca_tiles(HW) * C * sizeof(float);

@@ -22,6 +22,10 @@
 #include <algorithm>
 #include <cmath>
 
+#ifndef SEHIP_STFT_PROBE
+#define SEHIP_STFT_PROBE 0   // measurement probes of stft_fwd_ip_kernel (tools/stft_probe.sh); 0 = the kernel
+#endif
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -301,15 +305,16 @@ __device__ __forceinline__ float2* fft_any(float2* a, float2* b, int P, const Ff
 // different XCDs and each L2 would write back a partial line. The bijective
 // remap gives consecutive frame blocks of an utterance to one XCD, dispatched
 // back to back, so the halves merge in that L2 before write-back.
-__device__ __forceinline__ void xcd_frame_block(int& tb, int& b) {
+__device__ __forceinline__ void xcd_frame_group(int L, int total, int nx, int& tb, int& b) {
   constexpr int kXcd = 8;
-  const int total = gridDim.x * gridDim.y;
-  const int L = blockIdx.y * gridDim.x + blockIdx.x;
   const int xcd = L % kXcd, idx = L / kXcd;
   const int q = total / kXcd, r = total % kXcd;
   const int t = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
-  b = t / gridDim.x;
-  tb = t - b * gridDim.x;
+  b = t / nx;
+  tb = t - b * nx;
+}
+__device__ __forceinline__ void xcd_frame_block(int& tb, int& b) {
+  xcd_frame_group(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y, gridDim.x, tb, b);
 }
 
 // Storage type of the signal / spectrum tensors (SE_DTYPE_*). LP = false: fp32 (the
@@ -436,8 +441,12 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
     const bool ok = idx < P * N && n < a.win;
     const int nn = ok ? n : 0;
     const float w = ok ? a.window[nn] : 0.f;
+#if SEHIP_STFT_PROBE == 3   // measurement probe: no signal loads
+    const float xa = (float)(ta * a.hop + nn), xb = (float)(tb * a.hop + nn);
+#else
     const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
     const float xb = ldx<LP>(a.x, xo + reflect_index(min(tb, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+#endif
     ya[it] = ta < a.T ? w * xa : 0.f;
     yb[it] = tb < a.T ? w * xb : 0.f;
   }
@@ -447,8 +456,64 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
     if (idx < P * N) A[idx] = make_float2(ya[it], yb[it]);
   }
   __syncthreads();
+#if SEHIP_STFT_PROBE != 1   // probe 1: no FFT passes
   fft_pass_ip<N, P, 0, 1>(A, stw);
+#endif
+#if SEHIP_STFT_PROBE == 2   // probe 2: no spectrum stores (a runtime-false branch keeps the FFT alive)
+  if (a.mag_phase != 7) return;
+#endif
   unpack_store<CN, P, LP>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
+}
+
+// stft_fwd_ip_kernel's work with each block walking frame groups (2P frames of one
+// utterance) g = blockIdx.x, + gridDim.x, ... in turn: the signal loads of the next
+// group are issued right after the current group is in LDS, so their latency hides
+// behind its FFT passes and spectrum stores instead of stalling a fresh block.
+// ngroups = nx * B groups (nx = ceil(T / 2P)); gridDim.x is a multiple of 8, so a
+// block keeps its XCD's groups in xcd_frame_group's order.
+template <int CN, int P = kPairsIP, bool LP = false>
+__global__ void __launch_bounds__(kThreads) stft_fwd_pf_kernel(const StftArgs a, int nx, int ngroups) {
+  constexpr int N = CN;
+  __shared__ __attribute__((aligned(16))) float2 A[P * N];
+  __shared__ float2 stw[N];
+  for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
+  constexpr int IT = (P * N + kThreads - 1) / kThreads;
+  float ya[IT], yb[IT];
+  auto gather = [&](int g) __attribute__((always_inline)) {
+    int tb, b;
+    xcd_frame_group(g, ngroups, nx, tb, b);
+    const int t0 = tb * 2 * P;
+    const long long xo = (long long)b * a.L;
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = threadIdx.x + it * kThreads;
+      const int j = idx / N, n = idx - j * N;
+      const int ta = t0 + 2 * j, tb2 = ta + 1;
+      const bool ok = idx < P * N && n < a.win;
+      const int nn = ok ? n : 0;
+      const float w = ok ? a.window[nn] : 0.f;
+      const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+      const float xb = ldx<LP>(a.x, xo + reflect_index(min(tb2, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+      ya[it] = ta < a.T ? w * xa : 0.f;
+      yb[it] = tb2 < a.T ? w * xb : 0.f;
+    }
+  };
+  int g = blockIdx.x;
+  if (g < ngroups) gather(g);
+  for (; g < ngroups; g += gridDim.x) {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int idx = threadIdx.x + it * kThreads;
+      if (idx < P * N) A[idx] = make_float2(ya[it], yb[it]);
+    }
+    __syncthreads();
+    if (g + (int)gridDim.x < ngroups) gather(g + gridDim.x);   // in flight during this group's FFT
+    fft_pass_ip<N, P, 0, 1>(A, stw);
+    int tb, b;
+    xcd_frame_group(g, ngroups, nx, tb, b);
+    unpack_store<CN, P, LP>(A, P, N, tb * 2 * P, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
+    __syncthreads();   // the next group's frames overwrite A
+  }
 }
 
 struct IstftArgs {
@@ -873,6 +938,32 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
     const int P = ip_pairs;
     const dim3 grid(se::ceil_div(T, 2 * P), B);
     hipStream_t st = se::as_stream(stream);
+    // SEHIP_STFT_GPB = k > 0: the prefetching form, k frame groups per block (A/B knob)
+    static const int gpb = [] {
+      const char* e = std::getenv("SEHIP_STFT_GPB");
+      return e ? std::max(0, std::atoi(e)) : 0;
+    }();
+    if (gpb > 0 && P == kPairsIP) {
+      const int nx = (int)grid.x, ngroups = nx * B;
+      const int nblk = se::ceil_div(se::ceil_div(ngroups, gpb), 8) * 8;
+#define SE_STFT_PF(NF)                                                                              \
+  do {                                                                                              \
+    if (a.dt != SE_DTYPE_F32)                                                                       \
+      hipLaunchKernelGGL((stft_fwd_pf_kernel<NF, kPairsIP, true>), dim3(nblk), dim3(kThreads), 0, st, a, nx, ngroups); \
+    else                                                                                            \
+      hipLaunchKernelGGL((stft_fwd_pf_kernel<NF, kPairsIP, false>), dim3(nblk), dim3(kThreads), 0, st, a, nx, ngroups); \
+  } while (0)
+      switch (nfft) {
+        case 640: SE_STFT_PF(640); break;
+        case 512: SE_STFT_PF(512); break;
+        case 400: SE_STFT_PF(400); break;
+        case 320: SE_STFT_PF(320); break;
+        default: SE_STFT_PF(256); break;
+      }
+#undef SE_STFT_PF
+      SE_LAUNCH_CHECK();
+      return SE_OK;
+    }
 #define SE_STFT_IP(NF)                                                                              \
   do {                                                                                              \
     if (P == 2) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 2, grid, 0, st, a);                     \

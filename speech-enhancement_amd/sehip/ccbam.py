@@ -10,6 +10,8 @@ the unfused reference formulation for anyone calling them directly.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -82,6 +84,30 @@ def _call(fn, name, *args):
     N.check(fn(*args), name)
 
 
+def _mlp_weights(cab: "ChannelAttention", B: int, C: int):
+    """(w1r, w1i, w2r, w2i) when the channel branch's MLP is the reference's
+    (ComplexLinear(C, Hd, bias=False) -> ReLU -> ComplexLinear(Hd, C, bias=False),
+    ccbam.py:36-39) on fp32 tensors and fits se_ccbam_mlp_*; else None (the MLP then
+    runs as its own modules). SEHIP_CCBAM_MLP=0 turns the fused kernels off."""
+    if os.environ.get("SEHIP_CCBAM_MLP", "1") == "0":
+        return None
+    fc = cab.shared_fc_layer
+    if len(fc) != 2 or not all(isinstance(b, LinearBlock) for b in fc):
+        return None
+    l1, l2 = fc[0].linear, fc[1].linear
+    if not (isinstance(fc[0].act, nn.ReLU) and isinstance(fc[1].act, nn.Identity)):
+        return None
+    ws = (l1.real_linear.weight, l1.imag_linear.weight, l2.real_linear.weight, l2.imag_linear.weight)
+    if any(lin.bias is not None for lin in (l1.real_linear, l1.imag_linear, l2.real_linear, l2.imag_linear)):
+        return None
+    if any(w.dtype != torch.float32 or not w.is_cuda or not w.is_contiguous() for w in ws):
+        return None
+    Hd = 2 * ws[0].shape[0]
+    if ws[0].shape[1] * 2 != C or tuple(ws[2].shape) != (C // 2, Hd // 2) or (B * C + 2 * B * Hd) * 4 > 64 * 1024:
+        return None
+    return ws
+
+
 class _CCBAMFn(torch.autograd.Function):
     """out = CCBAM(x) with the full-tensor passes on se_ccbam_* kernels.
 
@@ -104,12 +130,20 @@ class _CCBAMFn(torch.autograd.Function):
         amax = torch.empty(B, C, device=dev, dtype=torch.int32)
         _call(lib.se_ccbam_channel_pool, "se_ccbam_channel_pool", x.data_ptr(), mean.data_ptr(),
               mx.data_ptr(), amax.data_ptr(), B, C, HW, st)
-        with torch.set_grad_enabled(need_grad):
-            pooled = torch.cat([mean, mx], 0)
-            if need_grad:
-                pooled.requires_grad_(True)
-            a, m = torch.chunk(cab.shared_fc_layer(pooled), 2, dim=0)
-            ca = torch.sigmoid(a + m).contiguous()                   # [B, C]
+        mlp = _mlp_weights(cab, B, C)
+        pooled = hs = None
+        if mlp is not None:   # the whole MLP + sigmoid in one launch (se_ccbam_mlp_fwd)
+            ca = torch.empty(B, C, device=dev)
+            hs = torch.empty(2 * B, 2 * mlp[0].shape[0], device=dev)
+            _call(lib.se_ccbam_mlp_fwd, "se_ccbam_mlp_fwd", mean.data_ptr(), mx.data_ptr(),
+                  *(w.data_ptr() for w in mlp), B, C, hs.shape[1], ca.data_ptr(), hs.data_ptr(), st)
+        else:
+            with torch.set_grad_enabled(need_grad):
+                pooled = torch.cat([mean, mx], 0)
+                if need_grad:
+                    pooled.requires_grad_(True)
+                a, m = torch.chunk(cab.shared_fc_layer(pooled), 2, dim=0)
+                ca = torch.sigmoid(a + m).contiguous()               # [B, C]
         P = torch.empty(B, 4, H, W, device=dev)
         idx = torch.empty(B, 2, H, W, device=dev, dtype=torch.int16)
         _call(lib.se_ccbam_spatial_pool, "se_ccbam_spatial_pool", x.data_ptr(), ca.data_ptr(),
@@ -127,6 +161,7 @@ class _CCBAMFn(torch.autograd.Function):
             ctx.save_for_backward(x, idx, amax)
             ctx.graphs = (pooled, ca, Pl, sa)
             ctx.mod = mod
+            ctx.mlp = (mlp, mean, mx, hs) if mlp is not None else None
         return out
 
     @staticmethod
@@ -148,8 +183,19 @@ class _CCBAMFn(torch.autograd.Function):
         ws = F._workspace(lib.se_ccbam_workspace_size(B, C, HW), dev)
         _call(lib.se_ccbam_bwd_dca, "se_ccbam_bwd_dca", gout.data_ptr(), x.data_ptr(), dP.data_ptr(),
               idx.data_ptr(), dca.data_ptr(), B, C, HW, ws.data_ptr(), ws.numel(), st)
-        gc = torch.autograd.grad(ca, [pooled] + ch, dca, allow_unused=True)
-        dmean, dmax = (t.contiguous() for t in torch.chunk(gc[0], 2, dim=0))
+        if ctx.mlp is not None:   # se_ccbam_mlp_bwd: dmean, dmax and the four weight gradients
+            mlp, mean, mx, hs = ctx.mlp
+            dmean, dmax = torch.empty(B, C, device=dev), torch.empty(B, C, device=dev)
+            dws = [torch.empty_like(w) for w in mlp]
+            _call(lib.se_ccbam_mlp_bwd, "se_ccbam_mlp_bwd", dca.data_ptr(), ca.data_ptr(), mean.data_ptr(),
+                  mx.data_ptr(), hs.data_ptr(), *(w.data_ptr() for w in mlp), B, C, hs.shape[1],
+                  dmean.data_ptr(), dmax.data_ptr(), *(d.data_ptr() for d in dws), st)
+            by_id = {id(w): d for w, d in zip(mlp, dws)}
+            gc = [None] + [by_id.get(id(p)) for p in ch]
+            ctx.mlp = None
+        else:
+            gc = torch.autograd.grad(ca, [pooled] + ch, dca, allow_unused=True)
+            dmean, dmax = (t.contiguous() for t in torch.chunk(gc[0], 2, dim=0))
         dx = torch.empty_like(x)
         _call(lib.se_ccbam_bwd_dx, "se_ccbam_bwd_dx", gout.data_ptr(), dP.data_ptr(), idx.data_ptr(),
               ca.data_ptr(), dmean.data_ptr(), dmax.data_ptr(), amax.data_ptr(), dx.data_ptr(),

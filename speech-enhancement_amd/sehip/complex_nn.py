@@ -180,9 +180,23 @@ class ComplexLinear(nn.Module):
 HIP_LSTM_HIDDEN = (64, 128, 256, 512, 1024)
 
 
+def _wide_group_fits(m: nn.LSTM) -> bool:
+    """The wide recurrence (H = 256 / 512 / 1024) runs one group of H/32 (H/16 at 1024)
+    workgroups that must all be resident: a device with fewer CUs than one group runs
+    nn.LSTM's own forward instead (se_lstm_wide_* would return SE_E_UNSUPPORTED)."""
+    H = m.hidden_size
+    if H not in (256, 512, 1024):
+        return True
+    p = next(m.parameters(), None)
+    if p is None or not p.is_cuda:
+        return True
+    members = H // (16 if H == 1024 else 32)
+    return torch.cuda.get_device_properties(p.device).multi_processor_count >= members
+
+
 def _hip_lstm_ok(m: nn.LSTM) -> bool:
     return (m.proj_size == 0 and m.hidden_size in HIP_LSTM_HIDDEN
-            and (m.dropout == 0 or not m.training) and m.mode == "LSTM")
+            and (m.dropout == 0 or not m.training) and m.mode == "LSTM" and _wide_group_fits(m))
 
 
 def stacked_lstms(x, lstms, batch_first=True, with_state=False):

@@ -81,3 +81,63 @@ def test_ccbam_fused_matches_unfused_on_gpu(gpu_device):
     assert _rel(x2.grad, x1.grad) < 1e-4
     for n, p in mod.named_parameters():
         assert _rel(p.grad, g1[n]) < 1e-4, n
+
+
+@pytest.mark.parametrize("B,C,Hd", [(64, 128, 8), (3, 32, 4), (2, 4, 2)])
+def test_ccbam_mlp_kernels_vs_fp64(B, C, Hd, gpu_device):
+    """se_ccbam_mlp_fwd / _bwd (the channel branch's shared MLP + sigmoid in one launch
+    each way) against the same math in fp64 on the CPU: ca, dmean, dmax and the four
+    weight gradients at rel-L2 1e-5 (fp32 sums in index order vs fp64)."""
+    from sehip import _native as N
+    gen = torch.Generator().manual_seed(B + C)
+    mean, mx = torch.randn(B, C, generator=gen), torch.randn(B, C, generator=gen) + 1.0
+    w = [torch.randn(Hd // 2, C // 2, generator=gen) * 0.3, torch.randn(Hd // 2, C // 2, generator=gen) * 0.3,
+         torch.randn(C // 2, Hd // 2, generator=gen) * 0.3, torch.randn(C // 2, Hd // 2, generator=gen) * 0.3]
+    dca = torch.randn(B, C, generator=gen)
+    # fp64 reference: ComplexLinear -> ReLU -> ComplexLinear on [mean; max], sigmoid(a + m)
+    p = torch.cat([mean, mx]).double().requires_grad_(True)
+    w64 = [t.double().requires_grad_(True) for t in w]
+    h = torch.relu(torch.cat([p[:, :C // 2] @ w64[0].t(), p[:, C // 2:] @ w64[1].t()], 1))
+    o = torch.cat([h[:, :Hd // 2] @ w64[2].t(), h[:, Hd // 2:] @ w64[3].t()], 1)
+    ca64 = torch.sigmoid(o[:B] + o[B:])
+    ca64.backward(dca.double())
+    dev = gpu_device
+    md, xd, wd = mean.to(dev), mx.to(dev), [t.to(dev) for t in w]
+    ca = torch.empty(B, C, device=dev)
+    hs = torch.empty(2 * B, Hd, device=dev)
+    st = torch.cuda.current_stream().cuda_stream
+    lib = N.lib()
+    N.check(lib.se_ccbam_mlp_fwd(md.data_ptr(), xd.data_ptr(), *(t.data_ptr() for t in wd), B, C, Hd,
+                                 ca.data_ptr(), hs.data_ptr(), st), "se_ccbam_mlp_fwd")
+    dm, dx = torch.empty(B, C, device=dev), torch.empty(B, C, device=dev)
+    dws = [torch.empty_like(t) for t in wd]
+    N.check(lib.se_ccbam_mlp_bwd(dca.to(dev).data_ptr(), ca.data_ptr(), md.data_ptr(), xd.data_ptr(), hs.data_ptr(),
+                                 *(t.data_ptr() for t in wd), B, C, Hd, dm.data_ptr(), dx.data_ptr(),
+                                 *(t.data_ptr() for t in dws), st), "se_ccbam_mlp_bwd")
+    torch.cuda.synchronize()
+    assert _rel(ca, ca64) < 1e-6
+    assert _rel(dm, p.grad[:B]) < 1e-5 and _rel(dx, p.grad[B:]) < 1e-5
+    for got, ref in zip(dws, w64):
+        assert _rel(got, ref.grad) < 1e-5
+
+
+def test_ccbam_fused_mlp_matches_module_mlp(gpu_device, monkeypatch):
+    """The fused MLP launch (default) against the MLP run as its own modules
+    (SEHIP_CCBAM_MLP=0) inside the fused CCBAM: outputs and every gradient."""
+    from sehip.ccbam import CCBAM
+    torch.manual_seed(11)
+    mod = CCBAM(128).to(gpu_device).train()
+    x = torch.randn(4, 128, 17, 403, device=gpu_device)
+    g = torch.randn_like(x)
+    res = []
+    for flag in ("0", "1"):
+        monkeypatch.setenv("SEHIP_CCBAM_MLP", flag)
+        mod.zero_grad(set_to_none=True)
+        xi = x.clone().requires_grad_(True)
+        y = mod(xi)
+        (y * g).sum().backward()
+        res.append((y.detach(), xi.grad, {n: p.grad.clone() for n, p in mod.named_parameters()}))
+    (y0, dx0, g0), (y1, dx1, g1) = res
+    assert _rel(y1, y0) < 1e-6 and _rel(dx1, dx0) < 1e-5
+    for n in g0:
+        assert _rel(g1[n], g0[n]) < 1e-5, n

@@ -98,8 +98,11 @@ def test_frcrn_level_spread_train_step_grads_vs_fp64(gpu_device):
     max(3x the fp32 oracle's error, 3x its 2-ulp sensitivity, 1e-3) of fp64, the
     median within 3x the fp32 oracle's median. The sensitivity is the largest move
     of the fp32 oracle over four perturbations of the input and the weights at
-    2^-21 relative, the HIP convs' own per-layer rounding (4.0e-7 rel-L2 f16x3,
-    6.4e-7 exact fp32 MFMA, vs fp64): a few CCBAM spatial-attention gradients route
+    2^-20 relative: the size of the HIP path's own deviation from fp64 (per conv
+    4.0e-7 f16x3 / 6.4e-7 exact fp32 MFMA; at the model output 1-2.6e-6 per
+    utterance, test_frcrn_b16_level_spread_per_utterance_vs_oracle). For a
+    well-conditioned gradient that move is ~1e-6, far under the 1e-3 floor, so the
+    gate only widens for the chaotic ones: a few CCBAM spatial-attention gradients route
     through channel max-pools whose argmax flips under any re-rounding. Measured on
     the CPU oracle for skip layer 3's spatial...norm.Wri (fp32 vs fp64: 6.2e-3):
     perturbations at 2^-22 move it up to 1.0e-2, at 2^-20 up to 5.7e-2, at 2^-18
@@ -114,7 +117,7 @@ def test_frcrn_level_spread_train_step_grads_vs_fp64(gpu_device):
     torch.cuda.synchronize()
     g64 = _oracle_grads(noisy, clean, torch.float64)
     g32 = _oracle_grads(noisy, clean, torch.float32)
-    g32ps = [_oracle_grads(noisy, clean, torch.float32, perturb=2.0 ** -21, seed=1234 + i) for i in range(4)]
+    g32ps = [_oracle_grads(noisy, clean, torch.float32, perturb=2.0 ** -20, seed=1234 + i) for i in range(4)]
     errs = []
     for n, p in m.named_parameters():
         d = g64[n].norm().item() + 1e-300
