@@ -555,12 +555,13 @@ int se_ccbam_mlp_bwd(const float* dca, const float* ca, const float* mean, const
  * [B, Cx, Fx, Tx] cropped / zero-padded at the end of each spatial dim to
  * s's [F, T] (x[..., :-1] and F.pad(x, (0, 0, 0, 1)) in the reference).
  * out: [B, Cx + Cs, F, T]. Backward writes gx over x's own grid (zeros where
- * x was cropped) and gs.
+ * x was cropped) and gs. dtype (SE_DTYPE_*, ABI 4): storage type of all the
+ * tensors (a bf16 / fp16 model's decoder, e.g. DCCRN's, dccrn.py:116-120).
  * ------------------------------------------------------------------------ */
-int se_complex_join(const float* x, int Cx, int Fx, int Tx, const float* s,
-                    int Cs, int F, int T, float* out, int B, void* stream);
-int se_complex_join_bwd(const float* gout, float* gx, int Cx, int Fx, int Tx,
-                        float* gs, int Cs, int F, int T, int B, void* stream);
+int se_complex_join(const void* x, int Cx, int Fx, int Tx, const void* s,
+                    int Cs, int F, int T, void* out, int B, int dtype, void* stream);
+int se_complex_join_bwd(const void* gout, void* gx, int Cx, int Fx, int Tx,
+                        void* gs, int Cs, int F, int T, int B, int dtype, void* stream);
 
 /* ------------------------------------------------------------------------
  * Data path: the reference mixes and crops on the host

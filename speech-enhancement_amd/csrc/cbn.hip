@@ -659,7 +659,19 @@ cbn_bwd_apply_fc_kernel(const float* __restrict__ gy, const float* __restrict__ 
                         int act, float slope, FirstConv fc, float* __restrict__ wpart) {
   static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
   constexpr int NT = CIN * KH * KW, NE = 2 * NT;
-  const int Cc = C / 2, c = blockIdx.x, b = blockIdx.y, B = gridDim.y;
+  // XCD-aware (channel, item) order: dispatch deals consecutive workgroups to the 8 XCDs in
+  // turn, so the remap hands each XCD a run of consecutive channels of one item; they share
+  // that item's conv-input plane x0[b] through the XCD's L2 instead of each re-fetching it
+  const int Cc = C / 2, B = gridDim.y;
+  int c, b;
+  {
+    constexpr int kXcd = 8;
+    const int total = gridDim.x * gridDim.y, L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xcd = L % kXcd, idx = L / kXcd, q = total / kXcd, r = total % kXcd;
+    const int t = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+    b = t / gridDim.x;
+    c = t - b * gridDim.x;
+  }
   const float* k = coef + c * kCoef;
   const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
   const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
@@ -671,23 +683,30 @@ cbn_bwd_apply_fc_kernel(const float* __restrict__ gy, const float* __restrict__ 
   float acc[NE];
 #pragma unroll
   for (int e = 0; e < NE; ++e) acc[e] = 0.f;
-  for (int i = threadIdx.x; i < HW; i += kThreads) {
-    const float xr = x[offr + i] - mr, xi = x[offi + i] - mi;
+  // positions i = threadIdx.x + kThreads * (U * it + u): the loads of U positions are
+  // issued before any arithmetic, and (qh, qw) step incrementally (no division per position)
+  constexpr int U = 4;
+  int qh = threadIdx.x / W, qw = threadIdx.x - (threadIdx.x / W) * W;
+  const int qstep_h = kThreads / W, qstep_w = kThreads - (kThreads / W) * W;
+  auto advance = [&]() __attribute__((always_inline)) {
+    qw += qstep_w;
+    qh += qstep_h;
+    if (qw >= W) { qw -= W; ++qh; }
+  };
+  auto body = [&](float fxr, float fxi, float dyr, float dyi, int ph, int pw) __attribute__((always_inline)) {
+    const float xr = fxr - mr, xi = fxi - mi;
     const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
-    const float dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
-    const float dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
     const float g1 = dyr * act_grad(zr, act, slope) - gbr;
     const float g2 = dyi * act_grad(zi, act, slope) - gbi;
     const float gr = a00 * g1 + a01 * g2 + grr * xr + gri * xi;   // dL/dy0 (the conv's dy), never stored
     const float gi = a10 * g1 + a11 * g2 + gri * xr + gii * xi;
-    const int qh = i / W, qw = i - qh * W;
 #pragma unroll
     for (int th = 0; th < KH; ++th) {
-      const int h = qh * fc.sh + th * fc.dh - fc.ph;
+      const int h = ph * fc.sh + th * fc.dh - fc.ph;
       const bool hok = (unsigned)h < (unsigned)fc.Hi;
 #pragma unroll
       for (int tw = 0; tw < KW; ++tw) {
-        const int w = qw * fc.sw + tw * fc.dw - fc.pw;
+        const int w = pw * fc.sw + tw * fc.dw - fc.pw;
         const bool ok = hok & ((unsigned)w < (unsigned)fc.Wi);
         const long long o = ok ? (long long)h * fc.Wi + w : 0;
 #pragma unroll
@@ -700,6 +719,30 @@ cbn_bwd_apply_fc_kernel(const float* __restrict__ gy, const float* __restrict__ 
         }
       }
     }
+  };
+  int i = threadIdx.x;
+  for (; i + (U - 1) * kThreads < HW; i += U * kThreads) {
+    float fr[U], fm[U], dr[U], dm[U];
+    int ph[U], pw[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int j = i + u * kThreads;
+      fr[u] = x[offr + j];
+      fm[u] = x[offi + j];
+      dr[u] = SRC == 1 ? gy[offr + j] + gy2[offr + j] : gy[offr + j];
+      dm[u] = SRC == 1 ? gy[offi + j] + gy2[offi + j] : gy[offi + j];
+      ph[u] = qh;
+      pw[u] = qw;
+      advance();
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) body(fr[u], fm[u], dr[u], dm[u], ph[u], pw[u]);
+  }
+  for (; i < HW; i += kThreads) {
+    const float dyr = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
+    const float dyi = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
+    body(x[offr + i], x[offi + i], dyr, dyi, qh, qw);
+    advance();
   }
   __shared__ float red[kThreads / 64][NE];
 #pragma unroll

@@ -32,44 +32,50 @@ __device__ __forceinline__ void join_src(const JoinGeom& g, int o, int& src, int
   else { src = 1; c = hs + (o - 2 * hx - hs); }
 }
 
-// One block per joined plane (b, o): rows f, lanes along t (coalesced).
+// One block per joined plane (b, o), a flat loop over its F x T positions (coalesced
+// along t). E: the element's bit pattern (fp32, or bf16 / fp16 storage: a copy
+// moves bits, and a zero is all-zero bits in every format).
 // grid (B * (Cx + Cs))
-__global__ __launch_bounds__(kThreads) void join_fwd_kernel(const float* __restrict__ x, const float* __restrict__ s,
-                                                            float* __restrict__ out, JoinGeom g) {
+template <typename E>
+__global__ __launch_bounds__(kThreads) void join_fwd_kernel(const E* __restrict__ x, const E* __restrict__ s,
+                                                            E* __restrict__ out, JoinGeom g) {
   const int Co = g.Cx + g.Cs;
   const int b = blockIdx.x / Co, o = blockIdx.x - b * Co;
   int src, c;
   join_src(g, o, src, c);
-  float* op = out + ((long long)b * Co + o) * g.F * g.T;
+  E* op = out + ((long long)b * Co + o) * g.F * g.T;
   if (src == 1) {
-    const float* sp = s + ((long long)b * g.Cs + c) * g.F * g.T;
+    const E* sp = s + ((long long)b * g.Cs + c) * g.F * g.T;
     for (int i = threadIdx.x; i < g.F * g.T; i += kThreads) op[i] = sp[i];   // same grid: flat copy
     return;
   }
-  const float* xp = x + ((long long)b * g.Cx + c) * g.Fx * g.Tx;
-  for (int f = 0; f < g.F; ++f)
-    for (int t = threadIdx.x; t < g.T; t += kThreads)
-      op[f * g.T + t] = (f < g.Fx && t < g.Tx) ? xp[f * g.Tx + t] : 0.f;
+  const E* xp = x + ((long long)b * g.Cx + c) * g.Fx * g.Tx;
+  for (int i = threadIdx.x; i < g.F * g.T; i += kThreads) {
+    const int f = i / g.T, t = i - f * g.T;
+    op[i] = (f < g.Fx && t < g.Tx) ? xp[f * g.Tx + t] : E(0);
+  }
 }
 
 // dx over x's own grid (zeros where x was cropped away), ds = its slots.
 // grid (B * (Cx + Cs))
-__global__ __launch_bounds__(kThreads) void join_bwd_kernel(const float* __restrict__ gout, float* __restrict__ gx,
-                                                            float* __restrict__ gs, JoinGeom g) {
+template <typename E>
+__global__ __launch_bounds__(kThreads) void join_bwd_kernel(const E* __restrict__ gout, E* __restrict__ gx,
+                                                            E* __restrict__ gs, JoinGeom g) {
   const int Co = g.Cx + g.Cs;
   const int b = blockIdx.x / Co, o = blockIdx.x - b * Co;
   int src, c;
   join_src(g, o, src, c);
-  const float* gp = gout + ((long long)b * Co + o) * g.F * g.T;
+  const E* gp = gout + ((long long)b * Co + o) * g.F * g.T;
   if (src == 1) {
-    float* sp = gs + ((long long)b * g.Cs + c) * g.F * g.T;
+    E* sp = gs + ((long long)b * g.Cs + c) * g.F * g.T;
     for (int i = threadIdx.x; i < g.F * g.T; i += kThreads) sp[i] = gp[i];
     return;
   }
-  float* xp = gx + ((long long)b * g.Cx + c) * g.Fx * g.Tx;
-  for (int f = 0; f < g.Fx; ++f)
-    for (int t = threadIdx.x; t < g.Tx; t += kThreads)
-      xp[f * g.Tx + t] = (f < g.F && t < g.T) ? gp[f * g.T + t] : 0.f;
+  E* xp = gx + ((long long)b * g.Cx + c) * g.Fx * g.Tx;
+  for (int i = threadIdx.x; i < g.Fx * g.Tx; i += kThreads) {
+    const int f = i / g.Tx, t = i - f * g.Tx;
+    xp[i] = (f < g.F && t < g.T) ? gp[f * g.T + t] : E(0);
+  }
 }
 
 int check(const JoinGeom& g) {
@@ -82,24 +88,34 @@ int check(const JoinGeom& g) {
 
 }  // namespace
 
-extern "C" int se_complex_join(const float* x, int Cx, int Fx, int Tx, const float* s, int Cs, int F, int T,
-                               float* out, int B, void* stream) {
+extern "C" int se_complex_join(const void* x, int Cx, int Fx, int Tx, const void* s, int Cs, int F, int T,
+                               void* out, int B, int dtype, void* stream) {
   JoinGeom g{B, Cx, Fx, Tx, Cs, F, T};
   if (int rc = check(g)) return rc;
-  if (!x || !s || !out) return SE_E_ARG;
+  if (!x || !s || !out || dtype < SE_DTYPE_F32 || dtype > SE_DTYPE_F16) return SE_E_ARG;
   dim3 grid(B * (Cx + Cs));
-  hipLaunchKernelGGL(join_fwd_kernel, grid, dim3(kThreads), 0, se::as_stream(stream), x, s, out, g);
+  if (dtype == SE_DTYPE_F32)
+    hipLaunchKernelGGL(join_fwd_kernel<unsigned>, grid, dim3(kThreads), 0, se::as_stream(stream),
+                       (const unsigned*)x, (const unsigned*)s, (unsigned*)out, g);
+  else
+    hipLaunchKernelGGL(join_fwd_kernel<unsigned short>, grid, dim3(kThreads), 0, se::as_stream(stream),
+                       (const unsigned short*)x, (const unsigned short*)s, (unsigned short*)out, g);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
 
-extern "C" int se_complex_join_bwd(const float* gout, float* gx, int Cx, int Fx, int Tx, float* gs, int Cs, int F,
-                                   int T, int B, void* stream) {
+extern "C" int se_complex_join_bwd(const void* gout, void* gx, int Cx, int Fx, int Tx, void* gs, int Cs, int F,
+                                   int T, int B, int dtype, void* stream) {
   JoinGeom g{B, Cx, Fx, Tx, Cs, F, T};
   if (int rc = check(g)) return rc;
-  if (!gout || !gx || !gs) return SE_E_ARG;
+  if (!gout || !gx || !gs || dtype < SE_DTYPE_F32 || dtype > SE_DTYPE_F16) return SE_E_ARG;
   dim3 grid(B * (Cx + Cs));
-  hipLaunchKernelGGL(join_bwd_kernel, grid, dim3(kThreads), 0, se::as_stream(stream), gout, gx, gs, g);
+  if (dtype == SE_DTYPE_F32)
+    hipLaunchKernelGGL(join_bwd_kernel<unsigned>, grid, dim3(kThreads), 0, se::as_stream(stream),
+                       (const unsigned*)gout, (unsigned*)gx, (unsigned*)gs, g);
+  else
+    hipLaunchKernelGGL(join_bwd_kernel<unsigned short>, grid, dim3(kThreads), 0, se::as_stream(stream),
+                       (const unsigned short*)gout, (unsigned short*)gx, (unsigned short*)gs, g);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

@@ -246,17 +246,17 @@ __device__ float2* fft_pass(float2* a, float2* b, const float2* __restrict__ tw)
 // inputs of the pass into registers, then (after a barrier) writes all outputs
 // into the SAME buffer. Half the LDS of the ping-pong form, so a block holds
 // twice the frames (16 at nfft 640) and writes 64-B row segments.
-template <int N, int P, int PS, int NS>
+template <int N, int P, int PS, int NS, int TPB = kThreads>
 __device__ void fft_pass_ip(float2* a, const float2* __restrict__ tw) {
   constexpr CPlan pl = make_cplan(N);
   if constexpr (PS < pl.npass) {
     constexpr int R = pl.radix[PS], nbf = N / R, tstep = N / (NS * R);
-    constexpr int ITER = (P * nbf + kThreads - 1) / kThreads;
+    constexpr int ITER = (P * nbf + TPB - 1) / TPB;
     float2 v[ITER][kMaxRadix];
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
-      const int idx = threadIdx.x + it * kThreads;
-      if (P * nbf % kThreads == 0 || idx < P * nbf) {
+      const int idx = threadIdx.x + it * TPB;
+      if (P * nbf % TPB == 0 || idx < P * nbf) {
         const int pr = idx / nbf, j = idx - pr * nbf;
         const float2* src = a + pr * N;
         const int k = j % NS;
@@ -271,15 +271,15 @@ __device__ void fft_pass_ip(float2* a, const float2* __restrict__ tw) {
     __syncthreads();
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
-      const int idx = threadIdx.x + it * kThreads;
-      if (P * nbf % kThreads == 0 || idx < P * nbf) {
+      const int idx = threadIdx.x + it * TPB;
+      if (P * nbf % TPB == 0 || idx < P * nbf) {
         const int pr = idx / nbf, j = idx - pr * nbf;
         const int k = j % NS;
         butterfly<R>(v[it], a + pr * N, (j / NS) * NS * R + k, NS);
       }
     }
     __syncthreads();
-    fft_pass_ip<N, P, PS + 1, NS * R>(a, tw);
+    fft_pass_ip<N, P, PS + 1, NS * R, TPB>(a, tw);
   }
 }
 
@@ -418,8 +418,10 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
 // (tools/stft_micro.py; the XCD-aware block order merges the 32-B row segments
 // of neighbouring blocks in one L2)
 constexpr int kPairsIP = 4;
-template <int CN, int P = kPairsIP, bool LP = false>
-__global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a) {
+// TPB: threads per block (SEHIP_STFT_TPB=320 at nfft 640: the 4 x 80 radix-8 butterflies of
+// the first two passes in one iteration instead of 1.25)
+template <int CN, int P = kPairsIP, bool LP = false, int TPB = kThreads>
+__global__ void __launch_bounds__(TPB) stft_fwd_ip_kernel(const StftArgs a) {
   constexpr int N = CN;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
   __shared__ float2 stw[N];
@@ -427,15 +429,15 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   xcd_frame_block(tb, b);
   const int t0 = tb * 2 * P;
   const long long xo = (long long)b * a.L;
-  for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
+  for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
   // frame gather: all of a thread's loads are issued before any is used
   // (compile-time trip count; branch-free clamped addresses and zero weights),
   // so the block pays one memory latency instead of one per element
-  constexpr int IT = (P * N + kThreads - 1) / kThreads;
+  constexpr int IT = (P * N + TPB - 1) / TPB;
   float ya[IT], yb[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int idx = threadIdx.x + it * kThreads;
+    const int idx = threadIdx.x + it * TPB;
     const int j = idx / N, n = idx - j * N;
     const int ta = t0 + 2 * j, tb = ta + 1;
     const bool ok = idx < P * N && n < a.win;
@@ -452,12 +454,12 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   }
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int idx = threadIdx.x + it * kThreads;
+    const int idx = threadIdx.x + it * TPB;
     if (idx < P * N) A[idx] = make_float2(ya[it], yb[it]);
   }
   __syncthreads();
 #if SEHIP_STFT_PROBE != 1   // probe 1: no FFT passes
-  fft_pass_ip<N, P, 0, 1>(A, stw);
+  fft_pass_ip<N, P, 0, 1, TPB>(A, stw);
 #endif
 #if SEHIP_STFT_PROBE == 2   // probe 2: no spectrum stores (a runtime-false branch keeps the FFT alive)
   if (a.mag_phase != 7) return;
@@ -961,6 +963,19 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
         default: SE_STFT_PF(256); break;
       }
 #undef SE_STFT_PF
+      SE_LAUNCH_CHECK();
+      return SE_OK;
+    }
+    // SEHIP_STFT_TPB = 320 at nfft 640 (A/B knob): 5 waves per block
+    static const int tpb = [] {
+      const char* e = std::getenv("SEHIP_STFT_TPB");
+      return e ? std::atoi(e) : kThreads;
+    }();
+    if (tpb == 320 && nfft == 640 && P == kPairsIP) {
+      if (a.dt != SE_DTYPE_F32)
+        hipLaunchKernelGGL((stft_fwd_ip_kernel<640, kPairsIP, true, 320>), grid, dim3(320), 0, st, a);
+      else
+        hipLaunchKernelGGL((stft_fwd_ip_kernel<640, kPairsIP, false, 320>), grid, dim3(320), 0, st, a);
       SE_LAUNCH_CHECK();
       return SE_OK;
     }

@@ -127,8 +127,8 @@ _SIGNATURES = {
     "se_ccbam_bwd_dx": (c_int, [_P] * 8 + [c_int] * 3 + [_P]),
     "se_ccbam_mlp_fwd": (c_int, [_P] * 6 + [c_int] * 3 + [_P] * 3),
     "se_ccbam_mlp_bwd": (c_int, [_P] * 9 + [c_int] * 3 + [_P] * 7),
-    "se_complex_join": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_int, c_int, _P, c_int, _P]),
-    "se_complex_join_bwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, c_int, c_int, c_int, c_int, _P]),
+    "se_complex_join": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_int, c_int, _P, c_int, c_int, _P]),
+    "se_complex_join_bwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P]),
 }
 
 

@@ -516,7 +516,7 @@ def _join_raw(x, s):
     _, Cs, F_, T = s.shape
     out = torch.empty((B, Cx + Cs, F_, T), device=x.device, dtype=x.dtype)
     N.check(N.lib().se_complex_join(x.data_ptr(), Cx, Fx, Tx, s.data_ptr(), Cs, F_, T, out.data_ptr(), B,
-                                    N.stream_of(x)), "se_complex_join")
+                                    N.dtype_code(x), N.stream_of(x)), "se_complex_join")
     return out
 
 
@@ -589,7 +589,7 @@ class _ConvJoined(torch.autograd.Function):
                 N.check(lib.se_conv2d_bwd_data(N.ctypes.byref(d), gy.data_ptr(), wr.data_ptr(), wi.data_ptr(),
                                                dj.data_ptr(), ws.data_ptr(), ws.numel(), st), "se_conv2d_bwd_data")
                 rc = lib.se_complex_join_bwd(dj.data_ptr(), gx.data_ptr(), x.shape[1], Fx, Tx, gs.data_ptr(),
-                                             s.shape[1], d.in_h, d.in_w, d.batch, st)
+                                             s.shape[1], d.in_h, d.in_w, d.batch, N.dtype_code(gy), st)
             N.check(rc, "se_conv2d_bwd_data_joined")
             if t0 is not None:
                 _TIMER.end(_gemm_tag("data", d, joined=True), t0, _conv_flops(d),
@@ -1326,13 +1326,13 @@ def lstm_layer(x, w_ih, w_hh, b_ih=None, b_hh=None, rev_mask: int = 0, with_cell
 class _ComplexJoin(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, s):
-        N.require_device(x, s)
+        N.require_device(x, s, dtype=x.dtype)   # fp32, or bf16 / fp16 storage (bits copied)
         x, s = x.contiguous(), s.contiguous()
         B, Cx, Fx, Tx = x.shape
         _, Cs, Fs, Ts = s.shape
         out = torch.empty((B, Cx + Cs, Fs, Ts), device=x.device, dtype=x.dtype)
         N.check(N.lib().se_complex_join(x.data_ptr(), Cx, Fx, Tx, s.data_ptr(), Cs, Fs, Ts,
-                                        out.data_ptr(), B, N.stream_of(x)), "se_complex_join")
+                                        out.data_ptr(), B, N.dtype_code(x), N.stream_of(x)), "se_complex_join")
         ctx.geom = (B, Cx, Fx, Tx, Cs, Fs, Ts)
         return out
 
@@ -1343,7 +1343,8 @@ class _ComplexJoin(torch.autograd.Function):
         gx = torch.empty((B, Cx, Fx, Tx), device=gout.device, dtype=gout.dtype)
         gs = torch.empty((B, Cs, Fs, Ts), device=gout.device, dtype=gout.dtype)
         N.check(N.lib().se_complex_join_bwd(gout.data_ptr(), gx.data_ptr(), Cx, Fx, Tx, gs.data_ptr(),
-                                            Cs, Fs, Ts, B, N.stream_of(gout)), "se_complex_join_bwd")
+                                            Cs, Fs, Ts, B, N.dtype_code(gout), N.stream_of(gout)),
+                "se_complex_join_bwd")
         return gx, gs
 
 

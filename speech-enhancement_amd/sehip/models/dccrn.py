@@ -7,6 +7,7 @@ import torch.nn.functional as TF
 
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLinear,
                           ComplexLSTM, LSTM, complex_concat, mark_data_fed, norm_act, real_conv2d)
+from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -126,7 +127,12 @@ class Decoder(nn.Module):
             skip = encoder_outputs.pop()
             # the reference trims one trailing frame of x (dccrn.py:116-117); the joined GEMMs
             # read the first T frames of x directly
-            y = layer.forward_joined(x, skip) if x.shape[-1] - skip.shape[-1] in (0, 1) else None
+            aligned = x.shape[-1] - skip.shape[-1] in (0, 1) and x.shape[2] == skip.shape[2]
+            y = layer.forward_joined(x, skip) if aligned else None
+            if y is None and aligned and x.is_cuda and x.dtype == skip.dtype:
+                # no joined GEMM for this mode / width (e.g. bf16 storage): the trim and
+                # complex_concat as one HIP pass each way (se_complex_join), any storage type
+                y = layer(F.complex_join(x, skip))
             if y is None:
                 if x.shape[-1] > skip.shape[-1]:
                     x = x[..., :-1]

@@ -174,6 +174,6 @@ def test_ccbam_and_join_validation_need_no_gpu():
     ws = lib.se_ccbam_workspace_size(2, 8, 10)
     assert lib.se_ccbam_bwd_dca(None, None, None, None, None, 2, 8, 10, None, ws, None) == -1
     # join: (x, Cx, Fx, Tx, s, Cs, F, T, out, B, stream)
-    assert lib.se_complex_join(None, 3, 4, 5, None, 4, 4, 5, None, 1, None) == -2   # odd Cx
-    assert lib.se_complex_join(None, 4, 4, 5, None, 4, 4, 5, None, 1, None) == -1   # null pointers
-    assert lib.se_complex_join_bwd(None, None, 4, 4, 5, None, 4, 0, 5, 1, None) == -1
+    assert lib.se_complex_join(None, 3, 4, 5, None, 4, 4, 5, None, 1, 0, None) == -2   # odd Cx
+    assert lib.se_complex_join(None, 4, 4, 5, None, 4, 4, 5, None, 1, 0, None) == -1   # null pointers
+    assert lib.se_complex_join_bwd(None, None, 4, 4, 5, None, 4, 0, 5, 1, 0, None) == -1
