@@ -83,7 +83,7 @@ def parse():
     ap.add_argument("--cpu-steps", type=int, default=20, help="timed oracle steps (BASELINE.md plan: >= 20)")
     ap.add_argument("--cpu-warmup", type=int, default=5, help="untimed oracle steps first (BASELINE.md plan: 5)")
     ap.add_argument("--cpu-batch", type=int, default=8)
-    ap.add_argument("--cpu-budget-s", type=float, default=330.0,
+    ap.add_argument("--cpu-budget-s", type=float, default=400.0,
                     help="wall-clock cap of the CPU baseline (warm-up + timed); the timed loop stops early "
                          "past it and the sample says how many steps ran")
     ap.add_argument("--no-cpu-baseline", action="store_true")

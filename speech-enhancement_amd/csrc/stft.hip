@@ -418,10 +418,9 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
 // (tools/stft_micro.py; the XCD-aware block order merges the 32-B row segments
 // of neighbouring blocks in one L2)
 constexpr int kPairsIP = 4;
-// TPB: threads per block (SEHIP_STFT_TPB=320 at nfft 640: the 4 x 80 radix-8 butterflies of
-// the first two passes in one iteration instead of 1.25)
-template <int CN, int P = kPairsIP, bool LP = false, int TPB = kThreads>
-__global__ void __launch_bounds__(TPB) stft_fwd_ip_kernel(const StftArgs a) {
+template <int CN, int P = kPairsIP, bool LP = false>
+__global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a) {
+  constexpr int TPB = kThreads;
   constexpr int N = CN;
   __shared__ __attribute__((aligned(16))) float2 A[P * N];
   __shared__ float2 stw[N];
@@ -465,57 +464,6 @@ __global__ void __launch_bounds__(TPB) stft_fwd_ip_kernel(const StftArgs a) {
   if (a.mag_phase != 7) return;
 #endif
   unpack_store<CN, P, LP>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
-}
-
-// stft_fwd_ip_kernel's work with each block walking frame groups (2P frames of one
-// utterance) g = blockIdx.x, + gridDim.x, ... in turn: the signal loads of the next
-// group are issued right after the current group is in LDS, so their latency hides
-// behind its FFT passes and spectrum stores instead of stalling a fresh block.
-// ngroups = nx * B groups (nx = ceil(T / 2P)); gridDim.x is a multiple of 8, so a
-// block keeps its XCD's groups in xcd_frame_group's order.
-template <int CN, int P = kPairsIP, bool LP = false>
-__global__ void __launch_bounds__(kThreads) stft_fwd_pf_kernel(const StftArgs a, int nx, int ngroups) {
-  constexpr int N = CN;
-  __shared__ __attribute__((aligned(16))) float2 A[P * N];
-  __shared__ float2 stw[N];
-  for (int i = threadIdx.x; i < N; i += kThreads) stw[i] = a.tw[i];
-  constexpr int IT = (P * N + kThreads - 1) / kThreads;
-  float ya[IT], yb[IT];
-  auto gather = [&](int g) __attribute__((always_inline)) {
-    int tb, b;
-    xcd_frame_group(g, ngroups, nx, tb, b);
-    const int t0 = tb * 2 * P;
-    const long long xo = (long long)b * a.L;
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = threadIdx.x + it * kThreads;
-      const int j = idx / N, n = idx - j * N;
-      const int ta = t0 + 2 * j, tb2 = ta + 1;
-      const bool ok = idx < P * N && n < a.win;
-      const int nn = ok ? n : 0;
-      const float w = ok ? a.window[nn] : 0.f;
-      const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
-      const float xb = ldx<LP>(a.x, xo + reflect_index(min(tb2, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
-      ya[it] = ta < a.T ? w * xa : 0.f;
-      yb[it] = tb2 < a.T ? w * xb : 0.f;
-    }
-  };
-  int g = blockIdx.x;
-  if (g < ngroups) gather(g);
-  for (; g < ngroups; g += gridDim.x) {
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int idx = threadIdx.x + it * kThreads;
-      if (idx < P * N) A[idx] = make_float2(ya[it], yb[it]);
-    }
-    __syncthreads();
-    if (g + (int)gridDim.x < ngroups) gather(g + gridDim.x);   // in flight during this group's FFT
-    fft_pass_ip<N, P, 0, 1>(A, stw);
-    int tb, b;
-    xcd_frame_group(g, ngroups, nx, tb, b);
-    unpack_store<CN, P, LP>(A, P, N, tb * 2 * P, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
-    __syncthreads();   // the next group's frames overwrite A
-  }
 }
 
 struct IstftArgs {
@@ -940,45 +888,6 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
     const int P = ip_pairs;
     const dim3 grid(se::ceil_div(T, 2 * P), B);
     hipStream_t st = se::as_stream(stream);
-    // SEHIP_STFT_GPB = k > 0: the prefetching form, k frame groups per block (A/B knob)
-    static const int gpb = [] {
-      const char* e = std::getenv("SEHIP_STFT_GPB");
-      return e ? std::max(0, std::atoi(e)) : 0;
-    }();
-    if (gpb > 0 && P == kPairsIP) {
-      const int nx = (int)grid.x, ngroups = nx * B;
-      const int nblk = se::ceil_div(se::ceil_div(ngroups, gpb), 8) * 8;
-#define SE_STFT_PF(NF)                                                                              \
-  do {                                                                                              \
-    if (a.dt != SE_DTYPE_F32)                                                                       \
-      hipLaunchKernelGGL((stft_fwd_pf_kernel<NF, kPairsIP, true>), dim3(nblk), dim3(kThreads), 0, st, a, nx, ngroups); \
-    else                                                                                            \
-      hipLaunchKernelGGL((stft_fwd_pf_kernel<NF, kPairsIP, false>), dim3(nblk), dim3(kThreads), 0, st, a, nx, ngroups); \
-  } while (0)
-      switch (nfft) {
-        case 640: SE_STFT_PF(640); break;
-        case 512: SE_STFT_PF(512); break;
-        case 400: SE_STFT_PF(400); break;
-        case 320: SE_STFT_PF(320); break;
-        default: SE_STFT_PF(256); break;
-      }
-#undef SE_STFT_PF
-      SE_LAUNCH_CHECK();
-      return SE_OK;
-    }
-    // SEHIP_STFT_TPB = 320 at nfft 640 (A/B knob): 5 waves per block
-    static const int tpb = [] {
-      const char* e = std::getenv("SEHIP_STFT_TPB");
-      return e ? std::atoi(e) : kThreads;
-    }();
-    if (tpb == 320 && nfft == 640 && P == kPairsIP) {
-      if (a.dt != SE_DTYPE_F32)
-        hipLaunchKernelGGL((stft_fwd_ip_kernel<640, kPairsIP, true, 320>), grid, dim3(320), 0, st, a);
-      else
-        hipLaunchKernelGGL((stft_fwd_ip_kernel<640, kPairsIP, false, 320>), grid, dim3(320), 0, st, a);
-      SE_LAUNCH_CHECK();
-      return SE_OK;
-    }
 #define SE_STFT_IP(NF)                                                                              \
   do {                                                                                              \
     if (P == 2) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 2, grid, 0, st, a);                     \
