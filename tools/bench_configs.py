@@ -75,6 +75,24 @@ def main():
                               "conv_math": "bf16", "storage": storage, "value": round(64 / dt, 2),
                               "unit": "utterances/sec", "ms_per_step": round(dt * 1e3, 3),
                               "roofline": roof(3, 64 / dt)}), flush=True)
+    def counted_flops(fn):
+        """FLOPs of one call as the op timer records them (conv passes: torch
+        FlopCounterMode's formula; LSTM: 2 L B T G H per recurrence), no timing."""
+        timer = F.OpTimer()
+        F.set_op_timer(timer)
+        try:
+            with torch.no_grad():
+                fn()
+            torch.cuda.synchronize()
+        finally:
+            F.set_op_timer(None)
+        return sum(v.get("flops", 0.0) for v in timer.summary().values())
+
+    def roof_of(flops, dt, peak, note):
+        tf = flops / dt / 1e12
+        return {"bound": "mfma", "achieved": round(tf, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(tf / peak, 5), "flops_per_utt": flops, "note": note}
+
     if "5" in cfgs:
         F.set_conv_math(F.DEFAULT_CONV_MATH)
         sr, secs = 48000, 30
@@ -84,17 +102,24 @@ def main():
             m = M.CARN(320, 160, 512).to(dev).eval().to(dtype)
             xd = x.to(dtype)
             dt = timeit(lambda: L.enhance_chunked(m, xd, chunk, overlap), a.iters, warm=1)
+            fl = counted_flops(lambda: L.enhance_chunked(m, xd, chunk, overlap))
             print(json.dumps({"config": 5, "workload": "CARN inference, 30 s @ 48 kHz [1, 1440000], 4 s chunks "
                               "(50 ms cross-fade) as one batch of 8", "storage": label,
                               "conv_math": F.get_conv_math(), "ms_per_utterance": round(dt * 1e3, 2),
                               "realtime_factor": round(secs / dt, 1), "value": round(1 / dt, 3),
-                              "unit": "utterances/sec (30 s each)"}), flush=True)
+                              "unit": "utterances/sec (30 s each)",
+                              "roofline": roof_of(fl, dt, BF16_PEAK, "fp16 storage: one-term fp16 MFMA; fp32: "
+                                                  "f16x3 (3 MFMA terms per FLOP counted once); the 512-wide "
+                                                  "LSTM recurrence is latency-bound")}), flush=True)
         m = M.CARN(320, 160, 512).to(dev).eval().half()
         with torch.no_grad():
             dt = timeit(lambda: m(x.half()), max(1, a.iters // 2), warm=1)
+        fl = counted_flops(lambda: m(x.half()))
         print(json.dumps({"config": 5, "workload": "CARN inference, 30 s @ 48 kHz as ONE sequence (T = 9002 frames)",
                           "storage": "fp16", "ms_per_utterance": round(dt * 1e3, 2),
-                          "realtime_factor": round(secs / dt, 1)}), flush=True)
+                          "realtime_factor": round(secs / dt, 1),
+                          "roofline": roof_of(fl, dt, BF16_PEAK, "dominated by the 9002-step LSTM recurrence "
+                                              "(latency-bound: 2 us per step)")}), flush=True)
 
 
 if __name__ == "__main__":
