@@ -234,11 +234,18 @@ cbn_apply_kernel(const T* __restrict__ x, T* __restrict__ y, int C, int HW,
   const float zir = s[S_ZIR], zii = s[S_ZII], br = s[S_BR], bi = s[S_BI];
   const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
   const int base = blockIdx.x * kThreads * 4 + threadIdx.x;
+  float fxr[4], fxi[4];   // the four positions' loads first (clamped index), stores guarded
+#pragma unroll
+  for (int u = 0; u < 4; ++u) {
+    const int j = min(base + u * kThreads, HW - 1);
+    fxr[u] = (float)x[offr + j];
+    fxi[u] = (float)x[offi + j];
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = base + u * kThreads;
     if (i < HW) {
-      const float xr = (float)x[offr + i] - mr, xi = (float)x[offi + i] - mi;
+      const float xr = fxr[u] - mr, xi = fxi[u] - mi;
       float yr = zrr * xr + zri * xi + br;
       float yi = zir * xr + zii * xi + bi;
       if (act == 1) { yr = yr > 0.f ? yr : yr * slope; yi = yi > 0.f ? yi : yi * slope; }
@@ -562,6 +569,32 @@ cbn_bwd_apply_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
   // forward Z = [[a00, a10], [a01, a11]] (coef holds Z^T)
   const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
   const int base = blockIdx.x * kThreads * 4 + threadIdx.x;
+  if constexpr (SRC != 2) {
+    // the four positions' loads first (clamped index; the stores stay guarded), so a thread
+    // keeps them all in flight instead of one position's latency after another
+    float fxr[4], fxi[4], fgr[4], fgi[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int j = min(base + u * kThreads, HW - 1);
+      fxr[u] = (float)x[offr + j];
+      fxi[u] = (float)x[offi + j];
+      fgr[u] = SRC == 1 ? (float)gy[offr + j] + (float)gy2[offr + j] : (float)gy[offr + j];
+      fgi[u] = SRC == 1 ? (float)gy[offi + j] + (float)gy2[offi + j] : (float)gy[offi + j];
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int i = base + u * kThreads;
+      if (i < HW) {
+        const float xr = fxr[u] - mr, xi = fxi[u] - mi;
+        const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
+        const float gr = fgr[u] * act_grad(zr, act, slope) - gbr;
+        const float gi = fgi[u] * act_grad(zi, act, slope) - gbi;
+        dx[offr + i] = (T)(a00 * gr + a01 * gi + grr * xr + gri * xi);
+        dx[offi + i] = (T)(a10 * gr + a11 * gi + gri * xr + gii * xi);
+      }
+    }
+    return;
+  }
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const int i = base + u * kThreads;
@@ -756,6 +789,108 @@ cbn_bwd_apply_fc_kernel(const float* __restrict__ gy, const float* __restrict__ 
 #pragma unroll
     for (int w = 0; w < kThreads / 64; ++w) s += red[w][threadIdx.x];
     wpart[((long long)c * B + b) * NE + threadIdx.x] = s;
+  }
+}
+
+// cbn_bwd_apply_fc_kernel over CPB channels per workgroup: a position's conv-input taps
+// (20 values of the spectrum at FRCRN's first conv) are loaded once and serve CPB channels,
+// instead of once per channel (those L2 loads are ~80 % of the one-channel form's loads).
+// grid (Cc / CPB, B); per channel the same products in the same position order as the
+// one-channel form, so the partials are bit-identical.
+template <int SRC, int CIN, int KH, int KW, int CPB>
+__global__ void __launch_bounds__(kThreads)
+cbn_bwd_apply_fcm_kernel(const float* __restrict__ gy, const float* __restrict__ gy2,
+                         const float* __restrict__ x, int C, int HW, int W, const float* __restrict__ coef,
+                         int act, float slope, FirstConv fc, float* __restrict__ wpart) {
+  static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
+  constexpr int NT = CIN * KH * KW, NE = 2 * NT;
+  const int Cc = C / 2, B = gridDim.y;
+  int cb, b;
+  {   // XCD-aware (channel block, item) order, as cbn_bwd_apply_fc_kernel
+    constexpr int kXcd = 8;
+    const int total = gridDim.x * gridDim.y, L = blockIdx.y * gridDim.x + blockIdx.x;
+    const int xcd = L % kXcd, idx = L / kXcd, q = total / kXcd, r = total % kXcd;
+    const int t = xcd < r ? xcd * (q + 1) + idx : r * (q + 1) + (xcd - r) * q + idx;
+    b = t / gridDim.x;
+    cb = t - b * gridDim.x;
+  }
+  const int c0 = cb * CPB;
+  const long long HiWi = (long long)fc.Hi * fc.Wi;
+  const float* x0r = fc.x0 + (long long)b * 2 * CIN * HiWi;
+  const float* x0i = x0r + CIN * HiWi;
+  float acc[CPB][NE];
+#pragma unroll
+  for (int cc = 0; cc < CPB; ++cc)
+#pragma unroll
+    for (int e = 0; e < NE; ++e) acc[cc][e] = 0.f;
+  int qh = threadIdx.x / W, qw = threadIdx.x - (threadIdx.x / W) * W;
+  const int qstep_h = kThreads / W, qstep_w = kThreads - (kThreads / W) * W;
+  for (int i = threadIdx.x; i < HW; i += kThreads) {
+    float vr[NT], vi[NT];
+#pragma unroll
+    for (int th = 0; th < KH; ++th) {
+      const int h = qh * fc.sh + th * fc.dh - fc.ph;
+      const bool hok = (unsigned)h < (unsigned)fc.Hi;
+#pragma unroll
+      for (int tw = 0; tw < KW; ++tw) {
+        const int w = qw * fc.sw + tw * fc.dw - fc.pw;
+        const bool ok = hok & ((unsigned)w < (unsigned)fc.Wi);
+        const long long o = ok ? (long long)h * fc.Wi + w : 0;
+#pragma unroll
+        for (int ci = 0; ci < CIN; ++ci) {
+          const int tap = (ci * KH + th) * KW + tw;
+          vr[tap] = ok ? x0r[ci * HiWi + o] : 0.f;
+          vi[tap] = ok ? x0i[ci * HiWi + o] : 0.f;
+        }
+      }
+    }
+    float fxr[CPB], fxi[CPB], dyr[CPB], dyi[CPB];
+#pragma unroll
+    for (int cc = 0; cc < CPB; ++cc) {
+      const long long offr = ((long long)b * C + c0 + cc) * HW, offi = ((long long)b * C + Cc + c0 + cc) * HW;
+      fxr[cc] = x[offr + i];
+      fxi[cc] = x[offi + i];
+      dyr[cc] = SRC == 1 ? gy[offr + i] + gy2[offr + i] : gy[offr + i];
+      dyi[cc] = SRC == 1 ? gy[offi + i] + gy2[offi + i] : gy[offi + i];
+    }
+#pragma unroll
+    for (int cc = 0; cc < CPB; ++cc) {
+      const float* k = coef + (c0 + cc) * kCoef;
+      const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
+      const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
+      const float br = k[11], bi = k[12];
+      const float xr = fxr[cc] - mr, xi = fxi[cc] - mi;
+      const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
+      const float g1 = dyr[cc] * act_grad(zr, act, slope) - gbr;
+      const float g2 = dyi[cc] * act_grad(zi, act, slope) - gbi;
+      const float gr = a00 * g1 + a01 * g2 + grr * xr + gri * xi;   // dL/dy0 (the conv's dy), never stored
+      const float gi = a10 * g1 + a11 * g2 + gri * xr + gii * xi;
+#pragma unroll
+      for (int tap = 0; tap < NT; ++tap) {
+        acc[cc][2 * tap] = fmaf(gr, vr[tap], fmaf(gi, vi[tap], acc[cc][2 * tap]));
+        acc[cc][2 * tap + 1] = fmaf(gi, vr[tap], fmaf(-gr, vi[tap], acc[cc][2 * tap + 1]));
+      }
+    }
+    qw += qstep_w;
+    qh += qstep_h;
+    if (qw >= W) { qw -= W; ++qh; }
+  }
+  __shared__ float red[kThreads / 64][NE];
+#pragma unroll
+  for (int cc = 0; cc < CPB; ++cc) {
+#pragma unroll
+    for (int e = 0; e < NE; ++e) {
+      const float v = se::wave_sum(acc[cc][e]);
+      if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][e] = v;
+    }
+    __syncthreads();
+    if (threadIdx.x < NE) {
+      float sm = 0.f;
+#pragma unroll
+      for (int w = 0; w < kThreads / 64; ++w) sm += red[w][threadIdx.x];
+      wpart[((long long)(c0 + cc) * B + b) * NE + threadIdx.x] = sm;
+    }
+    __syncthreads();
   }
 }
 
@@ -1049,12 +1184,29 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   if (fc) {   // (checked by the entry point: FRCRN's first conv, cin 1, kernel (5, 2); fp32)
     if constexpr (sizeof(T) == 4) {
       float* wpart = (float*)(((uintptr_t)ws + ws_bytes_ns(B, C, HW, 7) + 255) & ~(uintptr_t)255);
-      if (src == 1)
-        hipLaunchKernelGGL((cbn_bwd_apply_fc_kernel<1, 1, 5, 2>), dim3(Cc, B), mb, 0, st, (const float*)gy,
-                           (const float*)gy2, (const float*)x, C, HW, fc_w, coef, act, slope, *fc, wpart);
+      // SEHIP_FC_CPB = channels per workgroup (1: cbn_bwd_apply_fc_kernel; 2 / 4: the tap-sharing
+      // form; A/B knob)
+      const int cpb = [] {   // read per call (one host getenv per training step)
+        const char* e = std::getenv("SEHIP_FC_CPB");
+        const int v = e ? std::atoi(e) : 1;
+        return (v == 2 || v == 4) ? v : 1;
+      }();
+      const float* g1 = (const float*)gy;
+      const float* g2 = (const float*)gy2;
+      const float* xx = (const float*)x;
+#define SE_FCM(SRCV, CPBV)                                                                          \
+  hipLaunchKernelGGL((cbn_bwd_apply_fcm_kernel<SRCV, 1, 5, 2, CPBV>), dim3(Cc / CPBV, B), dim3(kThreads), 0, st, \
+                     g1, g2, xx, C, HW, fc_w, coef, act, slope, *fc, wpart)
+      if (cpb > 1 && Cc % cpb == 0) {
+        if (src == 1) { if (cpb == 4) SE_FCM(1, 4); else SE_FCM(1, 2); }
+        else { if (cpb == 4) SE_FCM(0, 4); else SE_FCM(0, 2); }
+      } else if (src == 1)
+        hipLaunchKernelGGL((cbn_bwd_apply_fc_kernel<1, 1, 5, 2>), dim3(Cc, B), mb, 0, st, g1, g2, xx, C, HW, fc_w,
+                           coef, act, slope, *fc, wpart);
       else
-        hipLaunchKernelGGL((cbn_bwd_apply_fc_kernel<0, 1, 5, 2>), dim3(Cc, B), mb, 0, st, (const float*)gy,
-                           (const float*)gy2, (const float*)x, C, HW, fc_w, coef, act, slope, *fc, wpart);
+        hipLaunchKernelGGL((cbn_bwd_apply_fc_kernel<0, 1, 5, 2>), dim3(Cc, B), mb, 0, st, g1, g2, xx, C, HW, fc_w,
+                           coef, act, slope, *fc, wpart);
+#undef SE_FCM
       SE_LAUNCH_CHECK();
       hipLaunchKernelGGL(cbn_first_conv_finish_kernel, dim3(Cc), dim3(64), 0, st, wpart, B, 20, fc->dwr, fc->dwi);
       SE_LAUNCH_CHECK();

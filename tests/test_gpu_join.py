@@ -147,3 +147,25 @@ def test_complex_join_matches_reference(gpu_device, xs, ss):
     (yd * g.to(gpu_device)).sum().backward()
     assert torch.equal(xd.grad.cpu(), xr.grad)
     assert torch.equal(sd.grad.cpu(), sr.grad)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("xs,ss", JOINED)
+def test_complex_join_16bit_storage_bit_exact(gpu_device, xs, ss, dtype):
+    """se_complex_join(_bwd) on bf16 / fp16 tensors (ABI 4 dtype argument; DCCRN's bf16
+    decoder): the same bits as the reference formulation's crop / pad / complex_concat in
+    that dtype, forward and both gradients."""
+    from sehip import functional as F
+    torch.manual_seed(3)
+    x = torch.randn(xs).to(dtype)
+    s = torch.randn(ss).to(dtype)
+    xr, sr = x.clone().requires_grad_(True), s.clone().requires_grad_(True)
+    yr = _ref(xr, sr)
+    g = torch.randn(yr.shape).to(dtype)
+    yr.backward(g)
+    xd, sd = x.to(gpu_device).requires_grad_(True), s.to(gpu_device).requires_grad_(True)
+    yd = F.complex_join(xd, sd)
+    yd.backward(g.to(gpu_device))
+    assert yd.dtype == dtype and xd.grad.dtype == dtype
+    assert torch.equal(yd.detach().cpu(), yr.detach())
+    assert torch.equal(xd.grad.cpu(), xr.grad) and torch.equal(sd.grad.cpu(), sr.grad)

@@ -294,3 +294,28 @@ def test_real_conv_models_backward_vs_oracle(i, gpu_device):
     print(f"{name}: grads vs fp64 hip {e_hip:.2e} cpu-fp32 {e_cpu:.2e}; worst param {p_hip:.2e} / {p_cpu:.2e}")
     assert e_hip < 2 * e_cpu and e_hip < 1e-5, (name, e_hip, e_cpu)
     assert p_hip < 5 * p_cpu and p_hip < 1e-3, (name, p_hip, p_cpu)
+
+
+@pytest.mark.timeout(450)
+def test_frcrn_bench_batch_b64_train_forward_vs_oracle(gpu_device):
+    """The bench's own workload at its full size: B = 64 x 4 s, bench.py's synthetic pairs
+    (sehip.data.synthetic_pairs, seed 2023, SNR U{-5..20} dB), train-mode forward (batch
+    statistics over all 64 utterances) against the CPU oracle, per utterance at the north
+    star's 1e-4, and the CBN running statistics after the step."""
+    from sehip import models as M
+    from sehip.data import synthetic_pairs
+    from oracle import models as O
+    noisy, _ = synthetic_pairs(64, 64000, seed=2023, device="cpu")
+    mo = paramfill.fill_(O.FRCRN(), seed=17).train()
+    m = paramfill.fill_(M.FRCRN(), seed=17).cuda().train()
+    with torch.no_grad():
+        so, wo = mo(noisy)
+        s, w = m(noisy.cuda())
+    s, w = s.cpu().numpy(), w.cpu().numpy()
+    worst = max(max(rel_l2(s[b], so[b].numpy()), rel_l2(w[b], wo[b].numpy())) for b in range(64))
+    print(f"B=64 bench batch: worst per-utterance rel-L2 {worst:.2e}")
+    assert worst < TOL
+    bo = dict(mo.named_buffers())
+    for n, buf in m.named_buffers():
+        if n.rsplit(".", 1)[-1] in ("RMr", "RMi", "RVrr", "RVri", "RVii"):
+            np.testing.assert_allclose(buf.cpu().numpy(), bo[n].numpy(), rtol=2e-4, atol=2e-6, err_msg=n)
