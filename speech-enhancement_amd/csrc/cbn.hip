@@ -1184,11 +1184,12 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   if (fc) {   // (checked by the entry point: FRCRN's first conv, cin 1, kernel (5, 2); fp32)
     if constexpr (sizeof(T) == 4) {
       float* wpart = (float*)(((uintptr_t)ws + ws_bytes_ns(B, C, HW, 7) + 255) & ~(uintptr_t)255);
-      // SEHIP_FC_CPB = channels per workgroup (1: cbn_bwd_apply_fc_kernel; 2 / 4: the tap-sharing
-      // form; A/B knob)
+      // SEHIP_FC_CPB = channels per workgroup: 4 (default; the tap-sharing form), 2, or 1 (the
+      // one-channel cbn_bwd_apply_fc_kernel). Bit-identical; same box, FRCRN step: 635.5 / 635.0
+      // (4) vs 634.0 / 631.6 utt/s (1)
       const int cpb = [] {   // read per call (one host getenv per training step)
         const char* e = std::getenv("SEHIP_FC_CPB");
-        const int v = e ? std::atoi(e) : 1;
+        const int v = e ? std::atoi(e) : 4;
         return (v == 2 || v == 4) ? v : 1;
       }();
       const float* g1 = (const float*)gy;

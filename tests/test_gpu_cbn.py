@@ -375,15 +375,15 @@ def test_cbn_prelu_fused(dtype, tol, gpu_device):
 
 @pytest.mark.parametrize("cpb", ["2", "4"])
 def test_first_block_channel_blocked_bit_identical(cpb, gpu_device, monkeypatch):
-    """SEHIP_FC_CPB = 2 / 4 (the fused first-block backward over several channels per
-    workgroup, sharing each position's spectrum taps) against the one-channel form:
+    """SEHIP_FC_CPB = 2 / 4 (4 is the default: the fused first-block backward over several
+    channels per workgroup, sharing each position's spectrum taps) against the one-channel form:
     dWr / dWi and every CBN gradient bit for bit (same products, same order)."""
     from sehip import functional as F
     from sehip.complex_nn import ComplexBatchNorm2d, ComplexConv2d
     gen = torch.Generator().manual_seed(33)
     x = (torch.randn((2, 2, 320, 101), generator=gen) * 0.8).cuda()
     res = []
-    for v in ("1", cpb):
+    for v in ("1", cpb):   # SEHIP_FC_CPB=1: the one-channel form
         monkeypatch.setenv("SEHIP_FC_CPB", v)
         c = paramfill.fill_(ComplexConv2d(2, 128, (5, 2), stride=(2, 1), bias=False), seed=5).cuda()
         n = paramfill.fill_(ComplexBatchNorm2d(128), seed=6).cuda().train()
