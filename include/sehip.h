@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 4   /* 4: SE_DTYPE storage types (CBN), first-block fused backward, se_resample */
+#define SEHIP_ABI_VERSION 5   /* 5: prepared data-grad weight images (se_conv2d_prep_data_weights);
+                                 4: SE_DTYPE storage types (CBN), first-block fused backward, se_resample */
 
 enum {
   SE_OK = 0,
@@ -178,7 +179,25 @@ typedef struct se_conv2d_desc {
    * the joined / CL16 forms and the fp32-only small weight-grad shapes, before any
    * launch). fp32 storage takes any math. */
   int dtype;
+  /* ABI 5, se_conv2d_bwd_data / se_conv2d_bwd_data_joined only, optional: the
+   * pass's weight image (the per-class GEMM weight tiles and tap tables) already
+   * built by se_conv2d_prep_data_weights from the same weights with a desc equal
+   * in shape, math, dtype and w_amax. The pass then reads it instead of building
+   * it in ws. A training step makes it in the forward, where the small prep
+   * launch runs beside nothing, instead of in the backward, where it waits for CU
+   * slots behind the side stream's weight-grad GEMMs. NULL = build it in ws. */
+  const void* data_weights;
 } se_conv2d_desc;
+
+/* Bytes of the data-grad weight image of d (0 on an invalid desc). */
+size_t se_conv2d_data_weights_size(const se_conv2d_desc* d);
+/* Builds the data-grad weight image of (wr, wi) for d into img (see
+ * se_conv2d_desc.data_weights). SE_MATH_F16X3 bakes the w_amax bound into the
+ * image: d->w_amax must be set (SE_E_ARG otherwise) and the data pass must
+ * pass the same bound. Replaces nothing in the reference (its conv re-reads the
+ * module weights in each pass, complex_nn.py:52-65). */
+int se_conv2d_prep_data_weights(const se_conv2d_desc* d, const float* wr, const float* wi, void* img,
+                                size_t img_bytes, void* stream);
 
 /* SE_MATH_F16 (5): operands rounded to fp16 (exact for fp16 storage), one MFMA
  * term on v_mfma_f32_32x32x16_f16, fp32 accumulate, no scaling (the reference's

@@ -1117,6 +1117,7 @@ struct ConvGeom {
   const void* dy_packed;
   int accum;      // se_conv2d_desc.accumulate_dx
   int sd;         // se_conv2d_desc.dtype (SE_DTYPE_*)
+  const void* data_w;   // se_conv2d_desc.data_weights (data-grad weight image, or nullptr)
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -1136,6 +1137,7 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.dy_packed = d->dy_packed;
   g.accum = d->accumulate_dx;
   g.sd = d->dtype;
+  g.data_w = d->data_weights;
   if (g.accum != 0 && g.accum != 1) return SE_E_ARG;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16) return SE_E_ARG;
   if (g.sd < SE_DTYPE_F32 || g.sd > SE_DTYPE_F16) return SE_E_ARG;
@@ -1388,6 +1390,65 @@ static bool pk_pass_any(const ConvGeom& g, Pass pass) {
   return (pass == kFwd ? g.x_packed : g.dy_packed) != nullptr;
 }
 
+// The weight image of a gather pass: per stride-phase class the GEMM weight
+// tiles Wp (Kp x ldw, in the layout of the kernel the pass runs) and the tap
+// table ktab, laid out 256-byte aligned from base. Built by the pass itself in
+// its workspace, or ahead of it (data-grad pass: se_conv2d_prep_data_weights).
+struct ClassImage {
+  float* Wp;
+  int4* ktab;
+};
+
+static size_t class_images_bytes(const std::vector<ClassPlan>& cls, int ldw) {
+  size_t b = 256;
+  for (const auto& c : cls)
+    b += round_up((long long)c.Kp * ldw * kWpBytesPerElem, 256) + round_up((long long)c.Kp * sizeof(int4), 256);
+  return b;
+}
+
+// split kernels: channel-block-major K order where Cg allows (split_k)
+static int korder_blk(int Cg) { return (Cg % 32 == 0 && !env_flag_off("SEHIP_KORDER")) ? 32 : 0; }
+
+static void class_images(const ConvGeom& g, Pass pass, const std::vector<ClassPlan>& cls, int ldw,
+                         const WeightView& wv, const float* wamax, char* base, bool build, hipStream_t st,
+                         std::vector<ClassImage>& out) {
+  const int N = (pass == kFwd) ? g.Co : g.Ci;
+  const int Cg = (pass == kFwd) ? g.Ci : g.Co;
+  const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
+  const bool bf1 = g.math == SE_MATH_BF16 && bf16_tiles(N, g.math);
+  const bool h1 = g.math == SE_MATH_F16 && bf16_tiles(N, g.math);
+  const bool f16 = g.math == SE_MATH_F16X3 && N > 64;
+  const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1 || h1 || f16;
+  const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
+  const int kblk = korder_blk(Cg);
+  const int dg = pass == kData ? 1 : 0;
+  char* p = align256(base);
+  out.clear();
+  for (const auto& c : cls) {
+    ClassImage im;
+    im.Wp = (float*)p;
+    p = align256(p + (size_t)c.Kp * ldw * kWpBytesPerElem);
+    im.ktab = (int4*)p;
+    p = align256(p + (size_t)c.Kp * sizeof(int4));
+    out.push_back(im);
+    if (!build) continue;
+    const long long tot = (long long)c.Kp * ldw;
+    const dim3 grid((unsigned)std::min<long long>((tot + 255) / 256, 4096));
+    if (x6)
+      hipLaunchKernelGGL(prep_class_x6_kernel, grid, dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi,
+                         Wi, dg, kblk, (unsigned short*)im.Wp, im.ktab);
+    else if (f16 || h1)   // h1: fp16 planes, unscaled (no weight bound)
+      hipLaunchKernelGGL(prep_class_x3_kernel<true>, grid, dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128,
+                         Hi, Wi, dg, kblk, (unsigned short*)im.Wp, im.ktab, f16 ? wamax : nullptr);
+    else if (x3)
+      hipLaunchKernelGGL(prep_class_x3_kernel<false>, grid, dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128,
+                         Hi, Wi, dg, kblk, (unsigned short*)im.Wp, im.ktab, (const float*)nullptr);
+    else
+      hipLaunchKernelGGL(prep_class_kernel, grid, dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, dg,
+                         im.Wp, im.ktab);
+  }
+}
+
 static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const float* wr,
                          const float* wi, const float* bias_br, const float* bias_bi, float* Y,
                          void* ws, size_t ws_bytes, hipStream_t st, const JoinIO* jn = nullptr) {
@@ -1397,6 +1458,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
   const int Ho = (pass == kFwd) ? g.Ho : g.Hi, Wo = (pass == kFwd) ? g.Wo : g.Wi;
   if (ws_bytes < gather_ws_bytes(cls, N, g.math)) return SE_E_WORKSPACE;
+  // a prepared split-fp16 image carries the caller's weight bound, which the GEMM unscales by
+  if (pass == kData && g.data_w && g.math == SE_MATH_F16X3 && N > 64 && !g.w_amax) return SE_E_ARG;
   if (g.accum) {   // dx += result: the split kernels' plain epilogue only (checked before any launch)
     const bool split = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3) && N > 64;
     if (pass != kData || jn || !split || g.dy_packed) return SE_E_UNSUPPORTED;
@@ -1476,30 +1539,16 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     for (const auto& c : cls)
       if (!tu_of(c)) return SE_E_UNSUPPORTED;
   }
-  // split kernels: channel-block-major K order where Cg allows (split_k)
-  const int kblk = (Cg % 32 == 0 && !env_flag_off("SEHIP_KORDER")) ? 32 : 0;
-  for (const auto& c : cls) {
-    float* Wp = (float*)p;
-    p = align256(p + (size_t)c.Kp * ldw * kWpBytesPerElem);
-    int4* ktab = (int4*)p;
-    p = align256(p + (size_t)c.Kp * sizeof(int4));
-    const long long tot = (long long)c.Kp * ldw;
-    if (x6)
-      hipLaunchKernelGGL(prep_class_x6_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
-                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab);
-    else if (f16 || h1)   // h1: fp16 planes, unscaled (no weight bound)
-      hipLaunchKernelGGL(prep_class_x3_kernel<true>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
-                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, f16 ? wamax : nullptr);
-    else if (x3)
-      hipLaunchKernelGGL(prep_class_x3_kernel<false>, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
-                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw / 128, Hi, Wi,
-                         pass == kData ? 1 : 0, kblk, (unsigned short*)Wp, ktab, (const float*)nullptr);
-    else
-      hipLaunchKernelGGL(prep_class_kernel, dim3((unsigned)std::min<long long>((tot + 255) / 256, 4096)),
-                         dim3(256), 0, st, wv, c.taps, Cg, N, c.Kp, ldw, Hi, Wi, pass == kData ? 1 : 0,
-                         Wp, ktab);
+  const int kblk = korder_blk(Cg);
+  // the weight images: prepared by the caller (data-grad pass, desc.data_weights)
+  // or built here in ws
+  const bool have_img = pass == kData && g.data_w;
+  std::vector<ClassImage> img;
+  class_images(g, pass, cls, ldw, wv, wamax, have_img ? (char*)g.data_w : p, !have_img, st, img);
+  for (size_t ic = 0; ic < cls.size(); ++ic) {
+    const ClassPlan& c = cls[ic];
+    float* Wp = img[ic].Wp;
+    int4* ktab = img[ic].ktab;
     GatherArgs a{};
     a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.zero = zero; a.Y = Y;
     a.amax_a = amax_a; a.amax_w = wamax;
@@ -1747,6 +1796,29 @@ extern "C" int se_conv2d_fwd(const se_conv2d_desc* d, const float* x, const floa
   if (rc) return rc;
   if (!x || !wr || !y || !ws || (g.complex_w && !wi) || (g.complex_w && br && !bi)) return SE_E_ARG;
   return launch_gather(g, kFwd, x, wr, wi, br, bi, y, ws, ws_bytes, se::as_stream(stream));
+}
+
+extern "C" size_t se_conv2d_data_weights_size(const se_conv2d_desc* d) {
+  ConvGeom g;
+  if (geom_of(d, g)) return 0;
+  return class_images_bytes(plan_pass(g, kData), ldw_for(g.Ci, g.math));
+}
+
+extern "C" int se_conv2d_prep_data_weights(const se_conv2d_desc* d, const float* wr, const float* wi,
+                                           void* img, size_t img_bytes, void* stream) {
+  ConvGeom g;
+  int rc = geom_of(d, g);
+  if (rc) return rc;
+  if (!wr || !img || (g.complex_w && !wi)) return SE_E_ARG;
+  if (g.math == SE_MATH_F16X3 && g.Ci > 64 && !g.w_amax) return SE_E_ARG;
+  const auto cls = plan_pass(g, kData);
+  const int ldw = ldw_for(g.Ci, g.math);
+  if (img_bytes < class_images_bytes(cls, ldw)) return SE_E_WORKSPACE;
+  const WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w, g.sd};
+  std::vector<ClassImage> out;
+  class_images(g, kData, cls, ldw, wv, g.w_amax, (char*)img, true, se::as_stream(stream), out);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
 }
 
 extern "C" int se_conv2d_bwd_data(const se_conv2d_desc* d, const float* dy, const float* wr,

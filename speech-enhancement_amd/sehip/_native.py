@@ -39,7 +39,8 @@ class ConvDesc(ctypes.Structure):
         ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p),   # CL16 operands (or NULL)
         ("w_amax", c_void_p),   # SE_MATH_F16X3 bound of max |w| (or NULL)
         ("accumulate_dx", c_int),   # se_conv2d_bwd_data: dx += dL/dx (ABI 3)
-        ("dtype", c_int)]           # SE_DTYPE_* storage of the conv's tensors (ABI 4)
+        ("dtype", c_int),           # SE_DTYPE_* storage of the conv's tensors (ABI 4)
+        ("data_weights", c_void_p)]   # prepared data-grad weight image (or NULL, ABI 5)
 
 
 class FirstConvDesc(ctypes.Structure):
@@ -51,6 +52,7 @@ class FirstConvDesc(ctypes.Structure):
 
 
 _P = c_void_p
+ABI_VERSION = 5   # SEHIP_ABI_VERSION (include/sehip.h)
 CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
@@ -74,6 +76,8 @@ _SIGNATURES = {
     "se_float_to_pcm16": (c_int, [_P, ctypes.c_longlong, _P, _P]),
     "se_resample": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int, c_int, _P, c_int, _P]),
     "se_conv2d_workspace_size": (c_size_t, [_P]),
+    "se_conv2d_data_weights_size": (c_size_t, [_P]),
+    "se_conv2d_prep_data_weights": (c_int, [_P] * 4 + [c_size_t, _P]),
     "se_conv2d_fwd": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_weight": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
@@ -160,6 +164,10 @@ def lib() -> ctypes.CDLL:
                 continue
             f.restype = res
             f.argtypes = args
+        if "se_abi_version" not in MISSING and handle.se_abi_version() != ABI_VERSION:
+            # a stale build: the struct mirrors above would not match its layout
+            raise RuntimeError(f"sehip: {LIB_PATH} has ABI {handle.se_abi_version()}, this package "
+                               f"needs {ABI_VERSION}; rebuild it")
         _lib = handle
     return _lib
 

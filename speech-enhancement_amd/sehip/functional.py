@@ -419,6 +419,41 @@ def conv_desc(x_shape, out_channels, kernel, stride, padding, dilation, output_p
     return d
 
 
+def _prep_data_weights(d, wr, wi, wa):
+    """The data-grad weight image of a conv call (se_conv2d_desc.data_weights), built
+    in the forward right after the forward GEMM: (uint8 image tensor, data-pass math),
+    or None with SEHIP_DATA_PREP=0 or when a split-fp16 data pass has no shared weight
+    bound. In the backward the same small prep launch would wait for CU slots behind
+    the side stream's weight-grad GEMMs, stalling the main stream."""
+    if os.environ.get("SEHIP_DATA_PREP", "1") == "0":
+        return None
+    m = _pass_math("data", d)
+    if m == F16X3 and d.in_channels > 64 and wa is None:
+        return None
+    lib, fm = N.lib(), d.math
+    d.math = m
+    try:
+        nb = lib.se_conv2d_data_weights_size(N.ctypes.byref(d))
+        img = torch.empty(nb, dtype=torch.uint8, device=wr.device)
+        N.check(lib.se_conv2d_prep_data_weights(N.ctypes.byref(d), wr.data_ptr(), N.ptr(wi), img.data_ptr(), nb,
+                                                N.stream_of(wr)), "se_conv2d_prep_data_weights")
+    finally:
+        d.math = fm
+    return img, m
+
+
+DATA_IMG_CALLS = [0]   # data-grad passes that read a forward-built weight image (tests)
+
+
+def _data_weights_of(ctx, d) -> int | None:
+    """ctx's prepared data-grad image pointer if it matches the pass's math now."""
+    img = getattr(ctx, "data_img", None)
+    if img is None or img[1] != _pass_math("data", d):
+        return None
+    DATA_IMG_CALLS[0] += 1
+    return img[0].data_ptr()
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wr, wi, br, bi, geom):
@@ -451,6 +486,7 @@ class _Conv2d(torch.autograd.Function):
                        x.element_size() * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
         ctx.save_for_backward(x, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax, ctx.w_amax = d, nbytes, br is not None, xa, wa
+        ctx.data_img = _prep_data_weights(d, wr, wi, wa) if ctx.needs_input_grad[0] else None
         return y
 
     @staticmethod
@@ -471,11 +507,12 @@ class _Conv2d(torch.autograd.Function):
             dx = acc if acc is not None else torch.empty_like(x)
             FORK_ACC_CALLS[0] += acc is not None
             d.accumulate_dx = int(acc is not None)
+            d.data_weights = _data_weights_of(ctx, d)
             t0 = _TIMER.begin() if _TIMER else None
             N.check(lib.se_conv2d_bwd_data(_with_math(d, "data"), gy.data_ptr(), wr.data_ptr(), N.ptr(wi),
                                            dx.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(gy)),
                     "se_conv2d_bwd_data")
-            d.accumulate_dx = 0
+            d.accumulate_dx, d.data_weights, ctx.data_img = 0, None, None
             if t0 is not None:
                 _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
                            4.0 * (gy.numel() + dx.numel() + wr.numel() * (2 if wi is not None else 1)))
@@ -563,6 +600,8 @@ class _ConvJoined(torch.autograd.Function):
                        4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
         ctx.save_for_backward(x, s, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax, ctx.w_amax = d, nbytes, br is not None, xa, wa
+        ctx.data_img = (_prep_data_weights(d, wr, wi, wa) if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
+                        else None)
         return y
 
     @staticmethod
@@ -581,6 +620,7 @@ class _ConvJoined(torch.autograd.Function):
         gx = gs = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
             gx, gs = torch.empty_like(x), torch.empty_like(s)
+            d.data_weights = _data_weights_of(ctx, d)
             t0 = _TIMER.begin() if _TIMER else None
             rc = lib.se_conv2d_bwd_data_joined(_with_math(d, "data"), gy.data_ptr(), wr.data_ptr(), wi.data_ptr(),
                                                gx.data_ptr(), Fx, Tx, gs.data_ptr(), ws.data_ptr(), ws.numel(), st)
@@ -591,6 +631,7 @@ class _ConvJoined(torch.autograd.Function):
                 rc = lib.se_complex_join_bwd(dj.data_ptr(), gx.data_ptr(), x.shape[1], Fx, Tx, gs.data_ptr(),
                                              s.shape[1], d.in_h, d.in_w, d.batch, N.dtype_code(gy), st)
             N.check(rc, "se_conv2d_bwd_data_joined")
+            d.data_weights, ctx.data_img = None, None
             if t0 is not None:
                 _TIMER.end(_gemm_tag("data", d, joined=True), t0, _conv_flops(d),
                            4.0 * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))

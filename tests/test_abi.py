@@ -17,7 +17,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), f"libsehip.so does not export {s}"
     assert N.MISSING == []
-    assert lib.se_abi_version() == 4
+    assert lib.se_abi_version() == 5
 
 
 def test_strerror():
@@ -67,6 +67,22 @@ def test_conv_argument_errors_need_no_gpu():
     assert lib.se_conv2d_fwd(ctypes.byref(d), None, None, None, None, None, None, None, 0, None) == -1
     d = F.conv_desc((1, 4, 8, 8), 4, (9, 9), (1, 1), (1, 1), (1, 1), (0, 0), False, True)
     assert lib.se_conv2d_out_shape(ctypes.byref(d), None, None) == -3   # 81 taps > 64
+
+
+def test_data_weight_image_validation_needs_no_gpu():
+    """se_conv2d_prep_data_weights (ABI 5): sized per desc, and a split-fp16 image
+    needs the caller's weight bound (it is baked in) -- rejected before any launch."""
+    lib = N.lib()
+    d = F.conv_desc((2, 180, 80, 40), 180, (5, 2), (2, 1), (2, 0), (1, 1), (0, 0), False, True)
+    d.math = 4   # SE_MATH_F16X3, 180 input channels: the split tiles
+    nb = lib.se_conv2d_data_weights_size(ctypes.byref(d))
+    assert nb > 0
+    fake = ctypes.c_void_p(256)   # never dereferenced: the call returns before launching
+    assert lib.se_conv2d_prep_data_weights(ctypes.byref(d), fake, fake, fake, nb, None) == -1
+    assert lib.se_conv2d_prep_data_weights(ctypes.byref(d), None, fake, fake, nb, None) == -1
+    d.math = 0
+    assert lib.se_conv2d_prep_data_weights(ctypes.byref(d), fake, fake, fake, 16, None) == -5   # image too small
+    assert lib.se_conv2d_data_weights_size(None) == 0
 
 
 @pytest.mark.parametrize("L,win,hop,nfft,center", [
