@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 5   /* 5: prepared data-grad weight images (se_conv2d_prep_data_weights);
+#define SEHIP_ABI_VERSION 5   /* 5: prepared data-grad weight images (se_conv2d_prep_data_weights),
+                                 CBN moments from the conv forward (se_conv2d_desc.moments);
                                  4: SE_DTYPE storage types (CBN), first-block fused backward, se_resample */
 
 enum {
@@ -187,7 +188,21 @@ typedef struct se_conv2d_desc {
    * launch runs beside nothing, instead of in the backward, where it waits for CU
    * slots behind the side stream's weight-grad GEMMs. NULL = build it in ws. */
   const void* data_weights;
+  /* ABI 5, se_conv2d_fwd / se_conv2d_fwd_joined only, optional: a device buffer of
+   * se_conv2d_moments_rows(d) = P rows that receives the ComplexBatchNorm moments of
+   * the output y, so that a following se_cbn_fwd_moments / se_cbn_head_fwd_moments
+   * skips its pass over y. Layout: [N/2][P][5] double sums of (yr, yi, yr^2, yr yi,
+   * yi^2) per complex channel (columns c and c + N/2) and output M-tile, then
+   * [N/2][P][4] float extrema (max yr, -min yr, max yi, -min yi): N/2 * P * 56 bytes.
+   * Supported on the split-fp16 forward (SE_MATH_F16X3, fp32 storage, 64 < N <= 256,
+   * not CL16-packed); other cases return SE_E_UNSUPPORTED before launching. NULL = none.
+   * The reference computes these moments inside ComplexBatchNorm2d.forward
+   * (complex_nn.py:235-260). */
+  void* moments;
 } se_conv2d_desc;
+
+/* Rows P of the moments buffer of a forward pass (0 on an invalid desc). */
+int se_conv2d_moments_rows(const se_conv2d_desc* d);
 
 /* Bytes of the data-grad weight image of d (0 on an invalid desc). */
 size_t se_conv2d_data_weights_size(const se_conv2d_desc* d);
@@ -313,6 +328,15 @@ int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
                float momentum, int act, float slope, float* y_amax,
                const void* prelu_w, int dtype, void* ws, size_t ws_bytes, void* stream);
 
+/* ABI 5: the training forward of se_cbn_fwd (fp32 storage) from moment rows a
+ * producing conv already wrote (se_conv2d_desc.moments, P =
+ * se_conv2d_moments_rows of that conv): no pass over x for the statistics, only
+ * the finalize (running update, save, y_amax) and the apply. */
+int se_cbn_fwd_moments(const void* moments, int P, const float* x, float* y, int B, int C, int HW,
+                       const float* const* params, float* const* running, int64_t* nbt, float* save,
+                       float eps, float momentum, int act, float slope, float* y_amax,
+                       const float* prelu_w, void* stream);
+
 /* Backward. gy = dL/dy (after the activation), x = forward input. y (the
  * forward output) is NOT read and may be NULL: the activation derivative is
  * taken from the pre-activation Z(x - M) + B recomputed from x and `save`.
@@ -358,6 +382,13 @@ int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, int W,
                     float* save, int training, float eps, float momentum, int act,
                     float slope, const float* w_head, int out_channels, int kernel_w,
                     void* ws, size_t ws_bytes, void* stream);
+
+/* ABI 5: se_cbn_head_fwd in training from the producing conv's moment rows (as
+ * se_cbn_fwd_moments; no workspace). */
+int se_cbn_head_fwd_moments(const void* moments, int P, const float* x, float* out, int B, int C, int H, int W,
+                            const float* const* params, float* const* running, int64_t* nbt, float* save,
+                            float eps, float momentum, int act, float slope, const float* w_head,
+                            int out_channels, int kernel_w, void* stream);
 
 int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int B, int C, int H, int W,
                     const float* const* params, const float* save, float* const* dparams,

@@ -1027,19 +1027,23 @@ static double* pwpart_of(void* ws, int Cc, int P, int ns) {
 namespace {
 
 // moments + finalize of the training forward (running update, save, y bound)
+// pre: the moment rows a producer already wrote (se_conv2d_desc.moments: [Cc][preP][5]
+// fp64 sums, then [Cc][preP][4] extrema, the layout of part / ext), so no moments pass.
 template <typename T>
 int cbn_stats(const T* x, int B, int C, int HW, const void* const* params, void* const* running,
               int64_t* nbt, float* save, int training, float eps, float momentum, float* y_amax,
-              void* ws, hipStream_t st) {
+              void* ws, hipStream_t st, const void* pre = nullptr, int preP = 0) {
   const int Cc = C / 2;
-  const int P = pick_P(B, Cc, HW);
-  double* part = (double*)ws;
-  float* ext = ext_of(ws, Cc, P, 7);
+  const int P = pre ? preP : pick_P(B, Cc, HW);
+  double* part = pre ? (double*)pre : (double*)ws;
+  float* ext = pre ? (float*)(part + (size_t)Cc * P * 5) : ext_of(ws, Cc, P, 7);
   Ptr5 pp{};
   MPtr5 rp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (running) for (int k = 0; k < 5; ++k) rp.p[k] = running[k];
-  if (training) {
+  if (training && pre) {
+    if (y_amax && hipMemsetAsync(y_amax, 0, sizeof(float), st) != hipSuccess) return SE_E_LAUNCH;
+  } else if (training) {
     hipLaunchKernelGGL(cbn_moments_kernel<T>, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part, ext,
                        y_amax);
     SE_LAUNCH_CHECK();
@@ -1054,8 +1058,9 @@ int cbn_stats(const T* x, int B, int C, int HW, const void* const* params, void*
 template <typename T>
 int cbn_fwd_t(const T* x, T* y, int B, int C, int HW, const void* const* params, void* const* running,
               int64_t* nbt, float* save, int training, float eps, float momentum, int act, float slope,
-              float* y_amax, const T* pw, void* ws, hipStream_t st) {
-  const int rc = cbn_stats<T>(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st);
+              float* y_amax, const T* pw, void* ws, hipStream_t st, const void* pre = nullptr, int preP = 0) {
+  const int rc = cbn_stats<T>(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st,
+                              pre, preP);
   if (rc != SE_OK) return rc;
   int64_t* nb = (training && running) ? nbt : nullptr;
   const dim3 grid(se::ceil_div(HW, kThreads * 4), C / 2, B);
@@ -1095,21 +1100,55 @@ extern "C" int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
   }
 }
 
+extern "C" int se_cbn_fwd_moments(const void* moments, int P, const float* x, float* y, int B, int C, int HW,
+                                  const float* const* params, float* const* running, int64_t* nbt, float* save,
+                                  float eps, float momentum, int act, float slope, float* y_amax,
+                                  const float* prelu_w, void* stream) {
+  if (!moments || P <= 0 || !x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || !act_ok(act, prelu_w))
+    return SE_E_ARG;
+  return cbn_fwd_t<float>(x, y, B, C, HW, (const void* const*)params, (void* const*)running, nbt, save, 1, eps,
+                          momentum, act, slope, y_amax, prelu_w, nullptr, se::as_stream(stream), moments, P);
+}
+
+static int cbn_head_fwd_impl(const void* pre, int preP, const float* x, float* out, int B, int C, int H, int W,
+                             const float* const* params, float* const* running, int64_t* nbt,
+                             float* save, int training, float eps, float momentum, int act,
+                             float slope, const float* w_head, int out_channels, int kernel_w,
+                             void* ws, size_t ws_bytes, void* stream);
+
+extern "C" int se_cbn_head_fwd_moments(const void* moments, int P, const float* x, float* out, int B, int C, int H,
+                                       int W, const float* const* params, float* const* running, int64_t* nbt,
+                                       float* save, float eps, float momentum, int act, float slope,
+                                       const float* w_head, int out_channels, int kernel_w, void* stream) {
+  if (!moments || P <= 0) return SE_E_ARG;
+  return cbn_head_fwd_impl(moments, P, x, out, B, C, H, W, params, running, nbt, save, 1, eps, momentum, act, slope,
+                           w_head, out_channels, kernel_w, nullptr, 0, stream);
+}
+
 extern "C" int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, int W,
                                const float* const* params, float* const* running, int64_t* nbt,
                                float* save, int training, float eps, float momentum, int act,
                                float slope, const float* w_head, int out_channels, int kernel_w,
                                void* ws, size_t ws_bytes, void* stream) {
+  return cbn_head_fwd_impl(nullptr, 0, x, out, B, C, H, W, params, running, nbt, save, training, eps, momentum, act,
+                           slope, w_head, out_channels, kernel_w, ws, ws_bytes, stream);
+}
+
+static int cbn_head_fwd_impl(const void* pre, int preP, const float* x, float* out, int B, int C, int H, int W,
+                             const float* const* params, float* const* running, int64_t* nbt,
+                             float* save, int training, float eps, float momentum, int act,
+                             float slope, const float* w_head, int out_channels, int kernel_w,
+                             void* ws, size_t ws_bytes, void* stream) {
   if (!x || !out || !save || !w_head || B <= 0 || C <= 0 || (C & 1) || H <= 0 || W < 2 || act < 0 || act > 2)
     return SE_E_ARG;
   if (out_channels != kHeadNO || kernel_w != kHeadKW) return SE_E_UNSUPPORTED;
   if ((long long)H * W >= (1LL << 31)) return SE_E_UNSUPPORTED;
   if (!training && !running) return SE_E_ARG;
   const int HW = H * W;
-  if (ws_bytes < se_cbn_head_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
+  if (!pre && (ws_bytes < se_cbn_head_workspace_size(B, C, HW) || !ws)) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
   const int rc = cbn_stats<float>(x, B, C, HW, (const void* const*)params, (void* const*)running, nbt, save,
-                                  training, eps, momentum, nullptr, ws, st);
+                                  training, eps, momentum, nullptr, ws, st, pre, preP);
   if (rc != SE_OK) return rc;
   const long long waves = (long long)B * ((HW + 62) / 63);
   const size_t lds = ((size_t)(C / 2) * 8 + (size_t)kHeadNO * C * kHeadKW) * sizeof(float);

@@ -186,6 +186,11 @@ struct GatherArgs {
   // channel n' - mrg_np of output row 1 + Sh * qh (rows >= Ho dropped); 0 = off
   int mrg_np;
   int accum;           // data-grad: Y += result (se_conv2d_desc.accumulate_dx)
+  // forward, se_conv2d_desc.moments: the CBN moment rows of each M-tile (rows
+  // mom_p0 + tile of mom_P; [N/2][mom_P][5] fp64 sums, then [N/2][mom_P][4] extrema)
+  double* mom;
+  float* mom_ext;
+  int mom_p0, mom_P;
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -1118,6 +1123,7 @@ struct ConvGeom {
   int accum;      // se_conv2d_desc.accumulate_dx
   int sd;         // se_conv2d_desc.dtype (SE_DTYPE_*)
   const void* data_w;   // se_conv2d_desc.data_weights (data-grad weight image, or nullptr)
+  void* mom;            // se_conv2d_desc.moments (forward CBN moment rows, or nullptr)
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -1138,6 +1144,7 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.accum = d->accumulate_dx;
   g.sd = d->dtype;
   g.data_w = d->data_weights;
+  g.mom = d->moments;
   if (g.accum != 0 && g.accum != 1) return SE_E_ARG;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16) return SE_E_ARG;
   if (g.sd < SE_DTYPE_F32 || g.sd > SE_DTYPE_F16) return SE_E_ARG;
@@ -1406,6 +1413,13 @@ static size_t class_images_bytes(const std::vector<ClassPlan>& cls, int ldw) {
   return b;
 }
 
+// CBN moment rows of a forward pass (se_conv2d_desc.moments): one per 128-position M-tile of each class
+static int moment_rows(const std::vector<ClassPlan>& cls, int B) {
+  long long r = 0;
+  for (const auto& c : cls) r += se::ceil_div((long long)B * c.h.Q * c.w.Q, (long long)kX3BM);
+  return r > INT32_MAX ? 0 : (int)r;
+}
+
 // split kernels: channel-block-major K order where Cg allows (split_k)
 static int korder_blk(int Cg) { return (Cg % 32 == 0 && !env_flag_off("SEHIP_KORDER")) ? 32 : 0; }
 
@@ -1468,7 +1482,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   {   // stride-phase classes merged along the columns (split-fp16, 256-column tiles)
     ClassPlan mp;
     const bool pk_in = (pass == kFwd ? g.x_packed : g.dy_packed) != nullptr;
-    if (pass == kFwd && g.transposed && g.math == SE_MATH_F16X3 && N > 64 && ldw == 128 && !pk_in &&
+    if (pass == kFwd && !g.mom && g.transposed && g.math == SE_MATH_F16X3 && N > 64 && ldw == 128 && !pk_in &&
         gemm_nw() == 2 && gemm_bm() != 256 && !gemm_pp() && fwd_merge_on() && merge_h_phases(cls, Cg, mp) &&
         ws_bytes >= gather_ws_bytes({mp}, 256)) {
       cls.assign(1, mp);
@@ -1477,6 +1491,15 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   }
   WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w, g.sd};
   if (g.sd != SE_DTYPE_F32 && (jn || pk_pass_any(g, pass))) return SE_E_UNSUPPORTED;   // fp32-only forms
+  if (g.mom) {   // CBN moments in the forward epilogue: one column tile of the split-fp16 kernel
+    const int bn = (ldw % 256 == 0 && gemm_nw() == 2) ? 256 : 128;
+    const bool ok = pass == kFwd && g.sd == SE_DTYPE_F32 && g.math == SE_MATH_F16X3 && N > 64 && !(N & 1) &&
+                    N <= bn && ldw == bn && !g.x_packed && gemm_bm() != 256 && !gemm_pp() && !SEHIP_GEMM_M16 &&
+                    !(jn && jn->y2);
+    if (!ok) return SE_E_UNSUPPORTED;
+  }
+  const int mom_P = g.mom ? moment_rows(cls, g.B) : 0;
+  int mom_p0 = 0;
 
   char* p = align256((char*)ws);
   const float* zero = zero_page();
@@ -1557,6 +1580,13 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
     a.mrg_np = c.mrg ? c.taps.mrg_np : 0;
     a.accum = g.accum;
+    if (g.mom) {
+      a.mom = (double*)g.mom;
+      a.mom_ext = (float*)(a.mom + (size_t)(N / 2) * mom_P * 5);
+      a.mom_P = mom_P;
+      a.mom_p0 = mom_p0;
+      mom_p0 += (int)se::ceil_div((long long)g.B * c.h.Q * c.w.Q, (long long)kX3BM);
+    }
     if (jn) {
       a.X2 = jn->x2; a.jh = jn->jh; a.H2 = jn->h2; a.W2 = jn->w2;
       a.Y2 = jn->y2; a.yjh = jn->yjh; a.YH2 = jn->yh2; a.YW2 = jn->yw2;
@@ -1796,6 +1826,12 @@ extern "C" int se_conv2d_fwd(const se_conv2d_desc* d, const float* x, const floa
   if (rc) return rc;
   if (!x || !wr || !y || !ws || (g.complex_w && !wi) || (g.complex_w && br && !bi)) return SE_E_ARG;
   return launch_gather(g, kFwd, x, wr, wi, br, bi, y, ws, ws_bytes, se::as_stream(stream));
+}
+
+extern "C" int se_conv2d_moments_rows(const se_conv2d_desc* d) {
+  ConvGeom g;
+  if (geom_of(d, g)) return 0;
+  return moment_rows(plan_pass(g, kFwd), g.B);
 }
 
 extern "C" size_t se_conv2d_data_weights_size(const se_conv2d_desc* d) {

@@ -656,6 +656,87 @@ gather_x3_kernel(const GatherArgs a) {
         }
       }
   }
+
+  // --- ComplexBatchNorm moments of this tile (se_conv2d_desc.moments) ---
+  // The output y = acc + bias of complex channel cc is columns cc (re) and
+  // cc + N/2 (im), both inside this tile (N <= BN, checked by the host). Per
+  // channel, over the tile's valid positions: the fp64 sums of yr, yi, yr^2,
+  // yr yi, yi^2 and the extrema max yr, -min yr, max yi, -min yi -- the row
+  // cbn_moments_kernel writes per partition, here partition mom_p0 + (M-tile).
+  // The CBN forward then skips its pass over y (se_cbn_fwd_moments).
+  // The tile goes through LDS in rounds of RQ positions ([RQ][BN + 4] fp32,
+  // in the dead sA stages); THR / Cc threads share a channel, their partial
+  // sums are added in a fixed order (deterministic).
+  if constexpr (SD == 0 && JM != 2 && BMX == 1 && !PP && !M16) {
+    if (a.mom) {
+      constexpr int RQ = 32 / NW, LDT = BN + 4;
+      float* T = reinterpret_cast<float*>(&sA[0][0]);
+      const int Cc = a.N >> 1;
+      const int tpc = THR / Cc;                     // threads per channel
+      const int cc = tid % Cc, r0 = tid / Cc;
+      const bool red = r0 < tpc;
+      double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+      float e[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+      for (int w = 0; w < WM; ++w)
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+#pragma unroll
+          for (int h = 0; h < NW; ++h) {
+            __syncthreads();
+            if (wm == w && lr / RQ == h) {   // the lanes of positions h RQ .. h RQ + RQ - 1 of block j
+#pragma unroll
+              for (int i = 0; i < RN; ++i)
+#pragma unroll
+                for (int g4 = 0; g4 < 4; ++g4) {
+                  const int nl = wn * TN + 32 * i + 4 * lh + 8 * g4;
+                  float4 q;
+                  q.x = acc[i][j][4 * g4 + 0] + sBias[nl + 0];
+                  q.y = acc[i][j][4 * g4 + 1] + sBias[nl + 1];
+                  q.z = acc[i][j][4 * g4 + 2] + sBias[nl + 2];
+                  q.w = acc[i][j][4 * g4 + 3] + sBias[nl + 3];
+                  *reinterpret_cast<float4*>(T + (lr - h * RQ) * LDT + nl) = q;
+                }
+            }
+            __syncthreads();
+            if (red) {
+              const int mb = m0 + w * TM + 32 * j + h * RQ;
+              for (int r = r0; r < RQ; r += tpc) {
+                if (mb + r >= a.M) break;
+                const float fr = T[r * LDT + cc], fm = T[r * LDT + cc + Cc];
+                e[0] = fmaxf(e[0], fr); e[1] = fmaxf(e[1], -fr); e[2] = fmaxf(e[2], fm); e[3] = fmaxf(e[3], -fm);
+                const double dr = fr, dm = fm;
+                v[0] += dr; v[1] += dm; v[2] += dr * dr; v[3] += dr * dm; v[4] += dm * dm;
+              }
+            }
+          }
+      __syncthreads();
+      double* R = reinterpret_cast<double*>(&sA[0][0]);   // [tpc][Cc][5], then [tpc][Cc][4] extrema
+      float* E = reinterpret_cast<float*>(R + (long long)THR * 5);
+      if (red) {
+#pragma unroll
+        for (int k = 0; k < 5; ++k) R[(r0 * Cc + cc) * 5 + k] = v[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) E[(r0 * Cc + cc) * 4 + k] = e[k];
+      }
+      __syncthreads();
+      if (tid < Cc) {
+        const long long row = (long long)tid * a.mom_P + a.mom_p0 + mt;
+        double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+        float x4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+        for (int t = 0; t < tpc; ++t) {
+#pragma unroll
+          for (int k = 0; k < 5; ++k) s[k] += R[(t * Cc + tid) * 5 + k];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) x4[k] = fmaxf(x4[k], E[(t * Cc + tid) * 4 + k]);
+        }
+#pragma unroll
+        for (int k = 0; k < 5; ++k) a.mom[row * 5 + k] = s[k];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) a.mom_ext[row * 4 + k] = x4[k];
+      }
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------

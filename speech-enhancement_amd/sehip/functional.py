@@ -240,6 +240,57 @@ def amax_of(t: torch.Tensor) -> torch.Tensor:
 
 
 # --------------------------------------------------------------------------
+# ComplexBatchNorm moments from the producing conv (se_conv2d_desc.moments, ABI 5).
+# A block whose training-mode CBN reads the conv output directly (FRCRN / DCCRN
+# encoder and decoder blocks, emit_moments) has the conv's split-fp16 forward GEMM
+# write the per-tile moment rows of its output in the epilogue; the CBN forward then
+# runs only its finalize and apply (se_cbn_fwd_moments / se_cbn_head_fwd_moments)
+# instead of its own pass over the tensor. SEHIP_CONV_MOMENTS=0 turns it off.
+# --------------------------------------------------------------------------
+_MOM: dict = {}
+_EMIT = [False]
+MOMENT_CALLS = [0, 0]   # [convs that wrote moment rows, CBN forwards that read them] (tests)
+
+
+@contextlib.contextmanager
+def emit_moments(on: bool = True):
+    """Convs run inside write the CBN moment rows of their output where their
+    forward kernel supports it (se_conv2d_moments_rows)."""
+    prev = _EMIT[0]
+    _EMIT[0] = bool(on) and os.environ.get("SEHIP_CONV_MOMENTS", "1") != "0"
+    try:
+        yield
+    finally:
+        _EMIT[0] = prev
+
+
+def _moments_for(d, x):
+    """(uint8 buffer, rows) for the forward pass of d, or None."""
+    if not (_EMIT[0] and x.dtype == torch.float32 and d.complex_weights and 64 < d.out_channels <= 256
+            and _pass_math("fwd", d) == F16X3 and not getattr(d, "exact", False)):
+        return None
+    rows = N.lib().se_conv2d_moments_rows(N.ctypes.byref(d))
+    if rows <= 0:
+        return None
+    return torch.empty(d.out_channels // 2 * rows * 56, dtype=torch.uint8, device=x.device), rows
+
+
+def moments_put(t: torch.Tensor, buf: torch.Tensor, rows: int) -> None:
+    for k in [k for k, e in _MOM.items() if e[2].expired()]:
+        del _MOM[k]
+    _MOM[t.data_ptr()] = (buf, rows, StorageWeakRef(t.untyped_storage()), tuple(t.shape), t._version)
+    MOMENT_CALLS[0] += 1
+
+
+def moments_take(t: torch.Tensor):
+    """The moment rows registered for t (and still describing it), removed from the table."""
+    e = _MOM.pop(t.data_ptr(), None)
+    if e is None or e[2].expired() or e[3] != tuple(t.shape) or e[4] != t._version:
+        return None
+    return e[0], e[1]
+
+
+# --------------------------------------------------------------------------
 # Forked outputs (ComplexBN fork=True: an FRCRN encoder block output feeding the
 # next block and a decoder skip). The skip consumer's backward (CCBAM) runs
 # first, during the decoder's backward; it hands its input gradient over here
@@ -478,9 +529,18 @@ class _Conv2d(torch.autograd.Function):
         wa = _weight_amax(d, wr, wi)
         d.w_amax = N.ptr(wa)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(lib.se_conv2d_fwd(_with_math(d, "fwd"), x.data_ptr(), wr.data_ptr(), N.ptr(wi),
-                                  N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(),
-                                  N.stream_of(x)), "se_conv2d_fwd")
+        mb = _moments_for(d, x)
+        while True:
+            d.moments = mb[0].data_ptr() if mb is not None else None
+            rc = lib.se_conv2d_fwd(_with_math(d, "fwd"), x.data_ptr(), wr.data_ptr(), N.ptr(wi),
+                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(x))
+            if rc != SE_E_UNSUPPORTED or mb is None:
+                break
+            mb = None   # no moments epilogue for this shape / mode: the CBN runs its own pass
+        d.moments = None
+        N.check(rc, "se_conv2d_fwd")
+        if mb is not None:
+            moments_put(y, *mb)
         if t0 is not None:   # bytes: x read + y written + the weights, once
             _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
                        x.element_size() * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
@@ -588,13 +648,22 @@ class _ConvJoined(torch.autograd.Function):
         wa = _weight_amax(d, wr, wi)
         d.w_amax = N.ptr(wa)
         t0 = _TIMER.begin() if _TIMER else None
-        rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
-                                      wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(),
-                                      ws.numel(), st)
-        if rc == SE_E_UNSUPPORTED:
-            rc = lib.se_conv2d_fwd(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), wr.data_ptr(), wi.data_ptr(),
-                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
+        mb = _moments_for(d, x)
+        while True:
+            d.moments = mb[0].data_ptr() if mb is not None else None
+            rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
+                                          wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(),
+                                          ws.numel(), st)
+            if rc == SE_E_UNSUPPORTED:
+                rc = lib.se_conv2d_fwd(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), wr.data_ptr(), wi.data_ptr(),
+                                       N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
+            if rc != SE_E_UNSUPPORTED or mb is None:
+                break
+            mb = None
+        d.moments = None
         N.check(rc, "se_conv2d_fwd_joined")
+        if mb is not None:
+            moments_put(y, *mb)
         if t0 is not None:
             _TIMER.end(_gemm_tag("fwd", d, joined=True), t0, _conv_flops(d),
                        4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
@@ -749,16 +818,25 @@ class _ComplexBN(torch.autograd.Function):
         # bound of max |y| for an f16x3 consumer (fp32 storage only)
         ya = new_amax(x.device) if training and dt == 0 else None
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
-                               N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
-                               save.data_ptr(), int(training), float(eps), mom, int(act),
-                               float(slope), N.ptr(ya), N.ptr(prelu), dt, ws.data_ptr(), ws.numel(),
-                               N.stream_of(x)),
-                "se_cbn_fwd")
+        pre = moments_take(x) if training and dt == 0 else None
+        if pre is not None:   # the producing conv wrote the moment rows (emit_moments)
+            N.check(lib.se_cbn_fwd_moments(pre[0].data_ptr(), pre[1], x.data_ptr(), y.data_ptr(), b, c, hw,
+                                           N.ptr_array(params), N.ptr_array(running), N.ptr(nbt), save.data_ptr(),
+                                           float(eps), mom, int(act), float(slope), N.ptr(ya), N.ptr(prelu),
+                                           N.stream_of(x)), "se_cbn_fwd_moments")
+            MOMENT_CALLS[1] += 1
+        else:
+            N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
+                                   N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
+                                   save.data_ptr(), int(training), float(eps), mom, int(act),
+                                   float(slope), N.ptr(ya), N.ptr(prelu), dt, ws.data_ptr(), ws.numel(),
+                                   N.stream_of(x)),
+                    "se_cbn_fwd")
         if ya is not None:
             amax_put(y, ya)
-        if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write
-            _TIMER.end("cbn_fwd", t0, 0.0, x.element_size() * x.numel() * (3 if training else 2))
+        if t0 is not None:   # 1 read for the moments (training, unless the conv wrote them) + 1 read + 1 write
+            _TIMER.end("cbn_fwd", t0, 0.0,
+                       x.element_size() * x.numel() * (3 if training and pre is None else 2))
         ctx.save_for_backward(x, save, prelu, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         if fork:   # (y, alias of y): two consumers, two gradients summed inside se_cbn_bwd2
@@ -944,13 +1022,23 @@ class _ComplexBNHead(torch.autograd.Function):
         ws = _workspace(lib.se_cbn_head_workspace_size(b, c, h * w), x.device)
         mom = -1.0 if momentum is None else float(momentum)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(lib.se_cbn_head_fwd(x.data_ptr(), out.data_ptr(), b, c, h, w,
-                                    N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
-                                    save.data_ptr(), int(training), float(eps), mom, int(act),
-                                    float(slope), w_head.data_ptr(), w_head.shape[0], w_head.shape[3],
-                                    ws.data_ptr(), ws.numel(), N.stream_of(x)), "se_cbn_head_fwd")
-        if t0 is not None:   # (1 read for the moments in training) + 1 read + the head's write
-            _TIMER.end("cbn_head_fwd", t0, 0.0, 4.0 * (x.numel() * (2 if training else 1) + out.numel()))
+        pre = moments_take(x) if training else None
+        if pre is not None:   # the producing conv wrote the moment rows (emit_moments)
+            N.check(lib.se_cbn_head_fwd_moments(pre[0].data_ptr(), pre[1], x.data_ptr(), out.data_ptr(), b, c, h, w,
+                                                N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
+                                                save.data_ptr(), float(eps), mom, int(act), float(slope),
+                                                w_head.data_ptr(), w_head.shape[0], w_head.shape[3],
+                                                N.stream_of(x)), "se_cbn_head_fwd_moments")
+            MOMENT_CALLS[1] += 1
+        else:
+            N.check(lib.se_cbn_head_fwd(x.data_ptr(), out.data_ptr(), b, c, h, w,
+                                        N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
+                                        save.data_ptr(), int(training), float(eps), mom, int(act),
+                                        float(slope), w_head.data_ptr(), w_head.shape[0], w_head.shape[3],
+                                        ws.data_ptr(), ws.numel(), N.stream_of(x)), "se_cbn_head_fwd")
+        if t0 is not None:   # (1 read for the moments in training, unless the conv wrote them) + 1 read + write
+            _TIMER.end("cbn_head_fwd", t0, 0.0,
+                       4.0 * (x.numel() * (2 if training and pre is None else 1) + out.numel()))
         ctx.save_for_backward(x, save, w_head, *(params or ()))
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         return out

@@ -16,7 +16,7 @@ import torch.nn.functional as TF
 
 from ..ccbam import CCBAM
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLSTM,
-                          complex_concat, mark_data_fed, norm_act, real_conv2d)
+                          cbn_reads_conv, complex_concat, mark_data_fed, norm_act, real_conv2d)
 from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
 
@@ -65,7 +65,8 @@ class _CausalConvBase(nn.Module):
         elif not lp:
             pad = None
         # the time pad of a plain conv is folded into its (asymmetric) padding
-        y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
+        with F.emit_moments(cbn_reads_conv(self.norm)):
+            y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
         return norm_act(self.norm, self.act, y, fork)
 
     def _first_block(self, x, conv, input_pad, fork):
@@ -97,7 +98,9 @@ class _CausalConvBase(nn.Module):
         if self.padding[1] or not isinstance(conv, (ComplexConv2d, ComplexConvTranspose2d)) \
                 or x.shape[1] != skip.shape[1]:
             return self(F.complex_join(x, skip))
-        return norm_act(self.norm, self.act, conv.forward_joined(x, skip))
+        with F.emit_moments(cbn_reads_conv(self.norm)):
+            y = conv.forward_joined(x, skip)
+        return norm_act(self.norm, self.act, y)
 
     def forward_joined_head(self, x, skip, head: nn.Conv2d):
         """head(self(complex_join(x, skip))) for FRCRN's final_conv (frcrn.py:115, 140):
@@ -115,7 +118,8 @@ class _CausalConvBase(nn.Module):
                    and head.groups == 1)
         if not fusable:
             return real_conv2d(head, self.forward_joined(x, skip))
-        y = conv.forward_joined(x, skip)
+        with F.emit_moments(cbn_reads_conv(self.norm)):
+            y = conv.forward_joined(x, skip)
         if w.shape[1] != y.shape[1]:
             raise ValueError(f"head takes {w.shape[1]} channels, the block gives {y.shape[1]}")
         n = self.norm
