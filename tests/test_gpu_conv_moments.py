@@ -16,6 +16,11 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+
+@pytest.fixture(autouse=True)
+def _moments_on(monkeypatch):
+    monkeypatch.setenv("SEHIP_CONV_MOMENTS", "1")   # opt-in path (off by default)
+
 GEOMS = [   # (x shape, out channels, kernel, stride, padding, transposed)
     ((2, 128, 33, 37), 128, (5, 2), (2, 1), (2, 0), False),    # FRCRN encoder conv: 4-wave tiles, M tail
     ((2, 128, 17, 37), 128, (5, 2), (2, 1), (2, 0), True),     # decoder convT: two stride-phase classes
@@ -114,11 +119,13 @@ def test_cbn_forward_from_conv_moments(gpu_device, act):
     wi = torch.randn(64, 64, 5, 2, device=gpu_device) * 0.05
     kw = dict(out_channels=128, kernel=(5, 2), stride=(2, 1), padding=(2, 0))
     outs = []
+    bn0 = ComplexBatchNorm2d(128).to(gpu_device).train()   # Wri is drawn at random: one state for both runs
+    with torch.no_grad():
+        bn0.Wrr.add_(0.3)
+        bn0.Br.add_(0.1)
     for emit in (True, False):
         bn = ComplexBatchNorm2d(128).to(gpu_device).train()
-        with torch.no_grad():
-            bn.Wrr.add_(0.3)
-            bn.Br.add_(0.1)
+        bn.load_state_dict(bn0.state_dict())
         xa = x.clone().requires_grad_(True)
         n1 = F.MOMENT_CALLS[1]
         with F.emit_moments(emit):
@@ -136,7 +143,7 @@ def test_cbn_forward_from_conv_moments(gpu_device, act):
 
 
 def test_frcrn_step_with_conv_moments(gpu_device, monkeypatch):
-    """FRCRN forward + backward with the epilogue moments (default) against
+    """FRCRN forward + backward with the epilogue moments (SEHIP_CONV_MOMENTS=1) against
     SEHIP_CONV_MOMENTS=0: every CBN fed by a split-fp16 conv (encoder blocks 1-5, the
     decoder blocks and the fused head) reads moment rows, every row written is read,
     and the output and gradients agree."""
