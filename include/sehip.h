@@ -28,7 +28,8 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 5   /* 5: prepared data-grad weight images (se_conv2d_prep_data_weights),
+#define SEHIP_ABI_VERSION 6   /* 6: LSTM layer GEMMs (se_gemm, se_colsum);
+                                 5: prepared data-grad weight images (se_conv2d_prep_data_weights),
                                  CBN moments from the conv forward (se_conv2d_desc.moments);
                                  4: SE_DTYPE storage types (CBN), first-block fused backward, se_resample */
 
@@ -447,6 +448,38 @@ int se_lstm_fwd(const float* xproj, long long x_lstm_stride, int x_row_stride,
 int se_lstm_bwd(const float* dy, const float* w_hh, const float* gates,
                 const float* c, float* dgates, int L, int B, int T, int H,
                 unsigned rev_mask, void* stream);
+
+/* The LSTM layer GEMMs (ABI 6; replace the torch.addmm / bmm calls that the
+ * nn.LSTM input projection and weight / input gradients ran on rocBLAS):
+ *   C[b](m, n) = sum_k A(b, m, k) B(b, k, n) (+ bias0[b sbias + n] + bias1[...])
+ *   A(b, m, k) = A[b stride_a + m lda + k] (a_mcontig 0) | A[b stride_a + k lda + m] (1)
+ *   B(b, k, n) = B[b stride_b + n ldb + k] (b_ncontig 0) | B[b stride_b + k ldb + n] (1)
+ *   C[b](m, n) at C[b stride_c + m ldc + n]; sum_batches = 1: one C, the sum of
+ *   the batch products (in batch order, inside the accumulation).
+ * A(m, k) reads as 0 where k % kmask_period == kmask_phase (period 0: none).
+ * Arithmetic: scaled split-fp16 (f16x3, as SE_MATH_F16X3) with per-tensor
+ * power-of-two scales from amax_a / amax_b (device fp32 upper bounds of max |A|,
+ * max |B|). splits: split-K slabs (0: the library picks from the shape); with
+ * more than one the workspace holds the fp32 slabs, added in split order.
+ * se_colsum: out[l][g] = sum_r x[l][r][g] (the LSTM bias gradient; 64 row chunks,
+ * each in row order, then the chunks in order) and, if amax is not NULL, max |x|
+ * into *amax (the scale source of the weight-gradient GEMMs over x). */
+typedef struct se_gemm_desc {
+  int M, N, K;
+  int batches, sum_batches;
+  int a_mcontig, b_ncontig;
+  int lda, ldb, ldc;
+  long long stride_a, stride_b, stride_c, stride_bias;
+  int kmask_period, kmask_phase;
+  int splits;
+} se_gemm_desc;
+size_t se_gemm_workspace_size(const se_gemm_desc* d);
+int se_gemm(const se_gemm_desc* d, const float* A, const float* B, float* C, const float* bias0,
+            const float* bias1, const float* amax_a, const float* amax_b, void* ws, size_t ws_bytes,
+            void* stream);
+size_t se_colsum_workspace_size(int L, long long R, int G);
+int se_colsum(const float* x, int L, long long R, int G, float* out, float* amax, void* ws, size_t ws_bytes,
+              void* stream);
 
 /* Wide hidden sizes, H in {256, 512, 1024} (CARN's nn.LSTM(512), models/
  * _2104_05267_carn.py:132; CRN's nn.LSTM(1024), models/_1809_01405_crn.py:90;

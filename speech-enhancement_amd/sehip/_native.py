@@ -52,8 +52,17 @@ class FirstConvDesc(ctypes.Structure):
         "dil_h", "dil_w")] + [("dwr", c_void_p), ("dwi", c_void_p)]
 
 
+class GemmDesc(ctypes.Structure):
+    """Mirror of se_gemm_desc (include/sehip.h, ABI 6)."""
+
+    _fields_ = [(n, c_int) for n in ("M", "N", "K", "batches", "sum_batches", "a_mcontig", "b_ncontig",
+                                     "lda", "ldb", "ldc")] + [
+        (n, ctypes.c_longlong) for n in ("stride_a", "stride_b", "stride_c", "stride_bias")] + [
+        (n, c_int) for n in ("kmask_period", "kmask_phase", "splits")]
+
+
 _P = c_void_p
-ABI_VERSION = 5   # SEHIP_ABI_VERSION (include/sehip.h)
+ABI_VERSION = 6   # SEHIP_ABI_VERSION (include/sehip.h)
 CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
@@ -105,6 +114,10 @@ _SIGNATURES = {
                                 c_float, _P, c_int, c_int, _P, c_size_t, _P]),
     "se_cbn_head_bwd": (c_int, [_P, _P, _P] + [c_int] * 4 + [_PP, _P, _PP, _P, _P, c_int, c_int, c_int, c_int,
                                 c_float, _P, _P, c_size_t, _P]),
+    "se_gemm_workspace_size": (c_size_t, [_P]),
+    "se_gemm": (c_int, [_P] * 8 + [_P, c_size_t, _P]),
+    "se_colsum_workspace_size": (c_size_t, [c_int, ctypes.c_longlong, c_int]),
+    "se_colsum": (c_int, [_P, c_int, ctypes.c_longlong, c_int, _P, _P, _P, c_size_t, _P]),
     "se_lstm_supported": (c_int, [c_int]),
     "se_lstm_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P, _P] + [c_int] * 4
                     + [ctypes.c_uint, _P]),

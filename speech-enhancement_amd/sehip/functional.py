@@ -13,6 +13,7 @@ import torch
 from torch.multiprocessing.reductions import StorageWeakRef
 
 from . import _native as N
+_NAT = N
 
 
 def _pair(v):
@@ -1291,6 +1292,113 @@ def _wide(H: int) -> bool:
     return H in (256, 512, 1024)
 
 
+# --------------------------------------------------------------------------
+# The LSTM layer GEMMs (input projection, input gradient, weight gradients, bias
+# gradient) on se_gemm / se_colsum (csrc/gemm.hip: scaled split-fp16 MFMA, the
+# conv GEMMs' f16x3 arithmetic) instead of torch.addmm / bmm on rocBLAS.
+# SEHIP_LSTM_GEMM=torch runs them on torch (A/B measurement).
+# --------------------------------------------------------------------------
+_UNIT: dict = {}
+
+
+def _unit_bound(dev) -> torch.Tensor:
+    """fp32 [1] = 1.0: the bound of max |h| of an LSTM output (|o tanh(c)| < 1)."""
+    t = _UNIT.get(dev)
+    if t is None:
+        t = _UNIT[dev] = torch.ones(1, device=dev)
+    return t
+
+
+def lstm_gemm_hip() -> bool:
+    return os.environ.get("SEHIP_LSTM_GEMM", "hip") != "torch"
+
+
+def gemm(A, B, C, *, M, N, K, lda, ldb, ldc, amax_a, amax_b, a_mcontig=False, b_ncontig=False, batches=1,
+         sum_batches=False, stride_a=0, stride_b=0, stride_c=0, bias0=None, bias1=None, stride_bias=0,
+         kmask=(0, 0)):
+    """C[b](m, n) = sum_k A(b, m, k) B(b, k, n) (+ bias0 + bias1) on se_gemm
+    (include/sehip.h): A, B, C are fp32 device tensors addressed from their
+    data_ptr with the given leading dimensions and batch strides."""
+    nat = _NAT   # (N is the column count here)
+    d = nat.GemmDesc(M=M, N=N, K=K, batches=batches, sum_batches=int(sum_batches), a_mcontig=int(a_mcontig),
+                   b_ncontig=int(b_ncontig), lda=lda, ldb=ldb, ldc=ldc, stride_a=stride_a, stride_b=stride_b,
+                   stride_c=stride_c, stride_bias=stride_bias, kmask_period=kmask[0], kmask_phase=kmask[1],
+                   splits=0)
+    lib = nat.lib()
+    ws = _workspace(lib.se_gemm_workspace_size(nat.ctypes.byref(d)), C.device)
+    nat.check(lib.se_gemm(nat.ctypes.byref(d), A.data_ptr(), B.data_ptr(), C.data_ptr(), nat.ptr(bias0), nat.ptr(bias1),
+                        amax_a.data_ptr(), amax_b.data_ptr(), ws.data_ptr(), ws.numel(), nat.stream_of(C)),
+            "se_gemm")
+    return C
+
+
+def _lstm_proj(x, w_ih, b_ih, b_hh, xa, wa):
+    """x W_ih^T + b_ih + b_hh for L LSTMs: x [B, T, I] (shared) -> [B*T, L*G], or
+    x [L, B, T, I] -> [L, B*T, G]."""
+    L, G, I = w_ih.shape
+    R = x.shape[-3] * x.shape[-2]
+    if x.dim() == 3:
+        out = torch.empty((R, L * G), device=x.device, dtype=torch.float32)
+        return gemm(x, w_ih, out, M=R, N=L * G, K=I, lda=I, ldb=I, ldc=L * G, amax_a=xa, amax_b=wa,
+                    bias0=b_ih, bias1=b_hh)
+    out = torch.empty((L, R, G), device=x.device, dtype=torch.float32)
+    return gemm(x, w_ih, out, M=R, N=G, K=I, lda=I, ldb=I, ldc=G, amax_a=xa, amax_b=wa, batches=L,
+                stride_a=R * I, stride_b=G * I, stride_c=R * G, bias0=b_ih, bias1=b_hh, stride_bias=G)
+
+
+def _lstm_grads_hip(ctx, x, w_ih, h, dg, xa, wa, need):
+    """dx, dW_ih, dW_hh, db of _LstmLayer on se_gemm / se_colsum. dg [L, B*T, G]."""
+    L, R, G = dg.shape
+    I, H = w_ih.shape[2], h.shape[-1]
+    T = h.shape[2]
+    shared = x.dim() == 3
+    dx = dw_ih = dw_hh = db = None
+    if need[3]:   # the bias gradient pass also bounds max |dgates| (the GEMMs' scale)
+        db = torch.empty((L, G), device=dg.device, dtype=torch.float32)
+        ga = torch.empty(1, device=dg.device, dtype=torch.float32)
+        lib = N.lib()
+        ws = _workspace(lib.se_colsum_workspace_size(L, R, G), dg.device)
+        N.check(lib.se_colsum(dg.data_ptr(), L, R, G, db.data_ptr(), ga.data_ptr(), ws.data_ptr(), ws.numel(),
+                              N.stream_of(dg)), "se_colsum")
+    else:
+        ga = amax_of(dg)
+    if need[0]:
+        if shared:
+            dx = torch.empty((x.shape[0], x.shape[1], I), device=dg.device, dtype=torch.float32)
+            gemm(dg, w_ih, dx, M=R, N=I, K=G, lda=G, ldb=I, ldc=I, amax_a=ga, amax_b=wa, b_ncontig=True,
+                 batches=L, sum_batches=True, stride_a=R * G, stride_b=G * I)
+        else:
+            dx = torch.empty_like(x)
+            gemm(dg, w_ih, dx, M=R, N=I, K=G, lda=G, ldb=I, ldc=I, amax_a=ga, amax_b=wa, b_ncontig=True,
+                 batches=L, stride_a=R * G, stride_b=G * I, stride_c=R * I)
+    if need[1]:
+        dw_ih = torch.empty_like(w_ih)
+        gemm(dg, x, dw_ih, M=G, N=I, K=R, lda=G, ldb=I, ldc=I, amax_a=ga, amax_b=xa, a_mcontig=True,
+             b_ncontig=True, batches=L, stride_a=R * G, stride_b=0 if shared else R * I, stride_c=G * I)
+    if need[2]:
+        dw_hh = torch.empty((L, G, H), device=dg.device, dtype=torch.float32)
+        if T == 1 or R < 2:   # every h_{t-1} is h_{-1} = 0
+            dw_hh.zero_()
+        else:
+            hf = h.reshape(L, R, H)
+            hb = _unit_bound(dg.device)
+            for rev in (0, 1):
+                ls = [l for l in range(L) if ((ctx.rev_mask >> l) & 1) == rev]
+                if not ls:
+                    continue
+                # forward: pairs (dgates row r, h row r - 1); reverse: (r, r + 1); the rows
+                # of the first / last step of a sequence pair with nothing (k % T == T - 1)
+                runs = [ls] if ls == list(range(ls[0], ls[0] + len(ls))) else [[l] for l in ls]
+                for run in runs:
+                    l0, n = run[0], len(run)
+                    a = dg[l0, 1:] if rev == 0 else dg[l0, :-1]
+                    b = hf[l0, :-1] if rev == 0 else hf[l0, 1:]
+                    gemm(a, b, dw_hh[l0], M=G, N=H, K=R - 1, lda=G, ldb=H, ldc=H, amax_a=ga, amax_b=hb,
+                         a_mcontig=True, b_ncontig=True, batches=n, stride_a=R * G, stride_b=R * H,
+                         stride_c=G * H, kmask=(T, T - 1))
+    return dx, dw_ih, dw_hh, db
+
+
 class _LstmLayer(torch.autograd.Function):
     """One layer of L independent LSTMs run together (torch.nn.LSTM math,
     gate order i, f, g, o, zero initial state).
@@ -1299,9 +1407,10 @@ class _LstmLayer(torch.autograd.Function):
     w_hh [L, 4H, H]; b_ih, b_hh [L, 4H] or None; bit l of rev_mask runs LSTM l
     right-to-left. Returns h [L, B, T, H].
 
-    The input projection and all weight/input gradients are plain GEMMs
-    (rocBLAS through torch); the time recurrence is one persistent HIP
-    launch per direction (fwd: se_lstm_fwd, bwd: se_lstm_bwd)."""
+    The input projection and all weight/input gradients are plain GEMMs on
+    se_gemm (split-fp16 MFMA, csrc/gemm.hip; SEHIP_LSTM_GEMM=torch: rocBLAS
+    through torch); the time recurrence is one persistent HIP launch per
+    direction (fwd: se_lstm_fwd, bwd: se_lstm_bwd)."""
 
     @staticmethod
     def forward(ctx, x, w_ih, w_hh, b_ih, b_hh, rev_mask):
@@ -1312,20 +1421,27 @@ class _LstmLayer(torch.autograd.Function):
         B, T = x.shape[-3], x.shape[-2]
         if x.shape[-1] != I or tuple(w_hh.shape) != (L, G, H):
             raise ValueError("sehip lstm: inconsistent shapes")
-        bias = None
-        if b_ih is not None or b_hh is not None:
-            bias = (b_ih if b_ih is not None else 0) + (b_hh if b_hh is not None else 0)
-        if shared:
-            x2 = x.reshape(B * T, I)
-            wt = w_ih.reshape(L * G, I).t()
-            xproj = torch.addmm(bias.reshape(L * G), x2, wt) if bias is not None else x2 @ wt
-            x_lstm, x_row = G, L * G
-        else:
-            x3 = x.reshape(L, B * T, I)
-            wt = w_ih.transpose(1, 2)
-            xproj = (torch.baddbmm(bias.unsqueeze(1), x3, wt) if bias is not None
-                     else torch.bmm(x3, wt))
-            x_lstm, x_row = B * T * G, G
+        xa = wa = None
+        x_lstm, x_row = (G, L * G) if shared else (B * T * G, G)
+        if lstm_gemm_hip():   # se_gemm (csrc/gemm.hip)
+            x, w_ih = x.contiguous(), w_ih.contiguous()
+            b_ih = b_ih.contiguous() if b_ih is not None else None
+            b_hh = b_hh.contiguous() if b_hh is not None else None
+            xa, wa = amax_of(x), amax_of(w_ih)
+            xproj = _lstm_proj(x, w_ih, b_ih, b_hh, xa, wa)
+        else:                 # torch / rocBLAS (SEHIP_LSTM_GEMM=torch)
+            bias = None
+            if b_ih is not None or b_hh is not None:
+                bias = (b_ih if b_ih is not None else 0) + (b_hh if b_hh is not None else 0)
+            if shared:
+                x2 = x.reshape(B * T, I)
+                wt = w_ih.reshape(L * G, I).t()
+                xproj = torch.addmm(bias.reshape(L * G), x2, wt) if bias is not None else x2 @ wt
+            else:
+                x3 = x.reshape(L, B * T, I)
+                wt = w_ih.transpose(1, 2)
+                xproj = (torch.baddbmm(bias.unsqueeze(1), x3, wt) if bias is not None
+                         else torch.bmm(x3, wt))
         w_hh = w_hh.contiguous()
         h = torch.empty((L, B, T, H), device=x.device, dtype=x.dtype)
         c = torch.empty_like(h)
@@ -1346,7 +1462,10 @@ class _LstmLayer(torch.autograd.Function):
                     "se_lstm_fwd")
         if t0 is not None:
             _TIMER.end("lstm_fwd", t0, 2.0 * L * B * T * G * H, 4.0 * L * B * T * (G + 2 * G + 2 * H))
+        if xa is not None:
+            amax_put(h, _unit_bound(h.device))   # |h| < 1: the next layer's input bound
         ctx.save_for_backward(x, w_ih, w_hh, h, c, gates)
+        ctx.amax = (xa, wa)
         ctx.rev_mask, ctx.has_b = int(rev_mask), (b_ih is not None, b_hh is not None)
         ctx.mark_non_differentiable(c)
         ctx.set_materialize_grads(False)
@@ -1377,9 +1496,15 @@ class _LstmLayer(torch.autograd.Function):
         if t0 is not None:
             _TIMER.end("lstm_bwd", t0, 2.0 * L * B * T * G * H, 4.0 * L * B * T * (H + 2 * G + 2 * H))
         dg = dgates.reshape(L, B * T, G)
-        dgt = dg.transpose(1, 2)
         shared = x.dim() == 3
         dx = dw_ih = dw_hh = db_ih = db_hh = None
+        need_b = ctx.has_b[0] and ctx.needs_input_grad[3] or ctx.has_b[1] and ctx.needs_input_grad[4]
+        if ctx.amax[0] is not None:   # the forward ran its projection on se_gemm
+            need = (ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2], need_b)
+            dx, dw_ih, dw_hh, db = _lstm_grads_hip(ctx, x, w_ih, h, dg, ctx.amax[0], ctx.amax[1], need)
+            db_ih = db if ctx.has_b[0] and need_b else None
+            db_hh = db if ctx.has_b[1] and need_b else None
+            return dx, dw_ih, dw_hh, db_ih, db_hh, None
         if ctx.needs_input_grad[0]:
             if shared:
                 dx = torch.bmm(dg, w_ih).sum(0).reshape(B, T, I)
@@ -1406,7 +1531,7 @@ class _LstmLayer(torch.autograd.Function):
                     if r is not None:   # rows b*T + T-1 (t = T-1) paired with the next sequence's first h
                         w -= dg[l, r - 1].t() @ hf[l, r]
                 dw_hh[l] = w
-        if ctx.has_b[0] and ctx.needs_input_grad[3] or ctx.has_b[1] and ctx.needs_input_grad[4]:
+        if need_b:
             db = _rows_sum(dg)
             db_ih = db if ctx.has_b[0] else None
             db_hh = db if ctx.has_b[1] else None

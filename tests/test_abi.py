@@ -17,7 +17,7 @@ def test_library_exports_header_symbols():
     for s in syms:
         assert hasattr(lib, s), f"libsehip.so does not export {s}"
     assert N.MISSING == []
-    assert lib.se_abi_version() == 5
+    assert lib.se_abi_version() == N.ABI_VERSION
 
 
 def test_strerror():
