@@ -607,6 +607,10 @@ int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out,
                    int B, int C, int HW, void* stream);
 int se_ccbam_bwd_sa(const float* gout, float* dsa, int B, int C, int HW,
                     void* stream);
+/* ABI 6: se_ccbam_bwd_sa with the spatial gate's sigmoid backward fused:
+ * dz = (sum of gout over each half's channels) * (1 - sa) * sa, sa = sigmoid(z) the gate
+ * [B, 2, HW]; bit-identical to se_ccbam_bwd_sa followed by torch's sigmoid_backward. */
+int se_ccbam_bwd_sa_sigmoid(const float* gout, const float* sa, float* dz, int B, int C, int HW, void* stream);
 int se_ccbam_bwd_dca(const float* gout, const float* x, const float* dpooled,
                      const short* idx, float* dca, int B, int C, int HW,
                      void* ws, size_t ws_bytes, void* stream);

@@ -216,6 +216,63 @@ __global__ void dca_reduce_kernel(const float* __restrict__ part, float* __restr
   dca[i] = s;
 }
 
+// The spatial gate's sigmoid backward fused into the channel sums (the gate sa =
+// sigmoid(z) of the spatial branch, ccbam.py:82-86): dz[b, h, hw] =
+// (sum_{c in half h} gout[b, c, hw]) * (1 - sa) * sa, the sums in channel order
+// and the product in ATen's sigmoid_backward order, so dz is bit-identical to
+// bwd_sa_kernel followed by torch's sigmoid backward. Four consecutive positions
+// per thread (16-B loads when HW % 4 == 0): a block streams 4-KB segments of each
+// channel plane instead of 1 KB.
+typedef float f32x4c __attribute__((ext_vector_type(4)));
+template <bool V4>
+__global__ __launch_bounds__(kThreads) void bwd_sa_sig_kernel(const float* __restrict__ g,
+                                                              const float* __restrict__ sa,
+                                                              float* __restrict__ dz, int C, int HW) {
+  const int b = blockIdx.y;
+  const int p0 = (blockIdx.x * kThreads + threadIdx.x) * 4;
+  if (p0 >= HW) return;
+  const int Ch = C / 2;
+  const float* gb = g + (size_t)b * C * HW + p0;
+  float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
+  if constexpr (V4) {
+    constexpr int U = 4;   // four channels of each half in flight
+    int c = 0;
+    for (; c + U <= Ch; c += U) {
+      f32x4c v0[U], v1[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        v0[u] = *reinterpret_cast<const f32x4c*>(gb + (size_t)(c + u) * HW);
+        v1[u] = *reinterpret_cast<const f32x4c*>(gb + (size_t)(Ch + c + u) * HW);
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s0[e] += v0[u][e]; s1[e] += v1[u][e]; }
+    }
+    for (; c < Ch; ++c) {
+      const f32x4c v0 = *reinterpret_cast<const f32x4c*>(gb + (size_t)c * HW);
+      const f32x4c v1 = *reinterpret_cast<const f32x4c*>(gb + (size_t)(Ch + c) * HW);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s0[e] += v0[e]; s1[e] += v1[e]; }
+    }
+  } else {
+    const int ne = min(4, HW - p0);
+    for (int c = 0; c < Ch; ++c) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (e < ne) { s0[e] += gb[(size_t)c * HW + e]; s1[e] += gb[(size_t)(Ch + c) * HW + e]; }
+    }
+  }
+  const size_t o0 = ((size_t)b * 2) * HW + p0, o1 = o0 + HW;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    if (p0 + e >= HW) break;
+    const float y0 = sa[o0 + e], y1 = sa[o1 + e];
+    dz[o0 + e] = s0[e] * (1.f - y0) * y0;
+    dz[o1 + e] = s1[e] * (1.f - y1) * y1;
+  }
+}
+
 // dx = gx1 * ca + dmean/HW + [hw is the HW-argmax of (b, c)] * dmax
 __global__ __launch_bounds__(kThreads) void bwd_dx_kernel(const float* __restrict__ g, const float* __restrict__ dP,
                                                           const short* __restrict__ idx, const float* __restrict__ ca,
@@ -443,6 +500,20 @@ extern "C" int se_ccbam_bwd_sa(const float* gout, float* dsa, int B, int C, int 
   if (int rc = check(B, C, HW)) return rc;
   if (!gout || !dsa) return SE_E_ARG;
   hipLaunchKernelGGL(bwd_sa_kernel, hw_grid(B, HW), dim3(kThreads), 0, se::as_stream(stream), gout, dsa, C, HW);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_ccbam_bwd_sa_sigmoid(const float* gout, const float* sa, float* dz, int B, int C, int HW,
+                                       void* stream) {
+  if (int rc = check(B, C, HW)) return rc;
+  if (!gout || !sa || !dz) return SE_E_ARG;
+  const dim3 grid((HW + 4 * kThreads - 1) / (4 * kThreads), B);
+  if (HW % 4 == 0 && ((uintptr_t)gout & 15) == 0)
+    hipLaunchKernelGGL(bwd_sa_sig_kernel<true>, grid, dim3(kThreads), 0, se::as_stream(stream), gout, sa, dz, C, HW);
+  else
+    hipLaunchKernelGGL(bwd_sa_sig_kernel<false>, grid, dim3(kThreads), 0, se::as_stream(stream), gout, sa, dz, C,
+                       HW);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

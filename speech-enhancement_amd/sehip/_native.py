@@ -146,6 +146,7 @@ _SIGNATURES = {
     "se_ccbam_spatial_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
     "se_ccbam_apply": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_sa": (c_int, [_P] * 2 + [c_int] * 3 + [_P]),
+    "se_ccbam_bwd_sa_sigmoid": (c_int, [_P] * 3 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_dca": (c_int, [_P] * 5 + [c_int] * 3 + [_P, c_size_t, _P]),
     "se_ccbam_bwd_dx": (c_int, [_P] * 8 + [c_int] * 3 + [_P]),
     "se_ccbam_mlp_fwd": (c_int, [_P] * 6 + [c_int] * 3 + [_P] * 3),

@@ -150,7 +150,10 @@ class _CCBAMFn(torch.autograd.Function):
               P.data_ptr(), idx.data_ptr(), B, C, HW, st)
         with torch.set_grad_enabled(need_grad):
             Pl = P.requires_grad_(True) if need_grad else P
-            sa = torch.sigmoid(sab.conv(Pl)).contiguous()             # [B, 2, H, W]
+            z = sab.conv(Pl)                                          # [B, 2, H, W] pre-sigmoid
+        # the gate's sigmoid outside autograd: its backward is fused into
+        # se_ccbam_bwd_sa_sigmoid
+        sa = torch.sigmoid(z.detach()).contiguous()
         out = torch.empty_like(x)
         _call(lib.se_ccbam_apply, "se_ccbam_apply", x.data_ptr(), ca.data_ptr(), sa.data_ptr(),
               out.data_ptr(), B, C, HW, st)
@@ -159,7 +162,7 @@ class _CCBAMFn(torch.autograd.Function):
             F.amax_put(out, xa + 1.0)
         if need_grad:
             ctx.save_for_backward(x, idx, amax)
-            ctx.graphs = (pooled, ca, Pl, sa)
+            ctx.graphs = (pooled, ca, Pl, z, sa)
             ctx.mod = mod
             ctx.mlp = (mlp, mean, mx, hs) if mlp is not None else None
         return out
@@ -167,17 +170,18 @@ class _CCBAMFn(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         x, idx, amax = ctx.saved_tensors
-        pooled, ca, Pl, sa = ctx.graphs
+        pooled, ca, Pl, z, sa = ctx.graphs
         mod = ctx.mod
         B, C, H, W = x.shape
         HW = H * W
         lib, st, dev = N.lib(), N.stream_of(gout), gout.device
         gout = gout.contiguous()
-        dsa = torch.empty(B, 2, H, W, device=dev)
-        _call(lib.se_ccbam_bwd_sa, "se_ccbam_bwd_sa", gout.data_ptr(), dsa.data_ptr(), B, C, HW, st)
+        dz = torch.empty(B, 2, H, W, device=dev)   # d loss / d (pre-sigmoid gate)
+        _call(lib.se_ccbam_bwd_sa_sigmoid, "se_ccbam_bwd_sa_sigmoid", gout.data_ptr(), sa.data_ptr(),
+              dz.data_ptr(), B, C, HW, st)
         sp = list(mod.spatial_attention_branch.parameters())
         ch = list(mod.channel_attention_branch.parameters())
-        gs = torch.autograd.grad(sa, [Pl] + sp, dsa, allow_unused=True)
+        gs = torch.autograd.grad(z, [Pl] + sp, dz, allow_unused=True)
         dP = gs[0].contiguous()
         dca = torch.empty(B, C, device=dev)
         ws = F._workspace(lib.se_ccbam_workspace_size(B, C, HW), dev)

@@ -141,3 +141,25 @@ def test_ccbam_fused_mlp_matches_module_mlp(gpu_device, monkeypatch):
     assert _rel(y1, y0) < 1e-6 and _rel(dx1, dx0) < 1e-5
     for n in g0:
         assert _rel(g1[n], g0[n]) < 1e-5, n
+
+
+@pytest.mark.parametrize("HW", [160 * 404, 10 * 403, 37])
+def test_bwd_sa_sigmoid_bit_identical(gpu_device, HW):
+    """se_ccbam_bwd_sa_sigmoid == se_ccbam_bwd_sa then torch's sigmoid backward, to the bit
+    (16-B path where HW % 4 == 0, guarded scalar path otherwise)."""
+    from sehip import _native as N
+    torch.manual_seed(7)
+    B, C = 3, 128
+    g = torch.randn(B, C, HW, device=gpu_device)
+    z = torch.randn(B, 2, HW, device=gpu_device, requires_grad=True)
+    sa = torch.sigmoid(z)
+    lib, st = N.lib(), N.stream_of(g)
+    dsa = torch.empty(B, 2, HW, device=gpu_device)
+    N.check(lib.se_ccbam_bwd_sa(g.data_ptr(), dsa.data_ptr(), B, C, HW, st), "se_ccbam_bwd_sa")
+    ref, = torch.autograd.grad(sa, z, dsa)
+    dz = torch.empty(B, 2, HW, device=gpu_device)
+    sad = sa.detach().contiguous()
+    N.check(lib.se_ccbam_bwd_sa_sigmoid(g.data_ptr(), sad.data_ptr(), dz.data_ptr(), B, C, HW, st),
+            "se_ccbam_bwd_sa_sigmoid")
+    torch.cuda.synchronize()
+    assert torch.equal(dz, ref)
