@@ -57,11 +57,23 @@ __device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float,
 
 // (x0, x1) * s -> packed fp16 hi pair and lo pair (element 0 in the low half);
 // v_cvt_pk_f16_f32 rounds to nearest even, s * x - hi is one exact FMA
+#ifndef SEHIP_SPLIT_MIX
+#define SEHIP_SPLIT_MIX 0
+#endif
 __device__ __forceinline__ void split_f16x2(float x0, float x1, float s, unsigned& hi, unsigned& lo) {
   const f32x2 v = (f32x2){x0, x1} * s;
   const f16x2 h = __builtin_convertvector(v, f16x2);
   hi = __builtin_bit_cast(unsigned, h);
+#if SEHIP_SPLIT_MIX
+  // lo = f16(x s - hi) by v_fma_mix{lo,hi}_f16 straight from the packed fp16 hi: the
+  // same single rounding of the exact x s - hi, two instructions instead of four
+  unsigned l;
+  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(x0), "v"(s), "v"(hi));
+  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(x1), "v"(s), "v"(hi));
+  lo = l;
+#else
   lo = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2));
+#endif
 }
 
 // one 32x32x16 MFMA on a pair of 16-B operand fragments: fp16 or bf16 elements

@@ -66,3 +66,51 @@ def test_ddp_two_ranks_one_gpu(tmp_path, gpu_device, mode):
         rels.append(float((g[0][n] - mean).norm() / (mean.norm() + 1e-12)))
     rels.sort()
     assert rels[len(rels) // 2] < 1e-5 and rels[-1] < 1e-3, (rels[len(rels) // 2], rels[-1])
+
+
+def _rccl_worker(port, out_dir):
+    """One rank over RCCL ("nccl" on ROCm): FlatDataParallel's broadcasts and its one
+    flattened gradient all-reduce execute on RCCL (a world of one is the most this
+    one-GPU box can host; RCCL refuses two ranks on one device)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1",
+                      LOCAL_RANK="0")
+    import torch.distributed as dist
+    from sehip.losses import SI_SNR_loss
+    from sehip.models import FRCRN
+    from sehip.train import FlatDataParallel, finish_grads, train_step, make_optimizer
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    dist.init_process_group(backend="nccl", rank=0, world_size=1, device_id=dev)
+    assert dist.get_backend() == "nccl"
+    model = paramfill.fill_(FRCRN(), seed=9).to(dev).train()
+    ddp = FlatDataParallel(model)
+    noisy, clean = (t.to(dev) for t in _shard(0))
+    _, wav = ddp(noisy)
+    SI_SNR_loss(wav, clean).backward()
+    finish_grads(ddp)
+    torch.cuda.synchronize()
+    torch.save({n: p.grad.detach().cpu() for n, p in model.named_parameters()}, os.path.join(out_dir, "g.pt"))
+    # a full train step (forward, SI-SNR, backward, all-reduce, clip, AdamW) through the wrapper
+    opt = make_optimizer(model)
+    loss = train_step(ddp, opt, noisy, clean)
+    torch.cuda.synchronize()
+    assert torch.isfinite(loss).all()
+    with open(os.path.join(out_dir, "rccl.txt"), "w") as f:
+        f.write(str(torch.cuda.nccl.version()))
+    dist.destroy_process_group()
+
+
+def test_flat_ddp_over_rccl_world_one(tmp_path, gpu_device):
+    port = _free_port()
+    mp.spawn(_rccl_worker, args=(port, str(tmp_path)), nprocs=1, join=True)
+    g = torch.load(tmp_path / "g.pt", weights_only=True)
+    from sehip.models import FRCRN
+    from sehip.losses import SI_SNR_loss
+    m = paramfill.fill_(FRCRN(), seed=9).cuda().train()
+    noisy, clean = (t.cuda() for t in _shard(0))
+    _, wav = m(noisy)
+    SI_SNR_loss(wav, clean).backward()
+    for n, p in m.named_parameters():   # the mean over one rank: the local gradient
+        ref = p.grad.cpu()
+        assert ((g[n] - ref).norm() / ref.norm().clamp_min(1e-30)).item() < 1e-5, n
+    assert (tmp_path / "rccl.txt").read_text()
