@@ -489,6 +489,68 @@ gather_smalln_kernel(const GatherArgs a) {
     if (n < a.N) st_s<SD>(a.Y, ybase + n * HoWo, acc[n] + (a.bias ? a.bias[n] : 0.f));
 }
 
+// Small-N stride-1 conv as an LDS stencil (CCBAM's spatial ComplexConv2d(4 -> 2, k7,
+// pad 3) and its data-grad, ccbam.py:65-86): a workgroup stages a CG x (32 + halo)
+// x (64 + halo) input tile once, and each thread forms kStR output rows of one
+// column from it, so a gathered element is loaded from HBM / L2 once per tile instead
+// of once per tap. Per output the products are added in gather_smalln_kernel's order
+// (k = tap * CG + c, fmaf), so the results are bit-identical to it. The weights of a
+// k are uniform (scalar loads); tap offsets come from the kernel arguments.
+constexpr int kStW = 64, kStRG = 4, kStR = 8;   // tile: 64 columns x (4 x 8) rows
+template <int NOUT, int CG>
+__global__ void __launch_bounds__(kThreads)
+gather_stencil_kernel(const GatherArgs a, int h0, int w0, int th, int tw) {
+  extern __shared__ float sx[];   // [CG][th][tw]
+  const int b = blockIdx.z;
+  const int qh0 = blockIdx.y * (kStRG * kStR), qw0 = blockIdx.x * kStW;
+  const long long HiWi = (long long)a.Hi * a.Wi;
+  const float* xb = a.X + (long long)b * CG * HiWi;
+  const int plane = th * tw;
+  for (int i = threadIdx.x; i < CG * plane; i += kThreads) {
+    const int c = i / plane, rr = i - c * plane;
+    const int r = rr / tw, col = rr - r * tw;
+    const int hi = qh0 + h0 + r, wi = qw0 + w0 + col;
+    sx[i] = ((unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi)
+                ? xb[(long long)c * HiWi + (long long)hi * a.Wi + wi] : 0.f;
+  }
+  __syncthreads();
+  const int lc = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * kStR;
+  float acc[kStR][NOUT];
+#pragma unroll
+  for (int r = 0; r < kStR; ++r)
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n) acc[r][n] = 0.f;
+  for (int t = 0; t < a.ntaps; ++t) {
+    const int base = (r0 + a.toffh[t] - h0) * tw + lc + a.toffw[t] - w0;
+#pragma unroll
+    for (int c = 0; c < CG; ++c) {
+      const float* wk = a.Wp + (long long)(t * CG + c) * a.ldw;
+      float w[NOUT];
+#pragma unroll
+      for (int n = 0; n < NOUT; ++n) w[n] = wk[n];
+      const float* src = sx + c * plane + base;
+#pragma unroll
+      for (int r = 0; r < kStR; ++r) {
+        const float v = src[r * tw];
+#pragma unroll
+        for (int n = 0; n < NOUT; ++n) acc[r][n] = fmaf(v, w[n], acc[r][n]);
+      }
+    }
+  }
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  const int qw = qw0 + lc;
+  if (qw >= a.Qw) return;
+#pragma unroll
+  for (int r = 0; r < kStR; ++r) {
+    const int qh = qh0 + r0 + r;
+    if (qh >= a.Qh) break;
+    const long long yb = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
+#pragma unroll
+    for (int n = 0; n < NOUT; ++n)
+      if (n < a.N) a.Y[yb + n * HoWo] = acc[r][n] + (a.bias ? a.bias[n] : 0.f);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Weight-grad reduction GEMM: dWp[k, n] = sum_m G[m, k] * D[m, n]
 // Each workgroup reduces one m-range (split) for one BKO x BNO tile and
@@ -1595,6 +1657,27 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     if (M > INT32_MAX) return SE_E_UNSUPPORTED;
     a.M = (int)M;
     if (N <= 16) {
+      // stride-1 single-class small convs (CCBAM's spatial conv and its data-grad): the
+      // LDS stencil, bit-identical to gather_smalln_kernel (SEHIP_STENCIL=0: off)
+      int h0 = 0, h1 = 0, w0 = 0, w1 = 0;
+      for (int t = 0; t < c.taps.n; ++t) {
+        h0 = std::min(h0, c.taps.offh[t]); h1 = std::max(h1, c.taps.offh[t]);
+        w0 = std::min(w0, c.taps.offw[t]); w1 = std::max(w1, c.taps.offw[t]);
+      }
+      const int th = kStRG * kStR + h1 - h0, tw = kStW + w1 - w0;
+      const bool stencil = g.sd == SE_DTYPE_F32 && !jn && !c.mrg && ldw <= 4 && (Cg == 2 || Cg == 4) &&
+                           c.h.s == 1 && c.w.s == 1 && (size_t)Cg * th * tw * sizeof(float) <= 48 * 1024 &&
+                           c.taps.n <= kMaxTaps && !env_flag_off("SEHIP_STENCIL");
+      if (stencil) {
+        a.ntaps = c.taps.n;
+        for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }
+        const dim3 sgrid(se::ceil_div(c.w.Q, kStW), se::ceil_div(c.h.Q, kStRG * kStR), g.B);
+        const size_t shs = (size_t)Cg * th * tw * sizeof(float);
+        if (Cg == 4) hipLaunchKernelGGL((gather_stencil_kernel<4, 4>), sgrid, dim3(kThreads), shs, st, a, h0, w0, th, tw);
+        else hipLaunchKernelGGL((gather_stencil_kernel<4, 2>), sgrid, dim3(kThreads), shs, st, a, h0, w0, th, tw);
+        SE_LAUNCH_CHECK();
+        continue;
+      }
       const size_t sh = (size_t)c.Kp * ldw * sizeof(float);
       if (sh > 64 * 1024) return SE_E_UNSUPPORTED;
       dim3 grid(se::ceil_div(M, kThreads));

@@ -163,3 +163,30 @@ def test_bwd_sa_sigmoid_bit_identical(gpu_device, HW):
             "se_ccbam_bwd_sa_sigmoid")
     torch.cuda.synchronize()
     assert torch.equal(dz, ref)
+
+
+@pytest.mark.parametrize("shape", [(3, 4, 160, 404), (2, 4, 37, 70), (1, 4, 5, 403)])
+def test_spatial_conv_stencil_bit_identical(gpu_device, monkeypatch, shape):
+    """The CCBAM spatial ComplexConv2d(4 -> 2, k7, pad 3) forward and data-grad on the LDS
+    stencil (gather_stencil_kernel) equal gather_smalln_kernel (SEHIP_STENCIL=0) to the
+    bit (same products, same order), including partial edge tiles."""
+    from sehip import functional as F
+    torch.manual_seed(11)
+    x = torch.randn(shape, device=gpu_device)
+    wr = torch.randn(1, 2, 7, 7, device=gpu_device) * 0.1
+    wi = torch.randn(1, 2, 7, 7, device=gpu_device) * 0.1
+    g = torch.randn(shape[0], 2, shape[2], shape[3], device=gpu_device)
+    outs = []
+    for flag in ("1", "0"):
+        monkeypatch.setenv("SEHIP_STENCIL", flag)
+        xa = x.clone().requires_grad_(True)
+        y = F.conv2d(xa, wr, wi, out_channels=2, kernel=(7, 7), padding=(3, 3))
+        y.backward(g)
+        torch.cuda.synchronize()
+        outs.append((y.detach(), xa.grad))
+    assert torch.equal(outs[0][0], outs[1][0])
+    assert torch.equal(outs[0][1], outs[1][1])
+    ref = torch.nn.functional.conv2d(x.double().cpu(),
+                                     torch.cat([torch.cat([wr, -wi], 1), torch.cat([wi, wr], 1)], 0).double().cpu(),
+                                     padding=3)
+    assert ((outs[0][0].double().cpu() - ref).norm() / ref.norm()).item() < 1e-6

@@ -68,7 +68,7 @@ def test_ddp_two_ranks_one_gpu(tmp_path, gpu_device, mode):
     assert rels[len(rels) // 2] < 1e-5 and rels[-1] < 1e-3, (rels[len(rels) // 2], rels[-1])
 
 
-def _rccl_worker(port, out_dir):
+def _rccl_worker(rank, port, out_dir):
     """One rank over RCCL ("nccl" on ROCm): FlatDataParallel's broadcasts and its one
     flattened gradient all-reduce execute on RCCL (a world of one is the most this
     one-GPU box can host; RCCL refuses two ranks on one device)."""
