@@ -228,21 +228,27 @@ template <bool V4>
 __global__ __launch_bounds__(kThreads) void bwd_sa_sig_kernel(const float* __restrict__ g,
                                                               const float* __restrict__ sa,
                                                               float* __restrict__ dz, int C, int HW) {
+  // a block covers 4 * kThreads consecutive positions: V4, thread t the four at
+  // 4 t (16-B loads); else the four at t + e kThreads (every load a 256-B segment)
   const int b = blockIdx.y;
-  const int p0 = (blockIdx.x * kThreads + threadIdx.x) * 4;
-  if (p0 >= HW) return;
+  const int base = blockIdx.x * 4 * kThreads;
   const int Ch = C / 2;
-  const float* gb = g + (size_t)b * C * HW + p0;
+  int pos[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) pos[e] = V4 ? base + 4 * threadIdx.x + e : base + threadIdx.x + e * kThreads;
+  if (pos[0] >= HW) return;
+  const float* gb = g + (size_t)b * C * HW;
   float s0[4] = {0.f, 0.f, 0.f, 0.f}, s1[4] = {0.f, 0.f, 0.f, 0.f};
+  constexpr int U = 4;   // four channels of each half in flight; each position sums in channel order
   if constexpr (V4) {
-    constexpr int U = 4;   // four channels of each half in flight
+    const float* gp = gb + pos[0];
     int c = 0;
     for (; c + U <= Ch; c += U) {
       f32x4c v0[U], v1[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
-        v0[u] = *reinterpret_cast<const f32x4c*>(gb + (size_t)(c + u) * HW);
-        v1[u] = *reinterpret_cast<const f32x4c*>(gb + (size_t)(Ch + c + u) * HW);
+        v0[u] = *reinterpret_cast<const f32x4c*>(gp + (size_t)(c + u) * HW);
+        v1[u] = *reinterpret_cast<const f32x4c*>(gp + (size_t)(Ch + c + u) * HW);
       }
 #pragma unroll
       for (int u = 0; u < U; ++u)
@@ -250,26 +256,41 @@ __global__ __launch_bounds__(kThreads) void bwd_sa_sig_kernel(const float* __res
         for (int e = 0; e < 4; ++e) { s0[e] += v0[u][e]; s1[e] += v1[u][e]; }
     }
     for (; c < Ch; ++c) {
-      const f32x4c v0 = *reinterpret_cast<const f32x4c*>(gb + (size_t)c * HW);
-      const f32x4c v1 = *reinterpret_cast<const f32x4c*>(gb + (size_t)(Ch + c) * HW);
+      const f32x4c v0 = *reinterpret_cast<const f32x4c*>(gp + (size_t)c * HW);
+      const f32x4c v1 = *reinterpret_cast<const f32x4c*>(gp + (size_t)(Ch + c) * HW);
 #pragma unroll
       for (int e = 0; e < 4; ++e) { s0[e] += v0[e]; s1[e] += v1[e]; }
     }
   } else {
-    const int ne = min(4, HW - p0);
-    for (int c = 0; c < Ch; ++c) {
+    int q[4];   // clamped positions: loads stay in range, results past HW are not stored
 #pragma unroll
-      for (int e = 0; e < 4; ++e)
-        if (e < ne) { s0[e] += gb[(size_t)c * HW + e]; s1[e] += gb[(size_t)(Ch + c) * HW + e]; }
+    for (int e = 0; e < 4; ++e) q[e] = min(pos[e], HW - 1);
+    int c = 0;
+    for (; c + U <= Ch; c += U) {
+      float v0[U][4], v1[U][4];
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          v0[u][e] = gb[(size_t)(c + u) * HW + q[e]];
+          v1[u][e] = gb[(size_t)(Ch + c + u) * HW + q[e]];
+        }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) { s0[e] += v0[u][e]; s1[e] += v1[u][e]; }
     }
+    for (; c < Ch; ++c)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) { s0[e] += gb[(size_t)c * HW + q[e]]; s1[e] += gb[(size_t)(Ch + c) * HW + q[e]]; }
   }
-  const size_t o0 = ((size_t)b * 2) * HW + p0, o1 = o0 + HW;
+  const size_t o0 = ((size_t)b * 2) * HW, o1 = o0 + HW;
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
-    if (p0 + e >= HW) break;
-    const float y0 = sa[o0 + e], y1 = sa[o1 + e];
-    dz[o0 + e] = s0[e] * (1.f - y0) * y0;
-    dz[o1 + e] = s1[e] * (1.f - y1) * y1;
+    if (pos[e] >= HW) continue;
+    const float y0 = sa[o0 + pos[e]], y1 = sa[o1 + pos[e]];
+    dz[o0 + pos[e]] = s0[e] * (1.f - y0) * y0;
+    dz[o1 + pos[e]] = s1[e] * (1.f - y1) * y1;
   }
 }
 
