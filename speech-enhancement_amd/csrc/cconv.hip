@@ -1483,11 +1483,17 @@ static int moment_rows(const std::vector<ClassPlan>& cls, int B) {
 }
 
 // split kernels: channel-block-major K order where Cg allows (split_k)
+// SEHIP_GEMM_3M=1: the split-fp16 forward GEMMs with 64 complex outputs run the
+// three-multiplication form (gather_3m_kernel); read per call
+static bool gemm_3m() {
+  const char* e = std::getenv("SEHIP_GEMM_3M");
+  return e && e[0] == '1';
+}
 static int korder_blk(int Cg) { return (Cg % 32 == 0 && !env_flag_off("SEHIP_KORDER")) ? 32 : 0; }
 
 static void class_images(const ConvGeom& g, Pass pass, const std::vector<ClassPlan>& cls, int ldw,
                          const WeightView& wv, const float* wamax, char* base, bool build, hipStream_t st,
-                         std::vector<ClassImage>& out) {
+                         std::vector<ClassImage>& out, bool m3 = false) {
   const int N = (pass == kFwd) ? g.Co : g.Ci;
   const int Cg = (pass == kFwd) ? g.Ci : g.Co;
   const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
@@ -1508,6 +1514,13 @@ static void class_images(const ConvGeom& g, Pass pass, const std::vector<ClassPl
     p = align256(p + (size_t)c.Kp * sizeof(int4));
     out.push_back(im);
     if (!build) continue;
+    if (m3) {   // gather_3m_kernel's per-step weight images (fit in the split image's space)
+      const int nk = c.taps.n * (Cg / 2 / k3mBKc);
+      const long long tot3 = (long long)nk * 64 * k3mBKc;
+      hipLaunchKernelGGL(prep_3m_kernel, dim3((unsigned)std::min<long long>((tot3 + 255) / 256, 4096)), dim3(256),
+                         0, st, wv, c.taps, Cg / 2, N, nk, wamax, (unsigned short*)im.Wp);
+      continue;
+    }
     const long long tot = (long long)c.Kp * ldw;
     const dim3 grid((unsigned)std::min<long long>((tot + 255) / 256, 4096));
     if (x6)
@@ -1628,8 +1641,13 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   // the weight images: prepared by the caller (data-grad pass, desc.data_weights)
   // or built here in ws
   const bool have_img = pass == kData && g.data_w;
+  // the three-multiplication complex forward (gather_3m_kernel): 64 complex outputs,
+  // 16-channel K-steps, fp32 storage, plain or joined gather (SEHIP_GEMM_3M=1)
+  bool m3 = pass == kFwd && f16 && g.complex_w && N == 128 && Cg % (2 * k3mBKc) == 0 && g.sd == SE_DTYPE_F32 &&
+            !join_out && !packed && !g.mom && (!join_in || jn->jh % k3mBKc == 0) && gemm_3m();
+  for (const auto& c : cls) m3 = m3 && !c.mrg && c.taps.n <= kMaxTaps;
   std::vector<ClassImage> img;
-  class_images(g, pass, cls, ldw, wv, wamax, have_img ? (char*)g.data_w : p, !have_img, st, img);
+  class_images(g, pass, cls, ldw, wv, wamax, have_img ? (char*)g.data_w : p, !have_img, st, img, m3);
   for (size_t ic = 0; ic < cls.size(); ++ic) {
     const ClassPlan& c = cls[ic];
     float* Wp = img[ic].Wp;
@@ -1656,6 +1674,15 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     const long long M = (long long)g.B * c.h.Q * c.w.Q;
     if (M > INT32_MAX) return SE_E_UNSUPPORTED;
     a.M = (int)M;
+    if (m3) {
+      a.ntaps = c.taps.n;
+      for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }
+      const dim3 grid3(se::ceil_div(M, 128));
+      if (join_in) hipLaunchKernelGGL(gather_3m_kernel<1>, grid3, dim3(kThreads), 0, st, a);
+      else hipLaunchKernelGGL(gather_3m_kernel<0>, grid3, dim3(kThreads), 0, st, a);
+      SE_LAUNCH_CHECK();
+      continue;
+    }
     if (N <= 16) {
       // stride-1 single-class small convs (CCBAM's spatial conv and its data-grad): the
       // LDS stencil, bit-identical to gather_smalln_kernel (SEHIP_STENCIL=0: off)

@@ -1377,3 +1377,198 @@ gather_x6_kernel(const GatherArgs a) {
       }
   }
 }
+
+// ---------------------------------------------------------------------------
+// Three-multiplication ("3M", Gauss) complex GEMM for the split-fp16 forward
+// (SE_MATH_F16X3, 64 complex outputs). With x = xr + i xi the gathered complex
+// input and W = Wr + i Wi the complex weight of a (tap, input, output) triple,
+//   k1 = (xr + xi) Wr,  k2 = xr (Wi - Wr),  k3 = xi (Wr + Wi)
+//   y_re = k1 - k3 = xr Wr - xi Wi,  y_im = k1 + k2 = xr Wi + xi Wr
+// so a complex multiply-add takes 3 real products instead of the 4 of the block
+// GEMM against [[Wr, Wi], [-Wi, Wr]]: 3/4 of the MFMA issues. Each of the three
+// operand pairs is split hi + lo fp16 with the tensor's power-of-two scale (the
+// pre-sums stay below 2^15, inside fp16's range) and multiplied with the three
+// terms hh + hl + lh; k1, k2, k3 accumulate in fp32 and are combined in the
+// epilogue. Per conv vs fp64 this stays fp32-class (numpy emulation of the
+// MFMA accumulation: 1.98e-7 vs 1.77e-7 for the 4-product form and 2.51e-7 for
+// exact fp32; measured on the GPU in tests/test_gpu_conv_3m.py).
+// Tile: 128 positions x 64 complex outputs, 4 waves of 64 positions x 32
+// outputs; a K-step is 16 complex input channels of one tap. LDS image of a
+// step: A [op 3][plane 2][chunk 2][128 rows] x 16 B (op 0 = xr + xi, 1 = xr,
+// 2 = xi), W [op][plane][chunk][64 rows] x 16 B (op 0 = Wr, 1 = Wi - Wr,
+// 2 = Wr + Wi), pre-built per step by prep_3m_kernel; chunk-major rows make
+// every fragment read and every store one contiguous 1-KB wave access.
+// JM = 1: the gathered tensor is the decoder skip join (GatherArgs::X2 = x,
+// X = s; complex channels [x (jh), s (jh)]).
+// ---------------------------------------------------------------------------
+constexpr int k3mBKc = 16;                          // complex channels per K-step
+constexpr int k3mImgU4 = 3 * 2 * 2 * 64;            // u32x4 of a step's weight image (12 KB)
+
+__global__ void prep_3m_kernel(WeightView w, TapList taps, int Cc, int N, int nk, const float* amax_w,
+                               unsigned short* img) {
+  const int Cco = N / 2, spt = Cc / k3mBKc;
+  const float sw = pow2f(kF16Top - amax_exp(amax_w));
+  const long long total = (long long)nk * 64 * k3mBKc;
+  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
+       idx += (long long)gridDim.x * blockDim.x) {
+    const int k = (int)(idx % k3mBKc), nc = (int)((idx / k3mBKc) % 64), s = (int)(idx / (64 * k3mBKc));
+    const int t = s / spt, c = (s - t * spt) * k3mBKc + k;
+    float wr = 0.f, wi = 0.f;
+    if (nc < Cco) {
+      wr = kernel_value(w, c, nc, taps.ti[t], taps.tj[t]);
+      wi = kernel_value(w, c, Cco + nc, taps.ti[t], taps.tj[t]);
+    }
+    const float vals[3] = {wr, wi - wr, wr + wi};
+    const int chunk = k >> 3, e = k & 7;
+    unsigned short* base = img + (long long)s * k3mImgU4 * 8;
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      const float v = vals[o] * sw;
+      const _Float16 h = (_Float16)v;
+      base[(((o * 2 + 0) * 2 + chunk) * 64 + nc) * 8 + e] = __builtin_bit_cast(unsigned short, h);
+      base[(((o * 2 + 1) * 2 + chunk) * 64 + nc) * 8 + e] =
+          __builtin_bit_cast(unsigned short, (_Float16)(v - (float)h));
+    }
+  }
+}
+
+template <int JM>
+__global__ void __launch_bounds__(kThreads, 2) gather_3m_kernel(const GatherArgs a) {
+  __shared__ __attribute__((aligned(16))) u32x4 sA[2][3 * 2 * 2 * 128];   // 24 KB per stage
+  __shared__ __attribute__((aligned(16))) u32x4 sW[2][k3mImgU4];          // 12 KB per stage
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wn = wave >> 1, wm = wave & 1;
+  const int Cc = a.Cg / 2, spt = Cc / k3mBKc, nk = a.ntaps * spt;
+  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * 128;
+  const int am = tid & 127, kh = tid >> 7;          // staging: position, 8-channel half of the step
+  const int m = m0 + am;
+  const bool mval = m < a.M;
+  int b = 0, hb = 0, wb = 0;
+  if (mval) {
+    const int qhw = a.Qh * a.Qw;
+    b = m / qhw;
+    const int r = m - b * qhw, qh = r / a.Qw, qw = r - qh * a.Qw;
+    hb = qh * a.sh;
+    wb = qw * a.sw;
+  }
+  const int ea = amax_exp(a.amax_a);
+  const float sa = pow2f(kF16Top - ea);
+  const int ush = ea + amax_exp(a.amax_w) - 2 * kF16Top;
+  const long long HiWi = (long long)a.Hi * a.Wi, H2W2 = (long long)a.H2 * a.W2;
+  float xr[8], xi[8];
+  u32x4 rw[3];
+  auto load = [&](int s) __attribute__((always_inline)) {
+    const int t = s / spt, cb = (s - t * spt) * k3mBKc + 8 * kh;   // first complex channel
+    const int hi = hb + a.toffh[t], wi = wb + a.toffw[t];
+    bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+    const float* src = a.X;
+    long long cs = HiWi, off;
+    int cre, cim;
+    if constexpr (JM == 1) {
+      const bool from_x = cb < a.jh;                // a step lies in one jh chunk (jh % 16 == 0)
+      const int c = from_x ? cb : cb - a.jh;
+      cre = c;
+      cim = a.jh + c;
+      ok &= !from_x | (hi < a.H2);                  // F.pad rows of x read 0
+      if (from_x) {
+        src = a.X2;
+        cs = H2W2;
+        off = (long long)b * 2 * a.jh * H2W2 + (long long)hi * a.W2 + wi;
+      } else {
+        off = (long long)b * 2 * a.jh * HiWi + (long long)hi * a.Wi + wi;
+      }
+    } else {
+      cre = cb;
+      cim = Cc + cb;
+      off = (long long)b * a.Cg * HiWi + (long long)hi * a.Wi + wi;
+    }
+    off = ok ? off : 0;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float v0 = src[off + (long long)(cre + j) * cs], v1 = src[off + (long long)(cim + j) * cs];
+      xr[j] = ok ? v0 : 0.f;
+      xi[j] = ok ? v1 : 0.f;
+    }
+    const u32x4* wsrc = reinterpret_cast<const u32x4*>(a.Wp) + (long long)s * k3mImgU4;
+#pragma unroll
+    for (int q = 0; q < 3; ++q) rw[q] = wsrc[tid + kThreads * q];
+  };
+  auto store = [&](int buf) __attribute__((always_inline)) {
+    u32x4 H[3], L[3];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      unsigned h, l;
+      split_f16x2(xr[2 * e] + xi[2 * e], xr[2 * e + 1] + xi[2 * e + 1], sa, h, l);
+      H[0][e] = h; L[0][e] = l;
+      split_f16x2(xr[2 * e], xr[2 * e + 1], sa, h, l);
+      H[1][e] = h; L[1][e] = l;
+      split_f16x2(xi[2 * e], xi[2 * e + 1], sa, h, l);
+      H[2][e] = h; L[2][e] = l;
+    }
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      sA[buf][((o * 2 + 0) * 2 + kh) * 128 + am] = H[o];
+      sA[buf][((o * 2 + 1) * 2 + kh) * 128 + am] = L[o];
+    }
+#pragma unroll
+    for (int q = 0; q < 3; ++q) sW[buf][tid + kThreads * q] = rw[q];
+  };
+  f32x16 acc[3][2];
+#pragma unroll
+  for (int o = 0; o < 3; ++o)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[o][j][r] = 0.f;
+  const int lh = lane >> 5, lr = lane & 31;
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+#pragma unroll
+    for (int o = 0; o < 3; ++o) {
+      u32x4 wf[2], af[2][2];
+#pragma unroll
+      for (int p = 0; p < 2; ++p) {
+        wf[p] = sW[buf][((o * 2 + p) * 2 + lh) * 64 + wn * 32 + lr];
+#pragma unroll
+        for (int j = 0; j < 2; ++j) af[j][p] = sA[buf][((o * 2 + p) * 2 + lh) * 128 + wm * 64 + 32 * j + lr];
+      }
+#pragma unroll
+      for (int t = 0; t < 3; ++t)   // hi*hi, hi*lo, lo*hi
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[o][j] = mfma_32x32x16<true>(wf[t == 2 ? 1 : 0], af[j][t == 1 ? 1 : 0], acc[o][j]);
+    }
+  };
+  if (nk > 0) {
+    load(0);
+    store(0);
+    __syncthreads();
+    for (int s = 0; s < nk; ++s) {
+      const bool more = s + 1 < nk;
+      if (more) load(s + 1);
+      compute(s & 1);
+      if (more) store((s + 1) & 1);
+      __syncthreads();
+    }
+  }
+  // accumulator map: block (o, j) element r2 is output nc = 32 wn + 4 lh + (r2 & 3) + 8 (r2 >> 2),
+  // position m = m0 + 64 wm + 32 j + lr
+  const int Cco = a.N / 2;
+  const long long HoWo = (long long)a.Ho * a.Wo;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int mm = m0 + wm * 64 + 32 * j + lr;
+    if (mm >= a.M) continue;
+    const int qhw = a.Qh * a.Qw;
+    const int bb = mm / qhw, r = mm - bb * qhw, qh = r / a.Qw, qw = r - qh * a.Qw;
+    const long long yb = (long long)bb * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
+#pragma unroll
+    for (int r2 = 0; r2 < 16; ++r2) {
+      const int nc = wn * 32 + 4 * lh + (r2 & 3) + 8 * (r2 >> 2);
+      if (nc >= Cco) continue;
+      const float yre = __builtin_ldexpf(acc[0][j][r2] - acc[2][j][r2], ush) + (a.bias ? a.bias[nc] : 0.f);
+      const float yim = __builtin_ldexpf(acc[0][j][r2] + acc[1][j][r2], ush) + (a.bias ? a.bias[Cco + nc] : 0.f);
+      a.Y[yb + (long long)nc * HoWo] = yre;
+      a.Y[yb + (long long)(Cco + nc) * HoWo] = yim;
+    }
+  }
+}
