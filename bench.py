@@ -433,7 +433,8 @@ def run(args):
                    "parallelism": f"dp{world}"},
         "final_loss": round(loss_v, 4),
         "dist": ({"world": world, "backend": dist_backend, "rccl_version": _rccl_version(),
-                  "launcher": "torchrun" if os.environ.get("TORCHELASTIC_RUN_ID") else "bench.py spawn"}
+                  "launcher": ("torchrun" if os.environ.get("TORCHELASTIC_RUN_ID")
+                               else "bench.py spawn" if os.environ.get("SEHIP_SPAWNED") else "env")}
                  if world > 1 else None),
         "conv_math": default_mode,
         "conv_math_note": "fp32 storage and accumulation everywhere; 'f16x3' scales each operand by a "

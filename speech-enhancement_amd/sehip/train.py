@@ -138,7 +138,8 @@ def free_port() -> int:
 
 def _rank_entry(rank, world, port, target, args):
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK=str(rank),
-                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world))
+                      WORLD_SIZE=str(world), LOCAL_RANK=str(rank), LOCAL_WORLD_SIZE=str(world),
+                      SEHIP_SPAWNED="1")
     target(*args)
 
 

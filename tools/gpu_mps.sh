@@ -1,13 +1,16 @@
-# Weight-grad m-split length A/B (SEHIP_WGRAD_MPS): micro timing + FETCH_SIZE per launch, then bench.
-#   gpurun --timeout 900 -- bash tools/gpu_mps.sh <tag> <mps values...>
-R=$GRAFT_REPO_ROOT
-TAG=${1:-mps}; shift
-O=$R/gpurun_out/$TAG
-mkdir -p $O
-cd /tmp && export TMPDIR=/tmp
-for v in 0 "$@"; do
-  echo "== MPS=$v" >> $O/mps.log
-  SEHIP_WGRAD_MPS=$v timeout -k 10 120 python3 $R/tools/conv_micro.py --layers dec5,enc1 --passes weight --math f16x3 >> $O/mps.log 2>&1 || exit $?
-  SEHIP_WGRAD_MPS=$v timeout -s KILL 120 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_$v -o run --output-format csv -- python3 $R/tools/conv_micro.py --layers dec5,enc1 --passes weight --math f16x3 --iters 1 > $O/pmc_$v.log 2>&1 || exit $?
+# Weight-grad m-split size: PMC traffic per instantiation and a same-box bench A/B per
+# SEHIP_WGRAD_MPS value: gpurun -- bash tools/gpu_mps.sh <tag> <mps values...>
+R=$GRAFT_REPO_ROOT; T=$1; shift; O=$R/gpurun_out/$T; mkdir -p $O; cd /tmp && export TMPDIR=/tmp
+B1="$R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-op-timing --no-compare"
+for v in "$@"; do
+  SEHIP_WGRAD_MPS=$v timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $O/f$v -o run --output-format csv -- python3 $B1 > $O/f$v.log 2>&1 || exit $?
+  SEHIP_WGRAD_MPS=$v timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $O/w$v -o run --output-format csv -- python3 $B1 > $O/w$v.log 2>&1 || exit $?
+  python3 $R/tools/pmc_summary.py $O/f$v $O/w$v $O/pmc_$v.json > $O/pmc_$v.log 2>&1 || exit $?
 done
-echo done > $O/ok
+B="$R/bench.py --steps 20 --warmup 5 --no-cpu-baseline --no-op-timing --no-compare"
+for i in 1 2; do
+  for v in "$@"; do
+    SEHIP_WGRAD_MPS=$v timeout -k 10 200 python3 $B > $O/bench_${v}_$i.json 2> $O/bench_${v}_$i.err || exit $?
+  done
+done
+echo ok > $O/ok
