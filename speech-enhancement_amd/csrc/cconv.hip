@@ -185,6 +185,9 @@ struct GatherArgs {
   // merged stride-phase classes (merge_h_phases): output columns n' >= mrg_np are
   // channel n' - mrg_np of output row 1 + Sh * qh (rows >= Ho dropped); 0 = off
   int mrg_np;
+  // merged classes: bit t set = tap t has no weight in phase 0 (mrg_zero0) / phase 1
+  // (mrg_zero1), so that half's waves skip the tap's K-steps (exact zero products)
+  unsigned long long mrg_zero0, mrg_zero1;
   int accum;           // data-grad: Y += result (se_conv2d_desc.accumulate_dx)
   // forward, se_conv2d_desc.moments: the CBN moment rows of each M-tile (rows
   // mom_p0 + tile of mom_P; [N/2][mom_P][5] fp64 sums, then [N/2][mom_P][4] extrema)
@@ -1659,6 +1662,14 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
     a.mrg_np = c.mrg ? c.taps.mrg_np : 0;
+    if (c.mrg && !env_flag_off("SEHIP_MERGE_SKIP")) {   // SEHIP_MERGE_SKIP=0: multiply the zero taps
+      for (int t = 0; t < c.taps.n; ++t) {
+        if (c.taps.ti[t] < 0) a.mrg_zero0 |= 1ull << t;
+        if (c.taps.ti2[t] < 0) a.mrg_zero1 |= 1ull << t;
+      }
+      a.ntaps = c.taps.n;
+      a.kblk = kblk;
+    }
     a.accum = g.accum;
     if (g.mom) {
       a.mom = (double*)g.mom;

@@ -565,6 +565,23 @@ gather_x3_kernel(const GatherArgs a) {
       __syncthreads();
     }
   } else {
+    // merged stride-phase classes on 256-column tiles: a wave whose 64 columns lie in
+    // a phase without weight at the step's tap skips that step's fragment reads and
+    // MFMAs (they would add exact zeros) and only stages; the other path keeps its
+    // interleaved schedule
+    constexpr bool MSK = NW == 2 && JM != 2;   // instantiations a merged class can run on
+    const unsigned long long zmask =
+        (MSK && a.mrg_np) ? (wn * TN < a.mrg_np ? a.mrg_zero0 : a.mrg_zero1) : 0ull;
+    auto skip = [&](int kt) __attribute__((always_inline)) {
+      if constexpr (!MSK) {
+        return false;
+      } else {
+        if (!zmask) return false;
+        int t, c;
+        split_k(kt * kBK, a.Cg, a.ntaps, a.kblk, t, c);
+        return ((zmask >> t) & 1ull) != 0;
+      }
+    };
     load_tile(s0, 0);
     store_tile(s0, 0);
     if (nk > 1) load_tile(s1, kBK);
@@ -572,17 +589,25 @@ gather_x3_kernel(const GatherArgs a) {
     int kt = 0;
     for (; kt + 1 < nk; kt += 2) {
       load_tile(s0, min(kt + 2, nk - 1) * kBK);
-      compute(0);
-      store_tile(s1, 1);
-      interleave();
+      if (skip(kt)) {
+        store_tile(s1, 1);
+      } else {
+        compute(0);
+        store_tile(s1, 1);
+        interleave();
+      }
       __syncthreads();
       load_tile(s1, min(kt + 3, nk - 1) * kBK);
-      compute(1);
-      store_tile(s0, 0);
-      interleave();
+      if (skip(kt + 1)) {
+        store_tile(s0, 0);
+      } else {
+        compute(1);
+        store_tile(s0, 0);
+        interleave();
+      }
       __syncthreads();
     }
-    if (kt < nk) compute(0);
+    if (kt < nk && !skip(kt)) compute(0);
   }
   if constexpr (F16 && TERMS == 3) {   // undo the operand scales (exact)
 #pragma unroll

@@ -242,3 +242,22 @@ def test_conv_16bit_storage(name, tr, cin, cout, shape, stride, dtype, tol, gpu_
               f"{torch.equal(nat[k], cast[k])}")
         assert torch.equal(nat[k], cast[k]), (name, k)
         assert e < tol, (name, k, e)
+
+
+def test_merged_phase_zero_tap_skip_frcrn(gpu_device, monkeypatch):
+    """The merged classes' zero-tap skip (a phase's waves skip the K-steps of taps it has no
+    weight at) on the FRCRN decoder's joined forward: the model output with SEHIP_FWD_MERGE=1
+    is bit-identical with and without the skip and to the default two-class form."""
+    import paramfill
+    from sehip.models import FRCRN
+    noisy, _ = (torch.from_numpy(t).cuda() for t in paramfill.structured_pair(2, 16000, seed=60))
+    outs = []
+    for merge, skip in (("0", "1"), ("1", "1"), ("1", "0")):
+        monkeypatch.setenv("SEHIP_FWD_MERGE", merge)
+        monkeypatch.setenv("SEHIP_MERGE_SKIP", skip)
+        m = paramfill.fill_(FRCRN(), seed=9).cuda().train()
+        spec, wav = m(noisy)
+        torch.cuda.synchronize()
+        outs.append((spec.detach(), wav.detach()))
+    for o in outs[1:]:
+        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])
