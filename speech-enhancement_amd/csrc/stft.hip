@@ -418,7 +418,12 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
 // (tools/stft_micro.py; the XCD-aware block order merges the 32-B row segments
 // of neighbouring blocks in one L2)
 constexpr int kPairsIP = 4;
-template <int CN, int P = kPairsIP, bool LP = false>
+// FUSE: the first FFT pass reads its butterfly inputs straight from the signal
+// (each thread gathers the R0 windowed samples j + q N/R0 of its butterfly, skipping
+// the zero padding past win) and writes only its outputs to LDS: one LDS round trip
+// and two barriers fewer per block, the same values and operations (bit-identical
+// up to the sign of exact zeros).
+template <int CN, int P = kPairsIP, bool LP = false, bool FUSE = false>
 __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a) {
   constexpr int TPB = kThreads;
   constexpr int N = CN;
@@ -429,6 +434,46 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   const int t0 = tb * 2 * P;
   const long long xo = (long long)b * a.L;
   for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
+  if constexpr (FUSE) {
+    constexpr CPlan pl = make_cplan(N);
+    constexpr int R0 = pl.radix[0], nbf0 = N / R0;
+    constexpr int IT0 = (P * nbf0 + TPB - 1) / TPB;
+    float2 v[IT0][kMaxRadix];
+#pragma unroll
+    for (int it = 0; it < IT0; ++it) {
+      const int idx = threadIdx.x + it * TPB;
+      const int pr = idx / nbf0, j = idx - pr * nbf0;
+      const int ta = t0 + 2 * pr, tb2 = ta + 1;
+      const bool live = idx < P * nbf0;
+#pragma unroll
+      for (int q = 0; q < R0; ++q) {
+        const int n = j + q * nbf0;
+        const bool ok = live && n < a.win;
+        const int nn = ok ? n : 0;
+        const float w = ok ? a.window[nn] : 0.f;
+        float ya = 0.f, yb = 0.f;
+        if (ok) {
+          const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+          const float xb = ldx<LP>(a.x, xo + reflect_index(min(tb2, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+          ya = ta < a.T ? w * xa : 0.f;
+          yb = tb2 < a.T ? w * xb : 0.f;
+        }
+        v[it][q] = make_float2(ya, yb);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < IT0; ++it) {
+      const int idx = threadIdx.x + it * TPB;
+      if (idx < P * nbf0) {
+        const int pr = idx / nbf0, j = idx - pr * nbf0;
+        butterfly<R0>(v[it], A + pr * N, j * R0, 1);
+      }
+    }
+    __syncthreads();
+    fft_pass_ip<N, P, 1, R0, TPB>(A, stw);
+    unpack_store<CN, P, LP>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
+    return;
+  }
   // frame gather: all of a thread's loads are issued before any is used
   // (compile-time trip count; branch-free clamped addresses and zero weights),
   // so the block pays one memory latency instead of one per element
@@ -860,6 +905,13 @@ extern "C" int se_stft_num_frames(int L, int win, int hop, int nfft, int center)
   return (Lp - win) / hop + 1;
 }
 
+// SEHIP_STFT_FUSE=0 / 1: the in-place ConvSTFT without / with the first FFT pass fused
+// into the signal gather (read per call)
+static bool stft_fuse_on() {
+  const char* e = std::getenv("SEHIP_STFT_FUSE");
+  return e && e[0] == '1';
+}
+
 extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, int win,
                            int hop, int nfft, int center, int mag_phase, const float* window,
                            const float* twiddle, int dtype, void* stream) {
@@ -888,9 +940,12 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
     const int P = ip_pairs;
     const dim3 grid(se::ceil_div(T, 2 * P), B);
     hipStream_t st = se::as_stream(stream);
+    const bool fuse = stft_fuse_on();
 #define SE_STFT_IP(NF)                                                                              \
   do {                                                                                              \
     if (P == 2) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 2, grid, 0, st, a);                     \
+    else if (P == 4 && fuse && a.dt == SE_DTYPE_F32)                                                \
+      hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 4, false, true>), grid, dim3(kThreads), 0, st, a); \
     else if (P == 4) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 4, grid, 0, st, a);                \
     else if (P == 16) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 16, grid, 0, st, a);              \
     else SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 8, grid, 0, st, a);                            \
