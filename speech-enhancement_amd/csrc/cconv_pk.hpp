@@ -384,7 +384,7 @@ wgrad_pk_kernel(const WgradArgs a) {
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const int s = 4 * j + s0;                   // position row of the LDS image
-      const int ch = sl ^ (((s & 3) << 2) | ((s >> 2) & 3));   // source chunk (16 B = 8 channels)
+      const int ch = sl ^ wx3_swz(s);   // source chunk (16 B = 8 channels)
       const int qw = qw0 + s;
       const _Float16* src = zero;
       if (isG) {

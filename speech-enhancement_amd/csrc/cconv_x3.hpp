@@ -131,9 +131,21 @@ __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, 
 // those reads conflict-free and also the 16x16x32 reads (lane -> row l & 15 of a
 // 16-row block, chunk l >> 4): in every lane group the 16 lanes hit the 16
 // distinct 16-B slots of a 256-B bank row.
+// SEHIP_SWZ2 (round 3): x3_swz = bit 2 of the row | (bit 1 ^ bit 4) << 1 keeps the
+// fragment reads conflict-free (in each ds_read_b128 lane group {0-3,12-15,20-27},
+// {4-11,16-19,28-31} the 16 (row & 3, swizzle) pairs are distinct) and also makes
+// the activation tile's ds_write_b128 stores conflict-free (8 consecutive rows in
+// one 8-lane store group land on 8 distinct 16-B slots of a 128-B bank row); the
+// (row >> 2) & 3 form left every store group 2-way conflicted (PMC: bank-conflict
+// cycles 12-20 % of the LDS-array cycles of the gather GEMMs, tools/pmc_lds.sh).
+#ifndef SEHIP_SWZ2
+#define SEHIP_SWZ2 1
+#endif
 __device__ __forceinline__ int x3_swz(int row) {
 #if SEHIP_GEMM_M16
   return (0x69F0 >> (((row >> 2) & 7) * 2)) & 3;
+#elif SEHIP_SWZ2
+  return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 4)) & 1) << 1);
 #else
   return (row >> 2) & 3;
 #endif
@@ -792,8 +804,20 @@ gather_x3_kernel(const GatherArgs a) {
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
+// chunk swizzle of position row s (an involution on the 16 chunks)
+__device__ __forceinline__ int wx3_swz(int s) {
+#if SEHIP_SWZ2
+  // bits 2-3 = s & 3 keep the transposed reads conflict-free (4 consecutive positions x 4
+  // chunks on 16 distinct 16-B slots); bits 0-2 = (s1, s2, s0) put 8 consecutive positions
+  // of one ds_write_b128 store group on 8 distinct slots (the form below: 2-way, which
+  // was a third of the weight-grads' LDS-array cycles, tools/pmc_lds.sh)
+  return ((s & 3) << 2) | (((s >> 2) & 1) << 1) | ((s >> 1) & 1);
+#else
+  return ((s & 3) << 2) | ((s >> 2) & 3);
+#endif
+}
 __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chunk ch of position row s
-  return 256 * s + 16 * (ch ^ (((s & 3) << 2) | ((s >> 2) & 3)));
+  return 256 * s + 16 * (ch ^ wx3_swz(s));
 }
 
 // DJ: D is the decoder skip join (WgradArgs::D2, a transposed conv's input).
