@@ -349,7 +349,15 @@ class ComplexBatchNorm2d(nn.Module):
         """BN followed by a fused activation (LeakyReLU / ReLU, or the weight of a
         one-parameter nn.PReLU). fork=True returns (y, alias of y) for two consumers
         (see functional.complex_batch_norm). x may be fp32, bf16 or fp16 storage, with
-        the module in the same dtype (model.to(bfloat16) / .half())."""
+        the module in the same dtype (model.to(bfloat16) / .half()). A module whose dtype
+        differs from x's (e.g. an fp32 module fed bf16 activations under autocast) runs
+        its kernels on x cast to the module dtype and returns the result in x's dtype,
+        as the reference's pure-torch CBN computes in the promoted type."""
+        mdt = _module_dtype(self, x.dtype)
+        if mdt != x.dtype:
+            y = self.forward_act(x.to(mdt), act, slope, False, None if prelu is None else prelu.to(mdt))
+            y = y.to(x.dtype)
+            return (y, y) if fork else y
         running = (self.RMr, self.RMi, self.RVrr, self.RVri, self.RVii) if self.track_running_stats else None
         training = self.training or not self.track_running_stats    # complex_nn.py:234
         return F.complex_batch_norm(
@@ -384,14 +392,14 @@ def norm_act(norm: nn.Module, act: nn.Module, x, fork: bool = False):
     the kinds the kernel knows; otherwise the two modules are applied in turn.
     fork=True returns (y, y2) for two consumers of y: with the CBN kernel y2 is an
     alias whose gradient the CBN backward sums itself; otherwise y2 is y."""
-    if isinstance(norm, ComplexBatchNorm2d) and _module_dtype(norm, x.dtype) == x.dtype:
+    if isinstance(norm, ComplexBatchNorm2d):     # forward_act casts a dtype mismatch itself
         if isinstance(act, nn.LeakyReLU):
             return norm.forward_act(x, F.ACT_LEAKY, act.negative_slope, fork)
         if isinstance(act, nn.ReLU):
             return norm.forward_act(x, F.ACT_RELU, 0.0, fork)
         if isinstance(act, nn.Identity):
             return norm.forward_act(x, fork=fork)
-        if isinstance(act, nn.PReLU) and act.weight.numel() == 1 and act.weight.dtype == x.dtype:
+        if isinstance(act, nn.PReLU) and act.weight.numel() == 1:
             return norm.forward_act(x, fork=fork, prelu=act.weight)   # DCCRN, dccrn.py:21,45
     y = act(norm(x))
     return (y, y) if fork else y

@@ -261,7 +261,11 @@ class AudioDataLoader:
     chunk_size and stacked on the device (AudioSpliter.collate, se_crop_pad).
     Items shorter than least_samples are dropped (audio_dataloader.py:32-34).
     Yields {'mix': [B, 1, chunk], 'ref': [[B, 1, chunk], ...]} on `device`;
-    len() is the dataset length, as the reference's."""
+    len() is the dataset length, as the reference's.
+    The chunk-start draws are made in this (main) process with `rng`. The reference
+    makes them inside its collate_fn, i.e. in each DataLoader worker's own seeded
+    `random` when num_workers > 0, so a seeded run picks the reference's crops only
+    with num_workers=0."""
 
     def __init__(self, dataset, chunk_size=32000, least_samples=16000, device="cuda", rng=None, **kwargs):
         from torch.utils.data import DataLoader

@@ -1244,9 +1244,13 @@ def _wide_launched(status: torch.Tensor) -> None:
     """After a wide launch: a non-blocking copy of its status word to pinned host
     memory, checked by lstm_wide_poll once the launch has finished."""
     host = torch.empty(1, dtype=torch.int32, pin_memory=True)
-    host.copy_(status, non_blocking=True)
-    ev = torch.cuda.Event()
-    ev.record()
+    # the launch went to status.device's current stream (N.stream_of), which need not
+    # be the current device's: copy and record on that stream
+    stream = torch.cuda.current_stream(status.device)
+    with torch.cuda.device(status.device), torch.cuda.stream(stream):
+        host.copy_(status, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(stream)
     _WIDE_PENDING.append((ev, host))
 
 

@@ -95,13 +95,13 @@ def test_frcrn_level_spread_train_step_grads_vs_fp64(gpu_device):
     items included): SI-SNR makes each utterance's gradient scale as 1/level,
     so the backward's operands spread as widely as the forward's. Gate as
     test_frcrn_train_step_golden: every parameter gradient within
-    max(3x the fp32 oracle's error, 3x its 2-ulp sensitivity, 1e-3) of fp64, the
+    max(3x the fp32 oracle's error, 3x its 2-ulp sensitivity, 1e-4) of fp64, the
     median within 3x the fp32 oracle's median. The sensitivity is the largest move
     of the fp32 oracle over four perturbations of the input and the weights at
     2^-20 relative: the size of the HIP path's own deviation from fp64 (per conv
     4.0e-7 f16x3 / 6.4e-7 exact fp32 MFMA; at the model output 1-2.6e-6 per
     utterance, test_frcrn_b16_level_spread_per_utterance_vs_oracle). For a
-    well-conditioned gradient that move is ~1e-6, far under the 1e-3 floor, so the
+    well-conditioned gradient that move is ~1e-6, under the 1e-4 floor, so the
     gate only widens for the chaotic ones: a few CCBAM spatial-attention gradients route
     through channel max-pools whose argmax flips under any re-rounding. Measured on
     the CPU oracle for skip layer 3's spatial...norm.Wri (fp32 vs fp64: 6.2e-3):
@@ -128,7 +128,7 @@ def test_frcrn_level_spread_train_step_grads_vs_fp64(gpu_device):
     worst = max(errs, key=lambda e: e[0] / max(e[1], e[2], 1e-12))
     print(f"gains {np.log2(gains).round(2)}: median grad err vs fp64 hip {med_hip:.2e} cpu-fp32 {med_32:.2e}; "
           f"worst ratio {worst}")
-    bad = [e for e in errs if e[0] > max(3 * e[1], 3 * e[2], 1e-3)]
+    bad = [e for e in errs if e[0] > max(3 * e[1], 3 * e[2], 1e-4)]
     assert not bad, bad[:5]
     assert med_hip < 3 * med_32, (med_hip, med_32)
 

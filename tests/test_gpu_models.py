@@ -82,10 +82,10 @@ def test_bf16_configs_within_oracle_bf16_drift(i, mode, storage, gpu_device):
             with torch.no_grad():
                 spec, wav = m(x)
         else:
-            spec, wav = m(x)
-            (wav.float().square().mean() + spec.float().square().mean()).backward()
-            assert all(p.grad is not None and p.grad.dtype == sdt and torch.isfinite(p.grad).all()
-                       for p in m.parameters() if p.requires_grad)
+            # forward drift only here; the training gradients of this config are gated
+            # per tensor against fp64 in test_dccrn_train_grads_vs_fp64 below
+            with torch.no_grad():
+                spec, wav = m(x)
         torch.cuda.synchronize()
         assert spec.dtype == sdt and wav.dtype == sdt
         es = rel_l2(spec.detach().float().cpu().numpy(), g[f"spec_{mode}"])
@@ -97,6 +97,79 @@ def test_bf16_configs_within_oracle_bf16_drift(i, mode, storage, gpu_device):
         assert es < 1.25 * ds and ew < 1.25 * dw, (name, es, ew, ds, dw)
     finally:
         F.set_conv_math(prev)
+
+
+def _dccrn_grads(dev, dtype, perturb=0.0, sehip=False):
+    """DCCRN-CL (_2008_00264_dccrn.py:148-212) train-mode forward on a structured
+    noisy/clean pair, SI-SNR (losses.py:62-84) on the fp32-cast waveform, backward.
+    Every parameter gradient (the conv encoder/decoder with output_padding, the CBN +
+    one-weight PReLU blocks, the LSTMBlock + ComplexLinear, the 'E' mask's tanh(|M|)
+    and atan2 phase path) as fp64 on the CPU."""
+    from oracle import models as O, train as OT
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=41)
+    if sehip:
+        from sehip import models as M
+        from sehip.losses import SI_SNR_loss as loss_fn, pad_or_truncate_wav as pad
+        m = M.DCCRN("dccrn-CL", 400, 100, 512)
+    else:
+        loss_fn, pad = OT.si_snr_loss, OT.pad_or_truncate_wav
+        m = O.DCCRN("dccrn-CL", 400, 100, 512)
+    m = paramfill.fill_(m, seed=21).to(dev).to(dtype).train()
+    x = torch.from_numpy(noisy).to(dtype)
+    if perturb:   # a ~1-ulp relative perturbation of the input (fixed seed)
+        gen = torch.Generator().manual_seed(1234)
+        x = x * (1 + perturb * torch.randn(x.shape, generator=gen, dtype=torch.float64)).to(dtype)
+    c = torch.from_numpy(clean).to(dev)
+    _, w = m(x.to(dev))
+    loss_fn(pad(w.float(), c), c).backward()
+    return {n: p.grad.detach().double().cpu() for n, p in m.named_parameters()}
+
+
+@pytest.mark.parametrize("storage", ["fp32", "bf16"])
+def test_dccrn_train_grads_vs_fp64(storage, gpu_device):
+    """BASELINE config 3 is DCCRN *training*: its gradients against an fp64 CPU run of the
+    oracle, per parameter tensor.
+    fp32: the default conv math (f16x3 split MFMA, exact-fp32 first conv), gated like
+    FRCRN's: each tensor within max(3x the fp32 oracle's error, 3x its sensitivity to a
+    2^-22 input perturbation, 1e-4) of fp64, and the median within 3x the fp32 oracle's.
+    bf16: model.to(torch.bfloat16) with SE_MATH_BF16 (the config's own precision) against
+    the oracle's own bf16 CPU backward: each tensor within max(3x the bf16 oracle's error,
+    3x its move under a 2^-7 input perturbation) of fp64, all gradients together within 2x
+    the bf16 oracle's error, and the median within 1.5x of its median."""
+    from sehip import functional as F
+    sdt = torch.float32 if storage == "fp32" else torch.bfloat16
+    g64 = _dccrn_grads("cpu", torch.float64)
+    go = _dccrn_grads("cpu", sdt)
+    gp = _dccrn_grads("cpu", sdt, perturb=2.0 ** -22 if storage == "fp32" else 2.0 ** -7)
+    prev = F.get_conv_math()
+    if storage == "bf16":
+        F.set_conv_math("bf16")
+    try:
+        gh = _dccrn_grads("cuda", sdt, sehip=True)
+    finally:
+        F.set_conv_math(prev)
+    assert sorted(gh) == sorted(g64) and len(gh) > 100
+    rows = []
+    for n in g64:
+        d = g64[n].norm().item() + 1e-30
+        rows.append(((gh[n] - g64[n]).norm().item() / d, (go[n] - g64[n]).norm().item() / d,
+                     (gp[n] - go[n]).norm().item() / d, n))
+    floor = 1e-4 if storage == "fp32" else 0.0
+    bad = [r for r in rows if r[0] > max(3 * r[1], 3 * r[2], floor)]
+    med_h, med_o = np.median([r[0] for r in rows]), np.median([r[1] for r in rows])
+    cat = lambda g: torch.cat([g[n].flatten() for n in sorted(g64)])
+    b = cat(g64)
+    e_h, e_o = ((cat(gh) - b).norm() / b.norm()).item(), ((cat(go) - b).norm() / b.norm()).item()
+    print(f"dccrn {storage}: median per-tensor vs fp64 hip {med_h:.2e} oracle {med_o:.2e}; "
+          f"all grads hip {e_h:.2e} oracle {e_o:.2e}; worst hip/oracle ratio "
+          f"{max(r[0] / max(r[1], r[2], 1e-30) for r in rows):.2f}")
+    assert not bad, sorted(bad, key=lambda r: -r[0])[:5]
+    if storage == "fp32":
+        assert med_h < 3 * med_o, (med_h, med_o)
+        assert e_h < 2 * e_o + 1e-6, (e_h, e_o)
+    else:
+        assert med_h < 1.5 * med_o, (med_h, med_o)
+        assert e_h < 2 * e_o, (e_h, e_o)
 
 
 def test_state_dict_keys_match_oracle(gpu_device):
@@ -149,7 +222,7 @@ def test_frcrn_train_step_golden(gpu_device):
     # measured two ways: the fp32 oracle's error, and how far the fp32 oracle
     # moves when the input is perturbed by ~2 ulps (an equally valid fp32
     # evaluation; it captures sensitivity to summation order). Every HIP
-    # gradient must be within max(3x either, 1e-3) of fp64 (rel-L2 per tensor),
+    # gradient must be within max(3x either, 1e-4) of fp64 (rel-L2 per tensor),
     # and the median over tensors within 3x the fp32 oracle's median.
     g64, g32 = _oracle_grads(torch.float64), _oracle_grads(torch.float32)
     g32p = _oracle_grads(torch.float32, perturb=2.0 ** -22)
@@ -159,7 +232,10 @@ def test_frcrn_train_step_golden(gpu_device):
         errs.append(((p.grad.double().cpu() - g64[n]).norm().item() / d,
                      (g32[n] - g64[n]).norm().item() / d,
                      (g32p[n] - g32[n]).norm().item() / d, n))
-    bad = [e for e in errs if e[0] > max(3 * e[1], 3 * e[2], 1e-3)]
+    bad = [e for e in errs if e[0] > max(3 * e[1], 3 * e[2], 1e-4)]
+    worst = max(errs, key=lambda e: e[0] / max(e[1], e[2], 1e-12))
+    print(f"frcrn grads vs fp64: median hip {np.median([e[0] for e in errs]):.2e} "
+          f"cpu-fp32 {np.median([e[1] for e in errs]):.2e}; worst ratio {worst}")
     assert not bad, bad[:5]
     assert np.median([e[0] for e in errs]) < 3 * np.median([e[1] for e in errs])
     total = torch.nn.utils.clip_grad_norm_(m.parameters(), 0.5)
