@@ -28,9 +28,11 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 6   /* 6: LSTM layer GEMMs (se_gemm, se_colsum);
-                                 5: prepared data-grad weight images (se_conv2d_prep_data_weights),
-                                 CBN moments from the conv forward (se_conv2d_desc.moments);
+#define SEHIP_ABI_VERSION 7   /* 7: measured-neutral variants removed (se_conv2d_desc.accumulate_dx /
+                                 .moments, se_cbn_*_fwd_moments, se_stream_create_cu_subset); CL16
+                                 operands read by the weight-grad only;
+                                 6: LSTM layer GEMMs (se_gemm, se_colsum);
+                                 5: prepared data-grad weight images (se_conv2d_prep_data_weights);
                                  4: SE_DTYPE storage types (CBN), first-block fused backward, se_resample */
 
 enum {
@@ -47,12 +49,6 @@ const char* se_strerror(int code);
 
 /* Loader self-test: out[i] = 3*i + 1 for i < n (one tiny kernel). */
 int se_probe(int* out, int n, void* stream);
-
-/* A HIP stream on a subset of the CUs (CU i enabled when i % den < num), and
- * its release. The deferred weight-grad side stream of the Python host uses one
- * (SEHIP_WGRAD_CUS=num/den). */
-int se_stream_create_cu_subset(int num, int den, void** stream);
-int se_stream_destroy(void* stream);
 
 /* ------------------------------------------------------------------------
  * ConvSTFT / ConviSTFT (models/conv_stft.py:7-116)
@@ -151,11 +147,12 @@ typedef struct se_conv2d_desc {
    * apply, se_amax) fill it for free. */
   const float* x_amax;
   const float* dy_amax;
-  /* SE_MATH_F16X3 only, optional: the conv input x (for the joined entry
-   * points: s in x_packed, x in x2_packed) and dy in CL16 form (se_pack_cl16,
-   * made with the x_amax / dy_amax bound passed here). When given, the
-   * forward / data-grad GEMMs stage them by LDS-DMA instead of gathering and
-   * splitting fp32. NULL = gather the fp32 tensor. */
+  /* SE_MATH_F16X3 weight-grad only, optional: the conv input x (for the joined
+   * entry points: s in x_packed, x in x2_packed) and dy in CL16 form
+   * (se_pack_cl16, made with the x_amax / dy_amax bound passed here). When all
+   * the pass reads are given, the weight-grad GEMM stages them by LDS-DMA
+   * instead of gathering and splitting fp32. NULL = gather the fp32 tensor.
+   * The forward / data-grad passes return SE_E_UNSUPPORTED when given one. */
   const void* x_packed;
   const void* x2_packed;
   const void* dy_packed;
@@ -164,15 +161,6 @@ typedef struct se_conv2d_desc {
    * and data-grad passes of one conv call share it (the weights do not change
    * between them); NULL = the pass computes it itself (two reductions). */
   const float* w_amax;
-  /* se_conv2d_bwd_data only (ABI 3): 1 = add the input gradient into dx
-   * (dx += dL/dx) instead of overwriting it. For a conv input with a second
-   * consumer whose gradient already sits in dx (FRCRN: an encoder block output
-   * that also feeds a decoder skip): the consumer's CBN backward then reads one
-   * gradient tensor instead of two. Supported on the split GEMM kernels
-   * (SE_MATH_BF16X3 / SE_MATH_BF16 / SE_MATH_F16X3 with more than 64 input
-   * channels, non-joined, fp32 dx); other shapes return SE_E_UNSUPPORTED before
-   * launching anything. */
-  int accumulate_dx;
   /* ABI 4: SE_DTYPE_* storage of x, y, dy, dx, the weights, the biases and their
    * gradients. 16-bit storage (the reference's model.to(bfloat16) / .half()
    * runs) reads and writes those tensors as they are and computes with the
@@ -189,21 +177,7 @@ typedef struct se_conv2d_desc {
    * launch runs beside nothing, instead of in the backward, where it waits for CU
    * slots behind the side stream's weight-grad GEMMs. NULL = build it in ws. */
   const void* data_weights;
-  /* ABI 5, se_conv2d_fwd / se_conv2d_fwd_joined only, optional: a device buffer of
-   * se_conv2d_moments_rows(d) = P rows that receives the ComplexBatchNorm moments of
-   * the output y, so that a following se_cbn_fwd_moments / se_cbn_head_fwd_moments
-   * skips its pass over y. Layout: [N/2][P][5] double sums of (yr, yi, yr^2, yr yi,
-   * yi^2) per complex channel (columns c and c + N/2) and output M-tile, then
-   * [N/2][P][4] float extrema (max yr, -min yr, max yi, -min yi): N/2 * P * 56 bytes.
-   * Supported on the split-fp16 forward (SE_MATH_F16X3, fp32 storage, 64 < N <= 256,
-   * not CL16-packed); other cases return SE_E_UNSUPPORTED before launching. NULL = none.
-   * The reference computes these moments inside ComplexBatchNorm2d.forward
-   * (complex_nn.py:235-260). */
-  void* moments;
 } se_conv2d_desc;
-
-/* Rows P of the moments buffer of a forward pass (0 on an invalid desc). */
-int se_conv2d_moments_rows(const se_conv2d_desc* d);
 
 /* Bytes of the data-grad weight image of d (0 on an invalid desc). */
 size_t se_conv2d_data_weights_size(const se_conv2d_desc* d);
@@ -329,15 +303,6 @@ int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
                float momentum, int act, float slope, float* y_amax,
                const void* prelu_w, int dtype, void* ws, size_t ws_bytes, void* stream);
 
-/* ABI 5: the training forward of se_cbn_fwd (fp32 storage) from moment rows a
- * producing conv already wrote (se_conv2d_desc.moments, P =
- * se_conv2d_moments_rows of that conv): no pass over x for the statistics, only
- * the finalize (running update, save, y_amax) and the apply. */
-int se_cbn_fwd_moments(const void* moments, int P, const float* x, float* y, int B, int C, int HW,
-                       const float* const* params, float* const* running, int64_t* nbt, float* save,
-                       float eps, float momentum, int act, float slope, float* y_amax,
-                       const float* prelu_w, void* stream);
-
 /* Backward. gy = dL/dy (after the activation), x = forward input. y (the
  * forward output) is NOT read and may be NULL: the activation derivative is
  * taken from the pre-activation Z(x - M) + B recomputed from x and `save`.
@@ -383,13 +348,6 @@ int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, int W,
                     float* save, int training, float eps, float momentum, int act,
                     float slope, const float* w_head, int out_channels, int kernel_w,
                     void* ws, size_t ws_bytes, void* stream);
-
-/* ABI 5: se_cbn_head_fwd in training from the producing conv's moment rows (as
- * se_cbn_fwd_moments; no workspace). */
-int se_cbn_head_fwd_moments(const void* moments, int P, const float* x, float* out, int B, int C, int H, int W,
-                            const float* const* params, float* const* running, int64_t* nbt, float* save,
-                            float eps, float momentum, int act, float slope, const float* w_head,
-                            int out_channels, int kernel_w, void* stream);
 
 int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int B, int C, int H, int W,
                     const float* const* params, const float* save, float* const* dparams,

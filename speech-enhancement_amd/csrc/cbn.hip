@@ -969,21 +969,9 @@ cbn_head_apply_kernel(const float* __restrict__ x, float* __restrict__ out, int 
   }
 }
 
-// 16-B apply kernels where HW % 4 == 0 (SEHIP_CBN_VEC=0: the scalar kernels; read once)
-bool vec_ok() {
-  static const bool on = [] {
-    const char* e = std::getenv("SEHIP_CBN_VEC");
-    return !(e && e[0] == '0');
-  }();
-  return on;
-}
-
-// moments workgroups per pass: Cc x P ~ 2048 (SEHIP_CBN_WG overrides; read once)
+// moments workgroups per pass: Cc x P ~ 2048 (1024 / 4096 measured slower)
 int pick_P(int B, int Cc, int HW) {
-  static const int wg = [] {
-    const char* e = std::getenv("SEHIP_CBN_WG");
-    return e ? std::max(64, std::atoi(e)) : 2048;
-  }();
+  constexpr int wg = 2048;
   const int rows = B * ((HW + kSeg - 1) / kSeg);
   return std::max(1, std::min(rows, std::max(1, wg / std::max(Cc, 1))));
 }
@@ -1027,23 +1015,19 @@ static double* pwpart_of(void* ws, int Cc, int P, int ns) {
 namespace {
 
 // moments + finalize of the training forward (running update, save, y bound)
-// pre: the moment rows a producer already wrote (se_conv2d_desc.moments: [Cc][preP][5]
-// fp64 sums, then [Cc][preP][4] extrema, the layout of part / ext), so no moments pass.
 template <typename T>
 int cbn_stats(const T* x, int B, int C, int HW, const void* const* params, void* const* running,
               int64_t* nbt, float* save, int training, float eps, float momentum, float* y_amax,
-              void* ws, hipStream_t st, const void* pre = nullptr, int preP = 0) {
+              void* ws, hipStream_t st) {
   const int Cc = C / 2;
-  const int P = pre ? preP : pick_P(B, Cc, HW);
-  double* part = pre ? (double*)pre : (double*)ws;
-  float* ext = pre ? (float*)(part + (size_t)Cc * P * 5) : ext_of(ws, Cc, P, 7);
+  const int P = pick_P(B, Cc, HW);
+  double* part = (double*)ws;
+  float* ext = ext_of(ws, Cc, P, 7);
   Ptr5 pp{};
   MPtr5 rp{};
   if (params) for (int k = 0; k < 5; ++k) pp.p[k] = params[k];
   if (running) for (int k = 0; k < 5; ++k) rp.p[k] = running[k];
-  if (training && pre) {
-    if (y_amax && hipMemsetAsync(y_amax, 0, sizeof(float), st) != hipSuccess) return SE_E_LAUNCH;
-  } else if (training) {
+  if (training) {
     hipLaunchKernelGGL(cbn_moments_kernel<T>, dim3(Cc, P), dim3(kThreads), 0, st, x, B, C, HW, P, part, ext,
                        y_amax);
     SE_LAUNCH_CHECK();
@@ -1058,13 +1042,12 @@ int cbn_stats(const T* x, int B, int C, int HW, const void* const* params, void*
 template <typename T>
 int cbn_fwd_t(const T* x, T* y, int B, int C, int HW, const void* const* params, void* const* running,
               int64_t* nbt, float* save, int training, float eps, float momentum, int act, float slope,
-              float* y_amax, const T* pw, void* ws, hipStream_t st, const void* pre = nullptr, int preP = 0) {
-  const int rc = cbn_stats<T>(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st,
-                              pre, preP);
+              float* y_amax, const T* pw, void* ws, hipStream_t st) {
+  const int rc = cbn_stats<T>(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st);
   if (rc != SE_OK) return rc;
   int64_t* nb = (training && running) ? nbt : nullptr;
   const dim3 grid(se::ceil_div(HW, kThreads * 4), C / 2, B);
-  if (HW % 4 == 0 && vec_ok())
+  if (HW % 4 == 0)
     hipLaunchKernelGGL(cbn_apply4_kernel<T>, grid, dim3(kThreads), 0, st, x, y, C, HW, save, act, slope, nb, pw);
   else
     hipLaunchKernelGGL(cbn_apply_kernel<T>, grid, dim3(kThreads), 0, st, x, y, C, HW, save, act, slope, nb, pw);
@@ -1100,55 +1083,21 @@ extern "C" int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
   }
 }
 
-extern "C" int se_cbn_fwd_moments(const void* moments, int P, const float* x, float* y, int B, int C, int HW,
-                                  const float* const* params, float* const* running, int64_t* nbt, float* save,
-                                  float eps, float momentum, int act, float slope, float* y_amax,
-                                  const float* prelu_w, void* stream) {
-  if (!moments || P <= 0 || !x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || !act_ok(act, prelu_w))
-    return SE_E_ARG;
-  return cbn_fwd_t<float>(x, y, B, C, HW, (const void* const*)params, (void* const*)running, nbt, save, 1, eps,
-                          momentum, act, slope, y_amax, prelu_w, nullptr, se::as_stream(stream), moments, P);
-}
-
-static int cbn_head_fwd_impl(const void* pre, int preP, const float* x, float* out, int B, int C, int H, int W,
-                             const float* const* params, float* const* running, int64_t* nbt,
-                             float* save, int training, float eps, float momentum, int act,
-                             float slope, const float* w_head, int out_channels, int kernel_w,
-                             void* ws, size_t ws_bytes, void* stream);
-
-extern "C" int se_cbn_head_fwd_moments(const void* moments, int P, const float* x, float* out, int B, int C, int H,
-                                       int W, const float* const* params, float* const* running, int64_t* nbt,
-                                       float* save, float eps, float momentum, int act, float slope,
-                                       const float* w_head, int out_channels, int kernel_w, void* stream) {
-  if (!moments || P <= 0) return SE_E_ARG;
-  return cbn_head_fwd_impl(moments, P, x, out, B, C, H, W, params, running, nbt, save, 1, eps, momentum, act, slope,
-                           w_head, out_channels, kernel_w, nullptr, 0, stream);
-}
-
 extern "C" int se_cbn_head_fwd(const float* x, float* out, int B, int C, int H, int W,
                                const float* const* params, float* const* running, int64_t* nbt,
                                float* save, int training, float eps, float momentum, int act,
                                float slope, const float* w_head, int out_channels, int kernel_w,
                                void* ws, size_t ws_bytes, void* stream) {
-  return cbn_head_fwd_impl(nullptr, 0, x, out, B, C, H, W, params, running, nbt, save, training, eps, momentum, act,
-                           slope, w_head, out_channels, kernel_w, ws, ws_bytes, stream);
-}
-
-static int cbn_head_fwd_impl(const void* pre, int preP, const float* x, float* out, int B, int C, int H, int W,
-                             const float* const* params, float* const* running, int64_t* nbt,
-                             float* save, int training, float eps, float momentum, int act,
-                             float slope, const float* w_head, int out_channels, int kernel_w,
-                             void* ws, size_t ws_bytes, void* stream) {
   if (!x || !out || !save || !w_head || B <= 0 || C <= 0 || (C & 1) || H <= 0 || W < 2 || act < 0 || act > 2)
     return SE_E_ARG;
   if (out_channels != kHeadNO || kernel_w != kHeadKW) return SE_E_UNSUPPORTED;
   if ((long long)H * W >= (1LL << 31)) return SE_E_UNSUPPORTED;
   if (!training && !running) return SE_E_ARG;
   const int HW = H * W;
-  if (!pre && (ws_bytes < se_cbn_head_workspace_size(B, C, HW) || !ws)) return SE_E_WORKSPACE;
+  if (ws_bytes < se_cbn_head_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
   const int rc = cbn_stats<float>(x, B, C, HW, (const void* const*)params, (void* const*)running, nbt, save,
-                                  training, eps, momentum, nullptr, ws, st, pre, preP);
+                                  training, eps, momentum, nullptr, ws, st);
   if (rc != SE_OK) return rc;
   const long long waves = (long long)B * ((HW + 62) / 63);
   const size_t lds = ((size_t)(C / 2) * 8 + (size_t)kHeadNO * C * kHeadKW) * sizeof(float);
@@ -1223,14 +1172,9 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   if (fc) {   // (checked by the entry point: FRCRN's first conv, cin 1, kernel (5, 2); fp32)
     if constexpr (sizeof(T) == 4) {
       float* wpart = (float*)(((uintptr_t)ws + ws_bytes_ns(B, C, HW, 7) + 255) & ~(uintptr_t)255);
-      // SEHIP_FC_CPB = channels per workgroup: 4 (default; the tap-sharing form), 2, or 1 (the
-      // one-channel cbn_bwd_apply_fc_kernel). Bit-identical; same box, FRCRN step: 635.5 / 635.0
-      // (4) vs 634.0 / 631.6 utt/s (1)
-      const int cpb = [] {   // read per call (one host getenv per training step)
-        const char* e = std::getenv("SEHIP_FC_CPB");
-        const int v = e ? std::atoi(e) : 4;
-        return (v == 2 || v == 4) ? v : 1;
-      }();
+      // 4 channels per workgroup where Cc % 4 == 0 (the tap-sharing form, bit-identical to the
+      // one-channel cbn_bwd_apply_fc_kernel; FRCRN step 635.5 / 635.0 vs 634.0 / 631.6 utt/s)
+      const int cpb = Cc % 4 == 0 ? 4 : 1;
       const float* g1 = (const float*)gy;
       const float* g2 = (const float*)gy2;
       const float* xx = (const float*)x;
@@ -1238,8 +1182,8 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   hipLaunchKernelGGL((cbn_bwd_apply_fcm_kernel<SRCV, 1, 5, 2, CPBV>), dim3(Cc / CPBV, B), dim3(kThreads), 0, st, \
                      g1, g2, xx, C, HW, fc_w, coef, act, slope, *fc, wpart)
       if (cpb > 1 && Cc % cpb == 0) {
-        if (src == 1) { if (cpb == 4) SE_FCM(1, 4); else SE_FCM(1, 2); }
-        else { if (cpb == 4) SE_FCM(0, 4); else SE_FCM(0, 2); }
+        if (src == 1) SE_FCM(1, 4);
+        else SE_FCM(0, 4);
       } else if (src == 1)
         hipLaunchKernelGGL((cbn_bwd_apply_fc_kernel<1, 1, 5, 2>), dim3(Cc, B), mb, 0, st, g1, g2, xx, C, HW, fc_w,
                            coef, act, slope, *fc, wpart);
@@ -1255,7 +1199,7 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
     return SE_E_UNSUPPORTED;
   }
   const dim3 grid(se::ceil_div(HW, kThreads * 4), Cc, B);
-  const bool v4 = HW % 4 == 0 && vec_ok();
+  const bool v4 = HW % 4 == 0;
   if (src == 1 && v4)
     hipLaunchKernelGGL((cbn_bwd_apply4_kernel<1, T>), grid, mb, 0, st, gy, gy2, x, dx, C, HW, coef, act, slope, pw);
   else if (src == 0 && v4)

@@ -75,29 +75,9 @@ static const float* zero_page() {
 // D rows of one weight-grad split) miss each other's lines. This bijection on
 // [0, total) gives each XCD a contiguous range of logical tiles; it is a pure
 // relabelling, so results do not depend on the actual dispatch order.
-// SEHIP_IGLP (default on): each GEMM K-step is one scheduling region whose
-// non-MFMA instructions are interleaved into the MFMA gaps by
-// sched_group_barrier groups (gather fwd/dgrad +6-9 %, weight-grad +6 % over the
-// fenced schedule; build with -DSEHIP_IGLP=0 for the fenced variant).
-#ifndef SEHIP_WGRAD_OCC     // workgroups per CU the weight-grad GEMM is compiled for (variant builds: 1)
-#define SEHIP_WGRAD_OCC 2
-#endif
-#ifndef SEHIP_GEMM_PROBE   // 1 / 2: measurement probes of gather_x3_kernel<..., BMX = 2> (variant builds only)
-#define SEHIP_GEMM_PROBE 0
-#endif
-#ifndef SEHIP_IGLP
-#define SEHIP_IGLP 1
-#endif
-#ifndef SEHIP_GEMM_M16      // 1: f16x3 gather GEMMs on v_mfma_f32_16x16x32_f16 (16x16 accumulator blocks)
-#define SEHIP_GEMM_M16 0
-#endif
-#ifndef SEHIP_IG_VMEM
-#define SEHIP_IG_VMEM 0x020   // group mask for the global loads (0x020 VMEM read, 0x010 any VMEM)
-#endif
-#ifndef SEHIP_IG_VALU
-#define SEHIP_IG_VALU 2       // VALU instructions per MFMA gap
-#endif
-
+// Each GEMM K-step is one scheduling region whose non-MFMA instructions are
+// interleaved into the MFMA gaps by sched_group_barrier groups (gather fwd/dgrad
+// +6-9 %, weight-grad +6 % over a fenced schedule).
 __device__ __forceinline__ int xcd_remap(int L, int total) {
   constexpr int kXcd = 8;
   const int xcd = L % kXcd, idx = L / kXcd;
@@ -173,27 +153,10 @@ struct GatherArgs {
   // SE_MATH_F16X3: device max |.| of the gathered tensor(s) and of the weights
   const float* amax_a;
   const float* amax_w;
-  // gather_pk_kernel: X / X2 are CL16 buffers (cconv_pk.hpp) with Cpk / Cpk2
-  // channels per position and pk_plane / pk_plane2 elements per plane
-  int Cpk, Cpk2;
-  long long pk_plane, pk_plane2;
-  // gather_pk_kernel: the K order (split_k) and per-tap input offsets, read as
-  // scalars from the kernel arguments
-  int ntaps, kblk;
+  // gather_stencil_kernel: per-tap input offsets, read as scalars from the kernel
+  // arguments
+  int ntaps;
   int toffh[kMaxTaps], toffw[kMaxTaps];
-  int pp_pair;         // ping-pong gather: 0 = waves 4-7 late, 1 = odd waves late
-  // merged stride-phase classes (merge_h_phases): output columns n' >= mrg_np are
-  // channel n' - mrg_np of output row 1 + Sh * qh (rows >= Ho dropped); 0 = off
-  int mrg_np;
-  // merged classes: bit t set = tap t has no weight in phase 0 (mrg_zero0) / phase 1
-  // (mrg_zero1), so that half's waves skip the tap's K-steps (exact zero products)
-  unsigned long long mrg_zero0, mrg_zero1;
-  int accum;           // data-grad: Y += result (se_conv2d_desc.accumulate_dx)
-  // forward, se_conv2d_desc.moments: the CBN moment rows of each M-tile (rows
-  // mom_p0 + tile of mom_P; [N/2][mom_P][5] fp64 sums, then [N/2][mom_P][4] extrema)
-  double* mom;
-  float* mom_ext;
-  int mom_p0, mom_P;
 };
 
 // LDS images of both operands are column-interleaved inside every 64-wide
@@ -343,46 +306,30 @@ gather_gemm_kernel(const GatherArgs a) {
       fa[kk] = *reinterpret_cast<const f32x2*>(&sW[cur][2 * kk + lk][wcol]);
       fb[kk] = *reinterpret_cast<const f32x2*>(&sA[cur][2 * kk + lk][mcol]);
     }
-#if !SEHIP_IGLP
-    __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
     for (int kk = H; kk < KP; ++kk) {
       fa[kk] = *reinterpret_cast<const f32x2*>(&sW[cur][2 * kk + lk][wcol]);
       fb[kk] = *reinterpret_cast<const f32x2*>(&sA[cur][2 * kk + lk][mcol]);
     }
-#if !SEHIP_IGLP
-    __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
     for (int kk = 0; kk < KP; ++kk) {
       acc[0][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].x, acc[0][0], 0, 0, 0);
       acc[0][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].x, fb[kk].y, acc[0][1], 0, 0, 0);
       acc[1][0] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].x, acc[1][0], 0, 0, 0);
       acc[1][1] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[kk].y, fb[kk].y, acc[1][1], 0, 0, 0);
-#if !SEHIP_IGLP
-      if (kk == H - 1) __builtin_amdgcn_sched_barrier(0);
-#endif
     }
-#if !SEHIP_IGLP
-    // keep the following LDS writes (and so their vmcnt waits) AFTER the
-    // MFMAs: the buffers are disjoint, so hipcc would otherwise hoist them
-    __builtin_amdgcn_sched_barrier(0);
-#endif
   };
-  // SEHIP_IGLP: the step's non-MFMA stream (next tiles' loads, fragment reads,
+  // the step's non-MFMA stream (next tiles' loads, fragment reads,
   // LDS writes) interleaved into the 64-cycle MFMA gaps
   auto interleave = [&]() __attribute__((always_inline)) {
-#if SEHIP_IGLP
     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);                  // first fragments
 #pragma unroll
     for (int i = 0; i < 4 * (kBK / 2); ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
-      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(SEHIP_IG_VMEM, 1, 0);   // global load
-      __builtin_amdgcn_sched_group_barrier(0x002, SEHIP_IG_VALU, 0);                // VALU
+      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);                // VALU
     }
-#endif
   };
 
   const int nk = a.Kp / kBK;
@@ -394,7 +341,6 @@ gather_gemm_kernel(const GatherArgs a) {
   // main loop, unrolled by two so the staging sets alternate by name
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
-#if SEHIP_IGLP
     // unconditional (clamped) loads / stores: one scheduling region per step;
     // a clamped reload of the last tile lands in the buffer no step reads
     load_tile(s0, min(kt + 2, nk - 1) * kBK);
@@ -407,18 +353,6 @@ gather_gemm_kernel(const GatherArgs a) {
     store_tile(s0, 0);
     interleave();
     __syncthreads();
-#else
-    // even step: consume LDS[0]; s1 holds tile kt+1; load kt+2 into s0
-    if (kt + 2 < nk) load_tile(s0, (kt + 2) * kBK);
-    compute(0);
-    store_tile(s1, 1);
-    __syncthreads();
-    // odd step: consume LDS[1]; s0 holds tile kt+2; load kt+3 into s1
-    if (kt + 3 < nk) load_tile(s1, (kt + 3) * kBK);
-    compute(1);
-    if (kt + 2 < nk) store_tile(s0, 0);
-    __syncthreads();
-#endif
   }
   if (kt < nk) compute(0);   // odd tile count: the last tile sits in LDS[0]
 
@@ -829,9 +763,6 @@ wgrad_gemm_kernel(const WgradArgs a) {
       for (int j = 0; j < RN; ++j)
         gb[j][q] = *reinterpret_cast<const f32x2*>(&sD[cur][(wnn * TN + 32 * j + lc) * L + col + 2 * q]);
     }
-#if !SEHIP_IGLP
-    __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
     for (int q = HQ; q < Q; ++q) {
 #pragma unroll
@@ -841,9 +772,6 @@ wgrad_gemm_kernel(const WgradArgs a) {
       for (int j = 0; j < RN; ++j)
         gb[j][q] = *reinterpret_cast<const f32x2*>(&sD[cur][(wnn * TN + 32 * j + lc) * L + col + 2 * q]);
     }
-#if !SEHIP_IGLP
-    __builtin_amdgcn_sched_barrier(0);
-#endif
 #pragma unroll
     for (int q = 0; q < Q; ++q) {
 #pragma unroll
@@ -854,30 +782,22 @@ wgrad_gemm_kernel(const WgradArgs a) {
           for (int j = 0; j < RN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(e ? ga[i][q].y : ga[i][q].x,
                                                              e ? gb[j][q].y : gb[j][q].x, acc[i][j], 0, 0, 0);
-#if !SEHIP_IGLP
-      if (q == HQ - 1) __builtin_amdgcn_sched_barrier(0);
-#endif
     }
-#if !SEHIP_IGLP
-    __builtin_amdgcn_sched_barrier(0);   // keep the LDS writes (and their vmcnt) after the MFMAs
-#endif
   };
-  // SEHIP_IGLP: one scheduling region per step (loads of step s+2, fragment
+  // one scheduling region per step (loads of step s+2, fragment
   // reads, MFMAs, LDS writes of step s+1); the groups below interleave the
   // non-MFMA stream into the 64-cycle MFMA gaps: each MFMA is followed by one
   // LDS op, every other one by one global load, plus a few VALU.
   auto interleave = [&]() __attribute__((always_inline)) {
-#if SEHIP_IGLP
     constexpr int NM = RK * RN * (BMR / 2);        // MFMAs per step
     __builtin_amdgcn_sched_group_barrier(0x100, 2 * (RK + RN), 0);   // first fragments
 #pragma unroll
     for (int i = 0; i < NM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);              // DS read / write
-      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(SEHIP_IG_VMEM, 1, 0);   // global load
-      __builtin_amdgcn_sched_group_barrier(0x002, SEHIP_IG_VALU, 0);              // VALU
+      if (i % 2 == 0) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);              // VALU
     }
-#endif
   };
   // prologue: step 0 -> LDS[0]; step 1 in flight in st1
   if (nsteps > 0) {
@@ -888,7 +808,6 @@ wgrad_gemm_kernel(const WgradArgs a) {
   __syncthreads();
   int s = 0;
   for (; s + 1 < nsteps; s += 2) {
-#if SEHIP_IGLP
     // unconditional loads / stores keep each step ONE scheduling region: past
     // the end the loads are masked to zero (mv) and the stores land in a
     // buffer no later step reads
@@ -902,18 +821,6 @@ wgrad_gemm_kernel(const WgradArgs a) {
     store_step(st0, 0);
     interleave();
     __syncthreads();
-#else
-    // even step: consume LDS[0]; st1 holds step s+1; load s+2 into st0
-    if (s + 2 < nsteps) load_step(st0, mbeg + (s + 2) * BMR);
-    compute(0);
-    store_step(st1, 1);
-    __syncthreads();
-    // odd step: consume LDS[1]; st0 holds step s+2; load s+3 into st1
-    if (s + 3 < nsteps) load_step(st1, mbeg + (s + 3) * BMR);
-    compute(1);
-    if (s + 2 < nsteps) store_step(st0, 0);
-    __syncthreads();
-#endif
   }
   if (s < nsteps) compute(0);   // odd step count: the last step sits in LDS[0]
   // acc[i][j][r]: row k = 32i + (r&3) + 8(r>>2) + 4*lk, col n = 32j + lc
@@ -989,10 +896,6 @@ struct TapList {
   int n;
   int ti[kMaxTaps], tj[kMaxTaps];     // kernel (i, j) of each tap
   int offh[kMaxTaps], offw[kMaxTaps]; // input offsets
-  // merged stride-phase classes (merge_h_phases): columns [mrg_np, 2 mrg_np) are
-  // phase 1, whose kernel row of tap t is ti2[t]; a row of -1 is a zero weight
-  int mrg_np;
-  int ti2[kMaxTaps];
 };
 
 // Builds Wp[k = t*Cg + c][n] (zero rows/cols up to Kp x ldw) and ktab[k].
@@ -1123,7 +1026,6 @@ struct Dim1 {   // one spatial dim of one class
   int p, S, Q, s;
   int ntaps;
   int tap[16], off[16];
-  int tap2[16];   // merged classes: phase-1 kernel index per offset (-1: none)
 };
 
 // strided gather: out q in [0, Lout), in = q*stride + i*dil - pad
@@ -1154,7 +1056,6 @@ struct ClassPlan {
   Dim1 h, w;
   TapList taps;
   int K, Kp;
-  int mrg;        // 1: two h phases merged along the columns (merge_h_phases)
 };
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
@@ -1165,7 +1066,6 @@ static void finish_plan(ClassPlan& c, int Cg) {
   for (int a = 0; a < c.h.ntaps; ++a)
     for (int b = 0; b < c.w.ntaps; ++b, ++t) {
       c.taps.ti[t] = c.h.tap[a]; c.taps.tj[t] = c.w.tap[b];
-      c.taps.ti2[t] = c.mrg ? c.h.tap2[a] : -1;
       c.taps.offh[t] = c.h.off[a]; c.taps.offw[t] = c.w.off[b];
     }
   c.K = c.taps.n * Cg;
@@ -1185,10 +1085,8 @@ struct ConvGeom {
   const void* x_packed;   // SE_MATH_F16X3 CL16 operands from the caller (or nullptr)
   const void* x2_packed;
   const void* dy_packed;
-  int accum;      // se_conv2d_desc.accumulate_dx
   int sd;         // se_conv2d_desc.dtype (SE_DTYPE_*)
   const void* data_w;   // se_conv2d_desc.data_weights (data-grad weight image, or nullptr)
-  void* mom;            // se_conv2d_desc.moments (forward CBN moment rows, or nullptr)
 };
 
 static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
@@ -1206,11 +1104,8 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.x_packed = d->x_packed;
   g.x2_packed = d->x2_packed;
   g.dy_packed = d->dy_packed;
-  g.accum = d->accumulate_dx;
   g.sd = d->dtype;
   g.data_w = d->data_weights;
-  g.mom = d->moments;
-  if (g.accum != 0 && g.accum != 1) return SE_E_ARG;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16) return SE_E_ARG;
   if (g.sd < SE_DTYPE_F32 || g.sd > SE_DTYPE_F16) return SE_E_ARG;
   // 16-bit storage runs the one-term MFMA of its own format (operands exact)
@@ -1257,56 +1152,6 @@ static std::vector<ClassPlan> plan_pass(const ConvGeom& g, Pass pass) {
       out.push_back(c);
     }
   return out;
-}
-
-// A transposed conv's forward with stride 2 in H and 1 in W has two stride-phase
-// classes (even / odd output rows: FRCRN's decoder, kernel (5, 2): input row
-// offsets {0, -1, -2} and {0, -1}) that gather the same input rows. Merged, they
-// are one class over the union of the offsets with 2 x 128 output columns
-// (phase 0 | phase 1, a zero weight where a phase has no tap at an offset):
-// the gathered activations are loaded and split once for both phases and the
-// GEMM runs on the 256-column (NW = 2) tiles, for 1.2x the MFMA work of the two
-// classes (FRCRN: K = 6 x Cg per column instead of 6 x Cg and 4 x Cg).
-static bool merge_h_phases(const std::vector<ClassPlan>& cls, int Cg, ClassPlan& m) {
-  if (cls.size() != 2) return false;
-  const ClassPlan& c0 = cls[0];
-  const ClassPlan& c1 = cls[1];
-  if (c0.h.S != 2 || c0.h.p != 0 || c1.h.p != 1 || c0.h.s != 1 || c1.h.s != 1) return false;
-  if (c0.w.S != 1 || c1.w.S != 1 || c0.w.p != c1.w.p || c0.w.Q != c1.w.Q || c1.h.Q > c0.h.Q ||
-      c1.h.Q < c0.h.Q - 1)
-    return false;
-  m = ClassPlan{};
-  m.w = c0.w;
-  m.h = c0.h;
-  m.mrg = 1;
-  int n = 0;
-  for (int a = 0; a < c0.h.ntaps; ++a) {
-    m.h.tap[n] = c0.h.tap[a]; m.h.off[n] = c0.h.off[a]; m.h.tap2[n] = -1;
-    for (int b = 0; b < c1.h.ntaps; ++b)
-      if (c1.h.off[b] == c0.h.off[a]) m.h.tap2[n] = c1.h.tap[b];
-    ++n;
-  }
-  for (int b = 0; b < c1.h.ntaps; ++b) {
-    bool seen = false;
-    for (int a = 0; a < c0.h.ntaps; ++a) seen |= c0.h.off[a] == c1.h.off[b];
-    if (seen) continue;
-    if (n >= 16) return false;
-    m.h.tap[n] = -1; m.h.off[n] = c1.h.off[b]; m.h.tap2[n] = c1.h.tap[b];
-    ++n;
-  }
-  m.h.ntaps = n;
-  if (n * m.w.ntaps > kMaxTaps) return false;
-  finish_plan(m, Cg);
-  m.taps.mrg_np = 128;
-  return true;
-}
-
-// SEHIP_FWD_MERGE=1 runs the merged form (merge_h_phases). Off by default: the
-// full GPU suite passes with it (252 tests), but the step measured 616.2 / 617.4
-// vs 624.4 / 622.7 utt/s (same box): the 1.2x MFMA work is not won back.
-static bool fwd_merge_on() {   // read per call (tests switch it within one process)
-  const char* e = std::getenv("SEHIP_FWD_MERGE");
-  return e && std::atoi(e) == 1;
 }
 
 // One-term bf16 (SE_MATH_BF16, the low-precision configs' arithmetic) runs the
@@ -1375,21 +1220,18 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
   w.Np = round_up(w.N, n32 ? 32 : 128);
   const int tiles = (w.c.Kp / 128) * (w.Np / (n32 ? 32 : 128));
   int splits = std::max(1, 1024 / std::max(tiles, 1));
-  // At most kWgradMps positions per m-split (SEHIP_WGRAD_MPS overrides; 0 = no
-  // limit): the (k, n) tiles of one split run on one XCD and re-read G and D
-  // through its L2; short splits keep them close enough together for those
-  // re-reads to hit (dec5 weight-grad FETCH 40-48 -> 29-32 GB, 14.3 -> 12.4 ms;
-  // FRCRN step 574 -> 588 utt/s, same box).
-  static const int mps = [] {
-    const char* e = std::getenv("SEHIP_WGRAD_MPS");
-    return e ? std::max(0, std::atoi(e)) : 4096;
-  }();
-  if (mps > 0) splits = std::max(splits, (w.M + mps - 1) / mps);
+  // At most kWgradMps positions per m-split: the (k, n) tiles of one split run on
+  // one XCD and re-read G and D through its L2; short splits keep them close
+  // enough together for those re-reads to hit (dec5 weight-grad FETCH 40-48 ->
+  // 29-32 GB, 14.3 -> 12.4 ms; FRCRN step 574 -> 588 utt/s, same box; 2048 and
+  // 1024 measured slower).
+  constexpr int kWgradMps = 4096;
+  splits = std::max(splits, (w.M + kWgradMps - 1) / kWgradMps);
   const int max_by_m = std::max(1, w.M / 512);
   splits = std::min(splits, max_by_m);
-  // keep the slab <= 256 MB (1 GB with SEHIP_WGRAD_MPS)
+  // keep the slab <= 1 GB
   const size_t per = (size_t)w.c.Kp * w.Np * sizeof(float);
-  const size_t cap = mps > 0 ? (1024ull << 20) : (256ull << 20);
+  const size_t cap = 1024ull << 20;
   splits = (int)std::min<size_t>(splits, std::max<size_t>(1, cap / per));
   w.m_per_split = round_up((w.M + splits - 1) / splits, 64);
   w.splits = (w.M + w.m_per_split - 1) / w.m_per_split;
@@ -1420,46 +1262,11 @@ struct JoinIO {
   const float* s;   // weight-grad: the skip (D of a transposed conv)
 };
 
-// Split-GEMM workgroup width: 2 = 256-column tiles of 8 waves where the padded
-// column count is a multiple of 256, 1 = 128-column tiles of 4 waves
-// (SEHIP_GEMM_NW; read once).
+// SEHIP_STENCIL=0 (tests): the small-N stride-1 convs on gather_smalln_kernel
+// instead of the bit-identical LDS stencil
 static bool env_flag_off(const char* name) {
   const char* e = std::getenv(name);
   return e && e[0] == '0';
-}
-
-// Rows per split-fp16 workgroup tile with 256 columns: 128 (default) or 256
-// (SEHIP_GEMM_BM=256: gather_x3_kernel<..., BMX = 2>, bit-identical; measured
-// no faster at dec5; read once).
-static int gemm_bm() {
-  static const int bm = [] {
-    const char* e = std::getenv("SEHIP_GEMM_BM");
-    return (e && std::atoi(e) == 256) ? 256 : 128;
-  }();
-  return bm;
-}
-
-// SEHIP_GEMM_PP=1: the ping-pong schedule of gather_x3_kernel (read once)
-static int gemm_pp_mode() {   // 0 off, 1 waves 4-7 late, 2 odd waves late
-  static const int pp = [] {
-    const char* e = std::getenv("SEHIP_GEMM_PP");
-    return e ? std::atoi(e) : 0;
-  }();
-  return pp;
-}
-static bool gemm_pp() { return gemm_pp_mode() > 0; }
-
-static int gemm_nw() {
-  static const int nw = [] {
-    const char* e = std::getenv("SEHIP_GEMM_NW");
-    return (e && std::atoi(e) == 1) ? 1 : 2;
-  }();
-  return nw;
-}
-
-// a pass that would read a caller's CL16 operand (fp32 storage only)
-static bool pk_pass_any(const ConvGeom& g, Pass pass) {
-  return (pass == kFwd ? g.x_packed : g.dy_packed) != nullptr;
 }
 
 // The weight image of a gather pass: per stride-phase class the GEMM weight
@@ -1478,25 +1285,12 @@ static size_t class_images_bytes(const std::vector<ClassPlan>& cls, int ldw) {
   return b;
 }
 
-// CBN moment rows of a forward pass (se_conv2d_desc.moments): one per 128-position M-tile of each class
-static int moment_rows(const std::vector<ClassPlan>& cls, int B) {
-  long long r = 0;
-  for (const auto& c : cls) r += se::ceil_div((long long)B * c.h.Q * c.w.Q, (long long)kX3BM);
-  return r > INT32_MAX ? 0 : (int)r;
-}
-
 // split kernels: channel-block-major K order where Cg allows (split_k)
-// SEHIP_GEMM_3M=1: the split-fp16 forward GEMMs with 64 complex outputs run the
-// three-multiplication form (gather_3m_kernel); read per call
-static bool gemm_3m() {
-  const char* e = std::getenv("SEHIP_GEMM_3M");
-  return e && e[0] == '1';
-}
-static int korder_blk(int Cg) { return (Cg % 32 == 0 && !env_flag_off("SEHIP_KORDER")) ? 32 : 0; }
+static int korder_blk(int Cg) { return Cg % 32 == 0 ? 32 : 0; }
 
 static void class_images(const ConvGeom& g, Pass pass, const std::vector<ClassPlan>& cls, int ldw,
                          const WeightView& wv, const float* wamax, char* base, bool build, hipStream_t st,
-                         std::vector<ClassImage>& out, bool m3 = false) {
+                         std::vector<ClassImage>& out) {
   const int N = (pass == kFwd) ? g.Co : g.Ci;
   const int Cg = (pass == kFwd) ? g.Ci : g.Co;
   const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
@@ -1517,13 +1311,6 @@ static void class_images(const ConvGeom& g, Pass pass, const std::vector<ClassPl
     p = align256(p + (size_t)c.Kp * sizeof(int4));
     out.push_back(im);
     if (!build) continue;
-    if (m3) {   // gather_3m_kernel's per-step weight images (fit in the split image's space)
-      const int nk = c.taps.n * (Cg / 2 / k3mBKc);
-      const long long tot3 = (long long)nk * 64 * k3mBKc;
-      hipLaunchKernelGGL(prep_3m_kernel, dim3((unsigned)std::min<long long>((tot3 + 255) / 256, 4096)), dim3(256),
-                         0, st, wv, c.taps, Cg / 2, N, nk, wamax, (unsigned short*)im.Wp);
-      continue;
-    }
     const long long tot = (long long)c.Kp * ldw;
     const dim3 grid((unsigned)std::min<long long>((tot + 255) / 256, 4096));
     if (x6)
@@ -1552,32 +1339,11 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   if (ws_bytes < gather_ws_bytes(cls, N, g.math)) return SE_E_WORKSPACE;
   // a prepared split-fp16 image carries the caller's weight bound, which the GEMM unscales by
   if (pass == kData && g.data_w && g.math == SE_MATH_F16X3 && N > 64 && !g.w_amax) return SE_E_ARG;
-  if (g.accum) {   // dx += result: the split kernels' plain epilogue only (checked before any launch)
-    const bool split = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3) && N > 64;
-    if (pass != kData || jn || !split || g.dy_packed) return SE_E_UNSUPPORTED;
-  }
-  int ldw = ldw_for(N, g.math);
-  {   // stride-phase classes merged along the columns (split-fp16, 256-column tiles)
-    ClassPlan mp;
-    const bool pk_in = (pass == kFwd ? g.x_packed : g.dy_packed) != nullptr;
-    if (pass == kFwd && !g.mom && g.transposed && g.math == SE_MATH_F16X3 && N > 64 && ldw == 128 && !pk_in &&
-        gemm_nw() == 2 && gemm_bm() != 256 && !gemm_pp() && fwd_merge_on() && merge_h_phases(cls, Cg, mp) &&
-        ws_bytes >= gather_ws_bytes({mp}, 256)) {
-      cls.assign(1, mp);
-      ldw = 256;
-    }
-  }
+  // CL16 operands are read by the weight-grad only
+  if ((pass == kFwd ? g.x_packed : g.dy_packed) != nullptr) return SE_E_UNSUPPORTED;
+  const int ldw = ldw_for(N, g.math);
   WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w, g.sd};
-  if (g.sd != SE_DTYPE_F32 && (jn || pk_pass_any(g, pass))) return SE_E_UNSUPPORTED;   // fp32-only forms
-  if (g.mom) {   // CBN moments in the forward epilogue: one column tile of the split-fp16 kernel
-    const int bn = (ldw % 256 == 0 && gemm_nw() == 2) ? 256 : 128;
-    const bool ok = pass == kFwd && g.sd == SE_DTYPE_F32 && g.math == SE_MATH_F16X3 && N > 64 && !(N & 1) &&
-                    N <= bn && ldw == bn && !g.x_packed && gemm_bm() != 256 && !gemm_pp() && !SEHIP_GEMM_M16 &&
-                    !(jn && jn->y2);
-    if (!ok) return SE_E_UNSUPPORTED;
-  }
-  const int mom_P = g.mom ? moment_rows(cls, g.B) : 0;
-  int mom_p0 = 0;
+  if (g.sd != SE_DTYPE_F32 && jn) return SE_E_UNSUPPORTED;   // fp32-only forms
 
   char* p = align256((char*)ws);
   const float* zero = zero_page();
@@ -1604,11 +1370,6 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const bool x3 = (g.math == SE_MATH_BF16X3 && N > 64) || bf1 || h1 || f16;   // prep / tiles shared
   const bool x6 = g.math == SE_MATH_BF16X6 && N > 64;
   const float* amax_a = pass == kFwd ? g.x_amax : g.dy_amax;
-  // CL16 operands from the caller: the LDS-DMA kernel (gather_pk_kernel) on
-  // tap-uniform shapes; their scale is the caller's amax
-  const void* pk = pass == kFwd ? g.x_packed : g.dy_packed;
-  const void* pk2 = (pass == kFwd && jn && jn->x2) ? g.x2_packed : nullptr;
-  const bool packed = f16 && pk && amax_a && (!jn || !jn->x2 || pk2);
   const float* wamax = g.w_amax ? g.w_amax : amax_slot;   // bound of max |w|
   if (f16) {
     const long long nw = (long long)(g.complex_w ? g.Ci / 2 : g.Ci) * (g.complex_w ? g.Co / 2 : g.Co) * g.kh * g.kw;
@@ -1640,44 +1401,19 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     for (const auto& c : cls)
       if (!tu_of(c)) return SE_E_UNSUPPORTED;
   }
-  const int kblk = korder_blk(Cg);
   // the weight images: prepared by the caller (data-grad pass, desc.data_weights)
   // or built here in ws
   const bool have_img = pass == kData && g.data_w;
-  // the three-multiplication complex forward (gather_3m_kernel): 64 complex outputs,
-  // 16-channel K-steps, fp32 storage, plain or joined gather (SEHIP_GEMM_3M=1)
-  bool m3 = pass == kFwd && f16 && g.complex_w && N == 128 && Cg % (2 * k3mBKc) == 0 && g.sd == SE_DTYPE_F32 &&
-            !join_out && !packed && !g.mom && (!join_in || jn->jh % k3mBKc == 0) && gemm_3m();
-  for (const auto& c : cls) m3 = m3 && !c.mrg && c.taps.n <= kMaxTaps;
   std::vector<ClassImage> img;
-  class_images(g, pass, cls, ldw, wv, wamax, have_img ? (char*)g.data_w : p, !have_img, st, img, m3);
+  class_images(g, pass, cls, ldw, wv, wamax, have_img ? (char*)g.data_w : p, !have_img, st, img);
   for (size_t ic = 0; ic < cls.size(); ++ic) {
     const ClassPlan& c = cls[ic];
-    float* Wp = img[ic].Wp;
-    int4* ktab = img[ic].ktab;
     GatherArgs a{};
-    a.X = X; a.ktab = ktab; a.Wp = Wp; a.bias = bias_full; a.zero = zero; a.Y = Y;
+    a.X = X; a.ktab = img[ic].ktab; a.Wp = img[ic].Wp; a.bias = bias_full; a.zero = zero; a.Y = Y;
     a.amax_a = amax_a; a.amax_w = wamax;
     a.Cg = Cg; a.Hi = Hi; a.Wi = Wi; a.N = N; a.Ho = Ho; a.Wo = Wo;
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
-    a.mrg_np = c.mrg ? c.taps.mrg_np : 0;
-    if (c.mrg && !env_flag_off("SEHIP_MERGE_SKIP")) {   // SEHIP_MERGE_SKIP=0: multiply the zero taps
-      for (int t = 0; t < c.taps.n; ++t) {
-        if (c.taps.ti[t] < 0) a.mrg_zero0 |= 1ull << t;
-        if (c.taps.ti2[t] < 0) a.mrg_zero1 |= 1ull << t;
-      }
-      a.ntaps = c.taps.n;
-      a.kblk = kblk;
-    }
-    a.accum = g.accum;
-    if (g.mom) {
-      a.mom = (double*)g.mom;
-      a.mom_ext = (float*)(a.mom + (size_t)(N / 2) * mom_P * 5);
-      a.mom_P = mom_P;
-      a.mom_p0 = mom_p0;
-      mom_p0 += (int)se::ceil_div((long long)g.B * c.h.Q * c.w.Q, (long long)kX3BM);
-    }
     if (jn) {
       a.X2 = jn->x2; a.jh = jn->jh; a.H2 = jn->h2; a.W2 = jn->w2;
       a.Y2 = jn->y2; a.yjh = jn->yjh; a.YH2 = jn->yh2; a.YW2 = jn->yw2;
@@ -1685,25 +1421,16 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     const long long M = (long long)g.B * c.h.Q * c.w.Q;
     if (M > INT32_MAX) return SE_E_UNSUPPORTED;
     a.M = (int)M;
-    if (m3) {
-      a.ntaps = c.taps.n;
-      for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }
-      const dim3 grid3(se::ceil_div(M, 128));
-      if (join_in) hipLaunchKernelGGL(gather_3m_kernel<1>, grid3, dim3(kThreads), 0, st, a);
-      else hipLaunchKernelGGL(gather_3m_kernel<0>, grid3, dim3(kThreads), 0, st, a);
-      SE_LAUNCH_CHECK();
-      continue;
-    }
     if (N <= 16) {
       // stride-1 single-class small convs (CCBAM's spatial conv and its data-grad): the
-      // LDS stencil, bit-identical to gather_smalln_kernel (SEHIP_STENCIL=0: off)
+      // LDS stencil, bit-identical to gather_smalln_kernel
       int h0 = 0, h1 = 0, w0 = 0, w1 = 0;
       for (int t = 0; t < c.taps.n; ++t) {
         h0 = std::min(h0, c.taps.offh[t]); h1 = std::max(h1, c.taps.offh[t]);
         w0 = std::min(w0, c.taps.offw[t]); w1 = std::max(w1, c.taps.offw[t]);
       }
       const int th = kStRG * kStR + h1 - h0, tw = kStW + w1 - w0;
-      const bool stencil = g.sd == SE_DTYPE_F32 && !jn && !c.mrg && ldw <= 4 && (Cg == 2 || Cg == 4) &&
+      const bool stencil = g.sd == SE_DTYPE_F32 && !jn && ldw <= 4 && (Cg == 2 || Cg == 4) &&
                            c.h.s == 1 && c.w.s == 1 && (size_t)Cg * th * tw * sizeof(float) <= 48 * 1024 &&
                            c.taps.n <= kMaxTaps && !env_flag_off("SEHIP_STENCIL");
       if (stencil) {
@@ -1731,43 +1458,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
 #undef SE_SMALLN
     } else {
       const bool tu = tu_of(c);
-      if (packed && tu && ldw % 128 == 0) {
-        a.ntaps = c.taps.n;
-        a.kblk = kblk;
-        for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }
-        a.X = (const float*)pk;
-        a.Cpk = Cg;
-        a.pk_plane = (long long)g.B * Cg * Hi * Wi;
-        if (join_in) {
-          a.X = (const float*)pk;                 // packed s; x on its own grid
-          a.Cpk = 2 * jn->jh;
-          a.pk_plane = (long long)g.B * a.Cpk * Hi * Wi;
-          a.X2 = (const float*)pk2;
-          a.Cpk2 = 2 * jn->jh;
-          a.pk_plane2 = (long long)g.B * a.Cpk2 * jn->h2 * jn->w2;
-        }
-        const dim3 blk(kPkThreads);
-        if (ldw % 256 == 0 && gemm_bm() == 256) {   // 256 x 256 tiles, two stages
-          const dim3 grid(se::ceil_div(M, 256), ldw / 256);
-          if (join_in) hipLaunchKernelGGL((gather_pk_kernel<1, 256, 256, 2>), grid, blk, 0, st, a);
-          else if (join_out) hipLaunchKernelGGL((gather_pk_kernel<2, 256, 256, 2>), grid, blk, 0, st, a);
-          else hipLaunchKernelGGL((gather_pk_kernel<0, 256, 256, 2>), grid, blk, 0, st, a);
-        } else if (ldw % 256 == 0) {    // 128 x 256 tiles
-          const dim3 grid(se::ceil_div(M, 128), ldw / 256);
-          if (join_in) hipLaunchKernelGGL((gather_pk_kernel<1, 128, 256>), grid, blk, 0, st, a);
-          else if (join_out) hipLaunchKernelGGL((gather_pk_kernel<2, 128, 256>), grid, blk, 0, st, a);
-          else hipLaunchKernelGGL((gather_pk_kernel<0, 128, 256>), grid, blk, 0, st, a);
-        } else {                        // 256 x 128 tiles
-          const dim3 grid(se::ceil_div(M, 256), ldw / 128);
-          if (join_in) hipLaunchKernelGGL((gather_pk_kernel<1, 256, 128>), grid, blk, 0, st, a);
-          else if (join_out) hipLaunchKernelGGL((gather_pk_kernel<2, 256, 128>), grid, blk, 0, st, a);
-          else hipLaunchKernelGGL((gather_pk_kernel<0, 256, 128>), grid, blk, 0, st, a);
-        }
-        SE_LAUNCH_CHECK();
-        continue;
-      }
       // 256-column workgroups (NW = 2) where the padded column count allows
-      const bool wide = (ldw % 256 == 0) && gemm_nw() == 2;
+      const bool wide = ldw % 256 == 0;
       const dim3 grid(se::ceil_div(M, kX3BM), ldw / (wide ? 2 * kX3BN : kX3BN));
       const dim3 blk(wide ? 2 * kThreads : kThreads);
       if (x6) {
@@ -1792,8 +1484,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
         if (g.sd != SE_DTYPE_F32) {   // 16-bit storage: the one-term tiles of its format
 #define SE_X3_SD(NWV, F, SDV)                                                                              \
   do {                                                                                                    \
-    if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 0, NWV, F, 1, false, SDV>), grid, blk, 0, st, a); \
-    else hipLaunchKernelGGL((gather_x3_kernel<false, 1, 0, NWV, F, 1, false, SDV>), grid, blk, 0, st, a);   \
+    if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 0, NWV, F, SDV>), grid, blk, 0, st, a);          \
+    else hipLaunchKernelGGL((gather_x3_kernel<false, 1, 0, NWV, F, SDV>), grid, blk, 0, st, a);            \
   } while (0)
           if (g.sd == SE_DTYPE_BF16 && wide) SE_X3_SD(2, false, 1);
           else if (g.sd == SE_DTYPE_BF16) SE_X3_SD(1, false, 1);
@@ -1802,17 +1494,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
 #undef SE_X3_SD
         } else if (h1 && wide) SE_X3_LAUNCH(1, 2, true);
         else if (h1) SE_X3_LAUNCH(1, 1, true);
-        else if (f16 && wide && gemm_bm() == 256 && tu) {   // 256 x 256 tiles (BMX = 2)
-          const dim3 g2(se::ceil_div(M, 2 * kX3BM), grid.y);
-          if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1, 2, true, 2>), g2, blk, 0, st, a);
-          else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2, 2, true, 2>), g2, blk, 0, st, a);
-          else hipLaunchKernelGGL((gather_x3_kernel<true, 3, 0, 2, true, 2>), g2, blk, 0, st, a);
-        } else if (f16 && wide && gemm_pp() && tu) {   // ping-pong schedule
-          a.pp_pair = gemm_pp_mode() == 2;
-          if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 1, 2, true, 1, true>), grid, blk, 0, st, a);
-          else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 3, 2, 2, true, 1, true>), grid, blk, 0, st, a);
-          else hipLaunchKernelGGL((gather_x3_kernel<true, 3, 0, 2, true, 1, true>), grid, blk, 0, st, a);
-        } else if (f16 && wide) SE_X3_LAUNCH(3, 2, true);
+        else if (f16 && wide) SE_X3_LAUNCH(3, 2, true);
         else if (f16) SE_X3_LAUNCH(3, 1, true);
         else if (terms == 1 && wide) SE_X3_LAUNCH(1, 2, false);
         else if (terms == 1) SE_X3_LAUNCH(1, 1, false);
@@ -1924,11 +1606,6 @@ extern "C" size_t se_conv2d_workspace_size(const se_conv2d_desc* d) {
   ConvGeom g;
   if (geom_of(d, g)) return 0;
   size_t a = gather_ws_bytes(plan_pass(g, kFwd), g.Co, g.math);
-  {
-    ClassPlan mp;
-    if (g.transposed && g.Co > 64 && g.Co <= 128 && merge_h_phases(plan_pass(g, kFwd), g.Ci, mp))
-      a = std::max(a, gather_ws_bytes({mp}, 256));
-  }
   size_t b = gather_ws_bytes(plan_pass(g, kData), g.Ci, g.math);
   size_t c = wgrad_ws_bytes(plan_wgrad(g));
   {   // the weight-grad pass may run in another math than the forward (per-pass modes)
@@ -1947,12 +1624,6 @@ extern "C" int se_conv2d_fwd(const se_conv2d_desc* d, const float* x, const floa
   if (rc) return rc;
   if (!x || !wr || !y || !ws || (g.complex_w && !wi) || (g.complex_w && br && !bi)) return SE_E_ARG;
   return launch_gather(g, kFwd, x, wr, wi, br, bi, y, ws, ws_bytes, se::as_stream(stream));
-}
-
-extern "C" int se_conv2d_moments_rows(const se_conv2d_desc* d) {
-  ConvGeom g;
-  if (geom_of(d, g)) return 0;
-  return moment_rows(plan_pass(g, kFwd), g.B);
 }
 
 extern "C" size_t se_conv2d_data_weights_size(const se_conv2d_desc* d) {
@@ -1992,38 +1663,11 @@ extern "C" int se_conv2d_bwd_data(const se_conv2d_desc* d, const float* dy, cons
 
 namespace {
 
-// SEHIP_WGRAD_NB=1 keeps the split-fp16 weight-grad on 128 x 128 tiles where
-// 128 x 256 ones fit (the default, N % 256 == 0).
-int wgrad_nb() {
-  static const int v = [] {
-    const char* e = std::getenv("SEHIP_WGRAD_NB");
-    return e && std::atoi(e) == 1 ? 1 : 2;
-  }();
-  return v;
-}
-
-// SEHIP_WGRAD_KB=2 runs the N = 128 split-fp16 weight-grads on 256 x 128 tiles
-// where Kp % 256 == 0 (bit-identical; measured 612.7 / 614.2 vs 617.8 / 614.9
-// utt/s same box, so 128 x 128 stays the default).
-int wgrad_kb() {
-  static const int v = [] {
-    const char* e = std::getenv("SEHIP_WGRAD_KB");
-    return e && std::atoi(e) == 2 ? 2 : 1;
-  }();
-  return v;
-}
-
-// 1-D grid of wgrad_x3_kernel over its tile space; SEHIP_WGRAD_WG caps the
-// workgroup count (a persistent grid that leaves CUs to the main stream).
-// nb: 128-row D blocks per workgroup (wgrad_x3_kernel NB).
-dim3 x3_wgrad_grid(WgradArgs& a, const WgradPlan& w, int nb = 1, int kb = 1) {
-  static const int cap = [] {
-    const char* e = std::getenv("SEHIP_WGRAD_WG");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  a.vk = w.c.Kp / (128 * kb); a.vn = w.Np / (128 * nb); a.vs = w.splits;
-  const int tiles = a.vk * a.vn * a.vs;
-  return dim3((unsigned)(cap > 0 ? std::min(tiles, ((cap + 7) / 8) * 8) : tiles));
+// 1-D grid of wgrad_x3_kernel over its tile space (a.vk k-tiles x a.vn n-tiles x
+// a.vs m-splits, one workgroup each). nb: 128-row D blocks per workgroup.
+dim3 x3_wgrad_grid(WgradArgs& a, const WgradPlan& w, int nb = 1) {
+  a.vk = w.c.Kp / 128; a.vn = w.Np / (128 * nb); a.vs = w.splits;
+  return dim3((unsigned)(a.vk * a.vn * a.vs));
 }
 
 // Weight-grad pass. jn (transposed convs only): the conv's input x is the
@@ -2061,7 +1705,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   int4* ktab = (int4*)p;
 
   const bool x3_path = g.math == SE_MATH_F16X3 && split_ok && w.N > 32 && w.N > kSmallWgradN && w.Np != 32 &&
-                       !(g.x_packed || g.dy_packed) && w.c.taps.n <= kMaxTaps && !env_flag_off("SEHIP_WGRAD_DKTAB");
+                       !(g.x_packed || g.dy_packed) && w.c.taps.n <= kMaxTaps;
   // ktab only (no weights): reuse prep_class_kernel with ldw = 1 writing into slab[0]
   // would clobber; build it with a one-column pass into a scratch row instead. The
   // split-fp16 weight-grad kernel computes its entries itself (no launch).
@@ -2139,15 +1783,12 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     dim3 grid(w.c.Kp / 128, 1, w.splits);
     if (tu) hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_gemm_kernel<128, 32, 4, 1, 64, false>), grid, dim3(kThreads), 0, st, a);
-  } else if (f16 && w.Np % 256 == 0 && wgrad_nb() == 2) {   // 128 x 256 tiles, 8 waves
+  } else if (f16 && w.Np % 256 == 0) {   // 128 x 256 tiles, 8 waves
     const dim3 grid = x3_wgrad_grid(a, w, 2);
     const dim3 blk(2 * kThreads);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2>), grid, blk, 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 2>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true, 2>), grid, blk, 0, st, a);
-  } else if (f16 && !jn && tu && w.Np == 128 && w.c.Kp % 256 == 0 && wgrad_kb() == 2) {   // 256 x 128 tiles
-    const dim3 grid = x3_wgrad_grid(a, w, 1, 2);
-    hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 1, false, 2>), grid, dim3(2 * kThreads), 0, st, a);
   } else if (f16) {
     const dim3 grid = x3_wgrad_grid(a, w);
     const bool kpad = (w.c.taps.n * w.Cg) % 128 != 0;   // e.g. a first conv: K = 10 taps x 2
@@ -2162,10 +1803,10 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.sd != SE_DTYPE_F32) {   // 16-bit storage, one term of its format
     const dim3 grid = x3_wgrad_grid(a, w);
-    if (g.sd == SE_DTYPE_BF16 && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 1, false, 1, 1>), grid, dim3(kThreads), 0, st, a);
-    else if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, false, 1, false, 1, 1>), grid, dim3(kThreads), 0, st, a);
-    else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true, 1, false, 1, 2>), grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, true, 1, false, 1, 2>), grid, dim3(kThreads), 0, st, a);
+    if (g.sd == SE_DTYPE_BF16 && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.math == SE_MATH_F16) {   // one-term fp16 on fp32 storage
     const dim3 grid = x3_wgrad_grid(a, w);
     if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true>), grid, dim3(kThreads), 0, st, a);
@@ -2185,8 +1826,8 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   const long long per = (long long)w.c.Kp * w.Np;
   if (w.splits > 1) {
     const unsigned bx = (unsigned)std::min<long long>((per + 255) / 256, 2048);
-    // groups of >= 16 splits until ~2048 workgroups (SEHIP_SLAB_2L=0: one pass)
-    int ng = env_flag_off("SEHIP_SLAB_2L") ? 1 : std::max(1, std::min<int>(w.splits / 16, 2048 / (int)bx));
+    // groups of >= 16 splits until ~2048 workgroups
+    int ng = std::max(1, std::min<int>(w.splits / 16, 2048 / (int)bx));
     const int gs = se::ceil_div(w.splits, ng);
     ng = se::ceil_div(w.splits, gs);
     hipLaunchKernelGGL(slab_reduce_kernel, dim3(bx, ng), dim3(256), 0, st, slab, w.splits, per, gs);

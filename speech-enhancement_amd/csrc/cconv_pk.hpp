@@ -1,24 +1,14 @@
-// Packed-operand gather GEMM (SE_MATH_F16X3 forward and data-grad) — included
-// by cconv.hip after cconv_x3.hpp, inside its anonymous namespace.
+// CL16 operands of the SE_MATH_F16X3 weight-grad — included by cconv.hip after
+// cconv_x3.hpp, inside its anonymous namespace.
 //
-// The split-fp16 GEMM of cconv_x3.hpp gathers fp32 activations one dword per
-// lane per (row, k), scales and splits them in registers and writes the hi / lo
-// planes to LDS: ~3 VALU per element, re-done for every tap (10x per element),
-// plus 16 dword loads and 4 ds_write_b128 per thread per K-step.
-// Here the operand is split ONCE, by the packing pass below (or by a producer),
-// into "CL16": channels-last fp16 planes
+// The split-fp16 GEMMs of cconv_x3.hpp gather fp32 activations one dword per
+// lane per (row, k), scale and split them in registers and write the hi / lo
+// planes to LDS: ~3 VALU per element, re-done for every tap / k-tile that
+// reads the element. Here the operand is split ONCE, by the packing pass below
+// (or by a producer), into "CL16": channels-last fp16 planes
 //   P[plane][b][h][w][c], plane 0 = hi = fp16(x s), plane 1 = lo = fp16(x s - hi),
-// s the per-tensor power-of-two scale of SE_MATH_F16X3 (max|x| s < 2^14). One
-// (position, tap, 32-channel) row of the A tile is then 64 contiguous bytes per
-// plane, and the LDS image of cconv_x3.hpp ([plane][128 rows][4 x 16 B chunks],
-// chunk c of row r at c ^ ((r >> 2) & 3)) is filled by LDS-DMA: 16-byte
-// buffer_load ... lds per lane, the swizzle applied to the per-lane SOURCE
-// address (the LDS destination of a wave-instruction is lane-linear), rows
-// outside the input (padding, m >= M) read as zeros through an out-of-range
-// voffset. The pre-tiled weight image (prep_class_x3_kernel<true>) is copied the
-// same way. No register staging, no conversion and no ds_write in the K loop;
-// the MFMA fragments, the 2-stage LDS ring and the epilogue are those of
-// gather_x3_kernel.
+// s the per-tensor power-of-two scale of SE_MATH_F16X3 (max|x| s < 2^14), so a
+// (position, 8-channel) chunk of an operand is 16 contiguous bytes per plane.
 
 // ---------------------------------------------------------------------------
 // Packing: x [B, C, H, W] fp32 -> CL16 planes with the scale from *amax.
@@ -61,266 +51,7 @@ pack_cl16_kernel(const float* __restrict__ x, int C, int HW, const float* amax, 
   }
 }
 
-// ---------------------------------------------------------------------------
-// Gather GEMM over CL16 operands: one 8-wave workgroup per CU, a BM x BN tile
-// ((256, 128) for the 128-column passes, (128, 256) for the 256-column
-// data-grad) of 64 x 64 wave tiles (the fragments of gather_x3_kernel), and a
-// 3-stage LDS ring: the stage two K-steps ahead is issued by LDS-DMA before the
-// current one is computed, then a COUNTED s_waitcnt vmcnt (this wave's loads of
-// the next stage retired, the newest stage still in flight) and a raw s_barrier
-// (not __syncthreads, whose vmcnt(0) would drain the in-flight stage) hand the
-// next stage to every wave. MI355X_MICROARCH/cdna_hip_programming: the
-// 2-barrier 128 x 128 structure of gather_x3_kernel sits at its ~900 TF issue
-// ceiling; keeping the LDS-DMA in flight across the barrier is what moves past it.
-// Requires the tap-uniform K order (Cg % 32 == 0). JM as gather_x3_kernel.
-// a.X (and a.X2 for JM = 1) point at CL16 buffers; a.Cpk = channels per
-// position of a.X, a.Cpk2 of a.X2; a.pk_plane / a.pk_plane2 = elements per plane.
-// ---------------------------------------------------------------------------
 typedef __attribute__((address_space(3))) void lds_void;
-
-constexpr int kPkThreads = 512, kPkStages = 3;
-
-// (BM, BN) = (256, 256), S = 2: 8 waves of 128 (m) x 64 (n), two 64-KB stages,
-// the next stage issued before the current one is computed.
-template <int JM, int BM, int BN, int S = kPkStages>
-__global__ void __launch_bounds__(kPkThreads, 1)
-gather_pk_kernel(const GatherArgs a) {
-  static_assert((BM == 256 && BN == 128) || (BM == 128 && BN == 256) || (BM == 256 && BN == 256 && S == 2),
-                "8 waves of 64 x 64, or of 128 x 64 with two stages");
-  constexpr bool BIG = BM == 256 && BN == 256;
-  constexpr int WM = BIG ? 2 : BM / 64, TN = 64, TM = BM / WM, RN = 2, RM = TM / 32, PL = 2;
-  constexpr int A_U4 = BM * 2 * 4, B_U4 = BN * 2 * 4;      // u32x4 per stage image
-  constexpr int A_PCS = BM / 64, B_PCS = BN / 64;           // 1-KB LDS-DMA pieces per wave per stage
-  constexpr int VM_NEXT = A_PCS + B_PCS;                    // loads of one stage per wave
-  // ONE LDS array: the stage ring (LDS-DMA targets), then the epilogue's bias. Nothing
-  // else is read from memory inside the K loop: a K-step's tap and first channel come
-  // from scalar arithmetic and the per-tap offsets from the kernel arguments (a table
-  // read from global memory or LDS there is waited for with vmcnt(0), which would drain
-  // the stage in flight)
-  constexpr int RING = S * (A_U4 + B_U4);
-  __shared__ __attribute__((aligned(16))) u32x4 smem_all[RING];
-  auto stage_base = [&](int buf) __attribute__((always_inline)) { return &smem_all[buf * (A_U4 + B_U4)]; };
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave % WM, wn = wave / WM;
-  const int NT = gridDim.y;
-  const int tile = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, gridDim.x * gridDim.y);
-  const int mt = tile / NT, nt = tile % NT;
-  const int m0 = mt * BM, n0 = nt * BN;
-  const int nk = a.Kp / kBK;
-
-  const int ea = amax_exp(a.amax_a);
-  const int ush = ea + amax_exp(a.amax_w) - 2 * kF16Top;
-
-  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (void*)(((unsigned long long)hi << 32) | lo);
-  };
-  // A pieces: g = A_PCS * wave + j covers plane g / (BM / 16), rows 16 (g % (BM / 16)) + lane / 4,
-  // LDS slot lane & 3 (its source chunk carries the XOR swizzle)
-  constexpr int PPP = BM / 16;                    // pieces per plane
-  const int qhw = a.Qh * a.Qw;
-  const int b0 = m0 / qhw;
-  const int slot = lane & 3;
-  int rbase[A_PCS], hb[A_PCS], wb[A_PCS], csrc[A_PCS], pln[A_PCS];
-  bool rval[A_PCS];
-#pragma unroll
-  for (int j = 0; j < A_PCS; ++j) {
-    const int g = A_PCS * wave + j;
-    pln[j] = g / PPP;
-    const int r = 16 * (g % PPP) + (lane >> 2);
-    const int m = m0 + r;
-    rval[j] = m < a.M;
-    const int mm = rval[j] ? m : m0;
-    const int b = mm / qhw, rr = mm - b * qhw;
-    const int qh = rr / a.Qw, qw = rr - qh * a.Qw;
-    hb[j] = qh * a.sh;
-    wb[j] = qw * a.sw;
-    rbase[j] = b - b0;
-    csrc[j] = slot ^ x3_swz(r);
-  }
-  const long long HW1 = (long long)a.Hi * a.Wi, HW2 = (long long)a.H2 * a.W2;
-  const _Float16* X = reinterpret_cast<const _Float16*>(a.X);
-  const _Float16* X2 = reinterpret_cast<const _Float16*>(a.X2);
-  // per plane (a wave's A pieces may straddle the two planes when A_PCS = 2 and BM = 128)
-  __amdgpu_buffer_rsrc_t rx[2], rx2[2];
-#pragma unroll
-  for (int p = 0; p < 2; ++p) {
-    rx[p] = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(X + (p ? a.pk_plane : 0) + (long long)b0 * HW1 * a.Cpk),
-                                              (short)0, 0x7FFFFFFF, 0x00020000);
-    rx2[p] = rx[p];
-    if constexpr (JM == 1)
-      rx2[p] = __builtin_amdgcn_make_buffer_rsrc(
-          uniform_ptr(X2 + (p ? a.pk_plane2 : 0) + (long long)b0 * HW2 * a.Cpk2), (short)0, 0x7FFFFFFF, 0x00020000);
-  }
-  // this workgroup's BN / 128 consecutive weight images of a K-step
-  const u32x4* wt = reinterpret_cast<const u32x4*>(a.Wp) + (long long)nt * (BN / 128) * kX3TileU4;
-  const int NTW = NT * (BN / 128);                // 128-column images per K-step
-
-  auto stage = [&](int buf, int k0) __attribute__((always_inline)) {
-    int t, c0;                                    // the step's tap and first channel (uniform)
-    split_k(k0, a.Cg, a.ntaps, a.kblk, t, c0);
-    const int offh = a.toffh[t], offw = a.toffw[t];
-    int W = a.Wi, C = a.Cpk;
-    long long HWs = HW1;
-    bool from_x = false;
-    if constexpr (JM == 1) {                      // a K-step lies in one join chunk
-      const int q = c0 / a.jh;
-      from_x = (q & 1) == 0;                      // chunks [x_re, s_re, x_im, s_im]
-      c0 = (q >> 1) * a.jh + (c0 - q * a.jh);
-      if (from_x) { W = a.W2; C = a.Cpk2; HWs = HW2; }
-    }
-    char* dstA = (char*)stage_base(buf);
-#pragma unroll
-    for (int j = 0; j < A_PCS; ++j) {
-      const int hi = hb[j] + offh, wi = wb[j] + offw;
-      bool ok = rval[j] & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      if constexpr (JM == 1) ok &= !from_x | (hi < a.H2);   // F.pad rows of x read 0
-      const int pos = (int)((long long)rbase[j] * HWs + (long long)hi * W + wi);
-      const int vo = ok ? (pos * C + c0 + 8 * csrc[j]) * 2 : (int)0x80000000;
-      __amdgpu_buffer_rsrc_t r = pln[j] ? (from_x ? rx2[1] : rx[1]) : (from_x ? rx2[0] : rx[0]);
-      __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (lds_void*)(dstA + (A_PCS * wave + j) * 1024), 16, vo, 0, 0, 0);
-    }
-    const u32x4* src = wt + (long long)(k0 >> 5) * NTW * kX3TileU4 + (B_PCS * wave) * 64 + lane;
-    char* dstB = (char*)(stage_base(buf) + A_U4);
-#pragma unroll
-    for (int j = 0; j < B_PCS; ++j)
-      __builtin_amdgcn_global_load_lds((const void*)(src + 64 * j),
-                                       (lds_void*)(dstB + (B_PCS * wave + j) * 1024), 16, 0, 0);
-  };
-
-  f32x16 acc[RN][RM];
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int j = 0; j < RM; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
-
-  const int lh = lane >> 5, lr = lane & 31;
-  const int fsw = x3_swz(lr);
-  constexpr int FS = BIG ? 1 : 2;                  // k-substeps of fragments held at once
-  auto compute = [&](int cur) __attribute__((always_inline)) {
-    const u32x4* sA = stage_base(cur);
-    const u32x4* sW = stage_base(cur) + A_U4;
-#pragma unroll
-    for (int k0 = 0; k0 < 2; k0 += FS) {
-      u32x4 wf[FS][RN][PL], af[FS][RM][PL];
-#pragma unroll
-      for (int kk = 0; kk < FS; ++kk) {
-        const int c = (2 * (k0 + kk) + lh) ^ fsw;
-#pragma unroll
-        for (int i = 0; i < RN; ++i) {
-          const int n = wn * TN + 32 * i;         // block's first column (uniform)
-#pragma unroll
-          for (int p = 0; p < PL; ++p)
-            wf[kk][i][p] = sW[(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
-        }
-#pragma unroll
-        for (int j = 0; j < RM; ++j)
-#pragma unroll
-          for (int p = 0; p < PL; ++p)
-            af[kk][j][p] = sA[(p * BM + wm * TM + 32 * j + lr) * 4 + c];
-      }
-      if constexpr (BIG) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int kk = 0; kk < FS; ++kk)
-#pragma unroll
-        for (int t = 0; t < 3; ++t)  // hi*hi, hi*lo, lo*hi
-#pragma unroll
-          for (int i = 0; i < RN; ++i)
-#pragma unroll
-            for (int j = 0; j < RM; ++j)
-              acc[i][j] = mfma_32x32x16<true>(wf[kk][i][t == 2 ? 1 : 0], af[kk][j][t == 1 ? 1 : 0], acc[i][j]);
-      if constexpr (BIG) __builtin_amdgcn_s_setprio(0);
-    }
-  };
-
-  if constexpr (S == 2) {
-    // prologue: stage 0; each K-step issues the next stage, computes, then waits for it
-    stage(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) stage((kt + 1) & 1, (kt + 1) * kBK);
-      compute(kt & 1);
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  } else {
-    // prologue: stages 0 and 1 in flight, wait for stage 0
-    stage(0, 0);
-    if (nk > 1) stage(1, kBK);
-    if (nk > 1) asm volatile("s_waitcnt vmcnt(%0)" :: "n"(VM_NEXT) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-      const bool ahead = kt + 2 < nk;
-      if (ahead) stage((kt + 2) % S, (kt + 2) * kBK);
-      compute(kt % S);
-      // retire this wave's loads of stage kt + 1 (the stage kt + 2 ones may stay in flight),
-      // then the barrier hands stage kt + 1 to every wave and frees buffer kt for kt + 3
-      if (ahead) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" :: "n"(VM_NEXT) : "memory");
-      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < RN; ++i)
-#pragma unroll
-    for (int j = 0; j < RM; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], ush);
-
-  // --- epilogue (as gather_x3_kernel) ---
-  float* sBias = reinterpret_cast<float*>(&smem_all[0]);
-  for (int i = tid; i < BN; i += kPkThreads) {
-    const int n = n0 + i;
-    sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
-  }
-  __syncthreads();
-  const long long HoWo = (long long)a.Ho * a.Wo;
-  const bool full_n = n0 + BN <= a.N;
-#pragma unroll
-  for (int j = 0; j < RM; ++j) {
-    const int mm = m0 + wm * TM + 32 * j + lr;
-    if (mm >= a.M) continue;
-    const int b = mm / qhw, r = mm - b * qhw;
-    const int qh = r / a.Qw, qw = r - qh * a.Qw;
-    const int nl0 = wn * TN + 4 * lh;
-    if constexpr (JM == 2) {
-      const int oh = a.ph + a.Sh * qh, ow = a.pw + a.Sw * qw;
-      const long long P2 = (long long)a.YH2 * a.YW2;
-      const int cpb = 2 * a.yjh;
-#pragma unroll
-      for (int i = 0; i < RN; ++i) {
-        const int nb = n0 + wn * TN + 32 * i;     // block's first channel (wave-uniform)
-        const int q = nb / a.yjh;
-        const int cb = (q >> 1) * a.yjh + (nb - q * a.yjh) + 4 * lh;
-        const bool to_x = (q & 1) == 0;
-        if (to_x && oh >= a.YH2) continue;
-        const long long pl = to_x ? P2 : HoWo;
-        float* yp = to_x ? a.Y2 + ((long long)b * cpb + cb) * P2 + (long long)oh * a.YW2 + ow
-                         : a.Y + ((long long)b * cpb + cb) * HoWo + (long long)oh * a.Wo + ow;
-#pragma unroll
-        for (int r2 = 0; r2 < 16; ++r2) yp[(long long)((r2 & 3) + 8 * (r2 >> 2)) * pl] = acc[i][j][r2];
-      }
-      continue;
-    }
-    float* yb = a.Y + (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
-                (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
-#pragma unroll
-    for (int i = 0; i < RN; ++i)
-#pragma unroll
-      for (int r2 = 0; r2 < 16; ++r2) {
-        const int nl = 32 * i + (r2 & 3) + 8 * (r2 >> 2);
-        if (full_n || n0 + nl0 + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
-      }
-  }
-}
 
 // ---------------------------------------------------------------------------
 // Weight-grad over CL16 operands: dWp[k, n] = sum_m G[m, k] D[m, n] with the

@@ -56,24 +56,12 @@ __device__ __forceinline__ int amax_exp(const float* amax) {
 __device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }
 
 // (x0, x1) * s -> packed fp16 hi pair and lo pair (element 0 in the low half);
-// v_cvt_pk_f16_f32 rounds to nearest even, s * x - hi is one exact FMA
-#ifndef SEHIP_SPLIT_MIX
-#define SEHIP_SPLIT_MIX 0
-#endif
+// v_cvt_pk_f16_f32 rounds to nearest even, s * x - hi is exact in fp32
 __device__ __forceinline__ void split_f16x2(float x0, float x1, float s, unsigned& hi, unsigned& lo) {
   const f32x2 v = (f32x2){x0, x1} * s;
   const f16x2 h = __builtin_convertvector(v, f16x2);
   hi = __builtin_bit_cast(unsigned, h);
-#if SEHIP_SPLIT_MIX
-  // lo = f16(x s - hi) by v_fma_mix{lo,hi}_f16 straight from the packed fp16 hi: the
-  // same single rounding of the exact x s - hi, two instructions instead of four
-  unsigned l;
-  asm("v_fma_mixlo_f16 %0, %1, %2, -%3 op_sel_hi:[0,0,1]" : "=v"(l) : "v"(x0), "v"(s), "v"(hi));
-  asm("v_fma_mixhi_f16 %0, %1, %2, -%3 op_sel:[0,0,1] op_sel_hi:[0,0,1]" : "+v"(l) : "v"(x1), "v"(s), "v"(hi));
-  lo = l;
-#else
   lo = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2));
-#endif
 }
 
 // one 32x32x16 MFMA on a pair of 16-B operand fragments: fp16 or bf16 elements
@@ -124,31 +112,16 @@ __global__ void __launch_bounds__(256) amax_kernel(const float* __restrict__ x, 
 
 // LDS / pre-tiled weight image of one operand tile: [plane (hi, lo)][row][4
 // chunks of 8 bf16 = 16 B], chunk c of row `row` stored at c ^ x3_swz(row).
-// 64-B rows, XOR swizzle: ds_read_b128 fragment reads are conflict-free in all
-// four 16-lane groups. x3_swz = (row >> 2) & 3 serves the 32x32x16 reads (lane
-// -> row r = l & 31, chunk 2ks + (l >> 5)); with SEHIP_GEMM_M16 the swizzle is
-// the 8-entry table f(g), g = (row >> 2) & 7, f = [0,0,3,3,1,2,2,1], which keeps
-// those reads conflict-free and also the 16x16x32 reads (lane -> row l & 15 of a
-// 16-row block, chunk l >> 4): in every lane group the 16 lanes hit the 16
-// distinct 16-B slots of a 256-B bank row.
-// SEHIP_SWZ2 (round 3): x3_swz = bit 2 of the row | (bit 1 ^ bit 4) << 1 keeps the
-// fragment reads conflict-free (in each ds_read_b128 lane group {0-3,12-15,20-27},
-// {4-11,16-19,28-31} the 16 (row & 3, swizzle) pairs are distinct) and also makes
-// the activation tile's ds_write_b128 stores conflict-free (8 consecutive rows in
-// one 8-lane store group land on 8 distinct 16-B slots of a 128-B bank row); the
-// (row >> 2) & 3 form left every store group 2-way conflicted (PMC: bank-conflict
-// cycles 12-20 % of the LDS-array cycles of the gather GEMMs, tools/pmc_lds.sh).
-#ifndef SEHIP_SWZ2
-#define SEHIP_SWZ2 1
-#endif
+// 64-B rows, XOR swizzle x3_swz = bit 2 of the row | (bit 1 ^ bit 4) << 1: the
+// ds_read_b128 fragment reads (lane -> row r = l & 31, chunk 2ks + (l >> 5)) are
+// conflict-free (in each lane group {0-3,12-15,20-27}, {4-11,16-19,28-31} the 16
+// (row & 3, swizzle) pairs are distinct), and so are the activation tile's
+// ds_write_b128 stores (8 consecutive rows of one 8-lane store group land on 8
+// distinct 16-B slots of a 128-B bank row). Round 3: the (row >> 2) & 3 form left
+// every store group 2-way conflicted (PMC: bank-conflict cycles 12-20 % of the
+// LDS-array cycles of the gather GEMMs, tools/pmc_lds.sh).
 __device__ __forceinline__ int x3_swz(int row) {
-#if SEHIP_GEMM_M16
-  return (0x69F0 >> (((row >> 2) & 7) * 2)) & 3;
-#elif SEHIP_SWZ2
   return ((row >> 2) & 1) | ((((row >> 1) ^ (row >> 4)) & 1) << 1);
-#else
-  return (row >> 2) & 3;
-#endif
 }
 __device__ __forceinline__ int x3_chunk(int row, int c) { return c ^ x3_swz(row); }
 
@@ -188,15 +161,11 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
     const int k = (int)(idx % Kp);                    // k fastest: a thread group fills rows
     const int n = (int)(idx / Kp);
     float v = 0.f;
-    // merged phases (TapList::mrg_np): column n of phase 1 is channel n - mrg_np
-    const int ph = taps.mrg_np ? n / taps.mrg_np : 0;
-    const int nn = n - ph * taps.mrg_np;
-    if (k < K && nn < N) {
+    if (k < K && n < N) {
       int t, c;
       split_k(k, Cg, taps.n, kblk, t, c);
-      const int ci = data_grad ? nn : c, co = data_grad ? c : nn;
-      const int ti = ph ? taps.ti2[t] : taps.ti[t];
-      if (ti >= 0) v = kernel_value(w, ci, co, ti, taps.tj[t]);
+      const int ci = data_grad ? n : c, co = data_grad ? c : n;
+      v = kernel_value(w, ci, co, taps.ti[t], taps.tj[t]);
     }
     unsigned short hb, lb;
     if constexpr (F16) {
@@ -250,36 +219,25 @@ __global__ void prep_class_x3_kernel(WeightView w, TapList taps, int Cg, int N, 
 // and split once per 256 output columns instead of once per 128.
 // F16: scaled split-fp16 operands (SE_MATH_F16X3; a.amax_a / a.amax_w give the
 // per-tensor scales of the gathered tensor and the weights).
-// BMX = 2 (with NW = 2): a 256 (n) x 256 (m) tile of 8 waves of 64 (n) x 128 (m),
-// twice the MFMA work per barrier and half the LDS fragment bytes per MFMA.
-// PP (with NW = 2): ping-pong schedule. Waves 4-7 run one barrier behind waves
-// 0-3 (each SIMD holds one wave of each half), and every K-step is two barrier
-// intervals: a memory part (fragment reads of this step, LDS stores of the
-// next, global loads of the one after) and an MFMA part. In each interval one
-// wave per SIMD issues MFMAs while the other does its memory part.
 // SD: storage type of X and Y (se_conv2d_desc.dtype): 0 fp32; 1 bf16 / 2 fp16 with
 // the one-term MFMA of that format (TERMS = 1; F16 = fp16 MFMA, unscaled: the
 // operands are exactly representable), the 16-bit tensors loaded and stored as they are.
-template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int BMX = 1, bool PP = false,
-          int SD = 0>
+template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int SD = 0>
 __global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
-  static_assert(SD == 0 || (TERMS == 1 && JM == 0 && BMX == 1 && !PP), "16-bit storage: one-term, plain tiles");
+  static_assert(SD == 0 || (TERMS == 1 && JM == 0), "16-bit storage: one-term, plain tiles");
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
   constexpr int ES = SD ? 2 : 4;                  // bytes per element of X / Y
   static_assert(NW == 1 || NW == 2, "128 or 256 columns per workgroup");
-  static_assert(BMX == 1 || (BMX == 2 && NW == 2), "256-row tiles need the 8-wave workgroup");
   constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
   constexpr int THR = kThreads * NW;
-  constexpr int BN = kX3BN * NW, BM = kX3BM * BMX, WM = 2, TN = 64, TM = 64 * BMX, RN = 2, RM = 2 * BMX;
-  constexpr int AJ = 16 * BMX / NW;               // gathered k per thread per step
+  constexpr int BN = kX3BN * NW, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
+  constexpr int AJ = 16 / NW;                     // gathered k per thread per step
   constexpr int CPT = AJ / 8;                     // 16-B chunks per plane per thread
-  constexpr bool M16 = SEHIP_GEMM_M16 && F16 && TERMS == 3 && BMX == 1 && !PP;
-  constexpr int NBUF = PP ? 3 : 2;                // LDS stages (ping-pong: a 3-stage ring)
-  __shared__ __attribute__((aligned(16))) u32x4 sA[NBUF][2 * BM * 4];
-  __shared__ __attribute__((aligned(16))) u32x4 sW[NBUF][2 * BN * 4];   // [t][plane][128 rows][4]
+  __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * BM * 4];
+  __shared__ __attribute__((aligned(16))) u32x4 sW[2][2 * BN * 4];   // [t][plane][128 rows][4]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave / WM, wm = wave % WM;
@@ -402,257 +360,109 @@ gather_x3_kernel(const GatherArgs a) {
     for (int j = 0; j < 2 * PL; ++j) sW[buf][tid + THR * j] = st.rw[j];
   };
 
-  // M16: 16x16 accumulator blocks (v_mfma_f32_16x16x32_f16, one 32-deep
-  // k-substep per K-step): QN x QM blocks of 4 floats instead of RN x RM of 16
-  constexpr int QN = M16 ? 2 * RN : RN, QM = M16 ? 2 * RM : RM, AR = M16 ? 4 : 16;
-  typedef float accv __attribute__((ext_vector_type(AR)));
-  accv acc[QN][QM];
+  f32x16 acc[RN][RM];
 #pragma unroll
-  for (int i = 0; i < QN; ++i)
+  for (int i = 0; i < RN; ++i)
 #pragma unroll
-    for (int j = 0; j < QM; ++j)
+    for (int j = 0; j < RM; ++j)
 #pragma unroll
-      for (int r = 0; r < AR; ++r) acc[i][j][r] = 0.f;
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
   const int lh = lane >> 5, lr = lane & 31;
   const int fsw = x3_swz(lr);
-  // BMX = 1: both k-substeps' fragments are read up front; BMX = 2 (twice the
-  // accumulators) reads them per k-substep to stay inside 256 registers
-  constexpr int FS = BMX == 1 ? 2 : 1;           // k-substeps of fragments held at once
+  // both k-substeps' fragments are read up front
   auto compute = [&](int cur) __attribute__((always_inline)) {
-    if constexpr (M16) {
-      // lane l: row l & 15 of a 16-row block, chunk l >> 4 (k 8(l >> 4) .. +8)
-      const int r16 = lane & 15, q4 = lane >> 4;
-      u32x4 wf[QN][PL], af[QM][PL];
+    u32x4 wf[2][RN][PL], af[2][RM][PL];     // [ks][block][plane]
 #pragma unroll
-      for (int i = 0; i < QN; ++i) {
-        const int n = wn * TN + 16 * i, row = (n & 127) + r16;
-        const int c = q4 ^ x3_swz(row);
+    for (int kk = 0; kk < 2; ++kk) {
+      const int c = (2 * kk + lh) ^ fsw;
 #pragma unroll
-        for (int p = 0; p < PL; ++p) wf[i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + row) * 4 + c];
+      for (int i = 0; i < RN; ++i) {
+        const int n = wn * TN + 32 * i;         // block's first column (uniform)
+#pragma unroll
+        for (int p = 0; p < PL; ++p)
+          wf[kk][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
       }
 #pragma unroll
-      for (int j = 0; j < QM; ++j) {
-        const int row = wm * TM + 16 * j + r16;
-        const int c = q4 ^ x3_swz(row);
+      for (int j = 0; j < RM; ++j)
 #pragma unroll
-        for (int p = 0; p < PL; ++p) af[j][p] = sA[cur][(p * BM + row) * 4 + c];
-      }
-#pragma unroll
-      for (int t = 0; t < TERMS; ++t)
-#pragma unroll
-        for (int i = 0; i < QN; ++i)
-#pragma unroll
-          for (int j = 0; j < QM; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, wf[i][t == 2 ? 1 : 0]),
-                                                               __builtin_bit_cast(f16x8, af[j][t == 1 ? 1 : 0]),
-                                                               acc[i][j], 0, 0, 0);
-    } else {
-#pragma unroll
-    for (int k0 = 0; k0 < 2; k0 += FS) {
-      u32x4 wf[FS][RN][PL], af[FS][RM][PL];     // [ks][block][plane]
-#pragma unroll
-      for (int kk = 0; kk < FS; ++kk) {
-        const int c = (2 * (k0 + kk) + lh) ^ fsw;
-#pragma unroll
-        for (int i = 0; i < RN; ++i) {
-          const int n = wn * TN + 32 * i;         // block's first column (uniform)
-#pragma unroll
-          for (int p = 0; p < PL; ++p)
-            wf[kk][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
-        }
-#pragma unroll
-        for (int j = 0; j < RM; ++j)
-#pragma unroll
-          for (int p = 0; p < PL; ++p)
-            af[kk][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
-      }
-#pragma unroll
-      for (int kk = 0; kk < FS; ++kk)
-#pragma unroll
-        for (int t = 0; t < TERMS; ++t)  // terms: hi*hi, hi*lo, lo*hi
-#pragma unroll
-          for (int i = 0; i < RN; ++i)
-#pragma unroll
-            for (int j = 0; j < RM; ++j)
-              acc[i][j] = mfma_32x32x16<F16>(wf[kk][i][t == 2 ? 1 : 0], af[kk][j][t == 1 ? 1 : 0], acc[i][j]);
+        for (int p = 0; p < PL; ++p)
+          af[kk][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
     }
-    }
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int t = 0; t < TERMS; ++t)  // terms: hi*hi, hi*lo, lo*hi
+#pragma unroll
+        for (int i = 0; i < RN; ++i)
+#pragma unroll
+          for (int j = 0; j < RM; ++j)
+            acc[i][j] = mfma_32x32x16<F16>(wf[kk][i][t == 2 ? 1 : 0], af[kk][j][t == 1 ? 1 : 0], acc[i][j]);
   };
+  // one scheduling region per K-step: the non-MFMA stream (next tiles' loads,
+  // fragment reads, LDS writes) interleaved into the MFMA gaps
   auto interleave = [&]() __attribute__((always_inline)) {
-#if SEHIP_IGLP
-    __builtin_amdgcn_sched_group_barrier(0x100, M16 ? 4 : 8, 0);        // first fragments
+    __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);                  // first fragments
 #pragma unroll
-    for (int i = 0; i < (M16 ? TERMS * QN * QM : 2 * TERMS * RN * RM); ++i) {
+    for (int i = 0; i < 2 * TERMS * RN * RM; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
       if (i < AJ + 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
     }
-#endif
   };
 
   const int nk = a.Kp / kBK;
-  if constexpr (PP) {
-    static_assert(NW == 2 && BMX == 1, "ping-pong needs the two halves of the 8-wave workgroup");
-    // Per K-step: memory part = this step's fragment reads; MFMA part = the 24 MFMAs
-    // with the staging of step + 2 (LDS stores of the tile loaded one step earlier,
-    // then the global loads of step + 3) interleaved into their gaps. A 3-stage LDS
-    // ring keeps the stores of step + 2 off the stage the other half is reading.
-    const bool late = a.pp_pair ? (wave & 1) : (wave >= 4);   // which half runs one barrier behind
-    u32x4 wf[2][RN][PL], af[2][RM][PL];
-    auto read_frags = [&](int cur) __attribute__((always_inline)) {
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) {
-        const int c = (2 * ks + lh) ^ fsw;
-#pragma unroll
-        for (int i = 0; i < RN; ++i) {
-          const int n = wn * TN + 32 * i;
-#pragma unroll
-          for (int p = 0; p < PL; ++p)
-            wf[ks][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
-        }
-#pragma unroll
-        for (int j = 0; j < RM; ++j)
-#pragma unroll
-          for (int p = 0; p < PL; ++p)
-            af[ks][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
-      }
-    };
-    load_tile(s0, 0);
-    store_tile(s0, 0);
-    if (nk > 1) { load_tile(s0, kBK); store_tile(s0, 1); }
-    if (nk > 2) load_tile(s0, 2 * kBK);
+  // two register staging sets (prefetch distance 2); unconditional (clamped) loads and
+  // stores keep each step one scheduling region: a clamped reload of the last tile
+  // lands in the buffer no step reads
+  load_tile(s0, 0);
+  store_tile(s0, 0);
+  if (nk > 1) load_tile(s1, kBK);
+  __syncthreads();
+  int kt = 0;
+  for (; kt + 1 < nk; kt += 2) {
+    load_tile(s0, min(kt + 2, nk - 1) * kBK);
+    compute(0);
+    store_tile(s1, 1);
+    interleave();
     __syncthreads();
-    if (late) __builtin_amdgcn_s_barrier();
-    for (int kt = 0; kt < nk; ++kt) {
-      read_frags(kt % 3);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-      if (kt + 2 < nk) {
-        store_tile(s0, (kt + 2) % 3);
-        if (kt + 3 < nk) load_tile(s0, (kt + 3) * kBK);
-      }
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int t = 0; t < TERMS; ++t)
-#pragma unroll
-          for (int i = 0; i < RN; ++i)
-#pragma unroll
-            for (int j = 0; j < RM; ++j)
-              acc[i][j] = mfma_32x32x16<F16>(wf[ks][i][t == 2 ? 1 : 0], af[ks][j][t == 1 ? 1 : 0], acc[i][j]);
-#if SEHIP_IGLP
-#pragma unroll
-      for (int i = 0; i < 2 * TERMS * RN * RM; ++i) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                  // MFMA
-        if (i < 6) __builtin_amdgcn_sched_group_barrier(0x200, 1, 0);       // DS write
-        if (i < AJ + 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // global load
-        __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                  // VALU
-      }
-#endif
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
-    }
-    if (!late) __builtin_amdgcn_s_barrier();   // every wave has passed the same number of barriers
-  } else if constexpr (BMX == 2) {
-    // one register staging set (prefetch distance 1): a K-step is 96 MFMAs per
-    // SIMD here, long enough to cover the next tile's loads
-    load_tile(s0, 0);
+    load_tile(s1, min(kt + 3, nk - 1) * kBK);
+    compute(1);
     store_tile(s0, 0);
+    interleave();
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-#if SEHIP_GEMM_PROBE == 1   // measurement probe: MFMA + fragment reads + barrier only
-      const bool more = false;
-#elif SEHIP_GEMM_PROBE == 2 // probe: no global loads (the LDS stores stay)
-      const bool more = kt + 1 < nk;
-      if (false) load_tile(s0, (kt + 1) * kBK);
-#else
-      const bool more = kt + 1 < nk;
-      if (more) load_tile(s0, (kt + 1) * kBK);
-#endif
-      compute(kt & 1);
-      if (more) store_tile(s0, (kt + 1) & 1);
-      interleave();
-      __syncthreads();
-    }
-  } else {
-    // merged stride-phase classes on 256-column tiles: a wave whose 64 columns lie in
-    // a phase without weight at the step's tap skips that step's fragment reads and
-    // MFMAs (they would add exact zeros) and only stages; the other path keeps its
-    // interleaved schedule
-    constexpr bool MSK = NW == 2 && JM != 2;   // instantiations a merged class can run on
-    const unsigned long long zmask =
-        (MSK && a.mrg_np) ? (wn * TN < a.mrg_np ? a.mrg_zero0 : a.mrg_zero1) : 0ull;
-    auto skip = [&](int kt) __attribute__((always_inline)) {
-      if constexpr (!MSK) {
-        return false;
-      } else {
-        if (!zmask) return false;
-        int t, c;
-        split_k(kt * kBK, a.Cg, a.ntaps, a.kblk, t, c);
-        return ((zmask >> t) & 1ull) != 0;
-      }
-    };
-    load_tile(s0, 0);
-    store_tile(s0, 0);
-    if (nk > 1) load_tile(s1, kBK);
-    __syncthreads();
-    int kt = 0;
-    for (; kt + 1 < nk; kt += 2) {
-      load_tile(s0, min(kt + 2, nk - 1) * kBK);
-      if (skip(kt)) {
-        store_tile(s1, 1);
-      } else {
-        compute(0);
-        store_tile(s1, 1);
-        interleave();
-      }
-      __syncthreads();
-      load_tile(s1, min(kt + 3, nk - 1) * kBK);
-      if (skip(kt + 1)) {
-        store_tile(s0, 0);
-      } else {
-        compute(1);
-        store_tile(s0, 0);
-        interleave();
-      }
-      __syncthreads();
-    }
-    if (kt < nk && !skip(kt)) compute(0);
   }
+  if (kt < nk) compute(0);
   if constexpr (F16 && TERMS == 3) {   // undo the operand scales (exact)
 #pragma unroll
-    for (int i = 0; i < QN; ++i)
+    for (int i = 0; i < RN; ++i)
 #pragma unroll
-      for (int j = 0; j < QM; ++j)
+      for (int j = 0; j < RM; ++j)
 #pragma unroll
-        for (int r = 0; r < AR; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], ush);
+        for (int r = 0; r < 16; ++r) acc[i][j][r] = __builtin_ldexpf(acc[i][j][r], ush);
   }
 
   // --- epilogue (as gather_gemm_kernel) ---
   __syncthreads();
   float* sBias = reinterpret_cast<float*>(&sW[0][0]);
   for (int i = tid; i < BN; i += THR) {
-    const int n = a.mrg_np ? (n0 + i) % a.mrg_np : n0 + i;
+    const int n = n0 + i;
     sBias[i] = (a.bias && n < a.N) ? a.bias[n] : 0.f;
   }
   __syncthreads();
   const long long HoWo = (long long)a.Ho * a.Wo;
   const bool full_n = n0 + BN <= a.N;
-  // accumulator map: block (i, j) element r2 is column (m) BLK j + lrow and row
-  // (n) BLK i + 4 lq + roff(r2) of the wave tile
-  constexpr int BLK = M16 ? 16 : 32;
-  const int lrow = M16 ? (lane & 15) : lr, lq = M16 ? (lane >> 4) : lh;
-  auto roff = [](int r2) { return M16 ? r2 : (r2 & 3) + 8 * (r2 >> 2); };
+  // accumulator map: block (i, j) element r2 is column (m) 32 j + lr and row
+  // (n) 32 i + 4 lh + (r2 & 3) + 8 (r2 >> 2) of the wave tile
 #pragma unroll
-  for (int j = 0; j < QM; ++j) {
-    const int mm = m0 + wm * TM + BLK * j + lrow;
+  for (int j = 0; j < RM; ++j) {
+    const int mm = m0 + wm * TM + 32 * j + lr;
     if (mm >= a.M) continue;
     const int qhw = a.Qh * a.Qw;
     const int b = mm / qhw, r = mm - b * qhw;
     const int qh = r / a.Qw, qw = r - qh * a.Qw;
-    const int nl0 = wn * TN + 4 * lq;
+    const int nl0 = wn * TN + 4 * lh;
     if constexpr (JM == 2) {
       // joined output: a 32-row block of n lies in one join chunk (yjh % 32 == 0);
       // s chunks -> Y over Ho x Wo, x chunks -> Y2 over YH2 x YW2 (rows >= YH2,
@@ -661,130 +471,29 @@ gather_x3_kernel(const GatherArgs a) {
       const long long P2 = (long long)a.YH2 * a.YW2;
       const int cpb = 2 * a.yjh;
 #pragma unroll
-      for (int i = 0; i < QN; ++i) {
-        const int nb = n0 + wn * TN + BLK * i;    // block's first channel (wave-uniform)
+      for (int i = 0; i < RN; ++i) {
+        const int nb = n0 + wn * TN + 32 * i;     // block's first channel (wave-uniform)
         const int q = nb / a.yjh;
-        const int cb = (q >> 1) * a.yjh + (nb - q * a.yjh) + 4 * lq;
+        const int cb = (q >> 1) * a.yjh + (nb - q * a.yjh) + 4 * lh;
         const bool to_x = (q & 1) == 0;
         if (to_x && oh >= a.YH2) continue;
         const long long pl = to_x ? P2 : HoWo;
         float* yp = to_x ? a.Y2 + ((long long)b * cpb + cb) * P2 + (long long)oh * a.YW2 + ow
                          : a.Y + ((long long)b * cpb + cb) * HoWo + (long long)oh * a.Wo + ow;
 #pragma unroll
-        for (int r2 = 0; r2 < AR; ++r2) yp[(long long)roff(r2) * pl] = acc[i][j][r2];
+        for (int r2 = 0; r2 < 16; ++r2) yp[(long long)((r2 & 3) + 8 * (r2 >> 2)) * pl] = acc[i][j][r2];
       }
-      continue;
-    }
-    if (a.mrg_np) {   // merged phases: this wave's 64 columns lie in one phase
-      const int mph = (n0 + wn * TN) / a.mrg_np;
-      const int oh = a.ph + mph + a.Sh * qh;
-      if (oh >= a.Ho) continue;
-      const int nc = n0 + nl0 - mph * a.mrg_np;    // channel of this lane's first column
-      const long long yb = (long long)b * a.N * HoWo + (long long)oh * a.Wo + (a.pw + a.Sw * qw) +
-                           (long long)nc * HoWo;
-#pragma unroll
-      for (int i = 0; i < QN; ++i)
-#pragma unroll
-        for (int r2 = 0; r2 < AR; ++r2) {
-          const int nl = BLK * i + roff(r2);
-          if (nc + nl < a.N) st_s<SD>(a.Y, yb + (long long)nl * HoWo, acc[i][j][r2] + sBias[nl0 + nl]);
-        }
       continue;
     }
     const long long yb = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo +
                          (a.pw + a.Sw * qw) + (long long)(n0 + nl0) * HoWo;
 #pragma unroll
-    for (int i = 0; i < QN; ++i)
+    for (int i = 0; i < RN; ++i)
 #pragma unroll
-      for (int r2 = 0; r2 < AR; ++r2) {
-        const int nl = BLK * i + roff(r2);
-        if (full_n || n0 + nl0 + nl < a.N) {
-          float v = acc[i][j][r2] + sBias[nl0 + nl];
-          if (a.accum) v += ld_s<SD>(a.Y, yb + (long long)nl * HoWo);   // = the consumer's gy + gy2, same fp32 add
-          st_s<SD>(a.Y, yb + (long long)nl * HoWo, v);
-        }
+      for (int r2 = 0; r2 < 16; ++r2) {
+        const int nl = 32 * i + (r2 & 3) + 8 * (r2 >> 2);
+        if (full_n || n0 + nl0 + nl < a.N) st_s<SD>(a.Y, yb + (long long)nl * HoWo, acc[i][j][r2] + sBias[nl0 + nl]);
       }
-  }
-
-  // --- ComplexBatchNorm moments of this tile (se_conv2d_desc.moments) ---
-  // The output y = acc + bias of complex channel cc is columns cc (re) and
-  // cc + N/2 (im), both inside this tile (N <= BN, checked by the host). Per
-  // channel, over the tile's valid positions: the fp64 sums of yr, yi, yr^2,
-  // yr yi, yi^2 and the extrema max yr, -min yr, max yi, -min yi -- the row
-  // cbn_moments_kernel writes per partition, here partition mom_p0 + (M-tile).
-  // The CBN forward then skips its pass over y (se_cbn_fwd_moments).
-  // The tile goes through LDS in rounds of RQ positions ([RQ][BN + 4] fp32,
-  // in the dead sA stages); THR / Cc threads share a channel, their partial
-  // sums are added in a fixed order (deterministic).
-  if constexpr (SD == 0 && JM != 2 && BMX == 1 && !PP && !M16) {
-    if (a.mom) {
-      constexpr int RQ = 32 / NW, LDT = BN + 4;
-      float* T = reinterpret_cast<float*>(&sA[0][0]);
-      const int Cc = a.N >> 1;
-      const int tpc = THR / Cc;                     // threads per channel
-      const int cc = tid % Cc, r0 = tid / Cc;
-      const bool red = r0 < tpc;
-      double v[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-      float e[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-#pragma unroll
-      for (int w = 0; w < WM; ++w)
-#pragma unroll
-        for (int j = 0; j < RM; ++j)
-#pragma unroll
-          for (int h = 0; h < NW; ++h) {
-            __syncthreads();
-            if (wm == w && lr / RQ == h) {   // the lanes of positions h RQ .. h RQ + RQ - 1 of block j
-#pragma unroll
-              for (int i = 0; i < RN; ++i)
-#pragma unroll
-                for (int g4 = 0; g4 < 4; ++g4) {
-                  const int nl = wn * TN + 32 * i + 4 * lh + 8 * g4;
-                  float4 q;
-                  q.x = acc[i][j][4 * g4 + 0] + sBias[nl + 0];
-                  q.y = acc[i][j][4 * g4 + 1] + sBias[nl + 1];
-                  q.z = acc[i][j][4 * g4 + 2] + sBias[nl + 2];
-                  q.w = acc[i][j][4 * g4 + 3] + sBias[nl + 3];
-                  *reinterpret_cast<float4*>(T + (lr - h * RQ) * LDT + nl) = q;
-                }
-            }
-            __syncthreads();
-            if (red) {
-              const int mb = m0 + w * TM + 32 * j + h * RQ;
-              for (int r = r0; r < RQ; r += tpc) {
-                if (mb + r >= a.M) break;
-                const float fr = T[r * LDT + cc], fm = T[r * LDT + cc + Cc];
-                e[0] = fmaxf(e[0], fr); e[1] = fmaxf(e[1], -fr); e[2] = fmaxf(e[2], fm); e[3] = fmaxf(e[3], -fm);
-                const double dr = fr, dm = fm;
-                v[0] += dr; v[1] += dm; v[2] += dr * dr; v[3] += dr * dm; v[4] += dm * dm;
-              }
-            }
-          }
-      __syncthreads();
-      double* R = reinterpret_cast<double*>(&sA[0][0]);   // [tpc][Cc][5], then [tpc][Cc][4] extrema
-      float* E = reinterpret_cast<float*>(R + (long long)THR * 5);
-      if (red) {
-#pragma unroll
-        for (int k = 0; k < 5; ++k) R[(r0 * Cc + cc) * 5 + k] = v[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) E[(r0 * Cc + cc) * 4 + k] = e[k];
-      }
-      __syncthreads();
-      if (tid < Cc) {
-        const long long row = (long long)tid * a.mom_P + a.mom_p0 + mt;
-        double s[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-        float x4[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
-        for (int t = 0; t < tpc; ++t) {
-#pragma unroll
-          for (int k = 0; k < 5; ++k) s[k] += R[(t * Cc + tid) * 5 + k];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) x4[k] = fmaxf(x4[k], E[(t * Cc + tid) * 4 + k]);
-        }
-#pragma unroll
-        for (int k = 0; k < 5; ++k) a.mom[row * 5 + k] = s[k];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) a.mom_ext[row * 4 + k] = x4[k];
-      }
-    }
   }
 }
 
@@ -806,15 +515,11 @@ typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
 
 // chunk swizzle of position row s (an involution on the 16 chunks)
 __device__ __forceinline__ int wx3_swz(int s) {
-#if SEHIP_SWZ2
   // bits 2-3 = s & 3 keep the transposed reads conflict-free (4 consecutive positions x 4
   // chunks on 16 distinct 16-B slots); bits 0-2 = (s1, s2, s0) put 8 consecutive positions
-  // of one ds_write_b128 store group on 8 distinct slots (the form below: 2-way, which
-  // was a third of the weight-grads' LDS-array cycles, tools/pmc_lds.sh)
+  // of one ds_write_b128 store group on 8 distinct slots (the round-2 form (s >> 2) & 3 was
+  // 2-way: a third of the weight-grads' LDS-array cycles, tools/pmc_lds.sh)
   return ((s & 3) << 2) | (((s >> 2) & 1) << 1) | ((s >> 1) & 1);
-#else
-  return ((s & 3) << 2) | ((s >> 2) & 3);
-#endif
 }
 __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chunk ch of position row s
   return 256 * s + 16 * (ch ^ wx3_swz(s));
@@ -827,28 +532,24 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // for 256 output columns (a thread stages 8 G rows and 16 D rows instead of
 // 16 + 16), a quarter fewer loads and splits per MFMA; every output keeps its
 // m-split and its order of positions, so the slabs are bit-identical.
-// KB: the same with two 128-row G blocks (tile 256 k x 128 n, 8 waves): the D
-// tile of a step is staged once for two taps (a thread stages 16 G rows and 8
-// D rows); for N = 128 (the encoder's weight-grads, 10 k-tiles per split).
 // KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
 // SD: storage type of X / D (as gather_x3_kernel; 16-bit with the one-term MFMA)
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int KB = 1,
-          int SD = 0>
-__global__ void __launch_bounds__(kThreads * NB * KB, SEHIP_WGRAD_OCC)
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0>
+__global__ void __launch_bounds__(kThreads * NB, 2)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(SD == 0 || (TERMS == 1 && !DJ), "16-bit storage: one-term, no join");
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   constexpr int ES = SD ? 2 : 4;             // bytes per element of X / D
-  static_assert(NB * KB <= 2, "one or two 128-row D blocks, or two G blocks");
+  static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
-  constexpr int BKO = 128 * KB, BNO = 128 * NB, WNn = 2 * NB, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
-  constexpr int RJ = 16 / KB;                // D rows per thread
+  constexpr int BKO = 128, BNO = 128 * NB, WNn = 2 * NB, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
+  constexpr int RJ = 16;                     // D rows per thread
   constexpr int RJG = 16 / NB;               // G rows per thread
   constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
   // per 128-row G block: G hi, G lo; then per 128-row D block: D hi, D lo
-  constexpr int DPL = 2 * KB;                // first D plane
-  __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 * KB + 2 * NB) * PLANE];
+  constexpr int DPL = 2;                     // first D plane
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 + 2 * NB) * PLANE];
   __shared__ int4 sK[BKO];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -874,9 +575,8 @@ wgrad_x3_kernel(const WgradArgs a) {
   const int kv = KP ? min(BKO, a.ntaps * a.Cg - k0) : BKO;
   const int kvw = kv - wk * TK;                       // ... of this wave's 64 MFMA rows
   const bool gact = (32 / NB) * wave < kv;            // this wave stages some valid G row
-  const int rbase = (32 / KB) * wave + RJ * lr;     // this thread's first D row
+  const int rbase = 32 * wave + RJ * lr;     // this thread's first D row
   const int rbase_g = (32 / NB) * wave + RJG * lr;  // ... and first G row
-  const int gblk = ((32 / NB) * wave) >> 7;         // G block of this wave's rows (wave-uniform)
 
   for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
   __syncthreads();
@@ -916,8 +616,8 @@ wgrad_x3_kernel(const WgradArgs a) {
   if constexpr (DJ)
     rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.D2 + (long long)bfirst * dcpb * QQ2), (short)0,
                                                 0x7FFFFFFF, 0x00020000);
-  const int4 tap_e = sK[128 * gblk];                // TU: one tap per 128-row block
-  const int cbase = (k0 + 128 * gblk) % a.Cg;
+  const int4 tap_e = sK[0];                         // TU: one tap per 128-row k-tile
+  const int cbase = k0 % a.Cg;
   const bool one_wrap = a.Qw >= BMR;
   auto advance = [&]() __attribute__((always_inline)) {
     if (one_wrap) {
@@ -946,12 +646,12 @@ wgrad_x3_kernel(const WgradArgs a) {
     // Np-padded tail; tail rows read 0 through an out-of-range voffset (they
     // must not be read: past the last batch item they leave the allocation).
     const bool dok = mv & (n0 + rbase < a.N);
-    int vd, ds = (int)(QQ * ES), srow = (32 / KB) * wave;
+    int vd, ds = (int)(QQ * ES), srow = 32 * wave;
     __amdgpu_buffer_rsrc_t rdr = rd_src;
     if constexpr (DJ) {
       // joined D: chunks [x_re, s_re, x_im, s_im] of djh rows; a wave's 32 rows
       // lie in one chunk (djh % 32 == 0)
-      const int nb = n0 + (32 / KB) * wave;
+      const int nb = n0 + 32 * wave;
       const int q = nb / a.djh;
       const bool from_x = (q & 1) == 0;
       const int cr = (q >> 1) * a.djh + (nb - q * a.djh) + RJ * lr;   // row in its source
@@ -1003,7 +703,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
     unsigned char* base = sm[buf];
     unsigned char* dbase = base + (DPL + 2 * (rbase >> 7)) * PLANE;   // this thread's D block
-    unsigned char* gbase = base + 2 * gblk * PLANE;                    // ... and G block
+    unsigned char* gbase = base;                                       // ... and G block
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       u32x4 GH, GL, DH, DL;
@@ -1083,7 +783,6 @@ wgrad_x3_kernel(const WgradArgs a) {
     }
   };
   auto interleave = [&]() __attribute__((always_inline)) {
-#if SEHIP_IGLP
     __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
     for (int i = 0; i < 24; ++i) {
@@ -1092,7 +791,6 @@ wgrad_x3_kernel(const WgradArgs a) {
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // global load
       __builtin_amdgcn_sched_group_barrier(0x002, 4, 0);              // VALU
     }
-#endif
   };
   if (nsteps > 0) {
     load_step(st0, mbeg);
@@ -1366,7 +1064,6 @@ gather_x6_kernel(const GatherArgs a) {
               acc[i][j], 0, 0, 0);
   };
   auto interleave = [&]() __attribute__((always_inline)) {
-#if SEHIP_IGLP
     __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);
 #pragma unroll
     for (int i = 0; i < 24; ++i) {
@@ -1375,7 +1072,6 @@ gather_x6_kernel(const GatherArgs a) {
       if (i < AJ + 3) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
     }
-#endif
   };
 
   const int nk = a.Kp / BK;
@@ -1424,200 +1120,5 @@ gather_x6_kernel(const GatherArgs a) {
         const int nl = 32 * i + (r2 & 3) + 8 * (r2 >> 2);
         if (full_n || n0 + nl0 + nl < a.N) yb[(long long)nl * HoWo] = acc[i][j][r2] + sBias[nl0 + nl];
       }
-  }
-}
-
-// ---------------------------------------------------------------------------
-// Three-multiplication ("3M", Gauss) complex GEMM for the split-fp16 forward
-// (SE_MATH_F16X3, 64 complex outputs). With x = xr + i xi the gathered complex
-// input and W = Wr + i Wi the complex weight of a (tap, input, output) triple,
-//   k1 = (xr + xi) Wr,  k2 = xr (Wi - Wr),  k3 = xi (Wr + Wi)
-//   y_re = k1 - k3 = xr Wr - xi Wi,  y_im = k1 + k2 = xr Wi + xi Wr
-// so a complex multiply-add takes 3 real products instead of the 4 of the block
-// GEMM against [[Wr, Wi], [-Wi, Wr]]: 3/4 of the MFMA issues. Each of the three
-// operand pairs is split hi + lo fp16 with the tensor's power-of-two scale (the
-// pre-sums stay below 2^15, inside fp16's range) and multiplied with the three
-// terms hh + hl + lh; k1, k2, k3 accumulate in fp32 and are combined in the
-// epilogue. Per conv vs fp64 this stays fp32-class (numpy emulation of the
-// MFMA accumulation: 1.98e-7 vs 1.77e-7 for the 4-product form and 2.51e-7 for
-// exact fp32; measured on the GPU in tests/test_gpu_conv_3m.py).
-// Tile: 128 positions x 64 complex outputs, 4 waves of 64 positions x 32
-// outputs; a K-step is 16 complex input channels of one tap. LDS image of a
-// step: A [op 3][plane 2][chunk 2][128 rows] x 16 B (op 0 = xr + xi, 1 = xr,
-// 2 = xi), W [op][plane][chunk][64 rows] x 16 B (op 0 = Wr, 1 = Wi - Wr,
-// 2 = Wr + Wi), pre-built per step by prep_3m_kernel; chunk-major rows make
-// every fragment read and every store one contiguous 1-KB wave access.
-// JM = 1: the gathered tensor is the decoder skip join (GatherArgs::X2 = x,
-// X = s; complex channels [x (jh), s (jh)]).
-// ---------------------------------------------------------------------------
-constexpr int k3mBKc = 16;                          // complex channels per K-step
-constexpr int k3mImgU4 = 3 * 2 * 2 * 64;            // u32x4 of a step's weight image (12 KB)
-
-__global__ void prep_3m_kernel(WeightView w, TapList taps, int Cc, int N, int nk, const float* amax_w,
-                               unsigned short* img) {
-  const int Cco = N / 2, spt = Cc / k3mBKc;
-  const float sw = pow2f(kF16Top - amax_exp(amax_w));
-  const long long total = (long long)nk * 64 * k3mBKc;
-  for (long long idx = blockIdx.x * (long long)blockDim.x + threadIdx.x; idx < total;
-       idx += (long long)gridDim.x * blockDim.x) {
-    const int k = (int)(idx % k3mBKc), nc = (int)((idx / k3mBKc) % 64), s = (int)(idx / (64 * k3mBKc));
-    const int t = s / spt, c = (s - t * spt) * k3mBKc + k;
-    float wr = 0.f, wi = 0.f;
-    if (nc < Cco) {
-      wr = kernel_value(w, c, nc, taps.ti[t], taps.tj[t]);
-      wi = kernel_value(w, c, Cco + nc, taps.ti[t], taps.tj[t]);
-    }
-    const float vals[3] = {wr, wi - wr, wr + wi};
-    const int chunk = k >> 3, e = k & 7;
-    unsigned short* base = img + (long long)s * k3mImgU4 * 8;
-#pragma unroll
-    for (int o = 0; o < 3; ++o) {
-      const float v = vals[o] * sw;
-      const _Float16 h = (_Float16)v;
-      base[(((o * 2 + 0) * 2 + chunk) * 64 + nc) * 8 + e] = __builtin_bit_cast(unsigned short, h);
-      base[(((o * 2 + 1) * 2 + chunk) * 64 + nc) * 8 + e] =
-          __builtin_bit_cast(unsigned short, (_Float16)(v - (float)h));
-    }
-  }
-}
-
-template <int JM>
-__global__ void __launch_bounds__(kThreads, 2) gather_3m_kernel(const GatherArgs a) {
-  __shared__ __attribute__((aligned(16))) u32x4 sA[2][3 * 2 * 2 * 128];   // 24 KB per stage
-  __shared__ __attribute__((aligned(16))) u32x4 sW[2][k3mImgU4];          // 12 KB per stage
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wn = wave >> 1, wm = wave & 1;
-  const int Cc = a.Cg / 2, spt = Cc / k3mBKc, nk = a.ntaps * spt;
-  const int m0 = xcd_remap(blockIdx.x, gridDim.x) * 128;
-  const int am = tid & 127, kh = tid >> 7;          // staging: position, 8-channel half of the step
-  const int m = m0 + am;
-  const bool mval = m < a.M;
-  int b = 0, hb = 0, wb = 0;
-  if (mval) {
-    const int qhw = a.Qh * a.Qw;
-    b = m / qhw;
-    const int r = m - b * qhw, qh = r / a.Qw, qw = r - qh * a.Qw;
-    hb = qh * a.sh;
-    wb = qw * a.sw;
-  }
-  const int ea = amax_exp(a.amax_a);
-  const float sa = pow2f(kF16Top - ea);
-  const int ush = ea + amax_exp(a.amax_w) - 2 * kF16Top;
-  const long long HiWi = (long long)a.Hi * a.Wi, H2W2 = (long long)a.H2 * a.W2;
-  float xr[8], xi[8];
-  u32x4 rw[3];
-  auto load = [&](int s) __attribute__((always_inline)) {
-    const int t = s / spt, cb = (s - t * spt) * k3mBKc + 8 * kh;   // first complex channel
-    const int hi = hb + a.toffh[t], wi = wb + a.toffw[t];
-    bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-    const float* src = a.X;
-    long long cs = HiWi, off;
-    int cre, cim;
-    if constexpr (JM == 1) {
-      const bool from_x = cb < a.jh;                // a step lies in one jh chunk (jh % 16 == 0)
-      const int c = from_x ? cb : cb - a.jh;
-      cre = c;
-      cim = a.jh + c;
-      ok &= !from_x | (hi < a.H2);                  // F.pad rows of x read 0
-      if (from_x) {
-        src = a.X2;
-        cs = H2W2;
-        off = (long long)b * 2 * a.jh * H2W2 + (long long)hi * a.W2 + wi;
-      } else {
-        off = (long long)b * 2 * a.jh * HiWi + (long long)hi * a.Wi + wi;
-      }
-    } else {
-      cre = cb;
-      cim = Cc + cb;
-      off = (long long)b * a.Cg * HiWi + (long long)hi * a.Wi + wi;
-    }
-    off = ok ? off : 0;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) {
-      const float v0 = src[off + (long long)(cre + j) * cs], v1 = src[off + (long long)(cim + j) * cs];
-      xr[j] = ok ? v0 : 0.f;
-      xi[j] = ok ? v1 : 0.f;
-    }
-    const u32x4* wsrc = reinterpret_cast<const u32x4*>(a.Wp) + (long long)s * k3mImgU4;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) rw[q] = wsrc[tid + kThreads * q];
-  };
-  auto store = [&](int buf) __attribute__((always_inline)) {
-    u32x4 H[3], L[3];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      unsigned h, l;
-      split_f16x2(xr[2 * e] + xi[2 * e], xr[2 * e + 1] + xi[2 * e + 1], sa, h, l);
-      H[0][e] = h; L[0][e] = l;
-      split_f16x2(xr[2 * e], xr[2 * e + 1], sa, h, l);
-      H[1][e] = h; L[1][e] = l;
-      split_f16x2(xi[2 * e], xi[2 * e + 1], sa, h, l);
-      H[2][e] = h; L[2][e] = l;
-    }
-#pragma unroll
-    for (int o = 0; o < 3; ++o) {
-      sA[buf][((o * 2 + 0) * 2 + kh) * 128 + am] = H[o];
-      sA[buf][((o * 2 + 1) * 2 + kh) * 128 + am] = L[o];
-    }
-#pragma unroll
-    for (int q = 0; q < 3; ++q) sW[buf][tid + kThreads * q] = rw[q];
-  };
-  f32x16 acc[3][2];
-#pragma unroll
-  for (int o = 0; o < 3; ++o)
-#pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int r = 0; r < 16; ++r) acc[o][j][r] = 0.f;
-  const int lh = lane >> 5, lr = lane & 31;
-  auto compute = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int o = 0; o < 3; ++o) {
-      u32x4 wf[2], af[2][2];
-#pragma unroll
-      for (int p = 0; p < 2; ++p) {
-        wf[p] = sW[buf][((o * 2 + p) * 2 + lh) * 64 + wn * 32 + lr];
-#pragma unroll
-        for (int j = 0; j < 2; ++j) af[j][p] = sA[buf][((o * 2 + p) * 2 + lh) * 128 + wm * 64 + 32 * j + lr];
-      }
-#pragma unroll
-      for (int t = 0; t < 3; ++t)   // hi*hi, hi*lo, lo*hi
-#pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[o][j] = mfma_32x32x16<true>(wf[t == 2 ? 1 : 0], af[j][t == 1 ? 1 : 0], acc[o][j]);
-    }
-  };
-  if (nk > 0) {
-    load(0);
-    store(0);
-    __syncthreads();
-    for (int s = 0; s < nk; ++s) {
-      const bool more = s + 1 < nk;
-      if (more) load(s + 1);
-      compute(s & 1);
-      if (more) store((s + 1) & 1);
-      __syncthreads();
-    }
-  }
-  // accumulator map: block (o, j) element r2 is output nc = 32 wn + 4 lh + (r2 & 3) + 8 (r2 >> 2),
-  // position m = m0 + 64 wm + 32 j + lr
-  const int Cco = a.N / 2;
-  const long long HoWo = (long long)a.Ho * a.Wo;
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int mm = m0 + wm * 64 + 32 * j + lr;
-    if (mm >= a.M) continue;
-    const int qhw = a.Qh * a.Qw;
-    const int bb = mm / qhw, r = mm - bb * qhw, qh = r / a.Qw, qw = r - qh * a.Qw;
-    const long long yb = (long long)bb * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
-#pragma unroll
-    for (int r2 = 0; r2 < 16; ++r2) {
-      const int nc = wn * 32 + 4 * lh + (r2 & 3) + 8 * (r2 >> 2);
-      if (nc >= Cco) continue;
-      const float yre = __builtin_ldexpf(acc[0][j][r2] - acc[2][j][r2], ush) + (a.bias ? a.bias[nc] : 0.f);
-      const float yim = __builtin_ldexpf(acc[0][j][r2] + acc[1][j][r2], ush) + (a.bias ? a.bias[Cco + nc] : 0.f);
-      a.Y[yb + (long long)nc * HoWo] = yre;
-      a.Y[yb + (long long)(Cco + nc) * HoWo] = yim;
-    }
   }
 }

@@ -28,28 +28,3 @@ extern "C" int se_probe(int* out, int n, void* stream) {
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
-
-// A HIP stream restricted to a subset of the CUs (hipExtStreamCreateWithCUMask):
-// CU i is enabled when (i % den) < num. Used for the deferred weight-grad side
-// stream, so the MFMA-bound weight-grads cannot take the CUs the main stream's
-// HBM-bound passes need.
-extern "C" int se_stream_create_cu_subset(int num, int den, void** stream) {
-  if (!stream || den <= 0 || num <= 0 || num > den) return SE_E_ARG;
-  int dev = 0, cus = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return SE_E_LAUNCH;
-  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess) return SE_E_LAUNCH;
-  const int words = (cus + 31) / 32;
-  uint32_t mask[64] = {0};
-  if (words > 64) return SE_E_UNSUPPORTED;
-  for (int i = 0; i < cus; ++i)
-    if ((i % den) < num) mask[i / 32] |= 1u << (i % 32);
-  hipStream_t s = nullptr;
-  if (hipExtStreamCreateWithCUMask(&s, (uint32_t)words, mask) != hipSuccess) return SE_E_LAUNCH;
-  *stream = (void*)s;
-  return SE_OK;
-}
-
-extern "C" int se_stream_destroy(void* stream) {
-  if (!stream) return SE_E_ARG;
-  return hipStreamDestroy((hipStream_t)stream) == hipSuccess ? SE_OK : SE_E_LAUNCH;
-}

@@ -3,7 +3,7 @@
 // which runs torch.nn.LSTM; gate order i, f, g, o; h0 = c0 = 0).
 //
 // The input projection X·W_ihᵀ + b_ih + b_hh and all weight gradients are
-// plain GEMMs done by the host (rocBLAS). What remains is the strictly
+// plain GEMMs (se_gemm, csrc/gemm.hip). What remains is the strictly
 // sequential part, which MIOpen runs as 2-3 launches per time step:
 //
 //   fwd:  z_t = xproj_t + W_hh h_{t-1};  i,f,o = σ(z), g = tanh(z)
@@ -13,14 +13,9 @@
 // One launch runs every time step. Each workgroup owns BS sequences of one
 // stacked LSTM and ALL of W_hh (4H x H fp32 = 256 KB at H = 128) in VGPRs —
 // thread r holds gate row r (fwd) or a 128-row slice of column k (bwd) — so
-// workgroups never talk to each other. The recurrent operand (h_{t-1} fwd,
-// dgates_t bwd) is the same for every lane of a wave: it is written to global
-// memory, then read back with SCALAR loads (s_load_dwordx16, never cached
-// before: each row is read exactly once after it is written) and consumed as
-// the SGPR operand of v_pk_fma_f32. Per step and workgroup that is
-// BS·4H·H MACs in 2·H packed FMAs per thread. Before the chunked loads, one
-// s_load_dword per 64-B line pulls the rows into the scalar cache with a
-// single L2 round trip (measured: 4.7 -> 2.7 us per forward step at H = 128).
+// workgroups never talk to each other; the recurrent operand goes through LDS
+// (below). Per step and workgroup that is BS·4H·H MACs in 2·H packed FMAs per
+// thread.
 #include "common.hpp"
 
 #include <cstdlib>
@@ -29,69 +24,10 @@
 namespace {
 
 typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef const __attribute__((address_space(4))) f32x2* sptr2;
-
-// Launder a uniform pointer through an empty asm so the scalar loads issued
-// from it cannot be hoisted above the barrier that publishes the data.
-// The value is uniform by construction; readfirstlane makes that explicit for
-// the divergence analysis (which cannot always prove it across the loop).
-__device__ __forceinline__ sptr2 scalar_view(const float* p) {
-  const unsigned long long v = reinterpret_cast<unsigned long long>(p);
-  // (readfirstlane returns int: go through unsigned, or the low word sign-extends)
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  unsigned long long u = ((unsigned long long)hi << 32) | lo;
-  asm volatile("" : "+s"(u));
-  return reinterpret_cast<sptr2>(u);
-}
-
-constexpr int kChunk = 32;
-
-// s_waitcnt vmcnt(n) (expcnt/lgkmcnt left open), via the builtin so the
-// compiler's waitcnt pass knows about it (an asm wait is invisible to it).
-template <int n>
-__device__ __forceinline__ void wait_vmcnt() {
-  static_assert(n >= 0 && n < 64, "vmcnt");
-  __builtin_amdgcn_s_waitcnt(0x0F70 | (n & 0xF) | ((n >> 4) << 14));
-}   // f32x2 pairs per row per scalar-load chunk
-
-// Pull the rows this step will scalar-load into the scalar cache with one
-// s_load_dword per 64-B line, all in flight together, one wait: ONE L2 round
-// trip per step instead of one per kChunk chunk (the chunk loads then hit K$).
-// The loads, their (discarded) destination and the lgkmcnt(0) wait are ONE asm
-// statement with an early-clobber output: as separate statements the compiler
-// saw the destination SGPR as dead right after each load and reused it for
-// address arithmetic while the load was still in flight; the late return then
-// overwrote a live scalar address (a wild s_load: memory-aperture violation
-// that came and went with the tensors' placement).
-__device__ __forceinline__ unsigned long long uniform_addr(const float* row) {
-  const unsigned long long v = reinterpret_cast<unsigned long long>(row);
-  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-  const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-  return ((unsigned long long)hi << 32) | lo;
-}
-#define SE_WARM4(P) "s_load_dword %0, " P ", 0x0\n s_load_dword %0, " P ", 0x40\n " \
-                    "s_load_dword %0, " P ", 0x80\n s_load_dword %0, " P ", 0xc0\n "
-#define SE_WARM8(P) SE_WARM4(P) "s_load_dword %0, " P ", 0x100\n s_load_dword %0, " P ", 0x140\n " \
-                    "s_load_dword %0, " P ", 0x180\n s_load_dword %0, " P ", 0x1c0\n "
-// two rows (BS = 2) of NLINES 64-B lines each, then s_waitcnt lgkmcnt(0)
-template <int NLINES>
-__device__ __forceinline__ void warm_kcache2(const float* r0, const float* r1) {
-  static_assert(NLINES == 4 || NLINES == 8, "H = 64 or 128");
-  const unsigned long long u0 = uniform_addr(r0), u1 = uniform_addr(r1);
-  unsigned dummy;
-  if constexpr (NLINES == 8)
-    asm volatile(SE_WARM8("%1") SE_WARM8("%2") "s_waitcnt lgkmcnt(0)"
-                 : "=&s"(dummy) : "s"(u0), "s"(u1) : "memory");
-  else
-    asm volatile(SE_WARM4("%1") SE_WARM4("%2") "s_waitcnt lgkmcnt(0)"
-                 : "=&s"(dummy) : "s"(u0), "s"(u1) : "memory");
-}
-
 __device__ __forceinline__ float sigmoidf(float x) { return 1.f / (1.f + expf(-x)); }
 
 // Branch-free tanh (ocml's tanhf branches, which splits the step loop into
-// many basic blocks and defeats the chunked scalar-load schedule). |x| < 1/16:
+// many basic blocks and defeats the unrolled step schedule). |x| < 1/16:
 // odd Taylor series to x^7 (truncation < 1e-11 rel); else (1-e)/(1+e) with
 // e = exp(-2|x|) (rel. error ~5e-7 from rounding of e).
 __device__ __forceinline__ float tanh_bf(float x) {
@@ -117,241 +53,16 @@ struct LstmArgs {
   unsigned rev_mask;    // bit l: LSTM l runs right-to-left (bidirectional reverse direction)
 };
 
-template <int H, int BS>
-__global__ __launch_bounds__(4 * H) void lstm_fwd_kernel(LstmArgs a) {
-  constexpr int G = 4 * H;
-  const int r = threadIdx.x;
-  const int l = blockIdx.y, b0 = blockIdx.x * BS;
-  const bool rev = (a.rev_mask >> l) & 1u;
-  const int T = a.T;
-  const size_t lb = (size_t)l * a.B + b0;            // first (lstm, sequence) row
-
-  f32x2 w[H / 2];
-  {
-    const f32x2* W = reinterpret_cast<const f32x2*>(a.w_hh + ((size_t)l * G + r) * H);
-#pragma unroll
-    for (int q = 0; q < H / 2; ++q) w[q] = W[q];
-  }
-  __shared__ float sg[BS][G];
-
-  const float* xp = a.xproj + (size_t)l * a.x_lstm + r;
-  int brow[BS];                                      // sequence rows, clamped (odd B: last group)
-#pragma unroll
-  for (int b = 0; b < BS; ++b) brow[b] = min(b0 + b, a.B - 1);
-  const int gate = __builtin_amdgcn_readfirstlane(r / H);   // wave-uniform (H % 64 == 0)
-  // Cell (b, j) = r mod BS*H: every thread runs a cell update (the 4H/(BS*H)
-  // copies of a cell compute identical values and store them to the same
-  // address), so the step body has no divergent branch. Rows past B are
-  // clamped onto row B-1 and reproduce its values exactly.
-  static_assert((4 * H) % (BS * H) == 0, "threads must cover the cells");
-  const int cb = (r % (BS * H)) / H, cj = r % H;
-  const size_t crow = (size_t)l * a.B + brow[cb];
-  float cst = 0.f;
-
-  // time runs t = t0 + dir*s (branch-free, so the step loop is not unswitched)
-  const int dir = rev ? -1 : 1, t0 = rev ? T - 1 : 0;
-  const long long xstep = (long long)dir * a.x_row;
-  // xproj ring, prefetch distance 2: the loads for step s+2 are issued after
-  // step s's stores, so the h_t publish wait (vmcnt(BS)) leaves them in flight
-  auto xload = [&](int sx, float* dst) __attribute__((always_inline)) {
-    const float* q = xp + (size_t)(t0 + dir * min(sx, T - 1)) * a.x_row;
-#pragma unroll
-    for (int b = 0; b < BS; ++b) dst[b] = q[(size_t)brow[b] * T * a.x_row];
-  };
-  // Unrolled by two over a two-slot ring (slot s&1 holds step s's xproj): no
-  // register rotation, so no copy of an in-flight load forces a vmcnt(0).
-  wait_vmcnt<0>();                                   // W_hh resident before the ring starts
-  float xa[BS], xb[BS];
-  xload(0, xa);
-  xload(1, xb);
-  auto step = [&](int s, float* xs) __attribute__((always_inline)) {
-    const int t = t0 + dir * s;
-    float z[BS];
-#pragma unroll
-    for (int b = 0; b < BS; ++b) z[b] = xs[b];
-    {
-      // h_{t-1} rows (a zero row at s = 0: uniform select, no peeled iteration)
-      const float* hbase = a.h + ((size_t)l * a.B * T + (t - dir)) * H;
-      const float* hb[BS];
-#pragma unroll
-      for (int b = 0; b < BS; ++b) hb[b] = s > 0 ? hbase + (size_t)brow[b] * T * H : a.zero;
-      f32x2 acc[BS][2];
-#pragma unroll
-      for (int b = 0; b < BS; ++b) acc[b][0] = acc[b][1] = f32x2{0.f, 0.f};
-      static_assert(BS == 2, "warm_kcache2 pulls two rows");
-      warm_kcache2<H * 4 / 64>(hb[0], hb[1]);
-#pragma unroll
-      for (int b = 0; b < BS; ++b)
-#pragma unroll
-        for (int q0 = 0; q0 < H / 2; q0 += kChunk) {
-          sptr2 hp = scalar_view(hb[b] + 2 * q0);
-#pragma unroll
-          for (int q = 0; q < kChunk; ++q)
-            acc[b][q & 1] = __builtin_elementwise_fma(w[q0 + q], hp[q], acc[b][q & 1]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-      for (int b = 0; b < BS; ++b) z[b] += (acc[b][0].x + acc[b][0].y) + (acc[b][1].x + acc[b][1].y);
-    }
-    float v[BS];
-#pragma unroll
-    for (int b = 0; b < BS; ++b) {
-      const float th = tanh_bf(z[b]), sg_ = sigmoidf(z[b]);   // both: branch-free step body
-      v[b] = gate == 2 ? th : sg_;
-      sg[b][r] = v[b];
-    }
-    // Branch-free partial group: an invalid row is clamped onto the last valid
-    // row (B-1), stored first, and overwritten by that row's own store.
-#pragma unroll
-    for (int b = BS - 1; b >= 0; --b) a.gates[(((size_t)l * a.B + brow[b]) * T + t) * G + r] = v[b];
-    __syncthreads();
-    {
-      const float ig = sg[cb][cj], fg = sg[cb][H + cj], gg = sg[cb][2 * H + cj], og = sg[cb][3 * H + cj];
-      cst = fg * cst + ig * gg;
-      const size_t o = (crow * T + t) * H + cj;
-      a.c[o] = cst;
-      a.h[o] = og * tanh_bf(cst);
-    }
-    asm volatile("" ::: "memory");                   // stores before the prefetch
-    xload(s + 2, xs);
-    // h_t must be in L2 before any wave scalar-loads it next step; only the
-    // BS prefetch loads (issued last) may still be outstanding
-    wait_vmcnt<BS>();
-    __syncthreads();
-  };
-  // both steps unconditional: the only edge into the loop header comes after a
-  // slot-b step, so the waitcnt pass sees slot a's loads as already drained
-  int s = 0;
-  for (; s + 1 < T; s += 2) {
-    step(s, xa);
-    step(s + 1, xb);
-  }
-  if (s < T) step(s, xa);
-}
-
-template <int H, int BS>
-__global__ __launch_bounds__(4 * H) void lstm_bwd_kernel(LstmArgs a) {
-  constexpr int G = 4 * H;
-  const int tid = threadIdx.x;
-  const int k = tid % H;
-  const int rq = __builtin_amdgcn_readfirstlane(tid / H);   // wave-uniform (H % 64 == 0)
-  const int l = blockIdx.y, b0 = blockIdx.x * BS;
-  const bool rev = (a.rev_mask >> l) & 1u;
-  const int T = a.T;
-  const size_t lb = (size_t)l * a.B + b0;
-
-  // column k of W_hh, rows rq*H .. rq*H+H-1, packed in row pairs
-  f32x2 w[H / 2];
-  {
-    const float* W = a.w_hh + ((size_t)l * G + rq * H) * H + k;
-#pragma unroll
-    for (int p = 0; p < H / 2; ++p) w[p] = f32x2{W[(2 * p) * H], W[(2 * p + 1) * H]};
-  }
-  __shared__ float sp[4][BS][H];
-
-  // Cell (b, j) = tid mod BS*H, duplicated across threads exactly as in
-  // lstm_fwd_kernel: identical values, identical addresses, no branch.
-  static_assert((4 * H) % (BS * H) == 0, "threads must cover the cells");
-  const int cb = (tid % (BS * H)) / H, cj = tid % H;
-  float dc = 0.f, dh_rec = 0.f;
-  const size_t rowc = ((size_t)l * a.B + min(b0 + cb, a.B - 1)) * T;
-  const int dir = rev ? -1 : 1, t0 = rev ? T - 1 : 0;
-
-  struct Pre { float dy, c, cp, g[4]; };
-  auto fetch = [&](int sx, Pre& p) __attribute__((always_inline)) {
-    sx = max(sx, 0);
-    const int t = t0 + dir * sx;
-    const int tp = t0 + dir * max(sx - 1, 0);
-    const size_t o = (rowc + t) * H + cj;
-    p.dy = a.dy[o];
-    p.c = a.c[o];
-    p.cp = a.c[(rowc + tp) * H + cj] * (sx > 0 ? 1.f : 0.f);
-    const float* gp = a.gates + (rowc + t) * G + cj;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) p.g[q] = gp[q * H];
-  };
-  wait_vmcnt<0>();                                   // W_hh resident before the ring starts
-  Pre pa, pb;                                        // two-slot ring (see lstm_fwd_kernel)
-  fetch(T - 1, pa);
-  fetch(T - 2, pb);
-
-  // cell update of step s: dgates_t from the prefetched operands
-  auto cell_step = [&](int s, const Pre& pc_) __attribute__((always_inline)) {
-    const int t = t0 + dir * s;
-    {
-      const float dh = pc_.dy + dh_rec, ct = pc_.c, cp = pc_.cp;
-      const float ig = pc_.g[0], fg = pc_.g[1], gg = pc_.g[2], og = pc_.g[3];
-      const float tc = tanh_bf(ct);
-      dc += dh * og * (1.f - tc * tc);
-      const float d0 = dc * gg * ig * (1.f - ig);
-      const float d1 = dc * cp * fg * (1.f - fg);
-      const float d2 = dc * ig * (1.f - gg * gg);
-      const float d3 = dh * tc * og * (1.f - og);
-      dc *= fg;
-      float* dg = a.dgates + (rowc + t) * G + cj;
-      dg[0] = d0;
-      dg[H] = d1;
-      dg[2 * H] = d2;
-      dg[3 * H] = d3;
-    }
-  };
-  // recurrence of step s >= 1: dh_rec for step s-1 = W_hh^T dgates_t
-  auto rec_step = [&](int s, Pre& pc_) __attribute__((always_inline)) {
-    const int t = t0 + dir * s;
-    asm volatile("" ::: "memory");                   // stores before the prefetch
-    fetch(s - 2, pc_);
-    wait_vmcnt<7>();                                 // dgates_t stored; 7 prefetch loads may fly
-    __syncthreads();
-    {
-      const float* grow = a.dgates + ((size_t)l * a.B * T + t) * G + rq * H;
-      static_assert(BS == 2, "warm_kcache2 pulls two rows");
-      warm_kcache2<H * 4 / 64>(grow + (size_t)min(b0, a.B - 1) * T * G, grow + (size_t)min(b0 + 1, a.B - 1) * T * G);
-      f32x2 acc[BS][2];
-#pragma unroll
-      for (int b = 0; b < BS; ++b) acc[b][0] = acc[b][1] = f32x2{0.f, 0.f};
-#pragma unroll
-      for (int b = 0; b < BS; ++b)
-#pragma unroll
-        for (int p0 = 0; p0 < H / 2; p0 += kChunk) {
-          sptr2 gp = scalar_view(grow + (size_t)min(b0 + b, a.B - 1) * T * G + 2 * p0);
-#pragma unroll
-          for (int p = 0; p < kChunk; ++p)
-            acc[b][p & 1] = __builtin_elementwise_fma(w[p0 + p], gp[p], acc[b][p & 1]);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-#pragma unroll
-      for (int b = 0; b < BS; ++b) sp[rq][b][k] = (acc[b][0].x + acc[b][0].y) + (acc[b][1].x + acc[b][1].y);
-    }
-    __syncthreads();
-    dh_rec = (sp[0][cb][cj] + sp[1][cb][cj]) + (sp[2][cb][cj] + sp[3][cb][cj]);
-  };
-  // step s uses slot (T-1-s)&1: pa for T-1, T-3, ...; pb for T-2, T-4, ...
-  int s = T - 1;
-  for (; s >= 2; s -= 2) {
-    cell_step(s, pa);
-    rec_step(s, pa);
-    cell_step(s - 1, pb);
-    rec_step(s - 1, pb);
-  }
-  if (s == 1) {
-    cell_step(1, pa);
-    rec_step(1, pa);
-    cell_step(0, pb);
-  } else {
-    cell_step(0, pa);
-  }
-}
-
 // ---------------------------------------------------------------------------
-// LDS-exchange forms (default): the recurrent operand (h_{t-1} forward,
-// dgates_t backward) never leaves the workgroup, so it goes through LDS:
-// written by the cell update, one barrier, then read by every lane as 16-B
-// broadcast loads (all lanes of a wave read the same address: no bank
-// conflict) straight into the packed FMAs. No global round trip and no wait
-// for the step's stores in the recurrence (they are only for the backward /
-// the weight gradients). The products are summed in the same order as the
-// scalar-operand kernels above (even pairs into acc[0], odd into acc[1]), so
-// the results are bit-identical.
+// LDS exchange: the recurrent operand (h_{t-1} forward, dgates_t backward)
+// never leaves the workgroup, so it goes through LDS: written by the cell
+// update, one barrier, then read by every lane as 16-B broadcast loads (all
+// lanes of a wave read the same address: no bank conflict) straight into the
+// packed FMAs. No global round trip and no wait for the step's stores in the
+// recurrence (they are only for the backward / the weight gradients). Round 2
+// replaced a form that stored the operand and read it back with scalar loads
+// as SGPR operands of v_pk_fma_f32 (fwd / bwd 1060 / 987 us vs 733 / 736 us per
+// launch at FRCRN size, bit-identical: the same products in the same order).
 // ---------------------------------------------------------------------------
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -548,21 +259,10 @@ constexpr int kBS = 2;
 template <int H>
 int launch(bool bwd, const LstmArgs& a, int L, hipStream_t st) {
   dim3 grid((a.B + kBS - 1) / kBS, L);
-  // SEHIP_LSTM_LDS=0: the scalar-load (global round trip) forms; read once.
-  // Isolated at FRCRN size (tools/gpu_lstm_modes.sh): fwd / bwd 1060 / 987 us
-  // (scalar loads) vs 733 / 736 us (LDS)
-  static const bool lds = [] {
-    const char* e = std::getenv("SEHIP_LSTM_LDS");
-    return !(e && e[0] == '0');
-  }();
-  if (bwd && lds)
+  if (bwd)
     hipLaunchKernelGGL((lstm_bwd_lds_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
-  else if (bwd)
-    hipLaunchKernelGGL((lstm_bwd_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
-  else if (lds)
-    hipLaunchKernelGGL((lstm_fwd_lds_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
   else
-    hipLaunchKernelGGL((lstm_fwd_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
+    hipLaunchKernelGGL((lstm_fwd_lds_kernel<H, kBS>), grid, dim3(4 * H), 0, st, a);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

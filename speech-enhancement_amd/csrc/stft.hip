@@ -22,9 +22,6 @@
 #include <algorithm>
 #include <cmath>
 
-#ifndef SEHIP_STFT_PROBE
-#define SEHIP_STFT_PROBE 0   // measurement probes of stft_fwd_ip_kernel (tools/stft_probe.sh); 0 = the kernel
-#endif
 
 namespace {
 
@@ -418,12 +415,7 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_kernel(const StftArgs a) {
 // (tools/stft_micro.py; the XCD-aware block order merges the 32-B row segments
 // of neighbouring blocks in one L2)
 constexpr int kPairsIP = 4;
-// FUSE: the first FFT pass reads its butterfly inputs straight from the signal
-// (each thread gathers the R0 windowed samples j + q N/R0 of its butterfly, skipping
-// the zero padding past win) and writes only its outputs to LDS: one LDS round trip
-// and two barriers fewer per block, the same values and operations (bit-identical
-// up to the sign of exact zeros).
-template <int CN, int P = kPairsIP, bool LP = false, bool FUSE = false>
+template <int CN, int P = kPairsIP, bool LP = false>
 __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a) {
   constexpr int TPB = kThreads;
   constexpr int N = CN;
@@ -434,46 +426,6 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   const int t0 = tb * 2 * P;
   const long long xo = (long long)b * a.L;
   for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
-  if constexpr (FUSE) {
-    constexpr CPlan pl = make_cplan(N);
-    constexpr int R0 = pl.radix[0], nbf0 = N / R0;
-    constexpr int IT0 = (P * nbf0 + TPB - 1) / TPB;
-    float2 v[IT0][kMaxRadix];
-#pragma unroll
-    for (int it = 0; it < IT0; ++it) {
-      const int idx = threadIdx.x + it * TPB;
-      const int pr = idx / nbf0, j = idx - pr * nbf0;
-      const int ta = t0 + 2 * pr, tb2 = ta + 1;
-      const bool live = idx < P * nbf0;
-#pragma unroll
-      for (int q = 0; q < R0; ++q) {
-        const int n = j + q * nbf0;
-        const bool ok = live && n < a.win;
-        const int nn = ok ? n : 0;
-        const float w = ok ? a.window[nn] : 0.f;
-        float ya = 0.f, yb = 0.f;
-        if (ok) {
-          const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
-          const float xb = ldx<LP>(a.x, xo + reflect_index(min(tb2, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
-          ya = ta < a.T ? w * xa : 0.f;
-          yb = tb2 < a.T ? w * xb : 0.f;
-        }
-        v[it][q] = make_float2(ya, yb);
-      }
-    }
-#pragma unroll
-    for (int it = 0; it < IT0; ++it) {
-      const int idx = threadIdx.x + it * TPB;
-      if (idx < P * nbf0) {
-        const int pr = idx / nbf0, j = idx - pr * nbf0;
-        butterfly<R0>(v[it], A + pr * N, j * R0, 1);
-      }
-    }
-    __syncthreads();
-    fft_pass_ip<N, P, 1, R0, TPB>(A, stw);
-    unpack_store<CN, P, LP>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
-    return;
-  }
   // frame gather: all of a thread's loads are issued before any is used
   // (compile-time trip count; branch-free clamped addresses and zero weights),
   // so the block pays one memory latency instead of one per element
@@ -487,12 +439,8 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
     const bool ok = idx < P * N && n < a.win;
     const int nn = ok ? n : 0;
     const float w = ok ? a.window[nn] : 0.f;
-#if SEHIP_STFT_PROBE == 3   // measurement probe: no signal loads
-    const float xa = (float)(ta * a.hop + nn), xb = (float)(tb * a.hop + nn);
-#else
     const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
     const float xb = ldx<LP>(a.x, xo + reflect_index(min(tb, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
-#endif
     ya[it] = ta < a.T ? w * xa : 0.f;
     yb[it] = tb < a.T ? w * xb : 0.f;
   }
@@ -502,12 +450,7 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
     if (idx < P * N) A[idx] = make_float2(ya[it], yb[it]);
   }
   __syncthreads();
-#if SEHIP_STFT_PROBE != 1   // probe 1: no FFT passes
   fft_pass_ip<N, P, 0, 1, TPB>(A, stw);
-#endif
-#if SEHIP_STFT_PROBE == 2   // probe 2: no spectrum stores (a runtime-false branch keeps the FFT alive)
-  if (a.mag_phase != 7) return;
-#endif
   unpack_store<CN, P, LP>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
 }
 
@@ -854,13 +797,9 @@ static bool make_plan(int N, FftPlan& pl) {
 // Frame pairs per block. kPairs (4) keeps a block's LDS at <= 40 KB for
 // nfft <= 640 so four blocks (16 waves) share a CU; larger nfft fall back to
 // what the LDS budget allows.
-#ifndef SEHIP_STFT_IP
-#define SEHIP_STFT_IP 1      // ConvSTFT forward on the in-place FFT kernel
-#endif
-#ifndef SEHIP_STFT_PAIRS
-#define SEHIP_STFT_PAIRS 4
-#endif
-constexpr int kPairs = SEHIP_STFT_PAIRS;
+constexpr int kPairs = 4;
+// the compiled radix plans run the in-place kernels
+static bool ip_plan(int nfft) { return nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256; }
 static int pick_pairs(int N) {
   const int p = kLdsBudget / (2 * N * (int)sizeof(float2));
   return std::max(1, std::min(kPairs, p));   // sums[] holds 2 floats for 32 frames
@@ -905,13 +844,6 @@ extern "C" int se_stft_num_frames(int L, int win, int hop, int nfft, int center)
   return (Lp - win) / hop + 1;
 }
 
-// SEHIP_STFT_FUSE=0 / 1: the in-place ConvSTFT without / with the first FFT pass fused
-// into the signal gather (read per call)
-static bool stft_fuse_on() {
-  const char* e = std::getenv("SEHIP_STFT_FUSE");
-  return e && e[0] == '1';
-}
-
 extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, int win,
                            int hop, int nfft, int center, int mag_phase, const float* window,
                            const float* twiddle, int dtype, void* stream) {
@@ -929,27 +861,12 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
   a.L = L; a.win = win; a.hop = hop; a.T = T; a.pad = pad; a.mag_phase = mag_phase;
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
-  if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
-    // in-place FFT, kPairsIP frame pairs per block (static LDS <= 25 KB at the default)
-    // frame pairs per block: kPairsIP, or SEHIP_STFT_IP_PAIRS = 2 / 4 / 8 / 16 (A/B knob)
-    static const int ip_pairs = [] {
-      const char* e = std::getenv("SEHIP_STFT_IP_PAIRS");
-      const int v = e ? std::atoi(e) : kPairsIP;
-      return (v == 2 || v == 4 || v == 8 || v == 16) ? v : kPairsIP;
-    }();
-    const int P = ip_pairs;
+  if (ip_plan(nfft)) {
+    // in-place FFT, kPairsIP frame pairs per block (static LDS <= 25 KB)
+    const int P = kPairsIP;
     const dim3 grid(se::ceil_div(T, 2 * P), B);
     hipStream_t st = se::as_stream(stream);
-    const bool fuse = stft_fuse_on();
-#define SE_STFT_IP(NF)                                                                              \
-  do {                                                                                              \
-    if (P == 2) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 2, grid, 0, st, a);                     \
-    else if (P == 4 && fuse && a.dt == SE_DTYPE_F32)                                                \
-      hipLaunchKernelGGL((stft_fwd_ip_kernel<NF, 4, false, true>), grid, dim3(kThreads), 0, st, a); \
-    else if (P == 4) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 4, grid, 0, st, a);                \
-    else if (P == 16) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 16, grid, 0, st, a);              \
-    else SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA 8, grid, 0, st, a);                            \
-  } while (0)
+#define SE_STFT_IP(NF) SE_LP_LAUNCH(stft_fwd_ip_kernel<NF SE_COMMA kPairsIP, grid, 0, st, a)
     switch (nfft) {
       case 640: SE_STFT_IP(640); break;
       case 512: SE_STFT_IP(512); break;
@@ -991,24 +908,15 @@ extern "C" int se_istft_fwd(const void* spec, void* out, int B, int T, int win, 
   if (!spec || !out || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
   if (out_len == 0) return SE_OK;
   a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
-  if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
-    // in-place FFT, SEHIP_ISTFT_IP_PAIRS = 4 / 8 frame pairs per block (A/B knob)
-    static const int ip_pairs = [] {
-      const char* e = std::getenv("SEHIP_ISTFT_IP_PAIRS");
-      const int v = e ? std::atoi(e) : kPairsIP;
-      return (v == 4 || v == 8) ? v : kPairsIP;
-    }();
-    const int P = ip_pairs;
+  if (ip_plan(nfft)) {
+    // in-place FFT, kPairsIP frame pairs per block (8 measured slower: 79.9 / 107 us)
+    const int P = kPairsIP;
     a.P = P;
     a.FT = 2 * P - 1 - (win - 1) / hop;
     if (a.FT >= 1) {
       const dim3 grid(se::ceil_div(out_len, a.FT * hop), B);
       hipStream_t st = se::as_stream(stream);
-#define SE_ISTFT_IP(NF)                                                                             \
-  do {                                                                                              \
-    if (P == 8) SE_LP_LAUNCH(istft_fwd_ip_kernel<NF SE_COMMA 8, grid, 0, st, a);                    \
-    else SE_LP_LAUNCH(istft_fwd_ip_kernel<NF SE_COMMA 4, grid, 0, st, a);                           \
-  } while (0)
+#define SE_ISTFT_IP(NF) SE_LP_LAUNCH(istft_fwd_ip_kernel<NF SE_COMMA kPairsIP, grid, 0, st, a)
       switch (nfft) {
         case 640: SE_ISTFT_IP(640); break;
         case 512: SE_ISTFT_IP(512); break;
@@ -1038,21 +946,12 @@ extern "C" int se_istft_bwd(const void* gout, void* gspec, int B, int T, int win
   if (rc) return rc;
   if (!gout || !gspec || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
   a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
-  if (SEHIP_STFT_IP && (nfft == 640 || nfft == 512 || nfft == 400 || nfft == 320 || nfft == 256)) {
-    // in-place FFT, SEHIP_ISTFT_IP_PAIRS = 4 / 8 frame pairs per block (A/B knob)
-    static const int ip_pairs = [] {
-      const char* e = std::getenv("SEHIP_ISTFT_IP_PAIRS");
-      const int v = e ? std::atoi(e) : kPairsIP;
-      return (v == 4 || v == 8) ? v : kPairsIP;
-    }();
-    const int P = ip_pairs;
+  if (ip_plan(nfft)) {
+    // in-place FFT, kPairsIP frame pairs per block (8 measured slower: 79.9 / 107 us)
+    const int P = kPairsIP;
     const dim3 grid(se::ceil_div(T, 2 * P), B);
     hipStream_t st = se::as_stream(stream);
-#define SE_ISTFT_BWD_IP(NF)                                                                         \
-  do {                                                                                              \
-    if (P == 8) SE_LP_LAUNCH(istft_bwd_ip_kernel<NF SE_COMMA 8, grid, 0, st, a);                    \
-    else SE_LP_LAUNCH(istft_bwd_ip_kernel<NF SE_COMMA 4, grid, 0, st, a);                           \
-  } while (0)
+#define SE_ISTFT_BWD_IP(NF) SE_LP_LAUNCH(istft_bwd_ip_kernel<NF SE_COMMA kPairsIP, grid, 0, st, a)
     switch (nfft) {
       case 640: SE_ISTFT_BWD_IP(640); break;
       case 512: SE_ISTFT_BWD_IP(512); break;

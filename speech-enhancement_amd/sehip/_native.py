@@ -38,10 +38,8 @@ class ConvDesc(ctypes.Structure):
         ("x_amax", c_void_p), ("dy_amax", c_void_p),   # SE_MATH_F16X3 scale sources (or NULL)
         ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p),   # CL16 operands (or NULL)
         ("w_amax", c_void_p),   # SE_MATH_F16X3 bound of max |w| (or NULL)
-        ("accumulate_dx", c_int),   # se_conv2d_bwd_data: dx += dL/dx (ABI 3)
         ("dtype", c_int),           # SE_DTYPE_* storage of the conv's tensors (ABI 4)
-        ("data_weights", c_void_p),   # prepared data-grad weight image (or NULL, ABI 5)
-        ("moments", c_void_p)]        # forward: CBN moment rows of y (or NULL, ABI 5)
+        ("data_weights", c_void_p)]   # prepared data-grad weight image (or NULL, ABI 5)
 
 
 class FirstConvDesc(ctypes.Structure):
@@ -62,15 +60,13 @@ class GemmDesc(ctypes.Structure):
 
 
 _P = c_void_p
-ABI_VERSION = 6   # SEHIP_ABI_VERSION (include/sehip.h)
+ABI_VERSION = 7   # SEHIP_ABI_VERSION (include/sehip.h)
 CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
     "se_abi_version": (c_int, []),
     "se_strerror": (c_char_p, [c_int]),
     "se_probe": (c_int, [_P, c_int, _P]),
-    "se_stream_create_cu_subset": (c_int, [c_int, c_int, _PP]),
-    "se_stream_destroy": (c_int, [_P]),
     "se_stft_num_frames": (c_int, [c_int] * 5),
     "se_stft_fwd": (c_int, [_P, _P, _P] + [c_int] * 7 + [_P, _P, c_int, _P]),
     "se_istft_fwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, c_int, _P]),
@@ -87,7 +83,6 @@ _SIGNATURES = {
     "se_resample": (c_int, [_P, c_int, c_int, c_int, c_int, _P, c_int, c_int, _P, c_int, _P]),
     "se_conv2d_workspace_size": (c_size_t, [_P]),
     "se_conv2d_data_weights_size": (c_size_t, [_P]),
-    "se_conv2d_moments_rows": (c_int, [_P]),
     "se_conv2d_prep_data_weights": (c_int, [_P] * 4 + [c_size_t, _P]),
     "se_conv2d_fwd": (c_int, [_P] * 7 + [_P, c_size_t, _P]),
     "se_conv2d_bwd_data": (c_int, [_P] * 5 + [_P, c_size_t, _P]),
@@ -102,10 +97,6 @@ _SIGNATURES = {
                            c_int, _P, c_size_t, _P]),
     "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
                             c_int, _P, c_size_t, _P]),
-    "se_cbn_fwd_moments": (c_int, [_P, c_int, _P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P, c_float, c_float,
-                                   c_int, c_float, _P, _P, _P]),
-    "se_cbn_head_fwd_moments": (c_int, [_P, c_int, _P, _P] + [c_int] * 4 + [_PP, _PP, _P, _P, c_float, c_float,
-                                        c_int, c_float, _P, c_int, c_int, _P]),
     "se_cbn_head_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "se_cbn_first_conv_workspace_size": (c_size_t, [c_int] * 6),
     "se_cbn_bwd_first_conv": (c_int, [_P, _P, _P] + [c_int] * 4 + [_PP, _P, _PP, c_int, c_int, c_float, _P, _P,

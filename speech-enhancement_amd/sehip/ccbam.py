@@ -207,8 +207,6 @@ class _CCBAMFn(torch.autograd.Function):
         grads = {id(p): g for p, g in zip(sp, gs[1:])}
         grads.update({id(p): g for p, g in zip(ch, gc[1:])})
         del ctx.graphs
-        if F.fork_stash(x, dx):   # x is a forked encoder output: the other consumer adds into dx
-            dx = None
         return (dx, None) + tuple(grads.get(id(p)) for p in mod.parameters())
 
 

@@ -380,13 +380,6 @@ def _module_dtype(m: nn.Module, default):
     return default
 
 
-def cbn_reads_conv(norm: nn.Module) -> bool:
-    """Whether a block's norm is a training-mode ComplexBatchNorm2d fed by the
-    block's conv output: the conv then writes the CBN moments in its forward
-    epilogue (functional.emit_moments)."""
-    return isinstance(norm, ComplexBatchNorm2d) and norm.training
-
-
 def norm_act(norm: nn.Module, act: nn.Module, x, fork: bool = False):
     """act(norm(x)) with the activation fused into the CBN kernel when both are
     the kinds the kernel knows; otherwise the two modules are applied in turn.

@@ -59,20 +59,6 @@ def deferred_weight_grads(enabled: bool = True):
             torch.cuda.current_stream(side.device).wait_stream(side)
 
 
-def _new_side_stream(dev):
-    """The deferred weight-grad stream: a plain torch stream, or with
-    SEHIP_WGRAD_CUS=num/den a HIP stream on that fraction of the CUs
-    (se_stream_create_cu_subset), wrapped as a torch ExternalStream."""
-    spec = os.environ.get("SEHIP_WGRAD_CUS")
-    if not spec:
-        return torch.cuda.Stream(dev)
-    num, den = (int(v) for v in spec.split("/"))
-    h = N.c_void_p()
-    with torch.cuda.device(dev):
-        N.check(N.lib().se_stream_create_cu_subset(num, den, N.ctypes.byref(h)), "se_stream_create_cu_subset")
-    return torch.cuda.ExternalStream(h.value, device=dev)
-
-
 def _wgrad_stream(*inputs):
     """Context for a weight-grad launch: a no-op, or (deferred_weight_grads) the
     device's side stream, after it waited for the current stream; the inputs are
@@ -82,7 +68,7 @@ def _wgrad_stream(*inputs):
     dev = inputs[0].device
     side = _DEFER_STREAMS.get(dev)
     if side is None:
-        side = _DEFER_STREAMS[dev] = _new_side_stream(dev)
+        side = _DEFER_STREAMS[dev] = torch.cuda.Stream(dev)
         SIDE_STREAMS.append(side)
     side.wait_stream(torch.cuda.current_stream(dev))
     for t in inputs:
@@ -145,17 +131,12 @@ _MATH_CODES = {"f32": 0, "bf16x3": 1, "bf16x6": 2, "bf16": 3, "f16x3": 4, "f16":
 _STORAGE_MATH = {torch.bfloat16: 3, torch.float16: 5}
 _PASSES = ("fwd", "data", "weight")
 _CONV_MATH = {p: 0 for p in _PASSES}
-# Optional override for the forward passes of transposed convs (the decoder) whose
-# input grid has at least _FWD_DEC[1] rows: key "fwd_dec" of the mode string
-# (None = follow "fwd"); min rows from "fwd_dec_min_h" or SEHIP_FWD_DEC_MIN_H.
-_FWD_DEC: list = [None, 0]
 
 
 def set_conv_math(mode: str, **passes: str) -> None:
     """set_conv_math("bf16x3") sets every pass; keyword overrides per pass
     (fwd=, data=, weight=). A mode string may also be the per-pass form
-    "fwd=bf16x3,data=f32,weight=bf16x3". Optional keys: fwd_dec=<mode> for the
-    forward of transposed convs with at least fwd_dec_min_h input rows."""
+    "fwd=bf16x3,data=f32,weight=bf16x3"."""
     spec = {}
     if "=" in mode:
         for item in mode.split(","):
@@ -164,19 +145,13 @@ def set_conv_math(mode: str, **passes: str) -> None:
     else:
         spec = {p: mode for p in _PASSES}
     spec.update(passes)
-    dec = spec.pop("fwd_dec", None)
-    dec_h = int(spec.pop("fwd_dec_min_h", os.environ.get("SEHIP_FWD_DEC_MIN_H", 0)))
     for k, v in spec.items():
         if k not in _PASSES:
             raise ValueError(f"conv pass must be one of {_PASSES} (got {k!r})")
         if v not in _MATH_CODES:
             raise ValueError(f"conv math must be one of {sorted(_MATH_CODES)} (got {v!r})")
-    if dec is not None and dec not in _MATH_CODES:
-        raise ValueError(f"conv math must be one of {sorted(_MATH_CODES)} (got {dec!r})")
     for k, v in spec.items():
         _CONV_MATH[k] = _MATH_CODES[v]
-    _FWD_DEC[0] = None if dec is None else _MATH_CODES[dec]
-    _FWD_DEC[1] = dec_h
 
 
 # Default: scaled split-fp16 on every pass. It is fp32-class: against fp64, each
@@ -193,9 +168,6 @@ def get_conv_math() -> str:
     """The current mode: one name when every pass agrees, else the per-pass form."""
     names = {v: k for k, v in _MATH_CODES.items()}
     modes = [names[_CONV_MATH[p]] for p in _PASSES]
-    if _FWD_DEC[0] is not None:
-        return ",".join(f"{p}={m}" for p, m in zip(_PASSES, modes)) + \
-            f",fwd_dec={names[_FWD_DEC[0]]},fwd_dec_min_h={_FWD_DEC[1]}"
     if len(set(modes)) == 1:
         return modes[0]
     return ",".join(f"{p}={m}" for p, m in zip(_PASSES, modes))
@@ -240,123 +212,6 @@ def amax_of(t: torch.Tensor) -> torch.Tensor:
     return a
 
 
-# --------------------------------------------------------------------------
-# ComplexBatchNorm moments from the producing conv (se_conv2d_desc.moments, ABI 5).
-# A block whose training-mode CBN reads the conv output directly (FRCRN / DCCRN
-# encoder and decoder blocks, emit_moments) has the conv's split-fp16 forward GEMM
-# write the per-tile moment rows of its output in the epilogue; the CBN forward then
-# runs only its finalize and apply (se_cbn_fwd_moments / se_cbn_head_fwd_moments)
-# instead of its own pass over the tensor. Opt-in (SEHIP_CONV_MOMENTS=1): the moments
-# are exact (tests/test_gpu_conv_moments.py) but the epilogue's LDS rounds cost the GEMM
-# more than the CBN pass they replace: 621.8 / 622.9 vs 628.5 / 627.5 utt/s (same box).
-# --------------------------------------------------------------------------
-_MOM: dict = {}
-_EMIT = [False]
-MOMENT_CALLS = [0, 0]   # [convs that wrote moment rows, CBN forwards that read them] (tests)
-
-
-@contextlib.contextmanager
-def emit_moments(on: bool = True):
-    """Convs run inside write the CBN moment rows of their output where their
-    forward kernel supports it (se_conv2d_moments_rows)."""
-    prev = _EMIT[0]
-    _EMIT[0] = bool(on) and os.environ.get("SEHIP_CONV_MOMENTS", "0") == "1"
-    try:
-        yield
-    finally:
-        _EMIT[0] = prev
-
-
-def _moments_for(d, x):
-    """(uint8 buffer, rows) for the forward pass of d, or None."""
-    if not (_EMIT[0] and x.dtype == torch.float32 and d.complex_weights and 64 < d.out_channels <= 256
-            and _pass_math("fwd", d) == F16X3 and not getattr(d, "exact", False)):
-        return None
-    rows = N.lib().se_conv2d_moments_rows(N.ctypes.byref(d))
-    if rows <= 0:
-        return None
-    return torch.empty(d.out_channels // 2 * rows * 56, dtype=torch.uint8, device=x.device), rows
-
-
-def moments_put(t: torch.Tensor, buf: torch.Tensor, rows: int) -> None:
-    for k in [k for k, e in _MOM.items() if e[2].expired()]:
-        del _MOM[k]
-    _MOM[t.data_ptr()] = (buf, rows, StorageWeakRef(t.untyped_storage()), tuple(t.shape), t._version)
-    MOMENT_CALLS[0] += 1
-
-
-def moments_take(t: torch.Tensor):
-    """The moment rows registered for t (and still describing it), removed from the table."""
-    e = _MOM.pop(t.data_ptr(), None)
-    if e is None or e[2].expired() or e[3] != tuple(t.shape) or e[4] != t._version:
-        return None
-    return e[0], e[1]
-
-
-# --------------------------------------------------------------------------
-# Forked outputs (ComplexBN fork=True: an FRCRN encoder block output feeding the
-# next block and a decoder skip). The skip consumer's backward (CCBAM) runs
-# first, during the decoder's backward; it hands its input gradient over here
-# instead of returning it, and the next encoder conv's data-grad adds its own
-# result into that tensor in the GEMM epilogue (se_conv2d_desc.accumulate_dx).
-# The CBN backward then reads one gradient tensor instead of two in both of its
-# passes. Same fp32 sum (gy + gy2) as se_cbn_bwd2, so bit-identical; if the
-# conv cannot accumulate (or runs first), the CBN backward takes the stashed
-# tensor as its second gradient. Opt-in (SEHIP_FORK_ACC=1): with it the FRCRN
-# gradients are bit-identical and the GPU suite passes, but the step measured
-# 612.8 / 616.5 vs 622.6 / 623.3 utt/s (same box): the epilogue's dependent
-# strided reads of dx cost the GEMM more than the two streaming reads it saves
-# in the CBN passes.
-# --------------------------------------------------------------------------
-_FORK: dict = {}
-FORK_ACC_CALLS = [0]   # data-grads that accumulated into a handed-over gradient (diagnostics)
-
-
-def fork_acc_on() -> bool:
-    return os.environ.get("SEHIP_FORK_ACC", "0") == "1"
-
-
-def fork_register(y: torch.Tensor) -> list:
-    """Entry [storage weakref, shape, stash (g, event) or None] for a forked output."""
-    if len(_FORK) > 64:
-        for k in [k for k, e in _FORK.items() if e[0].expired()]:
-            del _FORK[k]
-    e = [StorageWeakRef(y.untyped_storage()), tuple(y.shape), None]
-    _FORK[y.data_ptr()] = e
-    return e
-
-
-def _fork_entry(t: torch.Tensor):
-    e = _FORK.get(t.data_ptr())
-    if e is None or e[0].expired() or e[1] != tuple(t.shape):
-        return None
-    return e
-
-
-def fork_stash(t: torch.Tensor, g: torch.Tensor) -> bool:
-    """Keep g (the gradient of t from one consumer, made on the current stream) for
-    the other consumer; False if t is not a registered forked output."""
-    e = _fork_entry(t)
-    if e is None or e[2] is not None or not fork_acc_on():
-        return False
-    ev = torch.cuda.Event()
-    ev.record(torch.cuda.current_stream(g.device))
-    e[2] = (g, ev)
-    return True
-
-
-def fork_take(e) -> torch.Tensor | None:
-    """Pop the stashed gradient of entry e, ready for use on the current stream."""
-    if e is None or e[2] is None:
-        return None
-    g, ev = e[2]
-    e[2] = None
-    cur = torch.cuda.current_stream(g.device)
-    cur.wait_event(ev)
-    g.record_stream(cur)
-    return g
-
-
 def new_amax(device) -> torch.Tensor:
     return torch.empty(1, device=device, dtype=torch.float32)
 
@@ -364,11 +219,10 @@ def new_amax(device) -> torch.Tensor:
 def _weight_amax(d, wr, wi):
     """se_conv2d_desc.w_amax for one conv call: one single-workgroup launch in the
     forward, shared by the forward and data-grad GEMMs (which otherwise reduce the
-    weights twice each); None where no split-fp16 gather pass reads it, or with
-    SEHIP_WAMAX=0 (the passes then reduce the weights themselves)."""
+    weights twice each); None where no split-fp16 gather pass reads it."""
     need = ((_pass_math("fwd", d) == F16X3 and d.out_channels > 64)
             or (_pass_math("data", d) == F16X3 and d.in_channels > 64))
-    if not need or os.environ.get("SEHIP_WAMAX", "1") == "0":
+    if not need:
         return None
     a = new_amax(wr.device)
     n = wr.numel()
@@ -396,8 +250,6 @@ def _pass_math(pass_name, d) -> int:
     if fm is not None:   # 16-bit storage: the one-term MFMA of its format on every pass
         return fm
     m = _CONV_MATH[pass_name]
-    if pass_name == "fwd" and _FWD_DEC[0] is not None and d.transposed and d.in_h >= _FWD_DEC[1]:
-        m = _FWD_DEC[0]
     # a data-fed conv (exact=True: a model's first conv, whose input is the raw spectrum
     # and carries the batch's whole level spread) runs exact fp32 where the mode is the
     # per-tensor-scaled f16x3 (DESIGN.md §3.2 "Dynamic range")
@@ -423,10 +275,6 @@ def _gemm_tag(pass_name, d, joined=False):
     n = d.out_channels if pass_name == "fwd" else d.in_channels
     kind = "smalln" if n <= 16 else (names[_pass_math(pass_name, d)] if n > 64 else "f32")
     return f"conv_{pass_name}{j}_{kind}"
-
-
-# SE_MATH codes whose data-grad GEMM (N > 64) supports accumulate_dx: bf16x3, bf16, f16x3
-_ACC_MATHS = frozenset((1, 3, 4))
 
 
 def _with_math(d, pass_name):
@@ -532,18 +380,9 @@ class _Conv2d(torch.autograd.Function):
         wa = _weight_amax(d, wr, wi)
         d.w_amax = N.ptr(wa)
         t0 = _TIMER.begin() if _TIMER else None
-        mb = _moments_for(d, x)
-        while True:
-            d.moments = mb[0].data_ptr() if mb is not None else None
-            rc = lib.se_conv2d_fwd(_with_math(d, "fwd"), x.data_ptr(), wr.data_ptr(), N.ptr(wi),
-                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(x))
-            if rc != SE_E_UNSUPPORTED or mb is None:
-                break
-            mb = None   # no moments epilogue for this shape / mode: the CBN runs its own pass
-        d.moments = None
-        N.check(rc, "se_conv2d_fwd")
-        if mb is not None:
-            moments_put(y, *mb)
+        N.check(lib.se_conv2d_fwd(_with_math(d, "fwd"), x.data_ptr(), wr.data_ptr(), N.ptr(wi), N.ptr(br),
+                                  N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(x)),
+                "se_conv2d_fwd")
         if t0 is not None:   # bytes: x read + y written + the weights, once
             _TIMER.end(_gemm_tag("fwd", d), t0, _conv_flops(d),
                        x.element_size() * (x.numel() + y.numel() + wr.numel() * (2 if wi is not None else 1)))
@@ -562,20 +401,13 @@ class _Conv2d(torch.autograd.Function):
         d.x_amax, d.dy_amax, d.w_amax = N.ptr(ctx.x_amax), N.ptr(ga), N.ptr(ctx.w_amax)
         dx = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0]:
-            # x a forked output whose other consumer already handed its gradient
-            # over (fork_stash): add into it in the GEMM epilogue (split kernels only)
-            acc = None
-            if _pass_math("data", d) in _ACC_MATHS and d.in_channels > 64:
-                acc = fork_take(_fork_entry(x))
-            dx = acc if acc is not None else torch.empty_like(x)
-            FORK_ACC_CALLS[0] += acc is not None
-            d.accumulate_dx = int(acc is not None)
+            dx = torch.empty_like(x)
             d.data_weights = _data_weights_of(ctx, d)
             t0 = _TIMER.begin() if _TIMER else None
             N.check(lib.se_conv2d_bwd_data(_with_math(d, "data"), gy.data_ptr(), wr.data_ptr(), N.ptr(wi),
                                            dx.data_ptr(), ws.data_ptr(), ws.numel(), N.stream_of(gy)),
                     "se_conv2d_bwd_data")
-            d.accumulate_dx, d.data_weights, ctx.data_img = 0, None, None
+            d.data_weights, ctx.data_img = None, None
             if t0 is not None:
                 _TIMER.end(_gemm_tag("data", d), t0, _conv_flops(d),
                            4.0 * (gy.numel() + dx.numel() + wr.numel() * (2 if wi is not None else 1)))
@@ -583,7 +415,7 @@ class _Conv2d(torch.autograd.Function):
             # a conv without an input gradient (a model's first conv) is the last one in
             # the backward: its weight-grad runs on the current stream, beside the side
             # stream's still-queued weight-grads, instead of behind them
-            last = not ctx.needs_input_grad[0] and os.environ.get("SEHIP_LAST_WGRAD_INLINE", "1") != "0"
+            last = not ctx.needs_input_grad[0]
             with contextlib.nullcontext() if last else _wgrad_stream(x, gy, ctx.x_amax, ga):
                 if _DEFER is not None and not last:
                     ws = _workspace(ctx.nbytes, gy.device)
@@ -651,22 +483,12 @@ class _ConvJoined(torch.autograd.Function):
         wa = _weight_amax(d, wr, wi)
         d.w_amax = N.ptr(wa)
         t0 = _TIMER.begin() if _TIMER else None
-        mb = _moments_for(d, x)
-        while True:
-            d.moments = mb[0].data_ptr() if mb is not None else None
-            rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
-                                          wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(),
-                                          ws.numel(), st)
-            if rc == SE_E_UNSUPPORTED:
-                rc = lib.se_conv2d_fwd(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), wr.data_ptr(), wi.data_ptr(),
-                                       N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
-            if rc != SE_E_UNSUPPORTED or mb is None:
-                break
-            mb = None
-        d.moments = None
+        rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
+                                      wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
+        if rc == SE_E_UNSUPPORTED:
+            rc = lib.se_conv2d_fwd(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), wr.data_ptr(), wi.data_ptr(),
+                                   N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
         N.check(rc, "se_conv2d_fwd_joined")
-        if mb is not None:
-            moments_put(y, *mb)
         if t0 is not None:
             _TIMER.end(_gemm_tag("fwd", d, joined=True), t0, _conv_flops(d),
                        4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
@@ -821,48 +643,27 @@ class _ComplexBN(torch.autograd.Function):
         # bound of max |y| for an f16x3 consumer (fp32 storage only)
         ya = new_amax(x.device) if training and dt == 0 else None
         t0 = _TIMER.begin() if _TIMER else None
-        pre = moments_take(x) if training and dt == 0 else None
-        if pre is not None:   # the producing conv wrote the moment rows (emit_moments)
-            N.check(lib.se_cbn_fwd_moments(pre[0].data_ptr(), pre[1], x.data_ptr(), y.data_ptr(), b, c, hw,
-                                           N.ptr_array(params), N.ptr_array(running), N.ptr(nbt), save.data_ptr(),
-                                           float(eps), mom, int(act), float(slope), N.ptr(ya), N.ptr(prelu),
-                                           N.stream_of(x)), "se_cbn_fwd_moments")
-            MOMENT_CALLS[1] += 1
-        else:
-            N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
-                                   N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
-                                   save.data_ptr(), int(training), float(eps), mom, int(act),
-                                   float(slope), N.ptr(ya), N.ptr(prelu), dt, ws.data_ptr(), ws.numel(),
-                                   N.stream_of(x)),
-                    "se_cbn_fwd")
+        N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
+                               N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
+                               save.data_ptr(), int(training), float(eps), mom, int(act),
+                               float(slope), N.ptr(ya), N.ptr(prelu), dt, ws.data_ptr(), ws.numel(),
+                               N.stream_of(x)),
+                "se_cbn_fwd")
         if ya is not None:
             amax_put(y, ya)
-        if t0 is not None:   # 1 read for the moments (training, unless the conv wrote them) + 1 read + 1 write
-            _TIMER.end("cbn_fwd", t0, 0.0,
-                       x.element_size() * x.numel() * (3 if training and pre is None else 2))
+        if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write
+            _TIMER.end("cbn_fwd", t0, 0.0, x.element_size() * x.numel() * (3 if training else 2))
         ctx.save_for_backward(x, save, prelu, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         if fork:   # (y, alias of y): two consumers, two gradients summed inside se_cbn_bwd2
             ctx.set_materialize_grads(False)
-            ctx.fork = fork_register(y) if training and fork_acc_on() else None
             return y, y.view(y.shape)
-        ctx.fork = None
         return y
 
     @staticmethod
     def backward(ctx, gy, gy2=None):
         x, save, prelu, *params = ctx.saved_tensors
         training, act, slope, affine = ctx.cfg
-        if ctx.fork is not None:   # a gradient handed over but not accumulated by a conv
-            g3 = fork_take(ctx.fork)
-            ctx.fork = None
-            if g3 is not None:
-                if gy2 is None:
-                    gy2 = g3
-                elif gy is None:
-                    gy = g3
-                else:
-                    gy2 = gy2 + g3
         if gy is None:
             gy, gy2 = gy2, None
         if gy is None:
@@ -1025,23 +826,13 @@ class _ComplexBNHead(torch.autograd.Function):
         ws = _workspace(lib.se_cbn_head_workspace_size(b, c, h * w), x.device)
         mom = -1.0 if momentum is None else float(momentum)
         t0 = _TIMER.begin() if _TIMER else None
-        pre = moments_take(x) if training else None
-        if pre is not None:   # the producing conv wrote the moment rows (emit_moments)
-            N.check(lib.se_cbn_head_fwd_moments(pre[0].data_ptr(), pre[1], x.data_ptr(), out.data_ptr(), b, c, h, w,
-                                                N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
-                                                save.data_ptr(), float(eps), mom, int(act), float(slope),
-                                                w_head.data_ptr(), w_head.shape[0], w_head.shape[3],
-                                                N.stream_of(x)), "se_cbn_head_fwd_moments")
-            MOMENT_CALLS[1] += 1
-        else:
-            N.check(lib.se_cbn_head_fwd(x.data_ptr(), out.data_ptr(), b, c, h, w,
-                                        N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
-                                        save.data_ptr(), int(training), float(eps), mom, int(act),
-                                        float(slope), w_head.data_ptr(), w_head.shape[0], w_head.shape[3],
-                                        ws.data_ptr(), ws.numel(), N.stream_of(x)), "se_cbn_head_fwd")
-        if t0 is not None:   # (1 read for the moments in training, unless the conv wrote them) + 1 read + write
-            _TIMER.end("cbn_head_fwd", t0, 0.0,
-                       4.0 * (x.numel() * (2 if training and pre is None else 1) + out.numel()))
+        N.check(lib.se_cbn_head_fwd(x.data_ptr(), out.data_ptr(), b, c, h, w,
+                                    N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
+                                    save.data_ptr(), int(training), float(eps), mom, int(act),
+                                    float(slope), w_head.data_ptr(), w_head.shape[0], w_head.shape[3],
+                                    ws.data_ptr(), ws.numel(), N.stream_of(x)), "se_cbn_head_fwd")
+        if t0 is not None:   # (1 read for the moments in training) + 1 read + write
+            _TIMER.end("cbn_head_fwd", t0, 0.0, 4.0 * (x.numel() * (2 if training else 1) + out.numel()))
         ctx.save_for_backward(x, save, w_head, *(params or ()))
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         return out
@@ -1549,7 +1340,7 @@ def _tn_splitk(a, b):
     on S times the workgroups instead of a handful of long-K tiles."""
     R = a.shape[0]
     S = next((s for s in (32, 16, 8, 4, 2) if R // s >= 1024), 1)
-    if S == 1 or os.environ.get("SEHIP_LSTM_SPLITK", "1") == "0":
+    if S == 1:
         return a.t() @ b
     C = R // S
     out = torch.bmm(a[:S * C].view(S, C, -1).transpose(1, 2), b[:S * C].view(S, C, -1)).sum(0)
@@ -1564,7 +1355,7 @@ def _rows_sum(a):
     the S partial rows, in order."""
     L, R, G = a.shape
     S = next((s for s in (32, 16, 8, 4, 2) if R // s >= 1024), 1)
-    if S == 1 or os.environ.get("SEHIP_LSTM_SPLITK", "1") == "0":
+    if S == 1:
         return a.sum(1)
     C = R // S
     out = a[:, :S * C].reshape(L, S, C, G).sum(2).sum(1)

@@ -6,7 +6,7 @@ import torch.nn as nn
 import torch.nn.functional as TF
 
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLinear,
-                          ComplexLSTM, LSTM, cbn_reads_conv, complex_concat, mark_data_fed, norm_act,
+                          ComplexLSTM, LSTM, complex_concat, mark_data_fed, norm_act,
                           real_conv2d)
 from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
@@ -44,8 +44,7 @@ class _Block(nn.Module):
         elif not lp:
             pad = None
         # a conv's causal time pad is folded into its (asymmetric) padding, not materialised
-        with F.emit_moments(cbn_reads_conv(self.norm)):
-            y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
+        y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
         return norm_act(self.norm, self.act, y, fork)
 
     def forward_joined(self, x, skip):
@@ -55,8 +54,7 @@ class _Block(nn.Module):
         if (self.padding[1] or not isinstance(conv, ComplexConvTranspose2d) or x.dtype != torch.float32
                 or skip.dtype != torch.float32 or x.shape[2] != skip.shape[2] or x.shape[1] != skip.shape[1]):
             return None
-        with F.emit_moments(cbn_reads_conv(self.norm)):
-            y = conv.forward_joined(x, skip)
+        y = conv.forward_joined(x, skip)
         return norm_act(self.norm, self.act, y)
 
 

@@ -16,7 +16,7 @@ import torch.nn.functional as TF
 
 from ..ccbam import CCBAM
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLSTM,
-                          cbn_reads_conv, complex_concat, mark_data_fed, norm_act, real_conv2d)
+                          complex_concat, mark_data_fed, norm_act, real_conv2d)
 from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
 
@@ -27,9 +27,7 @@ _SIDE_STREAMS: dict = {}
 def _side_stream(dev):
     s = _SIDE_STREAMS.get(dev)
     if s is None:
-        # SEHIP_CCBAM_PRIO: HIP stream priority of the CCBAM side stream (0 = default,
-        # negative = higher; see sehip.train.train_step)
-        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev, priority=int(os.environ.get("SEHIP_CCBAM_PRIO", "0")))
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
         F.SIDE_STREAMS.append(s)
     return s
 
@@ -65,8 +63,7 @@ class _CausalConvBase(nn.Module):
         elif not lp:
             pad = None
         # the time pad of a plain conv is folded into its (asymmetric) padding
-        with F.emit_moments(cbn_reads_conv(self.norm)):
-            y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
+        y = real_conv2d(conv, x, pad) if plain else conv(x, pad)
         return norm_act(self.norm, self.act, y, fork)
 
     def _first_block(self, x, conv, input_pad, fork):
@@ -98,8 +95,7 @@ class _CausalConvBase(nn.Module):
         if self.padding[1] or not isinstance(conv, (ComplexConv2d, ComplexConvTranspose2d)) \
                 or x.shape[1] != skip.shape[1]:
             return self(F.complex_join(x, skip))
-        with F.emit_moments(cbn_reads_conv(self.norm)):
-            y = conv.forward_joined(x, skip)
+        y = conv.forward_joined(x, skip)
         return norm_act(self.norm, self.act, y)
 
     def forward_joined_head(self, x, skip, head: nn.Conv2d):
@@ -118,8 +114,7 @@ class _CausalConvBase(nn.Module):
                    and head.groups == 1)
         if not fusable:
             return real_conv2d(head, self.forward_joined(x, skip))
-        with F.emit_moments(cbn_reads_conv(self.norm)):
-            y = conv.forward_joined(x, skip)
+        y = conv.forward_joined(x, skip)
         if w.shape[1] != y.shape[1]:
             raise ValueError(f"head takes {w.shape[1]} channels, the block gives {y.shape[1]}")
         n = self.norm
@@ -286,20 +281,15 @@ class FRCRN(nn.Module):
         noisy = spec.view(spec.shape[0], 2, half, spec.shape[-1])[:, :, 1:]   # drop DC (:123-127)
         h, skips = noisy.contiguous(), []
         attended = self.decoder.gate_state(h)
-        # SEHIP_GATE_EARLY=1 starts each gate as soon as its skip exists, beside the encoder's
-        # GEMMs: measured 534 vs 538 utt/s (same box), so by default they start after the
-        # encoder, beside the half-idle LSTM recurrence
-        early = os.environ.get("SEHIP_GATE_EARLY", "0") == "1"
-        for i, layer in enumerate(self.encoder.layers):                # Encoder.forward, with each
-            h, skip = layer(h, fork=True)                              # skip gated on the side stream
-            skips.append(skip)                                         # as soon as it exists
-            if attended is not None and early:
-                self.decoder.attend_skip(attended, skip, i)
-        if attended is not None and not early:                         # all six after the encoder,
-            order = list(enumerate(skips))                             # in the decoder's order (the
-            if os.environ.get("SEHIP_GATE_ORDER", "dec") == "dec":     # smallest, deepest skip first):
-                order.reverse()                                        # the decoder starts right after
-            for i, skip in order:                                      # the LSTM, beside the big gates
+        for layer in self.encoder.layers:                              # Encoder.forward
+            h, skip = layer(h, fork=True)
+            skips.append(skip)
+        # the six gates on the side stream after the encoder (beside the half-idle LSTM
+        # recurrence; starting each beside the encoder's GEMMs measured 534 vs 538 utt/s),
+        # in the decoder's order: the smallest, deepest skip first, so the decoder starts
+        # right after the LSTM, beside the big gates
+        if attended is not None:
+            for i, skip in reversed(list(enumerate(skips))):
                 self.decoder.attend_skip(attended, skip, i)
         b, c, f, t = h.shape                                           # :133-137
         h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2))

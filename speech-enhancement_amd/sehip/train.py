@@ -55,37 +55,8 @@ def _defer_ok(model) -> bool:
         and os.environ.get("SEHIP_OVERLAP", "1") != "0"
 
 
-_MAIN_STREAMS: dict = {}
-
-
-def _main_stream(device):
-    """SEHIP_MAIN_PRIO (e.g. -1): run the step on a stream of that HIP priority, so the
-    command processor dispatches its (critical-path) workgroups ahead of the
-    deferred weight-grad side stream's when CUs free up. None = the current stream."""
-    prio = int(os.environ.get("SEHIP_MAIN_PRIO", "0"))
-    if not prio or device.type != "cuda":
-        return None
-    s = _MAIN_STREAMS.get(device)
-    if s is None:
-        s = _MAIN_STREAMS[device] = torch.cuda.Stream(device, priority=prio)
-    return s
-
-
 def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
     """One optimisation step; returns the (device) loss, no host sync."""
-    hp = _main_stream(noisy.device)
-    if hp is None:
-        return _train_step(model, optimizer, noisy, clean, clip_norm)
-    cur = torch.cuda.current_stream(noisy.device)
-    hp.wait_stream(cur)
-    with torch.cuda.stream(hp):
-        loss = _train_step(model, optimizer, noisy, clean, clip_norm)
-    cur.wait_stream(hp)
-    loss.record_stream(cur)
-    return loss
-
-
-def _train_step(model, optimizer, noisy, clean, clip_norm):
     from . import functional as F
     from .functional import deferred_weight_grads
     _, wav = model(noisy)

@@ -193,25 +193,3 @@ def test_ccbam_and_join_validation_need_no_gpu():
     assert lib.se_complex_join(None, 3, 4, 5, None, 4, 4, 5, None, 1, 0, None) == -2   # odd Cx
     assert lib.se_complex_join(None, 4, 4, 5, None, 4, 4, 5, None, 1, 0, None) == -1   # null pointers
     assert lib.se_complex_join_bwd(None, None, 4, 4, 5, None, 4, 0, 5, 1, 0, None) == -1
-
-
-def test_conv_moments_validation_needs_no_gpu():
-    """se_conv2d_desc.moments (ABI 5): one row per 128-position M-tile of each class;
-    passes without the epilogue return SE_E_UNSUPPORTED before launching anything."""
-    lib = N.lib()
-    d = F.conv_desc((2, 128, 33, 37), 128, (5, 2), (2, 1), (2, 0), (1, 1), (0, 0), False, True)
-    ho, wo = ctypes.c_int(), ctypes.c_int()
-    assert lib.se_conv2d_out_shape(ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo)) == 0
-    assert lib.se_conv2d_moments_rows(ctypes.byref(d)) == -(-2 * ho.value * wo.value // 128)
-    fake = ctypes.c_void_p(256)   # never dereferenced: each call returns before launching
-    big = 1 << 40
-    d.moments = 256
-    d.math = 0   # SE_MATH_F32: no epilogue moments
-    assert lib.se_conv2d_fwd(ctypes.byref(d), fake, fake, fake, None, None, fake, fake, big, None) == -3
-    d.math = 4   # the data-grad pass has none either
-    assert lib.se_conv2d_bwd_data(ctypes.byref(d), fake, fake, fake, fake, fake, big, None) == -3
-    d = F.conv_desc((2, 128, 33, 37), 512, (5, 2), (2, 1), (2, 0), (1, 1), (0, 0), False, True)
-    d.math, d.moments = 4, 256   # N = 512: more than one column tile
-    assert lib.se_conv2d_fwd(ctypes.byref(d), fake, fake, fake, None, None, fake, fake, big, None) == -3
-    assert lib.se_cbn_fwd_moments(None, 4, fake, fake, 2, 128, 100, None, None, None, fake, 1e-5, 0.1, 0, 0.0,
-                                  None, None, None) == -1

@@ -371,29 +371,3 @@ def test_cbn_prelu_fused(dtype, tol, gpu_device):
     assert rel_l2(p.weight.grad.float().cpu().numpy(), po.weight.grad.numpy()) < tol
     for k in ("Wrr", "Wri", "Br"):
         assert rel_l2(getattr(m, k).grad.float().cpu().numpy(), getattr(mo, k).grad.numpy()) < tol, k
-
-
-@pytest.mark.parametrize("cpb", ["2", "4"])
-def test_first_block_channel_blocked_bit_identical(cpb, gpu_device, monkeypatch):
-    """SEHIP_FC_CPB = 2 / 4 (4 is the default: the fused first-block backward over several
-    channels per workgroup, sharing each position's spectrum taps) against the one-channel form:
-    dWr / dWi and every CBN gradient bit for bit (same products, same order)."""
-    from sehip import functional as F
-    from sehip.complex_nn import ComplexBatchNorm2d, ComplexConv2d
-    gen = torch.Generator().manual_seed(33)
-    x = (torch.randn((2, 2, 320, 101), generator=gen) * 0.8).cuda()
-    res = []
-    for v in ("1", cpb):   # SEHIP_FC_CPB=1: the one-channel form
-        monkeypatch.setenv("SEHIP_FC_CPB", v)
-        c = paramfill.fill_(ComplexConv2d(2, 128, (5, 2), stride=(2, 1), bias=False), seed=5).cuda()
-        n = paramfill.fill_(ComplexBatchNorm2d(128), seed=6).cuda().train()
-        y, y2 = F.first_block(x, c.real_conv.weight, c.imag_conv.weight, n.Wrr, n.Wri, n.Wii, n.Br, n.Bi,
-                              (n.RMr, n.RMi, n.RVrr, n.RVri, n.RVii), n.num_batches_tracked, n.eps, n.momentum,
-                              F.ACT_LEAKY, 0.2, kernel=(5, 2), stride=(2, 1), padding=(0, 1), padding_end=(0, 0),
-                              dilation=(1, 1), fork=True)
-        g = torch.randn(y.shape, generator=torch.Generator().manual_seed(3)).cuda()
-        (y * g + y2 * g.flip(-1)).sum().backward()
-        torch.cuda.synchronize()
-        res.append([t.grad.clone() for t in (c.real_conv.weight, c.imag_conv.weight, n.Wrr, n.Wri, n.Wii, n.Br, n.Bi)])
-    for a, b in zip(*res):
-        assert torch.equal(a, b)

@@ -166,31 +166,6 @@ def test_amax_weights_exact(n, off, complex_w):
     ref = wr.abs().max() if wi is None else torch.maximum(wr.abs().max(), wi.abs().max())
     assert out.item() == ref.item()
 
-
-@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", [l for l in LAYERS if l[1] and l[3] == 128])
-def test_merged_phase_forward_vs_fp64(name, tr, cin, cout, shape, stride, gpu_device, monkeypatch):
-    """SEHIP_FWD_MERGE=1 (opt-in): the two stride-phase classes of the transposed-conv
-    forward run as one class over the union of input-row offsets on 256-column tiles.
-    Its output is bit-identical to the default two-class form (measured) and held to
-    the fp32-class bar against fp64."""
-    from sehip import functional as F
-    m, x, gy, ref = _fp64_ref(name, tr, cin, cout, shape, stride)
-    exact = _hip(F, m, x, gy, tr, stride, "f32")
-    monkeypatch.setenv("SEHIP_FWD_MERGE", "1")
-    merged = _hip(F, m, x, gy, tr, stride, "f16x3")
-    monkeypatch.setenv("SEHIP_FWD_MERGE", "0")
-    plain = _hip(F, m, x, gy, tr, stride, "f16x3")
-    r = ref["y"].numpy()
-    e32, em, ep = (rel_l2(t["y"].numpy(), r) for t in (exact, merged, plain))
-    same = torch.equal(merged["y"], plain["y"])
-    print(f"{name} fwd: f32 {e32:.2e}  f16x3 merged {em:.2e}  two-class {ep:.2e}  bit-identical {same}")
-    assert em < 1e-5 and em <= max(F16_VS_F32 * e32, 1e-7), (name, em, e32)
-    # phase 0 keeps its K order and phase 1 only gains exact zero products: same bits
-    assert same
-    for k in ("dx", "dwr", "dwi"):   # the backward passes do not depend on the knob
-        assert torch.equal(merged[k], plain[k]), k
-
-
 CONV16_CASES = LAYERS[:4] + [
     ("n32", False, 32, 64, (2, 32, 65, 37), (2, 1)),     # DCCRN enc1-like: 32 -> 64 channels (128-col tiles)
     ("t64", True, 128, 64, (2, 128, 17, 30), (2, 1)),    # convT 128 -> 64 (DCCRN decoder-like)
@@ -242,22 +217,3 @@ def test_conv_16bit_storage(name, tr, cin, cout, shape, stride, dtype, tol, gpu_
               f"{torch.equal(nat[k], cast[k])}")
         assert torch.equal(nat[k], cast[k]), (name, k)
         assert e < tol, (name, k, e)
-
-
-def test_merged_phase_zero_tap_skip_frcrn(gpu_device, monkeypatch):
-    """The merged classes' zero-tap skip (a phase's waves skip the K-steps of taps it has no
-    weight at) on the FRCRN decoder's joined forward: the model output with SEHIP_FWD_MERGE=1
-    is bit-identical with and without the skip and to the default two-class form."""
-    import paramfill
-    from sehip.models import FRCRN
-    noisy, _ = (torch.from_numpy(t).cuda() for t in paramfill.structured_pair(2, 16000, seed=60))
-    outs = []
-    for merge, skip in (("0", "1"), ("1", "1"), ("1", "0")):
-        monkeypatch.setenv("SEHIP_FWD_MERGE", merge)
-        monkeypatch.setenv("SEHIP_MERGE_SKIP", skip)
-        m = paramfill.fill_(FRCRN(), seed=9).cuda().train()
-        spec, wav = m(noisy)
-        torch.cuda.synchronize()
-        outs.append((spec.detach(), wav.detach()))
-    for o in outs[1:]:
-        assert torch.equal(o[0], outs[0][0]) and torch.equal(o[1], outs[0][1])

@@ -99,7 +99,7 @@ def test_bf16_configs_within_oracle_bf16_drift(i, mode, storage, gpu_device):
         F.set_conv_math(prev)
 
 
-def _dccrn_grads(dev, dtype, perturb=0.0, sehip=False):
+def _dccrn_grads(dev, dtype, perturb=0.0, sehip=False, seed=1234):
     """DCCRN-CL (_2008_00264_dccrn.py:148-212) train-mode forward on a structured
     noisy/clean pair, SI-SNR (losses.py:62-84) on the fp32-cast waveform, backward.
     Every parameter gradient (the conv encoder/decoder with output_padding, the CBN +
@@ -117,7 +117,7 @@ def _dccrn_grads(dev, dtype, perturb=0.0, sehip=False):
     m = paramfill.fill_(m, seed=21).to(dev).to(dtype).train()
     x = torch.from_numpy(noisy).to(dtype)
     if perturb:   # a ~1-ulp relative perturbation of the input (fixed seed)
-        gen = torch.Generator().manual_seed(1234)
+        gen = torch.Generator().manual_seed(seed)
         x = x * (1 + perturb * torch.randn(x.shape, generator=gen, dtype=torch.float64)).to(dtype)
     c = torch.from_numpy(clean).to(dev)
     _, w = m(x.to(dev))
@@ -125,22 +125,63 @@ def _dccrn_grads(dev, dtype, perturb=0.0, sehip=False):
     return {n: p.grad.detach().double().cpu() for n, p in m.named_parameters()}
 
 
+def _dccrn_prelu_abs_sums():
+    """For each one-weight nn.PReLU of DCCRN (_2008_00264_dccrn.py:21,45) the fp64
+    oracle's sum of |dL/dy * z| over z <= 0: the weight gradient is the signed sum of
+    these terms, so its attainable accuracy is u * (this sum) for per-term relative
+    accuracy u, whatever the cancellation (decoder.layers.2's sum cancels 2e4-fold)."""
+    from oracle import models as O, train as OT
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=41)
+    m = paramfill.fill_(O.DCCRN("dccrn-CL", 400, 100, 512), seed=21).double().train()
+    sums = {}
+
+    def hook(name):
+        def f(mod, inp, out):
+            z = inp[0]
+            out.register_hook(lambda g: sums.__setitem__(name + ".weight", (g * z).masked_fill(z > 0, 0).abs().sum().item()))
+        return f
+    for n, mod in m.named_modules():
+        if isinstance(mod, torch.nn.PReLU) and mod.weight.numel() == 1:
+            mod.register_forward_hook(hook(n))
+    c = torch.from_numpy(clean).double()
+    _, w = m(torch.from_numpy(noisy).double())
+    OT.si_snr_loss(OT.pad_or_truncate_wav(w, c), c).backward()
+    return sums
+
+
 @pytest.mark.parametrize("storage", ["fp32", "bf16"])
 def test_dccrn_train_grads_vs_fp64(storage, gpu_device):
     """BASELINE config 3 is DCCRN *training*: its gradients against an fp64 CPU run of the
     oracle, per parameter tensor.
     fp32: the default conv math (f16x3 split MFMA, exact-fp32 first conv), gated like
-    FRCRN's: each tensor within max(3x the fp32 oracle's error, 3x its sensitivity to a
-    2^-22 input perturbation, 1e-4) of fp64, and the median within 3x the fp32 oracle's.
+    FRCRN's: each tensor within max(3x the fp32 oracle's error, 3x its sensitivity, 1e-4)
+    of fp64, and the median within 3x the larger of the two medians. The sensitivity is
+    the largest move of the fp64 model's gradient over three 2^-22 relative perturbations
+    of the input: the gradient itself moves that much under an ulp-scale change, because
+    elements of the CBN + PReLU outputs sit on the PReLU kink (measured on the CPU: median
+    2.6e-5, while one unperturbed fp32 CPU run lands anywhere from 1e-6 to 4e-5 off fp64
+    depending on the machine's summation orders).
     bf16: model.to(torch.bfloat16) with SE_MATH_BF16 (the config's own precision) against
     the oracle's own bf16 CPU backward: each tensor within max(3x the bf16 oracle's error,
     3x its move under a 2^-7 input perturbation) of fp64, all gradients together within 2x
-    the bf16 oracle's error, and the median within 1.5x of its median."""
+    the bf16 oracle's error, and the median within 1.5x of its median.
+    The one-weight PReLU gradients are sums with cancellation (one cancels 2e4-fold, so
+    the fp32 oracle's own error there moves 2.6e-4 ... 1.7e-3 with the CPU's summation
+    order); each may instead be within u * sum |terms| of fp64 (_dccrn_prelu_abs_sums),
+    u = 2^-20 (fp32) / 2^-9 (bf16): the accuracy of the sum from per-term errors of
+    that size."""
     from sehip import functional as F
     sdt = torch.float32 if storage == "fp32" else torch.bfloat16
     g64 = _dccrn_grads("cpu", torch.float64)
     go = _dccrn_grads("cpu", sdt)
-    gp = _dccrn_grads("cpu", sdt, perturb=2.0 ** -22 if storage == "fp32" else 2.0 ** -7)
+    if storage == "fp32":
+        gps = [_dccrn_grads("cpu", torch.float64, perturb=2.0 ** -22, seed=1234 + i) for i in range(3)]
+        sens = {n: max((q[n] - g64[n]).norm().item() for q in gps) for n in g64}
+        sens_all = gps
+    else:
+        gp = _dccrn_grads("cpu", sdt, perturb=2.0 ** -7)
+        sens = {n: (gp[n] - go[n]).norm().item() for n in g64}
+        sens_all = []
     prev = F.get_conv_math()
     if storage == "bf16":
         F.set_conv_math("bf16")
@@ -152,21 +193,30 @@ def test_dccrn_train_grads_vs_fp64(storage, gpu_device):
     rows = []
     for n in g64:
         d = g64[n].norm().item() + 1e-30
-        rows.append(((gh[n] - g64[n]).norm().item() / d, (go[n] - g64[n]).norm().item() / d,
-                     (gp[n] - go[n]).norm().item() / d, n))
+        rows.append(((gh[n] - g64[n]).norm().item() / d, (go[n] - g64[n]).norm().item() / d, sens[n] / d, n))
     floor = 1e-4 if storage == "fp32" else 0.0
-    bad = [r for r in rows if r[0] > max(3 * r[1], 3 * r[2], floor)]
+    u = 2.0 ** -20 if storage == "fp32" else 2.0 ** -9
+    abs_sums = _dccrn_prelu_abs_sums()
+    assert len(abs_sums) == 12
+    cond_ok = lambda r: r[3] in abs_sums and r[0] * g64[r[3]].norm().item() <= u * abs_sums[r[3]]
+    bad = [r for r in rows if r[0] > max(3 * r[1], 3 * r[2], floor) and not cond_ok(r)]
+    for r in rows:
+        if r[3] in abs_sums:
+            print(f"  {r[3]}: hip {r[0]:.2e} oracle {r[1]:.2e}; hip error / sum|terms| "
+                  f"{r[0] * g64[r[3]].norm().item() / abs_sums[r[3]]:.2e}")
     med_h, med_o = np.median([r[0] for r in rows]), np.median([r[1] for r in rows])
+    med_s = np.median([r[2] for r in rows])
     cat = lambda g: torch.cat([g[n].flatten() for n in sorted(g64)])
     b = cat(g64)
     e_h, e_o = ((cat(gh) - b).norm() / b.norm()).item(), ((cat(go) - b).norm() / b.norm()).item()
-    print(f"dccrn {storage}: median per-tensor vs fp64 hip {med_h:.2e} oracle {med_o:.2e}; "
+    e_s = max([((cat(q) - b).norm() / b.norm()).item() for q in sens_all] or [0.0])
+    print(f"dccrn {storage}: median per-tensor vs fp64 hip {med_h:.2e} oracle {med_o:.2e} sensitivity {med_s:.2e}; "
           f"all grads hip {e_h:.2e} oracle {e_o:.2e}; worst hip/oracle ratio "
           f"{max(r[0] / max(r[1], r[2], 1e-30) for r in rows):.2f}")
     assert not bad, sorted(bad, key=lambda r: -r[0])[:5]
     if storage == "fp32":
-        assert med_h < 3 * med_o, (med_h, med_o)
-        assert e_h < 2 * e_o + 1e-6, (e_h, e_o)
+        assert med_h < 3 * max(med_o, med_s), (med_h, med_o, med_s)
+        assert e_h < 2 * max(e_o, e_s), (e_h, e_o, e_s)
     else:
         assert med_h < 1.5 * med_o, (med_h, med_o)
         assert e_h < 2 * e_o, (e_h, e_o)

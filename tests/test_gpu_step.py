@@ -147,38 +147,6 @@ def test_train_step_uses_fused_glue(gpu_device):
     loss = train_step(m2, make_optimizer(m2), x, c)
     assert torch.isfinite(loss)
 
-
-def test_frcrn_fork_gradient_handoff_bit_identical(gpu_device, monkeypatch):
-    """SEHIP_FORK_ACC=1 (opt-in, ABI 3 accumulate_dx): CCBAM's input gradient is handed
-    to the next encoder conv's data-grad, which adds into it in the GEMM epilogue. The
-    FRCRN gradients must equal the default two-tensor form bit for bit (the same fp32
-    add), and the five encoder data-grads must have accumulated."""
-    import paramfill
-    from sehip import functional as F
-    from sehip.losses import SI_SNR_loss
-    from sehip.models import FRCRN
-
-    def grads():
-        m = paramfill.fill_(FRCRN(), seed=9).cuda().train()
-        noisy, clean = (torch.from_numpy(t).cuda() for t in paramfill.structured_pair(2, 16000, seed=60))
-        _, wav = m(noisy)
-        SI_SNR_loss(wav, clean).backward()
-        torch.cuda.synchronize()
-        return {n: p.grad.detach().cpu() for n, p in m.named_parameters()}
-
-    monkeypatch.setenv("SEHIP_FORK_ACC", "0")
-    g0 = grads()
-    monkeypatch.setenv("SEHIP_FORK_ACC", "1")
-    before = F.FORK_ACC_CALLS[0]
-    g1 = grads()
-    # encoder blocks 1-4 accumulate; block 0's fork with the fused first block
-    # (se_cbn_bwd_first_conv) sums its two gradients in the CBN kernels instead
-    first_fused = os.environ.get("SEHIP_FIRST_FUSED", "1") != "0"
-    assert F.FORK_ACC_CALLS[0] - before == (4 if first_fused else 5)
-    bad = [n for n in g0 if not torch.equal(g0[n], g1[n])]
-    assert not bad, bad[:6]
-
-
 def test_clip_grad_norm_error_if_nonfinite(gpu_device):
     """error_if_nonfinite=True: finite gradients clip as usual, a non-finite one raises
     (as torch.nn.utils.clip_grad_norm_)."""

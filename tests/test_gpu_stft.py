@@ -110,24 +110,3 @@ def test_stft_istft_low_precision_storage(cfg, dtype, tol, gpu_device):
     (out * torch.from_numpy(g[f"igout_{tag}"]).cuda().to(dtype)).sum().backward()
     assert s.grad.dtype == dtype
     assert rel_l2(s.grad.float().cpu().numpy(), g[f"igspec_{tag}"]) < 2 * tol
-
-
-@pytest.mark.parametrize("cfg", STFT_CONFIGS[:5] + [(320, 160, 256)])
-@pytest.mark.parametrize("shape", [(64, 64000), (3, 5001)])
-def test_stft_fused_first_pass_bit_identical(cfg, shape, gpu_device, monkeypatch):
-    """SEHIP_STFT_FUSE=1: the first FFT pass gathers its butterfly inputs straight from the
-    signal. Same values and operations as the default in-place kernel: equal outputs (and
-    the golden bar), at the bench shape and a ragged one, for every compiled nfft plan."""
-    from sehip.conv_stft import ConvSTFT
-    win, hop, nfft = cfg
-    if win > nfft:
-        pytest.skip("win > nfft")
-    torch.manual_seed(5)
-    x = torch.randn(*shape, device="cuda") * 0.3
-    st = ConvSTFT(win, hop, nfft).cuda()
-    monkeypatch.setenv("SEHIP_STFT_FUSE", "0")
-    a = st(x)
-    monkeypatch.setenv("SEHIP_STFT_FUSE", "1")
-    b = st(x)
-    torch.cuda.synchronize()
-    assert torch.equal(a, b)
