@@ -147,12 +147,13 @@ typedef struct se_conv2d_desc {
    * apply, se_amax) fill it for free. */
   const float* x_amax;
   const float* dy_amax;
-  /* SE_MATH_F16X3 weight-grad only, optional: the conv input x (for the joined
-   * entry points: s in x_packed, x in x2_packed) and dy in CL16 form
-   * (se_pack_cl16, made with the x_amax / dy_amax bound passed here). When all
-   * the pass reads are given, the weight-grad GEMM stages them by LDS-DMA
-   * instead of gathering and splitting fp32. NULL = gather the fp32 tensor.
-   * The forward / data-grad passes return SE_E_UNSUPPORTED when given one. */
+  /* SE_MATH_F16X3, se_conv2d_bwd_weight_joined only, optional: the joined conv's
+   * inputs in CL16 form (se_pack_cl16 layout, written by their producers:
+   * se_cbn_fwd's y_packed, se_ccbam_apply's out_packed), s in x_packed (made with
+   * the x_amax bound) and x in x2_packed (made with x2_amax). The weight-grad GEMM
+   * then reads its D operand pre-split instead of splitting fp32 in the loop.
+   * Both or neither; dy_packed is reserved (NULL). Any other pass, or a shape
+   * the CL16 kernel does not tile, returns SE_E_UNSUPPORTED before launching. */
   const void* x_packed;
   const void* x2_packed;
   const void* dy_packed;
@@ -177,6 +178,10 @@ typedef struct se_conv2d_desc {
    * launch runs beside nothing, instead of in the backward, where it waits for CU
    * slots behind the side stream's weight-grad GEMMs. NULL = build it in ws. */
   const void* data_weights;
+  /* ABI 7, se_conv2d_bwd_weight_joined with CL16 operands only: the bound x2_packed
+   * (x) was made with; x_amax is then the bound of s alone (x_packed). Each source
+   * keeps its own scale. Required when x2_packed is given, else ignored. */
+  const float* x2_amax;
 } se_conv2d_desc;
 
 /* Bytes of the data-grad weight image of d (0 on an invalid desc). */
@@ -289,6 +294,11 @@ int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float* x, int x_h
  *          parameter applied after the norm (DCCRN, dccrn.py:21,45): LeakyReLU
  *          with the slope read on the device. The backward writes its gradient
  *          to dprelu_w (one element, overwritten).
+ * y_packed: NULL, or (ABI 7; fp32 training with y_amax, (C/2) % 8 == 0) a buffer of
+ *          se_pack_cl16_bytes(B, C, H, W) that also receives y in CL16 form, split
+ *          with the scale of the y_amax bound: the pre-split operand of a consuming
+ *          joined weight-grad (se_conv2d_desc.x2_packed), written in the apply pass
+ *          (SE_E_UNSUPPORTED otherwise, before any launch).
  * dtype  : SE_DTYPE_F32 / BF16 / F16, the storage type of x, y, gy, gy2, dx AND
  *          of params / dparams / running / prelu_w (a model.to(bfloat16) /
  *          .half() module keeps all of them in its dtype). Arithmetic is fp32
@@ -301,7 +311,8 @@ int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
                const void* const* params, void* const* running,
                int64_t* nbt, float* save, int training, float eps,
                float momentum, int act, float slope, float* y_amax,
-               const void* prelu_w, int dtype, void* ws, size_t ws_bytes, void* stream);
+               const void* prelu_w, void* y_packed, int dtype, void* ws, size_t ws_bytes,
+               void* stream);
 
 /* Backward. gy = dL/dy (after the activation), x = forward input. y (the
  * forward output) is NOT read and may be NULL: the activation derivative is
@@ -561,8 +572,11 @@ int se_ccbam_channel_pool(const float* x, float* mean, float* mx, int* amax,
                           int B, int C, int HW, void* stream);
 int se_ccbam_spatial_pool(const float* x, const float* ca, float* pooled,
                           short* idx, int B, int C, int HW, void* stream);
+/* out_packed (ABI 7): NULL, or a se_pack_cl16_bytes(B, C, H, W) buffer that also
+ * receives out in CL16 form, split with the scale of the out_amax bound (the joined
+ * weight-grad's x_packed operand); C % 8 == 0. */
 int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out,
-                   int B, int C, int HW, void* stream);
+                   void* out_packed, const float* out_amax, int B, int C, int HW, void* stream);
 int se_ccbam_bwd_sa(const float* gout, float* dsa, int B, int C, int HW,
                     void* stream);
 /* ABI 6: se_ccbam_bwd_sa with the spatial gate's sigmoid backward fused:

@@ -510,10 +510,14 @@ struct WgradArgs {
   // SE_MATH_F16X3: device max |.| of G (the gathered tensor) and of D (both sources)
   const float* amax_g;
   const float* amax_d;
-  // wgrad_pk_kernel: X / D / D2 are CL16 buffers (cconv_pk.hpp) with these
-  // elements per plane; m_per_split counts output rows; per-tap input offsets
-  long long pk_plane_g, pk_plane_d, pk_plane_d2;
+  // per-tap input offsets (wgrad_ktab)
   int toffh[kMaxTaps], toffw[kMaxTaps];
+  // wgrad_x3_kernel<..., DPK>: the joined D as CL16 s (dpk) and x (dpk2) with
+  // pk_plane_d / pk_plane_d2 elements per plane and x's own bound amax_d2
+  long long pk_plane_d, pk_plane_d2;
+  const void* dpk;
+  const void* dpk2;
+  const float* amax_d2;
   // wgrad_x3_kernel: tile space (k-tiles, n-tiles, m-splits) walked by its 1-D grid
   int vk, vn, vs;
   // wgrad_x3_kernel with ktab == nullptr: entries computed in the kernel from
@@ -1085,6 +1089,7 @@ struct ConvGeom {
   const void* x_packed;   // SE_MATH_F16X3 CL16 operands from the caller (or nullptr)
   const void* x2_packed;
   const void* dy_packed;
+  const float* x2_amax;   // the bound x2_packed was made with (se_conv2d_desc.x2_amax)
   int sd;         // se_conv2d_desc.dtype (SE_DTYPE_*)
   const void* data_w;   // se_conv2d_desc.data_weights (data-grad weight image, or nullptr)
 };
@@ -1104,6 +1109,7 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.x_packed = d->x_packed;
   g.x2_packed = d->x2_packed;
   g.dy_packed = d->dy_packed;
+  g.x2_amax = d->x2_amax;
   g.sd = d->dtype;
   g.data_w = d->data_weights;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16) return SE_E_ARG;
@@ -1697,6 +1703,16 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   const float* zero = zero_page();
   if (!zero) return SE_E_LAUNCH;
   float* amax_slot = (float*)(p + kZeroBytes);   // [0] x (joined: x and s), [1] dy
+  // CL16 operands: the joined D only (s in x_packed, x in x2_packed, each with its own
+  // bound), on the split-fp16 128 x 256 tiles; anything else is refused before any launch
+  const bool dpk = g.x_packed || g.x2_packed || g.dy_packed;
+  if (dpk) {
+    const long long QQs = (long long)w.Qh * w.Qw;
+    const bool ok = jn && g.math == SE_MATH_F16X3 && g.sd == SE_DTYPE_F32 && g.x_packed && g.x2_packed &&
+                    !g.dy_packed && g.x_amax && g.x2_amax && w.Np % 256 == 0 && w.Cg % 128 == 0 &&
+                    jn->jh % 64 == 0 && (long long)g.B * QQs < (1ll << 31);
+    if (!ok) return SE_E_UNSUPPORTED;
+  }
   if (g.math == SE_MATH_F16X3 && (!g.x_amax || !g.dy_amax))   // launch_amax targets below
     (void)hipMemsetAsync(amax_slot, 0, kAmaxBytes, st);
   p = align256(p + kZeroBytes + kAmaxBytes);
@@ -1705,7 +1721,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   int4* ktab = (int4*)p;
 
   const bool x3_path = g.math == SE_MATH_F16X3 && split_ok && w.N > 32 && w.N > kSmallWgradN && w.Np != 32 &&
-                       !(g.x_packed || g.dy_packed) && w.c.taps.n <= kMaxTaps;
+                       w.c.taps.n <= kMaxTaps;
   // ktab only (no weights): reuse prep_class_kernel with ldw = 1 writing into slab[0]
   // would clobber; build it with a one-column pass into a scratch row instead. The
   // split-fp16 weight-grad kernel computes its entries itself (no launch).
@@ -1749,32 +1765,13 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   }
   const bool tu = (w.Cg % 128 == 0) && span_w * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
                   span_w * (long long)w.Np * QQw * 4 < (1ll << 31);
-  // CL16 operands from the caller: G = packed dy (transposed) or x, D = the other
-  const void* pk_g = g.transposed ? g.dy_packed : g.x_packed;
-  const void* pk_d = g.transposed ? g.x_packed : g.dy_packed;
-  const bool packed = f16 && pk_g && pk_d && (!jn || (g.x2_packed && jn->jh % 8 == 0)) &&
-                      w.Cg % 128 == 0 && w.N % 128 == 0 && w.c.taps.n <= kMaxTaps;
-  if (packed) {
-    const int rows = g.B * w.Qh;
-    const int spr = se::ceil_div(w.Qw, 32);
-    const int tiles = (w.c.Kp / 128) * (w.Np / 128);
-    int splits = std::max(1, std::min(1024 / std::max(tiles, 1), rows * spr / 16));
-    splits = std::min(splits, w.splits);   // the slab was sized for w.splits
-    const int rps = se::ceil_div(rows, splits);
-    splits = se::ceil_div(rows, rps);
-    a.X = (const float*)pk_g; a.D = (const float*)pk_d;
-    a.m_per_split = rps;
-    a.pk_plane_g = (long long)g.B * w.Cg * w.Hi * w.Wi;
-    a.pk_plane_d = (long long)g.B * (jn ? 2 * jn->jh : w.N) * w.Qh * w.Qw;
-    if (jn) {
-      a.D2 = (const float*)g.x2_packed;
-      a.pk_plane_d2 = (long long)g.B * 2 * jn->jh * jn->h2 * jn->w2;
-    }
-    for (int t = 0; t < w.c.taps.n; ++t) { a.toffh[t] = w.c.taps.offh[t]; a.toffw[t] = w.c.taps.offw[t]; }
-    dim3 grid(w.c.Kp / 128, w.Np / 128, splits);
-    if (jn) hipLaunchKernelGGL(wgrad_pk_kernel<true>, grid, dim3(kThreads), 0, st, a);
-    else hipLaunchKernelGGL(wgrad_pk_kernel<false>, grid, dim3(kThreads), 0, st, a);
-    w.splits = splits;
+  if (dpk) {   // joined D from CL16: s (x_packed, bound x_amax) and x (x2_packed, bound x2_amax)
+    if (!tu) return SE_E_UNSUPPORTED;
+    a.dpk = g.x_packed; a.dpk2 = g.x2_packed; a.amax_d = g.x_amax; a.amax_d2 = g.x2_amax;
+    a.pk_plane_d = (long long)g.B * 2 * jn->jh * w.Qh * w.Qw;
+    a.pk_plane_d2 = (long long)g.B * 2 * jn->jh * jn->h2 * jn->w2;
+    const dim3 grid = x3_wgrad_grid(a, w, 2);
+    hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2, false, 0, true>), grid, dim3(2 * kThreads), 0, st, a);
   } else if (w.N <= kSmallWgradN) {
     dim3 grid(w.c.Kp / 16, w.splits);
     if (w.Np == 4) hipLaunchKernelGGL(wgrad_smalln_kernel<4>, grid, dim3(kThreads), 0, st, a);

@@ -44,25 +44,10 @@ __device__ __forceinline__ unsigned short bf16_bits(float x) {
 // ---------------------------------------------------------------------------
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-constexpr int kF16Top = 14;
-
-// e with *amax < 2^e (from the fp32 exponent field; 0 and denormals -> -126),
-// clamped so that 2^(kF16Top - e) is a normal float
-__device__ __forceinline__ int amax_exp(const float* amax) {
-  const unsigned bits = __builtin_bit_cast(unsigned, *amax) & 0x7fffffffu;
-  const int e = (int)(bits >> 23) - 126;
-  return e < -100 ? -100 : (e > 100 ? 100 : e);
-}
-__device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }
-
-// (x0, x1) * s -> packed fp16 hi pair and lo pair (element 0 in the low half);
-// v_cvt_pk_f16_f32 rounds to nearest even, s * x - hi is exact in fp32
-__device__ __forceinline__ void split_f16x2(float x0, float x1, float s, unsigned& hi, unsigned& lo) {
-  const f32x2 v = (f32x2){x0, x1} * s;
-  const f16x2 h = __builtin_convertvector(v, f16x2);
-  hi = __builtin_bit_cast(unsigned, h);
-  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2));
-}
+using se::kF16Top;
+using se::amax_exp;
+using se::pow2f;
+using se::split_f16x2;
 
 // one 32x32x16 MFMA on a pair of 16-B operand fragments: fp16 or bf16 elements
 template <bool F16>
@@ -534,9 +519,18 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // m-split and its order of positions, so the slabs are bit-identical.
 // KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
 // SD: storage type of X / D (as gather_x3_kernel; 16-bit with the one-term MFMA)
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0>
+// DPK (joined D, split-fp16, NB = 2): D is read pre-split, from the CL16 forms of s
+// (a.dpk) and x (a.dpk2) that their producers wrote (the CBN / CCBAM apply passes):
+// no D split in the loop, and a thread stages its D chunks with 16-B loads, a
+// wave's 64 lanes covering the 256-B channel rows of two positions (x_re, s_re,
+// x_im, s_im: four 128-B segments each). Each source carries its own scale
+// (a.amax_d for s, a.amax_d2 for x), undone per output column block in the slab
+// write; with equal bounds the slabs are bit-identical to the fp32-D form.
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0,
+          bool DPK = false>
 __global__ void __launch_bounds__(kThreads * NB, 2)
 wgrad_x3_kernel(const WgradArgs a) {
+  static_assert(!DPK || (DJ && F16 && TERMS == 3 && NB == 2 && SD == 0), "CL16 D: the joined split-fp16 8-wave tile");
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(SD == 0 || (TERMS == 1 && !DJ), "16-bit storage: one-term, no join");
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
@@ -587,6 +581,10 @@ wgrad_x3_kernel(const WgradArgs a) {
     sg = pow2f(kF16Top - eg);
     sd = pow2f(kF16Top - ed);
     ush = eg + ed - 2 * kF16Top;
+    if constexpr (DPK) {   // this wave's 64 output columns lie in one join chunk (djh % 64 == 0)
+      const bool wx = (((n0 + wnn * TN) / a.djh) & 1) == 0;
+      if (wx) ush = eg + amax_exp(a.amax_d2) - 2 * kF16Top;
+    }
   }
 
   int cb, cqh, cqw;
@@ -597,8 +595,23 @@ wgrad_x3_kernel(const WgradArgs a) {
     cqh = r / a.Qw;
     cqw = r - cqh * a.Qw;
   }
-  struct Stage { typename StageT<SD>::T rg[RJG], rd[RJ]; };   // 16-bit storage: raw bits
+  // DPK: a thread's D chunks are chunk dch (8 joined rows) of positions dpa and dpa + 16,
+  // both planes (4 x 16 B); the position cursors advance by BMR like the lane's own
+  constexpr int RJD = DPK ? 1 : RJ;
+  struct Stage { typename StageT<SD>::T rg[RJG], rd[RJD]; u32x4 dq[DPK ? 4 : 1]; };   // 16-bit storage: raw bits
   Stage st0, st1;
+  const int dch = tid & 31, dpa = tid >> 5;
+  int pcb[2] = {0, 0}, pqh[2] = {0, 0}, pqw[2] = {0, 0};
+  if constexpr (DPK) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const long long mm = mbeg + dpa + 16 * i;
+      pcb[i] = (int)(mm / QQ);
+      const int r = (int)(mm - pcb[i] * QQ);
+      pqh[i] = r / a.Qw;
+      pqw[i] = r - pqh[i] * a.Qw;
+    }
+  }
   auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
     const unsigned long long v = (unsigned long long)p;
     const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
@@ -619,25 +632,39 @@ wgrad_x3_kernel(const WgradArgs a) {
   const int4 tap_e = sK[0];                         // TU: one tap per 128-row k-tile
   const int cbase = k0 % a.Cg;
   const bool one_wrap = a.Qw >= BMR;
-  auto advance = [&]() __attribute__((always_inline)) {
+  auto advance1 = [&](int& b_, int& h_, int& w_) __attribute__((always_inline)) {
     if (one_wrap) {
-      cqw += BMR;
-      const bool w1 = cqw >= a.Qw;
-      cqw -= w1 ? a.Qw : 0;
-      cqh += w1 ? 1 : 0;
-      const bool w2 = cqh >= a.Qh;
-      cqh = w2 ? 0 : cqh;
-      cb += w2 ? 1 : 0;
+      w_ += BMR;
+      const bool w1 = w_ >= a.Qw;
+      w_ -= w1 ? a.Qw : 0;
+      h_ += w1 ? 1 : 0;
+      const bool w2 = h_ >= a.Qh;
+      h_ = w2 ? 0 : h_;
+      b_ += w2 ? 1 : 0;
     } else {
-      const int t = cqw + BMR;
+      const int t = w_ + BMR;
       const int dq = t / a.Qw;
-      cqw = t - dq * a.Qw;
-      const int u = cqh + dq;
+      w_ = t - dq * a.Qw;
+      const int u = h_ + dq;
       const int db = u / a.Qh;
-      cqh = u - db * a.Qh;
-      cb += db;
+      h_ = u - db * a.Qh;
+      b_ += db;
     }
   };
+  auto advance = [&]() __attribute__((always_inline)) {
+    advance1(cb, cqh, cqw);
+    if constexpr (DPK) {
+      advance1(pcb[0], pqh[0], pqw[0]);
+      advance1(pcb[1], pqh[1], pqw[1]);
+    }
+  };
+  // DPK: joined chunk dch -> its source (x or s), the channel in it, and the row image
+  const int djc = 8 * dch, djq = DPK ? djc / max(a.djh, 1) : 0;
+  const bool d_from_x = (djq & 1) == 0;
+  const int d_c = (djq >> 1) * a.djh + (djc - djq * a.djh);
+  const _Float16* d_src = reinterpret_cast<const _Float16*>(d_from_x ? a.dpk2 : a.dpk);
+  const long long d_plane = d_from_x ? a.pk_plane_d2 : a.pk_plane_d;
+  const _Float16* d_zero = reinterpret_cast<const _Float16*>(a.zero);
   auto load_step = [&](Stage& S, int mstep) __attribute__((always_inline)) {
     const bool mv = mstep + ml < mend;
     const int rb = cb - bfirst;
@@ -693,10 +720,22 @@ wgrad_x3_kernel(const WgradArgs a) {
         else S.rg[j] = ld_s<0>(src, ok ? xb + e.x : 0);
       }
     }
+    if constexpr (DPK) {
 #pragma unroll
-    for (int j = 0; j < RJ; ++j) {
-      if constexpr (SD != 0) S.rd[j] = bload_raw16(rdr, vd, (srow + j) * ds);
-      else S.rd[j] = bload<0>(rdr, vd, (srow + j) * ds);
+      for (int i = 0; i < 2; ++i) {
+        const bool ok = (mstep + dpa + 16 * i < mend) & (!d_from_x | (pqh[i] < a.DH2));   // F.pad rows of x: 0
+        const long long pos = d_from_x ? ((long long)pcb[i] * a.DH2 + pqh[i]) * a.DW2 + pqw[i]
+                                       : ((long long)pcb[i] * a.Qh + pqh[i]) * a.Qw + pqw[i];
+        const _Float16* p = ok ? d_src + pos * (2 * a.djh) + d_c : d_zero;
+        S.dq[i] = *reinterpret_cast<const u32x4*>(p);
+        S.dq[2 + i] = *reinterpret_cast<const u32x4*>(ok ? p + d_plane : d_zero);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RJ; ++j) {
+        if constexpr (SD != 0) S.rd[j] = bload_raw16(rdr, vd, (srow + j) * ds);
+        else S.rd[j] = bload<0>(rdr, vd, (srow + j) * ds);
+      }
     }
     advance();
   };
@@ -715,13 +754,13 @@ wgrad_x3_kernel(const WgradArgs a) {
           else split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
           GH[e] = h; GL[e] = l;
         }
-        if (q < RJ / 8) {
+        if (!DPK && q < RJ / 8) {
           if constexpr (SD != 0) h = S.rd[8 * q + 2 * e] | (S.rd[8 * q + 2 * e + 1] << 16);
           else split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
           DH[e] = h; DL[e] = l;
         }
       }
-      if (q < RJ / 8) {
+      if (!DPK && q < RJ / 8) {
         const int offd = wx3_off(ml, (rbase & 127) / 8 + q);
         *reinterpret_cast<u32x4*>(dbase + offd) = DH;
         if constexpr (PL == 2) *reinterpret_cast<u32x4*>(dbase + PLANE + offd) = DL;
@@ -730,6 +769,15 @@ wgrad_x3_kernel(const WgradArgs a) {
         const int offg = wx3_off(ml, (rbase_g & 127) / 8 + q);
         *reinterpret_cast<u32x4*>(gbase + offg) = GH;
         if constexpr (PL == 2) *reinterpret_cast<u32x4*>(gbase + PLANE + offg) = GL;
+      }
+    }
+    if constexpr (DPK) {   // joined row block dch >> 4, chunk dch & 15 of positions dpa, dpa + 16
+      unsigned char* db = base + (DPL + 2 * (dch >> 4)) * PLANE;
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int off = wx3_off(dpa + 16 * i, dch & 15);
+        *reinterpret_cast<u32x4*>(db + off) = S.dq[i];
+        *reinterpret_cast<u32x4*>(db + PLANE + off) = S.dq[2 + i];
       }
     }
   };

@@ -37,6 +37,30 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
+// SE_MATH_F16X3 operand scaling (the conv GEMMs, and the producers that write their
+// operands pre-split in CL16 form): a tensor with max |x| <= *amax < 2^e is
+// multiplied by s = 2^(kF16Top - e), so every scaled value is below 2^14 (fp16 max
+// 65504), then split as hi = fp16(x s), lo = fp16(x s - hi) (x s - hi is exact).
+constexpr int kF16Top = 14;
+// e with *amax < 2^e (from the fp32 exponent field; 0 and denormals -> -126),
+// clamped so that 2^(kF16Top - e) is a normal float
+__device__ __forceinline__ int amax_exp(const float* amax) {
+  const unsigned bits = __builtin_bit_cast(unsigned, *amax) & 0x7fffffffu;
+  const int e = (int)(bits >> 23) - 126;
+  return e < -100 ? -100 : (e > 100 ? 100 : e);
+}
+__device__ __forceinline__ float pow2f(int e) { return __builtin_bit_cast(float, (unsigned)(127 + e) << 23); }
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
+// (x0, x1) * s -> packed fp16 hi pair and lo pair (element 0 in the low half);
+// v_cvt_pk_f16_f32 rounds to nearest even
+__device__ __forceinline__ void split_f16x2(float x0, float x1, float s, unsigned& hi, unsigned& lo) {
+  const f32x2v v = (f32x2v){x0, x1} * s;
+  const f16x2v h = __builtin_convertvector(v, f16x2v);
+  hi = __builtin_bit_cast(unsigned, h);
+  lo = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(h, f32x2v), f16x2v));
+}
+
 static inline hipStream_t as_stream(void* s) { return reinterpret_cast<hipStream_t>(s); }
 
 static inline int ceil_div(long long a, long long b) { return (int)((a + b - 1) / b); }

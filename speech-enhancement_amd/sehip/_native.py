@@ -39,7 +39,8 @@ class ConvDesc(ctypes.Structure):
         ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p),   # CL16 operands (or NULL)
         ("w_amax", c_void_p),   # SE_MATH_F16X3 bound of max |w| (or NULL)
         ("dtype", c_int),           # SE_DTYPE_* storage of the conv's tensors (ABI 4)
-        ("data_weights", c_void_p)]   # prepared data-grad weight image (or NULL, ABI 5)
+        ("data_weights", c_void_p),   # prepared data-grad weight image (or NULL, ABI 5)
+        ("x2_amax", c_void_p)]        # joined CL16 operands: the bound of x (x2_packed) (ABI 7)
 
 
 class FirstConvDesc(ctypes.Structure):
@@ -92,7 +93,7 @@ _SIGNATURES = {
     "se_conv2d_bwd_weight_joined": (c_int, [_P, _P, c_int, c_int] + [_P] * 6 + [_P, c_size_t, _P]),
     "se_cbn_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P, c_int, c_float, c_float, c_int,
-                           c_float, _P, _P, c_int, _P, c_size_t, _P]),
+                           c_float, _P, _P, _P, c_int, _P, c_size_t, _P]),
     "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
                            c_int, _P, c_size_t, _P]),
     "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
@@ -135,7 +136,7 @@ _SIGNATURES = {
     "se_ccbam_workspace_size": (c_size_t, [c_int] * 3),
     "se_ccbam_channel_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
     "se_ccbam_spatial_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
-    "se_ccbam_apply": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
+    "se_ccbam_apply": (c_int, [_P] * 6 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_sa": (c_int, [_P] * 2 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_sa_sigmoid": (c_int, [_P] * 3 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_dca": (c_int, [_P] * 5 + [c_int] * 3 + [_P, c_size_t, _P]),
