@@ -23,8 +23,6 @@ def dump(path, batch=4, seconds=1):
     SI_SNR_loss(wav, clean).backward()
     torch.cuda.synchronize()
     torch.save({n: p.grad.detach().cpu() for n, p in m.named_parameters()}, path)
-    from sehip import functional as F
-    print(f"data-grads accumulated into a handed-over gradient: {F.FORK_ACC_CALLS[0]}")
 
 
 def cmp(a, b):

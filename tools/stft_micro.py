@@ -1,7 +1,7 @@
 """ConvSTFT / ConviSTFT fwd+bwd at the FRCRN bench shape (B=64, 4 s, 320/160/640):
 per-launch time over a burst of back-to-back launches and GB/s of the algorithmic
-bytes (wav read once + spectrum written once). SEHIP_STFT_IP_PAIRS picks the
-in-place kernel's frame pairs per block (A/B)."""
+bytes (wav read once + spectrum written once). Optional argv[1]: run only the
+named op (stft_fwd / istft_fwd / istft_bwd), e.g. for a PMC pass."""
 import os, sys
 import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "speech-enhancement_amd"))
@@ -19,8 +19,11 @@ y = ist(sr)
 gy = torch.randn_like(y)
 # istft_bwd: autograd.grad (no .grad accumulation) runs se_istft_bwd alone
 with torch.no_grad():
+    only = sys.argv[1] if len(sys.argv) > 1 else None
     for name, f in (("stft_fwd", lambda: st(x)), ("istft_fwd", lambda: ist(spec)),
                     ("istft_bwd", lambda: torch.autograd.grad(y, sr, gy, retain_graph=True))):
+        if only and name != only:
+            continue
         for _ in range(5):
             f()
         torch.cuda.synchronize()
@@ -31,4 +34,4 @@ with torch.no_grad():
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / 50
-        print(f"P={os.environ.get('SEHIP_STFT_IP_PAIRS', '4')} {name:9s} {ms * 1e3:7.1f} us  {nbytes / ms / 1e6:7.1f} GB/s", flush=True)
+        print(f"{name:9s} {ms * 1e3:7.1f} us  {nbytes / ms / 1e6:7.1f} GB/s", flush=True)
