@@ -227,9 +227,10 @@ CL16_CALLS = [0, 0]   # [copies written, weight-grads that read them] (tests)
 
 def cl16_wanted(x: torch.Tensor) -> bool:
     """Whether a producer should write the CL16 copy of its fp32 output x: a split-fp16
-    weight-grad will read it (gradients enabled, weight pass in f16x3)."""
+    weight-grad will read it (gradients enabled, weight pass in f16x3). SEHIP_CL16=0
+    turns the copies off (the weight-grads then split fp32 in the loop; A/B and tests)."""
     return (x.is_cuda and x.dtype == torch.float32 and torch.is_grad_enabled()
-            and _CONV_MATH["weight"] == F16X3)
+            and _CONV_MATH["weight"] == F16X3 and os.environ.get("SEHIP_CL16", "1") != "0")
 
 
 def new_cl16(x: torch.Tensor) -> torch.Tensor:

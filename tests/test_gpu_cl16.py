@@ -213,3 +213,28 @@ def test_frcrn_train_step_reads_cl16(gpu_device):
     torch.cuda.synchronize()
     assert F.CL16_CALLS[1] - r0 == 5
     assert all(torch.isfinite(p.grad).all() for p in m.parameters())
+
+
+def test_frcrn_train_step_cl16_matches_fp32_operands(gpu_device, monkeypatch):
+    """SEHIP_CL16=0 (the weight-grads split their fp32 D operand in the loop) vs the
+    default CL16 copies: identical forward outputs and data gradients (the copies do not
+    touch them); the joined weight gradients differ only by the per-source scale of x and
+    s (each split against its own bound instead of the joint one), within 1e-6."""
+    import paramfill
+    from sehip import models as M
+    from sehip.losses import SI_SNR_loss, pad_or_truncate_wav
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=8)
+    res = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("SEHIP_CL16", v)
+        m = paramfill.fill_(M.FRCRN(), seed=9).cuda().train()
+        _, wav = m(torch.from_numpy(noisy).cuda())
+        c = torch.from_numpy(clean).cuda()
+        SI_SNR_loss(pad_or_truncate_wav(wav, c), c).backward()
+        torch.cuda.synchronize()
+        res.append((wav.detach(), {n: p.grad.detach() for n, p in m.named_parameters()}))
+    assert torch.equal(res[0][0], res[1][0])
+    for n, g0 in res[0][1].items():
+        g1 = res[1][1][n]
+        e = ((g1 - g0).norm() / (g0.norm() + 1e-30)).item()
+        assert e < 1e-6 or torch.equal(g0, g1), (n, e)
