@@ -1064,7 +1064,7 @@ struct ClassPlan {
 
 static inline int round_up(int a, int b) { return (a + b - 1) / b * b; }
 
-static void finish_plan(ClassPlan& c, int Cg) {
+static void finish_plan(ClassPlan& c, int Cg, int kstep = kBK) {
   c.taps.n = c.h.ntaps * c.w.ntaps;
   int t = 0;
   for (int a = 0; a < c.h.ntaps; ++a)
@@ -1073,7 +1073,7 @@ static void finish_plan(ClassPlan& c, int Cg) {
       c.taps.offh[t] = c.h.off[a]; c.taps.offw[t] = c.w.off[b];
     }
   c.K = c.taps.n * Cg;
-  c.Kp = round_up(std::max(c.K, 1), kBK);
+  c.Kp = round_up(std::max(c.K, 1), kstep);
 }
 
 enum Pass { kFwd = 0, kData = 1 };
@@ -1133,6 +1133,12 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   return SE_OK;
 }
 
+// One-term bf16 (SE_MATH_BF16, the low-precision configs' arithmetic) runs the
+// 128-column MFMA tiles down to N = 17: even with 2-4x zero columns a bf16 MFMA tile
+// beats the fp32-MFMA tiles (1/16 of the bf16 rate) that the fp32-class modes keep
+// for N <= 64 (DCCRN / DCUNet's 32- and 64-channel layers).
+static inline bool bf16_tiles(int N, int math) { return (math == SE_MATH_BF16 || math == SE_MATH_F16) && N > 16; }
+
 // Classes of a gather pass. kFwd: conv -> strided, convT -> phase.
 // kData: conv -> phase (scatter back), convT -> strided.
 static std::vector<ClassPlan> plan_pass(const ConvGeom& g, Pass pass) {
@@ -1140,11 +1146,13 @@ static std::vector<ClassPlan> plan_pass(const ConvGeom& g, Pass pass) {
   const bool phase = (pass == kFwd) ? g.transposed : !g.transposed;
   const int Lh = (pass == kFwd) ? g.Ho : g.Hi, Lw = (pass == kFwd) ? g.Wo : g.Wi;
   const int Cg = (pass == kFwd) ? g.Ci : g.Co;
+  // the one-term MFMA tiles stage 64 k per round (gather_x3_kernel<., 1>)
+  const int kstep = bf16_tiles((pass == kFwd) ? g.Co : g.Ci, g.math) ? kX3OneTermHalves * kBK : kBK;
   if (!phase) {
     ClassPlan c{};
     c.h = strided_dim(Lh, g.kh, g.sh, g.ph, g.dh);
     c.w = strided_dim(Lw, g.kw, g.sw, g.pw, g.dw);
-    finish_plan(c, Cg);
+    finish_plan(c, Cg, kstep);
     out.push_back(c);
     return out;
   }
@@ -1154,17 +1162,12 @@ static std::vector<ClassPlan> plan_pass(const ConvGeom& g, Pass pass) {
       c.h = phase_dim(Lh, g.kh, g.sh, g.ph, g.dh, p);
       c.w = phase_dim(Lw, g.kw, g.sw, g.pw, g.dw, q);
       if (c.h.Q == 0 || c.w.Q == 0) continue;
-      finish_plan(c, Cg);
+      finish_plan(c, Cg, kstep);
       out.push_back(c);
     }
   return out;
 }
 
-// One-term bf16 (SE_MATH_BF16, the low-precision configs' arithmetic) runs the
-// 128-column MFMA tiles down to N = 17: even with 2-4x zero columns a bf16 MFMA tile
-// beats the fp32-MFMA tiles (1/16 of the bf16 rate) that the fp32-class modes keep
-// for N <= 64 (DCCRN / DCUNet's 32- and 64-channel layers).
-static inline bool bf16_tiles(int N, int math) { return (math == SE_MATH_BF16 || math == SE_MATH_F16) && N > 16; }
 
 static inline int ldw_for(int N, int math = SE_MATH_F32) {
   if (N <= 16) return N <= 4 ? 4 : (N <= 8 ? 8 : 16);  // = the small-N kernel's NOUT

@@ -111,6 +111,12 @@ __device__ __forceinline__ int x3_swz(int row) {
 __device__ __forceinline__ int x3_chunk(int row, int c) { return c ^ x3_swz(row); }
 
 constexpr int kX3BN = 128, kX3BM = 128;
+// 32-k halves per staging round of the one-term gather tiles (SE_X3_HALVES=1: the
+// round-3 32-k rounds, for A/B variant builds)
+#ifndef SE_X3_HALVES
+#define SE_X3_HALVES 2
+#endif
+constexpr int kX3OneTermHalves = SE_X3_HALVES;
 
 // K order of the split GEMMs' weight image / ktab. kblk = 0: tap-major,
 // k = tap * Cg + c. kblk = 32 (Cg % 32 == 0): channel-block-major, k =
@@ -219,8 +225,12 @@ gather_x3_kernel(const GatherArgs a) {
   constexpr int PL = TERMS == 1 ? 1 : 2;          // operand planes staged / read
   constexpr int THR = kThreads * NW;
   constexpr int BN = kX3BN * NW, BM = kX3BM, WM = 2, TN = 64, TM = 64, RN = 2, RM = 2;
-  constexpr int AJ = 16 / NW;                     // gathered k per thread per step
+  constexpr int AJ = 16 / NW;                     // gathered k per thread per 32-k half
   constexpr int CPT = AJ / 8;                     // 16-B chunks per plane per thread
+  // 32-k halves per staging round: one term stages two (BK = 64; the lo-plane LDS
+  // slots hold the second half), so a barrier feeds 16 MFMAs per wave, not 8
+  constexpr int KH = TERMS == 1 ? kX3OneTermHalves : 1;
+  constexpr int BKS = kBK * KH;
   __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * BM * 4];
   __shared__ __attribute__((aligned(16))) u32x4 sW[2][2 * BN * 4];   // [t][plane][128 rows][4]
 
@@ -253,7 +263,7 @@ gather_x3_kernel(const GatherArgs a) {
     sa = pow2f(kF16Top - ea);
     ush = ea + amax_exp(a.amax_w) - 2 * kF16Top;
   }
-  struct Stage { typename StageT<SD>::T ra[AJ]; u32x4 rw[4]; };   // 16-bit storage: raw bits
+  struct Stage { typename StageT<SD>::T ra[AJ * KH]; u32x4 rw[2 * PL * KH]; };   // 16-bit storage: raw bits
   Stage s0, s1;
   auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
     const unsigned long long v = (unsigned long long)p;
@@ -283,66 +293,74 @@ gather_x3_kernel(const GatherArgs a) {
     }
   }
   auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
-    if constexpr (TU) {
-      const int4 e0 = a.ktab[k0];                 // the step's tap and first channel (uniform)
-      int c0 = e0.w;
-      const int hi = hb + e0.y, wi = wb + e0.z;
-      bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-      int vo = xoff + (e0.y * a.Wi + e0.z) * ES, cs = (int)(HiWi * ES);
-      __amdgpu_buffer_rsrc_t r = rx;
-      if constexpr (JM == 1) {                    // a K-step lies in one join chunk
-        const int q = c0 / a.jh;
-        const bool from_x = (q & 1) == 0;         // chunks [x_re, s_re, x_im, s_im]
-        c0 = (q >> 1) * a.jh + (c0 - q * a.jh);
-        ok &= !from_x | (hi < a.H2);              // F.pad rows of x read 0
-        vo = from_x ? xoff2 + (e0.y * a.W2 + e0.z) * 4 : vo;
-        cs = from_x ? (int)(H2W2 * 4) : cs;
-        r = from_x ? rx2 : rx;
-      }
-      vo = ok ? vo : (int)0x80000000;
-      c0 += AJ * akr;
 #pragma unroll
-      for (int j = 0; j < AJ; ++j) {
-        if constexpr (SD != 0) st.ra[j] = bload_raw16(r, vo, (c0 + j) * cs);
-        else st.ra[j] = bload<0>(r, vo, (c0 + j) * cs);
-      }
-    } else {
+    for (int h = 0; h < KH; ++h) {
+      const int kh0 = k0 + kBK * h;
+      if constexpr (TU) {
+        const int4 e0 = a.ktab[kh0];              // the half's tap and first channel (uniform)
+        int c0 = e0.w;
+        const int hi = hb + e0.y, wi = wb + e0.z;
+        bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+        int vo = xoff + (e0.y * a.Wi + e0.z) * ES, cs = (int)(HiWi * ES);
+        __amdgpu_buffer_rsrc_t r = rx;
+        if constexpr (JM == 1) {                  // a K-step lies in one join chunk
+          const int q = c0 / a.jh;
+          const bool from_x = (q & 1) == 0;       // chunks [x_re, s_re, x_im, s_im]
+          c0 = (q >> 1) * a.jh + (c0 - q * a.jh);
+          ok &= !from_x | (hi < a.H2);            // F.pad rows of x read 0
+          vo = from_x ? xoff2 + (e0.y * a.W2 + e0.z) * 4 : vo;
+          cs = from_x ? (int)(H2W2 * 4) : cs;
+          r = from_x ? rx2 : rx;
+        }
+        vo = ok ? vo : (int)0x80000000;
+        c0 += AJ * akr;
 #pragma unroll
-      for (int j = 0; j < AJ; ++j) {
-        const int4 e = a.ktab[k0 + AJ * akr + j];   // uniform index -> s_load
-        const int hi = hb + e.y, wi = wb + e.z;
-        const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
-        const void* src = ok ? (const void*)a.X : (const void*)a.zero;
-        if constexpr (SD != 0) st.ra[j] = ld_raw16(src, ok ? xbase + e.x : 0);
-        else st.ra[j] = ld_s<0>(src, ok ? xbase + e.x : 0);
-      }
-    }
-    const u32x4* src = wt + (long long)(k0 >> 5) * NT * NW * kX3TileU4;
+        for (int j = 0; j < AJ; ++j) {
+          if constexpr (SD != 0) st.ra[AJ * h + j] = bload_raw16(r, vo, (c0 + j) * cs);
+          else st.ra[AJ * h + j] = bload<0>(r, vo, (c0 + j) * cs);
+        }
+      } else {
 #pragma unroll
-    for (int j = 0; j < 2 * PL; ++j) {
-      const int e = tid + THR * j;
-      st.rw[j] = src[PL == 2 ? e : e + (e >> 9) * 512];
+        for (int j = 0; j < AJ; ++j) {
+          const int4 e = a.ktab[kh0 + AJ * akr + j];   // uniform index -> s_load
+          const int hi = hb + e.y, wi = wb + e.z;
+          const bool ok = mval & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
+          const void* src = ok ? (const void*)a.X : (const void*)a.zero;
+          if constexpr (SD != 0) st.ra[AJ * h + j] = ld_raw16(src, ok ? xbase + e.x : 0);
+          else st.ra[AJ * h + j] = ld_s<0>(src, ok ? xbase + e.x : 0);
+        }
+      }
+      const u32x4* src = wt + (long long)((kh0 >> 5)) * NT * NW * kX3TileU4;
+#pragma unroll
+      for (int j = 0; j < 2 * PL; ++j) {
+        const int e = tid + THR * j;
+        st.rw[2 * PL * h + j] = src[PL == 2 ? e : e + (e >> 9) * 512];
+      }
     }
   };
   const int swz = x3_swz(am);
   auto store_tile = [&](const Stage& st, int buf) __attribute__((always_inline)) {
 #pragma unroll
-    for (int q = 0; q < CPT; ++q) {
-      u32x4 H, L;
+    for (int hk = 0; hk < KH; ++hk) {            // one term: half hk in the plane-hk slots
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        unsigned h, l = 0;
-        if constexpr (SD != 0) h = st.ra[8 * q + 2 * e] | (st.ra[8 * q + 2 * e + 1] << 16);   // = split2's hi, sa = 1
-        else split2<F16>(st.ra[8 * q + 2 * e], st.ra[8 * q + 2 * e + 1], sa, h, l);
-        H[e] = h;
-        L[e] = l;
+      for (int q = 0; q < CPT; ++q) {
+        u32x4 H, L;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i0 = AJ * hk + 8 * q + 2 * e;
+          unsigned h, l = 0;
+          if constexpr (SD != 0) h = st.ra[i0] | (st.ra[i0 + 1] << 16);   // = split2's hi, sa = 1
+          else split2<F16>(st.ra[i0], st.ra[i0 + 1], sa, h, l);
+          H[e] = h;
+          L[e] = l;
+        }
+        const int c = (CPT * akr + q) ^ swz;
+        sA[buf][hk * BM * 4 + am * 4 + c] = H;
+        if constexpr (PL == 2) sA[buf][BM * 4 + am * 4 + c] = L;
       }
-      const int c = (CPT * akr + q) ^ swz;
-      sA[buf][am * 4 + c] = H;
-      if constexpr (PL == 2) sA[buf][BM * 4 + am * 4 + c] = L;
-    }
 #pragma unroll
-    for (int j = 0; j < 2 * PL; ++j) sW[buf][tid + THR * j] = st.rw[j];
+      for (int j = 0; j < 2 * PL; ++j) sW[buf][hk * BN * 4 + tid + THR * j] = st.rw[2 * PL * hk + j];
+    }
   };
 
   f32x16 acc[RN][RM];
@@ -357,62 +375,66 @@ gather_x3_kernel(const GatherArgs a) {
   const int fsw = x3_swz(lr);
   // both k-substeps' fragments are read up front
   auto compute = [&](int cur) __attribute__((always_inline)) {
-    u32x4 wf[2][RN][PL], af[2][RM][PL];     // [ks][block][plane]
+    u32x4 wf[KH][2][RN][PL], af[KH][2][RM][PL];     // [half][ks][block][plane]
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      const int c = (2 * kk + lh) ^ fsw;
+    for (int hk = 0; hk < KH; ++hk)
 #pragma unroll
-      for (int i = 0; i < RN; ++i) {
-        const int n = wn * TN + 32 * i;         // block's first column (uniform)
+      for (int kk = 0; kk < 2; ++kk) {
+        const int c = (2 * kk + lh) ^ fsw;
 #pragma unroll
-        for (int p = 0; p < PL; ++p)
-          wf[kk][i][p] = sW[cur][(((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+        for (int i = 0; i < RN; ++i) {
+          const int n = wn * TN + 32 * i;       // block's first column (uniform)
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            wf[hk][kk][i][p] = sW[cur][hk * BN * 4 + (((n >> 7) * PL + p) * 128 + (n & 127) + lr) * 4 + c];
+        }
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+#pragma unroll
+          for (int p = 0; p < PL; ++p)
+            af[hk][kk][j][p] = sA[cur][((p + hk) * BM + wm * TM + 32 * j + lr) * 4 + c];
       }
 #pragma unroll
-      for (int j = 0; j < RM; ++j)
+    for (int hk = 0; hk < KH; ++hk)
 #pragma unroll
-        for (int p = 0; p < PL; ++p)
-          af[kk][j][p] = sA[cur][(p * BM + wm * TM + 32 * j + lr) * 4 + c];
-    }
+      for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+        for (int t = 0; t < TERMS; ++t)  // terms: hi*hi, hi*lo, lo*hi
 #pragma unroll
-      for (int t = 0; t < TERMS; ++t)  // terms: hi*hi, hi*lo, lo*hi
+          for (int i = 0; i < RN; ++i)
 #pragma unroll
-        for (int i = 0; i < RN; ++i)
-#pragma unroll
-          for (int j = 0; j < RM; ++j)
-            acc[i][j] = mfma_32x32x16<F16>(wf[kk][i][t == 2 ? 1 : 0], af[kk][j][t == 1 ? 1 : 0], acc[i][j]);
+            for (int j = 0; j < RM; ++j)
+              acc[i][j] = mfma_32x32x16<F16>(wf[hk][kk][i][t == 2 ? 1 : 0], af[hk][kk][j][t == 1 ? 1 : 0], acc[i][j]);
   };
   // one scheduling region per K-step: the non-MFMA stream (next tiles' loads,
   // fragment reads, LDS writes) interleaved into the MFMA gaps
   auto interleave = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);                  // first fragments
 #pragma unroll
-    for (int i = 0; i < 2 * TERMS * RN * RM; ++i) {
+    for (int i = 0; i < 2 * TERMS * RN * RM * KH; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
-      if (i < AJ + 4) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
+      if (i < (AJ + 2 * PL) * KH) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
       __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
     }
   };
 
-  const int nk = a.Kp / kBK;
+  const int nk = a.Kp / BKS;   // one term: Kp % 64 == 0 (plan_pass)
   // two register staging sets (prefetch distance 2); unconditional (clamped) loads and
   // stores keep each step one scheduling region: a clamped reload of the last tile
   // lands in the buffer no step reads
   load_tile(s0, 0);
   store_tile(s0, 0);
-  if (nk > 1) load_tile(s1, kBK);
+  if (nk > 1) load_tile(s1, BKS);
   __syncthreads();
   int kt = 0;
   for (; kt + 1 < nk; kt += 2) {
-    load_tile(s0, min(kt + 2, nk - 1) * kBK);
+    load_tile(s0, min(kt + 2, nk - 1) * BKS);
     compute(0);
     store_tile(s1, 1);
     interleave();
     __syncthreads();
-    load_tile(s1, min(kt + 3, nk - 1) * kBK);
+    load_tile(s1, min(kt + 3, nk - 1) * BKS);
     compute(1);
     store_tile(s0, 0);
     interleave();

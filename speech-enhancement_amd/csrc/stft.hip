@@ -454,6 +454,141 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
   unpack_store<CN, P, LP>(A, P, N, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
 }
 
+// ---------------------------------------------------------------------------
+// Wave-local forms: one frame pair per wave, its FFT passes synchronised by the
+// wave's own in-order LDS traffic (no block barrier between passes), so every
+// wave runs its load -> FFT chain independently and W of them share a block only
+// for the coalesced spectrum store (2W frames per row segment, one barrier).
+
+#ifndef SE_STFT_WV
+#define SE_STFT_WV 1
+#endif
+// W pairs per block: 8 (16 frames, 64-B row segments, 45 KB of LDS at nfft 640)
+#ifndef SE_STFT_WV_PAIRS
+#define SE_STFT_WV_PAIRS 8
+#endif
+constexpr int kWvPairs = SE_STFT_WV_PAIRS;
+using se::kWave;
+
+// compiler barrier between a wave's LDS writes and its reads of other lanes' data:
+// LDS instructions of one wave execute in issue order, so only code motion must stop
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+}
+
+// In-place pass PS of the compiled plan over ONE sequence a[0..N) by one wave:
+// every lane reads all inputs of its butterflies, then writes all outputs.
+template <int N, int PS, int NS>
+__device__ __forceinline__ void wfft_pass(float2* a, const float2* __restrict__ tw, int lane) {
+  constexpr CPlan pl = make_cplan(N);
+  if constexpr (PS < pl.npass) {
+    constexpr int R = pl.radix[PS], nbf = N / R, tstep = N / (NS * R);
+    constexpr int ITER = (nbf + kWave - 1) / kWave;
+    float2 v[ITER][kMaxRadix];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int j = lane + it * kWave;
+      if (nbf % kWave == 0 || j < nbf) {
+        const int k = j % NS;
+#pragma unroll
+        for (int q = 0; q < R; ++q) v[it][q] = a[j + q * nbf];
+        if constexpr (NS > 1) {
+#pragma unroll
+          for (int q = 1; q < R; ++q) v[it][q] = cmul(v[it][q], tw[q * k * tstep]);
+        }
+      }
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int j = lane + it * kWave;
+      if (nbf % kWave == 0 || j < nbf) butterfly<R>(v[it], a, (j / NS) * NS * R + j % NS, NS);
+    }
+    wave_lds_sync();
+    wfft_pass<N, PS + 1, NS * R>(a, tw, lane);
+  }
+}
+
+// Pair stride of the wave-local LDS image: N + 2 float2, so the unpack's reads of
+// W pairs at one bin fall in different banks
+template <int N> constexpr int wv_stride() { return N + 2; }
+
+// Unpack the W packed pair results of a wave-local block (pair stride NP) into
+// frames t0 + 2j (even) and t0 + 2j + 1 (odd); lanes run along frames, so a store
+// covers 2W consecutive frames of a spectrum row. out layout [B, N+2, T], or
+// mags / phase [B, N/2+1, T].
+template <int N, int W, bool LP>
+__device__ __forceinline__ void wv_unpack_store(const float2* A, int t0, int T, int b, void* out0, void* out1,
+                                                int mag_phase, int dt) {
+  constexpr int NP = wv_stride<N>(), TPB = kWave * W, half = N / 2 + 1, FT = 2 * W;
+  for (int idx = threadIdx.x; idx < half * FT; idx += TPB) {
+    const int k = idx / FT, f = idx - k * FT;
+    const int t = t0 + f;
+    if (t >= T) continue;
+    const int j = f >> 1;
+    const float2 zk = A[j * NP + k];
+    const float2 zc = A[j * NP + ((N - k) % N)];
+    float re, im;
+    if ((f & 1) == 0) {   // (Z[k] + conj Z[N-k]) / 2
+      re = 0.5f * (zk.x + zc.x);
+      im = 0.5f * (zk.y - zc.y);
+    } else {              // (Z[k] - conj Z[N-k]) / (2i)
+      re = 0.5f * (zk.y + zc.y);
+      im = -0.5f * (zk.x - zc.x);
+    }
+    im += 0.f;   // -0 -> +0 (atan2 branch cut)
+    if (!mag_phase) {
+      stx<LP>(out0, ((long long)b * (2 * half) + k) * T + t, re, dt);
+      stx<LP>(out0, ((long long)b * (2 * half) + half + k) * T + t, im, dt);
+    } else {
+      stx<LP>(out0, ((long long)b * half + k) * T + t, sqrtf(re * re + im * im), dt);
+      stx<LP>(out1, ((long long)b * half + k) * T + t, atan2f(im, re), dt);
+    }
+  }
+}
+
+// ConvSTFT, wave-local FFT: W frame pairs per block (wave w: frames t0 + 2w, +1).
+// grid (ceil(T / 2W), B), 64 W threads
+template <int CN, int W = kWvPairs, bool LP = false>
+__global__ void __launch_bounds__(kWave * W) stft_fwd_wv_kernel(const StftArgs a) {
+  constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W;
+  constexpr int half = N / 2 + 1, FT = 2 * W;
+  __shared__ __attribute__((aligned(16))) float2 A[W * NP];
+  __shared__ float2 stw[N];
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int t0 = tb * FT, ta = t0 + 2 * w, tbb = ta + 1;
+  const long long xo = (long long)b * a.L;
+  // the wave's two frames: loads for n < win only (the rest of the FFT input is
+  // zero), all issued before any is used
+  constexpr int IT = (N + kWave - 1) / kWave;
+  float ya[IT], yb[IT];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+    const bool ok = n < a.win;
+    const int nn = ok ? n : 0;
+    const float wv = ok ? a.window[nn] : 0.f;
+    const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+    const float xb = ldx<LP>(a.x, xo + reflect_index(min(tbb, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+    ya[it] = ta < a.T ? wv * xa : 0.f;
+    yb[it] = tbb < a.T ? wv * xb : 0.f;
+  }
+  for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
+  float2* Aw = A + w * NP;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+    if (N % kWave == 0 || n < N) Aw[n] = make_float2(ya[it], yb[it]);
+  }
+  __syncthreads();   // stw
+  wfft_pass<N, 0, 1>(Aw, stw, lane);
+  __syncthreads();   // every pair of the block transformed
+  wv_unpack_store<N, W, LP>(A, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
+}
+
 struct IstftArgs {
   const void* in;      // fwd: spec [B, N+2, T]; bwd: gout [B, out_len]
   void* out;           // fwd: out [B, out_len]; bwd: gspec [B, N+2, T]
@@ -777,6 +912,176 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
   unpack_store<N, P, LP>(A, P, N, t0, a.T, b, a.out, nullptr, 0, a.dt);
 }
 
+// ConviSTFT forward, wave-local FFT: W frame pairs per block. The spectrum gather
+// (lanes along frames: coalesced row segments) and the overlap-add store are
+// block-wide; each wave transforms its pair, takes its frames' parity sums and
+// writes its two synthesis frames without a block barrier.
+// grid (ceil(out_len / (FT*hop)), B), FT = 2W - 1 - (win-1)/hop, 64 W threads
+template <int CN, int W = kWvPairs, bool LP = false>
+__global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs a) {
+  constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W, half = N / 2 + 1, P = W;
+  __shared__ __attribute__((aligned(16))) float2 A[W * NP];
+  __shared__ float2 stw[N];
+  int sb, b;
+  xcd_frame_block(sb, b);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int s0 = a.offset + sb * a.FT * a.hop;
+  const int s1 = min(s0 + a.FT * a.hop, a.offset + a.out_len);
+  const int t_lo = max(0, ceil_div_i(s0 - a.win + 1, a.hop));
+  const int t_hi = min(a.T - 1, floor_div(s1 - 1, a.hop));
+  const long long so = (long long)b * 2 * half * a.T;
+  // spectrum gather, all loads issued first (clamped addresses, zeroed after the load)
+  constexpr int GT = (half * P + TPB - 1) / TPB;
+  float2 ga[GT], gb[GT];
+#pragma unroll
+  for (int it = 0; it < GT; ++it) {
+    const int idx = threadIdx.x + it * TPB;
+    const int k = min(idx / P, half - 1), j = idx % P;
+    const int ta = min(t_lo + 2 * j, t_hi), tb = min(t_lo + 2 * j + 1, t_hi);
+    const long long re = so + (long long)k * a.T, im = so + (long long)(half + k) * a.T;
+    ga[it] = make_float2(ldx<LP>(a.in, re + ta, a.dt), ldx<LP>(a.in, im + ta, a.dt));
+    gb[it] = make_float2(ldx<LP>(a.in, re + tb, a.dt), ldx<LP>(a.in, im + tb, a.dt));
+  }
+  for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
+  // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
+#pragma unroll
+  for (int it = 0; it < GT; ++it) {
+    const int idx = threadIdx.x + it * TPB;
+    if (idx >= half * P) break;
+    const int k = idx / P, j = idx - k * P;
+    const int ta = t_lo + 2 * j, tb = ta + 1;
+    const float2 zero = make_float2(0.f, 0.f);
+    const float2 xa = ta <= t_hi ? ga[it] : zero, xb = tb <= t_hi ? gb[it] : zero;
+    float2* c = A + j * NP;
+    if (k == 0 || k == N / 2) {
+      c[k] = make_float2(xa.x, -xb.x);
+    } else {
+      c[k] = make_float2(0.5f * (xa.x - xb.y), -0.5f * (xa.y + xb.x));
+      c[N - k] = make_float2(0.5f * (xa.x + xb.y), 0.5f * (xa.y - xb.x));
+    }
+  }
+  __syncthreads();
+  float2* Aw = A + w * NP;
+  wfft_pass<N, 0, 1>(Aw, stw, lane);
+  // z = conj(Aw): z_a = Aw.x, z_b = -Aw.y. Parity sums over n < win, then the
+  // windowed G-corrected frames written over the wave's own buffer as [2][win] floats
+  constexpr int IT = (N + kWave - 1) / kWave;
+  float2 z[IT];
+  float sea = 0.f, soa = 0.f, seb = 0.f, sob = 0.f;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+    z[it] = n < a.win ? Aw[n] : make_float2(0.f, 0.f);
+    z[it].y = -z[it].y;
+    if (n & 1) { soa += z[it].x; sob += z[it].y; } else { sea += z[it].x; seb += z[it].y; }
+  }
+  sea = se::wave_sum(sea); soa = se::wave_sum(soa);
+  seb = se::wave_sum(seb); sob = se::wave_sum(sob);
+  const float ah = 0.5f * N, inv_a = 1.f / ah;
+  const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
+  wave_lds_sync();
+  float* fw = reinterpret_cast<float*>(Aw);
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+    if (n < a.win) {
+      const float wn = a.window[n];
+      fw[n] = wn * apply_g(z[it].x, n, sea, soa, inv_a, ce, co);
+      fw[a.win + n] = wn * apply_g(z[it].y, n, seb, sob, inv_a, ce, co);
+    }
+  }
+  __syncthreads();
+  const long long oo = (long long)b * a.out_len;
+  for (int s = s0 + threadIdx.x; s < s1; s += TPB) {
+    const int tb0 = max(t_lo, ceil_div_i(s - a.win + 1, a.hop));
+    const int tb1 = min(t_hi, floor_div(s, a.hop));
+    float acc = 0.f, cf = 0.f;
+    for (int t = tb0; t <= tb1; ++t) {
+      const int n = s - t * a.hop, f = t - t_lo;
+      const float wn = a.window[n];
+      acc += reinterpret_cast<const float*>(A + (f >> 1) * NP)[(f & 1) * a.win + n];
+      cf += wn * wn;
+    }
+    stx<LP>(a.out, oo + s - a.offset, acc / (cf + 1e-8f), a.dt);
+  }
+}
+
+// Adjoint of istft_fwd, wave-local FFT: wave w gathers and normalises frames
+// t0 + 2w, +1 (contiguous gradient samples: coalesced), applies G with its own
+// parity sums, transforms its pair; one barrier before the block-wide spectrum
+// store. grid (ceil(T / 2W), B), 64 W threads
+template <int CN, int W = kWvPairs, bool LP = false>
+__global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs a) {
+  constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W;
+  __shared__ __attribute__((aligned(16))) float2 A[W * NP];
+  __shared__ float2 stw[N];
+  __shared__ float swin[N];
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int t0 = tb * 2 * W;
+  const long long go = (long long)b * a.out_len;
+  constexpr int IT = (N + kWave - 1) / kWave;
+  float ga[IT][2];
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int u = (t0 + 2 * w + h) * a.hop + min(n, a.win - 1);
+      ga[it][h] = a.out_len > 0 ? ldx<LP>(a.in, go + min(max(u - a.offset, 0), a.out_len - 1), a.dt) : 0.f;
+    }
+  }
+  for (int i = threadIdx.x; i < N; i += TPB) {
+    stw[i] = a.tw[i];
+    swin[i] = i < a.win ? a.window[i] : 0.f;
+  }
+  __syncthreads();
+  float v[IT][2];
+  float se2[2] = {0.f, 0.f}, so2[2] = {0.f, 0.f};
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      float val = 0.f;
+      const int t = t0 + 2 * w + h;
+      const int u = t * a.hop + n;
+      if (n < a.win && t < a.T && u >= a.offset && u < a.offset + a.out_len) {
+        // OLA normaliser at u (window^2 summed over covering frames)
+        const int tb0 = max(0, ceil_div_i(u - a.win + 1, a.hop));
+        const int tb1 = min(a.T - 1, floor_div(u, a.hop));
+        float cf = 0.f;
+        for (int tt = tb0; tt <= tb1; ++tt) {
+          const float ww = swin[u - tt * a.hop];
+          cf += ww * ww;
+        }
+        val = swin[n] * ga[it][h] / (cf + 1e-8f);
+      }
+      v[it][h] = val;
+      if (n & 1) so2[h] += val; else se2[h] += val;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) { se2[h] = se::wave_sum(se2[h]); so2[h] = se::wave_sum(so2[h]); }
+  const float ah = 0.5f * N, inv_a = 1.f / ah;
+  const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
+  float2* Aw = A + w * NP;
+#pragma unroll
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+    if (N % kWave == 0 || n < N) {
+      const bool in = n < a.win;
+      Aw[n] = make_float2(in ? apply_g(v[it][0], n, se2[0], so2[0], inv_a, ce, co) : 0.f,
+                          in ? apply_g(v[it][1], n, se2[1], so2[1], inv_a, ce, co) : 0.f);
+    }
+  }
+  wave_lds_sync();
+  wfft_pass<N, 0, 1>(Aw, stw, lane);
+  __syncthreads();
+  wv_unpack_store<N, W, LP>(A, t0, a.T, b, a.out, nullptr, 0, a.dt);
+}
+
 // ---------------------------------------------------------------------------
 static bool make_plan(int N, FftPlan& pl) {
   if (N < 2 || N > 1024) return false;
@@ -861,6 +1166,27 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
   a.L = L; a.win = win; a.hop = hop; a.T = T; a.pad = pad; a.mag_phase = mag_phase;
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
+  if (SE_STFT_WV && ip_plan(nfft)) {
+    // wave-local FFT, kWvPairs frame pairs per block
+    const dim3 grid(se::ceil_div(T, 2 * kWvPairs), B);
+    hipStream_t st = se::as_stream(stream);
+    const dim3 blk(se::kWave * kWvPairs);
+#define SE_STFT_WVL(NF)                                                                                 \
+    do {                                                                                                \
+      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((stft_fwd_wv_kernel<NF, kWvPairs, true>), grid, blk, 0, st, a);  \
+      else hipLaunchKernelGGL((stft_fwd_wv_kernel<NF, kWvPairs, false>), grid, blk, 0, st, a);          \
+    } while (0)
+    switch (nfft) {
+      case 640: SE_STFT_WVL(640); break;
+      case 512: SE_STFT_WVL(512); break;
+      case 400: SE_STFT_WVL(400); break;
+      case 320: SE_STFT_WVL(320); break;
+      default: SE_STFT_WVL(256); break;
+    }
+#undef SE_STFT_WVL
+    SE_LAUNCH_CHECK();
+    return SE_OK;
+  }
   if (ip_plan(nfft)) {
     // in-place FFT, kPairsIP frame pairs per block (static LDS <= 25 KB)
     const int P = kPairsIP;
@@ -908,6 +1234,30 @@ extern "C" int se_istft_fwd(const void* spec, void* out, int B, int T, int win, 
   if (!spec || !out || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
   if (out_len == 0) return SE_OK;
   a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
+  if (SE_STFT_WV && ip_plan(nfft)) {
+    // wave-local FFT, kWvPairs frame pairs per block
+    a.P = kWvPairs;
+    a.FT = 2 * kWvPairs - 1 - (win - 1) / hop;
+    if (a.FT >= 1) {
+      const dim3 grid(se::ceil_div(out_len, a.FT * hop), B), blk(se::kWave * kWvPairs);
+      hipStream_t st = se::as_stream(stream);
+#define SE_ISTFT_WVL(NF)                                                                                \
+      do {                                                                                              \
+        if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, kWvPairs, true>), grid, blk, 0, st, a); \
+        else hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, kWvPairs, false>), grid, blk, 0, st, a);      \
+      } while (0)
+      switch (nfft) {
+        case 640: SE_ISTFT_WVL(640); break;
+        case 512: SE_ISTFT_WVL(512); break;
+        case 400: SE_ISTFT_WVL(400); break;
+        case 320: SE_ISTFT_WVL(320); break;
+        default: SE_ISTFT_WVL(256); break;
+      }
+#undef SE_ISTFT_WVL
+      SE_LAUNCH_CHECK();
+      return SE_OK;
+    }
+  }
   if (ip_plan(nfft)) {
     // in-place FFT, kPairsIP frame pairs per block (8 measured slower: 79.9 / 107 us)
     const int P = kPairsIP;
@@ -946,6 +1296,26 @@ extern "C" int se_istft_bwd(const void* gout, void* gspec, int B, int T, int win
   if (rc) return rc;
   if (!gout || !gspec || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
   a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
+  if (SE_STFT_WV && ip_plan(nfft)) {
+    // wave-local FFT, kWvPairs frame pairs per block
+    const dim3 grid(se::ceil_div(T, 2 * kWvPairs), B), blk(se::kWave * kWvPairs);
+    hipStream_t st = se::as_stream(stream);
+#define SE_ISTFT_BWD_WVL(NF)                                                                            \
+    do {                                                                                                \
+      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_bwd_wv_kernel<NF, kWvPairs, true>), grid, blk, 0, st, a); \
+      else hipLaunchKernelGGL((istft_bwd_wv_kernel<NF, kWvPairs, false>), grid, blk, 0, st, a);        \
+    } while (0)
+    switch (nfft) {
+      case 640: SE_ISTFT_BWD_WVL(640); break;
+      case 512: SE_ISTFT_BWD_WVL(512); break;
+      case 400: SE_ISTFT_BWD_WVL(400); break;
+      case 320: SE_ISTFT_BWD_WVL(320); break;
+      default: SE_ISTFT_BWD_WVL(256); break;
+    }
+#undef SE_ISTFT_BWD_WVL
+    SE_LAUNCH_CHECK();
+    return SE_OK;
+  }
   if (ip_plan(nfft)) {
     // in-place FFT, kPairsIP frame pairs per block (8 measured slower: 79.9 / 107 us)
     const int P = kPairsIP;
