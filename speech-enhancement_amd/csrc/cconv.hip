@@ -488,6 +488,94 @@ gather_stencil_kernel(const GatherArgs a, int h0, int w0, int th, int tw) {
   }
 }
 
+// Small-N stride-1 conv over MANY channels as a chunked LDS stencil: DCUNet's final
+// ComplexConvTranspose2d (128 -> 2 channels, k (7, 5), stride (2, 2); its four phase
+// classes are stride-1 convs of 2-4 x 2-3 taps; _1903_03107_dcunet.py:80-83,
+// architectures.py:63-72). A workgroup owns a (kScRows x kStW) output tile of one
+// class; per chunk of kScC channels it stages the input tile plus halo in LDS (the
+// next chunk's loads are in flight meanwhile), and each thread forms kScR rows of one
+// column: per (channel, tap column) it reads the kScR + NTH - 1 input rows its NTH
+// row taps touch once and reuses them from registers. The class's row offsets are
+// consecutive and descending (offh[a] = offh[0] - a, phase_dim), so the tap-row
+// index into that window is a compile-time constant. Weights are uniform (scalar
+// loads): Wp[(t * Cg + c) * ldw + n], t = a * ntw + b.
+constexpr int kScC = 8, kScR = 4, kScRows = 4 * kScR;   // 8 channels, 16 x 64 outputs
+constexpr int kScPitch = kStW + 8;                        // LDS row: 64 columns + a halo <= 8
+template <int NO, int NTH, int SD>
+__global__ void __launch_bounds__(kThreads)
+gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw) {
+  constexpr int TH = kScRows + NTH - 1, WIN = kScR + NTH - 1;
+  constexpr int tw = kScPitch, plane = TH * tw, chunk = kScC * plane;   // compile-time indexing
+  extern __shared__ float sx[];   // [kScC][TH][kScPitch]
+  const int b = blockIdx.z;
+  const int qh0 = blockIdx.y * kScRows, qw0 = blockIdx.x * kStW;
+  const long long HiWi = (long long)a.Hi * a.Wi;
+  const long long xb = (long long)b * a.Cg * HiWi;
+  constexpr int PF = (chunk + kThreads - 1) / kThreads;
+  float pf[PF];
+  auto fetch = [&](int c0) __attribute__((always_inline)) {
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int i = threadIdx.x + j * kThreads;
+      const int c = i / plane, rr = i - c * plane;
+      const int r = rr / tw, col = rr - r * tw;
+      const int hi = qh0 + h0 + r, wi = qw0 + w0 + col;
+      const bool ok = (chunk % kThreads == 0 || i < chunk) && c0 + c < a.Cg && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+      const float v = ld_s<SD>(a.X, ok ? xb + (long long)(c0 + c) * HiWi + (long long)hi * a.Wi + wi : 0);
+      pf[j] = ok ? v : 0.f;
+    }
+  };
+  const int lc = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * kScR;
+  float acc[kScR][NO];
+#pragma unroll
+  for (int r = 0; r < kScR; ++r)
+#pragma unroll
+    for (int n = 0; n < NO; ++n) acc[r][n] = 0.f;
+  fetch(0);
+  for (int c0 = 0; c0 < a.Cg; c0 += kScC) {
+    __syncthreads();   // the previous chunk is consumed
+#pragma unroll
+    for (int j = 0; j < PF; ++j) {
+      const int i = threadIdx.x + j * kThreads;
+      if (chunk % kThreads == 0 || i < chunk) sx[i] = pf[j];
+    }
+    __syncthreads();
+    if (c0 + kScC < a.Cg) fetch(c0 + kScC);
+    const int nc = min(kScC, a.Cg - c0);
+    for (int c = 0; c < nc; ++c) {
+      for (int bw = 0; bw < ntw; ++bw) {
+        const float* src = sx + c * plane + r0 * tw + lc + a.toffw[bw] - w0;
+        float v[WIN];
+#pragma unroll
+        for (int i = 0; i < WIN; ++i) v[i] = src[i * tw];
+#pragma unroll
+        for (int ah = 0; ah < NTH; ++ah) {
+          const float* wk = a.Wp + (long long)((ah * ntw + bw) * a.Cg + c0 + c) * a.ldw;
+          float w[NO];
+#pragma unroll
+          for (int n = 0; n < NO; ++n) w[n] = wk[n];
+#pragma unroll
+          for (int r = 0; r < kScR; ++r)
+#pragma unroll
+            for (int n = 0; n < NO; ++n) acc[r][n] = fmaf(v[r + NTH - 1 - ah], w[n], acc[r][n]);
+        }
+      }
+    }
+  }
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  const int qw = qw0 + lc;
+  if (qw >= a.Qw) return;
+#pragma unroll
+  for (int r = 0; r < kScR; ++r) {
+    const int qh = qh0 + r0 + r;
+    if (qh >= a.Qh) break;
+    const long long yb = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
+#pragma unroll
+    for (int n = 0; n < NO; ++n)
+      if (n < a.N) st_s<SD>(a.Y, yb + n * HoWo, acc[r][n] + (a.bias ? a.bias[n] : 0.f));
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Weight-grad reduction GEMM: dWp[k, n] = sum_m G[m, k] * D[m, n]
 // Each workgroup reduces one m-range (split) for one BKO x BNO tile and
@@ -1449,6 +1537,39 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
         const size_t shs = (size_t)Cg * th * tw * sizeof(float);
         if (Cg == 4) hipLaunchKernelGGL((gather_stencil_kernel<4, 4>), sgrid, dim3(kThreads), shs, st, a, h0, w0, th, tw);
         else hipLaunchKernelGGL((gather_stencil_kernel<4, 2>), sgrid, dim3(kThreads), shs, st, a, h0, w0, th, tw);
+        SE_LAUNCH_CHECK();
+        continue;
+      }
+      // many-channel stride-1 classes (DCUNet's final convT): the chunked stencil
+      const int nth = c.h.ntaps, ntw = c.w.ntaps;
+      bool hdesc = nth >= 1 && nth <= 4 && ntw >= 1 && c.taps.n <= kMaxTaps;
+      for (int t = 0; hdesc && t < c.taps.n; ++t)
+        hdesc = c.taps.offh[t] == c.h.off[0] - t / ntw && c.taps.offw[t] == c.w.off[t % ntw];
+      int wmin = c.w.off[0], wmax = c.w.off[0];
+      for (int q = 1; q < ntw; ++q) { wmin = std::min(wmin, c.w.off[q]); wmax = std::max(wmax, c.w.off[q]); }
+      const int hmin = c.h.off[0] - (nth - 1);   // the window's first input row offset
+      const bool stencil_ch = !jn && ldw <= 4 && Cg > 4 && c.h.s == 1 && c.w.s == 1 && hdesc &&
+                              wmax - wmin <= kScPitch - kStW && !env_flag_off("SEHIP_STENCIL");
+      if (stencil_ch) {
+        a.ntaps = c.taps.n;
+        for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }
+        const dim3 sgrid(se::ceil_div(c.w.Q, kStW), se::ceil_div(c.h.Q, kScRows), g.B);
+        const size_t shs = (size_t)kScC * (kScRows + nth - 1) * kScPitch * sizeof(float);
+#define SE_STC(NO, NTH)                                                                                   \
+  do {                                                                                                    \
+    if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 1>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw); \
+    else if (g.sd == SE_DTYPE_F16) hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 2>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw); \
+    else hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 0>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw); \
+  } while (0)
+#define SE_STC_N(NTH) do { if (N <= 2) SE_STC(2, NTH); else SE_STC(4, NTH); } while (0)
+        switch (nth) {
+          case 1: SE_STC_N(1); break;
+          case 2: SE_STC_N(2); break;
+          case 3: SE_STC_N(3); break;
+          default: SE_STC_N(4); break;
+        }
+#undef SE_STC_N
+#undef SE_STC
         SE_LAUNCH_CHECK();
         continue;
       }

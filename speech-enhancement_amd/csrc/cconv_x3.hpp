@@ -565,6 +565,10 @@ wgrad_x3_kernel(const WgradArgs a) {
   constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
   // per 128-row G block: G hi, G lo; then per 128-row D block: D hi, D lo
   constexpr int DPL = 2;                     // first D plane
+  // 32-position halves per staging round: one term stages two (64 positions; the lo
+  // plane slots hold the second half), so a barrier feeds 16 MFMAs per wave, not 8;
+  // the positions are accumulated in the same order, so the slabs are unchanged
+  constexpr int KH = TERMS == 1 ? kX3OneTermHalves : 1;
   __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 + 2 * NB) * PLANE];
   __shared__ int4 sK[BKO];
 
@@ -620,7 +624,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   // DPK: a thread's D chunks are chunk dch (8 joined rows) of positions dpa and dpa + 16,
   // both planes (4 x 16 B); the position cursors advance by BMR like the lane's own
   constexpr int RJD = DPK ? 1 : RJ;
-  struct Stage { typename StageT<SD>::T rg[RJG], rd[RJD]; u32x4 dq[DPK ? 4 : 1]; };   // 16-bit storage: raw bits
+  struct Stage { typename StageT<SD>::T rg[RJG * KH], rd[RJD * KH]; u32x4 dq[DPK ? 4 : 1]; };   // 16-bit: raw bits
   Stage st0, st1;
   const int dch = tid & 31, dpa = tid >> 5;
   int pcb[2] = {0, 0}, pqh[2] = {0, 0}, pqw[2] = {0, 0};
@@ -687,7 +691,10 @@ wgrad_x3_kernel(const WgradArgs a) {
   const _Float16* d_src = reinterpret_cast<const _Float16*>(d_from_x ? a.dpk2 : a.dpk);
   const long long d_plane = d_from_x ? a.pk_plane_d2 : a.pk_plane_d;
   const _Float16* d_zero = reinterpret_cast<const _Float16*>(a.zero);
-  auto load_step = [&](Stage& S, int mstep) __attribute__((always_inline)) {
+  auto load_step = [&](Stage& S, int mstep0) __attribute__((always_inline)) {
+#pragma unroll
+   for (int hh = 0; hh < KH; ++hh) {
+    const int mstep = mstep0 + BMR * hh;
     const bool mv = mstep + ml < mend;
     const int rb = cb - bfirst;
     // D rows of this thread: n0 + rbase + j, j < RJ. The host runs this kernel
@@ -717,7 +724,7 @@ wgrad_x3_kernel(const WgradArgs a) {
     }
     if (KP && !gact) {
 #pragma unroll
-      for (int j = 0; j < RJG; ++j) S.rg[j] = 0.f;
+      for (int j = 0; j < RJG; ++j) S.rg[RJG * hh + j] = 0.f;
     } else if constexpr (TU) {
       const int hi = cqh * a.sh + tap_e.y, wi = cqw * a.sw + tap_e.z;
       const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
@@ -726,8 +733,8 @@ wgrad_x3_kernel(const WgradArgs a) {
       const int gs = (int)(HiWi * ES);
 #pragma unroll
       for (int j = 0; j < RJG; ++j) {
-        if constexpr (SD != 0) S.rg[j] = bload_raw16(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
-        else S.rg[j] = bload<0>(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
+        if constexpr (SD != 0) S.rg[RJG * hh + j] = bload_raw16(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
+        else S.rg[RJG * hh + j] = bload<0>(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
       }
     } else {
       const int hb = cqh * a.sh, wb = cqw * a.sw;
@@ -738,8 +745,8 @@ wgrad_x3_kernel(const WgradArgs a) {
         const int hi = hb + e.y, wi = wb + e.z;
         const bool ok = mv & ((unsigned)hi < (unsigned)a.Hi) & ((unsigned)wi < (unsigned)a.Wi);
         const void* src = ok ? (const void*)a.X : (const void*)a.zero;
-        if constexpr (SD != 0) S.rg[j] = ld_raw16(src, ok ? xb + e.x : 0);
-        else S.rg[j] = ld_s<0>(src, ok ? xb + e.x : 0);
+        if constexpr (SD != 0) S.rg[RJG * hh + j] = ld_raw16(src, ok ? xb + e.x : 0);
+        else S.rg[RJG * hh + j] = ld_s<0>(src, ok ? xb + e.x : 0);
       }
     }
     if constexpr (DPK) {
@@ -755,16 +762,19 @@ wgrad_x3_kernel(const WgradArgs a) {
     } else {
 #pragma unroll
       for (int j = 0; j < RJ; ++j) {
-        if constexpr (SD != 0) S.rd[j] = bload_raw16(rdr, vd, (srow + j) * ds);
-        else S.rd[j] = bload<0>(rdr, vd, (srow + j) * ds);
+        if constexpr (SD != 0) S.rd[RJ * hh + j] = bload_raw16(rdr, vd, (srow + j) * ds);
+        else S.rd[RJ * hh + j] = bload<0>(rdr, vd, (srow + j) * ds);
       }
     }
     advance();
+   }
   };
   auto store_step = [&](const Stage& S, int buf) __attribute__((always_inline)) {
-    unsigned char* base = sm[buf];
-    unsigned char* dbase = base + (DPL + 2 * (rbase >> 7)) * PLANE;   // this thread's D block
-    unsigned char* gbase = base;                                       // ... and G block
+   unsigned char* base = sm[buf];
+#pragma unroll
+   for (int hh = 0; hh < KH; ++hh) {   // one term: half hh in the plane-hh slots
+    unsigned char* dbase = base + (DPL + 2 * (rbase >> 7) + hh) * PLANE;   // this thread's D block
+    unsigned char* gbase = base + hh * PLANE;                              // ... and G block
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       u32x4 GH, GL, DH, DL;
@@ -772,13 +782,15 @@ wgrad_x3_kernel(const WgradArgs a) {
       for (int e = 0; e < 4; ++e) {
         unsigned h, l = 0;
         if (q < RJG / 8) {
-          if constexpr (SD != 0) h = S.rg[8 * q + 2 * e] | (S.rg[8 * q + 2 * e + 1] << 16);   // split2's hi, sg = 1
-          else split2<F16>(S.rg[8 * q + 2 * e], S.rg[8 * q + 2 * e + 1], sg, h, l);
+          const int ig = RJG * hh + 8 * q + 2 * e;
+          if constexpr (SD != 0) h = S.rg[ig] | (S.rg[ig + 1] << 16);   // split2's hi, sg = 1
+          else split2<F16>(S.rg[ig], S.rg[ig + 1], sg, h, l);
           GH[e] = h; GL[e] = l;
         }
         if (!DPK && q < RJ / 8) {
-          if constexpr (SD != 0) h = S.rd[8 * q + 2 * e] | (S.rd[8 * q + 2 * e + 1] << 16);
-          else split2<F16>(S.rd[8 * q + 2 * e], S.rd[8 * q + 2 * e + 1], sd, h, l);
+          const int id = RJD * hh + 8 * q + 2 * e;
+          if constexpr (SD != 0) h = S.rd[id] | (S.rd[id + 1] << 16);
+          else split2<F16>(S.rd[id], S.rd[id + 1], sd, h, l);
           DH[e] = h; DL[e] = l;
         }
       }
@@ -802,6 +814,7 @@ wgrad_x3_kernel(const WgradArgs a) {
         *reinterpret_cast<u32x4*>(db + PLANE + off) = S.dq[2 + i];
       }
     }
+   }
   };
 
   f32x16 acc[RK][RN];
@@ -812,7 +825,8 @@ wgrad_x3_kernel(const WgradArgs a) {
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
 
-  const int nsteps = (mend > mbeg) ? (mend - mbeg + BMR - 1) / BMR : 0;
+  constexpr int BMS = BMR * KH;              // positions per staging round
+  const int nsteps = (mend > mbeg) ? (mend - mbeg + BMS - 1) / BMS : 0;
   // transposed-read addressing (T10): group g = lane >> 4 takes columns
   // 16 (g & 1) .. +15 of a 32-row block and positions 8 (g >> 1) + 0..3 / 4..7;
   // lane 4q + p of the group addresses position row q, columns 4p .. 4p + 3
@@ -829,17 +843,18 @@ wgrad_x3_kernel(const WgradArgs a) {
   auto compute = [&](int cur) __attribute__((always_inline)) {
     const unsigned char* base = sm[cur];
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int hs = 0; hs < 2 * KH; ++hs) {   // (half, 16-position k-substep)
+      const int hh = hs >> 1, ks = hs & 1;
       bf16x8 ga[RK][PL], gb[RN][PL];
 #pragma unroll
       for (int p = 0; p < PL; ++p) {
 #pragma unroll
         for (int i = 0; i < RK; ++i)
           if (!KP || 32 * i < kvw)
-            ga[i][p] = frag(base + (2 * (wk >> 1) + p) * PLANE, (wk & 1) * TK + 32 * i, 16 * ks);
+            ga[i][p] = frag(base + (2 * (wk >> 1) + p + hh) * PLANE, (wk & 1) * TK + 32 * i, 16 * ks);
 #pragma unroll
         for (int j = 0; j < RN; ++j)
-          gb[j][p] = frag(base + (DPL + 2 * (wnn >> 1) + p) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
+          gb[j][p] = frag(base + (DPL + 2 * (wnn >> 1) + p + hh) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
       }
 #pragma unroll
       for (int t = 0; t < TERMS; ++t)
@@ -855,7 +870,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   auto interleave = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
 #pragma unroll
-    for (int i = 0; i < 24; ++i) {
+    for (int i = 0; i < 2 * TERMS * RK * RN * KH; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);              // MFMA
       __builtin_amdgcn_sched_group_barrier(0x080, 2, 0);              // DS
       __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);              // global load
@@ -866,20 +881,39 @@ wgrad_x3_kernel(const WgradArgs a) {
     load_step(st0, mbeg);
     store_step(st0, 0);
   }
-  if (nsteps > 1) load_step(st1, mbeg + BMR);
-  __syncthreads();
   int s = 0;
+  if constexpr (KH > 1) {
+    // one register staging set (prefetch distance one round = two 32-position steps,
+    // as the two sets of the 32-position form): a round's loads are in flight during
+    // the previous round's 16 MFMAs
+    __syncthreads();
+    for (; s + 1 < nsteps; s += 2) {
+      load_step(st0, mbeg + (s + 1) * BMS);
+      compute(0);
+      store_step(st0, 1);
+      interleave();
+      __syncthreads();
+      load_step(st0, mbeg + (s + 2) * BMS);
+      compute(1);
+      store_step(st0, 0);
+      interleave();
+      __syncthreads();
+    }
+  } else {
+  if (nsteps > 1) load_step(st1, mbeg + BMS);
+  __syncthreads();
   for (; s + 1 < nsteps; s += 2) {
-    load_step(st0, mbeg + (s + 2) * BMR);
+    load_step(st0, mbeg + (s + 2) * BMS);
     compute(0);
     store_step(st1, 1);
     interleave();
     __syncthreads();
-    load_step(st1, mbeg + (s + 3) * BMR);
+    load_step(st1, mbeg + (s + 3) * BMS);
     compute(1);
     store_step(st0, 0);
     interleave();
     __syncthreads();
+  }
   }
   if (s < nsteps) compute(0);
   float* out = a.slab + (long long)split * a.Kp * a.Np;

@@ -217,3 +217,44 @@ def test_conv_16bit_storage(name, tr, cin, cout, shape, stride, dtype, tol, gpu_
               f"{torch.equal(nat[k], cast[k])}")
         assert torch.equal(nat[k], cast[k]), (name, k)
         assert e < tol, (name, k, e)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("shape,kernel,stride,padding",
+                         [((2, 128, 33, 63), (7, 5), (2, 2), (3, 2)),    # DCUNet-16's final convT
+                          ((1, 96, 20, 70), (5, 3), (2, 1), (2, 1)),     # 3 row taps, ragged tiles
+                          ((2, 40, 9, 17), (3, 3), (1, 1), (1, 1))])     # stride 1, 5 channel chunks
+def test_many_channel_small_n_stencil(shape, kernel, stride, padding, dtype, gpu_device, monkeypatch):
+    """Small-N transposed convs over many channels (DCUNet's final 128 -> 2 layer,
+    _1903_03107_dcunet.py:80-83) run the chunked LDS stencil (gather_stencil_ch_kernel):
+    within fp32 summation-order rounding of the per-output gather (SEHIP_STENCIL=0), and
+    of fp64; 16-bit storage read and written natively."""
+    from sehip import functional as F
+    m = paramfill.fill_(O_cnn.ComplexConvTranspose2d(shape[1], 2, kernel, stride=stride, padding=padding),
+                        seed=5)
+    gen = torch.Generator().manual_seed(17)
+    x = torch.randn(*shape, generator=gen).to(dtype)
+    md = m.double()
+    wr16, wi16 = m.real_conv.weight.detach().to(dtype), m.imag_conv.weight.detach().to(dtype)
+    br, bi = m.real_conv.bias.detach().to(dtype), m.imag_conv.bias.detach().to(dtype)
+    with torch.no_grad():
+        md.real_conv.weight.copy_(wr16.double()); md.imag_conv.weight.copy_(wi16.double())
+        md.real_conv.bias.copy_(br.double()); md.imag_conv.bias.copy_(bi.double())
+        ref = md(x.double())
+
+    def run(stencil):
+        monkeypatch.setenv("SEHIP_STENCIL", "1" if stencil else "0")
+        with torch.no_grad():
+            y = F.conv2d(x.cuda(), wr16.cuda(), wi16.cuda(), br.cuda(), bi.cuda(), out_channels=2,
+                         kernel=kernel, stride=stride, padding=padding, transposed=True)
+        torch.cuda.synchronize()
+        assert y.dtype == dtype and y.shape == ref.shape
+        return y.float().cpu()
+
+    st, gath = run(True), run(False)
+    e_st = rel_l2(st.numpy(), ref.numpy())
+    e_ga = rel_l2(gath.numpy(), ref.numpy())
+    d = rel_l2(st.numpy(), gath.numpy())
+    print(f"{shape} {dtype}: stencil vs fp64 {e_st:.2e}, gather vs fp64 {e_ga:.2e}, stencil vs gather {d:.2e}")
+    tol = 1e-6 if dtype == torch.float32 else 6e-3
+    assert e_st < tol and d < (1e-6 if dtype == torch.float32 else 8e-3)
