@@ -158,7 +158,7 @@ class _CCBAMFn(torch.autograd.Function):
         xa = F.amax_get(x)
         oa = xa + 1.0 if xa is not None else None   # ca, sa in (0, 1): |x ca + sa| <= max |x| + 1
         # the CL16 copy of out for the decoder's joined weight-grad (scaled by oa)
-        pk = F.new_cl16(x) if pack and oa is not None and C % 8 == 0 and F.cl16_wanted(x) else None
+        pk = F.new_cl16(x) if pack and oa is not None and C % 8 == 0 else None
         _call(lib.se_ccbam_apply, "se_ccbam_apply", x.data_ptr(), ca.data_ptr(), sa.data_ptr(),
               out.data_ptr(), N.ptr(pk), N.ptr(oa if pk is not None else None), B, C, HW, st)
         if oa is not None:   # F16X3 scale source of the consumers
@@ -227,7 +227,8 @@ class CCBAM(nn.Module):
     def forward(self, x, pack: bool = False):
         """pack=True: also write the output's CL16 copy for a consuming joined conv's
         weight-grad (functional.cl16_put; training, fp32 only)."""
-        return _CCBAMFn.apply(x, self, bool(pack), *self.parameters())
+        # cl16_wanted reads the grad mode, which is off inside the Function's forward
+        return _CCBAMFn.apply(x, self, bool(pack) and F.cl16_wanted(x), *self.parameters())
 
     def forward_unfused(self, x):
         """The reference's op-by-op formulation (PyTorch device ops)."""

@@ -10,6 +10,7 @@ innermost, [2][B][H][W][C]. Layout and producers are checked bit-exactly against
 torch restatement; the weight-grad against its fp32-operand form (bit-identical
 when both sources share one bound) and against fp64 (each source its own bound).
 """
+import copy
 import ctypes
 
 import numpy as np
@@ -56,6 +57,7 @@ def test_cbn_forward_writes_cl16_copy(gpu_device):
     from sehip.complex_nn import ComplexBatchNorm2d
     torch.manual_seed(1)
     bn = ComplexBatchNorm2d(128).cuda().train()
+    bn2 = copy.deepcopy(bn)
     x = torch.randn(3, 128, 11, 41, device=gpu_device, requires_grad=True) * 2 + 0.5
     n0 = F.CL16_CALLS[0]
     y = bn.forward_act(x, F.ACT_LEAKY, 0.2, pack=True)
@@ -65,7 +67,6 @@ def test_cbn_forward_writes_cl16_copy(gpu_device):
     got = buf.view(2, 3, 11, 41, 128)
     assert torch.equal(got, _cl16_ref(y.detach(), ya))
     # and the fp32 y is the one the kernel without the copy writes
-    bn2 = ComplexBatchNorm2d(128).cuda().train()
     assert torch.equal(y.detach(), bn2.forward_act(x, F.ACT_LEAKY, 0.2).detach())
 
 
