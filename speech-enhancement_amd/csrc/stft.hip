@@ -1028,8 +1028,11 @@ __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs
     const int n = lane + it * kWave;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int u = (t0 + 2 * w + h) * a.hop + min(n, a.win - 1);
-      ga[it][h] = a.out_len > 0 ? ldx<LP>(a.in, go + min(max(u - a.offset, 0), a.out_len - 1), a.dt) : 0.f;
+      ga[it][h] = 0.f;
+      if (it * kWave < a.win && a.out_len > 0) {   // wave-uniform: frame samples n < win only
+        const int u = (t0 + 2 * w + h) * a.hop + min(n, a.win - 1);
+        ga[it][h] = ldx<LP>(a.in, go + min(max(u - a.offset, 0), a.out_len - 1), a.dt);
+      }
     }
   }
   for (int i = threadIdx.x; i < N; i += TPB) {

@@ -940,6 +940,30 @@ def complex_batch_norm_head(x, wrr, wri, wii, br, bi, w_head, running, nbt, trai
 # --------------------------------------------------------------------------
 # ConvSTFT / ConviSTFT — se_stft_* / se_istft_* (stft.hip)
 # --------------------------------------------------------------------------
+def stft_launch(x, out0, out1, window, twiddle, win, hop, nfft, center, mag_phase) -> None:
+    """se_stft_fwd into preallocated outputs (the autograd Function's launch; bench bursts)."""
+    b, length = x.shape
+    N.check(N.lib().se_stft_fwd(x.data_ptr(), out0.data_ptr(), N.ptr(out1), b, length, win, hop, nfft,
+                                int(center), int(mag_phase), window.data_ptr(), twiddle.data_ptr(),
+                                N.dtype_code(x), N.stream_of(x)), "se_stft_fwd")
+
+
+def istft_launch(spec, out, window, twiddle, win, hop, nfft, offset, out_len) -> None:
+    """se_istft_fwd into a preallocated [B, out_len] output."""
+    b, _, t = spec.shape
+    N.check(N.lib().se_istft_fwd(spec.data_ptr(), out.data_ptr(), b, t, win, hop, nfft, offset, out_len,
+                                 window.data_ptr(), twiddle.data_ptr(), N.dtype_code(spec),
+                                 N.stream_of(spec)), "se_istft_fwd")
+
+
+def istft_bwd_launch(gout, gspec, window, twiddle, win, hop, nfft, offset, out_len) -> None:
+    """se_istft_bwd (the ConviSTFT adjoint) into a preallocated [B, nfft+2, T] gradient."""
+    b, _, t = gspec.shape
+    N.check(N.lib().se_istft_bwd(gout.data_ptr(), gspec.data_ptr(), b, t, win, hop, nfft, offset, out_len,
+                                 window.data_ptr(), twiddle.data_ptr(), N.dtype_code(gout),
+                                 N.stream_of(gout)), "se_istft_bwd")
+
+
 class _Stft(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, window, twiddle, win, hop, nfft, center, mag_phase):
@@ -960,9 +984,7 @@ class _Stft(torch.autograd.Function):
             out0 = torch.empty((b, 2 * half, t), device=x.device, dtype=x.dtype)
             out1 = None
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(lib.se_stft_fwd(x.data_ptr(), out0.data_ptr(), N.ptr(out1), b, length, win, hop, nfft,
-                                int(center), int(mag_phase), window.data_ptr(), twiddle.data_ptr(), dt,
-                                N.stream_of(x)), "se_stft_fwd")
+        stft_launch(x, out0, out1, window, twiddle, win, hop, nfft, center, mag_phase)
         if t0 is not None:   # algorithmic bytes: read the wav once, write the spectrum once
             _TIMER.end("stft_fwd", t0, 0.0, x.element_size() * (x.numel() + out0.numel()
                                                                  + (out1.numel() if mag_phase else 0)))
@@ -991,9 +1013,7 @@ class _Istft(torch.autograd.Function):
             raise RuntimeError(f"sehip ConviSTFT: expected {nfft + 2} spectrum rows, got {rows}")
         out = torch.empty((b, out_len), device=spec.device, dtype=spec.dtype)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(N.lib().se_istft_fwd(spec.data_ptr(), out.data_ptr(), b, t, win, hop, nfft, offset,
-                                     out_len, window.data_ptr(), twiddle.data_ptr(), dt,
-                                     N.stream_of(spec)), "se_istft_fwd")
+        istft_launch(spec, out, window, twiddle, win, hop, nfft, offset, out_len)
         if t0 is not None:
             _TIMER.end("istft_fwd", t0, 0.0, spec.element_size() * (spec.numel() + out.numel()))
         ctx.save_for_backward(window, twiddle)
@@ -1007,9 +1027,7 @@ class _Istft(torch.autograd.Function):
         gout = gout.contiguous()
         gspec = torch.empty((b, nfft + 2, t), device=gout.device, dtype=gout.dtype)
         t0 = _TIMER.begin() if _TIMER else None
-        N.check(N.lib().se_istft_bwd(gout.data_ptr(), gspec.data_ptr(), b, t, win, hop, nfft,
-                                     offset, out_len, window.data_ptr(), twiddle.data_ptr(), N.dtype_code(gout),
-                                     N.stream_of(gout)), "se_istft_bwd")
+        istft_bwd_launch(gout, gspec, window, twiddle, win, hop, nfft, offset, out_len)
         if t0 is not None:
             _TIMER.end("istft_bwd", t0, 0.0, gout.element_size() * (gout.numel() + gspec.numel()))
         return gspec, None, None, None, None, None, None, None

@@ -14,14 +14,20 @@ st, ist = ConvSTFT(320, 160, 640).to(dev), ConviSTFT(320, 160, 640).to(dev)
 with torch.no_grad():
     spec = st(x)
 nbytes = 4 * (x.numel() + spec.numel())
-sr = spec.clone().requires_grad_(True)
-y = ist(sr)
-gy = torch.randn_like(y)
-# istft_bwd: autograd.grad (no .grad accumulation) runs se_istft_bwd alone
+from sehip import functional as F  # noqa: E402
+# launched straight into preallocated buffers, as bench.py's bursts (no autograd / allocation)
+x2 = x[:, 0].contiguous()
+wav = ist(spec)
+off = ist.pad if ist.center else 0
+wav_buf, gspec, gy = torch.empty_like(wav), torch.empty_like(spec), torch.randn_like(wav)
 with torch.no_grad():
     only = sys.argv[1] if len(sys.argv) > 1 else None
-    for name, f in (("stft_fwd", lambda: st(x)), ("istft_fwd", lambda: ist(spec)),
-                    ("istft_bwd", lambda: torch.autograd.grad(y, sr, gy, retain_graph=True))):
+    for name, f in (("stft_fwd", lambda: F.stft_launch(x2, spec, None, st._win, st._tw, st.window_size, st.hop_size,
+                                                       st.fft_size, st.center, False)),
+                    ("istft_fwd", lambda: F.istft_launch(spec, wav_buf, ist._win, ist._tw, ist.window_size,
+                                                         ist.hop_size, ist.fft_size, off, wav.shape[-1])),
+                    ("istft_bwd", lambda: F.istft_bwd_launch(gy, gspec, ist._win, ist._tw, ist.window_size,
+                                                             ist.hop_size, ist.fft_size, off, wav.shape[-1]))):
         if only and name != only:
             continue
         for _ in range(5):
