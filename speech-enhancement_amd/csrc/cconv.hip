@@ -503,16 +503,25 @@ constexpr int kScC = 8, kScR = 4, kScRows = 4 * kScR;   // 8 channels, 16 x 64 o
 constexpr int kScPitch = kStW + 8;                        // LDS row: 64 columns + a halo <= 8
 template <int NO, int NTH, int SD>
 __global__ void __launch_bounds__(kThreads)
-gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw) {
+gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, int cpg, float* part) {
   constexpr int TH = kScRows + NTH - 1, WIN = kScR + NTH - 1;
   constexpr int tw = kScPitch, plane = TH * tw, chunk = kScC * plane;   // compile-time indexing
   extern __shared__ float sx[];   // [kScC][TH][kScPitch]
-  const int b = blockIdx.z;
+  // blockIdx.z = (item, channel group): the group's channels [cg0, cg1)
+  const int b = blockIdx.z / ngrp, grp = blockIdx.z - b * ngrp;
+  const int cg0 = grp * cpg, cg1 = min(a.Cg, cg0 + cpg);
   const int qh0 = blockIdx.y * kScRows, qw0 = blockIdx.x * kStW;
-  const long long HiWi = (long long)a.Hi * a.Wi;
-  const long long xb = (long long)b * a.Cg * HiWi;
+  constexpr int ES = SD ? 2 : 4;
+  const int HiWi = a.Hi * a.Wi;   // the host checks Cg * Hi * Wi * ES < 2^31
+  // 32-bit offsets into the item's planes through a buffer resource (out-of-range
+  // offset: reads 0); 16-bit elements are staged as raw bits and converted when they
+  // are written to LDS, so no convert waits on a load in flight
+  const unsigned long long xa = (unsigned long long)((const char*)a.X + (long long)b * a.Cg * HiWi * ES);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa >> 32)) << 32) |
+              __builtin_amdgcn_readfirstlane((unsigned)xa)), (short)0, 0x7FFFFFFF, 0x00020000);
   constexpr int PF = (chunk + kThreads - 1) / kThreads;
-  float pf[PF];
+  typename StageT<SD>::T pf[PF];
   auto fetch = [&](int c0) __attribute__((always_inline)) {
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
@@ -520,10 +529,16 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw) {
       const int c = i / plane, rr = i - c * plane;
       const int r = rr / tw, col = rr - r * tw;
       const int hi = qh0 + h0 + r, wi = qw0 + w0 + col;
-      const bool ok = (chunk % kThreads == 0 || i < chunk) && c0 + c < a.Cg && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
-      const float v = ld_s<SD>(a.X, ok ? xb + (long long)(c0 + c) * HiWi + (long long)hi * a.Wi + wi : 0);
-      pf[j] = ok ? v : 0.f;
+      const bool ok = (chunk % kThreads == 0 || i < chunk) && c0 + c < cg1 && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
+      const int vo = ok ? ((c0 + c) * HiWi + hi * a.Wi + wi) * ES : (int)0x80000000;
+      if constexpr (SD == 0) pf[j] = bload<0>(rx, vo, 0);
+      else pf[j] = bload_raw16(rx, vo, 0);
     }
+  };
+  auto to_f32 = [](typename StageT<SD>::T v) __attribute__((always_inline)) {
+    if constexpr (SD == 0) return v;
+    else if constexpr (SD == 1) return __builtin_bit_cast(float, v << 16);
+    else return (float)__builtin_bit_cast(_Float16, (unsigned short)v);
   };
   const int lc = threadIdx.x & 63, r0 = (threadIdx.x >> 6) * kScR;
   float acc[kScR][NO];
@@ -531,17 +546,17 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw) {
   for (int r = 0; r < kScR; ++r)
 #pragma unroll
     for (int n = 0; n < NO; ++n) acc[r][n] = 0.f;
-  fetch(0);
-  for (int c0 = 0; c0 < a.Cg; c0 += kScC) {
+  fetch(cg0);
+  for (int c0 = cg0; c0 < cg1; c0 += kScC) {
     __syncthreads();   // the previous chunk is consumed
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int i = threadIdx.x + j * kThreads;
-      if (chunk % kThreads == 0 || i < chunk) sx[i] = pf[j];
+      if (chunk % kThreads == 0 || i < chunk) sx[i] = to_f32(pf[j]);
     }
     __syncthreads();
-    if (c0 + kScC < a.Cg) fetch(c0 + kScC);
-    const int nc = min(kScC, a.Cg - c0);
+    if (c0 + kScC < cg1) fetch(c0 + kScC);
+    const int nc = min(kScC, cg1 - c0);
     for (int c = 0; c < nc; ++c) {
       for (int bw = 0; bw < ntw; ++bw) {
         const float* src = sx + c * plane + r0 * tw + lc + a.toffw[bw] - w0;
@@ -562,18 +577,42 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw) {
       }
     }
   }
-  const long long HoWo = (long long)a.Ho * a.Wo;
+  const long long HoWo = (long long)a.Ho * a.Wo, QQ = (long long)a.Qh * a.Qw;
   const int qw = qw0 + lc;
   if (qw >= a.Qw) return;
 #pragma unroll
   for (int r = 0; r < kScR; ++r) {
     const int qh = qh0 + r0 + r;
     if (qh >= a.Qh) break;
+    if (part) {   // channel groups: this group's partial sums, [grp][b][n][qh][qw]
+      const long long pb = ((long long)grp * (gridDim.z / ngrp) + b) * a.N * QQ + (long long)qh * a.Qw + qw;
+#pragma unroll
+      for (int n = 0; n < NO; ++n)
+        if (n < a.N) part[pb + n * QQ] = acc[r][n];
+      continue;
+    }
     const long long yb = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
 #pragma unroll
     for (int n = 0; n < NO; ++n)
       if (n < a.N) st_s<SD>(a.Y, yb + n * HoWo, acc[r][n] + (a.bias ? a.bias[n] : 0.f));
   }
+}
+
+// Y at the class's positions = bias + the channel groups' partial sums, added in group
+// order (deterministic). grid ceil(B * N * Qh * Qw / 256)
+template <int SD>
+__global__ void __launch_bounds__(kThreads)
+stencil_ch_reduce_kernel(const GatherArgs a, int ngrp, const float* __restrict__ part) {
+  const long long QQ = (long long)a.Qh * a.Qw, per = (long long)(a.M / QQ) * a.N * QQ;
+  const long long i = blockIdx.x * (long long)kThreads + threadIdx.x;
+  if (i >= per) return;
+  float v = 0.f;
+  for (int gi = 0; gi < ngrp; ++gi) v += part[gi * per + i];
+  const long long bn = i / QQ, r = i - bn * QQ;
+  const int n = (int)(bn % a.N);
+  const int qh = (int)(r / a.Qw), qw = (int)(r - (long long)qh * a.Qw);
+  const long long HoWo = (long long)a.Ho * a.Wo;
+  st_s<SD>(a.Y, bn * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw), v + (a.bias ? a.bias[n] : 0.f));
 }
 
 // ---------------------------------------------------------------------------
@@ -1267,16 +1306,34 @@ static inline int ldw_for(int N, int math = SE_MATH_F32) {
 // (4) or the three-way split (6)
 constexpr size_t kWpBytesPerElem = 6;
 
-static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N, int math = SE_MATH_F32) {
+// Channel groups of the chunked stencil (gather_stencil_ch_kernel) for a class of
+// B x Qh x Qw outputs over Cg channels: enough workgroups to fill the chip (a B = 16
+// DCUNet final layer has ~600 tiles), each group >= 4 chunks of kScC channels.
+static int stencil_ch_groups(int B, int Qh, int Qw, int Cg) {
+  const long long tiles = (long long)se::ceil_div(Qw, kStW) * se::ceil_div(Qh, kScRows) * B;
+  int g = (int)std::max<long long>(1, std::min<long long>(8, 2048 / std::max<long long>(tiles, 1)));
+  g = std::min(g, std::max(1, Cg / (4 * kScC)));
+  const int cpg = round_up(se::ceil_div(Cg, g), kScC);
+  return se::ceil_div(Cg, cpg);
+}
+
+static size_t gather_ws_bytes(const std::vector<ClassPlan>& cls, int N, int math = SE_MATH_F32, int B = 0,
+                              int Cg = 0) {
   size_t bytes = 0;
-  (void)math;   // sized for the wider of the fp32 and bf16 tilings: a conv's passes may differ in math
+  (void)math;   // sized for the wider of the fp32 and bf16 tilings (and the one-term 64-k
+                // rounding of Kp): a conv's passes may differ in math
   const int ldw = std::max(ldw_for(N, SE_MATH_F32), ldw_for(N, SE_MATH_BF16));
+  size_t part = 0;
   for (const auto& c : cls) {
-    bytes += (size_t)c.Kp * ldw * kWpBytesPerElem;
-    bytes += (size_t)c.Kp * sizeof(int4);
+    bytes += (size_t)round_up(c.Kp, 2 * kBK) * ldw * kWpBytesPerElem;
+    bytes += (size_t)round_up(c.Kp, 2 * kBK) * sizeof(int4);
+    if (N <= 4 && Cg > 4 && B > 0) {   // the chunked stencil's channel-group partials
+      const int gr = stencil_ch_groups(B, c.h.Q, c.w.Q, Cg);
+      if (gr > 1) part = std::max(part, (size_t)gr * B * N * c.h.Q * c.w.Q * sizeof(float) + 256);
+    }
   }
   bytes += (size_t)round_up(N, 128) * sizeof(float);  // bias_full
-  return bytes + kZeroBytes + kAmaxBytes + 512;
+  return bytes + part + kZeroBytes + kAmaxBytes + 512;
 }
 
 constexpr int kSmallWgradN = 8;   // N at or below: wgrad_smalln_kernel
@@ -1433,7 +1490,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   const int Cg = (pass == kFwd) ? g.Ci : g.Co;
   const int Hi = (pass == kFwd) ? g.Hi : g.Ho, Wi = (pass == kFwd) ? g.Wi : g.Wo;
   const int Ho = (pass == kFwd) ? g.Ho : g.Hi, Wo = (pass == kFwd) ? g.Wo : g.Wi;
-  if (ws_bytes < gather_ws_bytes(cls, N, g.math)) return SE_E_WORKSPACE;
+  if (ws_bytes < gather_ws_bytes(cls, N, g.math, g.B, Cg)) return SE_E_WORKSPACE;
   // a prepared split-fp16 image carries the caller's weight bound, which the GEMM unscales by
   if (pass == kData && g.data_w && g.math == SE_MATH_F16X3 && N > 64 && !g.w_amax) return SE_E_ARG;
   // CL16 operands are read by the weight-grad only
@@ -1549,17 +1606,26 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
       for (int q = 1; q < ntw; ++q) { wmin = std::min(wmin, c.w.off[q]); wmax = std::max(wmax, c.w.off[q]); }
       const int hmin = c.h.off[0] - (nth - 1);   // the window's first input row offset
       const bool stencil_ch = !jn && ldw <= 4 && Cg > 4 && c.h.s == 1 && c.w.s == 1 && hdesc &&
+                              (long long)Cg * Hi * Wi * (g.sd == SE_DTYPE_F32 ? 4 : 2) < (1ll << 31) &&
                               wmax - wmin <= kScPitch - kStW && !env_flag_off("SEHIP_STENCIL");
       if (stencil_ch) {
         a.ntaps = c.taps.n;
         for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }
-        const dim3 sgrid(se::ceil_div(c.w.Q, kStW), se::ceil_div(c.h.Q, kScRows), g.B);
+        // channel groups write partials into the workspace's tail, summed by the reduce pass
+        const int ngrp = stencil_ch_groups(g.B, c.h.Q, c.w.Q, Cg);
+        const int cpg = round_up(se::ceil_div(Cg, ngrp), kScC);
+        float* part = nullptr;
+        if (ngrp > 1) {
+          const size_t need = (size_t)ngrp * g.B * N * c.h.Q * c.w.Q * sizeof(float);
+          part = (float*)align256((char*)ws + ws_bytes - need - 256);
+        }
+        const dim3 sgrid(se::ceil_div(c.w.Q, kStW), se::ceil_div(c.h.Q, kScRows), g.B * ngrp);
         const size_t shs = (size_t)kScC * (kScRows + nth - 1) * kScPitch * sizeof(float);
 #define SE_STC(NO, NTH)                                                                                   \
   do {                                                                                                    \
-    if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 1>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw); \
-    else if (g.sd == SE_DTYPE_F16) hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 2>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw); \
-    else hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 0>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw); \
+    if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 1>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw, ngrp, cpg, part); \
+    else if (g.sd == SE_DTYPE_F16) hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 2>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw, ngrp, cpg, part); \
+    else hipLaunchKernelGGL((gather_stencil_ch_kernel<NO, NTH, 0>), sgrid, dim3(kThreads), shs, st, a, hmin, wmin, ntw, ngrp, cpg, part); \
   } while (0)
 #define SE_STC_N(NTH) do { if (N <= 2) SE_STC(2, NTH); else SE_STC(4, NTH); } while (0)
         switch (nth) {
@@ -1571,6 +1637,13 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
 #undef SE_STC_N
 #undef SE_STC
         SE_LAUNCH_CHECK();
+        if (part) {
+          const dim3 rgrid(se::ceil_div((long long)g.B * N * c.h.Q * c.w.Q, kThreads));
+          if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL(stencil_ch_reduce_kernel<1>, rgrid, dim3(kThreads), 0, st, a, ngrp, part);
+          else if (g.sd == SE_DTYPE_F16) hipLaunchKernelGGL(stencil_ch_reduce_kernel<2>, rgrid, dim3(kThreads), 0, st, a, ngrp, part);
+          else hipLaunchKernelGGL(stencil_ch_reduce_kernel<0>, rgrid, dim3(kThreads), 0, st, a, ngrp, part);
+          SE_LAUNCH_CHECK();
+        }
         continue;
       }
       const size_t sh = (size_t)c.Kp * ldw * sizeof(float);
@@ -1735,8 +1808,8 @@ extern "C" int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out
 extern "C" size_t se_conv2d_workspace_size(const se_conv2d_desc* d) {
   ConvGeom g;
   if (geom_of(d, g)) return 0;
-  size_t a = gather_ws_bytes(plan_pass(g, kFwd), g.Co, g.math);
-  size_t b = gather_ws_bytes(plan_pass(g, kData), g.Ci, g.math);
+  size_t a = gather_ws_bytes(plan_pass(g, kFwd), g.Co, g.math, g.B, g.Ci);
+  size_t b = gather_ws_bytes(plan_pass(g, kData), g.Ci, g.math, g.B, g.Co);
   size_t c = wgrad_ws_bytes(plan_wgrad(g));
   {   // the weight-grad pass may run in another math than the forward (per-pass modes)
     ConvGeom g2 = g;

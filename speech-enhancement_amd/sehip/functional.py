@@ -227,10 +227,11 @@ CL16_CALLS = [0, 0]   # [copies written, weight-grads that read them] (tests)
 
 def cl16_wanted(x: torch.Tensor) -> bool:
     """Whether a producer should write the CL16 copy of its fp32 output x: a split-fp16
-    weight-grad will read it (gradients enabled, weight pass in f16x3). SEHIP_CL16=0
-    turns the copies off (the weight-grads then split fp32 in the loop; A/B and tests)."""
+    weight-grad will read it (gradients enabled, weight pass in f16x3) and SEHIP_CL16=1.
+    Off by default: at the FRCRN bench step the copies cost their producers more than the
+    weight-grads gain (110 vs 102 ms per step, same box)."""
     return (x.is_cuda and x.dtype == torch.float32 and torch.is_grad_enabled()
-            and _CONV_MATH["weight"] == F16X3 and os.environ.get("SEHIP_CL16", "1") != "0")
+            and _CONV_MATH["weight"] == F16X3 and os.environ.get("SEHIP_CL16", "0") == "1")
 
 
 def new_cl16(x: torch.Tensor) -> torch.Tensor:

@@ -1,5 +1,6 @@
 # CL16 tests, then a same-box A/B of the CL16 weight-grad operands (default vs SEHIP_CL16=0,
-# alternating), then the configs-2/3 profiles with PMC (gpu_cfg_prof.sh):
+# alternating), then the configs-2/3 profiles with PMC (gpu_cfg_prof.sh) and the STFT
+# micro with its SQ counters (pmc_stft.sh):
 #   gpurun --timeout 1200 -- bash tools/gpu_r4b.sh <tag>
 R=$GRAFT_REPO_ROOT
 TAG=$1
@@ -11,4 +12,5 @@ rc=$?; echo "pytest rc=$rc" >> $O/tests.log
 if [ $rc -gt 1 ]; then exit $rc; fi
 bash $R/tools/gpu_ab.sh ${TAG}_ab "SEHIP_CL16=0" "" "SEHIP_CL16=0" || exit $?
 bash $R/tools/gpu_cfg_prof.sh ${TAG}_cfg || exit $?
+bash $R/tools/pmc_stft.sh ${TAG}_stft || exit $?
 exit $rc

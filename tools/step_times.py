@@ -1,0 +1,28 @@
+"""Per-step wall time (synchronised) and allocator state of the FRCRN bench step, e.g. to
+see a slowdown that builds up over steps: python tools/step_times.py [steps]"""
+import os, sys, time
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "speech-enhancement_amd"))
+import torch
+from sehip import functional as SF
+from sehip.data import synthetic_pairs
+from sehip.models import FRCRN
+from sehip.train import make_optimizer, train_step
+
+steps = int(sys.argv[1]) if len(sys.argv) > 1 else 12
+dev = torch.device("cuda")
+torch.manual_seed(2023)
+model = FRCRN().to(dev).train()
+opt = make_optimizer(model)
+batches = [synthetic_pairs(64, 64000, seed=2023 + i, device=dev) for i in range(2)]
+print(f"SEHIP_CL16={os.environ.get('SEHIP_CL16', '1')}", flush=True)
+for i in range(steps):
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    noisy, clean = batches[i % 2]
+    train_step(model, opt, noisy, clean)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3
+    print(f"step {i:2d} {ms:8.1f} ms  alloc {torch.cuda.memory_allocated() / 2**30:6.2f} GiB  "
+          f"reserved {torch.cuda.memory_reserved() / 2**30:6.2f} GiB  cl16 entries {len(SF._CL16)} "
+          f"amax entries {len(SF._AMAX)}", flush=True)
