@@ -336,6 +336,15 @@ __device__ __forceinline__ int reflect_index(int i, int L) {
 }
 
 __device__ __forceinline__ int floor_div(int a, int b) { return (a >= 0) ? a / b : -((-a + b - 1) / b); }
+// floor(a / d) for 0 <= a < 2^22 from a float reciprocal rd = 1 / d, corrected by one
+// step either way (the product is off by less than one): a few VALU instead of the
+// ~40 of an integer division, in the per-sample overlap-add loops
+__device__ __forceinline__ int fdiv_nn(int a, int d, float rd) {
+  int q = (int)((float)a * rd);
+  q -= q * d > a ? 1 : 0;
+  q += (q + 1) * d <= a ? 1 : 0;
+  return q;
+}
 __device__ __forceinline__ int ceil_div_i(int a, int b) { return -floor_div(-a, b); }
 
 // Unpack two packed real-FFT results (pair j) and store rows k = 0..N/2 of frames
@@ -522,6 +531,8 @@ template <int N, int W, bool LP>
 __device__ __forceinline__ void wv_unpack_store(const float2* A, int t0, int T, int b, void* out0, void* out1,
                                                 int mag_phase, int dt) {
   constexpr int NP = wv_stride<N>(), TPB = kWave * W, half = N / 2 + 1, FT = 2 * W;
+  // offsets from the utterance's rows (32-bit: (N + 2) T elements per utterance)
+  const long long ub = (long long)b * (mag_phase ? half : 2 * half) * T;
   for (int idx = threadIdx.x; idx < half * FT; idx += TPB) {
     const int k = idx / FT, f = idx - k * FT;
     const int t = t0 + f;
@@ -538,12 +549,19 @@ __device__ __forceinline__ void wv_unpack_store(const float2* A, int t0, int T, 
       im = -0.5f * (zk.x - zc.x);
     }
     im += 0.f;   // -0 -> +0 (atan2 branch cut)
+    const int o = k * T + t;
     if (!mag_phase) {
-      stx<LP>(out0, ((long long)b * (2 * half) + k) * T + t, re, dt);
-      stx<LP>(out0, ((long long)b * (2 * half) + half + k) * T + t, im, dt);
+      if constexpr (!LP) {
+        float* op = static_cast<float*>(out0) + ub;
+        op[o] = re;
+        op[o + half * T] = im;
+      } else {
+        stx<LP>(out0, ub + o, re, dt);
+        stx<LP>(out0, ub + o + half * T, im, dt);
+      }
     } else {
-      stx<LP>(out0, ((long long)b * half + k) * T + t, sqrtf(re * re + im * im), dt);
-      stx<LP>(out1, ((long long)b * half + k) * T + t, atan2f(im, re), dt);
+      stx<LP>(out0, ub + o, sqrtf(re * re + im * im), dt);
+      stx<LP>(out1, ub + o, atan2f(im, re), dt);
     }
   }
 }
@@ -562,19 +580,35 @@ __global__ void __launch_bounds__(kWave * W) stft_fwd_wv_kernel(const StftArgs a
   const int t0 = tb * FT, ta = t0 + 2 * w, tbb = ta + 1;
   const long long xo = (long long)b * a.L;
   // the wave's two frames: loads for n < win only (the rest of the FFT input is
-  // zero), all issued before any is used
+  // zero), all issued before any is used. Frames clear of both signal ends (all but
+  // a few per utterance, wave-uniform) index the signal directly: 32-bit offsets from
+  // the utterance's base, no reflect
   constexpr int IT = (N + kWave - 1) / kWave;
   float ya[IT], yb[IT];
+  const int sa = ta * a.hop - a.pad;
+  if (!LP && sa >= 0 && tbb < a.T && sa + a.hop + a.win <= a.L) {
+    const float* xp = static_cast<const float*>(a.x) + xo + sa;
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
-    const int n = lane + it * kWave;
-    const bool ok = n < a.win;
-    const int nn = ok ? n : 0;
-    const float wv = ok ? a.window[nn] : 0.f;
-    const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
-    const float xb = ldx<LP>(a.x, xo + reflect_index(min(tbb, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
-    ya[it] = ta < a.T ? wv * xa : 0.f;
-    yb[it] = tbb < a.T ? wv * xb : 0.f;
+    for (int it = 0; it < IT; ++it) {
+      const int n = lane + it * kWave;
+      const bool ok = n < a.win;
+      const int nn = ok ? n : 0;
+      const float wv = ok ? a.window[nn] : 0.f;
+      ya[it] = wv * xp[nn];
+      yb[it] = wv * xp[a.hop + nn];
+    }
+  } else {
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int n = lane + it * kWave;
+      const bool ok = n < a.win;
+      const int nn = ok ? n : 0;
+      const float wv = ok ? a.window[nn] : 0.f;
+      const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+      const float xb = ldx<LP>(a.x, xo + reflect_index(min(tbb, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+      ya[it] = ta < a.T ? wv * xa : 0.f;
+      yb[it] = tbb < a.T ? wv * xb : 0.f;
+    }
   }
   for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
   float2* Aw = A + w * NP;
@@ -938,9 +972,15 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
     const int idx = threadIdx.x + it * TPB;
     const int k = min(idx / P, half - 1), j = idx % P;
     const int ta = min(t_lo + 2 * j, t_hi), tb = min(t_lo + 2 * j + 1, t_hi);
-    const long long re = so + (long long)k * a.T, im = so + (long long)(half + k) * a.T;
-    ga[it] = make_float2(ldx<LP>(a.in, re + ta, a.dt), ldx<LP>(a.in, im + ta, a.dt));
-    gb[it] = make_float2(ldx<LP>(a.in, re + tb, a.dt), ldx<LP>(a.in, im + tb, a.dt));
+    const int re = k * a.T, im = (half + k) * a.T;   // 32-bit offsets within the utterance
+    if constexpr (!LP) {
+      const float* sp = static_cast<const float*>(a.in) + so;
+      ga[it] = make_float2(sp[re + ta], sp[im + ta]);
+      gb[it] = make_float2(sp[re + tb], sp[im + tb]);
+    } else {
+      ga[it] = make_float2(ldx<LP>(a.in, so + re + ta, a.dt), ldx<LP>(a.in, so + im + ta, a.dt));
+      gb[it] = make_float2(ldx<LP>(a.in, so + re + tb, a.dt), ldx<LP>(a.in, so + im + tb, a.dt));
+    }
   }
   for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
   // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
@@ -992,9 +1032,13 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
   }
   __syncthreads();
   const long long oo = (long long)b * a.out_len;
+  const float rh = 1.f / (float)a.hop;
   for (int s = s0 + threadIdx.x; s < s1; s += TPB) {
-    const int tb0 = max(t_lo, ceil_div_i(s - a.win + 1, a.hop));
-    const int tb1 = min(t_hi, floor_div(s, a.hop));
+    // covering frames [tb0, tb1] of sample s: s = q hop + r; frame t covers it while
+    // s - t hop < win, i.e. t >= q - floor((win - 1 - r) / hop) (none if r >= win)
+    const int q = fdiv_nn(s, a.hop, rh), m = a.win - 1 - (s - q * a.hop);
+    const int tb0 = max(t_lo, m < 0 ? q + 1 : q - fdiv_nn(m, a.hop, rh));
+    const int tb1 = min(t_hi, q);
     float acc = 0.f, cf = 0.f;
     for (int t = tb0; t <= tb1; ++t) {
       const int n = s - t * a.hop, f = t - t_lo;
@@ -1042,21 +1086,24 @@ __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs
   __syncthreads();
   float v[IT][2];
   float se2[2] = {0.f, 0.f}, so2[2] = {0.f, 0.f};
+  const float rh = 1.f / (float)a.hop;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int n = lane + it * kWave;
+    // frames t + d covering sample u = t hop + n: d in [d0, d1] (n < win), the same
+    // for both of the wave's frames up to the clip to [0, T - 1]
+    const int nc = min(n, a.win - 1);
+    const int d1 = fdiv_nn(nc, a.hop, rh), d0 = -fdiv_nn(a.win - 1 - nc, a.hop, rh);
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       float val = 0.f;
       const int t = t0 + 2 * w + h;
       const int u = t * a.hop + n;
       if (n < a.win && t < a.T && u >= a.offset && u < a.offset + a.out_len) {
-        // OLA normaliser at u (window^2 summed over covering frames)
-        const int tb0 = max(0, ceil_div_i(u - a.win + 1, a.hop));
-        const int tb1 = min(a.T - 1, floor_div(u, a.hop));
+        // OLA normaliser at u (window^2 summed over covering frames, in frame order)
         float cf = 0.f;
-        for (int tt = tb0; tt <= tb1; ++tt) {
-          const float ww = swin[u - tt * a.hop];
+        for (int d = max(d0, -t); d <= min(d1, a.T - 1 - t); ++d) {
+          const float ww = swin[n - d * a.hop];
           cf += ww * ww;
         }
         val = swin[n] * ga[it][h] / (cf + 1e-8f);
