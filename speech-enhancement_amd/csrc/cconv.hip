@@ -499,6 +499,18 @@ gather_stencil_kernel(const GatherArgs a, int h0, int w0, int th, int tw) {
 // consecutive and descending (offh[a] = offh[0] - a, phase_dim), so the tap-row
 // index into that window is a compile-time constant. Weights are uniform (scalar
 // loads): Wp[(t * Cg + c) * ldw + n], t = a * ntw + b.
+#if SE_STC_DEBUG
+// bounds instrumentation of the chunked stencil (debug variant builds only): every
+// index is checked against its buffer and clamped into it; violations are counted
+// per kind with vector atomics and read back by se_debug_stencil_counts
+__device__ int g_stc_dbg[8];
+#define STC_CHECK(kind, idx, lim) \
+  do { if ((long long)(idx) < 0 || (long long)(idx) >= (long long)(lim)) atomicAdd(&g_stc_dbg[kind], 1); } while (0)
+#define STC_CLAMP(idx, lim) (max(0ll, min((long long)(idx), (long long)(lim) - 1)))
+#else
+#define STC_CHECK(kind, idx, lim) do { } while (0)
+#define STC_CLAMP(idx, lim) (idx)
+#endif
 constexpr int kScC = 8, kScR = 4, kScRows = 4 * kScR;   // 8 channels, 16 x 64 outputs
 constexpr int kScPitch = kStW + 8;                        // LDS row: 64 columns + a halo <= 8
 template <int NO, int NTH, int SD>
@@ -516,10 +528,13 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
   // 32-bit offsets into the item's planes through a buffer resource (out-of-range
   // offset: reads 0); 16-bit elements are staged as raw bits and converted when they
   // are written to LDS, so no convert waits on a load in flight
+  // (readfirstlane returns int: each half goes through unsigned before widening, or a
+  // low half >= 2^31 would sign-extend into the high half of the base)
   const unsigned long long xa = (unsigned long long)((const char*)a.X + (long long)b * a.Cg * HiWi * ES);
+  const unsigned xlo = __builtin_amdgcn_readfirstlane((unsigned)xa);
+  const unsigned xhi = __builtin_amdgcn_readfirstlane((unsigned)(xa >> 32));
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((unsigned long long)__builtin_amdgcn_readfirstlane((unsigned)(xa >> 32)) << 32) |
-              __builtin_amdgcn_readfirstlane((unsigned)xa)), (short)0, 0x7FFFFFFF, 0x00020000);
+      (void*)(((unsigned long long)xhi << 32) | xlo), (short)0, 0x7FFFFFFF, 0x00020000);
   constexpr int PF = (chunk + kThreads - 1) / kThreads;
   typename StageT<SD>::T pf[PF];
   auto fetch = [&](int c0) __attribute__((always_inline)) {
@@ -531,6 +546,7 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
       const int hi = qh0 + h0 + r, wi = qw0 + w0 + col;
       const bool ok = (chunk % kThreads == 0 || i < chunk) && c0 + c < cg1 && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
       const int vo = ok ? ((c0 + c) * HiWi + hi * a.Wi + wi) * ES : (int)0x80000000;
+      if (ok) STC_CHECK(0, vo, (long long)a.Cg * HiWi * ES);
       if constexpr (SD == 0) pf[j] = bload<0>(rx, vo, 0);
       else pf[j] = bload_raw16(rx, vo, 0);
     }
@@ -552,20 +568,22 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int i = threadIdx.x + j * kThreads;
-      if (chunk % kThreads == 0 || i < chunk) sx[i] = to_f32(pf[j]);
+      if (chunk % kThreads == 0 || i < chunk) { STC_CHECK(1, i, chunk); sx[STC_CLAMP(i, chunk)] = to_f32(pf[j]); }
     }
     __syncthreads();
     if (c0 + kScC < cg1) fetch(c0 + kScC);
     const int nc = min(kScC, cg1 - c0);
     for (int c = 0; c < nc; ++c) {
       for (int bw = 0; bw < ntw; ++bw) {
-        const float* src = sx + c * plane + r0 * tw + lc + a.toffw[bw] - w0;
+        const int sbase = c * plane + r0 * tw + lc + a.toffw[bw] - w0;
         float v[WIN];
 #pragma unroll
-        for (int i = 0; i < WIN; ++i) v[i] = src[i * tw];
+        for (int i = 0; i < WIN; ++i) { STC_CHECK(2, sbase + i * tw, chunk); v[i] = sx[STC_CLAMP(sbase + i * tw, chunk)]; }
 #pragma unroll
         for (int ah = 0; ah < NTH; ++ah) {
-          const float* wk = a.Wp + (long long)((ah * ntw + bw) * a.Cg + c0 + c) * a.ldw;
+          const long long wo = (long long)((ah * ntw + bw) * a.Cg + c0 + c) * a.ldw;
+          STC_CHECK(3, wo + NO - 1, (long long)a.Kp * a.ldw);
+          const float* wk = a.Wp + STC_CLAMP(wo, (long long)a.Kp * a.ldw - NO + 1);
           float w[NO];
 #pragma unroll
           for (int n = 0; n < NO; ++n) w[n] = wk[n];
@@ -588,15 +606,24 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
       const long long pb = ((long long)grp * (gridDim.z / ngrp) + b) * a.N * QQ + (long long)qh * a.Qw + qw;
 #pragma unroll
       for (int n = 0; n < NO; ++n)
-        if (n < a.N) part[pb + n * QQ] = acc[r][n];
+        if (n < a.N) { STC_CHECK(4, pb + n * QQ, (long long)gridDim.z * a.N * QQ); part[STC_CLAMP(pb + n * QQ, (long long)gridDim.z * a.N * QQ)] = acc[r][n]; }
       continue;
     }
     const long long yb = (long long)b * a.N * HoWo + (long long)(a.ph + a.Sh * qh) * a.Wo + (a.pw + a.Sw * qw);
 #pragma unroll
     for (int n = 0; n < NO; ++n)
-      if (n < a.N) st_s<SD>(a.Y, yb + n * HoWo, acc[r][n] + (a.bias ? a.bias[n] : 0.f));
+      if (n < a.N) {
+        STC_CHECK(5, yb + n * HoWo, (long long)(gridDim.z / ngrp) * a.N * HoWo);
+        st_s<SD>(a.Y, STC_CLAMP(yb + n * HoWo, (long long)(gridDim.z / ngrp) * a.N * HoWo), acc[r][n] + (a.bias ? a.bias[n] : 0.f));
+      }
   }
 }
+
+#if SE_STC_DEBUG
+extern "C" int se_debug_stencil_counts(int* out8) {
+  return hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_stc_dbg), 8 * sizeof(int)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 // Y at the class's positions = bias + the channel groups' partial sums, added in group
 // order (deterministic). grid ceil(B * N * Qh * Qw / 256)
