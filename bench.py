@@ -44,7 +44,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-in MFMA dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 / f16 MFMA dense peak (no sparsity)
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
 SR, SECONDS = 16000, 4
-PROFILE_STATS = os.path.join(ROOT, "profiles", "r3_bench_kernel_stats.csv")
+PROFILE_STATS = os.path.join(ROOT, "profiles", "r4_bench_kernel_stats.csv")
 
 # OpTimer tag -> (kernel instantiation as rocprof names it, launches per call, description).
 # The decoder's joined passes are one launch of one instantiation per call (the data-grad of
