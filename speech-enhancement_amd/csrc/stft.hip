@@ -1094,19 +1094,29 @@ __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs
     // for both of the wave's frames up to the clip to [0, T - 1]
     const int nc = min(n, a.win - 1);
     const int d1 = fdiv_nn(nc, a.hop, rh), d0 = -fdiv_nn(a.win - 1 - nc, a.hop, rh);
+    // OLA normaliser at u (window^2 summed over the covering frames, in frame order): the
+    // same for both frames unless a frame sits at a signal end (clipped range)
+    float cfi = 0.f;
+    for (int d = d0; d <= d1; ++d) {
+      const float ww = swin[n - d * a.hop];
+      cfi += ww * ww;
+    }
+    const float wn = swin[nc];
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       float val = 0.f;
       const int t = t0 + 2 * w + h;
       const int u = t * a.hop + n;
       if (n < a.win && t < a.T && u >= a.offset && u < a.offset + a.out_len) {
-        // OLA normaliser at u (window^2 summed over covering frames, in frame order)
-        float cf = 0.f;
-        for (int d = max(d0, -t); d <= min(d1, a.T - 1 - t); ++d) {
-          const float ww = swin[n - d * a.hop];
-          cf += ww * ww;
+        float cf = cfi;
+        if (t + d0 < 0 || t + d1 > a.T - 1) {
+          cf = 0.f;
+          for (int d = max(d0, -t); d <= min(d1, a.T - 1 - t); ++d) {
+            const float ww = swin[n - d * a.hop];
+            cf += ww * ww;
+          }
         }
-        val = swin[n] * ga[it][h] / (cf + 1e-8f);
+        val = wn * ga[it][h] / (cf + 1e-8f);
       }
       v[it][h] = val;
       if (n & 1) so2[h] += val; else se2[h] += val;
