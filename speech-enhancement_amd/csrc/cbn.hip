@@ -87,10 +87,18 @@ __device__ __forceinline__ void block_reduce_store(double (&v)[NS], double* out)
   }
 }
 
-__device__ __forceinline__ float act_grad(float y, int act, float slope) {
-  if (act == 1) return y > 0.f ? 1.f : slope;
-  if (act == 2) return y > 0.f ? 1.f : 0.f;
-  return 1.f;
+// act 0 none, 1 LeakyReLU(slope), 2 ReLU. Branch-free in the element: act and slope
+// are uniform, so the negative-side factor is a scalar select hoisted out of the loops
+// and an element costs one compare + select (a branch on act per element splits every
+// loop body into scalar-branch blocks).
+__device__ __forceinline__ float act_neg(int act, float slope) {
+  return act == 1 ? slope : (act == 2 ? 0.f : 1.f);
+}
+__device__ __forceinline__ float act_grad(float z, int act, float slope) {
+  return z > 0.f ? 1.f : act_neg(act, slope);
+}
+__device__ __forceinline__ float act_fwd(float z, int act, float slope) {
+  return z > 0.f ? z : (act == 2 ? 0.f : z * act_neg(act, slope));
 }
 
 // grid (Cc, P). Row r = (b, segment) of channel c; rows strided over P.
@@ -246,10 +254,8 @@ cbn_apply_kernel(const T* __restrict__ x, T* __restrict__ y, int C, int HW,
     const int i = base + u * kThreads;
     if (i < HW) {
       const float xr = fxr[u] - mr, xi = fxi[u] - mi;
-      float yr = zrr * xr + zri * xi + br;
-      float yi = zir * xr + zii * xi + bi;
-      if (act == 1) { yr = yr > 0.f ? yr : yr * slope; yi = yi > 0.f ? yi : yi * slope; }
-      else if (act == 2) { yr = fmaxf(yr, 0.f); yi = fmaxf(yi, 0.f); }
+      const float yr = act_fwd(zrr * xr + zri * xi + br, act, slope);
+      const float yi = act_fwd(zir * xr + zii * xi + bi, act, slope);
       y[offr + i] = (T)yr;
       y[offi + i] = (T)yi;
     }
@@ -278,12 +284,8 @@ cbn_apply4_kernel(const T* __restrict__ x, T* __restrict__ y, int C, int HW,
 #pragma unroll
   for (int u = 0; u < 4; ++u) {
     const float xr = xr4[u] - mr, xi = xi4[u] - mi;
-    float yr = zrr * xr + zri * xi + br;
-    float yi = zir * xr + zii * xi + bi;
-    if (act == 1) { yr = yr > 0.f ? yr : yr * slope; yi = yi > 0.f ? yi : yi * slope; }
-    else if (act == 2) { yr = fmaxf(yr, 0.f); yi = fmaxf(yi, 0.f); }
-    yr4[u] = yr;
-    yi4[u] = yi;
+    yr4[u] = act_fwd(zrr * xr + zri * xi + br, act, slope);
+    yi4[u] = act_fwd(zir * xr + zii * xi + bi, act, slope);
   }
   st4(y + offr + i, yr4);
   st4(y + offi + i, yi4);
@@ -326,10 +328,8 @@ cbn_apply_pk_kernel(const float* __restrict__ x, float* __restrict__ y, int C, i
     for (int u = 0; u < 8; ++u) {
       const float* k = scf + (c0 + u) * 8;
       const float xr = fr[u] - k[0], xi = fi[u] - k[1];
-      float vr = k[2] * xr + k[3] * xi + k[6];
-      float vi = k[4] * xr + k[5] * xi + k[7];
-      if (act == 1) { vr = vr > 0.f ? vr : vr * slope; vi = vi > 0.f ? vi : vi * slope; }
-      else if (act == 2) { vr = fmaxf(vr, 0.f); vi = fmaxf(vi, 0.f); }
+      const float vr = act_fwd(k[2] * xr + k[3] * xi + k[6], act, slope);
+      const float vi = act_fwd(k[4] * xr + k[5] * xi + k[7], act, slope);
       yr[u] = vr;
       yi[u] = vi;
       y[xb + (long long)(c0 + u) * HW] = vr;
@@ -388,12 +388,6 @@ __device__ __forceinline__ float head_gy(const HeadG& g, const float* wc, int C)
 #pragma unroll
   for (int o = 0; o < kHeadNO; ++o) s += wc[o * C * kHeadKW] * g.g0[o] + wc[o * C * kHeadKW + 1] * g.g1[o];
   return s;
-}
-
-__device__ __forceinline__ float act_fwd(float z, int act, float slope) {
-  if (act == 1) return z > 0.f ? z : z * slope;
-  if (act == 2) return fmaxf(z, 0.f);
-  return z;
 }
 
 // Backward moments: g = dL/dy * act'(z), xt = x - M, with dL/dy = gy (SRC 0),

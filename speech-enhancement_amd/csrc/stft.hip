@@ -478,6 +478,15 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
 #endif
 constexpr int kWvPairs = SE_STFT_WV_PAIRS;
 using se::kWave;
+// SE_STFT_WV_TWL: the twiddle table staged in LDS (1) or read through L1 (0)
+#ifndef SE_STFT_WV_TWL
+#define SE_STFT_WV_TWL 1
+#endif
+// SE_STFT_WV_FIT: pairs per block from the LDS budget of four blocks per CU (40 KiB),
+// at most kWvPairs, instead of kWvPairs
+#ifndef SE_STFT_WV_FIT
+#define SE_STFT_WV_FIT 0
+#endif
 
 // compiler barrier between a wave's LDS writes and its reads of other lanes' data:
 // LDS instructions of one wave execute in issue order, so only code motion must stop
@@ -522,6 +531,16 @@ __device__ __forceinline__ void wfft_pass(float2* a, const float2* __restrict__ 
 // Pair stride of the wave-local LDS image: N + 2 float2, so the unpack's reads of
 // W pairs at one bin fall in different banks
 template <int N> constexpr int wv_stride() { return N + 2; }
+// frame pairs per block of the wave-local kernels (the adjoint also keeps the window, N floats)
+template <int N> constexpr int wv_pairs() {
+  if constexpr (!SE_STFT_WV_FIT) {
+    return kWvPairs;
+  } else {
+    constexpr int fixed = (SE_STFT_WV_TWL ? N * 8 : 0) + N * 4;
+    constexpr int w = (40960 - fixed) / (wv_stride<N>() * 8);
+    return w < 1 ? 1 : (w > kWvPairs ? kWvPairs : w);
+  }
+}
 
 // Unpack the W packed pair results of a wave-local block (pair stride NP) into
 // frames t0 + 2j (even) and t0 + 2j + 1 (odd); lanes run along frames, so a store
@@ -568,12 +587,16 @@ __device__ __forceinline__ void wv_unpack_store(const float2* A, int t0, int T, 
 
 // ConvSTFT, wave-local FFT: W frame pairs per block (wave w: frames t0 + 2w, +1).
 // grid (ceil(T / 2W), B), 64 W threads
-template <int CN, int W = kWvPairs, bool LP = false>
+template <int CN, int W = wv_pairs<CN>(), bool LP = false>
 __global__ void __launch_bounds__(kWave * W) stft_fwd_wv_kernel(const StftArgs a) {
   constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W;
   constexpr int half = N / 2 + 1, FT = 2 * W;
   __shared__ __attribute__((aligned(16))) float2 A[W * NP];
+#if SE_STFT_WV_TWL
   __shared__ float2 stw[N];
+#else
+  const float2* stw = a.tw;
+#endif
   int tb, b;
   xcd_frame_block(tb, b);
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -610,7 +633,9 @@ __global__ void __launch_bounds__(kWave * W) stft_fwd_wv_kernel(const StftArgs a
       yb[it] = tbb < a.T ? wv * xb : 0.f;
     }
   }
+#if SE_STFT_WV_TWL
   for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
+#endif
   float2* Aw = A + w * NP;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
@@ -951,11 +976,15 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
 // block-wide; each wave transforms its pair, takes its frames' parity sums and
 // writes its two synthesis frames without a block barrier.
 // grid (ceil(out_len / (FT*hop)), B), FT = 2W - 1 - (win-1)/hop, 64 W threads
-template <int CN, int W = kWvPairs, bool LP = false>
+template <int CN, int W = wv_pairs<CN>(), bool LP = false>
 __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs a) {
   constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W, half = N / 2 + 1, P = W;
   __shared__ __attribute__((aligned(16))) float2 A[W * NP];
+#if SE_STFT_WV_TWL
   __shared__ float2 stw[N];
+#else
+  const float2* stw = a.tw;
+#endif
   int sb, b;
   xcd_frame_block(sb, b);
   const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
@@ -982,7 +1011,9 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
       gb[it] = make_float2(ldx<LP>(a.in, so + re + tb, a.dt), ldx<LP>(a.in, so + im + tb, a.dt));
     }
   }
+#if SE_STFT_WV_TWL
   for (int i = threadIdx.x; i < N; i += TPB) stw[i] = a.tw[i];
+#endif
   // conj(C[k]) with C = E_a + i E_b, E the Hermitian completion of X / 2
 #pragma unroll
   for (int it = 0; it < GT; ++it) {
@@ -1054,11 +1085,15 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
 // t0 + 2w, +1 (contiguous gradient samples: coalesced), applies G with its own
 // parity sums, transforms its pair; one barrier before the block-wide spectrum
 // store. grid (ceil(T / 2W), B), 64 W threads
-template <int CN, int W = kWvPairs, bool LP = false>
+template <int CN, int W = wv_pairs<CN>(), bool LP = false>
 __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs a) {
   constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W;
   __shared__ __attribute__((aligned(16))) float2 A[W * NP];
+#if SE_STFT_WV_TWL
   __shared__ float2 stw[N];
+#else
+  const float2* stw = a.tw;
+#endif
   __shared__ float swin[N];
   int tb, b;
   xcd_frame_block(tb, b);
@@ -1080,7 +1115,9 @@ __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs
     }
   }
   for (int i = threadIdx.x; i < N; i += TPB) {
+#if SE_STFT_WV_TWL
     stw[i] = a.tw[i];
+#endif
     swin[i] = i < a.win ? a.window[i] : 0.f;
   }
   __syncthreads();
@@ -1227,14 +1264,14 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
   if (SE_STFT_WV && ip_plan(nfft)) {
-    // wave-local FFT, kWvPairs frame pairs per block
-    const dim3 grid(se::ceil_div(T, 2 * kWvPairs), B);
+    // wave-local FFT, wv_pairs<nfft>() frame pairs per block
     hipStream_t st = se::as_stream(stream);
-    const dim3 blk(se::kWave * kWvPairs);
 #define SE_STFT_WVL(NF)                                                                                 \
     do {                                                                                                \
-      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((stft_fwd_wv_kernel<NF, kWvPairs, true>), grid, blk, 0, st, a);  \
-      else hipLaunchKernelGGL((stft_fwd_wv_kernel<NF, kWvPairs, false>), grid, blk, 0, st, a);          \
+      constexpr int W = wv_pairs<NF>();                                                                 \
+      const dim3 grid(se::ceil_div(T, 2 * W), B), blk(se::kWave * W);                                   \
+      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((stft_fwd_wv_kernel<NF, W, true>), grid, blk, 0, st, a); \
+      else hipLaunchKernelGGL((stft_fwd_wv_kernel<NF, W, false>), grid, blk, 0, st, a);                 \
     } while (0)
     switch (nfft) {
       case 640: SE_STFT_WVL(640); break;
@@ -1295,16 +1332,18 @@ extern "C" int se_istft_fwd(const void* spec, void* out, int B, int T, int win, 
   if (out_len == 0) return SE_OK;
   a.in = spec; a.out = out; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
   if (SE_STFT_WV && ip_plan(nfft)) {
-    // wave-local FFT, kWvPairs frame pairs per block
-    a.P = kWvPairs;
-    a.FT = 2 * kWvPairs - 1 - (win - 1) / hop;
+    // wave-local FFT, wv_pairs<nfft>() frame pairs per block
+    const int W = nfft == 640 ? wv_pairs<640>() : nfft == 512 ? wv_pairs<512>() : nfft == 400 ? wv_pairs<400>()
+                : nfft == 320 ? wv_pairs<320>() : wv_pairs<256>();
+    a.P = W;
+    a.FT = 2 * W - 1 - (win - 1) / hop;
     if (a.FT >= 1) {
-      const dim3 grid(se::ceil_div(out_len, a.FT * hop), B), blk(se::kWave * kWvPairs);
+      const dim3 grid(se::ceil_div(out_len, a.FT * hop), B), blk(se::kWave * W);
       hipStream_t st = se::as_stream(stream);
 #define SE_ISTFT_WVL(NF)                                                                                \
       do {                                                                                              \
-        if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, kWvPairs, true>), grid, blk, 0, st, a); \
-        else hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, kWvPairs, false>), grid, blk, 0, st, a);      \
+        if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, wv_pairs<NF>(), true>), grid, blk, 0, st, a); \
+        else hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, wv_pairs<NF>(), false>), grid, blk, 0, st, a);  \
       } while (0)
       switch (nfft) {
         case 640: SE_ISTFT_WVL(640); break;
@@ -1357,13 +1396,14 @@ extern "C" int se_istft_bwd(const void* gout, void* gspec, int B, int T, int win
   if (!gout || !gspec || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
   a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
   if (SE_STFT_WV && ip_plan(nfft)) {
-    // wave-local FFT, kWvPairs frame pairs per block
-    const dim3 grid(se::ceil_div(T, 2 * kWvPairs), B), blk(se::kWave * kWvPairs);
+    // wave-local FFT, wv_pairs<nfft>() frame pairs per block
     hipStream_t st = se::as_stream(stream);
 #define SE_ISTFT_BWD_WVL(NF)                                                                            \
     do {                                                                                                \
-      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_bwd_wv_kernel<NF, kWvPairs, true>), grid, blk, 0, st, a); \
-      else hipLaunchKernelGGL((istft_bwd_wv_kernel<NF, kWvPairs, false>), grid, blk, 0, st, a);        \
+      constexpr int W = wv_pairs<NF>();                                                                 \
+      const dim3 grid(se::ceil_div(T, 2 * W), B), blk(se::kWave * W);                                   \
+      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_bwd_wv_kernel<NF, W, true>), grid, blk, 0, st, a); \
+      else hipLaunchKernelGGL((istft_bwd_wv_kernel<NF, W, false>), grid, blk, 0, st, a);               \
     } while (0)
     switch (nfft) {
       case 640: SE_ISTFT_BWD_WVL(640); break;

@@ -1,14 +1,16 @@
 """ConvSTFT / ConviSTFT fwd+bwd at the FRCRN bench shape (B=64, 4 s, 320/160/640):
 per-launch time over a burst of back-to-back launches and GB/s of the algorithmic
 bytes (wav read once + spectrum written once). Optional argv[1]: run only the
-named op (stft_fwd / istft_fwd / istft_bwd), e.g. for a PMC pass."""
+named op (stft_fwd / istft_fwd / istft_bwd), e.g. for a PMC pass. STFT_B=n: batch n
+instead of 64 (per-launch time against the batch shows whether the grid's last round
+of workgroups dominates)."""
 import os, sys
 import torch
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "speech-enhancement_amd"))
 from sehip.conv_stft import ConvSTFT, ConviSTFT  # noqa: E402
 
 dev = torch.device("cuda")
-B, L = 64, 64000
+B, L = int(os.environ.get("STFT_B", "64")), 64000
 x = torch.randn(B, 1, L, device=dev) * 0.3
 st, ist = ConvSTFT(320, 160, 640).to(dev), ConviSTFT(320, 160, 640).to(dev)
 with torch.no_grad():
