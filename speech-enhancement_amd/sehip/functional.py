@@ -78,19 +78,6 @@ def _wgrad_stream(*inputs):
     return torch.cuda.stream(side)
 
 
-_CBN_FENCE = os.environ.get("SEHIP_CBN_FENCE", "0") == "1"
-
-
-def _fence_side(dev):
-    """(SEHIP_CBN_FENCE=1, experiment) make the current stream wait for the deferred
-    weight-grads queued so far, so the next HBM-bound pass runs with the whole chip."""
-    if _DEFER is None or not _CBN_FENCE:
-        return
-    side = _DEFER_STREAMS.get(dev)
-    if side is not None and side in _DEFER:
-        torch.cuda.current_stream(dev).wait_stream(side)
-
-
 class OpTimer:
     """Live per-entry-point timing with HIP events on the launching stream
     (used by bench.py for the roofline numbers). Disabled unless installed
@@ -753,7 +740,6 @@ class _ComplexBN(torch.autograd.Function):
         lib = N.lib()
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
         dxa = new_amax(x.device) if training and dt == 0 else None   # bound of max |dx| (the conv's dy)
-        _fence_side(x.device)
         t0 = _TIMER.begin() if _TIMER else None
         if gy2 is None:
             N.check(lib.se_cbn_bwd(gy.data_ptr(), None, x.data_ptr(), dx.data_ptr(), b, c, hw,
