@@ -28,6 +28,11 @@
 namespace {
 
 constexpr int kThreads = 256;
+// SE_CBN_FUSED_FIN: the backward finalize runs in the moments pass's last workgroup per
+// channel (fused_finalize) instead of its own launch
+#ifndef SE_CBN_FUSED_FIN
+#define SE_CBN_FUSED_FIN 1
+#endif
 constexpr int kSeg = 8192;   // elements of one (b, c) plane per reduction row
 constexpr int kSave = 20;    // floats of per-channel state (SE_CBN_SAVE_FLOATS)
 // save layout (S_DR / S_DI: max |x_r - Mr|, max |x_i - Mi| of the training batch)
@@ -390,6 +395,171 @@ __device__ __forceinline__ float head_gy(const HeadG& g, const float* wc, int C)
   return s;
 }
 
+// coef layout per channel (16 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi Br Bi pad
+constexpr int kCoef = 16;
+
+// One wave per channel, as cbn_finalize_kernel; the bound of max |dx| goes to
+// *dx_amax by atomicMax (zeroed by the backward moments pass).
+// HEAD: part holds the head's 8 weight-grad sums after the 6 moments (stride
+// 6 + kHeadNS); they are added in the same fixed order and written to dwh.
+// PR: the 7th sum (the PReLU weight's gradient, per channel) goes to pw_part[c]
+// chb != NULL: the channel's dx bound goes to chb[c] (the fused form below) instead.
+template <bool HEAD, typename T = float, bool PR = false>
+__device__ __forceinline__ void bwd_finalize_wave(int c, int lane, const double* part, const float* ext, int P,
+                                                  double count, int Cc, const float* save, const Ptr5& params,
+                                                  int affine, const MPtr5& dparams, int has_dparams, int training,
+                                                  float* coef, float* dx_amax, float* dwh, double* pw_part,
+                                                  float* chb) {
+  constexpr int NS = HEAD ? 6 + kHeadNS : (PR ? 7 : 6);
+  double sm[NS];
+#pragma unroll
+  for (int k = 0; k < NS; ++k) sm[k] = 0;
+  float gmr = 0.f, gmi = 0.f;
+  for (int p = lane; p < P; p += 64) {
+#pragma unroll
+    for (int k = 0; k < NS; ++k) sm[k] += part[((long long)c * P + p) * NS + k];
+    gmr = fmaxf(gmr, ext[((long long)c * P + p) * 2 + 0]);
+    gmi = fmaxf(gmi, ext[((long long)c * P + p) * 2 + 1]);
+  }
+#pragma unroll
+  for (int k = 0; k < NS; ++k) sm[k] = se::wave_sum(sm[k]);
+  gmr = se::wave_max(gmr);
+  gmi = se::wave_max(gmi);
+  if (lane != 0) return;
+  if constexpr (PR) pw_part[c] = sm[NS - 1];
+  if (HEAD) {   // dw[o, ch, k] at (o * C + ch) * KW + k, C = 2 Cc
+    const int C = 2 * Cc;
+#pragma unroll
+    for (int o = 0; o < kHeadNO; ++o)
+#pragma unroll
+      for (int k = 0; k < kHeadKW; ++k) {
+        dwh[((long long)o * C + c) * kHeadKW + k] = (float)sm[6 + 2 * o + k];
+        dwh[((long long)o * C + Cc + c) * kHeadKW + k] = (float)sm[10 + 2 * o + k];
+      }
+  }
+  {
+    const float* s = save + (long long)c * kSave;
+    const double urr = s[S_URR], uri = s[S_URI], uii = s[S_UII];
+    const double vrr = s[S_VRR], vri = s[S_VRI], vii = s[S_VII];
+    const double ss = s[S_S], tt = s[S_T];
+    // dZ = sum g xt^T
+    const double dz00 = sm[2], dz01 = sm[3], dz10 = sm[4], dz11 = sm[5];
+    double wrr = 1, wri = 0, wii = 1;
+    if (affine) { wrr = ldv<T>(params.p[0], c); wri = ldv<T>(params.p[1], c); wii = ldv<T>(params.p[2], c); }
+    double gurr, guri, guii;
+    if (affine) {
+      // dW = dZ U (U symmetric); W symmetric -> Wri collects both off-diagonals
+      const double dw00 = dz00 * urr + dz01 * uri, dw01 = dz00 * uri + dz01 * uii;
+      const double dw10 = dz10 * urr + dz11 * uri, dw11 = dz10 * uri + dz11 * uii;
+      if (has_dparams) {
+        stv<T>(dparams.p[0], c, (float)dw00);
+        stv<T>(dparams.p[1], c, (float)(dw01 + dw10));
+        stv<T>(dparams.p[2], c, (float)dw11);
+        stv<T>(dparams.p[3], c, (float)sm[0]);
+        stv<T>(dparams.p[4], c, (float)sm[1]);
+      }
+      // dU = W^T dZ = W dZ
+      gurr = wrr * dz00 + wri * dz10;
+      guii = wri * dz01 + wii * dz11;
+      guri = (wrr * dz01 + wri * dz11) + (wri * dz00 + wii * dz10);
+    } else {
+      gurr = dz00; guii = dz11; guri = dz01 + dz10;
+    }
+    const double zrr = s[S_ZRR], zri = s[S_ZRI], zir = s[S_ZIR], zii = s[S_ZII];
+    double gbr = 0, gbi = 0, grr = 0, gri = 0, gii = 0;
+    if (training) {
+      // back through U(Vrr, Vri, Vii) = closed form with s = sqrt(det), t = sqrt(tr + 2s)
+      const double r = 1.0 / (ss * tt);
+      const double g_r = gurr * (ss + vii) + guii * (ss + vrr) - guri * vri;
+      const double g_t = -g_r * r / tt;
+      const double g_s = (gurr + guii) * r - g_r * r / ss + g_t / tt;
+      const double g_tau = g_t / (2.0 * tt);
+      const double g_del = g_s / (2.0 * ss);
+      const double gvrr = guii * r + g_tau + g_del * vii;
+      const double gvii = gurr * r + g_tau + g_del * vrr;
+      const double gvri = -guri * r - 2.0 * vri * g_del;
+      grr = 2.0 * gvrr / count; gri = gvri / count; gii = 2.0 * gvii / count;
+      gbr = sm[0] / count; gbi = sm[1] / count;
+    }
+    float* o = coef + (long long)c * kCoef;
+    o[0] = (float)zrr; o[1] = (float)zir;   // dxr = Zrr g_r + Zir g_i
+    o[2] = (float)zri; o[3] = (float)zii;   // dxi = Zri g_r + Zii g_i
+    o[4] = (float)gbr; o[5] = (float)gbi;
+    o[6] = (float)grr; o[7] = (float)gri; o[8] = (float)gii;
+    o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = s[S_BR]; o[12] = s[S_BI];
+    o[13] = o[14] = o[15] = 0.f;
+    if (training && dx_amax) {   // dx = Z^T (g - gb) + Gamma (x - M), bounded term by term
+      const float gr = gmr + fabsf(o[4]);
+      const float gi = gmi + fabsf(o[5]);
+      const float dr = s[S_DR], di = s[S_DI];
+      const float br = fabsf(o[0]) * gr + fabsf(o[1]) * gi + fabsf(o[6]) * dr + fabsf(o[7]) * di;
+      const float bi = fabsf(o[2]) * gr + fabsf(o[3]) * gi + fabsf(o[7]) * dr + fabsf(o[8]) * di;
+      if (chb) chb[c] = fmaxf(br, bi) * 1.0001f;
+      else atomicMax(reinterpret_cast<unsigned*>(dx_amax), __float_as_uint(fmaxf(br, bi) * 1.0001f));
+    }
+  }
+}
+
+template <bool HEAD, typename T = float, bool PR = false>
+__global__ void __launch_bounds__(64 * kFinWaves)
+cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
+                        const float* save, Ptr5 params, int affine,
+                        MPtr5 dparams, int has_dparams, int training,
+                        float* coef, float* dx_amax, float* dwh, double* pw_part) {
+  const int lane = threadIdx.x & 63;
+  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
+  if (c >= Cc) return;
+  bwd_finalize_wave<HEAD, T, PR>(c, lane, part, ext, P, count, Cc, save, params, affine, dparams, has_dparams,
+                                 training, coef, dx_amax, dwh, pw_part, nullptr);
+}
+
+// The backward finalize inside the moments pass (SE_CBN_FUSED_FIN): the last of a
+// channel's P moments workgroups to arrive (an arrival count in the channel's save
+// pad word S_PAD0, zero from the forward finalize and reset to zero here) runs that
+// channel's finalize; the last channel to finish (a count in channel 0's S_PAD1) writes
+// the max of the per-channel dx bounds. One launch fewer per backward on the main
+// stream, whose small launches wait for CU slots beside the side-stream weight-grads.
+struct FinArgs {
+  int on;
+  double count;
+  Ptr5 params;
+  int affine;
+  MPtr5 dparams;
+  int has_dparams, training;
+  float* coef;
+  float* dwh;
+  double* pw_part;
+  float* chb;   // [Cc] per-channel dx bounds
+};
+
+template <bool HEAD, typename T, bool PR>
+__device__ __forceinline__ void fused_finalize(const FinArgs& fa, int c, int P, int Cc, const double* part,
+                                               const float* ext, const float* save, float* dx_amax) {
+  __shared__ unsigned s_last;
+  __threadfence();   // this workgroup's partial sums, before its arrival
+  __syncthreads();
+  unsigned* cnt = reinterpret_cast<unsigned*>(const_cast<float*>(save) + (long long)c * kSave + S_PAD0);
+  if (threadIdx.x == 0) s_last = atomicAdd(cnt, 1u) == (unsigned)(P - 1) ? 1u : 0u;
+  __syncthreads();
+  if (!s_last) return;
+  __threadfence();   // the other workgroups' partial sums
+  if (threadIdx.x < 64)
+    bwd_finalize_wave<HEAD, T, PR>(c, threadIdx.x, part, ext, P, fa.count, Cc, save, fa.params, fa.affine,
+                                   fa.dparams, fa.has_dparams, fa.training, fa.coef, dx_amax, fa.dwh, fa.pw_part,
+                                   dx_amax ? fa.chb : nullptr);
+  if (threadIdx.x != 0) return;
+  atomicExch(cnt, 0u);
+  if (!dx_amax) return;
+  __threadfence();   // chb[c]
+  unsigned* gcnt = reinterpret_cast<unsigned*>(const_cast<float*>(save) + S_PAD1);
+  if (atomicAdd(gcnt, 1u) != (unsigned)(Cc - 1)) return;
+  __threadfence();
+  float m = 0.f;
+  for (int i = 0; i < Cc; ++i) m = fmaxf(m, fa.chb[i]);
+  *dx_amax = m;
+  atomicExch(gcnt, 0u);
+}
+
 // Backward moments: g = dL/dy * act'(z), xt = x - M, with dL/dy = gy (SRC 0),
 // gy + gy2 (SRC 1: a forked output, se_cbn_bwd2, summed on the fly) or formed
 // from the head gradient (SRC 2, see HeadArgs; then the head's 8 weight-grad
@@ -401,7 +571,7 @@ __global__ void __launch_bounds__(kThreads)
 cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
                        const T* __restrict__ x, int B, int C, int HW, int P,
                        const float* __restrict__ save, int act, float slope, double* part, float* ext,
-                       float* dx_amax, HeadArgs hd, const T* pw) {
+                       float* dx_amax, HeadArgs hd, const T* pw, FinArgs fa) {
   static_assert(!PR || SRC != 2, "no PReLU on the head path");
   static_assert(SRC != 2 || sizeof(T) == 4, "the head path is fp32");
   constexpr int NS = SRC == 2 ? 6 + kHeadNS : (PR ? 7 : 6);
@@ -502,113 +672,9 @@ cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
     ext[((long long)c * P + p) * 2 + 0] = gmr;
     ext[((long long)c * P + p) * 2 + 1] = gmi;
   }
+  if (fa.on) fused_finalize<SRC == 2, T, PR>(fa, c, P, Cc, part, ext, save, dx_amax);
 }
 
-// coef layout per channel (16 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi Br Bi pad
-constexpr int kCoef = 16;
-
-// One wave per channel, as cbn_finalize_kernel; the bound of max |dx| goes to
-// *dx_amax by atomicMax (zeroed by the backward moments pass).
-// HEAD: part holds the head's 8 weight-grad sums after the 6 moments (stride
-// 6 + kHeadNS); they are added in the same fixed order and written to dwh.
-// PR: the 7th sum (the PReLU weight's gradient, per channel) goes to pw_part[c]
-template <bool HEAD, typename T = float, bool PR = false>
-__global__ void __launch_bounds__(64 * kFinWaves)
-cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double count, int Cc,
-                        const float* save, Ptr5 params, int affine,
-                        MPtr5 dparams, int has_dparams, int training,
-                        float* coef, float* dx_amax, float* dwh, double* pw_part) {
-  constexpr int NS = HEAD ? 6 + kHeadNS : (PR ? 7 : 6);
-  const int lane = threadIdx.x & 63;
-  const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
-  if (c >= Cc) return;
-  double sm[NS];
-#pragma unroll
-  for (int k = 0; k < NS; ++k) sm[k] = 0;
-  float gmr = 0.f, gmi = 0.f;
-  for (int p = lane; p < P; p += 64) {
-#pragma unroll
-    for (int k = 0; k < NS; ++k) sm[k] += part[((long long)c * P + p) * NS + k];
-    gmr = fmaxf(gmr, ext[((long long)c * P + p) * 2 + 0]);
-    gmi = fmaxf(gmi, ext[((long long)c * P + p) * 2 + 1]);
-  }
-#pragma unroll
-  for (int k = 0; k < NS; ++k) sm[k] = se::wave_sum(sm[k]);
-  gmr = se::wave_max(gmr);
-  gmi = se::wave_max(gmi);
-  if (lane != 0) return;
-  if constexpr (PR) pw_part[c] = sm[NS - 1];
-  if (HEAD) {   // dw[o, ch, k] at (o * C + ch) * KW + k, C = 2 Cc
-    const int C = 2 * Cc;
-#pragma unroll
-    for (int o = 0; o < kHeadNO; ++o)
-#pragma unroll
-      for (int k = 0; k < kHeadKW; ++k) {
-        dwh[((long long)o * C + c) * kHeadKW + k] = (float)sm[6 + 2 * o + k];
-        dwh[((long long)o * C + Cc + c) * kHeadKW + k] = (float)sm[10 + 2 * o + k];
-      }
-  }
-  {
-    const float* s = save + (long long)c * kSave;
-    const double urr = s[S_URR], uri = s[S_URI], uii = s[S_UII];
-    const double vrr = s[S_VRR], vri = s[S_VRI], vii = s[S_VII];
-    const double ss = s[S_S], tt = s[S_T];
-    // dZ = sum g xt^T
-    const double dz00 = sm[2], dz01 = sm[3], dz10 = sm[4], dz11 = sm[5];
-    double wrr = 1, wri = 0, wii = 1;
-    if (affine) { wrr = ldv<T>(params.p[0], c); wri = ldv<T>(params.p[1], c); wii = ldv<T>(params.p[2], c); }
-    double gurr, guri, guii;
-    if (affine) {
-      // dW = dZ U (U symmetric); W symmetric -> Wri collects both off-diagonals
-      const double dw00 = dz00 * urr + dz01 * uri, dw01 = dz00 * uri + dz01 * uii;
-      const double dw10 = dz10 * urr + dz11 * uri, dw11 = dz10 * uri + dz11 * uii;
-      if (has_dparams) {
-        stv<T>(dparams.p[0], c, (float)dw00);
-        stv<T>(dparams.p[1], c, (float)(dw01 + dw10));
-        stv<T>(dparams.p[2], c, (float)dw11);
-        stv<T>(dparams.p[3], c, (float)sm[0]);
-        stv<T>(dparams.p[4], c, (float)sm[1]);
-      }
-      // dU = W^T dZ = W dZ
-      gurr = wrr * dz00 + wri * dz10;
-      guii = wri * dz01 + wii * dz11;
-      guri = (wrr * dz01 + wri * dz11) + (wri * dz00 + wii * dz10);
-    } else {
-      gurr = dz00; guii = dz11; guri = dz01 + dz10;
-    }
-    const double zrr = s[S_ZRR], zri = s[S_ZRI], zir = s[S_ZIR], zii = s[S_ZII];
-    double gbr = 0, gbi = 0, grr = 0, gri = 0, gii = 0;
-    if (training) {
-      // back through U(Vrr, Vri, Vii) = closed form with s = sqrt(det), t = sqrt(tr + 2s)
-      const double r = 1.0 / (ss * tt);
-      const double g_r = gurr * (ss + vii) + guii * (ss + vrr) - guri * vri;
-      const double g_t = -g_r * r / tt;
-      const double g_s = (gurr + guii) * r - g_r * r / ss + g_t / tt;
-      const double g_tau = g_t / (2.0 * tt);
-      const double g_del = g_s / (2.0 * ss);
-      const double gvrr = guii * r + g_tau + g_del * vii;
-      const double gvii = gurr * r + g_tau + g_del * vrr;
-      const double gvri = -guri * r - 2.0 * vri * g_del;
-      grr = 2.0 * gvrr / count; gri = gvri / count; gii = 2.0 * gvii / count;
-      gbr = sm[0] / count; gbi = sm[1] / count;
-    }
-    float* o = coef + (long long)c * kCoef;
-    o[0] = (float)zrr; o[1] = (float)zir;   // dxr = Zrr g_r + Zir g_i
-    o[2] = (float)zri; o[3] = (float)zii;   // dxi = Zri g_r + Zii g_i
-    o[4] = (float)gbr; o[5] = (float)gbi;
-    o[6] = (float)grr; o[7] = (float)gri; o[8] = (float)gii;
-    o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = s[S_BR]; o[12] = s[S_BI];
-    o[13] = o[14] = o[15] = 0.f;
-    if (training && dx_amax) {   // dx = Z^T (g - gb) + Gamma (x - M), bounded term by term
-      const float gr = gmr + fabsf(o[4]);
-      const float gi = gmi + fabsf(o[5]);
-      const float dr = s[S_DR], di = s[S_DI];
-      const float br = fabsf(o[0]) * gr + fabsf(o[1]) * gi + fabsf(o[6]) * dr + fabsf(o[7]) * di;
-      const float bi = fabsf(o[2]) * gr + fabsf(o[3]) * gi + fabsf(o[7]) * dr + fabsf(o[8]) * di;
-      atomicMax(reinterpret_cast<unsigned*>(dx_amax), __float_as_uint(fmaxf(br, bi) * 1.0001f));
-    }
-  }
-}
 
 template <int SRC, typename T = float>   // dL/dy source as cbn_bwd_moments_kernel
 __global__ void __launch_bounds__(kThreads)
@@ -1205,26 +1271,40 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   float* xa = training ? dx_amax : nullptr;
   const dim3 mg(Cc, P), mb(kThreads);
   const bool pr = pw != nullptr;
+  FinArgs fa{};
+  fa.on = SE_CBN_FUSED_FIN;
+  fa.count = (double)B * HW;
+  fa.params = pp;
+  fa.affine = params ? 1 : 0;
+  fa.dparams = dp;
+  fa.has_dparams = dparams ? 1 : 0;
+  fa.training = training;
+  fa.coef = coef;
+  fa.dwh = dwh;
+  fa.pw_part = pwp;
+  fa.chb = ext + (size_t)Cc * P * 2;   // the ext region holds [Cc][P][4] floats, the backward uses 2
   if constexpr (sizeof(T) == 4) {
     if (src == 2)
       hipLaunchKernelGGL((cbn_bwd_moments_kernel<2, float>), mg, mb, 0, st, (const float*)gy, (const float*)gy2,
-                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr);
+                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr, fa);
   }
   if (src == 1 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw);
+                       slope, part, ext, xa, hd, pw, fa);
   else if (src == 1)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw);
+                       part, ext, xa, hd, pw, fa);
   else if (src == 0 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw);
+                       slope, part, ext, xa, hd, pw, fa);
   else if (src == 0)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw);
+                       part, ext, xa, hd, pw, fa);
   SE_LAUNCH_CHECK();
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
-  if (src == 2)
+  if (fa.on) {
+    // finalized inside the moments pass
+  } else if (src == 2)
     hipLaunchKernelGGL((cbn_bwd_finalize_kernel<true, T>), fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
                        params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, dwh, pwp);
   else if (pr)

@@ -1406,7 +1406,10 @@ static WgradPlan plan_wgrad(const ConvGeom& g) {
   // enough together for those re-reads to hit (dec5 weight-grad FETCH 40-48 ->
   // 29-32 GB, 14.3 -> 12.4 ms; FRCRN step 574 -> 588 utt/s, same box; 2048 and
   // 1024 measured slower).
-  constexpr int kWgradMps = 4096;
+#ifndef SE_WGRAD_MPS
+#define SE_WGRAD_MPS 4096
+#endif
+  constexpr int kWgradMps = SE_WGRAD_MPS;
   splits = std::max(splits, (w.M + kWgradMps - 1) / kWgradMps);
   const int max_by_m = std::max(1, w.M / 512);
   splits = std::min(splits, max_by_m);

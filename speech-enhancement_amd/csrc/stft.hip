@@ -491,15 +491,7 @@ using se::kWave;
 #ifndef SE_STFT_TWL_IBWD
 #define SE_STFT_TWL_IBWD 0
 #endif
-// SE_STFT_WV_REGS: the first FFT pass from registers where the plan allows (wfft_from_regs)
-#ifndef SE_STFT_WV_REGS
-#define SE_STFT_WV_REGS 1
-#endif
-// SE_STFT_WV_FIT: pairs per block from the LDS budget of four blocks per CU (40 KiB),
-// at most kWvPairs, instead of kWvPairs
-#ifndef SE_STFT_WV_FIT
-#define SE_STFT_WV_FIT 0
-#endif
+
 
 // compiler barrier between a wave's LDS writes and its reads of other lanes' data:
 // LDS instructions of one wave execute in issue order, so only code motion must stop
@@ -510,33 +502,9 @@ __device__ __forceinline__ void wave_lds_sync() {
 
 // In-place pass PS of the compiled plan over ONE sequence a[0..N) by one wave:
 // every lane reads all inputs of its butterflies, then writes all outputs.
-// Plan of the wave-local FFT: a first radix R0 that leaves N / R0 a multiple of 64, so
-// the inputs of a lane's first butterflies (n = j + q N / R0, j = lane + 64 i) are the
-// samples that lane already holds (n = lane + 64 it): that pass runs from registers,
-// with no LDS image of the input (wfft_from_regs); the rest as make_cplan. 640 =
-// 10*8*8, 512 = 8*8*8, 320 = 5*8*8, 256 = 4*8*8; 400 has none (make_cplan).
-constexpr CPlan make_wplan(int N) {
-  const int first[6] = {10, 8, 5, 4, 2, 3};
-  for (int i = 0; i < 6; ++i) {
-    const int r = first[i];
-    if (N % r == 0 && (N / r) % 64 == 0) {
-      const CPlan rest = make_cplan(N / r);
-      CPlan p{};
-      p.radix[p.npass++] = r;
-      for (int k = 0; k < rest.npass && p.npass < kMaxPasses; ++k) p.radix[p.npass++] = rest.radix[k];
-      return p;
-    }
-  }
-  return make_cplan(N);
-}
-template <int N> constexpr bool wfft_regs_ok() {
-  return N % 64 == 0 && (N / make_wplan(N).radix[0]) % 64 == 0;
-}
-
-// RG: the plan of wfft_from_regs (make_wplan), else make_cplan
-template <int N, int PS, int NS, bool RG = false>
+template <int N, int PS, int NS>
 __device__ __forceinline__ void wfft_pass(float2* a, const float2* __restrict__ tw, int lane) {
-  constexpr CPlan pl = RG ? make_wplan(N) : make_cplan(N);
+  constexpr CPlan pl = make_cplan(N);
   if constexpr (PS < pl.npass) {
     constexpr int R = pl.radix[PS], nbf = N / R, tstep = N / (NS * R);
     constexpr int ITER = (nbf + kWave - 1) / kWave;
@@ -561,41 +529,17 @@ __device__ __forceinline__ void wfft_pass(float2* a, const float2* __restrict__ 
       if (nbf % kWave == 0 || j < nbf) butterfly<R>(v[it], a, (j / NS) * NS * R + j % NS, NS);
     }
     wave_lds_sync();
-    wfft_pass<N, PS + 1, NS * R, RG>(a, tw, lane);
+    wfft_pass<N, PS + 1, NS * R>(a, tw, lane);
   }
 }
 
-// The whole wave-local FFT of the pair (y0[it], y1[it]) at n = lane + 64 it (wfft_regs_ok):
-// the first pass's butterflies from registers into a, then the LDS passes
-template <int N>
-__device__ __forceinline__ void wfft_from_regs(const float (&y0)[N / 64], const float (&y1)[N / 64], float2* a,
-                                               const float2* __restrict__ tw, int lane) {
-  static_assert(wfft_regs_ok<N>(), "first radix must leave N / R0 a multiple of 64");
-  constexpr int R = make_wplan(N).radix[0], IR = N / R / 64;
-#pragma unroll
-  for (int i = 0; i < IR; ++i) {
-    float2 v[kMaxRadix];
-#pragma unroll
-    for (int q = 0; q < R; ++q) v[q] = make_float2(y0[i + q * IR], y1[i + q * IR]);
-    butterfly<R>(v, a, (lane + 64 * i) * R, 1);
-  }
-  wave_lds_sync();
-  wfft_pass<N, 1, R, true>(a, tw, lane);
-}
 
 // Pair stride of the wave-local LDS image: N + 2 float2, so the unpack's reads of
 // W pairs at one bin fall in different banks
 template <int N> constexpr int wv_stride() { return N + 2; }
-// frame pairs per block of the wave-local kernels (the adjoint also keeps the window, N floats)
-template <int N> constexpr int wv_pairs() {
-  if constexpr (!SE_STFT_WV_FIT) {
-    return kWvPairs;
-  } else {
-    constexpr int fixed = N * 8 + N * 4;   // the staged twiddles, the adjoint's window
-    constexpr int w = (40960 - fixed) / (wv_stride<N>() * 8);
-    return w < 1 ? 1 : (w > kWvPairs ? kWvPairs : w);
-  }
-}
+// frame pairs per block of the wave-local kernels (7 per block to fit four blocks per
+// CU, and 4 or 16 per block, measured slower: profiles/ab/r4_stft_regs_pairs_ab.txt)
+template <int N> constexpr int wv_pairs() { return kWvPairs; }
 
 // Unpack the W packed pair results of a wave-local block (pair stride NP) into
 // frames t0 + 2j (even) and t0 + 2j + 1 (odd); lanes run along frames, so a store
@@ -695,17 +639,13 @@ __global__ void __launch_bounds__(kWave * W) stft_fwd_wv_kernel(const StftArgs a
 #if SE_STFT_TWL_FWD
   __syncthreads();   // stw
 #endif
-  if constexpr (SE_STFT_WV_REGS && wfft_regs_ok<N>()) {
-    wfft_from_regs<N>(ya, yb, Aw, stw, lane);
-  } else {
 #pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int n = lane + it * kWave;
-      if (N % kWave == 0 || n < N) Aw[n] = make_float2(ya[it], yb[it]);
-    }
-    wave_lds_sync();   // the wave's own pair only
-    wfft_pass<N, 0, 1>(Aw, stw, lane);
+  for (int it = 0; it < IT; ++it) {
+    const int n = lane + it * kWave;
+    if (N % kWave == 0 || n < N) Aw[n] = make_float2(ya[it], yb[it]);
   }
+  wave_lds_sync();   // the wave's own pair only
+  wfft_pass<N, 0, 1>(Aw, stw, lane);
   __syncthreads();   // every pair of the block transformed
   wv_unpack_store<N, W, LP>(A, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
 }
@@ -1226,25 +1166,17 @@ __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs
   const float ah = 0.5f * N, inv_a = 1.f / ah;
   const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
   float2* Aw = A + w * NP;
-  float y0[IT], y1[IT];
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int n = lane + it * kWave;
-    const bool in = n < a.win;
-    y0[it] = in ? apply_g(v[it][0], n, se2[0], so2[0], inv_a, ce, co) : 0.f;
-    y1[it] = in ? apply_g(v[it][1], n, se2[1], so2[1], inv_a, ce, co) : 0.f;
-  }
-  if constexpr (SE_STFT_WV_REGS && wfft_regs_ok<N>()) {
-    wfft_from_regs<N>(y0, y1, Aw, stw, lane);
-  } else {
-#pragma unroll
-    for (int it = 0; it < IT; ++it) {
-      const int n = lane + it * kWave;
-      if (N % kWave == 0 || n < N) Aw[n] = make_float2(y0[it], y1[it]);
+    if (N % kWave == 0 || n < N) {
+      const bool in = n < a.win;
+      Aw[n] = make_float2(in ? apply_g(v[it][0], n, se2[0], so2[0], inv_a, ce, co) : 0.f,
+                          in ? apply_g(v[it][1], n, se2[1], so2[1], inv_a, ce, co) : 0.f);
     }
-    wave_lds_sync();
-    wfft_pass<N, 0, 1>(Aw, stw, lane);
   }
+  wave_lds_sync();
+  wfft_pass<N, 0, 1>(Aw, stw, lane);
   __syncthreads();
   wv_unpack_store<N, W, LP>(A, t0, a.T, b, a.out, nullptr, 0, a.dt);
 }
