@@ -283,10 +283,6 @@ int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float* x, int x_h
  *          NULL when track_running_stats=False; updated in place in training.
  * nbt    : device int64 num_batches_tracked (NULL if not tracking).
  * save   : device fp32 [SE_CBN_SAVE_FLOATS*Cc] per-channel state for se_cbn_bwd.
- *          Its two pad words per channel are left zero by the forward; the
- *          backward uses them as workgroup arrival counts (its finalize runs in
- *          the moments pass) and leaves them zero again, so one save must not be
- *          in two concurrent backward calls.
  * act    : 0 none, 1 LeakyReLU(slope), 2 ReLU (applied after the affine).
  * training: 1 = batch statistics (+ running update when running != NULL),
  *          0 = running statistics.

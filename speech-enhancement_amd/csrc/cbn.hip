@@ -28,11 +28,6 @@
 namespace {
 
 constexpr int kThreads = 256;
-// SE_CBN_FUSED_FIN: the backward finalize runs in the moments pass's last workgroup per
-// channel (fused_finalize) instead of its own launch
-#ifndef SE_CBN_FUSED_FIN
-#define SE_CBN_FUSED_FIN 1
-#endif
 constexpr int kSeg = 8192;   // elements of one (b, c) plane per reduction row
 constexpr int kSave = 20;    // floats of per-channel state (SE_CBN_SAVE_FLOATS)
 // save layout (S_DR / S_DI: max |x_r - Mr|, max |x_i - Mi| of the training batch)
@@ -403,7 +398,7 @@ constexpr int kCoef = 16;
 // HEAD: part holds the head's 8 weight-grad sums after the 6 moments (stride
 // 6 + kHeadNS); they are added in the same fixed order and written to dwh.
 // PR: the 7th sum (the PReLU weight's gradient, per channel) goes to pw_part[c]
-// chb != NULL: the channel's dx bound goes to chb[c] (the fused form below) instead.
+// chb != NULL: the channel's dx bound goes to chb[c] instead.
 template <bool HEAD, typename T = float, bool PR = false>
 __device__ __forceinline__ void bwd_finalize_wave(int c, int lane, const double* part, const float* ext, int P,
                                                   double count, int Cc, const float* save, const Ptr5& params,
@@ -513,52 +508,6 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
                                  training, coef, dx_amax, dwh, pw_part, nullptr);
 }
 
-// The backward finalize inside the moments pass (SE_CBN_FUSED_FIN): the last of a
-// channel's P moments workgroups to arrive (an arrival count in the channel's save
-// pad word S_PAD0, zero from the forward finalize and reset to zero here) runs that
-// channel's finalize; the last channel to finish (a count in channel 0's S_PAD1) writes
-// the max of the per-channel dx bounds. One launch fewer per backward on the main
-// stream, whose small launches wait for CU slots beside the side-stream weight-grads.
-struct FinArgs {
-  int on;
-  double count;
-  Ptr5 params;
-  int affine;
-  MPtr5 dparams;
-  int has_dparams, training;
-  float* coef;
-  float* dwh;
-  double* pw_part;
-  float* chb;   // [Cc] per-channel dx bounds
-};
-
-template <bool HEAD, typename T, bool PR>
-__device__ __forceinline__ void fused_finalize(const FinArgs& fa, int c, int P, int Cc, const double* part,
-                                               const float* ext, const float* save, float* dx_amax) {
-  __shared__ unsigned s_last;
-  __threadfence();   // this workgroup's partial sums, before its arrival
-  __syncthreads();
-  unsigned* cnt = reinterpret_cast<unsigned*>(const_cast<float*>(save) + (long long)c * kSave + S_PAD0);
-  if (threadIdx.x == 0) s_last = atomicAdd(cnt, 1u) == (unsigned)(P - 1) ? 1u : 0u;
-  __syncthreads();
-  if (!s_last) return;
-  __threadfence();   // the other workgroups' partial sums
-  if (threadIdx.x < 64)
-    bwd_finalize_wave<HEAD, T, PR>(c, threadIdx.x, part, ext, P, fa.count, Cc, save, fa.params, fa.affine,
-                                   fa.dparams, fa.has_dparams, fa.training, fa.coef, dx_amax, fa.dwh, fa.pw_part,
-                                   dx_amax ? fa.chb : nullptr);
-  if (threadIdx.x != 0) return;
-  atomicExch(cnt, 0u);
-  if (!dx_amax) return;
-  __threadfence();   // chb[c]
-  unsigned* gcnt = reinterpret_cast<unsigned*>(const_cast<float*>(save) + S_PAD1);
-  if (atomicAdd(gcnt, 1u) != (unsigned)(Cc - 1)) return;
-  __threadfence();
-  float m = 0.f;
-  for (int i = 0; i < Cc; ++i) m = fmaxf(m, fa.chb[i]);
-  *dx_amax = m;
-  atomicExch(gcnt, 0u);
-}
 
 // Backward moments: g = dL/dy * act'(z), xt = x - M, with dL/dy = gy (SRC 0),
 // gy + gy2 (SRC 1: a forked output, se_cbn_bwd2, summed on the fly) or formed
@@ -571,7 +520,7 @@ __global__ void __launch_bounds__(kThreads)
 cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
                        const T* __restrict__ x, int B, int C, int HW, int P,
                        const float* __restrict__ save, int act, float slope, double* part, float* ext,
-                       float* dx_amax, HeadArgs hd, const T* pw, FinArgs fa) {
+                       float* dx_amax, HeadArgs hd, const T* pw) {
   static_assert(!PR || SRC != 2, "no PReLU on the head path");
   static_assert(SRC != 2 || sizeof(T) == 4, "the head path is fp32");
   constexpr int NS = SRC == 2 ? 6 + kHeadNS : (PR ? 7 : 6);
@@ -672,7 +621,6 @@ cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
     ext[((long long)c * P + p) * 2 + 0] = gmr;
     ext[((long long)c * P + p) * 2 + 1] = gmi;
   }
-  if (fa.on) fused_finalize<SRC == 2, T, PR>(fa, c, P, Cc, part, ext, save, dx_amax);
 }
 
 
@@ -1271,40 +1219,26 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   float* xa = training ? dx_amax : nullptr;
   const dim3 mg(Cc, P), mb(kThreads);
   const bool pr = pw != nullptr;
-  FinArgs fa{};
-  fa.on = SE_CBN_FUSED_FIN;
-  fa.count = (double)B * HW;
-  fa.params = pp;
-  fa.affine = params ? 1 : 0;
-  fa.dparams = dp;
-  fa.has_dparams = dparams ? 1 : 0;
-  fa.training = training;
-  fa.coef = coef;
-  fa.dwh = dwh;
-  fa.pw_part = pwp;
-  fa.chb = ext + (size_t)Cc * P * 2;   // the ext region holds [Cc][P][4] floats, the backward uses 2
   if constexpr (sizeof(T) == 4) {
     if (src == 2)
       hipLaunchKernelGGL((cbn_bwd_moments_kernel<2, float>), mg, mb, 0, st, (const float*)gy, (const float*)gy2,
-                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr, fa);
+                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr);
   }
   if (src == 1 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw, fa);
+                       slope, part, ext, xa, hd, pw);
   else if (src == 1)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw, fa);
+                       part, ext, xa, hd, pw);
   else if (src == 0 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw, fa);
+                       slope, part, ext, xa, hd, pw);
   else if (src == 0)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw, fa);
+                       part, ext, xa, hd, pw);
   SE_LAUNCH_CHECK();
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
-  if (fa.on) {
-    // finalized inside the moments pass
-  } else if (src == 2)
+  if (src == 2)
     hipLaunchKernelGGL((cbn_bwd_finalize_kernel<true, T>), fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
                        params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, dwh, pwp);
   else if (pr)
