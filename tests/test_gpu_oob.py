@@ -1,5 +1,4 @@
-"""Guard-region out-of-bounds regression (the tools/oob_probe*.py checks as
-tests). Every operand of a conv pass / the LSTM recurrence lives in the
+"""Guard-region out-of-bounds regression. Every operand of a conv pass / the LSTM recurrence lives in the
 middle of a buffer padded on both sides: inputs' padding is filled with 0 in
 one run and NaN in another (an out-of-bounds READ changes the result or makes
 it non-finite), outputs' padding with a sentinel (an out-of-bounds WRITE
