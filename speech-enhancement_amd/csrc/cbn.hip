@@ -28,6 +28,10 @@
 namespace {
 
 constexpr int kThreads = 256;
+// SE_CBN_APPLY_FIN: the backward finalize in the apply pass's prologue (cbn_bwd_apply_fin_kernel)
+#ifndef SE_CBN_APPLY_FIN
+#define SE_CBN_APPLY_FIN 1
+#endif
 constexpr int kSeg = 8192;   // elements of one (b, c) plane per reduction row
 constexpr int kSave = 20;    // floats of per-channel state (SE_CBN_SAVE_FLOATS)
 // save layout (S_DR / S_DI: max |x_r - Mr|, max |x_i - Mi| of the training batch)
@@ -398,13 +402,14 @@ constexpr int kCoef = 16;
 // HEAD: part holds the head's 8 weight-grad sums after the 6 moments (stride
 // 6 + kHeadNS); they are added in the same fixed order and written to dwh.
 // PR: the 7th sum (the PReLU weight's gradient, per channel) goes to pw_part[c]
-// chb != NULL: the channel's dx bound goes to chb[c] instead.
+// o: the channel's kCoef floats; side: also write the parameter gradients, the head
+// weight gradient, the PReLU partial and the dx bound (once per channel)
 template <bool HEAD, typename T = float, bool PR = false>
 __device__ __forceinline__ void bwd_finalize_wave(int c, int lane, const double* part, const float* ext, int P,
                                                   double count, int Cc, const float* save, const Ptr5& params,
                                                   int affine, const MPtr5& dparams, int has_dparams, int training,
-                                                  float* coef, float* dx_amax, float* dwh, double* pw_part,
-                                                  float* chb) {
+                                                  float* o, float* dx_amax, float* dwh, double* pw_part,
+                                                  bool side) {
   constexpr int NS = HEAD ? 6 + kHeadNS : (PR ? 7 : 6);
   double sm[NS];
 #pragma unroll
@@ -421,8 +426,10 @@ __device__ __forceinline__ void bwd_finalize_wave(int c, int lane, const double*
   gmr = se::wave_max(gmr);
   gmi = se::wave_max(gmi);
   if (lane != 0) return;
-  if constexpr (PR) pw_part[c] = sm[NS - 1];
-  if (HEAD) {   // dw[o, ch, k] at (o * C + ch) * KW + k, C = 2 Cc
+  if constexpr (PR) {
+    if (side) pw_part[c] = sm[NS - 1];
+  }
+  if (HEAD && side) {   // dw[o, ch, k] at (o * C + ch) * KW + k, C = 2 Cc
     const int C = 2 * Cc;
 #pragma unroll
     for (int o = 0; o < kHeadNO; ++o)
@@ -446,7 +453,7 @@ __device__ __forceinline__ void bwd_finalize_wave(int c, int lane, const double*
       // dW = dZ U (U symmetric); W symmetric -> Wri collects both off-diagonals
       const double dw00 = dz00 * urr + dz01 * uri, dw01 = dz00 * uri + dz01 * uii;
       const double dw10 = dz10 * urr + dz11 * uri, dw11 = dz10 * uri + dz11 * uii;
-      if (has_dparams) {
+      if (has_dparams && side) {
         stv<T>(dparams.p[0], c, (float)dw00);
         stv<T>(dparams.p[1], c, (float)(dw01 + dw10));
         stv<T>(dparams.p[2], c, (float)dw11);
@@ -476,21 +483,19 @@ __device__ __forceinline__ void bwd_finalize_wave(int c, int lane, const double*
       grr = 2.0 * gvrr / count; gri = gvri / count; gii = 2.0 * gvii / count;
       gbr = sm[0] / count; gbi = sm[1] / count;
     }
-    float* o = coef + (long long)c * kCoef;
     o[0] = (float)zrr; o[1] = (float)zir;   // dxr = Zrr g_r + Zir g_i
     o[2] = (float)zri; o[3] = (float)zii;   // dxi = Zri g_r + Zii g_i
     o[4] = (float)gbr; o[5] = (float)gbi;
     o[6] = (float)grr; o[7] = (float)gri; o[8] = (float)gii;
     o[9] = s[S_MR]; o[10] = s[S_MI]; o[11] = s[S_BR]; o[12] = s[S_BI];
     o[13] = o[14] = o[15] = 0.f;
-    if (training && dx_amax) {   // dx = Z^T (g - gb) + Gamma (x - M), bounded term by term
+    if (side && training && dx_amax) {   // dx = Z^T (g - gb) + Gamma (x - M), bounded term by term
       const float gr = gmr + fabsf(o[4]);
       const float gi = gmi + fabsf(o[5]);
       const float dr = s[S_DR], di = s[S_DI];
       const float br = fabsf(o[0]) * gr + fabsf(o[1]) * gi + fabsf(o[6]) * dr + fabsf(o[7]) * di;
       const float bi = fabsf(o[2]) * gr + fabsf(o[3]) * gi + fabsf(o[7]) * dr + fabsf(o[8]) * di;
-      if (chb) chb[c] = fmaxf(br, bi) * 1.0001f;
-      else atomicMax(reinterpret_cast<unsigned*>(dx_amax), __float_as_uint(fmaxf(br, bi) * 1.0001f));
+      atomicMax(reinterpret_cast<unsigned*>(dx_amax), __float_as_uint(fmaxf(br, bi) * 1.0001f));
     }
   }
 }
@@ -505,7 +510,98 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
   const int c = blockIdx.x * kFinWaves + (threadIdx.x >> 6);
   if (c >= Cc) return;
   bwd_finalize_wave<HEAD, T, PR>(c, lane, part, ext, P, count, Cc, save, params, affine, dparams, has_dparams,
-                                 training, coef, dx_amax, dwh, pw_part, nullptr);
+                                 training, coef + (long long)c * kCoef, dx_amax, dwh, pw_part, true);
+}
+
+// The backward apply (SRC 0 / 1, cbn_bwd_apply(4)_kernel's arithmetic) with the finalize in
+// its prologue: a workgroup per (channel, item) runs the channel's finalize into LDS (wave
+// 0; the parameter gradients and the dx bound from the item-0 workgroups) and then streams
+// the item's two planes. One main-stream launch fewer per CBN backward: beside the
+// side-stream weight-grads the 16-workgroup finalize launch waited 60-310 us for CU slots
+// (profiles/r4_main_stream_kernels.txt). V4: 16-B accesses (HW % 4 == 0). grid (Cc, B)
+template <int SRC, typename T, bool V4>
+__global__ void __launch_bounds__(kThreads)
+cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, const T* __restrict__ x,
+                         T* __restrict__ dx, int C, int HW, int act, float slope, const double* part,
+                         const float* ext, int P, double count, const float* save, Ptr5 params, int affine,
+                         MPtr5 dparams, int has_dparams, int training, float* dx_amax) {
+  static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
+  __shared__ float k[kCoef];
+  const int Cc = C / 2, c = blockIdx.x, b = blockIdx.y;
+  if (threadIdx.x < 64)
+    bwd_finalize_wave<false, T, false>(c, threadIdx.x, part, ext, P, count, Cc, save, params, affine, dparams,
+                                       has_dparams, training, k, dx_amax, nullptr, nullptr, b == 0);
+  __syncthreads();
+  const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
+  const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
+  const float br = k[11], bi = k[12];
+  const float neg = act_neg(act, slope);
+  const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+  auto one = [&](float fxr, float fxi, float fgr, float fgi, float& dr, float& di) __attribute__((always_inline)) {
+    const float xr = fxr - mr, xi = fxi - mi;
+    const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
+    const float gr = (zr > 0.f ? fgr : fgr * neg) - gbr;
+    const float gi = (zi > 0.f ? fgi : fgi * neg) - gbi;
+    dr = a00 * gr + a01 * gi + grr * xr + gri * xi;
+    di = a10 * gr + a11 * gi + gri * xr + gii * xi;
+  };
+  if constexpr (V4) {
+    constexpr int U = 2;   // float4s per plane and tensor in flight
+    for (int i0 = threadIdx.x * 4; i0 < HW; i0 += kThreads * 4 * U) {
+      f32x4v xr4[U], xi4[U], gr4[U], gi4[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = min(i0 + u * kThreads * 4, HW - 4);   // clamped loads, guarded stores
+        xr4[u] = ld4(x + offr + i);
+        xi4[u] = ld4(x + offi + i);
+        gr4[u] = ld4(gy + offr + i);
+        gi4[u] = ld4(gy + offi + i);
+        if (SRC == 1) {
+          gr4[u] += ld4(gy2 + offr + i);
+          gi4[u] += ld4(gy2 + offi + i);
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * kThreads * 4;
+        if (i < HW) {
+          f32x4v dr4, di4;
+#pragma unroll
+          for (int l = 0; l < 4; ++l) {
+            float dr, di;
+            one(xr4[u][l], xi4[u][l], gr4[u][l], gi4[u][l], dr, di);
+            dr4[l] = dr;
+            di4[l] = di;
+          }
+          st4(dx + offr + i, dr4);
+          st4(dx + offi + i, di4);
+        }
+      }
+    }
+  } else {
+    constexpr int U = 4;
+    for (int i0 = threadIdx.x; i0 < HW; i0 += kThreads * U) {
+      float fxr[U], fxi[U], fgr[U], fgi[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int j = min(i0 + u * kThreads, HW - 1);
+        fxr[u] = (float)x[offr + j];
+        fxi[u] = (float)x[offi + j];
+        fgr[u] = SRC == 1 ? (float)gy[offr + j] + (float)gy2[offr + j] : (float)gy[offr + j];
+        fgi[u] = SRC == 1 ? (float)gy[offi + j] + (float)gy2[offi + j] : (float)gy[offi + j];
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        const int i = i0 + u * kThreads;
+        if (i < HW) {
+          float dr, di;
+          one(fxr[u], fxi[u], fgr[u], fgi[u], dr, di);
+          dx[offr + i] = (T)dr;
+          dx[offi + i] = (T)di;
+        }
+      }
+    }
+  }
 }
 
 
@@ -1238,6 +1334,19 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
                        part, ext, xa, hd, pw);
   SE_LAUNCH_CHECK();
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
+  if (SE_CBN_APPLY_FIN && (src == 0 || src == 1) && !pr && !fc) {
+    const bool v4 = HW % 4 == 0;
+#define SE_AF(S, V)                                                                                            \
+  hipLaunchKernelGGL((cbn_bwd_apply_fin_kernel<S, T, V>), dim3(Cc, B), mb, 0, st, gy, gy2, x, dx, C, HW, act, slope, \
+                     part, ext, P, (double)B * HW, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, xa)
+    if (src == 1 && v4) SE_AF(1, true);
+    else if (src == 1) SE_AF(1, false);
+    else if (v4) SE_AF(0, true);
+    else SE_AF(0, false);
+#undef SE_AF
+    SE_LAUNCH_CHECK();
+    return SE_OK;
+  }
   if (src == 2)
     hipLaunchKernelGGL((cbn_bwd_finalize_kernel<true, T>), fg, fb, 0, st, part, ext, P, (double)B * HW, Cc, save, pp,
                        params ? 1 : 0, dp, dparams ? 1 : 0, training, coef, xa, dwh, pwp);
