@@ -254,7 +254,11 @@ __global__ __launch_bounds__(4 * H) void lstm_bwd_lds_kernel(LstmArgs a) {
   }
 }
 
-constexpr int kBS = 2;
+// sequences per workgroup (SE_LSTM_BS, build-time)
+#ifndef SE_LSTM_BS
+#define SE_LSTM_BS 2
+#endif
+constexpr int kBS = SE_LSTM_BS;
 
 template <int H>
 int launch(bool bwd, const LstmArgs& a, int L, hipStream_t st) {
