@@ -44,7 +44,7 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-in MFMA dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 / f16 MFMA dense peak (no sparsity)
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
 SR, SECONDS = 16000, 4
-PROFILE_STATS = os.path.join(ROOT, "profiles", "r4_bench_kernel_stats.csv")
+PROFILE_STATS = os.path.join(ROOT, "profiles", "r5_bench_kernel_stats.csv")
 
 # OpTimer tag -> (kernel instantiation as rocprof names it, launches per call, description).
 # The decoder's joined passes are one launch of one instantiation per call (the data-grad of
@@ -58,7 +58,7 @@ KERNEL_OF = {
     "conv_fwd_joined_f16x3": ("gather_x3_kernel<true, 3, 1, 1, true, 0>", 2,
                               "gather_x3_kernel<F16, joined fwd> (se_conv2d_fwd_joined, 2 stride-phase "
                               "launches per call)"),
-    "conv_wgrad_joined_f16x3": ("wgrad_x3_kernel<true, 3, true, true, 2, false, 0, false>", 1,
+    "conv_wgrad_joined_f16x3": ("wgrad_x3_kernel<true, 3, true, true, 2, false, 0>", 1,
                                 "wgrad_x3_kernel<F16, joined, 128 x 256 tiles> (se_conv2d_bwd_weight_joined)"),
     "conv_data_joined_bf16x3": ("gather_x3_kernel<true, 3, 2, 2, false, 0>", 1,
                                 "gather_x3_kernel<bf16x3, joined data-grad> (se_conv2d_bwd_data_joined)"),
@@ -88,10 +88,11 @@ def parse():
                          "past it and the sample says how many steps ran")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-op-timing", action="store_true")
-    ap.add_argument("--compare", default="f32",
+    ap.add_argument("--compare", default="f32;bf16",
                     help="';'-separated conv math modes timed beside the default step: the all-fp32 MFMA "
                          "step (reported as f32_exact, with its own warm-up and roofline) and the coarser "
-                         "split-bf16 / one-term bf16 steps; '' for none")
+                         "split-bf16 / one-term bf16 steps (bf16 = SURVEY 8(d) config 4's 'bf16 (speed)' "
+                         "leg, reported as bf16_speed); '' for none")
     ap.add_argument("--no-compare", "--no-compare-f32", dest="compare", action="store_const", const="",
                     help="skip the comparison runs")
     ap.add_argument("--math", default=os.environ.get("SEHIP_CONV_MATH"),
@@ -374,8 +375,11 @@ def run(args):
         else:
             os.environ["SEHIP_OVERLAP"] = prev
 
-    # ConvSTFT / iSTFT are ~50 us kernels: per-call events inside the step also catch host
-    # launch gaps, so their GB/s use 20 back-to-back calls between one event pair
+    # ConvSTFT / iSTFT are ~30-50 us kernels: per-call events inside the step also catch host
+    # launch gaps, so each launch is timed alone here (one HIP event pair around ONE launch,
+    # the device idle before it; median of 20). The roofline frac itself uses the kernel's
+    # own duration from the committed rocprofv3 --stats summary of the same bench command
+    # (profiles/r5_bench_kernel_stats.csv), and falls back to this median only without it.
     bursts = {}
     if kern and rank == 0:
         mod = model.module if hasattr(model, "module") else model
@@ -384,13 +388,15 @@ def run(args):
         def burst(fn):
             fn()
             torch.cuda.synchronize()
-            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            e0.record()
+            ts = []
             for _ in range(20):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
                 fn()
-            e1.record()
-            torch.cuda.synchronize()
-            return e0.elapsed_time(e1) / 20
+                e1.record()
+                torch.cuda.synchronize()
+                ts.append(e0.elapsed_time(e1))
+            return sorted(ts)[len(ts) // 2]
 
         # the kernels launched straight into preallocated buffers (the launch helpers the
         # autograd Functions call): per-call host work (autograd, allocation) would
@@ -458,6 +464,11 @@ def run(args):
     }
     if "f32" in compare:
         out["f32_exact"] = compare.pop("f32")
+    if "bf16" in compare:   # "fp32 (parity) and bf16 (speed)"
+        out["bf16_speed"] = compare.pop("bf16")
+        out["bf16_speed"]["note"] = ("the same FRCRN train step with every conv GEMM on one-term bf16 MFMA "
+                                     "(operands rounded to bf16, fp32 accumulate and storage: the arithmetic "
+                                     "of a bf16 autocast conv); not fp32-class, not the headline")
     if compare:
         out["other_conv_math"] = list(compare.values())
     if kern:
@@ -481,15 +492,22 @@ def run(args):
             if not (st and name in bursts):
                 continue
             per_call = st["bytes"] / st["calls"]
-            gbs = per_call / (bursts[name] * 1e-3) / 1e9
+            rp = _rocprof_avg_ms(kname)
+            dur = rp if rp else bursts[name]
+            gbs = per_call / (dur * 1e-3) / 1e9
             pmc = _pmc(kname)
             out[f"{name}_roofline"] = {
                 "bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(gbs / HBM_PEAK_GBS, 4), "traffic": pmc["hbm_bytes_per_launch"] if pmc else None,
-                "kernel": f"{kname} (se_{name})", "avg_ms_per_call": round(bursts[name], 4),
-                "rocprof_avg_ms": _rocprof_avg_ms(kname),
-                "timing": "20 back-to-back launches (sehip.functional.*_launch into preallocated buffers) "
-                          "between one HIP event pair, after the timed region",
+                "kernel": f"{kname} (se_{name})", "duration_ms": round(dur, 4),
+                "duration_source": ("rocprofv3 --stats average of this kernel over the bench run "
+                                    f"({os.path.relpath(PROFILE_STATS, ROOT)})") if rp else
+                                   "median single-launch HIP event span (no rocprof summary found)",
+                "rocprof_avg_ms": rp,
+                "single_launch_event_ms": round(bursts[name], 4),
+                "single_launch_note": "one HIP event pair around one launch (sehip.functional.*_launch into "
+                                      "preallocated buffers) on an idle device, median of 20, after the "
+                                      "timed region; includes the event / launch edges",
                 "algorithmic_bytes_per_call": per_call}
         out["op_breakdown"] = _breakdown(kern, args.steps)
         total_conv = sum(v["flops"] for k, v in kern.items() if k.startswith("conv"))

@@ -28,7 +28,10 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 7   /* 7: measured-neutral variants removed (se_conv2d_desc.accumulate_dx /
+#define SEHIP_ABI_VERSION 8   /* 8: CL16 operands removed (se_pack_cl16*, se_conv2d_desc.x_packed /
+                                 .x2_packed / .dy_packed / .x2_amax, se_cbn_fwd's y_packed,
+                                 se_ccbam_apply's out_packed / out_amax: measured slower);
+                                 7: measured-neutral variants removed (se_conv2d_desc.accumulate_dx /
                                  .moments, se_cbn_*_fwd_moments, se_stream_create_cu_subset); CL16
                                  operands read by the weight-grad only;
                                  6: LSTM layer GEMMs (se_gemm, se_colsum);
@@ -147,16 +150,6 @@ typedef struct se_conv2d_desc {
    * apply, se_amax) fill it for free. */
   const float* x_amax;
   const float* dy_amax;
-  /* SE_MATH_F16X3, se_conv2d_bwd_weight_joined only, optional: the joined conv's
-   * inputs in CL16 form (se_pack_cl16 layout, written by their producers:
-   * se_cbn_fwd's y_packed, se_ccbam_apply's out_packed), s in x_packed (made with
-   * the x_amax bound) and x in x2_packed (made with x2_amax). The weight-grad GEMM
-   * then reads its D operand pre-split instead of splitting fp32 in the loop.
-   * Both or neither; dy_packed is reserved (NULL). Any other pass, or a shape
-   * the CL16 kernel does not tile, returns SE_E_UNSUPPORTED before launching. */
-  const void* x_packed;
-  const void* x2_packed;
-  const void* dy_packed;
   /* SE_MATH_F16X3 only, optional: device fp32 [1] holding an upper bound of
    * max |w| over the real and imaginary weights (se_amax_weights). The forward
    * and data-grad passes of one conv call share it (the weights do not change
@@ -167,7 +160,7 @@ typedef struct se_conv2d_desc {
    * runs) reads and writes those tensors as they are and computes with the
    * one-term MFMA of its own format, whose operands are then exact: bf16 needs
    * math SE_MATH_BF16, fp16 needs SE_MATH_F16 (SE_E_UNSUPPORTED otherwise, and for
-   * the joined / CL16 forms and the fp32-only small weight-grad shapes, before any
+   * the joined forms and the fp32-only small weight-grad shapes, before any
    * launch). fp32 storage takes any math. */
   int dtype;
   /* ABI 5, se_conv2d_bwd_data / se_conv2d_bwd_data_joined only, optional: the
@@ -178,10 +171,6 @@ typedef struct se_conv2d_desc {
    * launch runs beside nothing, instead of in the backward, where it waits for CU
    * slots behind the side stream's weight-grad GEMMs. NULL = build it in ws. */
   const void* data_weights;
-  /* ABI 7, se_conv2d_bwd_weight_joined with CL16 operands only: the bound x2_packed
-   * (x) was made with; x_amax is then the bound of s alone (x_packed). Each source
-   * keeps its own scale. Required when x2_packed is given, else ignored. */
-  const float* x2_amax;
 } se_conv2d_desc;
 
 /* Bytes of the data-grad weight image of d (0 on an invalid desc). */
@@ -204,13 +193,6 @@ enum { SE_MATH_F32 = 0, SE_MATH_BF16X3 = 1, SE_MATH_BF16X6 = 2, SE_MATH_BF16 = 3
  * (the reference's model.to(bfloat16) / model.half() runs, BASELINE configs
  * 2, 3, 5). Entry points without a dtype argument take fp32. */
 enum { SE_DTYPE_F32 = 0, SE_DTYPE_BF16 = 1, SE_DTYPE_F16 = 2 };
-
-/* CL16: x [B, C, H, W] fp32 -> two channels-last fp16 planes [2][B][H][W][C],
- * hi = fp16(x s), lo = fp16(x s - hi), s = 2^(14 - e) with max|x| <= *amax < 2^e
- * (the SE_MATH_F16X3 scale). C % 8 == 0. */
-size_t se_pack_cl16_bytes(int B, int C, int H, int W);
-int se_pack_cl16(const float* x, int B, int C, int H, int W, const float* amax,
-                 void* out, void* stream);
 
 /* amax[0] = max(amax[0], max_i |x[i]|) over n elements (atomic; zero amax[0]
  * first for a fresh maximum). The scale source of SE_MATH_F16X3. */
@@ -294,11 +276,6 @@ int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float* x, int x_h
  *          parameter applied after the norm (DCCRN, dccrn.py:21,45): LeakyReLU
  *          with the slope read on the device. The backward writes its gradient
  *          to dprelu_w (one element, overwritten).
- * y_packed: NULL, or (ABI 7; fp32 training with y_amax, (C/2) % 8 == 0) a buffer of
- *          se_pack_cl16_bytes(B, C, H, W) that also receives y in CL16 form, split
- *          with the scale of the y_amax bound: the pre-split operand of a consuming
- *          joined weight-grad (se_conv2d_desc.x2_packed), written in the apply pass
- *          (SE_E_UNSUPPORTED otherwise, before any launch).
  * dtype  : SE_DTYPE_F32 / BF16 / F16, the storage type of x, y, gy, gy2, dx AND
  *          of params / dparams / running / prelu_w (a model.to(bfloat16) /
  *          .half() module keeps all of them in its dtype). Arithmetic is fp32
@@ -311,7 +288,7 @@ int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
                const void* const* params, void* const* running,
                int64_t* nbt, float* save, int training, float eps,
                float momentum, int act, float slope, float* y_amax,
-               const void* prelu_w, void* y_packed, int dtype, void* ws, size_t ws_bytes,
+               const void* prelu_w, int dtype, void* ws, size_t ws_bytes,
                void* stream);
 
 /* Backward. gy = dL/dy (after the activation), x = forward input. y (the
@@ -572,11 +549,8 @@ int se_ccbam_channel_pool(const float* x, float* mean, float* mx, int* amax,
                           int B, int C, int HW, void* stream);
 int se_ccbam_spatial_pool(const float* x, const float* ca, float* pooled,
                           short* idx, int B, int C, int HW, void* stream);
-/* out_packed (ABI 7): NULL, or a se_pack_cl16_bytes(B, C, H, W) buffer that also
- * receives out in CL16 form, split with the scale of the out_amax bound (the joined
- * weight-grad's x_packed operand); C % 8 == 0. */
 int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out,
-                   void* out_packed, const float* out_amax, int B, int C, int HW, void* stream);
+                   int B, int C, int HW, void* stream);
 int se_ccbam_bwd_sa(const float* gout, float* dsa, int B, int C, int HW,
                     void* stream);
 /* ABI 6: se_ccbam_bwd_sa with the spatial gate's sigmoid backward fused:

@@ -100,19 +100,25 @@ class FRCRN(nn.Module):
 
 # ----------------------------------------------------------------- DCCRN ---
 class _DCCRNLSTM(nn.Module):
-    """dccrn.py:59-86 (complex branch)."""
+    """dccrn.py:59-86: two one-layer ComplexLSTMs + ComplexLinear, or (is_complex=False,
+    :73-75) one two-layer nn.LSTM + nn.Linear."""
 
-    def __init__(self, in_ch, hid, lin, bidirectional, **kw):
+    def __init__(self, in_ch, hid, lin, bidirectional, is_complex=True, **kw):
         super().__init__()
         nd = 2 if bidirectional else 1
-        self.layers = nn.ModuleList([
-            ComplexLSTM(in_ch, hid, num_layers=1, bidirectional=bidirectional, **kw),
-            ComplexLSTM(nd * hid, hid, num_layers=1, bidirectional=bidirectional, **kw),
-            ComplexLinear(nd * hid, lin)])
+        if is_complex:
+            self.layers = nn.ModuleList([
+                ComplexLSTM(in_ch, hid, num_layers=1, bidirectional=bidirectional, **kw),
+                ComplexLSTM(nd * hid, hid, num_layers=1, bidirectional=bidirectional, **kw),
+                ComplexLinear(nd * hid, lin)])
+        else:
+            self.layers = nn.ModuleList([nn.LSTM(in_ch, hid, num_layers=2, bidirectional=bidirectional, **kw),
+                                         nn.Linear(nd * hid, lin)])
 
     def forward(self, x):
         for layer in self.layers:
             x = layer(x)
+            x = x[0] if isinstance(x, tuple) else x   # nn.LSTM returns (output, (h_n, c_n))
         return x
 
 
@@ -143,7 +149,7 @@ class DCCRN(nn.Module):
             self.decoder.layers.append(_CausalBlock(True, cin * 2, c, (5, 2), (2, 0), nn.PReLU(),
                                                     is_complex, stride=(2, 1), output_padding=(1, 0)))
             cin = c
-        self.lstm = _DCCRNLSTM(freq_ch, lstm_channels, linear_channels, bidirectional, batch_first=True)
+        self.lstm = _DCCRNLSTM(freq_ch, lstm_channels, linear_channels, bidirectional, is_complex, batch_first=True)
         self.fft_size = fft_size
 
     def forward(self, x):

@@ -295,66 +295,6 @@ cbn_apply4_kernel(const T* __restrict__ x, T* __restrict__ y, int C, int HW,
   st4(y + offi + i, yi4);
 }
 
-// cbn_apply_kernel (fp32) that also writes y in CL16 form (channels innermost,
-// [2][B][HW][C], the SE_MATH_F16X3 split with the scale of *y_amax, see
-// se::split_f16x2): the pre-split operand of a consuming weight-grad GEMM
-// (se_conv2d_desc.x_packed / x2_packed), written here instead of split again in
-// every k-tile of that GEMM. One thread per position runs over the channel pairs
-// in groups of 8, so its two 16-B CL16 chunks per group and plane are contiguous
-// and a wave's y stores stay coalesced along the positions. grid (ceil(HW /
-// kThreads), B), dynamic LDS Cc * 8 floats; Cc % 8 == 0.
-__global__ void __launch_bounds__(kThreads)
-cbn_apply_pk_kernel(const float* __restrict__ x, float* __restrict__ y, int C, int HW,
-                    const float* __restrict__ save, int act, float slope, int64_t* nbt, const float* pw,
-                    const float* y_amax, _Float16* __restrict__ ypk, long long plane) {
-  extern __shared__ float scf[];   // [Cc][8]: Mr, Mi, Zrr, Zri, Zir, Zii, Br, Bi
-  const int Cc = C / 2, b = blockIdx.y;
-  if (pw) slope = pw[0];
-  if (nbt && blockIdx.x == 0 && b == 0 && threadIdx.x == 0) *nbt += 1;   // num_batches_tracked
-  constexpr int kIdx[8] = {S_MR, S_MI, S_ZRR, S_ZRI, S_ZIR, S_ZII, S_BR, S_BI};
-  for (int i = threadIdx.x; i < Cc * 8; i += kThreads) scf[i] = save[(i >> 3) * kSave + kIdx[i & 7]];
-  __syncthreads();
-  const int p = blockIdx.x * kThreads + threadIdx.x;
-  if (p >= HW) return;
-  const float sc = se::pow2f(se::kF16Top - se::amax_exp(y_amax));
-  const long long xb = (long long)b * C * HW + p;
-  _Float16* hp = ypk + ((long long)b * HW + p) * C;
-  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-  for (int c0 = 0; c0 < Cc; c0 += 8) {
-    float fr[8], fi[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      fr[u] = x[xb + (long long)(c0 + u) * HW];
-      fi[u] = x[xb + (long long)(Cc + c0 + u) * HW];
-    }
-    float yr[8], yi[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      const float* k = scf + (c0 + u) * 8;
-      const float xr = fr[u] - k[0], xi = fi[u] - k[1];
-      const float vr = act_fwd(k[2] * xr + k[3] * xi + k[6], act, slope);
-      const float vi = act_fwd(k[4] * xr + k[5] * xi + k[7], act, slope);
-      yr[u] = vr;
-      yi[u] = vi;
-      y[xb + (long long)(c0 + u) * HW] = vr;
-      y[xb + (long long)(Cc + c0 + u) * HW] = vi;
-    }
-    u32x4v hr, lr, hi, li;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      unsigned h, l;
-      se::split_f16x2(yr[2 * e], yr[2 * e + 1], sc, h, l);
-      hr[e] = h; lr[e] = l;
-      se::split_f16x2(yi[2 * e], yi[2 * e + 1], sc, h, l);
-      hi[e] = h; li[e] = l;
-    }
-    *reinterpret_cast<u32x4v*>(hp + c0) = hr;
-    *reinterpret_cast<u32x4v*>(hp + plane + c0) = lr;
-    *reinterpret_cast<u32x4v*>(hp + Cc + c0) = hi;
-    *reinterpret_cast<u32x4v*>(hp + plane + Cc + c0) = li;
-  }
-}
-
 // Output head of FRCRN (frcrn.py:115, 140-144): final_conv = nn.Conv2d(C, 2, (1, 2),
 // bias=False) applied to y = act(CBN(x)) of the last decoder block. Nothing else
 // reads that y, so it is never written: the forward computes the head straight
@@ -1208,19 +1148,10 @@ int cbn_stats(const T* x, int B, int C, int HW, const void* const* params, void*
 template <typename T>
 int cbn_fwd_t(const T* x, T* y, int B, int C, int HW, const void* const* params, void* const* running,
               int64_t* nbt, float* save, int training, float eps, float momentum, int act, float slope,
-              float* y_amax, const T* pw, void* ws, hipStream_t st, void* y_packed = nullptr) {
+              float* y_amax, const T* pw, void* ws, hipStream_t st) {
   const int rc = cbn_stats<T>(x, B, C, HW, params, running, nbt, save, training, eps, momentum, y_amax, ws, st);
   if (rc != SE_OK) return rc;
   int64_t* nb = (training && running) ? nbt : nullptr;
-  if constexpr (sizeof(T) == 4) {
-    if (y_packed) {   // y and its CL16 form in one pass (checked by the entry point)
-      hipLaunchKernelGGL(cbn_apply_pk_kernel, dim3(se::ceil_div(HW, kThreads), B), dim3(kThreads),
-                         (size_t)(C / 2) * 8 * sizeof(float), st, (const float*)x, (float*)y, C, HW, save, act,
-                         slope, nb, (const float*)pw, y_amax, (_Float16*)y_packed, (long long)B * C * HW);
-      SE_LAUNCH_CHECK();
-      return SE_OK;
-    }
-  }
   const dim3 grid(se::ceil_div(HW, kThreads * 4), C / 2, B);
   if (HW % 4 == 0)
     hipLaunchKernelGGL(cbn_apply4_kernel<T>, grid, dim3(kThreads), 0, st, x, y, C, HW, save, act, slope, nb, pw);
@@ -1237,20 +1168,16 @@ bool act_ok(int act, const void* prelu_w) { return act >= 0 && act <= 2 && (!pre
 extern "C" int se_cbn_fwd(const void* x, void* y, int B, int C, int HW,
                           const void* const* params, void* const* running, int64_t* nbt,
                           float* save, int training, float eps, float momentum, int act,
-                          float slope, float* y_amax, const void* prelu_w, void* y_packed, int dtype, void* ws,
+                          float slope, float* y_amax, const void* prelu_w, int dtype, void* ws,
                           size_t ws_bytes, void* stream) {
   if (!x || !y || !save || B <= 0 || C <= 0 || (C & 1) || HW <= 0 || !act_ok(act, prelu_w)) return SE_E_ARG;
   if (!training && !running) return SE_E_ARG;  // eval needs running statistics
-  // the CL16 copy: fp32 training (its scale is the y_amax bound), complex channels in 16-B groups
-  if (y_packed && (dtype != SE_DTYPE_F32 || !training || !y_amax || (C / 2) % 8 ||
-                   (long long)B * C * HW >= (1ll << 40)))
-    return SE_E_UNSUPPORTED;
   if (ws_bytes < se_cbn_workspace_size(B, C, HW) || !ws) return SE_E_WORKSPACE;
   hipStream_t st = se::as_stream(stream);
   switch (dtype) {
     case SE_DTYPE_F32:
       return cbn_fwd_t<float>((const float*)x, (float*)y, B, C, HW, params, running, nbt, save, training, eps,
-                              momentum, act, slope, y_amax, (const float*)prelu_w, ws, st, y_packed);
+                              momentum, act, slope, y_amax, (const float*)prelu_w, ws, st);
     case SE_DTYPE_BF16:
       return cbn_fwd_t<__bf16>((const __bf16*)x, (__bf16*)y, B, C, HW, params, running, nbt, save, training, eps,
                                momentum, act, slope, y_amax, (const __bf16*)prelu_w, ws, st);

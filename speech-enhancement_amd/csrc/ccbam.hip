@@ -124,47 +124,6 @@ __global__ __launch_bounds__(kThreads) void apply_kernel(const float* __restrict
   for (int c = 0; c < C; ++c) out[base + (size_t)c * HW] = x[base + (size_t)c * HW] * sca[c] + (c < Ch ? s0 : s1);
 }
 
-// apply_kernel that also writes out in CL16 form ([2][B][HW][C], channels innermost,
-// the SE_MATH_F16X3 split with the scale of *out_amax, se::split_f16x2): the gated
-// skip is the joined D operand of the decoder's weight-grad GEMM, which then reads
-// it pre-split. Channels in groups of 8 (one 16-B chunk per plane); C % 8 == 0.
-__global__ __launch_bounds__(kThreads) void apply_pk_kernel(const float* __restrict__ x, const float* __restrict__ ca,
-                                                            const float* __restrict__ sa, float* __restrict__ out,
-                                                            _Float16* __restrict__ opk, const float* out_amax,
-                                                            long long plane, int C, int HW) {
-  const int b = blockIdx.y;
-  const int hw = blockIdx.x * kThreads + threadIdx.x;
-  extern __shared__ float sca[];
-  for (int c = threadIdx.x; c < C; c += kThreads) sca[c] = ca[(size_t)b * C + c];
-  __syncthreads();
-  if (hw >= HW) return;
-  const int Ch = C / 2;
-  const float s0 = sa[((size_t)b * 2) * HW + hw], s1 = sa[((size_t)b * 2 + 1) * HW + hw];
-  const float sc = se::pow2f(se::kF16Top - se::amax_exp(out_amax));
-  const size_t base = (size_t)b * C * HW + hw;
-  _Float16* hp = opk + ((size_t)b * HW + hw) * C;
-  typedef unsigned u32x4v __attribute__((ext_vector_type(4)));
-  for (int c0 = 0; c0 < C; c0 += 8) {
-    float v[8];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) v[u] = x[base + (size_t)(c0 + u) * HW];
-#pragma unroll
-    for (int u = 0; u < 8; ++u) {
-      v[u] = v[u] * sca[c0 + u] + (c0 + u < Ch ? s0 : s1);
-      out[base + (size_t)(c0 + u) * HW] = v[u];
-    }
-    u32x4v h4, l4;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      unsigned h, l;
-      se::split_f16x2(v[2 * e], v[2 * e + 1], sc, h, l);
-      h4[e] = h; l4[e] = l;
-    }
-    *reinterpret_cast<u32x4v*>(hp + c0) = h4;
-    *reinterpret_cast<u32x4v*>(hp + plane + c0) = l4;
-  }
-}
-
 // ---------------------------------------------------------------- backward
 // dsa[b, h, hw] = sum_{c in half h} gout[b, c, hw]
 __global__ __launch_bounds__(kThreads) void bwd_sa_kernel(const float* __restrict__ g, float* __restrict__ dsa, int C,
@@ -548,17 +507,12 @@ extern "C" int se_ccbam_spatial_pool(const float* x, const float* ca, float* poo
   return SE_OK;
 }
 
-extern "C" int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out, void* out_packed,
-                              const float* out_amax, int B, int C, int HW, void* stream) {
+extern "C" int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out, int B, int C, int HW,
+                              void* stream) {
   if (int rc = check(B, C, HW)) return rc;
-  if (!x || !ca || !sa || !out || (out_packed && !out_amax)) return SE_E_ARG;
-  if (out_packed && C % 8) return SE_E_UNSUPPORTED;
-  if (out_packed)
-    hipLaunchKernelGGL(apply_pk_kernel, hw_grid(B, HW), dim3(kThreads), C * sizeof(float), se::as_stream(stream), x,
-                       ca, sa, out, (_Float16*)out_packed, out_amax, (long long)B * C * HW, C, HW);
-  else
-    hipLaunchKernelGGL(apply_kernel, hw_grid(B, HW), dim3(kThreads), C * sizeof(float), se::as_stream(stream), x, ca,
-                       sa, out, C, HW);
+  if (!x || !ca || !sa || !out) return SE_E_ARG;
+  hipLaunchKernelGGL(apply_kernel, hw_grid(B, HW), dim3(kThreads), C * sizeof(float), se::as_stream(stream), x, ca,
+                     sa, out, C, HW);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

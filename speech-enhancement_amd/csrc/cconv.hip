@@ -214,14 +214,7 @@ gather_gemm_kernel(const GatherArgs a) {
   Stage s0, s1;
   // TU path: buffer descriptors built from wave-uniform values only
   const int b0 = m0 / (a.Qh * a.Qw);               // first batch item of the tile
-  // descriptor inputs made PROVABLY uniform (readfirstlane on both pointer
-  // halves), else hipcc wraps every buffer op in a waterfall loop (guide T20)
-  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (void*)(((unsigned long long)hi << 32) | lo);
-  };
+  using se::uniform_ptr;   // descriptor inputs made provably uniform
   __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr(a.X + (long long)b0 * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
   __amdgpu_buffer_rsrc_t rwp = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.Wp), (short)0, 0x7FFFFFFF, 0x00020000);
@@ -528,13 +521,10 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
   // 32-bit offsets into the item's planes through a buffer resource (out-of-range
   // offset: reads 0); 16-bit elements are staged as raw bits and converted when they
   // are written to LDS, so no convert waits on a load in flight
-  // (readfirstlane returns int: each half goes through unsigned before widening, or a
-  // low half >= 2^31 would sign-extend into the high half of the base)
-  const unsigned long long xa = (unsigned long long)((const char*)a.X + (long long)b * a.Cg * HiWi * ES);
-  const unsigned xlo = __builtin_amdgcn_readfirstlane((unsigned)xa);
-  const unsigned xhi = __builtin_amdgcn_readfirstlane((unsigned)(xa >> 32));
+  // (se::uniform_ptr widens the two words as unsigned: a low word >= 2^31 must not
+  // sign-extend into the high half of the base)
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)(((unsigned long long)xhi << 32) | xlo), (short)0, 0x7FFFFFFF, 0x00020000);
+      se::uniform_ptr((const char*)a.X + (long long)b * a.Cg * HiWi * ES), (short)0, 0x7FFFFFFF, 0x00020000);
   constexpr int PF = (chunk + kThreads - 1) / kThreads;
   typename StageT<SD>::T pf[PF];
   auto fetch = [&](int c0) __attribute__((always_inline)) {
@@ -666,12 +656,6 @@ struct WgradArgs {
   const float* amax_d;
   // per-tap input offsets (wgrad_ktab)
   int toffh[kMaxTaps], toffw[kMaxTaps];
-  // wgrad_x3_kernel<..., DPK>: the joined D as CL16 s (dpk) and x (dpk2) with
-  // pk_plane_d / pk_plane_d2 elements per plane and x's own bound amax_d2
-  long long pk_plane_d, pk_plane_d2;
-  const void* dpk;
-  const void* dpk2;
-  const float* amax_d2;
   // wgrad_x3_kernel: tile space (k-tiles, n-tiles, m-splits) walked by its 1-D grid
   int vk, vn, vs;
   // wgrad_x3_kernel with ktab == nullptr: entries computed in the kernel from
@@ -807,12 +791,7 @@ wgrad_gemm_kernel(const WgradArgs a) {
   struct Stage { float rg[GJ], rd[DJ]; };
   Stage st0, st1;   // two register staging sets: prefetch distance 2
   // TU buffer descriptors over the split's first batch item (uniform inputs)
-  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (void*)(((unsigned long long)hi << 32) | lo);
-  };
+  using se::uniform_ptr;
   const int bfirst = (int)(mbeg / QQ);
   __amdgpu_buffer_rsrc_t rg_src = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr(a.X + (long long)bfirst * a.Cg * HiWi), (short)0, 0x7FFFFFFF, 0x00020000);
@@ -1089,7 +1068,6 @@ __global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int
 }
 
 #include "cconv_x3.hpp"
-#include "cconv_pk.hpp"
 
 // bias_full[n] for the fused complex conv: re = br - bi, im = bi + br.
 __global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out, int sd) {
@@ -1240,10 +1218,6 @@ struct ConvGeom {
   const float* x_amax;    // SE_MATH_F16X3 scale sources from the caller (or nullptr)
   const float* dy_amax;
   const float* w_amax;    // bound of max |w| from the caller (or nullptr)
-  const void* x_packed;   // SE_MATH_F16X3 CL16 operands from the caller (or nullptr)
-  const void* x2_packed;
-  const void* dy_packed;
-  const float* x2_amax;   // the bound x2_packed was made with (se_conv2d_desc.x2_amax)
   int sd;         // se_conv2d_desc.dtype (SE_DTYPE_*)
   const void* data_w;   // se_conv2d_desc.data_weights (data-grad weight image, or nullptr)
 };
@@ -1260,10 +1234,6 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.x_amax = d->x_amax;
   g.dy_amax = d->dy_amax;
   g.w_amax = d->w_amax;
-  g.x_packed = d->x_packed;
-  g.x2_packed = d->x2_packed;
-  g.dy_packed = d->dy_packed;
-  g.x2_amax = d->x2_amax;
   g.sd = d->dtype;
   g.data_w = d->data_weights;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16) return SE_E_ARG;
@@ -1523,8 +1493,6 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   if (ws_bytes < gather_ws_bytes(cls, N, g.math, g.B, Cg)) return SE_E_WORKSPACE;
   // a prepared split-fp16 image carries the caller's weight bound, which the GEMM unscales by
   if (pass == kData && g.data_w && g.math == SE_MATH_F16X3 && N > 64 && !g.w_amax) return SE_E_ARG;
-  // CL16 operands are read by the weight-grad only
-  if ((pass == kFwd ? g.x_packed : g.dy_packed) != nullptr) return SE_E_UNSUPPORTED;
   const int ldw = ldw_for(N, g.math);
   WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w, g.sd};
   if (g.sd != SE_DTYPE_F32 && jn) return SE_E_UNSUPPORTED;   // fp32-only forms
@@ -1754,21 +1722,6 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
 // ---------------------------------------------------------------------------
 // C ABI
 // ---------------------------------------------------------------------------
-extern "C" size_t se_pack_cl16_bytes(int B, int C, int H, int W) {
-  if (B <= 0 || C <= 0 || H <= 0 || W <= 0) return 0;
-  return (size_t)2 * B * C * H * W * sizeof(_Float16);
-}
-
-extern "C" int se_pack_cl16(const float* x, int B, int C, int H, int W, const float* amax, void* out,
-                            void* stream) {
-  if (!x || !amax || !out || B <= 0 || C <= 0 || H <= 0 || W <= 0 || C % 8) return SE_E_ARG;
-  const int HW = H * W;
-  hipLaunchKernelGGL(pack_cl16_kernel, dim3(se::ceil_div(HW, 64), se::ceil_div(C, 64), B), dim3(256), 0,
-                     se::as_stream(stream), x, C, HW, amax, (_Float16*)out, (long long)B * C * HW);
-  SE_LAUNCH_CHECK();
-  return SE_OK;
-}
-
 // one workgroup: max |.| over wr (and wi), written straight to *out (no zeroed
 // slot needed, so no extra launch). 16-B loads, four in flight per thread when
 // both tensors are 16-B aligned (a 64x64x5x2 complex weight: 20 per thread).
@@ -1916,7 +1869,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   const bool split_ok = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3 ||
                          g.math == SE_MATH_F16) && w.N % 16 == 0;
   // 16-bit storage: the one-term split tiles only (the fp32 kernels read fp32)
-  if (g.sd != SE_DTYPE_F32 && (jn || !split_ok || w.N <= kSmallWgradN || w.Np == 32 || g.x_packed || g.dy_packed))
+  if (g.sd != SE_DTYPE_F32 && (jn || !split_ok || w.N <= kSmallWgradN || w.Np == 32))
     return SE_E_UNSUPPORTED;
   if (jn) {
     const int dcpb = 2 * jn->jh;
@@ -1930,16 +1883,6 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   const float* zero = zero_page();
   if (!zero) return SE_E_LAUNCH;
   float* amax_slot = (float*)(p + kZeroBytes);   // [0] x (joined: x and s), [1] dy
-  // CL16 operands: the joined D only (s in x_packed, x in x2_packed, each with its own
-  // bound), on the split-fp16 128 x 256 tiles; anything else is refused before any launch
-  const bool dpk = g.x_packed || g.x2_packed || g.dy_packed;
-  if (dpk) {
-    const long long QQs = (long long)w.Qh * w.Qw;
-    const bool ok = jn && g.math == SE_MATH_F16X3 && g.sd == SE_DTYPE_F32 && g.x_packed && g.x2_packed &&
-                    !g.dy_packed && g.x_amax && g.x2_amax && w.Np % 256 == 0 && w.Cg % 128 == 0 &&
-                    jn->jh % 64 == 0 && (long long)g.B * QQs < (1ll << 31);
-    if (!ok) return SE_E_UNSUPPORTED;
-  }
   if (g.math == SE_MATH_F16X3 && (!g.x_amax || !g.dy_amax))   // launch_amax targets below
     (void)hipMemsetAsync(amax_slot, 0, kAmaxBytes, st);
   p = align256(p + kZeroBytes + kAmaxBytes);
@@ -1992,14 +1935,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   }
   const bool tu = (w.Cg % 128 == 0) && span_w * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
                   span_w * (long long)w.Np * QQw * 4 < (1ll << 31);
-  if (dpk) {   // joined D from CL16: s (x_packed, bound x_amax) and x (x2_packed, bound x2_amax)
-    if (!tu) return SE_E_UNSUPPORTED;
-    a.dpk = g.x_packed; a.dpk2 = g.x2_packed; a.amax_d = g.x_amax; a.amax_d2 = g.x2_amax;
-    a.pk_plane_d = (long long)g.B * 2 * jn->jh * w.Qh * w.Qw;
-    a.pk_plane_d2 = (long long)g.B * 2 * jn->jh * jn->h2 * jn->w2;
-    const dim3 grid = x3_wgrad_grid(a, w, 2);
-    hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2, false, 0, true>), grid, dim3(2 * kThreads), 0, st, a);
-  } else if (w.N <= kSmallWgradN) {
+  if (w.N <= kSmallWgradN) {
     dim3 grid(w.c.Kp / 16, w.splits);
     if (w.Np == 4) hipLaunchKernelGGL(wgrad_smalln_kernel<4>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_smalln_kernel<8>, grid, dim3(kThreads), 0, st, a);

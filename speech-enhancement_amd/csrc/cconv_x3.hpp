@@ -265,12 +265,7 @@ gather_x3_kernel(const GatherArgs a) {
   }
   struct Stage { typename StageT<SD>::T ra[AJ * KH]; u32x4 rw[2 * PL * KH]; };   // 16-bit storage: raw bits
   Stage s0, s1;
-  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (void*)(((unsigned long long)hi << 32) | lo);
-  };
+  using se::uniform_ptr;
   const int b0 = m0 / (a.Qh * a.Qw);
   const int cpb = JM == 1 ? 2 * a.jh : a.Cg;      // channels per batch item of X
   const long long H2W2 = (long long)a.H2 * a.W2;
@@ -541,18 +536,9 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // m-split and its order of positions, so the slabs are bit-identical.
 // KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
 // SD: storage type of X / D (as gather_x3_kernel; 16-bit with the one-term MFMA)
-// DPK (joined D, split-fp16, NB = 2): D is read pre-split, from the CL16 forms of s
-// (a.dpk) and x (a.dpk2) that their producers wrote (the CBN / CCBAM apply passes):
-// no D split in the loop, and a thread stages its D chunks with 16-B loads, a
-// wave's 64 lanes covering the 256-B channel rows of two positions (x_re, s_re,
-// x_im, s_im: four 128-B segments each). Each source carries its own scale
-// (a.amax_d for s, a.amax_d2 for x), undone per output column block in the slab
-// write; with equal bounds the slabs are bit-identical to the fp32-D form.
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0,
-          bool DPK = false>
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0>
 __global__ void __launch_bounds__(kThreads * NB, 2)
 wgrad_x3_kernel(const WgradArgs a) {
-  static_assert(!DPK || (DJ && F16 && TERMS == 3 && NB == 2 && SD == 0), "CL16 D: the joined split-fp16 8-wave tile");
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(SD == 0 || (TERMS == 1 && !DJ), "16-bit storage: one-term, no join");
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
@@ -607,10 +593,6 @@ wgrad_x3_kernel(const WgradArgs a) {
     sg = pow2f(kF16Top - eg);
     sd = pow2f(kF16Top - ed);
     ush = eg + ed - 2 * kF16Top;
-    if constexpr (DPK) {   // this wave's 64 output columns lie in one join chunk (djh % 64 == 0)
-      const bool wx = (((n0 + wnn * TN) / a.djh) & 1) == 0;
-      if (wx) ush = eg + amax_exp(a.amax_d2) - 2 * kF16Top;
-    }
   }
 
   int cb, cqh, cqw;
@@ -621,29 +603,9 @@ wgrad_x3_kernel(const WgradArgs a) {
     cqh = r / a.Qw;
     cqw = r - cqh * a.Qw;
   }
-  // DPK: a thread's D chunks are chunk dch (8 joined rows) of positions dpa and dpa + 16,
-  // both planes (4 x 16 B); the position cursors advance by BMR like the lane's own
-  constexpr int RJD = DPK ? 1 : RJ;
-  struct Stage { typename StageT<SD>::T rg[RJG * KH], rd[RJD * KH]; u32x4 dq[DPK ? 4 : 1]; };   // 16-bit: raw bits
+  struct Stage { typename StageT<SD>::T rg[RJG * KH], rd[RJ * KH]; };   // 16-bit: raw bits
   Stage st0, st1;
-  const int dch = tid & 31, dpa = tid >> 5;
-  int pcb[2] = {0, 0}, pqh[2] = {0, 0}, pqw[2] = {0, 0};
-  if constexpr (DPK) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const long long mm = mbeg + dpa + 16 * i;
-      pcb[i] = (int)(mm / QQ);
-      const int r = (int)(mm - pcb[i] * QQ);
-      pqh[i] = r / a.Qw;
-      pqw[i] = r - pqh[i] * a.Qw;
-    }
-  }
-  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (void*)(((unsigned long long)hi << 32) | lo);
-  };
+  using se::uniform_ptr;
   const int bfirst = (int)(mbeg / QQ);
   __amdgpu_buffer_rsrc_t rg_src = __builtin_amdgcn_make_buffer_rsrc(
       uniform_ptr((const char*)a.X + (long long)bfirst * a.Cg * HiWi * ES), (short)0, 0x7FFFFFFF, 0x00020000);
@@ -677,20 +639,7 @@ wgrad_x3_kernel(const WgradArgs a) {
       b_ += db;
     }
   };
-  auto advance = [&]() __attribute__((always_inline)) {
-    advance1(cb, cqh, cqw);
-    if constexpr (DPK) {
-      advance1(pcb[0], pqh[0], pqw[0]);
-      advance1(pcb[1], pqh[1], pqw[1]);
-    }
-  };
-  // DPK: joined chunk dch -> its source (x or s), the channel in it, and the row image
-  const int djc = 8 * dch, djq = DPK ? djc / max(a.djh, 1) : 0;
-  const bool d_from_x = (djq & 1) == 0;
-  const int d_c = (djq >> 1) * a.djh + (djc - djq * a.djh);
-  const _Float16* d_src = reinterpret_cast<const _Float16*>(d_from_x ? a.dpk2 : a.dpk);
-  const long long d_plane = d_from_x ? a.pk_plane_d2 : a.pk_plane_d;
-  const _Float16* d_zero = reinterpret_cast<const _Float16*>(a.zero);
+  auto advance = [&]() __attribute__((always_inline)) { advance1(cb, cqh, cqw); };
   auto load_step = [&](Stage& S, int mstep0) __attribute__((always_inline)) {
 #pragma unroll
    for (int hh = 0; hh < KH; ++hh) {
@@ -749,22 +698,10 @@ wgrad_x3_kernel(const WgradArgs a) {
         else S.rg[RJG * hh + j] = ld_s<0>(src, ok ? xb + e.x : 0);
       }
     }
-    if constexpr (DPK) {
 #pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const bool ok = (mstep + dpa + 16 * i < mend) & (!d_from_x | (pqh[i] < a.DH2));   // F.pad rows of x: 0
-        const long long pos = d_from_x ? ((long long)pcb[i] * a.DH2 + pqh[i]) * a.DW2 + pqw[i]
-                                       : ((long long)pcb[i] * a.Qh + pqh[i]) * a.Qw + pqw[i];
-        const _Float16* p = ok ? d_src + pos * (2 * a.djh) + d_c : d_zero;
-        S.dq[i] = *reinterpret_cast<const u32x4*>(p);
-        S.dq[2 + i] = *reinterpret_cast<const u32x4*>(ok ? p + d_plane : d_zero);
-      }
-    } else {
-#pragma unroll
-      for (int j = 0; j < RJ; ++j) {
-        if constexpr (SD != 0) S.rd[RJ * hh + j] = bload_raw16(rdr, vd, (srow + j) * ds);
-        else S.rd[RJ * hh + j] = bload<0>(rdr, vd, (srow + j) * ds);
-      }
+    for (int j = 0; j < RJ; ++j) {
+      if constexpr (SD != 0) S.rd[RJ * hh + j] = bload_raw16(rdr, vd, (srow + j) * ds);
+      else S.rd[RJ * hh + j] = bload<0>(rdr, vd, (srow + j) * ds);
     }
     advance();
    }
@@ -787,14 +724,14 @@ wgrad_x3_kernel(const WgradArgs a) {
           else split2<F16>(S.rg[ig], S.rg[ig + 1], sg, h, l);
           GH[e] = h; GL[e] = l;
         }
-        if (!DPK && q < RJ / 8) {
-          const int id = RJD * hh + 8 * q + 2 * e;
+        if (q < RJ / 8) {
+          const int id = RJ * hh + 8 * q + 2 * e;
           if constexpr (SD != 0) h = S.rd[id] | (S.rd[id + 1] << 16);
           else split2<F16>(S.rd[id], S.rd[id + 1], sd, h, l);
           DH[e] = h; DL[e] = l;
         }
       }
-      if (!DPK && q < RJ / 8) {
+      if (q < RJ / 8) {
         const int offd = wx3_off(ml, (rbase & 127) / 8 + q);
         *reinterpret_cast<u32x4*>(dbase + offd) = DH;
         if constexpr (PL == 2) *reinterpret_cast<u32x4*>(dbase + PLANE + offd) = DL;
@@ -803,15 +740,6 @@ wgrad_x3_kernel(const WgradArgs a) {
         const int offg = wx3_off(ml, (rbase_g & 127) / 8 + q);
         *reinterpret_cast<u32x4*>(gbase + offg) = GH;
         if constexpr (PL == 2) *reinterpret_cast<u32x4*>(gbase + PLANE + offg) = GL;
-      }
-    }
-    if constexpr (DPK) {   // joined row block dch >> 4, chunk dch & 15 of positions dpa, dpa + 16
-      unsigned char* db = base + (DPL + 2 * (dch >> 4)) * PLANE;
-#pragma unroll
-      for (int i = 0; i < 2; ++i) {
-        const int off = wx3_off(dpa + 16 * i, dch & 15);
-        *reinterpret_cast<u32x4*>(db + off) = S.dq[i];
-        *reinterpret_cast<u32x4*>(db + PLANE + off) = S.dq[2 + i];
       }
     }
    }
@@ -1042,12 +970,7 @@ gather_x6_kernel(const GatherArgs a) {
   }
   struct Stage { float ra[AJ]; u32x4 rw[3]; };
   Stage s0, s1;
-  auto uniform_ptr = [](const void* p) __attribute__((always_inline)) {
-    const unsigned long long v = (unsigned long long)p;
-    const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)v);
-    const unsigned hi = __builtin_amdgcn_readfirstlane((unsigned)(v >> 32));
-    return (void*)(((unsigned long long)hi << 32) | lo);
-  };
+  using se::uniform_ptr;
   const int b0 = m0 / (a.Qh * a.Qw);
   const int cpb = JG ? 2 * a.jh : a.Cg;           // channels per batch item of X
   const long long H2W2 = (long long)a.H2 * a.W2;

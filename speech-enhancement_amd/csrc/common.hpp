@@ -19,6 +19,22 @@ namespace se {
 
 constexpr int kWave = 64;
 
+// A 64-bit pointer from its two 32-bit words. Both words are unsigned: widening a
+// signed low word (what __builtin_amdgcn_readfirstlane returns) sign-extends any
+// address whose low word is >= 2^31 into the high word (the d630867 fault in the
+// chunked stencil). tests/test_uniform_ptr_cpu.py checks this on the host.
+__host__ __device__ __forceinline__ unsigned long long ptr_from_words(unsigned lo, unsigned hi) {
+  return ((unsigned long long)hi << 32) | lo;
+}
+
+// p made provably wave-uniform (readfirstlane on both halves) for a buffer resource
+// base; otherwise hipcc wraps every buffer op in a waterfall loop.
+__device__ __forceinline__ void* uniform_ptr(const void* p) {
+  const unsigned long long v = (unsigned long long)p;
+  return (void*)ptr_from_words((unsigned)__builtin_amdgcn_readfirstlane((unsigned)v),
+                               (unsigned)__builtin_amdgcn_readfirstlane((unsigned)(v >> 32)));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -37,8 +53,7 @@ __device__ __forceinline__ float wave_max(float v) {
   return v;
 }
 
-// SE_MATH_F16X3 operand scaling (the conv GEMMs, and the producers that write their
-// operands pre-split in CL16 form): a tensor with max |x| <= *amax < 2^e is
+// SE_MATH_F16X3 operand scaling (the conv and LSTM GEMMs): a tensor with max |x| <= *amax < 2^e is
 // multiplied by s = 2^(kF16Top - e), so every scaled value is below 2^14 (fp16 max
 // 65504), then split as hi = fp16(x s), lo = fp16(x s - hi) (x s - hi is exact).
 constexpr int kF16Top = 14;

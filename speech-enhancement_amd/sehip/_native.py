@@ -36,11 +36,9 @@ class ConvDesc(ctypes.Structure):
         "dil_h", "dil_w", "out_pad_h", "out_pad_w", "transposed",
         "complex_weights", "pad_h_end", "pad_w_end", "math")] + [
         ("x_amax", c_void_p), ("dy_amax", c_void_p),   # SE_MATH_F16X3 scale sources (or NULL)
-        ("x_packed", c_void_p), ("x2_packed", c_void_p), ("dy_packed", c_void_p),   # CL16 operands (or NULL)
         ("w_amax", c_void_p),   # SE_MATH_F16X3 bound of max |w| (or NULL)
         ("dtype", c_int),           # SE_DTYPE_* storage of the conv's tensors (ABI 4)
-        ("data_weights", c_void_p),   # prepared data-grad weight image (or NULL, ABI 5)
-        ("x2_amax", c_void_p)]        # joined CL16 operands: the bound of x (x2_packed) (ABI 7)
+        ("data_weights", c_void_p)]   # prepared data-grad weight image (or NULL, ABI 5)
 
 
 class FirstConvDesc(ctypes.Structure):
@@ -61,7 +59,7 @@ class GemmDesc(ctypes.Structure):
 
 
 _P = c_void_p
-ABI_VERSION = 7   # SEHIP_ABI_VERSION (include/sehip.h)
+ABI_VERSION = 8   # SEHIP_ABI_VERSION (include/sehip.h)
 CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
@@ -75,8 +73,6 @@ _SIGNATURES = {
     "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
     "se_amax": (c_int, [_P, ctypes.c_longlong, _P, _P]),
     "se_amax_weights": (c_int, [_P, ctypes.c_longlong, _P, _P, _P]),
-    "se_pack_cl16_bytes": (c_size_t, [c_int] * 4),
-    "se_pack_cl16": (c_int, [_P] + [c_int] * 4 + [_P, _P, _P]),
     "se_mix_snr": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P, _P]),
     "se_crop_pad": (c_int, [_P, _P, _P, _P, c_int, c_int, _P, _P]),
     "se_pcm16_to_float": (c_int, [_P, ctypes.c_longlong, _P, _P]),
@@ -93,7 +89,7 @@ _SIGNATURES = {
     "se_conv2d_bwd_weight_joined": (c_int, [_P, _P, c_int, c_int] + [_P] * 6 + [_P, c_size_t, _P]),
     "se_cbn_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "se_cbn_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _PP, _PP, _P, _P, c_int, c_float, c_float, c_int,
-                           c_float, _P, _P, _P, c_int, _P, c_size_t, _P]),
+                           c_float, _P, _P, c_int, _P, c_size_t, _P]),
     "se_cbn_bwd": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
                            c_int, _P, c_size_t, _P]),
     "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
@@ -136,7 +132,7 @@ _SIGNATURES = {
     "se_ccbam_workspace_size": (c_size_t, [c_int] * 3),
     "se_ccbam_channel_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
     "se_ccbam_spatial_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
-    "se_ccbam_apply": (c_int, [_P] * 6 + [c_int] * 3 + [_P]),
+    "se_ccbam_apply": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_sa": (c_int, [_P] * 2 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_sa_sigmoid": (c_int, [_P] * 3 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_dca": (c_int, [_P] * 5 + [c_int] * 3 + [_P, c_size_t, _P]),

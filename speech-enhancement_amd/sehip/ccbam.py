@@ -117,7 +117,7 @@ class _CCBAMFn(torch.autograd.Function):
     (and CBN's HIP kernels) are used unchanged."""
 
     @staticmethod
-    def forward(ctx, x, mod, pack, *params):
+    def forward(ctx, x, mod, *params):
         N.require_device(x)
         x = x.contiguous()
         B, C, H, W = x.shape
@@ -157,14 +157,10 @@ class _CCBAMFn(torch.autograd.Function):
         out = torch.empty_like(x)
         xa = F.amax_get(x)
         oa = xa + 1.0 if xa is not None else None   # ca, sa in (0, 1): |x ca + sa| <= max |x| + 1
-        # the CL16 copy of out for the decoder's joined weight-grad (scaled by oa)
-        pk = F.new_cl16(x) if pack and oa is not None and C % 8 == 0 else None
         _call(lib.se_ccbam_apply, "se_ccbam_apply", x.data_ptr(), ca.data_ptr(), sa.data_ptr(),
-              out.data_ptr(), N.ptr(pk), N.ptr(oa if pk is not None else None), B, C, HW, st)
+              out.data_ptr(), B, C, HW, st)
         if oa is not None:   # F16X3 scale source of the consumers
             F.amax_put(out, oa)
-        if pk is not None:
-            F.cl16_put(out, pk, oa)
         if need_grad:
             ctx.save_for_backward(x, idx, amax)
             ctx.graphs = (pooled, ca, Pl, z, sa)
@@ -212,7 +208,7 @@ class _CCBAMFn(torch.autograd.Function):
         grads = {id(p): g for p, g in zip(sp, gs[1:])}
         grads.update({id(p): g for p, g in zip(ch, gc[1:])})
         del ctx.graphs
-        return (dx, None, None) + tuple(grads.get(id(p)) for p in mod.parameters())
+        return (dx, None) + tuple(grads.get(id(p)) for p in mod.parameters())
 
 
 class CCBAM(nn.Module):
@@ -224,11 +220,8 @@ class CCBAM(nn.Module):
         self.channel_attention_branch = ChannelAttention(feature_map_channels, reduction)
         self.spatial_attention_branch = SpatialAttention()
 
-    def forward(self, x, pack: bool = False):
-        """pack=True: also write the output's CL16 copy for a consuming joined conv's
-        weight-grad (functional.cl16_put; training, fp32 only)."""
-        # cl16_wanted reads the grad mode, which is off inside the Function's forward
-        return _CCBAMFn.apply(x, self, bool(pack) and F.cl16_wanted(x), *self.parameters())
+    def forward(self, x):
+        return _CCBAMFn.apply(x, self, *self.parameters())
 
     def forward_unfused(self, x):
         """The reference's op-by-op formulation (PyTorch device ops)."""

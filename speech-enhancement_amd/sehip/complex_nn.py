@@ -345,26 +345,26 @@ class ComplexBatchNorm2d(nn.Module):
                 self.Wrr.fill_(1); self.Wii.fill_(1)
                 self.Wri.uniform_(-.9, +.9)
 
-    def forward_act(self, x, act=F.ACT_NONE, slope=0.0, fork=False, prelu=None, pack=False):
+    def forward_act(self, x, act=F.ACT_NONE, slope=0.0, fork=False, prelu=None):
         """BN followed by a fused activation (LeakyReLU / ReLU, or the weight of a
         one-parameter nn.PReLU). fork=True returns (y, alias of y) for two consumers
         (see functional.complex_batch_norm). x may be fp32, bf16 or fp16 storage, with
         the module in the same dtype (model.to(bfloat16) / .half()). A module whose dtype
         differs from x's (e.g. an fp32 module fed bf16 activations under autocast) runs
-        its kernels on x cast to the module dtype and returns the result in x's dtype,
-        as the reference's pure-torch CBN computes in the promoted type. pack=True: y's
-        CL16 copy for a consuming joined conv's weight-grad (functional.cl16_put)."""
+        its kernels on x cast to the module dtype and returns the result in the promoted
+        type of x and the parameters, as the reference's pure-torch CBN does (its
+        `Zrr * xr + ... + Br` promotes against the fp32 parameters, complex_nn.py:300-320)."""
         mdt = _module_dtype(self, x.dtype)
         if mdt != x.dtype:
             y = self.forward_act(x.to(mdt), act, slope, False, None if prelu is None else prelu.to(mdt))
-            y = y.to(x.dtype)
+            y = y.to(torch.promote_types(x.dtype, mdt))
             return (y, y) if fork else y
         running = (self.RMr, self.RMi, self.RVrr, self.RVri, self.RVii) if self.track_running_stats else None
         training = self.training or not self.track_running_stats    # complex_nn.py:234
         return F.complex_batch_norm(
             x, self.Wrr, self.Wri, self.Wii, self.Br, self.Bi, running,
             self.num_batches_tracked if self.track_running_stats else None,
-            training, self.eps, self.momentum, act, slope, fork, prelu, pack)
+            training, self.eps, self.momentum, act, slope, fork, prelu)
 
     def forward(self, inputs):
         return self.forward_act(inputs)
@@ -381,21 +381,20 @@ def _module_dtype(m: nn.Module, default):
     return default
 
 
-def norm_act(norm: nn.Module, act: nn.Module, x, fork: bool = False, pack: bool = False):
+def norm_act(norm: nn.Module, act: nn.Module, x, fork: bool = False):
     """act(norm(x)) with the activation fused into the CBN kernel when both are
     the kinds the kernel knows; otherwise the two modules are applied in turn.
     fork=True returns (y, y2) for two consumers of y: with the CBN kernel y2 is an
-    alias whose gradient the CBN backward sums itself; otherwise y2 is y. pack=True: the
-    CBN kernel also writes y's CL16 copy (ComplexBatchNorm2d.forward_act)."""
+    alias whose gradient the CBN backward sums itself; otherwise y2 is y."""
     if isinstance(norm, ComplexBatchNorm2d):     # forward_act casts a dtype mismatch itself
         if isinstance(act, nn.LeakyReLU):
-            return norm.forward_act(x, F.ACT_LEAKY, act.negative_slope, fork, pack=pack)
+            return norm.forward_act(x, F.ACT_LEAKY, act.negative_slope, fork)
         if isinstance(act, nn.ReLU):
-            return norm.forward_act(x, F.ACT_RELU, 0.0, fork, pack=pack)
+            return norm.forward_act(x, F.ACT_RELU, 0.0, fork)
         if isinstance(act, nn.Identity):
-            return norm.forward_act(x, fork=fork, pack=pack)
+            return norm.forward_act(x, fork=fork)
         if isinstance(act, nn.PReLU) and act.weight.numel() == 1:
-            return norm.forward_act(x, fork=fork, prelu=act.weight, pack=pack)   # DCCRN, dccrn.py:21,45
+            return norm.forward_act(x, fork=fork, prelu=act.weight)   # DCCRN, dccrn.py:21,45
     y = act(norm(x))
     return (y, y) if fork else y
 

@@ -212,47 +212,6 @@ def amax_of(t: torch.Tensor) -> torch.Tensor:
     return a
 
 
-# --------------------------------------------------------------------------
-# CL16 copies (se_pack_cl16 layout: scaled hi / lo fp16 planes, channels innermost)
-# of the decoder's joined-conv inputs, written by their producers in the pass that
-# makes them (ComplexBN forward: se_cbn_fwd's y_packed; CCBAM: se_ccbam_apply's
-# out_packed), each with its own bound. The joined conv's weight-grad then reads its
-# D operand pre-split (se_conv2d_desc.x_packed / x2_packed). Keyed like the amax
-# table (address, storage weakref, shape, version); an entry holds its buffer until
-# the tensor's storage dies, and dead entries are dropped at every insertion.
-# --------------------------------------------------------------------------
-_CL16: dict = {}
-CL16_CALLS = [0, 0]   # [copies written, weight-grads that read them] (tests)
-
-
-def cl16_wanted(x: torch.Tensor) -> bool:
-    """Whether a producer should write the CL16 copy of its fp32 output x: a split-fp16
-    weight-grad will read it (gradients enabled, weight pass in f16x3) and SEHIP_CL16=1.
-    Off by default: at the FRCRN bench step the copies cost their producers more than the
-    weight-grads gain (110 vs 102 ms per step, same box)."""
-    return (x.is_cuda and x.dtype == torch.float32 and torch.is_grad_enabled()
-            and _CONV_MATH["weight"] == F16X3 and os.environ.get("SEHIP_CL16", "0") == "1")
-
-
-def new_cl16(x: torch.Tensor) -> torch.Tensor:
-    return torch.empty(2 * x.numel(), dtype=torch.float16, device=x.device)
-
-
-def cl16_put(t: torch.Tensor, buf: torch.Tensor, amax: torch.Tensor) -> None:
-    for k in [k for k, e in _CL16.items() if e[2].expired()]:
-        del _CL16[k]
-    _CL16[t.data_ptr()] = (buf, amax, StorageWeakRef(t.untyped_storage()), tuple(t.shape), t._version)
-    CL16_CALLS[0] += 1
-
-
-def cl16_get(t: torch.Tensor):
-    """(CL16 buffer, its bound) registered for t, or None."""
-    e = _CL16.get(t.data_ptr())
-    if e is None or e[2].expired() or e[3] != tuple(t.shape) or e[4] != t._version:
-        return None
-    return e[0], e[1]
-
-
 def new_amax(device) -> torch.Tensor:
     return torch.empty(1, device=device, dtype=torch.float32)
 
@@ -397,12 +356,31 @@ def _data_weights_of(ctx, d) -> int | None:
     return img[0].data_ptr()
 
 
+def _check_weights(in_channels, out_channels, kernel, transposed, wr, wi, br, bi):
+    """The kernels read the weights at the shape the descriptor implies: refuse a mismatch
+    the way nn.Conv2d / nn.ConvTranspose2d do (RuntimeError) instead of reading past them.
+    conv: [Cout, Cin, kh, kw]; convT: [Cin, Cout, kh, kw]; complex: each of wr / wi at half
+    of both channel counts (complex_nn.py:67-91)."""
+    h = 2 if wi is not None else 1
+    ci, co = in_channels // h, out_channels // h
+    want = (ci, co, *kernel) if transposed else (co, ci, *kernel)
+    for w in (wr, wi):
+        if w is not None and tuple(w.shape) != want:
+            raise RuntimeError(f"sehip conv2d: weight of size {list(w.shape)}, expected {list(want)} for an input "
+                               f"with {in_channels} channels ({'transposed, ' if transposed else ''}"
+                               f"{out_channels} output channels)")
+    for b in (br, bi):
+        if b is not None and tuple(b.shape) != (co,):
+            raise RuntimeError(f"sehip conv2d: bias of size {list(b.shape)}, expected [{co}]")
+
+
 class _Conv2d(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, wr, wi, br, bi, geom):
         (out_channels, kernel, stride, padding, dilation, output_padding, transposed, complex_w,
          padding_end, exact, force_math) = geom
         N.require_device(x, wr, wi, br, bi, dtype=x.dtype)
+        _check_weights(x.shape[1], out_channels, kernel, transposed, wr, wi, br, bi)
         x = x.contiguous()
         d = conv_desc(tuple(x.shape), out_channels, kernel, stride, padding, dilation,
                       output_padding, transposed, complex_w, padding_end, exact)
@@ -505,6 +483,7 @@ class _ConvJoined(torch.autograd.Function):
     def forward(ctx, x, s, wr, wi, br, bi, geom):
         out_channels, kernel, stride, padding, dilation, output_padding, transposed = geom
         N.require_device(x, s, wr, wi, br, bi)
+        _check_weights(2 * s.shape[1], out_channels, kernel, transposed, wr, wi, br, bi)
         x, s = x.contiguous(), s.contiguous()
         B, Cs, F_, T = s.shape
         Fx, Tx = x.shape[2], x.shape[3]
@@ -535,8 +514,6 @@ class _ConvJoined(torch.autograd.Function):
                        4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
         ctx.save_for_backward(x, s, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax, ctx.w_amax = d, nbytes, br is not None, xa, wa
-        px, ps = cl16_get(x), cl16_get(s)   # CL16 copies from the producers (weight-grad D operand)
-        ctx.pk = (px, ps) if px is not None and ps is not None and any(ctx.needs_input_grad[2:4]) else None
         ctx.data_img = (_prep_data_weights(d, wr, wi, wa) if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
                         else None)
         return y
@@ -573,10 +550,7 @@ class _ConvJoined(torch.autograd.Function):
                 _TIMER.end(_gemm_tag("data", d, joined=True), t0, _conv_flops(d),
                            4.0 * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))
         if any(ctx.needs_input_grad[2:6]):
-            pk = ctx.pk if _pass_math("weight", d) == F16X3 else None
-            ctx.pk = None
-            extra = (pk[0][0], pk[0][1], pk[1][0], pk[1][1]) if pk is not None else ()
-            with _wgrad_stream(x, s, gy, xa, ga, *extra):
+            with _wgrad_stream(x, s, gy, xa, ga):
                 if _DEFER is not None:
                     ws = _workspace(ctx.nbytes, gy.device)
                 st = N.stream_of(gy)
@@ -586,20 +560,9 @@ class _ConvJoined(torch.autograd.Function):
                     dbr = torch.empty(nb, device=gy.device, dtype=gy.dtype)
                     dbi = torch.empty(nb, device=gy.device, dtype=gy.dtype)
                 t0 = _TIMER.begin() if _TIMER else None
-                rc = SE_E_UNSUPPORTED
-                if pk is not None:   # D pre-split: s in x_packed (its bound), x in x2_packed (its bound)
-                    d.x_packed, d.x_amax, d.x2_packed, d.x2_amax = (pk[1][0].data_ptr(), pk[1][1].data_ptr(),
-                                                                    pk[0][0].data_ptr(), pk[0][1].data_ptr())
-                    rc = lib.se_conv2d_bwd_weight_joined(_with_math(d, "weight"), x.data_ptr(), Fx, Tx, s.data_ptr(),
-                                                         gy.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr),
-                                                         N.ptr(dbi), ws.data_ptr(), ws.numel(), st)
-                    d.x_packed = d.x2_packed = d.x2_amax = None
-                    d.x_amax = N.ptr(xa)
-                    CL16_CALLS[1] += rc == 0
-                if rc == SE_E_UNSUPPORTED:
-                    rc = lib.se_conv2d_bwd_weight_joined(_with_math(d, "weight"), x.data_ptr(), Fx, Tx, s.data_ptr(),
-                                                         gy.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr),
-                                                         N.ptr(dbi), ws.data_ptr(), ws.numel(), st)
+                rc = lib.se_conv2d_bwd_weight_joined(_with_math(d, "weight"), x.data_ptr(), Fx, Tx, s.data_ptr(),
+                                                     gy.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr),
+                                                     N.ptr(dbi), ws.data_ptr(), ws.numel(), st)
                 if rc == SE_E_UNSUPPORTED:
                     rc = lib.se_conv2d_bwd_weight(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), gy.data_ptr(),
                                                   dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr), N.ptr(dbi),
@@ -682,7 +645,7 @@ class _ComplexBN(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum, act, slope,
-                fork=False, prelu=None, pack=False):
+                fork=False, prelu=None):
         N.require_device(x, dtype=x.dtype)
         N.require_device(wrr, wri, wii, br, bi, prelu, *(running or ()), dtype=x.dtype)
         dt = N.dtype_code(x)
@@ -699,21 +662,17 @@ class _ComplexBN(torch.autograd.Function):
             act, slope = ACT_LEAKY, 0.0
         # bound of max |y| for an f16x3 consumer (fp32 storage only)
         ya = new_amax(x.device) if training and dt == 0 else None
-        # the CL16 copy of y for a consumer's split-fp16 weight-grad (se_cbn_fwd's y_packed)
-        pk = new_cl16(x) if pack and ya is not None and (c // 2) % 8 == 0 else None
         t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_cbn_fwd(x.data_ptr(), y.data_ptr(), b, c, hw,
                                N.ptr_array(params), N.ptr_array(running), N.ptr(nbt),
                                save.data_ptr(), int(training), float(eps), mom, int(act),
-                               float(slope), N.ptr(ya), N.ptr(prelu), N.ptr(pk), dt, ws.data_ptr(), ws.numel(),
+                               float(slope), N.ptr(ya), N.ptr(prelu), dt, ws.data_ptr(), ws.numel(),
                                N.stream_of(x)),
                 "se_cbn_fwd")
         if ya is not None:
             amax_put(y, ya)
-        if pk is not None:
-            cl16_put(y, pk, ya)
-        if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write (+ the CL16 write)
-            _TIMER.end("cbn_fwd", t0, 0.0, x.element_size() * x.numel() * ((3 if training else 2) + (pk is not None)))
+        if t0 is not None:   # 1 read for the moments (training) + 1 read + 1 write
+            _TIMER.end("cbn_fwd", t0, 0.0, x.element_size() * x.numel() * (3 if training else 2))
         ctx.save_for_backward(x, save, prelu, *(params or ()))   # y is not needed: se_cbn_bwd recomputes act' from x
         ctx.cfg = (int(training), int(act), float(slope), params is not None)
         if fork:   # (y, alias of y): two consumers, two gradients summed inside se_cbn_bwd2
@@ -757,20 +716,18 @@ class _ComplexBN(torch.autograd.Function):
         if t0 is not None:   # (gy [, gy2], x) read twice + dx written
             _TIMER.end("cbn_bwd", t0, 0.0, x.element_size() * x.numel() * (5 if gy2 is None else 7))
         g = dparams or [None] * 5
-        return (dx, *g, None, None, None, None, None, None, None, None, dprelu, None)
+        return (dx, *g, None, None, None, None, None, None, None, None, dprelu)
 
 
 def complex_batch_norm(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
-                       act=ACT_NONE, slope=0.0, fork=False, prelu=None, pack=False):
+                       act=ACT_NONE, slope=0.0, fork=False, prelu=None):
     """ComplexBatchNorm2d forward (+ optional fused activation) on the HIP path.
     running: (RMr, RMi, RVrr, RVri, RVii) or None; nbt: int64 tensor or None.
     prelu: the weight of a one-parameter nn.PReLU applied after the norm (fused).
     fork=True returns (y, alias of y) for two consumers: their two gradients are summed inside
-    the backward kernels (se_cbn_bwd2) instead of by autograd's accumulation add.
-    pack=True also writes y's CL16 copy (cl16_put) where a split-fp16 weight-grad will
-    read it (training, fp32)."""
+    the backward kernels (se_cbn_bwd2) instead of by autograd's accumulation add."""
     return _ComplexBN.apply(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
-                            act, slope, fork, prelu, pack and training and cl16_wanted(x))
+                            act, slope, fork, prelu)
 
 
 class _FirstBlock(torch.autograd.Function):
@@ -812,7 +769,7 @@ class _FirstBlock(torch.autograd.Function):
         t0 = _TIMER.begin() if _TIMER else None
         N.check(lib.se_cbn_fwd(y0.data_ptr(), y.data_ptr(), b, c, hw, N.ptr_array(params), N.ptr_array(running),
                                N.ptr(nbt), save.data_ptr(), 1, float(eps), mom, int(act), float(slope), ya.data_ptr(),
-                               None, None, 0, ws.data_ptr(), ws.numel(), N.stream_of(x0)), "se_cbn_fwd")
+                               None, 0, ws.data_ptr(), ws.numel(), N.stream_of(x0)), "se_cbn_fwd")
         if t0 is not None:
             _TIMER.end("cbn_fwd", t0, 0.0, 4.0 * y0.numel() * 3)
         amax_put(y, ya)

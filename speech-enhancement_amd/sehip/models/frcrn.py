@@ -88,16 +88,15 @@ class _CausalConvBase(nn.Module):
                              slope, kernel=c.kernel_size, stride=c.stride, padding=begin, padding_end=end,
                              dilation=c.dilation, fork=fork)
 
-    def forward_joined(self, x, skip, pack: bool = False):
+    def forward_joined(self, x, skip):
         """self(complex_join(x, skip)) (frcrn.py:95-101) without writing the
-        joined tensor: the conv GEMMs gather from x and skip directly. pack=True: the
-        output feeds another joined conv, whose weight-grad reads its CL16 copy."""
+        joined tensor: the conv GEMMs gather from x and skip directly."""
         conv = self._conv()
         if self.padding[1] or not isinstance(conv, (ComplexConv2d, ComplexConvTranspose2d)) \
                 or x.shape[1] != skip.shape[1]:
             return self(F.complex_join(x, skip))
         y = conv.forward_joined(x, skip)
-        return norm_act(self.norm, self.act, y, pack=pack)
+        return norm_act(self.norm, self.act, y)
 
     def forward_joined_head(self, x, skip, head: nn.Conv2d):
         """head(self(complex_join(x, skip))) for FRCRN's final_conv (frcrn.py:115, 140):
@@ -220,7 +219,7 @@ class Decoder(nn.Module):
         j = len(self.skip_connection_attention_layers) - 1 - i
         with torch.cuda.stream(side):
             skip.record_stream(side)
-            state[0][j] = self.skip_connection_attention_layers[j](skip, pack=True)
+            state[0][j] = self.skip_connection_attention_layers[j](skip)
             ev = torch.cuda.Event()
             ev.record(side)
             state[1][j] = ev   # the decoder waits per gate, not for all six
@@ -248,7 +247,7 @@ class Decoder(nn.Module):
                 skip = gated.pop()
                 skip.record_stream(main)
             else:
-                skip = attention(encoder_outputs.pop(), pack=True)
+                skip = attention(encoder_outputs.pop())
             # frcrn.py:95-99: x[..., :-1] if wider, F.pad(x, (0, 0, 0, 1)) if shorter, then
             # complex_concat([x, skip]): folded into the convT's GEMMs (se_conv2d_*_joined);
             # modes without a joined kernel materialise it in one pass (se_complex_join)
@@ -256,7 +255,7 @@ class Decoder(nn.Module):
                 raise ValueError(f"decoder/skip grids do not align: {tuple(x.shape)} vs {tuple(skip.shape)}")
             if head is not None and layer is self.layers[-1]:
                 return layer.forward_joined_head(x, skip, head)
-            x = layer.forward_joined(x, skip, pack=layer is not self.layers[-1])
+            x = layer.forward_joined(x, skip)
         return real_conv2d(head, x) if head is not None else x
 
 

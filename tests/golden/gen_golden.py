@@ -210,6 +210,40 @@ def gen_models():
         save(f"model_{name}", **out)
 
 
+def variant_cases():
+    """Drop-in constructor variants beyond the BASELINE configs:
+    (name, reference constructor, input length, batch). DCCRN masks 'R' / 'C'
+    (_2008_00264_dccrn.py:127-132,188-193) and bidirectional=True (:124,143, LSTMBlock
+    :60-64); DCUNet-10 / -20 / -20-large (architectures.py:55-98), the last at the
+    reference's own test.py settings (1024/256/1024, 2 s, test.py:8-19); the real-valued
+    (is_complex=False) DCCRN."""
+    return [
+        ("dccrn_r", lambda: R_dccrn.DCCRN("dccrn-R", 400, 100, 512), 16000, 1),
+        ("dccrn_c", lambda: R_dccrn.DCCRN("dccrn-C", 400, 100, 512), 16000, 1),
+        ("dccrn_bi", lambda: R_dccrn.DCCRN("dccrn-CL", 400, 100, 512, bidirectional=True), 16000, 1),
+        ("dccrn_real", lambda: R_dccrn.DCCRN("dccrn-CL", 400, 100, 512, is_complex=False), 16000, 1),
+        ("dcunet10", lambda: R_dcunet.DCUNet("dcunet10", 512, 128, 512), 32000, 1),
+        ("dcunet20", lambda: R_dcunet.DCUNet("dcunet20", 512, 128, 512), 32000, 1),
+        ("dcunet20_large", lambda: R_dcunet.DCUNet("dcunet20-large", 1024, 256, 1024), 32000, 1),
+    ]
+
+
+def gen_variants(only=None):
+    for i, (name, ctor, L, B) in enumerate(variant_cases()):
+        if only and name not in only:
+            continue
+        noisy, _ = paramfill.structured_pair(B, L, seed=60 + i)
+        x = torch.from_numpy(noisy)
+        out = {"x": x}
+        m = paramfill.fill_(ctor(), seed=70 + i)
+        with torch.no_grad():
+            spec, wav = m.train()(x)
+            out["spec_train"], out["wav_train"] = spec, wav
+            spec, wav = m.eval()(x)
+            out["spec_eval"], out["wav_eval"] = spec, wav
+        save(f"variant_{name}", **out)
+
+
 def gen_train_step():
     """One FRCRN training step exactly as trainer.py:99-124 + 210-221."""
     noisy, clean = paramfill.structured_pair(2, 16000, seed=12)
@@ -244,7 +278,7 @@ def gen_train_step():
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["stft", "cconv", "cbn", "blocks", "models", "train"]
+    which = sys.argv[1:] or ["stft", "cconv", "cbn", "blocks", "models", "train", "variants"]
     torch.manual_seed(0)
     if "stft" in which: gen_stft()
     if "cconv" in which: gen_cconv()
@@ -252,3 +286,4 @@ if __name__ == "__main__":
     if "blocks" in which: gen_blocks()
     if "models" in which: gen_models()
     if "train" in which: gen_train_step()
+    if "variants" in which: gen_variants()

@@ -2,6 +2,7 @@
 include/sehip.h declares, and its host-side planning/validation entry points
 (no kernel launches) behave like the reference's shape rules."""
 import ctypes
+import os
 
 import pytest
 import torch
@@ -186,10 +187,37 @@ def test_ccbam_and_join_validation_need_no_gpu():
     # (x, mean, max, amax, B, C, HW, stream): odd C -> SE_E_SHAPE, null -> SE_E_ARG
     assert lib.se_ccbam_channel_pool(None, None, None, None, 2, 7, 10, None) == -2
     assert lib.se_ccbam_channel_pool(None, None, None, None, 2, 8, 10, None) == -1
-    assert lib.se_ccbam_apply(None, None, None, None, None, None, 0, 8, 10, None) == -1
+    assert lib.se_ccbam_apply(None, None, None, None, 2, 8, 10, None) == -1
     ws = lib.se_ccbam_workspace_size(2, 8, 10)
     assert lib.se_ccbam_bwd_dca(None, None, None, None, None, 2, 8, 10, None, ws, None) == -1
     # join: (x, Cx, Fx, Tx, s, Cs, F, T, out, B, stream)
     assert lib.se_complex_join(None, 3, 4, 5, None, 4, 4, 5, None, 1, 0, None) == -2   # odd Cx
     assert lib.se_complex_join(None, 4, 4, 5, None, 4, 4, 5, None, 1, 0, None) == -1   # null pointers
     assert lib.se_complex_join_bwd(None, None, 4, 4, 5, None, 4, 0, 5, 1, 0, None) == -1
+
+
+def test_python_call_sites_match_the_ctypes_signatures():
+    """Every `<lib>.se_*(...)` call in the host package, the tools, bench.py and the tests
+    passes as many arguments as its ctypes signature (and so the C header) declares: an ABI
+    change that misses a call site fails here on the CPU instead of on the GPU box."""
+    import ast
+    import glob
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    files = (glob.glob(os.path.join(root, "speech-enhancement_amd", "sehip", "**", "*.py"), recursive=True)
+             + glob.glob(os.path.join(root, "tools", "*.py")) + glob.glob(os.path.join(root, "tests", "*.py"))
+             + [os.path.join(root, "bench.py")])
+    bad, n = [], 0
+    for f in files:
+        for node in ast.walk(ast.parse(open(f).read())):
+            if not (isinstance(node, ast.Call) and isinstance(node.func, ast.Attribute)
+                    and node.func.attr.startswith("se_") and node.func.attr in N._SIGNATURES):
+                continue
+            if any(isinstance(a, ast.Starred) for a in node.args) or node.keywords:
+                continue
+            n += 1
+            want = len(N._SIGNATURES[node.func.attr][1])
+            if len(node.args) != want:
+                bad.append(f"{os.path.relpath(f, root)}:{node.lineno} {node.func.attr}: {len(node.args)} args, "
+                           f"signature has {want}")
+    assert n > 50, n
+    assert not bad, bad

@@ -371,3 +371,25 @@ def test_cbn_prelu_fused(dtype, tol, gpu_device):
     assert rel_l2(p.weight.grad.float().cpu().numpy(), po.weight.grad.numpy()) < tol
     for k in ("Wrr", "Wri", "Br"):
         assert rel_l2(getattr(m, k).grad.float().cpu().numpy(), getattr(mo, k).grad.numpy()) < tol, k
+
+
+def test_cbn_fp32_module_on_bf16_input_promotes(gpu_device):
+    """An fp32 ComplexBatchNorm2d fed bf16 activations (autocast-style) returns the promoted
+    type, fp32, as the reference's pure-torch CBN does (complex_nn.py:300-320: Z * x + B
+    against fp32 parameters), and is at least as close to an fp64 evaluation on the same
+    (bf16-valued) input as the oracle's own mixed-precision run. Eval mode: in training the
+    reference's fp32 running-stat lerp_ against bf16 batch means raises (complex_nn.py:250)."""
+    from sehip.complex_nn import ComplexBatchNorm2d
+    from oracle.complex_nn import ComplexBatchNorm2d as OCBN
+    gen = torch.Generator().manual_seed(9)
+    x = (torch.randn(2, 16, 9, 37, generator=gen) * 2 + 0.3).to(torch.bfloat16)
+    m = paramfill.fill_(ComplexBatchNorm2d(16), seed=4).cuda().eval()
+    y = m(x.cuda())
+    assert y.dtype == torch.float32
+    mo = paramfill.fill_(OCBN(16), seed=4).eval()
+    yo = mo(x)
+    assert yo.dtype == torch.float32
+    y64 = paramfill.fill_(OCBN(16), seed=4).double().eval()(x.double())
+    e_h = rel_l2(y.detach().cpu().numpy(), y64.detach().numpy())
+    e_o = rel_l2(yo.detach().numpy(), y64.detach().numpy())
+    assert e_h <= max(e_o, 1e-5), (e_h, e_o)

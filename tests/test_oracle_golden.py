@@ -142,6 +142,32 @@ def test_model_forward(i, case):
         assert rel_l2(wav.numpy(), g["wav_eval"]) < 1e-5, "eval wav"
 
 
+# drop-in constructor variants beyond the BASELINE configs (tests/golden/gen_golden.py
+# variant_cases: same order, seeds 70 + i)
+VARIANTS = [
+    ("dccrn_r", lambda: O_models.DCCRN("dccrn-R", 400, 100, 512)),
+    ("dccrn_c", lambda: O_models.DCCRN("dccrn-C", 400, 100, 512)),
+    ("dccrn_bi", lambda: O_models.DCCRN("dccrn-CL", 400, 100, 512, bidirectional=True)),
+    ("dccrn_real", lambda: O_models.DCCRN("dccrn-CL", 400, 100, 512, is_complex=False)),
+    ("dcunet10", lambda: O_models.DCUNet("dcunet10", 512, 128, 512)),
+    ("dcunet20", lambda: O_models.DCUNet("dcunet20", 512, 128, 512)),
+    ("dcunet20_large", lambda: O_models.DCUNet("dcunet20-large", 1024, 256, 1024)),
+]
+
+
+@pytest.mark.parametrize("i,case", list(enumerate(VARIANTS)), ids=[v[0] for v in VARIANTS])
+def test_variant_forward(i, case):
+    name, ctor = case
+    g = golden(f"variant_{name}")
+    m = paramfill.fill_(ctor(), seed=70 + i)
+    x = torch.from_numpy(g["x"])
+    with torch.no_grad():
+        for mode in ("train", "eval"):
+            spec, wav = (m.train() if mode == "train" else m.eval())(x)
+            assert rel_l2(spec.numpy(), g[f"spec_{mode}"]) < 1e-5, (name, mode, "spec")
+            assert rel_l2(wav.numpy(), g[f"wav_{mode}"]) < 1e-5, (name, mode, "wav")
+
+
 def test_frcrn_train_step():
     g = golden("train_step_frcrn")
     m = paramfill.fill_(O_models.FRCRN(320, 160, 640), seed=30).train()

@@ -17,9 +17,6 @@ ap.add_argument("--layers", default="enc1,dec5")
 ap.add_argument("--iters", type=int, default=5)
 ap.add_argument("--passes", default="fwd,data,weight")
 ap.add_argument("--math", default="f32,bf16x3,bf16x6", help="conv math modes to time (se_conv2d_desc.math)")
-ap.add_argument("--packed", action="store_true",
-                help="also time f16x3 with CL16 operands (se_pack_cl16 + the LDS-DMA GEMM) and check it is "
-                     "bit-identical to the unpacked f16x3 GEMM at the same scale source")
 args = ap.parse_args()
 dev = torch.device("cuda")
 for name in args.layers.split(","):
@@ -46,47 +43,6 @@ for name in args.layers.split(","):
     }
     outs = {"fwd": lambda: y, "data": lambda: dx, "weight": lambda: dwr}
     y0 = y.clone()
-    if args.packed:
-        xa = torch.zeros(1, device=dev); lib.se_amax(x.data_ptr(), x.numel(), xa.data_ptr(), st)
-        ya = torch.zeros(1, device=dev); lib.se_amax(y0.data_ptr(), y0.numel(), ya.data_ptr(), st)
-        xp = torch.empty(lib.se_pack_cl16_bytes(*shape), dtype=torch.uint8, device=dev)
-        yp = torch.empty(lib.se_pack_cl16_bytes(*y0.shape), dtype=torch.uint8, device=dev)
-        pack_x = lambda: lib.se_pack_cl16(x.data_ptr(), *shape, xa.data_ptr(), xp.data_ptr(), st)
-        pack_y = lambda: lib.se_pack_cl16(y0.data_ptr(), *y0.shape, ya.data_ptr(), yp.data_ptr(), st)
-        pack_xy = lambda: pack_x() | pack_y()
-        for pname, pk in (("fwd", pack_x), ("data", pack_y), ("weight", pack_xy)):
-            if pname not in args.passes.split(","):
-                continue
-            d.math = F._MATH_CODES["f16x3"]
-            y.copy_(y0)   # dy of the data-grad pass (the forward above overwrote y)
-            d.x_amax, d.dy_amax = xa.data_ptr(), ya.data_ptr()
-            d.x_packed = d.dy_packed = None
-            assert calls[pname]() == 0
-            torch.cuda.synchronize()
-            ref = outs[pname]().clone()
-            assert pk() == 0
-            d.x_packed, d.dy_packed = xp.data_ptr(), yp.data_ptr()
-            assert calls[pname]() == 0
-            torch.cuda.synchronize()
-            # the packed weight-grad splits M by output rows: same products, other partial sums
-            same = torch.equal(outs[pname](), ref) if pname != "weight" else \
-                f"rel-L2 {((outs[pname]() - ref).norm() / ref.norm()).item():.2e}"
-            t0 = time.perf_counter()
-            for _ in range(args.iters):
-                calls[pname]()
-            torch.cuda.synchronize()
-            dt = (time.perf_counter() - t0) / args.iters
-            t0 = time.perf_counter()
-            for _ in range(args.iters):
-                pk()
-            torch.cuda.synchronize()
-            dp = (time.perf_counter() - t0) / args.iters
-            if pname == "fwd":
-                y.copy_(y0)
-            print(f"{name:5s} {pname:6s} f16x3-packed {dt*1e3:8.2f} ms  {fl/dt/1e12:7.1f} TF  (+pack {dp*1e3:.2f} ms)"
-                  f"  vs unpacked: {same}", flush=True)
-            d.x_packed = d.dy_packed = None
-            d.x_amax = d.dy_amax = None
     for p in args.passes.split(","):
         f = calls[p]
         ref = None

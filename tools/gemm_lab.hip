@@ -1,0 +1,406 @@
+// GEMM schedule lab (not product code): the scaled split-fp16 three-term GEMM
+// C[n][m] = sum_k W[n][k] X[m][k] (hi*hi + hi*lo + lo*hi on v_mfma_f32_32x32x16_f16)
+// on operands already split and tiled in HBM, to measure what a schedule reaches
+// at the FRCRN decoder data-grad shape (M = 64 x 158 x 403, N = 256, K = 1280)
+// independently of the gather. Build: hipcc -O3 --offload-arch=gfx950 -std=c++17
+// tools/gemm_lab.hip -o gemm_lab; run: ./gemm_lab [M] [iters]
+//
+// v1: 256 x 256 tile, 8 waves (4 n x 2 m, 64 x 128 each), K-stages of 16 in a
+//     4-deep LDS ring filled by global_load_lds (16 B per lane), three stages in
+//     flight, ONE barrier per stage; the fragments of stage s + 1 are read while the
+//     MFMAs of stage s run (two fragment register sets).
+#include <hip/hip_runtime.h>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <cmath>
+#include <vector>
+#include <random>
+
+#define CHECK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s at %d\n", hipGetErrorString(e), __LINE__); exit(1); } } while (0)
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int BN = 256, BM = 256, BKS = 16;       // tile, k per stage
+constexpr int NSTAGE = 4;                          // LDS ring depth
+constexpr int PLANE_B = 256 * 32;                  // one plane: 256 rows x 32 B (16 f16)
+constexpr int OPER_B = 2 * PLANE_B;                // hi + lo = 16 KB
+constexpr int STAGE_B = 2 * OPER_B;                // W + X = 32 KB
+
+// chunk (16 B) swizzle of a 32-B row: rows 16..31 of each 32 swap their two chunks, so
+// every ds_read_b128 lane group of a 32-row fragment hits 16 distinct 16-B slots
+__host__ __device__ inline int swz(int row) { return (row >> 4) & 1; }
+
+__device__ __forceinline__ f32x16 mfma(u32x4 a, u32x4 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+
+// image layout (both operands): [tile][stage][plane][256 rows][2 chunks] (swizzled), 16 KB per
+// (tile, stage): a buffer_load ... lds of 1 KB per wave copies 32 rows straight into LDS
+struct Frags { u32x4 w[4], x[8]; };   // w[2 i + p]: W block i plane p; x[2 j + p]: X block j plane p
+
+__global__ void __launch_bounds__(512, 1)
+lab_v1(const unsigned char* __restrict__ Wimg, const unsigned char* __restrict__ Ximg, float* __restrict__ C,
+       int M, int nk, int mtiles) {
+  __shared__ __attribute__((aligned(1024))) unsigned char sm[NSTAGE * STAGE_B];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 3, wm = wave >> 2;
+  const int mt = blockIdx.x, nt = blockIdx.y;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Wimg + (size_t)nt * nk * OPER_B), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Ximg + (size_t)mt * nk * OPER_B), (short)0, 0x7FFFFFFF, 0x00020000);
+  const unsigned vo = (unsigned)(wave * 64 + lane) * 16;   // this lane's 16 B of piece j: + 8 KB j
+  typedef __attribute__((address_space(3))) void lds_t;
+  auto issue = [&](int slot, int s) __attribute__((always_inline)) {
+    unsigned char* dst = sm + (slot % NSTAGE) * STAGE_B + wave * 1024;
+    const unsigned so = (unsigned)s * OPER_B;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_t*)dst, 16, vo, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rw, (lds_t*)(dst + 8192), 16, vo, so, 8192, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_t*)(dst + OPER_B), 16, vo, so, 0, 0);
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(rx, (lds_t*)(dst + OPER_B + 8192), 16, vo, so, 8192, 0);
+  };
+  const int lr = lane & 31, lh = lane >> 5;
+  const int fc = (lh ^ swz(lr)) * 16;               // chunk byte offset of this lane's fragment half
+  const int wofs = (wn * 64 + lr) * 32 + fc, xofs = OPER_B + (wm * 128 + lr) * 32 + fc;
+  auto read_w = [&](Frags& F, int s) __attribute__((always_inline)) {
+    const unsigned char* b = sm + (s % NSTAGE) * STAGE_B;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        F.w[2 * i + p] = *reinterpret_cast<const u32x4*>(b + wofs + p * PLANE_B + 32 * i * 32);
+  };
+  auto read_x = [&](Frags& F, int s, int j) __attribute__((always_inline)) {
+    const unsigned char* b = sm + (s % NSTAGE) * STAGE_B;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      F.x[2 * j + p] = *reinterpret_cast<const u32x4*>(b + xofs + p * PLANE_B + 32 * j * 32);
+  };
+  auto read = [&](Frags& F, int s) __attribute__((always_inline)) {
+    read_w(F, s);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) read_x(F, s, j);
+  };
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  // the MFMAs of the current stage block by block (X block j outer), each block's fragment
+  // registers re-filled with the next stage's right after its six MFMAs
+  auto compute_read = [&](const Frags& F, Frags& G, int sn, bool rd) __attribute__((always_inline)) {
+    if (rd) read_w(G, sn);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][j] = mfma(F.w[2 * i + (t == 2)], F.x[2 * j + (t == 1)], acc[i][j]);
+      if (rd) read_x(G, sn, j);
+    }
+    __builtin_amdgcn_sched_group_barrier(0x100, 4, 0);     // next W fragments
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);   // block j's MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);   // next block j fragments
+    }
+  };
+  Frags F0, F1;
+  // uniform schedule (nk even, >= 4): every stage issues one (clamped) load group, so
+  // vmcnt(4) always retires exactly the stage about to be read; past the end the loads
+  // re-fetch the last stage into a slot nobody reads, and the last "next" fragments are
+  // read from a slot whose contents are never used
+  issue(0, 0);
+  issue(1, 1);
+  issue(2, 2);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  read(F0, 0);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  for (int s = 0; s < nk; s += 2) {
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(s + 3, min(s + 3, nk - 1));
+    compute_read(F0, F1, s + 1, true);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue(s + 4, min(s + 4, nk - 1));
+    compute_read(F1, F0, s + 2, true);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // epilogue: block (i, j) element r is row (n) 32 i + 4 lh + (r & 3) + 8 (r >> 2), column (m) 32 j + lr
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = mt * BM + wm * 128 + 32 * j + lr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = nt * BN + wn * 64 + 32 * i + 4 * lh + (r & 3) + 8 * (r >> 2);
+        C[(size_t)n * M + m] = acc[i][j][r];
+      }
+    }
+}
+
+// v2: the same tile, wave split and per-stage fragment pipelining, with both operands
+// REGISTER-staged as the conv gather must do it: W as pre-split 16-B pieces, X as fp32
+// [K][M] (m contiguous) loaded 8 k per thread, split into hi / lo fp16 with a power-of-two
+// scale, and written with ds_write_b128. 3-slot LDS ring (96 KB); loads two stages ahead
+// (two register sets), one barrier per stage.
+constexpr int NS2 = 3;
+__global__ void __launch_bounds__(512, 1)
+lab_v2(const unsigned char* __restrict__ Wimg, const float* __restrict__ X, float* __restrict__ C,
+       int M, int nk, float xscale, float unscale) {
+  __shared__ __attribute__((aligned(1024))) unsigned char sm[NS2 * STAGE_B];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wn = wave & 3, wm = wave >> 2;
+  const int mt = blockIdx.x, nt = blockIdx.y;
+  const __amdgpu_buffer_rsrc_t rw = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(Wimg + (size_t)nt * nk * OPER_B), (short)0, 0x7FFFFFFF, 0x00020000);
+  // X: thread -> (m = tid % 256, chunk = tid / 256), 8 consecutive k of that chunk
+  const int xm = tid & 255, xch = tid >> 8;
+  const bool mok = mt * BM + xm < M;
+  const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)(X + (size_t)mt * BM), (short)0, 0x7FFFFFFF, 0x00020000);
+  const int xvo = mok ? xm * 4 : (int)0x80000000;
+  struct Stg { u32x4 w[2]; float x[8]; };
+  auto load = [&](Stg& g, int s) __attribute__((always_inline)) {
+    const unsigned so = (unsigned)s * OPER_B;
+    g.w[0] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, tid * 16, so, 0));
+    g.w[1] = __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(rw, tid * 16 + 8192, so, 0));
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      g.x[j] = __builtin_amdgcn_raw_buffer_load_b32(rx, xvo, (16 * s + 8 * xch + j) * M * 4, 0);
+  };
+  const int xrow = xm * 32 + ((xch ^ swz(xm)) * 16);
+  auto store = [&](const Stg& g, int slot) __attribute__((always_inline)) {
+    unsigned char* b = sm + slot * STAGE_B;
+    *reinterpret_cast<u32x4*>(b + tid * 16) = g.w[0];
+    *reinterpret_cast<u32x4*>(b + 8192 + tid * 16) = g.w[1];
+    u32x4 H, L;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const float a0 = g.x[2 * e] * xscale, a1 = g.x[2 * e + 1] * xscale;
+      const _Float16 h0 = (_Float16)a0, h1 = (_Float16)a1;
+      const _Float16 l0 = (_Float16)(a0 - (float)h0), l1 = (_Float16)(a1 - (float)h1);
+      H[e] = (unsigned)__builtin_bit_cast(unsigned short, h0) | ((unsigned)__builtin_bit_cast(unsigned short, h1) << 16);
+      L[e] = (unsigned)__builtin_bit_cast(unsigned short, l0) | ((unsigned)__builtin_bit_cast(unsigned short, l1) << 16);
+    }
+    *reinterpret_cast<u32x4*>(b + OPER_B + xrow) = H;
+    *reinterpret_cast<u32x4*>(b + OPER_B + PLANE_B + xrow) = L;
+  };
+  const int lr = lane & 31, lh = lane >> 5;
+  const int fc = (lh ^ swz(lr)) * 16;
+  const int wofs = (wn * 64 + lr) * 32 + fc, xofs = OPER_B + (wm * 128 + lr) * 32 + fc;
+  auto read_w = [&](Frags& F, int slot) __attribute__((always_inline)) {
+    const unsigned char* b = sm + slot * STAGE_B;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int p = 0; p < 2; ++p)
+        F.w[2 * i + p] = *reinterpret_cast<const u32x4*>(b + wofs + p * PLANE_B + 32 * i * 32);
+  };
+  auto read_x = [&](Frags& F, int slot, int j) __attribute__((always_inline)) {
+    const unsigned char* b = sm + slot * STAGE_B;
+#pragma unroll
+    for (int p = 0; p < 2; ++p)
+      F.x[2 * j + p] = *reinterpret_cast<const u32x4*>(b + xofs + p * PLANE_B + 32 * j * 32);
+  };
+  f32x16 acc[2][4];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[i][j][r] = 0.f;
+  auto compute_read = [&](const Frags& F, Frags& G, int slot_next) __attribute__((always_inline)) {
+    read_w(G, slot_next);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+#pragma unroll
+      for (int t = 0; t < 3; ++t)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[i][j] = mfma(F.w[2 * i + (t == 2)], F.x[2 * j + (t == 1)], acc[i][j]);
+      read_x(G, slot_next, j);
+    }
+  };
+  Frags F0, F1;
+  Stg g0, g1;
+  // prologue: stages 0, 1 in LDS, 2 and 3 loading
+  load(g0, 0);
+  load(g1, 1);
+  store(g0, 0);
+  load(g0, 2);
+  store(g1, 1);
+  load(g1, 3);
+  __syncthreads();
+  {
+    read_w(F0, 0);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) read_x(F0, 0, j);
+  }
+  // iteration s: MFMAs of stage s, fragments of s + 1 (slot (s + 1) % 3), stage s + 2 stored
+  // into slot (s + 2) % 3 from registers, stage s + 4 loaded (clamped past the end)
+  int slot = 0;
+  for (int s = 0; s < nk; s += 2) {
+    const int s1 = slot == 2 ? 0 : slot + 1, s2 = s1 == 2 ? 0 : s1 + 1;
+    compute_read(F0, F1, s1);
+    store(g0, s2);
+    load(g0, min(s + 4, nk - 1));
+    __syncthreads();
+    const int s3 = s2 == 2 ? 0 : s2 + 1;
+    compute_read(F1, F0, s2);
+    store(g1, s3);
+    load(g1, min(s + 5, nk - 1));
+    __syncthreads();
+    slot = s2;
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int m = mt * BM + wm * 128 + 32 * j + lr;
+      if (m >= M) continue;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int n = nt * BN + wn * 64 + 32 * i + 4 * lh + (r & 3) + 8 * (r >> 2);
+        C[(size_t)n * M + m] = acc[i][j][r] * unscale;
+      }
+    }
+}
+
+// deterministic pseudo-random x[k][m] in (-1000, 1000), same on host and device
+__host__ __device__ inline float xval(long long k, long long m) {
+  unsigned long long h = (unsigned long long)(k * 0x9E3779B97F4A7C15ull) ^ (unsigned long long)(m * 0xC2B2AE3D27D4EB4Full);
+  h ^= h >> 29; h *= 0xBF58476D1CE4E5B9ull; h ^= h >> 32;
+  return ((float)(h & 0xFFFFFF) / 16777216.f * 2.f - 1.f) * 1000.f;
+}
+// pre-split X image element (m, k, plane): hi = fp16(xval), lo = small
+__host__ __device__ inline _Float16 ximg_val(long long m, long long k, int p) {
+  const float v = xval(k + 7777, m);
+  return p == 0 ? (_Float16)v : (_Float16)(v * 1e-3f);
+}
+__global__ void fill_ximg(unsigned char* img, int M, int nk, int mtiles) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;   // one f16 element
+  const long long total = (long long)mtiles * nk * OPER_B / 2;
+  if (i >= total) return;
+  const long long byte = 2 * i;
+  const long long tile_stage = byte / OPER_B;
+  const int rem = (int)(byte % OPER_B);
+  const int p = rem / PLANE_B, row = (rem % PLANE_B) / 32, cc = (rem % 32) / 16, e = (rem % 16) / 2;
+  const int mt = (int)(tile_stage / nk), s = (int)(tile_stage % nk);
+  const int c = cc ^ swz(row);
+  const long long m = (long long)mt * BM + row;
+  const long long k = (long long)s * BKS + 8 * c + e;
+  reinterpret_cast<_Float16*>(img)[i] = ximg_val(m, k, p);
+}
+__global__ void fill_x(float* X, int K, int M) {
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  if (i < (long long)K * M) X[i] = xval(i / M, i % M);
+}
+
+// ---------------------------------------------------------------- host
+static unsigned short f2h(float f) { _Float16 h = (_Float16)f; unsigned short u; memcpy(&u, &h, 2); return u; }
+static float h2f(unsigned short u) { _Float16 h; memcpy(&h, &u, 2); return (float)h; }
+
+// byte offset of element (row, k) of plane p in a [tile][stage][plane][256][2 chunks] image
+static size_t img_off(int tile, int nk, int row_in_tile, int k, int p) {
+  const int s = k / BKS, kk = k % BKS, c = kk / 8, e = kk % 8;
+  return ((size_t)tile * nk + s) * OPER_B + (size_t)p * PLANE_B + (size_t)row_in_tile * 32 + ((c ^ swz(row_in_tile)) * 16) + e * 2;
+}
+
+int main(int argc, char** argv) {
+  const int M = argc > 1 ? atoi(argv[1]) : 64 * 158 * 403;
+  const int iters = argc > 2 ? atoi(argv[2]) : 10;
+  const int N = 256, K = 1280, nk = K / BKS;
+  const int mtiles = (M + BM - 1) / BM, ntiles = N / BN;
+  const size_t wbytes = (size_t)ntiles * nk * OPER_B, xbytes = (size_t)mtiles * nk * OPER_B;
+  std::vector<unsigned char> hw(wbytes);
+  std::mt19937 rng(1);
+  std::uniform_real_distribution<float> U(-1.f, 1.f);
+  // random hi / lo split values written straight into the images
+  auto fill = [&](std::vector<unsigned char>& img) {
+    unsigned short* p = (unsigned short*)img.data();
+    for (size_t i = 0; i < img.size() / 2; ++i) p[i] = f2h(U(rng) * 1000.f);
+  };
+  fill(hw);
+  // lo planes small (|lo| <= ulp(hi) / 2 in a real split): rescale every second plane
+  for (size_t base = 0; base < hw.size(); base += 2 * PLANE_B)
+    for (size_t i = PLANE_B; i < 2 * PLANE_B; i += 2) { unsigned short* q = (unsigned short*)&hw[base + i]; *q = f2h(h2f(*q) * 1e-3f); }
+  unsigned char *dw, *dx; float* dc;
+  CHECK(hipMalloc(&dw, wbytes)); CHECK(hipMalloc(&dx, xbytes)); CHECK(hipMalloc(&dc, (size_t)N * M * 4));
+  CHECK(hipMemcpy(dw, hw.data(), wbytes, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(fill_ximg, dim3((unsigned)((xbytes / 2 + 255) / 256)), dim3(256), 0, 0, dx, M, nk, mtiles);
+  dim3 grid(mtiles, ntiles);
+  hipLaunchKernelGGL(lab_v1, grid, dim3(512), 0, 0, dw, dx, dc, M, nk, mtiles);
+  CHECK(hipDeviceSynchronize());
+  // check a sample of outputs against the three-term sum in double
+  std::vector<float> hc((size_t)N * M);
+  CHECK(hipMemcpy(hc.data(), dc, hc.size() * 4, hipMemcpyDeviceToHost));
+  double maxrel = 0;
+  for (int t = 0; t < 2000; ++t) {
+    const int n = rng() % N, m = rng() % M;
+    double ref = 0, mag = 0;
+    for (int k = 0; k < K; ++k) {
+      const float wh = h2f(*(unsigned short*)&hw[img_off(n / BN, nk, n % BN, k, 0)]);
+      const float wl = h2f(*(unsigned short*)&hw[img_off(n / BN, nk, n % BN, k, 1)]);
+      const float xh = (float)ximg_val(m, k, 0);
+      const float xl = (float)ximg_val(m, k, 1);
+      const double v = (double)wh * xh + (double)wh * xl + (double)wl * xh;
+      ref += v; mag += fabs(v);
+    }
+    maxrel = fmax(maxrel, fabs(hc[(size_t)n * M + m] - ref) / (mag + 1e-30));
+  }
+  printf("v1 check: max |err| / sum|terms| over 2000 samples = %.3e %s\n", maxrel, maxrel < 1e-5 ? "OK" : "FAIL");
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0)); CHECK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(lab_v1, grid, dim3(512), 0, 0, dw, dx, dc, M, nk, mtiles);
+  CHECK(hipEventRecord(e0));
+  for (int it = 0; it < iters; ++it) hipLaunchKernelGGL(lab_v1, grid, dim3(512), 0, 0, dw, dx, dc, M, nk, mtiles);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  float ms; CHECK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= iters;
+  const double fl = 2.0 * M * N * K * 3;
+  printf("v1: M %d N %d K %d: %.3f ms  %.1f TF of fp16 MFMA issue (%.3f of 2.5 PF)\n", M, N, K, ms, fl / ms / 1e9, fl / ms / 1e9 / 2500.0);
+  // ---- v2: X as fp32 [K][M], split in the kernel with scale 16 (max |x| = 1000 < 2^10)
+  float* dxf;
+  CHECK(hipMalloc(&dxf, (size_t)K * M * 4));
+  hipLaunchKernelGGL(fill_x, dim3((unsigned)(((long long)K * M + 255) / 256)), dim3(256), 0, 0, dxf, K, M);
+  hipLaunchKernelGGL(lab_v2, grid, dim3(512), 0, 0, dw, dxf, dc, M, nk, 16.f, 1.f / 16.f);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipMemcpy(hc.data(), dc, hc.size() * 4, hipMemcpyDeviceToHost));
+  double maxrel2 = 0;
+  for (int t = 0; t < 2000; ++t) {
+    const int n = rng() % N, m = rng() % M;
+    double ref = 0, mag = 0;
+    for (int k = 0; k < K; ++k) {
+      const double w = (double)h2f(*(unsigned short*)&hw[img_off(n / BN, nk, n % BN, k, 0)]) +
+                       (double)h2f(*(unsigned short*)&hw[img_off(n / BN, nk, n % BN, k, 1)]);
+      const double v = w * xval(k, m);
+      ref += v; mag += fabs(v);
+    }
+    maxrel2 = fmax(maxrel2, fabs(hc[(size_t)n * M + m] - ref) / (mag + 1e-30));
+  }
+  printf("v2 check: max |err| / sum|terms| over 2000 samples = %.3e %s\n", maxrel2, maxrel2 < 1e-5 ? "OK" : "FAIL");
+  for (int w = 0; w < 3; ++w) hipLaunchKernelGGL(lab_v2, grid, dim3(512), 0, 0, dw, dxf, dc, M, nk, 16.f, 1.f / 16.f);
+  CHECK(hipEventRecord(e0));
+  for (int it = 0; it < iters; ++it) hipLaunchKernelGGL(lab_v2, grid, dim3(512), 0, 0, dw, dxf, dc, M, nk, 16.f, 1.f / 16.f);
+  CHECK(hipEventRecord(e1));
+  CHECK(hipEventSynchronize(e1));
+  CHECK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= iters;
+  printf("v2: M %d N %d K %d: %.3f ms  %.1f TF of fp16 MFMA issue (%.3f of 2.5 PF)\n", M, N, K, ms, fl / ms / 1e9, fl / ms / 1e9 / 2500.0);
+  return (maxrel < 1e-5 && maxrel2 < 1e-5) ? 0 : 1;
+}

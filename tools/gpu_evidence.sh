@@ -2,7 +2,7 @@
 # their summaries copied into this box's profiles/ (the files bench.py reads for
 # rocprof_avg_ms_per_launch and roofline.traffic), then the default bench line (CPU baseline
 # included) against them:  gpurun --timeout 1200 -- bash tools/gpu_evidence.sh <tag> <round, e.g. r4>
-R=$GRAFT_REPO_ROOT; TAG=${1:-ev}; RND=${2:-r4}; O=$R/gpurun_out/$TAG; mkdir -p $O; cd /tmp && export TMPDIR=/tmp
+R=$GRAFT_REPO_ROOT; TAG=${1:-ev}; RND=${2:-r5}; O=$R/gpurun_out/$TAG; mkdir -p $O; cd /tmp && export TMPDIR=/tmp
 timeout -k 10 240 rocprofv3 --kernel-trace --stats --output-format csv -d $O/prof -o run -- python3 $R/bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-op-timing --no-compare > $O/prof_bench.log 2>&1 || exit $?
 B="$R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-op-timing --no-compare"
 timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch -o run --output-format csv -- python3 $B > $O/pmc_fetch.log 2>&1 || exit $?

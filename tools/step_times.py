@@ -15,7 +15,6 @@ torch.manual_seed(2023)
 model = FRCRN().to(dev).train()
 opt = make_optimizer(model)
 batches = [synthetic_pairs(64, 64000, seed=2023 + i, device=dev) for i in range(2)]
-print(f"SEHIP_CL16={os.environ.get('SEHIP_CL16', '1')}", flush=True)
 for i in range(steps):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -24,5 +23,5 @@ for i in range(steps):
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3
     print(f"step {i:2d} {ms:8.1f} ms  alloc {torch.cuda.memory_allocated() / 2**30:6.2f} GiB  "
-          f"reserved {torch.cuda.memory_reserved() / 2**30:6.2f} GiB  cl16 entries {len(SF._CL16)} "
+          f"reserved {torch.cuda.memory_reserved() / 2**30:6.2f} GiB  "
           f"amax entries {len(SF._AMAX)}", flush=True)
