@@ -171,6 +171,12 @@ typedef struct se_conv2d_desc {
    * launch runs beside nothing, instead of in the backward, where it waits for CU
    * slots behind the side stream's weight-grad GEMMs. NULL = build it in ws. */
   const void* data_weights;
+  /* ABI 8, the *_joined entry points only: the order of the joined input's channel
+   * chunks. 0: complex_concat([x, s]) = [x_re, s_re, x_im, s_im] (FRCRN / DCCRN,
+   * complex_nn.py:4-16), x_w >= in_w (x's extra columns cropped). 1: torch.cat([x, s])
+   * = [x_re, x_im, s_re, s_im] (DCUNet's decoder, _1903_03107_dcunet.py:89-93),
+   * x_w <= in_w (x zero-padded to the skip's grid, F.pad). x_h <= in_h either way. */
+  int join_cat;
 } se_conv2d_desc;
 
 /* Bytes of the data-grad weight image of d (0 on an invalid desc). */
@@ -229,20 +235,23 @@ int se_conv2d_bwd_weight(const se_conv2d_desc* d, const float* x,
 /* Decoder skip join folded into the conv GEMMs (frcrn.py:93-101: trim /
  * pad the decoder state x, complex_concat([x, s]), ConvTransposeBlock). The
  * conv input is the joined tensor [B, in_channels, in_h, in_w] with channel
- * chunks [x_re, s_re, x_im, s_im] of in_channels/4 each; it is never written.
+ * chunks [x_re, s_re, x_im, s_im] of in_channels/4 each (d->join_cat = 1: [x_re,
+ * x_im, s_re, s_im], torch.cat, DCUNet's decoder); it is never written.
  * s: [B, in_channels/2, in_h, in_w] (the CCBAM output); x: [B, in_channels/2,
  * x_h, x_w] with x_h <= in_h (missing rows read as zeros, F.pad(x, (0,0,0,1)))
- * and x_w >= in_w (extra columns unread, x[..., :-1]). Complex weights only,
- * in_channels/4 a multiple of 32. Returns SE_E_UNSUPPORTED when the math mode
- * or shape has no joined kernel (the split-bf16 / bf16 tap-uniform GEMMs have
- * one; the weight-grad only for transposed convs): the caller then
- * materialises the join (se_complex_join) and uses the plain entry points. */
+ * and x_w >= in_w (extra columns unread, x[..., :-1]); with join_cat, x_w <= in_w
+ * (missing columns read as zeros). Complex weights only, in_channels/4 a multiple
+ * of 32. 16-bit storage (d->dtype) takes the one-term math of its format.
+ * Returns SE_E_UNSUPPORTED when the math mode or shape has no joined kernel (the
+ * split-bf16 / bf16 / f16 tap-uniform GEMMs have one; the weight-grad only for
+ * transposed convs): the caller then materialises the join (se_complex_join, or a
+ * concatenation for join_cat) and uses the plain entry points. */
 int se_conv2d_fwd_joined(const se_conv2d_desc* d, const float* x, int x_h, int x_w,
                          const float* s, const float* wr, const float* wi,
                          const float* br, const float* bi, float* y, void* ws,
                          size_t ws_bytes, void* stream);
 /* gx [B, in_channels/2, x_h, x_w] (zeros in the cropped columns and no
- * contribution from the padded rows) and gs [B, in_channels/2, in_h, in_w]. */
+ * contribution from the padded rows / columns) and gs [B, in_channels/2, in_h, in_w]. */
 int se_conv2d_bwd_data_joined(const se_conv2d_desc* d, const float* dy, const float* wr,
                               const float* wi, float* gx, int x_h, int x_w, float* gs,
                               void* ws, size_t ws_bytes, void* stream);

@@ -146,6 +146,7 @@ struct GatherArgs {
   // F.pad; columns >= Wi are never read: x[..., :-1]).
   const float* X2;
   int jh, H2, W2;
+  int jcat;            // join order: 0 complex_concat [x_re, s_re, x_im, s_im], 1 torch.cat [x, s]
   // Output side (yjh > 0, data-grad): the chunks of Y go to Y (s chunks, grid
   // Ho x Wo) and Y2 (x chunks, grid YH2 x YW2; rows >= YH2 are dropped).
   float* Y2;
@@ -651,6 +652,7 @@ struct WgradArgs {
   // D holds s (2*djh channels, grid Qh x Qw), D2 holds x on DH2 x DW2.
   const float* D2;
   int djh, DH2, DW2;
+  int djcat;           // join order (GatherArgs::jcat)
   // SE_MATH_F16X3: device max |.| of G (the gathered tensor) and of D (both sources)
   const float* amax_g;
   const float* amax_d;
@@ -1219,6 +1221,7 @@ struct ConvGeom {
   const float* dy_amax;
   const float* w_amax;    // bound of max |w| from the caller (or nullptr)
   int sd;         // se_conv2d_desc.dtype (SE_DTYPE_*)
+  int jcat;       // se_conv2d_desc.join_cat
   const void* data_w;   // se_conv2d_desc.data_weights (data-grad weight image, or nullptr)
 };
 
@@ -1235,7 +1238,9 @@ static int geom_of(const se_conv2d_desc* d, ConvGeom& g) {
   g.dy_amax = d->dy_amax;
   g.w_amax = d->w_amax;
   g.sd = d->dtype;
+  g.jcat = d->join_cat;
   g.data_w = d->data_weights;
+  if (g.jcat != 0 && g.jcat != 1) return SE_E_ARG;
   if (g.math < SE_MATH_F32 || g.math > SE_MATH_F16) return SE_E_ARG;
   if (g.sd < SE_DTYPE_F32 || g.sd > SE_DTYPE_F16) return SE_E_ARG;
   // 16-bit storage runs the one-term MFMA of its own format (operands exact)
@@ -1412,6 +1417,7 @@ static inline char* align256(char* p) { return (char*)(((uintptr_t)p + 255) & ~(
 // gets the s chunks and y2 the x chunks on (yh2, yw2) (output side).
 struct JoinIO {
   const float* x2; int jh, h2, w2;
+  int cat;          // se_conv2d_desc.join_cat
   float* y2; int yjh, yh2, yw2;
   const float* s;   // weight-grad: the skip (D of a transposed conv)
 };
@@ -1495,7 +1501,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   if (pass == kData && g.data_w && g.math == SE_MATH_F16X3 && N > 64 && !g.w_amax) return SE_E_ARG;
   const int ldw = ldw_for(N, g.math);
   WeightView wv{wr, wi, g.Ci, g.Co, g.kh, g.kw, g.transposed, g.complex_w, g.sd};
-  if (g.sd != SE_DTYPE_F32 && jn) return SE_E_UNSUPPORTED;   // fp32-only forms
+  // 16-bit storage joins on the one-term tiles of its format only (the split forms read fp32)
+  if (g.sd != SE_DTYPE_F32 && jn && !(g.math == SE_MATH_BF16 || g.math == SE_MATH_F16)) return SE_E_UNSUPPORTED;
 
   char* p = align256((char*)ws);
   const float* zero = zero_page();
@@ -1567,7 +1574,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     a.ph = c.h.p; a.pw = c.w.p; a.Sh = c.h.S; a.Sw = c.w.S; a.Qh = c.h.Q; a.Qw = c.w.Q;
     a.sh = c.h.s; a.sw = c.w.s; a.Kp = c.Kp; a.ldw = ldw;
     if (jn) {
-      a.X2 = jn->x2; a.jh = jn->jh; a.H2 = jn->h2; a.W2 = jn->w2;
+      a.X2 = jn->x2; a.jh = jn->jh; a.H2 = jn->h2; a.W2 = jn->w2; a.jcat = jn->cat;
       a.Y2 = jn->y2; a.yjh = jn->yjh; a.YH2 = jn->yh2; a.YW2 = jn->yw2;
     }
     const long long M = (long long)g.B * c.h.Q * c.w.Q;
@@ -1685,7 +1692,9 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
         if (g.sd != SE_DTYPE_F32) {   // 16-bit storage: the one-term tiles of its format
 #define SE_X3_SD(NWV, F, SDV)                                                                              \
   do {                                                                                                    \
-    if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 0, NWV, F, SDV>), grid, blk, 0, st, a);          \
+    if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 1, NWV, F, SDV>), grid, blk, 0, st, a);     \
+    else if (join_out) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 2, NWV, F, SDV>), grid, blk, 0, st, a); \
+    else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 0, NWV, F, SDV>), grid, blk, 0, st, a);     \
     else hipLaunchKernelGGL((gather_x3_kernel<false, 1, 0, NWV, F, SDV>), grid, blk, 0, st, a);            \
   } while (0)
           if (g.sd == SE_DTYPE_BF16 && wide) SE_X3_SD(2, false, 1);
@@ -1869,7 +1878,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   const bool split_ok = (g.math == SE_MATH_BF16X3 || g.math == SE_MATH_BF16 || g.math == SE_MATH_F16X3 ||
                          g.math == SE_MATH_F16) && w.N % 16 == 0;
   // 16-bit storage: the one-term split tiles only (the fp32 kernels read fp32)
-  if (g.sd != SE_DTYPE_F32 && (jn || !split_ok || w.N <= kSmallWgradN || w.Np == 32))
+  if (g.sd != SE_DTYPE_F32 && (!split_ok || w.N <= kSmallWgradN || w.Np == 32))
     return SE_E_UNSUPPORTED;
   if (jn) {
     const int dcpb = 2 * jn->jh;
@@ -1911,7 +1920,7 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   a.N = w.N; a.Qh = w.Qh; a.Qw = w.Qw; a.sh = w.c.h.s; a.sw = w.c.w.s;
   a.Kp = w.c.Kp; a.Np = w.Np; a.M = w.M; a.m_per_split = w.m_per_split;
   if (jn) {
-    a.D = jn->s; a.D2 = jn->x2; a.djh = jn->jh; a.DH2 = jn->h2; a.DW2 = jn->w2;
+    a.D = jn->s; a.D2 = jn->x2; a.djh = jn->jh; a.DH2 = jn->h2; a.DW2 = jn->w2; a.djcat = jn->cat;
   }
   const bool f16 = split_ok && g.math == SE_MATH_F16X3 && w.N > 32;
   if (f16) {   // scale sources of x (conv input) and dy, unless the caller has them
@@ -1963,7 +1972,9 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.sd != SE_DTYPE_F32) {   // 16-bit storage, one term of its format
     const dim3 grid = x3_wgrad_grid(a, w);
-    if (g.sd == SE_DTYPE_BF16 && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
+    if (g.sd == SE_DTYPE_BF16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (g.sd == SE_DTYPE_F16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
+    else if (g.sd == SE_DTYPE_BF16 && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
     else if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
@@ -2029,7 +2040,9 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
 // (extra columns: x[..., :-1]); chunks of Ci/4 channels, a multiple of 32.
 int joined_geom(const ConvGeom& g, int x_h, int x_w) {
   if (!g.complex_w) return SE_E_UNSUPPORTED;
-  if (x_h <= 0 || x_w <= 0 || x_h > g.Hi || x_w < g.Wi) return SE_E_SHAPE;
+  // complex_concat (FRCRN / DCCRN): x's missing rows read 0, its extra columns are cropped;
+  // torch.cat (DCUNet): x is zero-padded to the skip's grid in both dimensions
+  if (x_h <= 0 || x_w <= 0 || x_h > g.Hi || (g.jcat ? x_w > g.Wi : x_w < g.Wi)) return SE_E_SHAPE;
   if (g.Ci % 4 || (g.Ci / 4) % 32) return SE_E_UNSUPPORTED;
   return SE_OK;
 }
@@ -2057,7 +2070,7 @@ extern "C" int se_conv2d_fwd_joined(const se_conv2d_desc* d, const float* x, int
   if ((rc = joined_geom(g, x_h, x_w))) return rc;
   if (!x || !s || !wr || !wi || !y || !ws || (br && !bi)) return SE_E_ARG;
   JoinIO jn{};
-  jn.x2 = x; jn.jh = g.Ci / 4; jn.h2 = x_h; jn.w2 = x_w;
+  jn.x2 = x; jn.jh = g.Ci / 4; jn.h2 = x_h; jn.w2 = x_w; jn.cat = g.jcat;
   return launch_gather(g, kFwd, s, wr, wi, br, bi, y, ws, ws_bytes, se::as_stream(stream), &jn);
 }
 
@@ -2071,13 +2084,13 @@ extern "C" int se_conv2d_bwd_data_joined(const se_conv2d_desc* d, const float* d
   if (!dy || !wr || !wi || !gx || !gs || !ws) return SE_E_ARG;
   hipStream_t st = se::as_stream(stream);
   JoinIO jn{};
-  jn.y2 = gx; jn.yjh = g.Ci / 4; jn.yh2 = x_h; jn.yw2 = x_w;
+  jn.y2 = gx; jn.yjh = g.Ci / 4; jn.yh2 = x_h; jn.yw2 = x_w; jn.cat = g.jcat;
   if ((rc = launch_gather(g, kData, dy, wr, wi, nullptr, nullptr, gs, ws, ws_bytes, st, &jn))) return rc;
   // x's cropped columns (x[..., :-1]) get a zero gradient
   if (x_w > g.Wi) {
-    const size_t rows = (size_t)g.B * (g.Ci / 2) * x_h;
-    if (hipMemset2DAsync(gx + g.Wi, (size_t)x_w * sizeof(float), 0, (size_t)(x_w - g.Wi) * sizeof(float),
-                         rows, st) != hipSuccess)
+    const size_t rows = (size_t)g.B * (g.Ci / 2) * x_h, es = g.sd == SE_DTYPE_F32 ? 4 : 2;
+    if (hipMemset2DAsync((char*)gx + g.Wi * es, (size_t)x_w * es, 0, (size_t)(x_w - g.Wi) * es, rows, st) !=
+        hipSuccess)
       return SE_E_LAUNCH;
   }
   return SE_OK;
@@ -2094,6 +2107,6 @@ extern "C" int se_conv2d_bwd_weight_joined(const se_conv2d_desc* d, const float*
   if (!x || !s || !dy || !dwr || !dwi || !ws || (dbr && !dbi)) return SE_E_ARG;
   if (!g.transposed) return SE_E_UNSUPPORTED;   // a plain conv would gather the join as G
   JoinIO jn{};
-  jn.s = s; jn.x2 = x; jn.jh = g.Ci / 4; jn.h2 = x_h; jn.w2 = x_w;
+  jn.s = s; jn.x2 = x; jn.jh = g.Ci / 4; jn.h2 = x_h; jn.w2 = x_w; jn.cat = g.jcat;
   return wgrad_pass(g, s, dy, dwr, dwi, dbr, dbi, ws, ws_bytes, se::as_stream(stream), &jn);
 }

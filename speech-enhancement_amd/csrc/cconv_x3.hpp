@@ -217,7 +217,7 @@ template <bool TU, int TERMS = 3, int JM = 0, int NW = 1, bool F16 = false, int 
 __global__ void __launch_bounds__(kThreads * NW, NW == 1 ? 2 : 1)
 gather_x3_kernel(const GatherArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi, or hi*hi + hi*lo + lo*hi");
-  static_assert(SD == 0 || (TERMS == 1 && JM == 0), "16-bit storage: one-term, plain tiles");
+  static_assert(SD == 0 || TERMS == 1, "16-bit storage: one-term tiles");
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   static_assert(JM == 0 || TU, "the joined gather / epilogue run on the tap-uniform path");
   constexpr int ES = SD ? 2 : 4;                  // bytes per element of X / Y
@@ -273,7 +273,7 @@ gather_x3_kernel(const GatherArgs a) {
       uniform_ptr((const char*)a.X + (long long)b0 * cpb * HiWi * ES), (short)0, 0x7FFFFFFF, 0x00020000);
   __amdgpu_buffer_rsrc_t rx2 = rx;
   if constexpr (JM == 1)
-    rx2 = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.X2 + (long long)b0 * cpb * H2W2), (short)0,
+    rx2 = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr((const char*)a.X2 + (long long)b0 * cpb * H2W2 * ES), (short)0,
                                             0x7FFFFFFF, 0x00020000);
   // this workgroup's NW consecutive 128-column images of one k-step; a
   // thread's element e = tid + THR j (j < 2 PL) of [t][plane][row][4]; with
@@ -284,7 +284,7 @@ gather_x3_kernel(const GatherArgs a) {
     if (mval) {
       const int b = m / (a.Qh * a.Qw);
       xoff = (int)(((long long)(b - b0) * cpb * HiWi + (long long)hb * a.Wi + wb) * ES);
-      if constexpr (JM == 1) xoff2 = (int)(((long long)(b - b0) * cpb * H2W2 + (long long)hb * a.W2 + wb) * 4);
+      if constexpr (JM == 1) xoff2 = (int)(((long long)(b - b0) * cpb * H2W2 + (long long)hb * a.W2 + wb) * ES);
     }
   }
   auto load_tile = [&](Stage& st, int k0) __attribute__((always_inline)) {
@@ -299,12 +299,14 @@ gather_x3_kernel(const GatherArgs a) {
         int vo = xoff + (e0.y * a.Wi + e0.z) * ES, cs = (int)(HiWi * ES);
         __amdgpu_buffer_rsrc_t r = rx;
         if constexpr (JM == 1) {                  // a K-step lies in one join chunk
+          // chunks [x_re, s_re, x_im, s_im] (complex_concat), or [x_re, x_im, s_re, s_im]
+          // (torch.cat, a.jcat: DCUNet's decoder, _1903_03107_dcunet.py:93)
           const int q = c0 / a.jh;
-          const bool from_x = (q & 1) == 0;       // chunks [x_re, s_re, x_im, s_im]
-          c0 = (q >> 1) * a.jh + (c0 - q * a.jh);
-          ok &= !from_x | (hi < a.H2);            // F.pad rows of x read 0
-          vo = from_x ? xoff2 + (e0.y * a.W2 + e0.z) * 4 : vo;
-          cs = from_x ? (int)(H2W2 * 4) : cs;
+          const bool from_x = a.jcat ? q < 2 : (q & 1) == 0;
+          c0 = (a.jcat ? (q & 1) : (q >> 1)) * a.jh + (c0 - q * a.jh);
+          ok &= !from_x | ((hi < a.H2) & (wi < a.W2));   // F.pad rows / columns of x read 0
+          vo = from_x ? xoff2 + (e0.y * a.W2 + e0.z) * ES : vo;
+          cs = from_x ? (int)(H2W2 * ES) : cs;
           r = from_x ? rx2 : rx;
         }
         vo = ok ? vo : (int)0x80000000;
@@ -467,8 +469,8 @@ gather_x3_kernel(const GatherArgs a) {
     const int nl0 = wn * TN + 4 * lh;
     if constexpr (JM == 2) {
       // joined output: a 32-row block of n lies in one join chunk (yjh % 32 == 0);
-      // s chunks -> Y over Ho x Wo, x chunks -> Y2 over YH2 x YW2 (rows >= YH2,
-      // the F.pad rows, have no x gradient)
+      // s chunks -> Y over Ho x Wo, x chunks -> Y2 over YH2 x YW2 (rows >= YH2 and, for a
+      // padded x (a.jcat), columns >= YW2 are the F.pad zeros: no x gradient)
       const int oh = a.ph + a.Sh * qh, ow = a.pw + a.Sw * qw;
       const long long P2 = (long long)a.YH2 * a.YW2;
       const int cpb = 2 * a.yjh;
@@ -476,14 +478,15 @@ gather_x3_kernel(const GatherArgs a) {
       for (int i = 0; i < RN; ++i) {
         const int nb = n0 + wn * TN + 32 * i;     // block's first channel (wave-uniform)
         const int q = nb / a.yjh;
-        const int cb = (q >> 1) * a.yjh + (nb - q * a.yjh) + 4 * lh;
-        const bool to_x = (q & 1) == 0;
-        if (to_x && oh >= a.YH2) continue;
+        const int cb = (a.jcat ? (q & 1) : (q >> 1)) * a.yjh + (nb - q * a.yjh) + 4 * lh;
+        const bool to_x = a.jcat ? q < 2 : (q & 1) == 0;
+        if (to_x && (oh >= a.YH2 || ow >= a.YW2)) continue;
         const long long pl = to_x ? P2 : HoWo;
-        float* yp = to_x ? a.Y2 + ((long long)b * cpb + cb) * P2 + (long long)oh * a.YW2 + ow
-                         : a.Y + ((long long)b * cpb + cb) * HoWo + (long long)oh * a.Wo + ow;
+        const long long yo = to_x ? ((long long)b * cpb + cb) * P2 + (long long)oh * a.YW2 + ow
+                                  : ((long long)b * cpb + cb) * HoWo + (long long)oh * a.Wo + ow;
+        void* yb = to_x ? (void*)a.Y2 : (void*)a.Y;
 #pragma unroll
-        for (int r2 = 0; r2 < 16; ++r2) yp[(long long)((r2 & 3) + 8 * (r2 >> 2)) * pl] = acc[i][j][r2];
+        for (int r2 = 0; r2 < 16; ++r2) st_s<SD>(yb, yo + (long long)((r2 & 3) + 8 * (r2 >> 2)) * pl, acc[i][j][r2]);
       }
       continue;
     }
@@ -540,7 +543,7 @@ template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1,
 __global__ void __launch_bounds__(kThreads * NB, 2)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
-  static_assert(SD == 0 || (TERMS == 1 && !DJ), "16-bit storage: one-term, no join");
+  static_assert(SD == 0 || TERMS == 1, "16-bit storage: one-term tiles");
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   constexpr int ES = SD ? 2 : 4;             // bytes per element of X / D
   static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
@@ -615,7 +618,7 @@ wgrad_x3_kernel(const WgradArgs a) {
       uniform_ptr((const char*)a.D + (long long)bfirst * dcpb * QQ * ES), (short)0, 0x7FFFFFFF, 0x00020000);
   __amdgpu_buffer_rsrc_t rd2_src = rd_src;
   if constexpr (DJ)
-    rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr(a.D2 + (long long)bfirst * dcpb * QQ2), (short)0,
+    rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr((const char*)a.D2 + (long long)bfirst * dcpb * QQ2 * ES), (short)0,
                                                 0x7FFFFFFF, 0x00020000);
   const int4 tap_e = sK[0];                         // TU: one tap per 128-row k-tile
   const int cbase = k0 % a.Cg;
@@ -654,17 +657,18 @@ wgrad_x3_kernel(const WgradArgs a) {
     int vd, ds = (int)(QQ * ES), srow = 32 * wave;
     __amdgpu_buffer_rsrc_t rdr = rd_src;
     if constexpr (DJ) {
-      // joined D: chunks [x_re, s_re, x_im, s_im] of djh rows; a wave's 32 rows
-      // lie in one chunk (djh % 32 == 0)
+      // joined D: chunks [x_re, s_re, x_im, s_im] (complex_concat) or [x_re, x_im, s_re,
+      // s_im] (torch.cat, a.djcat) of djh rows; a wave's 32 rows lie in one chunk
+      // (djh % 32 == 0)
       const int nb = n0 + 32 * wave;
       const int q = nb / a.djh;
-      const bool from_x = (q & 1) == 0;
-      const int cr = (q >> 1) * a.djh + (nb - q * a.djh) + RJ * lr;   // row in its source
-      const bool okx = dok & (!from_x | (cqh < a.DH2));                // F.pad rows of x: 0
-      vd = from_x ? (int)(((long long)rb * dcpb * QQ2 + (long long)cr * QQ2 + (long long)cqh * a.DW2 + cqw) * 4)
-                  : (int)(((long long)rb * dcpb * QQ + (long long)cr * QQ + (long long)cqh * a.Qw + cqw) * 4);
+      const bool from_x = a.djcat ? q < 2 : (q & 1) == 0;
+      const int cr = (a.djcat ? (q & 1) : (q >> 1)) * a.djh + (nb - q * a.djh) + RJ * lr;   // row in its source
+      const bool okx = dok & (!from_x | ((cqh < a.DH2) & (cqw < a.DW2)));   // F.pad rows / columns of x: 0
+      vd = from_x ? (int)(((long long)rb * dcpb * QQ2 + (long long)cr * QQ2 + (long long)cqh * a.DW2 + cqw) * ES)
+                  : (int)(((long long)rb * dcpb * QQ + (long long)cr * QQ + (long long)cqh * a.Qw + cqw) * ES);
       vd = okx ? vd : (int)0x80000000;
-      ds = from_x ? (int)(QQ2 * 4) : ds;
+      ds = from_x ? (int)(QQ2 * ES) : ds;
       rdr = from_x ? rd2_src : rd_src;
       srow = 0;
     } else {
@@ -998,10 +1002,10 @@ gather_x6_kernel(const GatherArgs a) {
       int vo = xoff + (e0.y * a.Wi + e0.z) * 4, cs = (int)(HiWi * 4);
       __amdgpu_buffer_rsrc_t r = rx;
       if constexpr (JG) {                         // a K-step lies in one join chunk
-        const int q = c0 / a.jh;
-        const bool from_x = (q & 1) == 0;         // chunks [x_re, s_re, x_im, s_im]
-        c0 = (q >> 1) * a.jh + (c0 - q * a.jh);
-        ok &= !from_x | (hi < a.H2);              // F.pad rows of x read 0
+        const int q = c0 / a.jh;                  // chunk order as gather_x3_kernel
+        const bool from_x = a.jcat ? q < 2 : (q & 1) == 0;
+        c0 = (a.jcat ? (q & 1) : (q >> 1)) * a.jh + (c0 - q * a.jh);
+        ok &= !from_x | ((hi < a.H2) & (wi < a.W2));   // F.pad rows / columns of x read 0
         vo = from_x ? xoff2 + (e0.y * a.W2 + e0.z) * 4 : vo;
         cs = from_x ? (int)(H2W2 * 4) : cs;
         r = from_x ? rx2 : rx;

@@ -38,7 +38,8 @@ class ConvDesc(ctypes.Structure):
         ("x_amax", c_void_p), ("dy_amax", c_void_p),   # SE_MATH_F16X3 scale sources (or NULL)
         ("w_amax", c_void_p),   # SE_MATH_F16X3 bound of max |w| (or NULL)
         ("dtype", c_int),           # SE_DTYPE_* storage of the conv's tensors (ABI 4)
-        ("data_weights", c_void_p)]   # prepared data-grad weight image (or NULL, ABI 5)
+        ("data_weights", c_void_p),   # prepared data-grad weight image (or NULL, ABI 5)
+        ("join_cat", c_int)]          # joined forms: 0 complex_concat, 1 torch.cat order (ABI 8)
 
 
 class FirstConvDesc(ctypes.Structure):

@@ -110,15 +110,16 @@ class _FusedComplexConv(nn.Module):
                      transposed=self.transposed, exact=self.exact_fp32)
         return rebuild(y)
 
-    def forward_joined(self, x, skip):
+    def forward_joined(self, x, skip, cat=False):
         """self(complex_concat([align(x), skip])) with the FRCRN decoder's
-        trim / pad / concat (frcrn.py:93-100) folded into the GEMMs."""
+        trim / pad / concat (frcrn.py:93-100) folded into the GEMMs; cat=True:
+        self(torch.cat([F.pad(x, to skip's grid), skip])) (DCUNet, dcunet.py:89-93)."""
         c = self._geometry()
         return F.conv2d_joined(x, skip, c.weight, self.imag_conv.weight, c.bias, self.imag_conv.bias,
                                out_channels=2 * c.out_channels, kernel=c.kernel_size, stride=c.stride,
                                padding=c.padding, dilation=c.dilation,
                                output_padding=getattr(c, "output_padding", (0, 0)),
-                               transposed=self.transposed)
+                               transposed=self.transposed, cat=cat)
 
 
 class ComplexConv2d(_FusedComplexConv):

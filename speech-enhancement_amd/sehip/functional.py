@@ -460,11 +460,14 @@ class _Conv2d(torch.autograd.Function):
 SE_E_UNSUPPORTED = -3
 
 
-def _join_raw(x, s):
+def _join_raw(x, s, cat=False):
     """complex_concat([align(x), s]) materialised (no autograd): the fallback
-    of the joined conv passes when no joined kernel covers the mode/shape."""
+    of the joined conv passes when no joined kernel covers the mode/shape.
+    cat=True: torch.cat([F.pad(x, to s's grid), s]) (DCUNet, dcunet.py:89-93)."""
     B, Cx, Fx, Tx = x.shape
     _, Cs, F_, T = s.shape
+    if cat:
+        return torch.cat([torch.nn.functional.pad(x, (0, T - Tx, 0, F_ - Fx)), s], dim=1)
     out = torch.empty((B, Cx + Cs, F_, T), device=x.device, dtype=x.dtype)
     N.check(N.lib().se_complex_join(x.data_ptr(), Cx, Fx, Tx, s.data_ptr(), Cs, F_, T, out.data_ptr(), B,
                                     N.dtype_code(x), N.stream_of(x)), "se_complex_join")
@@ -474,21 +477,26 @@ def _join_raw(x, s):
 class _ConvJoined(torch.autograd.Function):
     """Complex (transposed) conv over complex_concat([align(x), s]) — the FRCRN
     decoder's trim / pad / concat + ConvTransposeBlock conv (frcrn.py:93-101) —
+    or over torch.cat([pad(x), s]) (cat: DCUNet's decoder, dcunet.py:89-93),
     without writing the joined tensor: the forward GEMM gathers from x and s,
     the data-grad epilogue writes dx and ds directly, the weight-grad reads
     both as its D operand (se_conv2d_*_joined). Modes or shapes without a
-    joined kernel (SE_E_UNSUPPORTED) materialise the join for that pass."""
+    joined kernel (SE_E_UNSUPPORTED) materialise the join for that pass.
+    force_math (16-bit storage): the one-term MFMA of the storage format, the
+    tensors read and written as they are (se_conv2d_desc.dtype)."""
 
     @staticmethod
     def forward(ctx, x, s, wr, wi, br, bi, geom):
-        out_channels, kernel, stride, padding, dilation, output_padding, transposed = geom
-        N.require_device(x, s, wr, wi, br, bi)
+        out_channels, kernel, stride, padding, dilation, output_padding, transposed, cat, force_math = geom
+        N.require_device(x, s, wr, wi, br, bi, dtype=x.dtype)
         _check_weights(2 * s.shape[1], out_channels, kernel, transposed, wr, wi, br, bi)
         x, s = x.contiguous(), s.contiguous()
         B, Cs, F_, T = s.shape
         Fx, Tx = x.shape[2], x.shape[3]
         d = conv_desc((B, 2 * Cs, F_, T), out_channels, kernel, stride, padding, dilation,
                       output_padding, transposed, True)
+        d.join_cat, d.force_math, d.dtype = int(cat), force_math, N.dtype_code(x)
+        es = x.element_size()
         lib = N.lib()
         ho, wo = N.c_int(), N.c_int()
         N.check(lib.se_conv2d_out_shape(N.ctypes.byref(d), N.ctypes.byref(ho), N.ctypes.byref(wo)),
@@ -506,12 +514,12 @@ class _ConvJoined(torch.autograd.Function):
         rc = lib.se_conv2d_fwd_joined(_with_math(d, "fwd"), x.data_ptr(), Fx, Tx, s.data_ptr(), wr.data_ptr(),
                                       wi.data_ptr(), N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
         if rc == SE_E_UNSUPPORTED:
-            rc = lib.se_conv2d_fwd(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), wr.data_ptr(), wi.data_ptr(),
+            rc = lib.se_conv2d_fwd(N.ctypes.byref(d), _join_raw(x, s, cat).data_ptr(), wr.data_ptr(), wi.data_ptr(),
                                    N.ptr(br), N.ptr(bi), y.data_ptr(), ws.data_ptr(), ws.numel(), st)
         N.check(rc, "se_conv2d_fwd_joined")
         if t0 is not None:
             _TIMER.end(_gemm_tag("fwd", d, joined=True), t0, _conv_flops(d),
-                       4.0 * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
+                       es * (x.numel() + s.numel() + y.numel() + 2 * wr.numel()))
         ctx.save_for_backward(x, s, wr, wi)
         ctx.desc, ctx.nbytes, ctx.has_bias, ctx.x_amax, ctx.w_amax = d, nbytes, br is not None, xa, wa
         ctx.data_img = (_prep_data_weights(d, wr, wi, wa) if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]
@@ -542,13 +550,19 @@ class _ConvJoined(torch.autograd.Function):
                 dj = torch.empty((d.batch, d.in_channels, d.in_h, d.in_w), device=gy.device, dtype=gy.dtype)
                 N.check(lib.se_conv2d_bwd_data(N.ctypes.byref(d), gy.data_ptr(), wr.data_ptr(), wi.data_ptr(),
                                                dj.data_ptr(), ws.data_ptr(), ws.numel(), st), "se_conv2d_bwd_data")
-                rc = lib.se_complex_join_bwd(dj.data_ptr(), gx.data_ptr(), x.shape[1], Fx, Tx, gs.data_ptr(),
-                                             s.shape[1], d.in_h, d.in_w, d.batch, N.dtype_code(gy), st)
+                if d.join_cat:   # torch.cat order: x's gradient is the first half, cropped to x's grid
+                    Cx = x.shape[1]
+                    gx.copy_(dj[:, :Cx, :Fx, :Tx])
+                    gs.copy_(dj[:, Cx:])
+                    rc = 0
+                else:
+                    rc = lib.se_complex_join_bwd(dj.data_ptr(), gx.data_ptr(), x.shape[1], Fx, Tx, gs.data_ptr(),
+                                                 s.shape[1], d.in_h, d.in_w, d.batch, N.dtype_code(gy), st)
             N.check(rc, "se_conv2d_bwd_data_joined")
             d.data_weights, ctx.data_img = None, None
             if t0 is not None:
                 _TIMER.end(_gemm_tag("data", d, joined=True), t0, _conv_flops(d),
-                           4.0 * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))
+                           gy.element_size() * (gy.numel() + gx.numel() + gs.numel() + 2 * wr.numel()))
         if any(ctx.needs_input_grad[2:6]):
             with _wgrad_stream(x, s, gy, xa, ga):
                 if _DEFER is not None:
@@ -564,37 +578,43 @@ class _ConvJoined(torch.autograd.Function):
                                                      gy.data_ptr(), dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr),
                                                      N.ptr(dbi), ws.data_ptr(), ws.numel(), st)
                 if rc == SE_E_UNSUPPORTED:
-                    rc = lib.se_conv2d_bwd_weight(N.ctypes.byref(d), _join_raw(x, s).data_ptr(), gy.data_ptr(),
+                    rc = lib.se_conv2d_bwd_weight(N.ctypes.byref(d), _join_raw(x, s, d.join_cat).data_ptr(), gy.data_ptr(),
                                                   dwr.data_ptr(), dwi.data_ptr(), N.ptr(dbr), N.ptr(dbi),
                                                   ws.data_ptr(), ws.numel(), st)
                 N.check(rc, "se_conv2d_bwd_weight_joined")
                 if t0 is not None:
                     _TIMER.end(_gemm_tag("weight", d, joined=True), t0, _conv_flops(d),
-                               4.0 * (x.numel() + s.numel() + gy.numel() + 2 * wr.numel()))
+                               gy.element_size() * (x.numel() + s.numel() + gy.numel() + 2 * wr.numel()))
         return gx, gs, dwr, dwi, dbr, dbi, None
 
 
 def conv2d_joined(x, s, wr, wi, br=None, bi=None, *, out_channels, kernel, stride=1, padding=0,
-                  dilation=1, output_padding=0, transposed=False):
+                  dilation=1, output_padding=0, transposed=False, cat=False):
     """conv2d(complex_join(x, s), ...) with the join folded into the GEMMs.
-    x: [B, C, Fx, Tx] decoder state, s: [B, C, F, T] skip, Fx <= F, Tx >= T.
-    (fp32; other storage types run on fp32 copies.)"""
-    if x.shape[1] != s.shape[1] or x.shape[2] > s.shape[2] or x.shape[3] < s.shape[3]:
+    x: [B, C, Fx, Tx] decoder state, s: [B, C, F, T] skip, Fx <= F, Tx >= T
+    (frcrn.py:95-99); cat=True: conv2d(torch.cat([F.pad(x, to s's grid), s])) with
+    Fx <= F, Tx <= T (DCUNet, dcunet.py:89-93). bf16 / fp16 tensors run natively on the
+    one-term MFMA of their format where every pass has a kernel (_native16_ok); other
+    storage types run on fp32 copies."""
+    if x.shape[1] != s.shape[1] or x.shape[2] > s.shape[2] or (x.shape[3] > s.shape[3] if cat else x.shape[3] < s.shape[3]):
         raise ValueError(f"sehip conv2d_joined: cannot align {tuple(x.shape)} to {tuple(s.shape)}")
-    if x.dtype != torch.float32:
-        f32 = lambda t: None if t is None else t.float()
-        return conv2d_joined(x.float(), s.float(), f32(wr), f32(wi), f32(br), f32(bi), out_channels=out_channels,
-                             kernel=kernel, stride=stride, padding=padding, dilation=dilation,
-                             output_padding=output_padding, transposed=transposed).to(x.dtype)
     geom = (int(out_channels), _pair(kernel), _pair(stride), _pair(padding), _pair(dilation),
-            _pair(output_padding), bool(transposed))
-    return _ConvJoined.apply(x, s, wr, wi, br, bi, geom)
+            _pair(output_padding), bool(transposed), bool(cat))
+    if x.dtype == torch.float32:
+        return _ConvJoined.apply(x, s, wr, wi, br, bi, geom + (None,))
+    if x.dtype in _STORAGE_MATH and s.dtype == x.dtype and \
+            _native16_ok(x, wr, wi, br, bi, out_channels, transposed, in_channels=2 * s.shape[1]):
+        NATIVE16_CALLS[0] += 1
+        return _ConvJoined.apply(x, s, wr, wi, br, bi, geom + (_STORAGE_MATH[x.dtype],))
+    f32 = lambda t: None if t is None else t.float()
+    return _ConvJoined.apply(x.float(), s.float(), f32(wr), f32(wi), f32(br), f32(bi),
+                             geom + (_STORAGE_MATH.get(x.dtype),)).to(x.dtype)
 
 
 NATIVE16_CALLS = [0]   # convs run on 16-bit storage natively (diagnostics / tests)
 
 
-def _native16_ok(x, wr, wi, br, bi, out_channels, transposed) -> bool:
+def _native16_ok(x, wr, wi, br, bi, out_channels, transposed, in_channels=None) -> bool:
     """Whether every pass of a 16-bit-storage conv runs natively (se_conv2d_desc.dtype):
     the weight-grad's direct operand channels N (out for a conv, in for a convT) on the
     one-term split tiles (N % 16 == 0, N > 8) when the weights take a gradient."""
@@ -603,7 +623,7 @@ def _native16_ok(x, wr, wi, br, bi, out_channels, transposed) -> bool:
         return False
     if not any(t.requires_grad for t in ts) or not torch.is_grad_enabled():
         return True
-    n = x.shape[1] if transposed else out_channels
+    n = (x.shape[1] if in_channels is None else in_channels) if transposed else out_channels
     return n % 16 == 0 and n > 8
 
 

@@ -51,8 +51,8 @@ class _Block(nn.Module):
         """self(complex_concat([x[..., :T], skip])) (dccrn.py:116-120) with the concat folded
         into the convT's GEMMs (se_conv2d_*_joined); None where that path does not apply."""
         conv = getattr(self, self._attr)
-        if (self.padding[1] or not isinstance(conv, ComplexConvTranspose2d) or x.dtype != torch.float32
-                or skip.dtype != torch.float32 or x.shape[2] != skip.shape[2] or x.shape[1] != skip.shape[1]):
+        if (self.padding[1] or not isinstance(conv, ComplexConvTranspose2d) or x.dtype != skip.dtype
+                or x.shape[2] != skip.shape[2] or x.shape[1] != skip.shape[1]):
             return None
         y = conv.forward_joined(x, skip)
         return norm_act(self.norm, self.act, y)
@@ -132,8 +132,8 @@ class Decoder(nn.Module):
             aligned = x.shape[-1] - skip.shape[-1] in (0, 1) and x.shape[2] == skip.shape[2]
             y = layer.forward_joined(x, skip) if aligned else None
             if y is None and aligned and x.is_cuda and x.dtype == skip.dtype:
-                # no joined GEMM for this mode / width (e.g. bf16 storage): the trim and
-                # complex_concat as one HIP pass each way (se_complex_join), any storage type
+                # no joined GEMM for this mode / width: the trim and complex_concat as one
+                # HIP pass each way (se_complex_join), any storage type
                 y = layer(F.complex_join(x, skip))
             if y is None:
                 if x.shape[-1] > skip.shape[-1]:

@@ -52,6 +52,18 @@ class _Block(nn.Module):
         y = real_conv2d(conv, x) if isinstance(conv, (nn.Conv2d, nn.ConvTranspose2d)) else conv(x)
         return norm_act(self.norm, self.act, y)
 
+    def forward_joined(self, x, skip):
+        """self(torch.cat([pad(x), skip])) (dcunet.py:84-94) with the pad and cat folded into the
+        convT's GEMMs (se_conv2d_*_joined, join_cat); None where no joined GEMM covers the
+        layer (a real conv, the 2-channel mask layer, or jh = C/2 not a multiple of 32)."""
+        conv = getattr(self, self._attr)
+        if (not isinstance(conv, ComplexConvTranspose2d) or not x.is_cuda or x.dtype != skip.dtype
+                or x.shape[1] != skip.shape[1] or x.shape[2] > skip.shape[2] or x.shape[3] > skip.shape[3]
+                or (x.shape[1] // 2) % 32 or conv.real_conv.out_channels * 2 <= 64):
+            return None
+        y = conv.forward_joined(x, skip, cat=True)
+        return norm_act(self.norm, self.act, y)
+
 
 class ConvBlock(_Block):
     """dcunet.py:12-27."""
@@ -111,6 +123,12 @@ class Decoder(nn.Module):
         for layer in self.layers:
             if encoder_outputs is not None:
                 skip = encoder_outputs.pop()
+                # dcunet.py:89-93: x zero-padded to the skip's grid, then a plain torch.cat (not
+                # complex_concat); folded into the convT's GEMMs where a joined kernel exists
+                y = layer.forward_joined(x, skip)
+                if y is not None:
+                    x = y
+                    continue
                 if skip.shape != x.shape:                      # dcunet.py:89-92
                     x = TF.pad(x, (0, abs(skip.shape[3] - x.shape[3]), 0, abs(skip.shape[2] - x.shape[2])))
                 x = torch.cat([x, skip], dim=1)                # plain cat, not complex_concat (:93)

@@ -24,7 +24,7 @@ JOINED = [   # (x shape, skip shape): decoder state vs skip, FRCRN alignments
 ]
 
 
-@pytest.mark.parametrize("math", ["bf16x3", "fwd=bf16x6,data=bf16x3,weight=bf16x3", "bf16", "f32"])
+@pytest.mark.parametrize("math", ["f16x3", "bf16x3", "fwd=bf16x6,data=bf16x3,weight=bf16x3", "bf16", "f32"])
 @pytest.mark.parametrize("xs,ss", JOINED)
 def test_joined_conv_matches_materialised_join(gpu_device, xs, ss, math):
     """The decoder convT over complex_join(x, skip) with the join folded into
@@ -169,3 +169,79 @@ def test_complex_join_16bit_storage_bit_exact(gpu_device, xs, ss, dtype):
     assert yd.dtype == dtype and xd.grad.dtype == dtype
     assert torch.equal(yd.detach().cpu(), yr.detach())
     assert torch.equal(xd.grad.cpu(), xr.grad) and torch.equal(sd.grad.cpu(), sr.grad)
+
+
+CAT_JOINED = [   # (x shape, skip shape, kernel, stride, padding): DCUNet decoder alignments
+    ((2, 64, 8, 20), (2, 64, 9, 21), (5, 3), (2, 1), (2, 1)),     # x padded in both dims
+    ((2, 64, 9, 21), (2, 64, 9, 21), (5, 3), (2, 2), (2, 1)),     # aligned
+    ((1, 128, 16, 31), (1, 128, 17, 33), (7, 5), (2, 2), (3, 2)), # DCUNet-16 width (jh = 64)
+]
+
+
+def _cat_ref(x, s):
+    """dcunet.py:89-93: x zero-padded to the skip's grid, then a plain torch.cat."""
+    if x.shape != s.shape:
+        x = torch.nn.functional.pad(x, (0, s.shape[3] - x.shape[3], 0, s.shape[2] - x.shape[2]))
+    return torch.cat([x, s], dim=1)
+
+
+def _joined_pair(gpu_device, xs, ss, kernel, stride, padding, cat, dtype, cout=128):
+    """(y, dx, dskip, dwr, dwi) of the materialised join + plain conv and of the joined
+    conv (se_conv2d_*_joined), same inputs, the storage type dtype throughout."""
+    from sehip import functional as F
+    torch.manual_seed(1)
+    cin = 2 * xs[1]
+    x, s = torch.randn(xs, device=gpu_device).to(dtype), torch.randn(ss, device=gpu_device).to(dtype)
+    wr = (torch.randn(cin // 2, cout // 2, *kernel, device=gpu_device) * 0.05).to(dtype)
+    wi = (torch.randn(cin // 2, cout // 2, *kernel, device=gpu_device) * 0.05).to(dtype)
+    kw = dict(out_channels=cout, kernel=kernel, stride=stride, padding=padding, transposed=True)
+    outs = []
+    for joined in (False, True):
+        xa, sa = x.clone().requires_grad_(True), s.clone().requires_grad_(True)
+        wra, wia = wr.clone().requires_grad_(True), wi.clone().requires_grad_(True)
+        if joined:
+            y = F.conv2d_joined(xa, sa, wra, wia, cat=cat, **kw)
+        else:
+            y = F.conv2d(_cat_ref(xa, sa) if cat else F.complex_join(xa, sa), wra, wia, **kw)
+        g = torch.randn(y.shape, device=gpu_device, generator=torch.Generator(gpu_device).manual_seed(5)).to(dtype)
+        y.backward(g)
+        outs.append((y.detach(), xa.grad, sa.grad, wra.grad, wia.grad))
+    torch.cuda.synchronize()
+    return outs
+
+
+@pytest.mark.parametrize("math", ["f16x3", "bf16x3", "bf16"])
+@pytest.mark.parametrize("xs,ss,kernel,stride,padding", CAT_JOINED)
+def test_cat_joined_conv_matches_materialised_cat(gpu_device, xs, ss, kernel, stride, padding, math):
+    """DCUNet's decoder join (torch.cat order, x padded to the skip's grid in both
+    dimensions, se_conv2d_desc.join_cat) folded into the GEMMs: outputs and all four
+    gradients bit-identical to pad + torch.cat + the plain conv."""
+    from sehip import functional as F
+    prev = F.get_conv_math()
+    F.set_conv_math(math)
+    try:
+        ref, got = _joined_pair(gpu_device, xs, ss, kernel, stride, padding, True, torch.float32)
+        for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), ref, got):
+            assert a.shape == b.shape and torch.equal(a, b), (math, name, (a - b).abs().max().item())
+    finally:
+        F.set_conv_math(prev)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("cat", [False, True])
+def test_joined_conv_16bit_storage_matches_materialised(gpu_device, dtype, cat):
+    """16-bit storage (model.to(bfloat16) / .half(): BASELINE configs 2 / 3) on the joined
+    GEMMs, the one-term MFMA of the storage format reading and writing x, s, dx and ds as
+    they are: bit-identical to materialise-then-conv in the same storage type, for the
+    complex_concat join (DCCRN) and the torch.cat join (DCUNet)."""
+    from sehip import functional as F
+    if cat:
+        xs, ss, k, st, p = (2, 64, 8, 20), (2, 64, 9, 21), (5, 3), (2, 1), (2, 1)
+    else:
+        xs, ss, k, st, p = (2, 64, 8, 22), (2, 64, 9, 21), (5, 2), (2, 1), (2, 0)
+    n0 = F.NATIVE16_CALLS[0]
+    ref, got = _joined_pair(gpu_device, xs, ss, k, st, p, cat, dtype)
+    assert F.NATIVE16_CALLS[0] > n0   # the joined form ran natively, not on fp32 copies
+    for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), ref, got):
+        assert a.dtype == dtype and b.dtype == dtype
+        assert a.shape == b.shape and torch.equal(a, b), (dtype, cat, name, (a.float() - b.float()).abs().max().item())
