@@ -496,6 +496,7 @@ class _ConvJoined(torch.autograd.Function):
         d = conv_desc((B, 2 * Cs, F_, T), out_channels, kernel, stride, padding, dilation,
                       output_padding, transposed, True)
         d.join_cat, d.force_math, d.dtype = int(cat), force_math, N.dtype_code(x)
+        d.math = _pass_math("fwd", d)
         es = x.element_size()
         lib = N.lib()
         ho, wo = N.c_int(), N.c_int()
