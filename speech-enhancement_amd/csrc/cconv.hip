@@ -1070,12 +1070,6 @@ __global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int
 }
 
 #include "cconv_x3.hpp"
-#include "cconv_p.hpp"
-// SE_GATHER_P=0 (variant builds): the split-fp16 gathers on gather_x3_kernel instead of the
-// pipelined gather_p_kernel (bit-identical; A/B and the bit-identity test)
-#ifndef SE_GATHER_P
-#define SE_GATHER_P 1
-#endif
 
 // bias_full[n] for the fused complex conv: re = br - bi, im = bi + br.
 __global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out, int sd) {
@@ -1554,7 +1548,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
   // batch items one M-tile can span (for both sources of a joined gather)
   auto tu_of = [&](const ClassPlan& c) {
     const long long qhw = (long long)c.h.Q * c.w.Q;
-    const int bm = (ldw == 64 || (f16 && SE_GATHER_P)) ? 256 : 128;   // gather_p_kernel: 256-position tiles
+    const int bm = ldw == 64 ? 256 : 128;
     const long long span = (bm + qhw - 1) / qhw + 1;
     bool ok = (Cg % kBK == 0) && span * cpb * (long long)Hi * Wi * 4 < (1ll << 31) &&
               (long long)c.Kp * ldw * 4 < (1ll << 31);
@@ -1695,19 +1689,7 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     else if (tu) hipLaunchKernelGGL((gather_x3_kernel<true, T, 0, NWV, F>), grid, blk, 0, st, a);         \
     else hipLaunchKernelGGL((gather_x3_kernel<false, T, 0, NWV, F>), grid, blk, 0, st, a);                \
   } while (0)
-        if (f16 && tu && SE_GATHER_P && (ldw == 128 || ldw == 256)) {   // pipelined split-fp16 tiles
-          const bool n256 = ldw == 256;
-          const dim3 pgrid(se::ceil_div(M, kPBM), 1), pblk(n256 ? 512 : 256);
-#define SE_P_LAUNCH(NWN)                                                                                  \
-  do {                                                                                                    \
-    if (join_in) hipLaunchKernelGGL((gather_p_kernel<1, NWN>), pgrid, pblk, 0, st, a);                    \
-    else if (join_out) hipLaunchKernelGGL((gather_p_kernel<2, NWN>), pgrid, pblk, 0, st, a);              \
-    else hipLaunchKernelGGL((gather_p_kernel<0, NWN>), pgrid, pblk, 0, st, a);                            \
-  } while (0)
-          if (n256) SE_P_LAUNCH(4);
-          else SE_P_LAUNCH(2);
-#undef SE_P_LAUNCH
-        } else if (g.sd != SE_DTYPE_F32) {   // 16-bit storage: the one-term tiles of its format
+        if (g.sd != SE_DTYPE_F32) {   // 16-bit storage: the one-term tiles of its format
 #define SE_X3_SD(NWV, F, SDV)                                                                              \
   do {                                                                                                    \
     if (join_in) hipLaunchKernelGGL((gather_x3_kernel<true, 1, 1, NWV, F, SDV>), grid, blk, 0, st, a);     \

@@ -259,83 +259,3 @@ def test_many_channel_small_n_stencil(shape, kernel, stride, padding, dtype, gpu
     tol = 1e-6 if dtype == torch.float32 else 6e-3
     assert e_st < tol and d < (1e-6 if dtype == torch.float32 else 8e-3)
 
-
-def _refx3_lib():
-    """libsehip_refx3.so: the same library built with SE_GATHER_P=0 (the round-4
-    gather_x3_kernel on every split-fp16 gather pass), loaded beside libsehip.so."""
-    import ctypes
-    import os
-    from sehip import _native as N
-    path = os.path.join(os.path.dirname(N.LIB_PATH), "libsehip_refx3.so")
-    assert os.path.exists(path), f"{path} missing: run __graft_entry__.build()"
-    h = ctypes.CDLL(path, mode=ctypes.RTLD_LOCAL)
-    for name, (res, args) in N._SIGNATURES.items():
-        f = getattr(h, name, None)
-        if f is not None:
-            f.restype, f.argtypes = res, args
-    assert h.se_abi_version() == N.ABI_VERSION
-    return h
-
-
-P_CASES = [   # (name, transposed, cin, cout, x shape, skip shape or None, kernel, stride, causal pad)
-    ("enc", False, 128, 128, (3, 128, 40, 41), None, (5, 2), (2, 1), True),      # NWN = 2, fwd + data
-    ("enc_ragged", False, 128, 128, (1, 128, 21, 37), None, (5, 2), (2, 1), True),
-    ("dec_joined", True, 256, 128, (2, 128, 17, 41), (2, 128, 17, 40), (5, 2), (2, 1), False),   # data NWN = 4
-    ("dec_joined_pad", True, 256, 128, (3, 128, 8, 38), (3, 128, 9, 37), (5, 2), (2, 1), False),
-]
-
-
-@pytest.mark.parametrize("case", P_CASES, ids=[c[0] for c in P_CASES])
-def test_gather_p_bit_identical_to_gather_x3(case, gpu_device):
-    """gather_p_kernel (the pipelined split-fp16 gather, cconv_p.hpp) against the round-4
-    gather_x3_kernel it replaces (a variant build of the same library): same split, same
-    weight image, same MFMA sequence per accumulator, so the forward and data-grad outputs
-    must be equal to the bit, for plain and joined passes, ragged M tiles included."""
-    import ctypes
-    from sehip import functional as F, _native as N
-    name, tr, cin, cout, xs, ss, k, st, causal = case
-    ref = _refx3_lib()
-    lib = N.lib()
-    g = torch.Generator(device=gpu_device).manual_seed(11)
-    joined = ss is not None
-    din = (xs[0], 2 * ss[1], ss[2], ss[3]) if joined else xs
-    d = F.conv_desc(din, cout, k, st, (0, 0), (1, 1), (0, 0), tr, True,
-                    padding_end=None if not causal else None)
-    if causal:
-        d.pad_w, d.pad_w_end = 1, 0
-    d.math = F._MATH_CODES["f16x3"]
-    ho, wo = ctypes.c_int(), ctypes.c_int()
-    assert lib.se_conv2d_out_shape(ctypes.byref(d), ctypes.byref(ho), ctypes.byref(wo)) == 0
-    wsh = (cin // 2, cout // 2, *k) if tr else (cout // 2, cin // 2, *k)
-    x = torch.randn(xs, device=gpu_device, generator=g)
-    s = torch.randn(ss, device=gpu_device, generator=g) if joined else None
-    wr = torch.randn(wsh, device=gpu_device, generator=g) * .05
-    wi = torch.randn(wsh, device=gpu_device, generator=g) * .05
-    dy = torch.randn(xs[0], cout, ho.value, wo.value, device=gpu_device, generator=g)
-    nws = lib.se_conv2d_workspace_size(ctypes.byref(d))
-    st_ = N.stream_of(x)
-    res = []
-    for L in (lib, ref):
-        ws = torch.zeros(nws, dtype=torch.uint8, device=gpu_device)
-        y = torch.full((xs[0], cout, ho.value, wo.value), float("nan"), device=gpu_device)
-        b = ctypes.byref(d)
-        if joined:
-            gx, gs = torch.full_like(x, float("nan")), torch.full_like(s, float("nan"))
-            rc = [L.se_conv2d_fwd_joined(b, x.data_ptr(), xs[2], xs[3], s.data_ptr(), wr.data_ptr(), wi.data_ptr(),
-                                         None, None, y.data_ptr(), ws.data_ptr(), nws, st_),
-                  L.se_conv2d_bwd_data_joined(b, dy.data_ptr(), wr.data_ptr(), wi.data_ptr(), gx.data_ptr(),
-                                              xs[2], xs[3], gs.data_ptr(), ws.data_ptr(), nws, st_)]
-            outs = (y, gx, gs)
-        else:
-            dx = torch.full_like(x, float("nan"))
-            rc = [L.se_conv2d_fwd(b, x.data_ptr(), wr.data_ptr(), wi.data_ptr(), None, None, y.data_ptr(),
-                                  ws.data_ptr(), nws, st_),
-                  L.se_conv2d_bwd_data(b, dy.data_ptr(), wr.data_ptr(), wi.data_ptr(), dx.data_ptr(),
-                                       ws.data_ptr(), nws, st_)]
-            outs = (y, dx)
-        torch.cuda.synchronize()
-        assert rc == [0, 0], rc
-        res.append([o.clone() for o in outs])
-    for n_, a_, b_ in zip(("y", "dx", "ds"), *res):
-        assert torch.isfinite(a_).all(), n_
-        assert torch.equal(a_, b_), (name, n_, (a_ - b_).abs().max().item())
