@@ -1881,12 +1881,14 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   if (g.sd != SE_DTYPE_F32 && (!split_ok || w.N <= kSmallWgradN || w.Np == 32))
     return SE_E_UNSUPPORTED;
   if (jn) {
+    // the joined D operand (either gather form of G): 32-bit offsets from the split's
+    // first batch item; one-term fp16 on fp32 storage has no joined instantiation
     const int dcpb = 2 * jn->jh;
-    const bool tu = g.transposed && (w.Cg % 128 == 0) &&
-                    span_w * w.Cg * (long long)w.Hi * w.Wi * 4 < (1ll << 31) &&
-                    span_w * dcpb * QQw * 4 < (1ll << 31) &&
-                    span_w * dcpb * (long long)jn->h2 * jn->w2 * 4 < (1ll << 31);
-    if (!tu || !split_ok || w.N <= 32 || w.N != 4 * jn->jh) return SE_E_UNSUPPORTED;
+    const bool dj_ok = g.transposed && span_w * dcpb * QQw * 4 < (1ll << 31) &&
+                       span_w * dcpb * (long long)jn->h2 * jn->w2 * 4 < (1ll << 31);
+    if (!dj_ok || !split_ok || w.N <= 32 || w.N != 4 * jn->jh ||
+        (g.math == SE_MATH_F16 && g.sd == SE_DTYPE_F32))
+      return SE_E_UNSUPPORTED;
   }
   char* p = align256((char*)ws);
   const float* zero = zero_page();
@@ -1955,25 +1957,30 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   } else if (f16 && w.Np % 256 == 0) {   // 128 x 256 tiles, 8 waves
     const dim3 grid = x3_wgrad_grid(a, w, 2);
     const dim3 blk(2 * kThreads);
-    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2>), grid, blk, 0, st, a);
+    if (jn && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2>), grid, blk, 0, st, a);
+    else if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, true, true, 2>), grid, blk, 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 2>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true, 2>), grid, blk, 0, st, a);
   } else if (f16) {
     const dim3 grid = x3_wgrad_grid(a, w);
     const bool kpad = (w.c.taps.n * w.Cg) % 128 != 0;   // e.g. a first conv: K = 10 taps x 2
-    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true>), grid, dim3(kThreads), 0, st, a);
+    if (jn && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true>), grid, dim3(kThreads), 0, st, a);
+    else if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, true, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true>), grid, dim3(kThreads), 0, st, a);
     else if (kpad) hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true, 1, true>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, false, true>), grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.math == SE_MATH_BF16X3) {
     const dim3 grid = x3_wgrad_grid(a, w);
-    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true>), grid, dim3(kThreads), 0, st, a);
+    if (jn && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true>), grid, dim3(kThreads), 0, st, a);
+    else if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
   } else if (split_ok && g.sd != SE_DTYPE_F32) {   // 16-bit storage, one term of its format
     const dim3 grid = x3_wgrad_grid(a, w);
-    if (g.sd == SE_DTYPE_BF16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
-    else if (g.sd == SE_DTYPE_F16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
+    if (g.sd == SE_DTYPE_BF16 && jn && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (g.sd == SE_DTYPE_BF16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, true, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
+    else if (g.sd == SE_DTYPE_F16 && jn && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
+    else if (g.sd == SE_DTYPE_F16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, true, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
     else if (g.sd == SE_DTYPE_BF16 && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
     else if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true, 1, false, 2>), grid, dim3(kThreads), 0, st, a);
@@ -1984,7 +1991,8 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, false, true>), grid, dim3(kThreads), 0, st, a);
   } else if (split_ok) {   // SE_MATH_BF16
     const dim3 grid = x3_wgrad_grid(a, w);
-    if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true>), grid, dim3(kThreads), 0, st, a);
+    if (jn && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true>), grid, dim3(kThreads), 0, st, a);
+    else if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<false, 1, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1>), grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<false, 1>), grid, dim3(kThreads), 0, st, a);
   } else {

@@ -32,9 +32,41 @@ __device__ __forceinline__ void join_src(const JoinGeom& g, int o, int& src, int
   else { src = 1; c = hs + (o - 2 * hx - hs); }
 }
 
-// One block per joined plane (b, o), a flat loop over its F x T positions (coalesced
-// along t). E: the element's bit pattern (fp32, or bf16 / fp16 storage: a copy
-// moves bits, and a zero is all-zero bits in every format).
+// Plane copy of n elements: 16-B vectors when both planes start 16-B aligned (the
+// element count of a plane decides it, the same for every plane of a launch), scalars
+// for the tail and otherwise.
+template <typename E>
+__device__ __forceinline__ void copy_plane(E* __restrict__ d, const E* __restrict__ s, long long n) {
+  constexpr int V = 16 / sizeof(E);
+  long long done = 0;
+  if (((reinterpret_cast<uintptr_t>(d) | reinterpret_cast<uintptr_t>(s)) & 15) == 0) {
+    const long long nv = n / V;
+    for (long long i = threadIdx.x; i < nv; i += kThreads)
+      reinterpret_cast<uint4*>(d)[i] = reinterpret_cast<const uint4*>(s)[i];
+    done = nv * V;
+  }
+  for (long long i = done + threadIdx.x; i < n; i += kThreads) d[i] = s[i];
+}
+
+// rows [0, rows_out) of width w_out from rows of width w_in (rows >= rows_in and
+// columns >= w_in read 0): one wave per row, lanes along the row
+template <typename E>
+__device__ __forceinline__ void copy_rows(E* __restrict__ d, int rows_out, int w_out, const E* __restrict__ s,
+                                          int rows_in, int w_in) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  for (int f = wave; f < rows_out; f += kThreads / 64) {
+    E* dr = d + (long long)f * w_out;
+    if (f < rows_in) {
+      const E* sr = s + (long long)f * w_in;
+      for (int t = lane; t < w_out; t += 64) dr[t] = t < w_in ? sr[t] : E(0);
+    } else {
+      for (int t = lane; t < w_out; t += 64) dr[t] = E(0);
+    }
+  }
+}
+
+// One block per joined plane (b, o). E: the element's bit pattern (fp32, or bf16 /
+// fp16 storage: a copy moves bits, and a zero is all-zero bits in every format).
 // grid (B * (Cx + Cs))
 template <typename E>
 __global__ __launch_bounds__(kThreads) void join_fwd_kernel(const E* __restrict__ x, const E* __restrict__ s,
@@ -44,16 +76,10 @@ __global__ __launch_bounds__(kThreads) void join_fwd_kernel(const E* __restrict_
   int src, c;
   join_src(g, o, src, c);
   E* op = out + ((long long)b * Co + o) * g.F * g.T;
-  if (src == 1) {
-    const E* sp = s + ((long long)b * g.Cs + c) * g.F * g.T;
-    for (int i = threadIdx.x; i < g.F * g.T; i += kThreads) op[i] = sp[i];   // same grid: flat copy
-    return;
-  }
-  const E* xp = x + ((long long)b * g.Cx + c) * g.Fx * g.Tx;
-  for (int i = threadIdx.x; i < g.F * g.T; i += kThreads) {
-    const int f = i / g.T, t = i - f * g.T;
-    op[i] = (f < g.Fx && t < g.Tx) ? xp[f * g.Tx + t] : E(0);
-  }
+  if (src == 1)   // same grid: flat copy
+    copy_plane(op, s + ((long long)b * g.Cs + c) * g.F * g.T, (long long)g.F * g.T);
+  else
+    copy_rows(op, g.F, g.T, x + ((long long)b * g.Cx + c) * g.Fx * g.Tx, g.Fx, g.Tx);
 }
 
 // dx over x's own grid (zeros where x was cropped away), ds = its slots.
@@ -66,16 +92,10 @@ __global__ __launch_bounds__(kThreads) void join_bwd_kernel(const E* __restrict_
   int src, c;
   join_src(g, o, src, c);
   const E* gp = gout + ((long long)b * Co + o) * g.F * g.T;
-  if (src == 1) {
-    E* sp = gs + ((long long)b * g.Cs + c) * g.F * g.T;
-    for (int i = threadIdx.x; i < g.F * g.T; i += kThreads) sp[i] = gp[i];
-    return;
-  }
-  E* xp = gx + ((long long)b * g.Cx + c) * g.Fx * g.Tx;
-  for (int i = threadIdx.x; i < g.Fx * g.Tx; i += kThreads) {
-    const int f = i / g.Tx, t = i - f * g.Tx;
-    xp[i] = (f < g.F && t < g.T) ? gp[f * g.T + t] : E(0);
-  }
+  if (src == 1)
+    copy_plane(gs + ((long long)b * g.Cs + c) * g.F * g.T, gp, (long long)g.F * g.T);
+  else
+    copy_rows(gx + ((long long)b * g.Cx + c) * g.Fx * g.Tx, g.Fx, g.Tx, gp, g.F, g.T);
 }
 
 int check(const JoinGeom& g) {

@@ -55,11 +55,12 @@ class _Block(nn.Module):
     def forward_joined(self, x, skip):
         """self(torch.cat([pad(x), skip])) (dcunet.py:84-94) with the pad and cat folded into the
         convT's GEMMs (se_conv2d_*_joined, join_cat); None where no joined GEMM covers the
-        layer (a real conv, the 2-channel mask layer, or jh = C/2 not a multiple of 32)."""
+        layer (a real conv, the 2-channel mask layer, or jh = C/2 not a multiple of 32). A pass
+        without a joined kernel for its shape materialises the cat for that pass only."""
         conv = getattr(self, self._attr)
         if (not isinstance(conv, ComplexConvTranspose2d) or not x.is_cuda or x.dtype != skip.dtype
                 or x.shape[1] != skip.shape[1] or x.shape[2] > skip.shape[2] or x.shape[3] > skip.shape[3]
-                or (x.shape[1] // 2) % 32 or conv.real_conv.out_channels * 2 <= 64):
+                or (x.shape[1] // 2) % 32 or conv.real_conv.out_channels * 2 <= 16):
             return None
         y = conv.forward_joined(x, skip, cat=True)
         return norm_act(self.norm, self.act, y)

@@ -24,19 +24,23 @@ JOINED = [   # (x shape, skip shape): decoder state vs skip, FRCRN alignments
 ]
 
 
-@pytest.mark.parametrize("math", ["f16x3", "bf16x3", "fwd=bf16x6,data=bf16x3,weight=bf16x3", "bf16", "f32"])
+@pytest.mark.parametrize("cout", [128, 64])
+@pytest.mark.parametrize("math", ["f16x3", "bf16x3", "fwd=bf16x6,data=bf16x3,weight=bf16x3", "bf16", "f16", "f32"])
 @pytest.mark.parametrize("xs,ss", JOINED)
-def test_joined_conv_matches_materialised_join(gpu_device, xs, ss, math):
+def test_joined_conv_matches_materialised_join(gpu_device, xs, ss, math, cout):
     """The decoder convT over complex_join(x, skip) with the join folded into
     the GEMMs (se_conv2d_*_joined) gives bit-identical outputs and gradients to
     the materialised join + plain conv (same K order, same MFMA sequence); f32
-    has no joined kernel and takes the materialising fallback."""
+    has no joined kernel and takes the materialising fallback. cout = 64: the
+    weight-grad's gathered operand (dy, 64 channels) is not tap-uniform, so the
+    joined weight-grad runs on the per-row tap table (DCCRN's 128 -> 64 / 64 -> 32
+    decoder layers)."""
     from sehip import functional as F
     prev = F.get_conv_math()
     F.set_conv_math(math)
     try:
         torch.manual_seed(1)
-        cin, cout = 2 * xs[1], 128
+        cin = 2 * xs[1]
         x, s = torch.randn(xs, device=gpu_device), torch.randn(ss, device=gpu_device)
         wr = (torch.randn(cin // 2, cout // 2, 5, 2, device=gpu_device) * 0.05)
         wi = (torch.randn(cin // 2, cout // 2, 5, 2, device=gpu_device) * 0.05)
@@ -175,6 +179,8 @@ CAT_JOINED = [   # (x shape, skip shape, kernel, stride, padding): DCUNet decode
     ((2, 64, 8, 20), (2, 64, 9, 21), (5, 3), (2, 1), (2, 1)),     # x padded in both dims
     ((2, 64, 9, 21), (2, 64, 9, 21), (5, 3), (2, 2), (2, 1)),     # aligned
     ((1, 128, 16, 31), (1, 128, 17, 33), (7, 5), (2, 2), (3, 2)), # DCUNet-16 width (jh = 64)
+    ((2, 128, 8, 20), (2, 128, 9, 21), (5, 3), (2, 1), (2, 1), 64),   # 64 outputs (DCUNet-16 dec.)
+    ((2, 64, 8, 20), (2, 64, 9, 21), (5, 3), (2, 1), (2, 1), 32),     # 32 outputs
 ]
 
 
@@ -211,8 +217,8 @@ def _joined_pair(gpu_device, xs, ss, kernel, stride, padding, cat, dtype, cout=1
 
 
 @pytest.mark.parametrize("math", ["f16x3", "bf16x3", "bf16"])
-@pytest.mark.parametrize("xs,ss,kernel,stride,padding", CAT_JOINED)
-def test_cat_joined_conv_matches_materialised_cat(gpu_device, xs, ss, kernel, stride, padding, math):
+@pytest.mark.parametrize("case", CAT_JOINED)
+def test_cat_joined_conv_matches_materialised_cat(gpu_device, case, math):
     """DCUNet's decoder join (torch.cat order, x padded to the skip's grid in both
     dimensions, se_conv2d_desc.join_cat) folded into the GEMMs: outputs and all four
     gradients bit-identical to pad + torch.cat + the plain conv."""
@@ -220,7 +226,9 @@ def test_cat_joined_conv_matches_materialised_cat(gpu_device, xs, ss, kernel, st
     prev = F.get_conv_math()
     F.set_conv_math(math)
     try:
-        ref, got = _joined_pair(gpu_device, xs, ss, kernel, stride, padding, True, torch.float32)
+        xs, ss, kernel, stride, padding = case[:5]
+        cout = case[5] if len(case) > 5 else 128
+        ref, got = _joined_pair(gpu_device, xs, ss, kernel, stride, padding, True, torch.float32, cout)
         for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), ref, got):
             assert a.shape == b.shape and torch.equal(a, b), (math, name, (a - b).abs().max().item())
     finally:
@@ -229,7 +237,8 @@ def test_cat_joined_conv_matches_materialised_cat(gpu_device, xs, ss, kernel, st
 
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
 @pytest.mark.parametrize("cat", [False, True])
-def test_joined_conv_16bit_storage_matches_materialised(gpu_device, dtype, cat):
+@pytest.mark.parametrize("cout", [128, 64])
+def test_joined_conv_16bit_storage_matches_materialised(gpu_device, dtype, cat, cout):
     """16-bit storage (model.to(bfloat16) / .half(): BASELINE configs 2 / 3) on the joined
     GEMMs, the one-term MFMA of the storage format reading and writing x, s, dx and ds as
     they are: bit-identical to materialise-then-conv in the same storage type, for the
@@ -240,7 +249,7 @@ def test_joined_conv_16bit_storage_matches_materialised(gpu_device, dtype, cat):
     else:
         xs, ss, k, st, p = (2, 64, 8, 22), (2, 64, 9, 21), (5, 2), (2, 1), (2, 0)
     n0 = F.NATIVE16_CALLS[0]
-    ref, got = _joined_pair(gpu_device, xs, ss, k, st, p, cat, dtype)
+    ref, got = _joined_pair(gpu_device, xs, ss, k, st, p, cat, dtype, cout)
     assert F.NATIVE16_CALLS[0] > n0   # the joined form ran natively, not on fp32 copies
     for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), ref, got):
         assert a.dtype == dtype and b.dtype == dtype
