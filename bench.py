@@ -58,8 +58,8 @@ KERNEL_OF = {
     "conv_fwd_joined_f16x3": ("gather_x3_kernel<true, 3, 1, 1, true, 0>", 2,
                               "gather_x3_kernel<F16, joined fwd> (se_conv2d_fwd_joined, 2 stride-phase "
                               "launches per call)"),
-    "conv_wgrad_joined_f16x3": ("wgrad_x3_kernel<true, 3, true, true, 2, false, 0>", 1,
-                                "wgrad_x3_kernel<F16, joined, 128 x 256 tiles> (se_conv2d_bwd_weight_joined)"),
+    "conv_wgrad_joined_f16x3": ("wgrad_x3_kernel<true, 3, true, true, 2, false, 0, 2>", 1,
+                                "wgrad_x3_kernel<F16, joined, 256 x 256 tiles> (se_conv2d_bwd_weight_joined)"),
     "conv_data_joined_bf16x3": ("gather_x3_kernel<true, 3, 2, 2, false, 0>", 1,
                                 "gather_x3_kernel<bf16x3, joined data-grad> (se_conv2d_bwd_data_joined)"),
     "conv_data_joined_f32": (None, 1, "gather_gemm_kernel<128, 128, 2, 2, true> on the materialised join "

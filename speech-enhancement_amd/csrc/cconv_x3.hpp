@@ -539,7 +539,11 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // m-split and its order of positions, so the slabs are bit-identical.
 // KP: the K range ends inside the last k-tile (ntaps * Cg % 128 != 0).
 // SD: storage type of X / D (as gather_x3_kernel; 16-bit with the one-term MFMA)
-template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0>
+// KB: 128-row G blocks per workgroup (KB = 2 with NB = 2: 256 k x 256 n tiles, 8 waves of
+// 128 x 64, one register staging set; a staged G row serves 256 columns and a staged D
+// row 256 k rows, a third fewer loads and splits per MFMA than 128 x 256)
+template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0,
+          int KB = 1>
 __global__ void __launch_bounds__(kThreads * NB, 2)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
@@ -547,18 +551,20 @@ wgrad_x3_kernel(const WgradArgs a) {
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   constexpr int ES = SD ? 2 : 4;             // bytes per element of X / D
   static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
+  static_assert(KB == 1 || (KB == 2 && NB == 2 && TERMS == 3 && !KP), "256 x 256 tiles: split-fp16 / bf16, full K");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
-  constexpr int BKO = 128, BNO = 128 * NB, WNn = 2 * NB, TK = 64, TN = 64, RK = 2, RN = 2, BMR = 32;
+  constexpr int BKO = 128 * KB, BNO = 128 * NB, WNn = 2 * NB, TK = 64 * KB, TN = 64, RK = 2 * KB, RN = 2, BMR = 32;
   constexpr int RJ = 16;                     // D rows per thread
-  constexpr int RJG = 16 / NB;               // G rows per thread
+  constexpr int RJG = 16 * KB / NB;          // G rows per thread
+  constexpr int GW = 32 * KB / NB;           // G rows per wave
   constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
   // per 128-row G block: G hi, G lo; then per 128-row D block: D hi, D lo
-  constexpr int DPL = 2;                     // first D plane
+  constexpr int DPL = 2 * KB;                // first D plane
   // 32-position halves per staging round: one term stages two (64 positions; the lo
   // plane slots hold the second half), so a barrier feeds 16 MFMAs per wave, not 8;
   // the positions are accumulated in the same order, so the slabs are unchanged
   constexpr int KH = TERMS == 1 ? kX3OneTermHalves : 1;
-  __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 + 2 * NB) * PLANE];
+  __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 * KB + 2 * NB) * PLANE];
   __shared__ int4 sK[BKO];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -583,9 +589,9 @@ wgrad_x3_kernel(const WgradArgs a) {
   // cost the full tiles their MFMA interleave: 627 vs 629 utt/s when always on)
   const int kv = KP ? min(BKO, a.ntaps * a.Cg - k0) : BKO;
   const int kvw = kv - wk * TK;                       // ... of this wave's 64 MFMA rows
-  const bool gact = (32 / NB) * wave < kv;            // this wave stages some valid G row
+  const bool gact = GW * wave < kv;                   // this wave stages some valid G row
   const int rbase = 32 * wave + RJ * lr;     // this thread's first D row
-  const int rbase_g = (32 / NB) * wave + RJG * lr;  // ... and first G row
+  const int rbase_g = GW * wave + RJG * lr;  // ... and first G row
 
   for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
   __syncthreads();
@@ -620,8 +626,8 @@ wgrad_x3_kernel(const WgradArgs a) {
   if constexpr (DJ)
     rd2_src = __builtin_amdgcn_make_buffer_rsrc(uniform_ptr((const char*)a.D2 + (long long)bfirst * dcpb * QQ2 * ES), (short)0,
                                                 0x7FFFFFFF, 0x00020000);
-  const int4 tap_e = sK[0];                         // TU: one tap per 128-row k-tile
-  const int cbase = k0 % a.Cg;
+  const int4 tap_e = sK[rbase_g & ~127];           // TU: one tap per 128-row G block
+  const int cbase = (k0 + (rbase_g & ~127)) % a.Cg;
   const bool one_wrap = a.Qw >= BMR;
   auto advance1 = [&](int& b_, int& h_, int& w_) __attribute__((always_inline)) {
     if (one_wrap) {
@@ -686,8 +692,8 @@ wgrad_x3_kernel(const WgradArgs a) {
       const int gs = (int)(HiWi * ES);
 #pragma unroll
       for (int j = 0; j < RJG; ++j) {
-        if constexpr (SD != 0) S.rg[RJG * hh + j] = bload_raw16(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
-        else S.rg[RJG * hh + j] = bload<0>(rg_src, vg, ((((32 / NB) * wave) & 127) + j) * gs);
+        if constexpr (SD != 0) S.rg[RJG * hh + j] = bload_raw16(rg_src, vg, (((GW * wave) & 127) + j) * gs);
+        else S.rg[RJG * hh + j] = bload<0>(rg_src, vg, (((GW * wave) & 127) + j) * gs);
       }
     } else {
       const int hb = cqh * a.sh, wb = cqw * a.sw;
@@ -715,7 +721,7 @@ wgrad_x3_kernel(const WgradArgs a) {
 #pragma unroll
    for (int hh = 0; hh < KH; ++hh) {   // one term: half hh in the plane-hh slots
     unsigned char* dbase = base + (DPL + 2 * (rbase >> 7) + hh) * PLANE;   // this thread's D block
-    unsigned char* gbase = base + hh * PLANE;                              // ... and G block
+    unsigned char* gbase = base + (2 * (rbase_g >> 7) + hh) * PLANE;      // ... and G block
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       u32x4 GH, GL, DH, DL;
@@ -777,13 +783,37 @@ wgrad_x3_kernel(const WgradArgs a) {
 #pragma unroll
     for (int hs = 0; hs < 2 * KH; ++hs) {   // (half, 16-position k-substep)
       const int hh = hs >> 1, ks = hs & 1;
+      if constexpr (KB > 1) {   // 128-row waves: one G row block's fragments live at a time
+        bf16x8 gb[RN][PL];
+#pragma unroll
+        for (int p = 0; p < PL; ++p)
+#pragma unroll
+          for (int j = 0; j < RN; ++j)
+            gb[j][p] = frag(base + (DPL + 2 * (wnn >> 1) + p + hh) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
+#pragma unroll
+        for (int i = 0; i < RK; ++i) {
+          const int krow = wk * TK + 32 * i;
+          bf16x8 gi[PL];
+#pragma unroll
+          for (int p = 0; p < PL; ++p) gi[p] = frag(base + (2 * (krow >> 7) + p + hh) * PLANE, krow & 127, 16 * ks);
+#pragma unroll
+          for (int t = 0; t < TERMS; ++t)
+#pragma unroll
+            for (int j = 0; j < RN; ++j)
+              acc[i][j] = mfma_32x32x16<F16>(__builtin_bit_cast(u32x4, gi[t == 2 ? 1 : 0]),
+                                             __builtin_bit_cast(u32x4, gb[j][t == 1 ? 1 : 0]), acc[i][j]);
+        }
+        continue;
+      }
       bf16x8 ga[RK][PL], gb[RN][PL];
 #pragma unroll
       for (int p = 0; p < PL; ++p) {
 #pragma unroll
         for (int i = 0; i < RK; ++i)
-          if (!KP || 32 * i < kvw)
-            ga[i][p] = frag(base + (2 * (wk >> 1) + p + hh) * PLANE, (wk & 1) * TK + 32 * i, 16 * ks);
+          if (!KP || 32 * i < kvw) {
+            const int krow = wk * TK + 32 * i;   // G block krow / 128
+            ga[i][p] = frag(base + (2 * (krow >> 7) + p + hh) * PLANE, krow & 127, 16 * ks);
+          }
 #pragma unroll
         for (int j = 0; j < RN; ++j)
           gb[j][p] = frag(base + (DPL + 2 * (wnn >> 1) + p + hh) * PLANE, (wnn & 1) * TN + 32 * j, 16 * ks);
@@ -814,7 +844,7 @@ wgrad_x3_kernel(const WgradArgs a) {
     store_step(st0, 0);
   }
   int s = 0;
-  if constexpr (KH > 1) {
+  if constexpr (KH > 1 || KB > 1) {
     // one register staging set (prefetch distance one round = two 32-position steps,
     // as the two sets of the 32-position form): a round's loads are in flight during
     // the previous round's 16 MFMAs
