@@ -723,7 +723,7 @@ wgrad_x3_kernel(const WgradArgs a) {
     unsigned char* dbase = base + (DPL + 2 * (rbase >> 7) + hh) * PLANE;   // this thread's D block
     unsigned char* gbase = base + (2 * (rbase_g >> 7) + hh) * PLANE;      // ... and G block
 #pragma unroll
-    for (int q = 0; q < 2; ++q) {
+    for (int q = 0; q < (RJG > RJ ? RJG : RJ) / 8; ++q) {
       u32x4 GH, GL, DH, DL;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
