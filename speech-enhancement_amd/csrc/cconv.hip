@@ -1982,6 +1982,18 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     else if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<false, 3, true>), grid, dim3(kThreads), 0, st, a);
     else if (tu) hipLaunchKernelGGL(wgrad_x3_kernel<true>, grid, dim3(kThreads), 0, st, a);
     else hipLaunchKernelGGL(wgrad_x3_kernel<false>, grid, dim3(kThreads), 0, st, a);
+  } else if (split_ok && (g.sd != SE_DTYPE_F32 || g.math == SE_MATH_BF16) && w.Np % 256 == 0 && tu &&
+             w.c.Kp % 256 == 0) {
+    // one term on 256 x 256 tiles (as the split-fp16 ones above): DCCRN-CL bf16 train step
+    // 1276 -> 1321 utt/s (same box, profiles/ab/r5_wgrad_256x256_one_term_configs_ab.log)
+    const dim3 grid = x3_wgrad_grid(a, w, 2, 2);
+    const dim3 blk(2 * kThreads);
+    if (g.sd == SE_DTYPE_BF16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, false, 2, false, 1, 2>), grid, blk, 0, st, a);
+    else if (g.sd == SE_DTYPE_BF16) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 2, false, 1, 2>), grid, blk, 0, st, a);
+    else if (g.sd == SE_DTYPE_F16 && jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, true, 2, false, 2, 2>), grid, blk, 0, st, a);
+    else if (g.sd == SE_DTYPE_F16) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, true, 2, false, 2, 2>), grid, blk, 0, st, a);
+    else if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, false, 2, false, 0, 2>), grid, blk, 0, st, a);
+    else hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, false, false, 2, false, 0, 2>), grid, blk, 0, st, a);
   } else if (split_ok && g.sd != SE_DTYPE_F32) {   // 16-bit storage, one term of its format
     const dim3 grid = x3_wgrad_grid(a, w);
     if (g.sd == SE_DTYPE_BF16 && jn && tu) hipLaunchKernelGGL((wgrad_x3_kernel<true, 1, true, false, 1, false, 1>), grid, dim3(kThreads), 0, st, a);

@@ -551,7 +551,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   constexpr int ES = SD ? 2 : 4;             // bytes per element of X / D
   static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
-  static_assert(KB == 1 || (KB == 2 && NB == 2 && TERMS == 3 && !KP), "256 x 256 tiles: split-fp16 / bf16, full K");
+  static_assert(KB == 1 || (KB == 2 && NB == 2 && !KP), "256 x 256 tiles: full K");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
   constexpr int BKO = 128 * KB, BNO = 128 * NB, WNn = 2 * NB, TK = 64 * KB, TN = 64, RK = 2 * KB, RN = 2, BMR = 32;
   constexpr int RJ = 16;                     // D rows per thread
@@ -563,7 +563,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   // 32-position halves per staging round: one term stages two (64 positions; the lo
   // plane slots hold the second half), so a barrier feeds 16 MFMAs per wave, not 8;
   // the positions are accumulated in the same order, so the slabs are unchanged
-  constexpr int KH = TERMS == 1 ? kX3OneTermHalves : 1;
+  constexpr int KH = TERMS == 1 && KB == 1 ? kX3OneTermHalves : 1;   // 256 x 256: one half (registers)
   __shared__ __attribute__((aligned(16))) unsigned char sm[2][(2 * KB + 2 * NB) * PLANE];
   __shared__ int4 sK[BKO];
 
