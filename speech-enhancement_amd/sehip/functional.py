@@ -1253,6 +1253,17 @@ def _lstm_grads_hip(ctx, x, w_ih, h, dg, xa, wa, need):
     return dx, dw_ih, dw_hh, db
 
 
+def _bias_grads(ctx, db):
+    """(d b_ih, d b_hh): both equal sum_t dgates_t, as separate tensors. Handing autograd
+    the same tensor twice made the two parameters' .grad views of one buffer, which
+    clip_grad_norm_'s in-place scaling then visited twice, racing (run-to-run differences
+    in the LSTM biases, tools/determinism_probe.py)."""
+    if db is None:
+        return None, None
+    both = ctx.has_b[0] and ctx.has_b[1]
+    return (db if ctx.has_b[0] else None), ((db.clone() if both else db) if ctx.has_b[1] else None)
+
+
 class _LstmLayer(torch.autograd.Function):
     """One layer of L independent LSTMs run together (torch.nn.LSTM math,
     gate order i, f, g, o, zero initial state).
@@ -1356,8 +1367,7 @@ class _LstmLayer(torch.autograd.Function):
         if ctx.amax[0] is not None:   # the forward ran its projection on se_gemm
             need = (ctx.needs_input_grad[0], ctx.needs_input_grad[1], ctx.needs_input_grad[2], need_b)
             dx, dw_ih, dw_hh, db = _lstm_grads_hip(ctx, x, w_ih, h, dg, ctx.amax[0], ctx.amax[1], need)
-            db_ih = db if ctx.has_b[0] and need_b else None
-            db_hh = db if ctx.has_b[1] and need_b else None
+            db_ih, db_hh = _bias_grads(ctx, db if need_b else None)
             return dx, dw_ih, dw_hh, db_ih, db_hh, None
         if ctx.needs_input_grad[0]:
             if shared:
@@ -1386,9 +1396,7 @@ class _LstmLayer(torch.autograd.Function):
                         w -= dg[l, r - 1].t() @ hf[l, r]
                 dw_hh[l] = w
         if need_b:
-            db = _rows_sum(dg)
-            db_ih = db if ctx.has_b[0] else None
-            db_hh = db if ctx.has_b[1] else None
+            db_ih, db_hh = _bias_grads(ctx, _rows_sum(dg))
         return dx, dw_ih, dw_hh, db_ih, db_hh, None
 
 
