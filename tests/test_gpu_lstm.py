@@ -137,3 +137,28 @@ def test_lstm_rejects_cpu_and_bad_shapes(gpu_device):
         F.lstm_layer(torch.zeros(2, 3, 16), w_ih, w_hh)
     with pytest.raises(ValueError):
         F.lstm_layer(torch.zeros(2, 3, 8, device=gpu_device), w_ih.to(gpu_device), w_hh.to(gpu_device))
+
+
+@pytest.mark.parametrize("gemm", ["hip", "torch"])
+def test_bias_grads_do_not_share_storage(gpu_device, monkeypatch, gemm):
+    """b_ih and b_hh get the same gradient (sum over t of dgates) but must own separate
+    storage, as nn.LSTM's do: shared storage made clip_grad_norm_'s in-place kernel scale
+    it twice, racing (run-to-run differences in the LSTM biases after a train step)."""
+    from sehip.complex_nn import ComplexLSTM
+    from sehip.optim import clip_grad_norm_
+    monkeypatch.setenv("SEHIP_LSTM_GEMM", gemm)
+    torch.manual_seed(0)
+    m = ComplexLSTM(64, 64, num_layers=1, batch_first=True).to(gpu_device)
+    x = torch.randn(2, 7, 64, device=gpu_device)
+    (m(x) ** 2).sum().backward()
+    ptrs = [p.grad.untyped_storage().data_ptr() for p in m.parameters()]
+    assert len(set(ptrs)) == len(ptrs)
+    for lstm in (m.real_lstm, m.imag_lstm):
+        g_ih, g_hh = lstm.bias_ih_l0.grad.clone(), lstm.bias_hh_l0.grad.clone()
+        assert torch.equal(g_ih, g_hh)
+    # clipping scales each gradient once
+    ref = [p.grad.clone() for p in m.parameters()]
+    norm = clip_grad_norm_(m.parameters(), 1e-3)
+    s = 1e-3 / (norm.item() + 1e-6)
+    for p, r in zip(m.parameters(), ref):
+        assert torch.allclose(p.grad, r * s, rtol=1e-6, atol=0)
