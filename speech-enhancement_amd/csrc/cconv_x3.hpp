@@ -544,7 +544,7 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // row 256 k rows, a third fewer loads and splits per MFMA than 128 x 256)
 template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0,
           int KB = 1>
-__global__ void __launch_bounds__(kThreads * NB, 2)
+__global__ void __launch_bounds__(NB == 2 || KB == 2 ? 2 * kThreads : kThreads, 2)
 wgrad_x3_kernel(const WgradArgs a) {
   static_assert(TERMS == 1 || TERMS == 3, "hi*hi (SE_MATH_BF16), or hi*hi + hi*lo + lo*hi");
   static_assert(SD == 0 || TERMS == 1, "16-bit storage: one-term tiles");
@@ -553,10 +553,14 @@ wgrad_x3_kernel(const WgradArgs a) {
   static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
   static_assert(KB == 1 || (KB == 2 && NB == 2 && !KP), "256 x 256 tiles: full K");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
-  constexpr int BKO = 128 * KB, BNO = 128 * NB, WNn = 2 * NB, TK = 64 * KB, TN = 64, RK = 2 * KB, RN = 2, BMR = 32;
-  constexpr int RJ = 16;                     // D rows per thread
-  constexpr int RJG = 16 * KB / NB;          // G rows per thread
-  constexpr int GW = 32 * KB / NB;           // G rows per wave
+  // waves: 4 (128 x 128) or 8 (128 x 256, 256 x 256)
+  constexpr int NWV = NB == 2 || KB == 2 ? 8 : 4, THR = 64 * NWV;
+  constexpr int BKO = 128 * KB, BNO = 128 * NB, WNn = 2 * NB, TK = BKO * WNn / NWV, TN = 64, RK = TK / 32, RN = 2;
+  constexpr int BMR = 32;
+  constexpr int DWR = BNO / NWV;             // D rows per wave
+  constexpr int RJ = DWR / 2;                // D rows per thread
+  constexpr int GW = BKO / NWV;              // G rows per wave
+  constexpr int RJG = GW / 2;                // G rows per thread
   constexpr int PLANE = BMR * 256;           // bytes of one [32 positions][128 rows] bf16 plane
   // per 128-row G block: G hi, G lo; then per 128-row D block: D hi, D lo
   constexpr int DPL = 2 * KB;                // first D plane
@@ -590,10 +594,10 @@ wgrad_x3_kernel(const WgradArgs a) {
   const int kv = KP ? min(BKO, a.ntaps * a.Cg - k0) : BKO;
   const int kvw = kv - wk * TK;                       // ... of this wave's 64 MFMA rows
   const bool gact = GW * wave < kv;                   // this wave stages some valid G row
-  const int rbase = 32 * wave + RJ * lr;     // this thread's first D row
+  const int rbase = DWR * wave + RJ * lr;    // this thread's first D row
   const int rbase_g = GW * wave + RJG * lr;  // ... and first G row
 
-  for (int i = tid; i < BKO; i += kThreads) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
+  for (int i = tid; i < BKO; i += THR) sK[i] = a.ktab ? a.ktab[k0 + i] : wgrad_ktab(a, k0 + i);
   __syncthreads();
   float sg = 1.f, sd = 1.f;   // F16 (three terms): operand scales; the slab gets acc * 2^ush
   int ush = 0;
@@ -660,13 +664,13 @@ wgrad_x3_kernel(const WgradArgs a) {
     // Np-padded tail; tail rows read 0 through an out-of-range voffset (they
     // must not be read: past the last batch item they leave the allocation).
     const bool dok = mv & (n0 + rbase < a.N);
-    int vd, ds = (int)(QQ * ES), srow = 32 * wave;
+    int vd, ds = (int)(QQ * ES), srow = DWR * wave;
     __amdgpu_buffer_rsrc_t rdr = rd_src;
     if constexpr (DJ) {
       // joined D: chunks [x_re, s_re, x_im, s_im] (complex_concat) or [x_re, x_im, s_re,
       // s_im] (torch.cat, a.djcat) of djh rows; a wave's 32 rows lie in one chunk
       // (djh % 32 == 0)
-      const int nb = n0 + 32 * wave;
+      const int nb = n0 + DWR * wave;
       const int q = nb / a.djh;
       const bool from_x = a.djcat ? q < 2 : (q & 1) == 0;
       const int cr = (a.djcat ? (q & 1) : (q >> 1)) * a.djh + (nb - q * a.djh) + RJ * lr;   // row in its source
