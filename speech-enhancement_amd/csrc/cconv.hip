@@ -1901,8 +1901,9 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
   p = align256(p + (size_t)w.splits * w.c.Kp * w.Np * sizeof(float));
   int4* ktab = (int4*)p;
 
-  const bool x3_path = g.math == SE_MATH_F16X3 && split_ok && w.N > 32 && w.N > kSmallWgradN && w.Np != 32 &&
-                       w.c.taps.n <= kMaxTaps;
+  // every wgrad_x3_kernel launch below (split or one-term tiles) computes its tap table in
+  // the kernel; the fp32 / 32-column / small-N kernels read the prep pass's
+  const bool x3_path = split_ok && w.N > kSmallWgradN && w.Np != 32 && w.c.taps.n <= kMaxTaps;
   // ktab only (no weights): reuse prep_class_kernel with ldw = 1 writing into slab[0]
   // would clobber; build it with a one-column pass into a scratch row instead. The
   // split-fp16 weight-grad kernel computes its entries itself (no launch).
