@@ -524,22 +524,32 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
   // are written to LDS, so no convert waits on a load in flight
   // (se::uniform_ptr widens the two words as unsigned: a low word >= 2^31 must not
   // sign-extend into the high half of the base)
+  // joined input (a.X2, torch.cat order [x, s], DCUNet's decoder join): X holds s (2 jh
+  // channels per item, grid Hi x Wi), X2 holds x on its grid H2 x W2 (the F.pad zeros outside);
+  // a chunk of kScC channels lies in one source (jh % kScC == 0, checked by the host)
+  const bool jn = a.X2 != nullptr;
+  const int cpb = jn ? 2 * a.jh : a.Cg, H2W2 = a.H2 * a.W2;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
-      se::uniform_ptr((const char*)a.X + (long long)b * a.Cg * HiWi * ES), (short)0, 0x7FFFFFFF, 0x00020000);
+      se::uniform_ptr((const char*)a.X + (long long)b * cpb * HiWi * ES), (short)0, 0x7FFFFFFF, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rx2 = jn ? __builtin_amdgcn_make_buffer_rsrc(
+      se::uniform_ptr((const char*)a.X2 + (long long)b * cpb * H2W2 * ES), (short)0, 0x7FFFFFFF, 0x00020000) : rx;
   constexpr int PF = (chunk + kThreads - 1) / kThreads;
   typename StageT<SD>::T pf[PF];
   auto fetch = [&](int c0) __attribute__((always_inline)) {
+    const bool from_x = jn && c0 < cpb;                 // chunk-uniform source
+    const int cs = jn ? (from_x ? c0 : c0 - cpb) : c0;  // the chunk's first channel in its source
+    const int sh = from_x ? a.H2 : a.Hi, sw = from_x ? a.W2 : a.Wi, spl = from_x ? H2W2 : HiWi;
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int i = threadIdx.x + j * kThreads;
       const int c = i / plane, rr = i - c * plane;
       const int r = rr / tw, col = rr - r * tw;
       const int hi = qh0 + h0 + r, wi = qw0 + w0 + col;
-      const bool ok = (chunk % kThreads == 0 || i < chunk) && c0 + c < cg1 && (unsigned)hi < (unsigned)a.Hi && (unsigned)wi < (unsigned)a.Wi;
-      const int vo = ok ? ((c0 + c) * HiWi + hi * a.Wi + wi) * ES : (int)0x80000000;
-      if (ok) STC_CHECK(0, vo, (long long)a.Cg * HiWi * ES);
-      if constexpr (SD == 0) pf[j] = bload<0>(rx, vo, 0);
-      else pf[j] = bload_raw16(rx, vo, 0);
+      const bool ok = (chunk % kThreads == 0 || i < chunk) && c0 + c < cg1 && (unsigned)hi < (unsigned)sh && (unsigned)wi < (unsigned)sw;
+      const int vo = ok ? ((cs + c) * spl + hi * sw + wi) * ES : (int)0x80000000;
+      if (ok) STC_CHECK(0, vo, (long long)(jn ? cpb : a.Cg) * spl * ES);
+      if constexpr (SD == 0) pf[j] = bload<0>(from_x ? rx2 : rx, vo, 0);
+      else pf[j] = bload_raw16(from_x ? rx2 : rx, vo, 0);
     }
   };
   auto to_f32 = [](typename StageT<SD>::T v) __attribute__((always_inline)) {
@@ -1555,10 +1565,34 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     if (join_in) ok = ok && span * cpb * (long long)jn->h2 * jn->w2 * 4 < (1ll << 31);
     return ok;
   };
-  if (jn) {   // the joined forms exist on the split-bf16 / bf16 tap-uniform kernels only
-    if (!(x3 || x6) || (join_out && x6)) return SE_E_UNSUPPORTED;
-    for (const auto& c : cls)
-      if (!tu_of(c)) return SE_E_UNSUPPORTED;
+  // the chunked stencil's shape rules (many-channel stride-1 classes with N <= 4, e.g.
+  // DCUNet's final convT), shared by the dispatch below and the joined check
+  auto stc_ok = [&](const ClassPlan& c, int& hmin, int& wmin) {
+    const int nth = c.h.ntaps, ntw = c.w.ntaps;
+    bool hdesc = nth >= 1 && nth <= 4 && ntw >= 1 && c.taps.n <= kMaxTaps;
+    for (int t = 0; hdesc && t < c.taps.n; ++t)
+      hdesc = c.taps.offh[t] == c.h.off[0] - t / ntw && c.taps.offw[t] == c.w.off[t % ntw];
+    int wmax = c.w.off[0];
+    wmin = c.w.off[0];
+    for (int q = 1; q < ntw; ++q) { wmin = std::min(wmin, c.w.off[q]); wmax = std::max(wmax, c.w.off[q]); }
+    hmin = c.h.off[0] - (nth - 1);   // the window's first input row offset
+    const long long es = g.sd == SE_DTYPE_F32 ? 4 : 2;
+    bool ok = ldw <= 4 && Cg > 4 && c.h.s == 1 && c.w.s == 1 && hdesc && (long long)Cg * Hi * Wi * es < (1ll << 31) &&
+              wmax - wmin <= kScPitch - kStW && !env_flag_off("SEHIP_STENCIL");
+    // joined: gather side, torch.cat order, chunk-aligned sources
+    if (jn) ok = ok && join_in && !join_out && jn->cat && jn->jh % kScC == 0;
+    return ok;
+  };
+  if (jn) {   // the joined forms exist on the split-bf16 / bf16 tap-uniform kernels and the chunked stencil
+    const bool stc = N <= 4 && std::all_of(cls.begin(), cls.end(), [&](const ClassPlan& c) {
+      int hm, wm;
+      return stc_ok(c, hm, wm);
+    });
+    if (!stc) {
+      if (!(x3 || x6) || (join_out && x6)) return SE_E_UNSUPPORTED;
+      for (const auto& c : cls)
+        if (!tu_of(c)) return SE_E_UNSUPPORTED;
+    }
   }
   // the weight images: prepared by the caller (data-grad pass, desc.data_weights)
   // or built here in ws
@@ -1602,17 +1636,12 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
         SE_LAUNCH_CHECK();
         continue;
       }
-      // many-channel stride-1 classes (DCUNet's final convT): the chunked stencil
+      // many-channel stride-1 classes (DCUNet's final convT, also over its decoder join): the
+      // chunked stencil
       const int nth = c.h.ntaps, ntw = c.w.ntaps;
-      bool hdesc = nth >= 1 && nth <= 4 && ntw >= 1 && c.taps.n <= kMaxTaps;
-      for (int t = 0; hdesc && t < c.taps.n; ++t)
-        hdesc = c.taps.offh[t] == c.h.off[0] - t / ntw && c.taps.offw[t] == c.w.off[t % ntw];
-      int wmin = c.w.off[0], wmax = c.w.off[0];
-      for (int q = 1; q < ntw; ++q) { wmin = std::min(wmin, c.w.off[q]); wmax = std::max(wmax, c.w.off[q]); }
-      const int hmin = c.h.off[0] - (nth - 1);   // the window's first input row offset
-      const bool stencil_ch = !jn && ldw <= 4 && Cg > 4 && c.h.s == 1 && c.w.s == 1 && hdesc &&
-                              (long long)Cg * Hi * Wi * (g.sd == SE_DTYPE_F32 ? 4 : 2) < (1ll << 31) &&
-                              wmax - wmin <= kScPitch - kStW && !env_flag_off("SEHIP_STENCIL");
+      int hmin = 0, wmin = 0;
+      const bool stencil_ch = stc_ok(c, hmin, wmin);
+      if (jn && !stencil_ch) return SE_E_UNSUPPORTED;   // (excluded by the check above)
       if (stencil_ch) {
         a.ntaps = c.taps.n;
         for (int t = 0; t < c.taps.n; ++t) { a.toffh[t] = c.taps.offh[t]; a.toffw[t] = c.taps.offw[t]; }

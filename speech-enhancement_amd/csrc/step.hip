@@ -330,6 +330,79 @@ mask_bwd_kernel(const float* __restrict__ gest, const float* __restrict__ h, con
   }
 }
 
+// Magnitude / phase masks of the inference forward (no gradient), one pass instead of the
+// reference's ~20 elementwise kernels:
+//   mode 0, DCUNet bounded_tanh (_1903_03107_dcunet.py:167-189):
+//     ph = n_ph + m_ph / m_mag, gain = n_mag * tanh(m_mag)
+//   mode 1, DCCRN 'E' (_2008_00264_dccrn.py:194-207):
+//     m_ph = atan2(mi / m_mag, mr / m_mag), ph = n_ph + m_ph, gain = n_mag * tanh(m_mag)
+// with mag = sqrt(re^2 + im^2 + 1e-8), phase = atan2(im, re); out = gain * (cos ph, sin ph)
+// into [B, 2, F, T]. Each intermediate is rounded to the storage type T exactly where the
+// reference's tensors are (a bf16 / fp16 model computes every op in fp32 and stores T), in the
+// reference's operation order without contraction; the transcendental functions are this
+// toolchain's (torch's build may differ in the last ulp, which the phase terms can amplify).
+// m / n rows: batch stride, row stride (elements), time contiguous. grid (ceil(F T / 256), B)
+template <typename T>
+__device__ __forceinline__ float rt(float v) { return (float)(T)v; }
+template <typename T, int MODE>
+__global__ void __launch_bounds__(kThreads)
+polar_mask_fwd_kernel(const T* __restrict__ mr, const T* __restrict__ mi, long long msb, long long msr,
+                      const T* __restrict__ nr, const T* __restrict__ ni, long long nsb, long long nsr, int F, int Tn,
+                      T* __restrict__ out) {
+#pragma clang fp contract(off)   // one rounding per reference op: no fused multiply-adds
+  const int b = blockIdx.y;
+  const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (long long)F * Tn) return;
+  const int f = (int)(i / Tn), t = (int)(i - (long long)f * Tn);
+  const long long mo = b * msb + f * msr + t, no = b * nsb + f * nsr + t;
+  const float a = (float)mr[mo], c = (float)mi[mo], x = (float)nr[no], y = (float)ni[no];
+  auto mag = [](float re, float im) __attribute__((always_inline)) {
+    return rt<T>(sqrtf(rt<T>(rt<T>(rt<T>(re * re) + rt<T>(im * im)) + 1e-8f)));
+  };
+  const float m_mag = mag(a, c), n_mag = mag(x, y);
+  const float n_ph = rt<T>(atan2f(y, x));
+  float ph;
+  if constexpr (MODE == 0) {
+    const float m_ph = rt<T>(atan2f(c, a));
+    ph = rt<T>(n_ph + rt<T>(m_ph / m_mag));
+  } else {
+    const float m_ph = rt<T>(atan2f(rt<T>(c / m_mag), rt<T>(a / m_mag)));
+    ph = rt<T>(n_ph + m_ph);
+  }
+  const float gain = rt<T>(n_mag * rt<T>(tanhf(m_mag)));
+  const long long oo = (long long)b * 2 * F * Tn + i;
+  out[oo] = (T)(gain * rt<T>(cosf(ph)));
+  out[oo + (long long)F * Tn] = (T)(gain * rt<T>(sinf(ph)));
+}
+
+extern "C" int se_polar_mask_fwd(const void* mr, const void* mi, long long m_batch_stride, long long m_row_stride,
+                                 const void* nr, const void* ni, long long n_batch_stride, long long n_row_stride,
+                                 int B, int F, int T, int mode, int dtype, void* out, void* stream) {
+  if (!mr || !mi || !nr || !ni || !out || B <= 0 || F <= 0 || T <= 0 || (mode != 0 && mode != 1)) return SE_E_ARG;
+  const dim3 grid((unsigned)se::ceil_div((long long)F * T, kThreads), B);
+  hipStream_t st = se::as_stream(stream);
+#define SE_PM(TY)                                                                                                  \
+  do {                                                                                                             \
+    if (mode == 0)                                                                                                 \
+      hipLaunchKernelGGL((polar_mask_fwd_kernel<TY, 0>), grid, dim3(kThreads), 0, st, (const TY*)mr, (const TY*)mi, \
+                         m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, n_row_stride, F, \
+                         T, (TY*)out);                                                                            \
+    else                                                                                                           \
+      hipLaunchKernelGGL((polar_mask_fwd_kernel<TY, 1>), grid, dim3(kThreads), 0, st, (const TY*)mr, (const TY*)mi, \
+                         m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, n_row_stride, F, \
+                         T, (TY*)out);                                                                            \
+  } while (0)
+  switch (dtype) {
+    case SE_DTYPE_F32: SE_PM(float); break;
+    case SE_DTYPE_BF16: SE_PM(__bf16); break;
+    case SE_DTYPE_F16: SE_PM(_Float16); break;
+    default: return SE_E_ARG;
+  }
+#undef SE_PM
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
 extern "C" int se_mask_fwd(const float* h, const float* spec, int B, int half, int T, float* est, void* stream) {
   if (!h || !spec || !est || B <= 0 || half < 3 || T <= 0) return SE_E_ARG;
   hipLaunchKernelGGL(mask_fwd_kernel, dim3(se::ceil_div((long long)half * T, 4 * kThreads), 2 * B), dim3(kThreads), 0,

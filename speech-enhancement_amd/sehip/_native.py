@@ -60,7 +60,7 @@ class GemmDesc(ctypes.Structure):
 
 
 _P = c_void_p
-ABI_VERSION = 8   # SEHIP_ABI_VERSION (include/sehip.h)
+ABI_VERSION = 9   # SEHIP_ABI_VERSION (include/sehip.h)
 CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
@@ -118,6 +118,9 @@ _SIGNATURES = {
                           c_float, _P, _P, _P, _P, c_int, _P, c_size_t, _P]),
     "se_sisnr_save_bytes": (c_size_t, [c_int]),
     "se_mask_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P]),
+    "se_polar_mask_fwd": (c_int, [_P, _P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, ctypes.c_longlong,
+                                  ctypes.c_longlong, c_int, c_int,
+                                  c_int, c_int, c_int, _P, _P]),
     "se_mask_bwd": (c_int, [_P, _P, _P, c_int, c_int, c_int, _P, _P]),
     "se_sisnr_fwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P]),
     "se_sisnr_bwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P,

@@ -1045,6 +1045,31 @@ class _Mask(torch.autograd.Function):
         return gh, None, None
 
 
+POLAR_MASK_CALLS = [0]   # inference masks run by se_polar_mask_fwd (diagnostics / tests)
+
+
+def polar_mask_nograd(mr, mi, nr, ni, mode):
+    """The magnitude / phase masks of an inference forward in one pass (se_polar_mask_fwd):
+    mode 0 DCUNet's bounded_tanh (dcunet.py:167-189), mode 1 DCCRN's 'E' (dccrn.py:194-207).
+    mr / mi (mask) and nr / ni (noisy) are [B, F, T] planes, time contiguous. Returns
+    [B, 2, F, T] (real, imaginary), or None where autograd needs the graph (a training
+    forward keeps the reference's ops) or the planes do not fit the kernel's layout."""
+    ts = (mr, mi, nr, ni)
+    if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
+        return None
+    if (not mr.is_cuda or mr.dtype not in N.DTYPES or any(t.dtype != mr.dtype or t.device != mr.device for t in ts)
+            or any(t.dim() != 3 or t.shape != mr.shape or t.stride(2) != 1 for t in ts)
+            or mr.stride() != mi.stride() or nr.stride() != ni.stride()):
+        return None
+    B, Fq, T = mr.shape
+    out = torch.empty((B, 2, Fq, T), device=mr.device, dtype=mr.dtype)
+    N.check(N.lib().se_polar_mask_fwd(mr.data_ptr(), mi.data_ptr(), mr.stride(0), mr.stride(1), nr.data_ptr(),
+                                      ni.data_ptr(), nr.stride(0), nr.stride(1), B, Fq, T, int(mode),
+                                      N.dtype_code(mr), out.data_ptr(), N.stream_of(mr)), "se_polar_mask_fwd")
+    POLAR_MASK_CALLS[0] += 1
+    return out
+
+
 def complex_mask(h, spec, half):
     """FRCRN's est spectrum from the final_conv output h [B, 2, half-2, T] and the
     ConvSTFT output spec [B, 2 half, T] (no gradient into spec)."""

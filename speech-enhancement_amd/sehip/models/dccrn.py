@@ -175,8 +175,12 @@ class DCCRN(nn.Module):
         mr, mi = h[:, 0], h[:, 1]
         if mr.shape[-1] > nr.shape[-1]:
             mr, mi = mr[..., :-1], mi[..., :-1]
-        re, im = self._mask_processing(nr, ni, mr, mi)
-        est = torch.cat([re, im], dim=1)
+        est = F.polar_mask_nograd(mr, mi, nr, ni, 1) if self.masking == "E" else None
+        if est is not None:   # inference: mask and concat in one pass (se_polar_mask_fwd), the same values
+            est = est.view(est.shape[0], -1, est.shape[-1])
+        else:
+            re, im = self._mask_processing(nr, ni, mr, mi)
+            est = torch.cat([re, im], dim=1)
         return est, torch.clamp_(self.istft(est), -1, 1)
 
     def _mask_processing(self, noisy_real, noisy_imag, mask_real, mask_imag):

@@ -8,6 +8,7 @@ import torch.nn.functional as TF
 
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLeakyReLU,
                           mark_data_fed, norm_act, real_conv2d)
+from .. import functional as F
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 # name -> per-layer ((complex channels, real channels), kernel, stride, padding)
@@ -54,13 +55,14 @@ class _Block(nn.Module):
 
     def forward_joined(self, x, skip):
         """self(torch.cat([pad(x), skip])) (dcunet.py:84-94) with the pad and cat folded into the
-        convT's GEMMs (se_conv2d_*_joined, join_cat); None where no joined GEMM covers the
-        layer (a real conv, the 2-channel mask layer, or jh = C/2 not a multiple of 32). A pass
-        without a joined kernel for its shape materialises the cat for that pass only."""
+        convT's GEMMs (se_conv2d_*_joined, join_cat; the 2-channel mask layer's forward on the
+        chunked stencil); None where no joined kernel covers the layer (a real conv, or jh = C/2
+        not a multiple of 32). A pass without a joined kernel for its shape materialises the cat
+        for that pass only."""
         conv = getattr(self, self._attr)
         if (not isinstance(conv, ComplexConvTranspose2d) or not x.is_cuda or x.dtype != skip.dtype
                 or x.shape[1] != skip.shape[1] or x.shape[2] > skip.shape[2] or x.shape[3] > skip.shape[3]
-                or (x.shape[1] // 2) % 32 or conv.real_conv.out_channels * 2 <= 16):
+                or (x.shape[1] // 2) % 32):
             return None
         y = conv.forward_joined(x, skip, cat=True)
         return norm_act(self.norm, self.act, y)
@@ -181,6 +183,9 @@ class DCUNet(nn.Module):
             return noisy_spec * x
         if method == "bounded_sigmoid":
             return noisy_spec * torch.sigmoid(x)
+        fused = F.polar_mask_nograd(x[:, 0], x[:, 1], noisy_spec[:, 0], noisy_spec[:, 1], 0)
+        if fused is not None:   # inference: one pass (se_polar_mask_fwd), the same values
+            return fused
         m_mag, m_ph = self._return_mag_phase(x[:, 0], x[:, 1])
         n_mag, n_ph = self._return_mag_phase(noisy_spec[:, 0], noisy_spec[:, 1])
         ph = n_ph + m_ph / m_mag

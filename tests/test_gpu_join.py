@@ -181,6 +181,7 @@ CAT_JOINED = [   # (x shape, skip shape, kernel, stride, padding): DCUNet decode
     ((1, 128, 16, 31), (1, 128, 17, 33), (7, 5), (2, 2), (3, 2)), # DCUNet-16 width (jh = 64)
     ((2, 128, 8, 20), (2, 128, 9, 21), (5, 3), (2, 1), (2, 1), 64),   # 64 outputs (DCUNet-16 dec.)
     ((2, 64, 8, 20), (2, 64, 9, 21), (5, 3), (2, 1), (2, 1), 32),     # 32 outputs
+    ((2, 64, 16, 31), (2, 64, 17, 33), (7, 5), (2, 2), (3, 2), 2),   # DCUNet-16 mask layer: stencil
 ]
 
 
@@ -254,3 +255,29 @@ def test_joined_conv_16bit_storage_matches_materialised(gpu_device, dtype, cat, 
     for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), ref, got):
         assert a.dtype == dtype and b.dtype == dtype
         assert a.shape == b.shape and torch.equal(a, b), (dtype, cat, name, (a.float() - b.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_mask_layer_join_runs_on_the_chunked_stencil(gpu_device, dtype, monkeypatch):
+    """DCUNet's 2-output mask layer over its decoder join (dcunet.py:89-93 + the final convT):
+    the forward gathers x (zero-padded) and the skip straight into the chunked stencil's LDS
+    tiles, no materialised torch.cat; bit-identical to pad + cat + the plain conv in the
+    storage type, gradients included (the weight-grad of N = 2 materialises its join)."""
+    from sehip import functional as F
+    calls = []
+    raw = F._join_raw
+    monkeypatch.setattr(F, "_join_raw", lambda *a, **k: calls.append(1) or raw(*a, **k))
+    torch.manual_seed(2)
+    x = torch.randn(2, 64, 16, 31, device=gpu_device).to(dtype)
+    s = torch.randn(2, 64, 17, 33, device=gpu_device).to(dtype)
+    wr = (torch.randn(64, 1, 7, 5, device=gpu_device) * 0.05).to(dtype)
+    wi = (torch.randn(64, 1, 7, 5, device=gpu_device) * 0.05).to(dtype)
+    kw = dict(out_channels=2, kernel=(7, 5), stride=(2, 2), padding=(3, 2), transposed=True)
+    with torch.no_grad():
+        y = F.conv2d_joined(x, s, wr, wi, cat=True, **kw)
+        y_ref = F.conv2d(_cat_ref(x, s), wr, wi, **kw)
+    assert not calls, "the mask layer's joined forward materialised the cat"
+    assert torch.equal(y, y_ref), (y.float() - y_ref.float()).abs().max().item()
+    ref, got = _joined_pair(gpu_device, (2, 64, 16, 31), (2, 64, 17, 33), (7, 5), (2, 2), (3, 2), True, dtype, 2)
+    for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), ref, got):
+        assert a.shape == b.shape and torch.equal(a, b), (dtype, name, (a.float() - b.float()).abs().max().item())

@@ -1,0 +1,89 @@
+"""se_polar_mask_fwd (the inference masks of DCUNet / DCCRN, ABI 9) against the reference's
+own op sequences: DCUNet bounded_tanh (/root/reference/models/_1903_03107_dcunet.py:167-189)
+and DCCRN 'E' (/root/reference/models/_2008_00264_dccrn.py:194-207). The kernel rounds every
+intermediate to the storage type where the reference's tensors are rounded, in the same order
+and without contraction; its sin / cos / tanh / atan2 are this toolchain's, which may differ from
+torch's build in the last ulp, and the phase terms amplify such an ulp. So the gate is the
+reference's own: against an fp64 evaluation of the formula, the fused pass's error is within
+1.5x (+ a floor) of the torch op sequence's error in the same storage type."""
+import pytest
+import torch
+
+from sehip import functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _mag_phase(re, im):
+    return torch.sqrt(re ** 2 + im ** 2 + 1e-8), torch.atan2(im, re)
+
+
+def _ref(mr, mi, nr, ni, mode):
+    n_mag, n_ph = _mag_phase(nr, ni)
+    m_mag, m_ph = _mag_phase(mr, mi)
+    if mode == 0:
+        ph = n_ph + m_ph / m_mag
+    else:
+        ph = n_ph + torch.atan2(mi / m_mag, mr / m_mag)
+    gain = n_mag * torch.tanh(m_mag)
+    return torch.stack([gain * torch.cos(ph), gain * torch.sin(ph)], dim=1)
+
+
+def _rms(a, b):
+    return (a.double() - b.double()).pow(2).mean().sqrt().item()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_polar_mask_matches_reference_ops(dtype, mode):
+    g = torch.Generator(device="cuda").manual_seed(3 + mode)
+    B, Fq, T = 3, 65, 77
+    # strided planes as the models pass them: the mask trimmed out of a wider decoder
+    # output, the noisy halves of one spectrum
+    h = torch.randn(B, 2, Fq + 2, T + 3, device="cuda", generator=g)[:, :, :Fq, :T]
+    spec = 3 * torch.randn(B, 2 * Fq, T, device="cuda", generator=g)
+    if dtype != torch.float16:   # the atan2 / eps corners (1e-8 underflows in fp16)
+        h[0, :, :2, :5] = 0
+        spec[1, :3, :4] = 0
+        spec[1, Fq:Fq + 3, :4] = 0
+    h, spec = h.to(dtype), spec.to(dtype)
+    mr, mi, nr, ni = h[:, 0], h[:, 1], spec[:, :Fq], spec[:, Fq:]
+    with torch.no_grad():
+        got = F.polar_mask_nograd(mr, mi, nr, ni, mode)
+        want = _ref(mr, mi, nr, ni, mode)
+        exact = _ref(*(t.double() for t in (mr, mi, nr, ni)), mode)
+    assert got is not None and got.dtype == dtype and got.shape == (B, 2, Fq, T)
+    assert torch.isfinite(got).all() and torch.isfinite(want).all()
+    floor = 4 * torch.finfo(dtype).eps * exact.abs().max().item() / 64
+    e_got, e_ref = _rms(got, exact), _rms(want, exact)
+    assert e_got <= 1.5 * e_ref + floor, (e_got, e_ref, floor)
+
+
+def test_polar_mask_declines_a_training_forward():
+    m = torch.randn(2, 5, 7, device="cuda", requires_grad=True)
+    n = torch.randn(2, 5, 7, device="cuda")
+    assert F.polar_mask_nograd(m, m, n, n, 0) is None
+    with torch.no_grad():
+        assert F.polar_mask_nograd(m, m, n, n, 0) is not None
+
+
+def test_models_route_inference_through_the_fused_mask():
+    """A no-grad forward of DCUNet / DCCRN runs the fused mask; a grad-enabled one the
+    reference ops; the two agree to fp32 rounding (rel-L2 1e-5, north_star's 1e-4 bar).
+    Inputs: the variant goldens' waveforms (lengths the models' grids accept)."""
+    from conftest import golden
+    from sehip import models as M
+    torch.manual_seed(0)
+    for name, m in (("dcunet10", M.DCUNet("dcunet10", 512, 128, 512)),
+                    ("dccrn_bi", M.DCCRN("dccrn-CL", 400, 100, 512, bidirectional=True))):
+        x = torch.from_numpy(golden(f"variant_{name}")["x"]).cuda()
+        m = m.cuda().eval()
+        n0 = F.POLAR_MASK_CALLS[0]
+        with torch.no_grad():
+            est_f, wav_f = m(x)
+        assert F.POLAR_MASK_CALLS[0] == n0 + 1, name
+        est_r, wav_r = m(x)   # grad enabled, parameters require grad: the reference ops
+        assert F.POLAR_MASK_CALLS[0] == n0 + 1
+        for a, b in ((est_f, est_r.detach()), (wav_f, wav_r.detach())):
+            rel = ((a.double() - b.double()).norm() / b.double().norm()).item()
+            assert rel <= 1e-5, (name, rel)
