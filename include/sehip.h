@@ -28,7 +28,7 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 9   /* 9: se_polar_mask_fwd; 8: CL16 operands removed (se_pack_cl16*, se_conv2d_desc.x_packed /
+#define SEHIP_ABI_VERSION 9   /* 9: se_polar_mask_fwd / _bwd; 8: CL16 operands removed (se_pack_cl16*, se_conv2d_desc.x_packed /
                                  .x2_packed / .dy_packed / .x2_amax, se_cbn_fwd's y_packed,
                                  se_ccbam_apply's out_packed / out_amax: measured slower);
                                  7: measured-neutral variants removed (se_conv2d_desc.accumulate_dx /
@@ -523,7 +523,7 @@ int se_mask_fwd(const float* h, const float* spec, int B, int half, int T, float
 int se_mask_bwd(const float* gest, const float* h, const float* spec, int B, int half, int T, float* gh,
                 void* stream);
 
-/* The magnitude / phase masks of an inference forward (no gradient), ABI 9. mode 0: DCUNet's
+/* The magnitude / phase masks (DCUNet, DCCRN), ABI 9. mode 0: DCUNet's
  * bounded_tanh (models/_1903_03107_dcunet.py:167-189, ph = n_ph + m_ph / m_mag); mode 1: DCCRN's
  * 'E' (models/_2008_00264_dccrn.py:194-207, m_ph = atan2(mi / m_mag, mr / m_mag), ph = n_ph + m_ph);
  * both gain = n_mag * tanh(m_mag), mag = sqrt(re^2 + im^2 + 1e-8), phase = atan2(im, re).
@@ -533,6 +533,12 @@ int se_mask_bwd(const float* gest, const float* h, const float* spec, int B, int
 int se_polar_mask_fwd(const void* mr, const void* mi, long long m_batch_stride, long long m_row_stride,
                       const void* nr, const void* ni, long long n_batch_stride, long long n_row_stride, int B, int F,
                       int T, int mode, int dtype, void* out, void* stream);
+/* Its backward for a training forward (ABI 9): g = dL/dout [B, 2, F, T] -> dm [B, 2, F, T] =
+ * (dL/dmr, dL/dmi); the noisy planes take no gradient. fp32 arithmetic on the storage values
+ * (the forward's intermediates recomputed), gradients rounded to dtype once. */
+int se_polar_mask_bwd(const void* g, const void* mr, const void* mi, long long m_batch_stride,
+                      long long m_row_stride, const void* nr, const void* ni, long long n_batch_stride,
+                      long long n_row_stride, int B, int F, int T, int mode, int dtype, void* dm, void* stream);
 
 size_t se_sisnr_save_bytes(int B);
 int se_sisnr_fwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,

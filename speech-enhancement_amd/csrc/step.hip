@@ -403,6 +403,98 @@ extern "C" int se_polar_mask_fwd(const void* mr, const void* mi, long long m_bat
   return SE_OK;
 }
 
+// Backward of the masks above for a training forward (the mask takes the gradient, the
+// noisy spectrum none): from g = dL/d(re, im) [B, 2, F, T],
+//   d_gain = g_re cos ph + g_im sin ph,   d_ph = gain (g_im cos ph - g_re sin ph)
+//   d_mag  = d_gain n_mag (1 - tanh^2 m_mag)  (+ the phase path's m_mag terms)
+// through atan2 (d/dy = x / (x^2 + y^2), d/dx = -y / (x^2 + y^2), as torch's atan2 backward)
+// and m_mag = sqrt(mr^2 + mi^2 + 1e-8) (d/dmr = mr / m_mag). fp32 arithmetic on the storage
+// values, the forward's intermediates recomputed (T-rounded as in the forward), gradients
+// rounded to T once. dm [B, 2, F, T]: (d mr, d mi).
+template <typename T, int MODE>
+__global__ void __launch_bounds__(kThreads)
+polar_mask_bwd_kernel(const T* __restrict__ g, const T* __restrict__ mr, const T* __restrict__ mi, long long msb,
+                      long long msr, const T* __restrict__ nr, const T* __restrict__ ni, long long nsb, long long nsr,
+                      int F, int Tn, T* __restrict__ dm) {
+#pragma clang fp contract(off)
+  const int b = blockIdx.y;
+  const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= (long long)F * Tn) return;
+  const int f = (int)(i / Tn), t = (int)(i - (long long)f * Tn);
+  const long long mo = b * msb + f * msr + t, no = b * nsb + f * nsr + t;
+  const float a = (float)mr[mo], c = (float)mi[mo], x = (float)nr[no], y = (float)ni[no];
+  auto mag = [](float re, float im) __attribute__((always_inline)) {
+    return rt<T>(sqrtf(rt<T>(rt<T>(rt<T>(re * re) + rt<T>(im * im)) + 1e-8f)));
+  };
+  const float m_mag = mag(a, c), n_mag = mag(x, y);
+  const float n_ph = rt<T>(atan2f(y, x));
+  const float th = rt<T>(tanhf(m_mag));
+  const float gain = rt<T>(n_mag * th);
+  float ph, m_ph, u = 0.f, v = 0.f;
+  if constexpr (MODE == 0) {
+    m_ph = rt<T>(atan2f(c, a));
+    ph = rt<T>(n_ph + rt<T>(m_ph / m_mag));
+  } else {
+    u = rt<T>(a / m_mag);
+    v = rt<T>(c / m_mag);
+    m_ph = rt<T>(atan2f(v, u));
+    ph = rt<T>(n_ph + m_ph);
+  }
+  const long long oo = (long long)b * 2 * F * Tn + i, FT = (long long)F * Tn;
+  const float gre = (float)g[oo], gim = (float)g[oo + FT];
+  const float cp = cosf(ph), sp = sinf(ph);
+  const float d_gain = gre * cp + gim * sp;
+  const float d_ph = gain * (gim * cp - gre * sp);
+  float d_mag = d_gain * n_mag * (1.f - th * th);
+  float da, dc;
+  if constexpr (MODE == 0) {
+    const float d_mph = d_ph / m_mag;                 // ph = n_ph + m_ph / m_mag
+    d_mag += d_ph * (-m_ph / (m_mag * m_mag));
+    const float r2 = a * a + c * c;
+    da = d_mph * (-c / r2);
+    dc = d_mph * (a / r2);
+  } else {
+    const float r2 = u * u + v * v;                   // m_ph = atan2(v, u), u = mr / m_mag, v = mi / m_mag
+    const float du = d_ph * (-v / r2), dv = d_ph * (u / r2);
+    d_mag += du * (-a / (m_mag * m_mag)) + dv * (-c / (m_mag * m_mag));
+    da = du / m_mag;
+    dc = dv / m_mag;
+  }
+  da += d_mag * (a / m_mag);
+  dc += d_mag * (c / m_mag);
+  dm[oo] = (T)da;
+  dm[oo + FT] = (T)dc;
+}
+
+extern "C" int se_polar_mask_bwd(const void* g, const void* mr, const void* mi, long long m_batch_stride,
+                                 long long m_row_stride, const void* nr, const void* ni, long long n_batch_stride,
+                                 long long n_row_stride, int B, int F, int T, int mode, int dtype, void* dm,
+                                 void* stream) {
+  if (!g || !mr || !mi || !nr || !ni || !dm || B <= 0 || F <= 0 || T <= 0 || (mode != 0 && mode != 1)) return SE_E_ARG;
+  const dim3 grid((unsigned)se::ceil_div((long long)F * T, kThreads), B);
+  hipStream_t st = se::as_stream(stream);
+#define SE_PMB(TY)                                                                                                 \
+  do {                                                                                                             \
+    if (mode == 0)                                                                                                 \
+      hipLaunchKernelGGL((polar_mask_bwd_kernel<TY, 0>), grid, dim3(kThreads), 0, st, (const TY*)g, (const TY*)mr,  \
+                         (const TY*)mi, m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, \
+                         n_row_stride, F, T, (TY*)dm);                                                            \
+    else                                                                                                           \
+      hipLaunchKernelGGL((polar_mask_bwd_kernel<TY, 1>), grid, dim3(kThreads), 0, st, (const TY*)g, (const TY*)mr,  \
+                         (const TY*)mi, m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, \
+                         n_row_stride, F, T, (TY*)dm);                                                            \
+  } while (0)
+  switch (dtype) {
+    case SE_DTYPE_F32: SE_PMB(float); break;
+    case SE_DTYPE_BF16: SE_PMB(__bf16); break;
+    case SE_DTYPE_F16: SE_PMB(_Float16); break;
+    default: return SE_E_ARG;
+  }
+#undef SE_PMB
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
 extern "C" int se_mask_fwd(const float* h, const float* spec, int B, int half, int T, float* est, void* stream) {
   if (!h || !spec || !est || B <= 0 || half < 3 || T <= 0) return SE_E_ARG;
   hipLaunchKernelGGL(mask_fwd_kernel, dim3(se::ceil_div((long long)half * T, 4 * kThreads), 2 * B), dim3(kThreads), 0,

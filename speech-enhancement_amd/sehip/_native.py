@@ -122,6 +122,8 @@ _SIGNATURES = {
                                   ctypes.c_longlong, c_int, c_int,
                                   c_int, c_int, c_int, _P, _P]),
     "se_mask_bwd": (c_int, [_P, _P, _P, c_int, c_int, c_int, _P, _P]),
+    "se_polar_mask_bwd": (c_int, [_P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, ctypes.c_longlong,
+                                  ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, _P, _P]),
     "se_sisnr_fwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P]),
     "se_sisnr_bwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P,
                              ctypes.c_longlong, _P]),

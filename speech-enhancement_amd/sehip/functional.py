@@ -1045,7 +1045,58 @@ class _Mask(torch.autograd.Function):
         return gh, None, None
 
 
-POLAR_MASK_CALLS = [0]   # inference masks run by se_polar_mask_fwd (diagnostics / tests)
+POLAR_MASK_CALLS = [0]   # masks run by se_polar_mask_fwd (diagnostics / tests)
+
+
+def _polar_planes_ok(ts):
+    mr, mi, nr, ni = ts
+    return (mr.is_cuda and mr.dtype in N.DTYPES and all(t.dtype == mr.dtype and t.device == mr.device for t in ts)
+            and all(t.dim() == 3 and t.shape == mr.shape and t.stride(2) == 1 for t in ts)
+            and mr.stride() == mi.stride() and nr.stride() == ni.stride())
+
+
+def _polar_fwd(mr, mi, nr, ni, mode):
+    B, Fq, T = mr.shape
+    out = torch.empty((B, 2, Fq, T), device=mr.device, dtype=mr.dtype)
+    N.check(N.lib().se_polar_mask_fwd(mr.data_ptr(), mi.data_ptr(), mr.stride(0), mr.stride(1), nr.data_ptr(),
+                                      ni.data_ptr(), nr.stride(0), nr.stride(1), B, Fq, T, int(mode),
+                                      N.dtype_code(mr), out.data_ptr(), N.stream_of(mr)), "se_polar_mask_fwd")
+    POLAR_MASK_CALLS[0] += 1
+    return out
+
+
+class _PolarMask(torch.autograd.Function):
+    """DCCRN's 'E' mask (dccrn.py:194-207; or DCUNet's bounded_tanh, mode 0) as one pass each
+    way (se_polar_mask_fwd / _bwd); the noisy planes take no gradient."""
+
+    @staticmethod
+    def forward(ctx, mr, mi, nr, ni, mode):
+        ctx.save_for_backward(mr, mi, nr, ni)
+        ctx.mode = mode
+        return _polar_fwd(mr, mi, nr, ni, mode)
+
+    @staticmethod
+    def backward(ctx, g):
+        mr, mi, nr, ni = ctx.saved_tensors
+        g = g.contiguous()
+        B, Fq, T = mr.shape
+        dm = torch.empty((B, 2, Fq, T), device=g.device, dtype=g.dtype)
+        N.check(N.lib().se_polar_mask_bwd(g.data_ptr(), mr.data_ptr(), mi.data_ptr(), mr.stride(0), mr.stride(1),
+                                          nr.data_ptr(), ni.data_ptr(), nr.stride(0), nr.stride(1), B, Fq, T,
+                                          int(ctx.mode), N.dtype_code(mr), dm.data_ptr(), N.stream_of(g)),
+                "se_polar_mask_bwd")
+        return dm[:, 0], dm[:, 1], None, None, None
+
+
+def polar_mask(mr, mi, nr, ni, mode):
+    """The magnitude / phase mask as a differentiable HIP op (_PolarMask): [B, 2, F, T], or
+    None where the planes do not fit the kernels or the noisy planes need a gradient."""
+    ts = (mr, mi, nr, ni)
+    if not _polar_planes_ok(ts) or (torch.is_grad_enabled() and (nr.requires_grad or ni.requires_grad)):
+        return None
+    if torch.is_grad_enabled() and (mr.requires_grad or mi.requires_grad):
+        return _PolarMask.apply(mr, mi, nr, ni, int(mode))
+    return _polar_fwd(mr, mi, nr, ni, mode)
 
 
 def polar_mask_nograd(mr, mi, nr, ni, mode):
@@ -1057,17 +1108,9 @@ def polar_mask_nograd(mr, mi, nr, ni, mode):
     ts = (mr, mi, nr, ni)
     if torch.is_grad_enabled() and any(t.requires_grad for t in ts):
         return None
-    if (not mr.is_cuda or mr.dtype not in N.DTYPES or any(t.dtype != mr.dtype or t.device != mr.device for t in ts)
-            or any(t.dim() != 3 or t.shape != mr.shape or t.stride(2) != 1 for t in ts)
-            or mr.stride() != mi.stride() or nr.stride() != ni.stride()):
+    if not _polar_planes_ok(ts):
         return None
-    B, Fq, T = mr.shape
-    out = torch.empty((B, 2, Fq, T), device=mr.device, dtype=mr.dtype)
-    N.check(N.lib().se_polar_mask_fwd(mr.data_ptr(), mi.data_ptr(), mr.stride(0), mr.stride(1), nr.data_ptr(),
-                                      ni.data_ptr(), nr.stride(0), nr.stride(1), B, Fq, T, int(mode),
-                                      N.dtype_code(mr), out.data_ptr(), N.stream_of(mr)), "se_polar_mask_fwd")
-    POLAR_MASK_CALLS[0] += 1
-    return out
+    return _polar_fwd(mr, mi, nr, ni, mode)
 
 
 def complex_mask(h, spec, half):

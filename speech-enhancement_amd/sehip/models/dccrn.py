@@ -175,8 +175,8 @@ class DCCRN(nn.Module):
         mr, mi = h[:, 0], h[:, 1]
         if mr.shape[-1] > nr.shape[-1]:
             mr, mi = mr[..., :-1], mi[..., :-1]
-        est = F.polar_mask_nograd(mr, mi, nr, ni, 1) if self.masking == "E" else None
-        if est is not None:   # inference: mask and concat in one pass (se_polar_mask_fwd), the same values
+        est = F.polar_mask(mr, mi, nr, ni, 1) if self.masking == "E" else None
+        if est is not None:   # mask and concat in one pass each way (se_polar_mask_fwd / _bwd)
             est = est.view(est.shape[0], -1, est.shape[-1])
         else:
             re, im = self._mask_processing(nr, ni, mr, mi)

@@ -67,23 +67,70 @@ def test_polar_mask_declines_a_training_forward():
         assert F.polar_mask_nograd(m, m, n, n, 0) is not None
 
 
+def _ref_grads(mr, mi, nr, ni, mode, g):
+    a, c = mr.detach().clone().requires_grad_(True), mi.detach().clone().requires_grad_(True)
+    out = _ref(a, c, nr, ni, mode)
+    out.backward(g.to(out.dtype))
+    return out.detach(), a.grad, c.grad
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("mode", [0, 1])
+def test_polar_mask_backward_matches_autograd(dtype, mode):
+    """_PolarMask's backward (se_polar_mask_bwd) against autograd of the reference op sequence:
+    against fp64 autograd, its gradient error is within 1.5x (+ a floor) of torch's own in the
+    same storage type. Mask magnitudes >= 0.3 keep the phase terms (m_ph / m_mag,
+    atan2(v, u)) well conditioned, so the comparison measures the arithmetic, not the chaos."""
+    g = torch.Generator(device="cuda").manual_seed(11 + mode)
+    B, Fq, T = 2, 33, 51
+    r = 0.3 + torch.rand(B, Fq, T, device="cuda", generator=g)
+    th = 2 * torch.pi * torch.rand(B, Fq, T, device="cuda", generator=g)
+    mr, mi = (r * torch.cos(th)).to(dtype), (r * torch.sin(th)).to(dtype)
+    spec = (2 * torch.randn(B, 2, Fq, T, device="cuda", generator=g)).to(dtype)
+    nr, ni = spec[:, 0], spec[:, 1]
+    gout = torch.randn(B, 2, Fq, T, device="cuda", generator=g).to(dtype)
+    a, c = mr.clone().requires_grad_(True), mi.clone().requires_grad_(True)
+    n0 = F.POLAR_MASK_CALLS[0]
+    out = F.polar_mask(a, c, nr, ni, mode)
+    assert out is not None and F.POLAR_MASK_CALLS[0] == n0 + 1
+    out.backward(gout)
+    want = _ref_grads(mr, mi, nr, ni, mode, gout)
+    exact = _ref_grads(*(t.double() for t in (mr, mi, nr, ni)), mode, gout.double())
+    for name, x, w, e in zip(("out", "dmr", "dmi"), (out.detach(), a.grad, c.grad), want, exact):
+        floor = 4 * torch.finfo(dtype).eps * e.abs().max().item() / 64
+        e_got, e_ref = _rms(x, e), _rms(w, e)
+        assert e_got <= 1.5 * e_ref + floor, (name, e_got, e_ref, floor)
+
+
 def test_models_route_inference_through_the_fused_mask():
-    """A no-grad forward of DCUNet / DCCRN runs the fused mask; a grad-enabled one the
-    reference ops; the two agree to fp32 rounding (rel-L2 1e-5, north_star's 1e-4 bar).
-    Inputs: the variant goldens' waveforms (lengths the models' grids accept)."""
+    """DCUNet: a no-grad forward runs the fused mask, a grad-enabled one the reference ops.
+    DCCRN ('E'): both run the differentiable fused op; with it switched off the reference ops.
+    The two agree to fp32 rounding (rel-L2 1e-5, north_star's 1e-4 bar). Inputs: the variant
+    goldens' waveforms (lengths the models' grids accept)."""
     from conftest import golden
     from sehip import models as M
     torch.manual_seed(0)
-    for name, m in (("dcunet10", M.DCUNet("dcunet10", 512, 128, 512)),
-                    ("dccrn_bi", M.DCCRN("dccrn-CL", 400, 100, 512, bidirectional=True))):
-        x = torch.from_numpy(golden(f"variant_{name}")["x"]).cuda()
-        m = m.cuda().eval()
-        n0 = F.POLAR_MASK_CALLS[0]
-        with torch.no_grad():
-            est_f, wav_f = m(x)
-        assert F.POLAR_MASK_CALLS[0] == n0 + 1, name
-        est_r, wav_r = m(x)   # grad enabled, parameters require grad: the reference ops
-        assert F.POLAR_MASK_CALLS[0] == n0 + 1
-        for a, b in ((est_f, est_r.detach()), (wav_f, wav_r.detach())):
-            rel = ((a.double() - b.double()).norm() / b.double().norm()).item()
-            assert rel <= 1e-5, (name, rel)
+    x = torch.from_numpy(golden("variant_dcunet10")["x"]).cuda()
+    m = M.DCUNet("dcunet10", 512, 128, 512).cuda().eval()
+    n0 = F.POLAR_MASK_CALLS[0]
+    with torch.no_grad():
+        est_f, wav_f = m(x)
+    assert F.POLAR_MASK_CALLS[0] == n0 + 1
+    est_r, wav_r = m(x)   # grad enabled, parameters require grad: the reference ops
+    assert F.POLAR_MASK_CALLS[0] == n0 + 1
+    pairs = [(est_f, est_r.detach()), (wav_f, wav_r.detach())]
+    x = torch.from_numpy(golden("variant_dccrn_bi")["x"]).cuda()
+    m = M.DCCRN("dccrn-CL", 400, 100, 512, bidirectional=True).cuda().eval()
+    n0 = F.POLAR_MASK_CALLS[0]
+    est_f, wav_f = m(x)
+    assert F.POLAR_MASK_CALLS[0] == n0 + 1
+    polar = F.polar_mask
+    try:
+        F.polar_mask = lambda *a, **k: None
+        est_r, wav_r = m(x)
+    finally:
+        F.polar_mask = polar
+    pairs += [(est_f.detach(), est_r.detach()), (wav_f.detach(), wav_r.detach())]
+    for a, b in pairs:
+        rel = ((a.double() - b.double()).norm() / b.double().norm()).item()
+        assert rel <= 1e-5, rel
