@@ -28,7 +28,11 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 9   /* 9: se_polar_mask_fwd / _bwd; 8: CL16 operands removed (se_pack_cl16*, se_conv2d_desc.x_packed /
+#define SEHIP_ABI_VERSION 10  /* 10: 16-bit storage and row biases in se_gemm (the Linear layers), se_bias_grad,
+                                 se_copy_strided, the CARN mask / attention-gate / clamp passes, the
+                                 ComplexLSTM re/im combine, long-form chunking, 16-bit SI-SNR / clip / AdamW,
+                                 the polar masks' leading zero rows;
+                                 9: se_polar_mask_fwd / _bwd; 8: CL16 operands removed (se_pack_cl16*, se_conv2d_desc.x_packed /
                                  .x2_packed / .dy_packed / .x2_amax, se_cbn_fwd's y_packed,
                                  se_ccbam_apply's out_packed / out_amax: measured slower);
                                  7: measured-neutral variants removed (se_conv2d_desc.accumulate_dx /
@@ -405,20 +409,28 @@ int se_lstm_bwd(const float* dy, const float* w_hh, const float* gates,
                 unsigned rev_mask, void* stream);
 
 /* The LSTM layer GEMMs (ABI 6; replace the torch.addmm / bmm calls that the
- * nn.LSTM input projection and weight / input gradients ran on rocBLAS):
- *   C[b](m, n) = sum_k A(b, m, k) B(b, k, n) (+ bias0[b sbias + n] + bias1[...])
+ * nn.LSTM input projection and weight / input gradients ran on rocBLAS) and,
+ * ABI 10, every nn.Linear / ComplexLinear of the models (complex_nn.py:93-113,
+ * DCCRN's LSTMBlock dccrn.py:71-86, CARN's head carn.py:133,157-159):
+ *   C[b](m, n) = sum_k A(b, m, k) B(b, k, n) (+ bias0 + bias1)
  *   A(b, m, k) = A[b stride_a + m lda + k] (a_mcontig 0) | A[b stride_a + k lda + m] (1)
  *   B(b, k, n) = B[b stride_b + n ldb + k] (b_ncontig 0) | B[b stride_b + k ldb + n] (1)
  *   C[b](m, n) at C[b stride_c + m ldc + n]; sum_batches = 1: one C, the sum of
  *   the batch products (in batch order, inside the accumulation).
+ *   bias (bias0[b stride_bias + i] + bias1[...]) with i = n (bias_rows 0) or m (1).
  * A(m, k) reads as 0 where k % kmask_period == kmask_phase (period 0: none).
- * Arithmetic: scaled split-fp16 (f16x3, as SE_MATH_F16X3) with per-tensor
+ * dtype SE_DTYPE_F32: scaled split-fp16 (f16x3, as SE_MATH_F16X3) with per-tensor
  * power-of-two scales from amax_a / amax_b (device fp32 upper bounds of max |A|,
- * max |B|). splits: split-K slabs (0: the library picks from the shape); with
- * more than one the workspace holds the fp32 slabs, added in split order.
+ * max |B|). SE_DTYPE_BF16 / _F16 (ABI 10): A, B, C and the biases in that format,
+ * one-term MFMA of it (exact products, fp32 accumulation, C rounded once; amax
+ * pointers unused). splits: split-K slabs (0: the library picks from the shape);
+ * with more than one the workspace holds the fp32 slabs, added in split order.
  * se_colsum: out[l][g] = sum_r x[l][r][g] (the LSTM bias gradient; 64 row chunks,
  * each in row order, then the chunks in order) and, if amax is not NULL, max |x|
- * into *amax (the scale source of the weight-gradient GEMMs over x). */
+ * into *amax (the scale source of the weight-gradient GEMMs over x).
+ * se_bias_grad (ABI 10): out[g] = sum_l sum_r x[l sl + r sr + g sg] in fp32, rounded
+ * to dtype once (a Linear's bias gradient over any layout of dy; chunked like
+ * se_colsum when sg = 1, one wave per g over contiguous rows when sr = 1). */
 typedef struct se_gemm_desc {
   int M, N, K;
   int batches, sum_batches;
@@ -427,14 +439,43 @@ typedef struct se_gemm_desc {
   long long stride_a, stride_b, stride_c, stride_bias;
   int kmask_period, kmask_phase;
   int splits;
+  int dtype;       /* ABI 10: SE_DTYPE_* of A, B, C and the biases */
+  int bias_rows;   /* ABI 10: 1 = bias indexed by m */
 } se_gemm_desc;
 size_t se_gemm_workspace_size(const se_gemm_desc* d);
-int se_gemm(const se_gemm_desc* d, const float* A, const float* B, float* C, const float* bias0,
-            const float* bias1, const float* amax_a, const float* amax_b, void* ws, size_t ws_bytes,
+int se_gemm(const se_gemm_desc* d, const void* A, const void* B, void* C, const void* bias0,
+            const void* bias1, const float* amax_a, const float* amax_b, void* ws, size_t ws_bytes,
             void* stream);
 size_t se_colsum_workspace_size(int L, long long R, int G);
 int se_colsum(const float* x, int L, long long R, int G, float* out, float* amax, void* ws, size_t ws_bytes,
               void* stream);
+size_t se_bias_grad_workspace_size(int L, long long R, int G);
+int se_bias_grad(const void* x, int L, long long R, int G, long long sl, long long sr, long long sg, int dtype,
+                 void* out, void* ws, size_t ws_bytes, void* stream);
+
+/* Strided copy with a storage-type conversion (ABI 10): dst[i] = (dst type) src[i]
+ * over an ndim <= SE_COPY_MAX_DIMS index space (host arrays sizes / src_strides /
+ * dst_strides, in elements). The layout changes and casts of the models' glue
+ * (.contiguous() of a transposed or sliced view, .float() / .to(dtype), the
+ * re / im stacking of ComplexLSTM, the per-layer LSTM weight stacks) as one pass. */
+#define SE_COPY_MAX_DIMS 5
+int se_copy_strided(const void* src, int src_dtype, void* dst, int dst_dtype, int ndim, const long long* sizes,
+                    const long long* src_strides, const long long* dst_strides, void* stream);
+
+/* ComplexLSTM's output (complex_nn.py:134-142), ABI 10: from the stacked
+ * recurrence h [2][2B][T][H] fp32 (LSTM 0 = real_lstm, 1 = imag_lstm; batch rows
+ * [0, B) ran the real part, [B, 2B) the imaginary part; h_lstm_stride between the
+ * LSTMs) -> out[b, t, k] (dtype): re = real(re) - imag(im) for k < H,
+ * im = imag(re) + real(im) for k >= H, at out + b out_batch_stride + t out_row_stride +
+ * k out_feature_stride (feature stride 1: [B, T, 2H] rows; row stride 1: the [B, 2H, T]
+ * layout a conv stack reads next). The backward scatters gout (same stride convention)
+ * into dh [2][2B][T][H] fp32 (every element written). */
+int se_complex_lstm_combine_fwd(const float* h, long long h_lstm_stride, int B, int T, int H, void* out,
+                                long long out_batch_stride, long long out_row_stride, long long out_feature_stride,
+                                int dtype, void* stream);
+int se_complex_lstm_combine_bwd(const void* gout, long long g_batch_stride, long long g_row_stride,
+                                long long g_feature_stride, int B, int T, int H, int dtype, float* dh,
+                                long long dh_lstm_stride, void* stream);
 
 /* Wide hidden sizes, H in {256, 512, 1024} (CARN's nn.LSTM(512), models/
  * _2104_05267_carn.py:132; CRN's nn.LSTM(1024), models/_1809_01405_crn.py:90;
@@ -532,25 +573,38 @@ int se_mask_bwd(const float* gest, const float* h, const float* spec, int B, int
  * rounded to it as the reference's tensors are. Replaces ~20 elementwise kernels. */
 int se_polar_mask_fwd(const void* mr, const void* mi, long long m_batch_stride, long long m_row_stride,
                       const void* nr, const void* ni, long long n_batch_stride, long long n_row_stride, int B, int F,
-                      int T, int mode, int dtype, void* out, void* stream);
-/* Its backward for a training forward (ABI 9): g = dL/dout [B, 2, F, T] -> dm [B, 2, F, T] =
- * (dL/dmr, dL/dmi); the noisy planes take no gradient. fp32 arithmetic on the storage values
- * (the forward's intermediates recomputed), gradients rounded to dtype once. */
+                      int T, int mode, int dtype, int m_row0, void* out, void* stream);
+/* Its backward for a training forward (ABI 9): g = dL/dout [B, 2, F, T] -> dm = (dL/dmr, dL/dmi);
+ * the noisy planes take no gradient. fp32 arithmetic on the storage values (the forward's
+ * intermediates recomputed), gradients rounded to dtype once.
+ * ABI 10, m_row0: the mask's first m_row0 rows are zeros that are not stored (DCCRN's
+ * F.pad(mask, (0, 0, 1, 0)), dccrn.py:172): mask row f >= m_row0 is read at stored row
+ * f - m_row0. dm is [B, 2, F - m_row0, dm_T] (dm_T >= T; columns t >= T written as 0: the
+ * frame the reference trims off the mask, dccrn.py:180-182), the gradient of the stored mask. */
 int se_polar_mask_bwd(const void* g, const void* mr, const void* mi, long long m_batch_stride,
                       long long m_row_stride, const void* nr, const void* ni, long long n_batch_stride,
-                      long long n_row_stride, int B, int F, int T, int mode, int dtype, void* dm, void* stream);
+                      long long n_row_stride, int B, int F, int T, int mode, int dtype, int m_row0, int dm_T,
+                      void* dm, void* stream);
 
+/* ABI 10: dtype (SE_DTYPE_*) is the storage type of est, target, loss, grad_loss and
+ * grad_est (a model.to(bfloat16) / .half() run); the sums stay fp64, the loss and the
+ * gradient are rounded to dtype once. The slot tables' param / grad / exp_avg /
+ * exp_avg_sq are all of the slot functions' dtype: 16-bit AdamW rounds each
+ * intermediate to it where torch's foreach AdamW stores one (p *= 1 - lr wd;
+ * m.lerp_(g, 1 - b1); v *= b2; v.addcmul_(g, g, 1 - b2); d = sqrt(v) / bc2_sqrt + eps in
+ * three rounded steps; p.addcdiv_(m, d, -step_size)), and 16-bit clipping scales by
+ * the coefficient rounded to dtype (torch multiplies by a dtype tensor). */
 size_t se_sisnr_save_bytes(int B);
-int se_sisnr_fwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
-                 int zero_mean, float eps, float* loss, void* save, void* stream);
-int se_sisnr_bwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
-                 int zero_mean, float eps, const void* save, const float* grad_loss, float* grad_est,
-                 long long grad_stride, void* stream);
-int se_grad_sumsq(const se_tensor_slot* slots, int nslots, long long total, double* sumsq, void* stream);
+int se_sisnr_fwd(const void* est, int le, long long est_stride, const void* target, int lt, int B,
+                 int zero_mean, float eps, void* loss, void* save, int dtype, void* stream);
+int se_sisnr_bwd(const void* est, int le, long long est_stride, const void* target, int lt, int B,
+                 int zero_mean, float eps, const void* save, const void* grad_loss, void* grad_est,
+                 long long grad_stride, int dtype, void* stream);
+int se_grad_sumsq(const se_tensor_slot* slots, int nslots, long long total, double* sumsq, int dtype, void* stream);
 int se_clip_grads(const se_tensor_slot* slots, int nslots, long long total, const double* sumsq,
-                  float max_norm, float* total_norm, void* stream);
+                  float max_norm, float* total_norm, int dtype, void* stream);
 int se_adamw_step(const se_tensor_slot* slots, int nslots, long long total, double lr, double beta1,
-                  double beta2, double eps, double weight_decay, long long step, void* stream);
+                  double beta2, double eps, double weight_decay, long long step, int dtype, void* stream);
 
 /* ------------------------------------------------------------------------
  * Complex CBAM skip attention (models/modules/ccbam.py:28-106), the passes
@@ -607,6 +661,50 @@ int se_ccbam_mlp_bwd(const float* dca, const float* ca, const float* mean, const
                      const float* hsave, const float* w1r, const float* w1i, const float* w2r,
                      const float* w2i, int B, int C, int Hd, float* dmean, float* dmx,
                      float* dw1r, float* dw1i, float* dw2r, float* dw2i, void* stream);
+
+/* ------------------------------------------------------------------------
+ * CARN / GCARN glue (models/_2104_05267_carn.py), ABI 10. dtype SE_DTYPE_* of
+ * every tensor; fp32 arithmetic, rounded to dtype where the reference's tensors are.
+ *
+ * se_carn_mask_fwd (carn.py:161-168): m [B, 2, half, T] (the head Linear's output,
+ * batch stride m_batch_stride, planes contiguous), spec [B, 2 half, T] (the
+ * ConvSTFT output: rows [0, half) real, [half, 2 half) imag) ->
+ *   est[b, f]        = mr nr - mi ni
+ *   est[b, half + f] = mr ni - mi nr        (the reference's sign, as written)
+ * se_carn_mask_bwd: gest -> dm [B, 2, half, T] and, if dspec is not NULL, dspec.
+ * se_add_sigmoid_fwd: y = sigmoid(a + b) (Attention, carn.py:70-72); se_sigmoid_bwd:
+ * dz = g (1 - y) y (torch's sigmoid_backward), the gradient of both a and b.
+ * se_gate_cat_fwd: out [B, 2C, HW] = cat(sigmoid(c) * skip, skip) (carn.py:74-76 and
+ * the decoder's torch.cat, :112-113); se_gate_cat_bwd: dc, dskip (both halves).
+ * se_glu_fwd / _bwd: y = a * sigmoid(b) (ConvGLU / DeConvGLU, carn.py:9-27).
+ * se_clamp_fwd / _bwd: y = clamp(x, lo, hi); dx = g where lo <= x <= hi else 0
+ * (the models' torch.clamp_(wav, -1, 1), e.g. carn.py:170, frcrn.py:154).
+ * ------------------------------------------------------------------------ */
+int se_carn_mask_fwd(const void* m, long long m_batch_stride, const void* spec, int B, int half, int T, int dtype,
+                     void* est, void* stream);
+int se_carn_mask_bwd(const void* gest, const void* m, long long m_batch_stride, const void* spec, int B, int half,
+                     int T, int dtype, void* dm, void* dspec, void* stream);
+int se_add_sigmoid_fwd(const void* a, const void* b, void* y, long long n, int dtype, void* stream);
+int se_sigmoid_bwd(const void* g, const void* y, void* dz, long long n, int dtype, void* stream);
+int se_gate_cat_fwd(const void* c, const void* skip, void* out, int B, int C, long long HW, int dtype, void* stream);
+int se_gate_cat_bwd(const void* gout, const void* c, const void* skip, void* dc, void* dskip, int B, int C,
+                    long long HW, int dtype, void* stream);
+int se_glu_fwd(const void* a, const void* b, void* y, long long n, int dtype, void* stream);
+int se_glu_bwd(const void* g, const void* a, const void* b, void* da, void* db, long long n, int dtype,
+               void* stream);
+int se_clamp_fwd(const void* x, void* y, long long n, float lo, float hi, int dtype, void* stream);
+int se_clamp_bwd(const void* g, const void* x, void* dx, long long n, float lo, float hi, int dtype, void* stream);
+
+/* Long-form chunking (sehip/longform.py, BASELINE config 5), ABI 10:
+ * se_chunk_split: out [n, chunk] = x[i hop + s] (0 at or past L);
+ * se_chunk_overlap_add: y [n, width] (the enhanced chunks, 0 past width) ->
+ * out [length]: each chunk weighted by a linear cross-fade over its overlaps
+ * (fade in (j + 0.5) / overlap on its first `overlap` samples unless first, fade out
+ * 1 - that on its last unless last), summed in chunk order, rounded to dtype at
+ * each step as the reference-side loop does. */
+int se_chunk_split(const void* x, long long L, int n, int chunk, int hop, int dtype, void* out, void* stream);
+int se_chunk_overlap_add(const void* y, int n, int width, int chunk, int overlap, long long length, int dtype,
+                         void* out, void* stream);
 
 /* ------------------------------------------------------------------------
  * Decoder skip join (models/_2206_07293_frcrn.py:93-100 + complex_concat,

@@ -20,6 +20,14 @@
 // swizzled [plane][row][4 x 16 B] layout. Long reductions (the weight
 // gradients: K = B*T rows) are split over K into fp32 slabs, added in split
 // order by gemm_reduce_kernel (deterministic).
+//
+// 16-bit storage (se_gemm_desc.dtype = SE_DTYPE_BF16 / _F16, ABI 10: the
+// Linear layers of a model.to(bfloat16) / .half() model, nn.Linear's own
+// arithmetic): A, B, C and the biases are read and written in that format,
+// the products run on the one-term v_mfma_f32_32x32x16_{bf16,f16} (exact
+// products, fp32 accumulation), no scales; C is rounded once. bias_rows = 1
+// adds the bias by row m instead of column n (a Linear evaluated as W x^T,
+// whose output rows are the features).
 #include "common.hpp"
 
 #include <algorithm>
@@ -31,6 +39,8 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kTop = 14;                 // scaled values stay below 2^14 (fp16 max 65504)
@@ -51,9 +61,16 @@ __device__ __forceinline__ void split_f16x2(float x0, float x1, float s, unsigne
   lo = __builtin_bit_cast(unsigned, __builtin_convertvector(v - __builtin_convertvector(h, f32x2), f16x2));
 }
 
-__device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
-  return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
-                                                0, 0);
+// storage formats: S = float (split-fp16 x3 arithmetic), __bf16 / _Float16 (one term)
+template <typename S> constexpr bool is16() { return sizeof(S) == 2; }
+template <typename S>
+__device__ __forceinline__ f32x16 mfma1(u32x4 a, u32x4 b, f32x16 c) {
+  if constexpr (__is_same(S, __bf16))
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0,
+                                                   0, 0);
+  else
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0,
+                                                  0, 0);
 }
 
 // 16-B chunk c of image row `row` sits at c ^ swz(row): the 32x32x16 fragment
@@ -61,11 +78,11 @@ __device__ __forceinline__ f32x16 mfma16(u32x4 a, u32x4 b, f32x16 c) {
 __device__ __forceinline__ int swz(int row) { return (row >> 2) & 3; }
 
 struct GemmArgs {
-  const float* A;
-  const float* B;
-  float* C;
-  const float* bias0;
-  const float* bias1;
+  const void* A;
+  const void* B;
+  void* C;
+  const void* bias0;
+  const void* bias1;
   const float* amax_a;
   const float* amax_b;
   float* slab;                 // splits > 1: [nbz][splits][M][N]
@@ -76,6 +93,7 @@ struct GemmArgs {
   int splits, kps;             // K-steps per split
   int kmask_T, kmask_p;
   int vec_a, vec_b;            // the K-contiguous operand may use 16-B loads
+  int bias_rows;               // bias by row m (1) or column n (0)
 };
 
 // 16 consecutive k of one row of a K-contiguous operand (row stride ld): 16-B
@@ -100,10 +118,43 @@ __device__ __forceinline__ void load_kcol(const float* p, long long ld, bool rok
   for (int j = 0; j < 16; ++j) v[j] = (rok && j < kleft) ? p[(long long)j * ld] : 0.f;
 }
 
-template <bool AM, bool BNC>
+// 16-bit storage: the 16 values as the 8 packed pairs the MFMA operand image holds
+// (element 2i in the low half of word i), straight from memory; 0 bits are +0
+__device__ __forceinline__ void load_krow16(const unsigned short* p, bool rok, int kleft, bool vec,
+                                            unsigned (&w)[8]) {
+  if (rok && vec && kleft >= 16) {
+    const u32x4 t0 = reinterpret_cast<const u32x4*>(p)[0];
+    const u32x4 t1 = reinterpret_cast<const u32x4*>(p)[1];
+    w[0] = t0.x; w[1] = t0.y; w[2] = t0.z; w[3] = t0.w;
+    w[4] = t1.x; w[5] = t1.y; w[6] = t1.z; w[7] = t1.w;
+  } else {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const unsigned lo = (rok && 2 * j < kleft) ? p[2 * j] : 0u;
+      const unsigned hi = (rok && 2 * j + 1 < kleft) ? p[2 * j + 1] : 0u;
+      w[j] = lo | (hi << 16);
+    }
+  }
+}
+
+__device__ __forceinline__ void load_kcol16(const unsigned short* p, long long ld, bool rok, int kleft,
+                                            unsigned (&w)[8]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const unsigned lo = (rok && 2 * j < kleft) ? p[(long long)(2 * j) * ld] : 0u;
+    const unsigned hi = (rok && 2 * j + 1 < kleft) ? p[(long long)(2 * j + 1) * ld] : 0u;
+    w[j] = lo | (hi << 16);
+  }
+}
+
+template <bool AM, bool BNC, typename S>
 __global__ void __launch_bounds__(kThr, 2) gemm_x3_kernel(const GemmArgs a) {
-  __shared__ __attribute__((aligned(16))) u32x4 sA[2][2 * kBM * 4];   // [buf][plane][row][4]
-  __shared__ __attribute__((aligned(16))) u32x4 sB[2][2 * kBN * 4];
+  constexpr bool X3 = !is16<S>();
+  constexpr int NP = X3 ? 2 : 1;                                     // LDS planes: hi (+ lo)
+  __shared__ __attribute__((aligned(16))) u32x4 sA[2][NP * kBM * 4];   // [buf][plane][row][4]
+  __shared__ __attribute__((aligned(16))) u32x4 sB[2][NP * kBN * 4];
+  const S* Ap = static_cast<const S*>(a.A);
+  const S* Bp = static_cast<const S*>(a.B);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wn = wave >> 1, wm = wave & 1;
   const int NT = (a.N + kBN - 1) / kBN;
@@ -114,16 +165,23 @@ __global__ void __launch_bounds__(kThr, 2) gemm_x3_kernel(const GemmArgs a) {
   const int ktot = a.sum_b ? a.nb * ksb : ksb;
   const int kbeg = split * a.kps, kend = min(ktot, kbeg + a.kps);
 
-  const int ea = amax_exp(a.amax_a), eb = amax_exp(a.amax_b);
-  const float sa = pow2f(kTop - ea), sbs = pow2f(kTop - eb);
-  const int ush = ea + eb - 2 * kTop;
+  float sa = 1.f, sbs = 1.f;
+  int ush = 0;
+  if constexpr (X3) {
+    const int ea = amax_exp(a.amax_a), eb = amax_exp(a.amax_b);
+    sa = pow2f(kTop - ea);
+    sbs = pow2f(kTop - eb);
+    ush = ea + eb - 2 * kTop;
+  }
 
   // staging roles: a K-contiguous operand takes (row = tid / 2, k half = tid & 1),
   // a row-contiguous one (row = tid & 127, k half = tid >> 7)
   const int ra = AM ? (tid & 127) : (tid >> 1), kha = AM ? (tid >> 7) * 16 : (tid & 1) * 16;
   const int rb = BNC ? (tid & 127) : (tid >> 1), khb = BNC ? (tid >> 7) * 16 : (tid & 1) * 16;
   const int ma = m0 + ra, nbr = n0 + rb;
-  float va[16], vb[16];
+  // fp32: 16 values per operand row segment; 16-bit: the same 16 as 8 packed pairs
+  float va[X3 ? 16 : 1], vb[X3 ? 16 : 1];
+  unsigned wa[X3 ? 1 : 8], wb[X3 ? 1 : 8];
 
   auto load = [&](int ks) __attribute__((always_inline)) {
     const int bb = a.sum_b ? ks / ksb : bz;
@@ -131,28 +189,36 @@ __global__ void __launch_bounds__(kThr, 2) gemm_x3_kernel(const GemmArgs a) {
     {
       const int kk = k0 + kha, kleft = a.K - kk;
       const bool rok = ma < a.M;
-      if constexpr (AM) {
-        const float* p = a.A + bb * a.sa + (long long)kk * a.lda + (rok ? ma : 0);
-        load_kcol(p, a.lda, rok, kleft, va);
-      } else {
-        const float* p = a.A + bb * a.sa + (long long)(rok ? ma : 0) * a.lda + kk;
-        load_krow(p, rok, kleft, a.vec_a, va);
-      }
-      if (a.kmask_T) {
+      const long long off = AM ? bb * a.sa + (long long)kk * a.lda + (rok ? ma : 0)
+                               : bb * a.sa + (long long)(rok ? ma : 0) * a.lda + kk;
+      if constexpr (X3) {
+        const float* p = reinterpret_cast<const float*>(Ap) + off;
+        if constexpr (AM) load_kcol(p, a.lda, rok, kleft, va);
+        else load_krow(p, rok, kleft, a.vec_a, va);
+        if (a.kmask_T) {
 #pragma unroll
-        for (int j = 0; j < 16; ++j)
-          if ((kk + j) % a.kmask_T == a.kmask_p) va[j] = 0.f;
+          for (int j = 0; j < 16; ++j)
+            if ((kk + j) % a.kmask_T == a.kmask_p) va[j] = 0.f;
+        }
+      } else {
+        const unsigned short* p = reinterpret_cast<const unsigned short*>(Ap) + off;
+        if constexpr (AM) load_kcol16(p, a.lda, rok, kleft, wa);
+        else load_krow16(p, rok, kleft, a.vec_a, wa);
       }
     }
     {
       const int kk = k0 + khb, kleft = a.K - kk;
       const bool rok = nbr < a.N;
-      if constexpr (BNC) {
-        const float* p = a.B + bb * a.sb + (long long)kk * a.ldb + (rok ? nbr : 0);
-        load_kcol(p, a.ldb, rok, kleft, vb);
+      const long long off = BNC ? bb * a.sb + (long long)kk * a.ldb + (rok ? nbr : 0)
+                                : bb * a.sb + (long long)(rok ? nbr : 0) * a.ldb + kk;
+      if constexpr (X3) {
+        const float* p = reinterpret_cast<const float*>(Bp) + off;
+        if constexpr (BNC) load_kcol(p, a.ldb, rok, kleft, vb);
+        else load_krow(p, rok, kleft, a.vec_b, vb);
       } else {
-        const float* p = a.B + bb * a.sb + (long long)(rok ? nbr : 0) * a.ldb + kk;
-        load_krow(p, rok, kleft, a.vec_b, vb);
+        const unsigned short* p = reinterpret_cast<const unsigned short*>(Bp) + off;
+        if constexpr (BNC) load_kcol16(p, a.ldb, rok, kleft, wb);
+        else load_krow16(p, rok, kleft, a.vec_b, wb);
       }
     }
   };
@@ -160,19 +226,26 @@ __global__ void __launch_bounds__(kThr, 2) gemm_x3_kernel(const GemmArgs a) {
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       u32x4 H, L, HB, LB;
+      if constexpr (X3) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        unsigned h, l;
-        split_f16x2(va[8 * q + 2 * e], va[8 * q + 2 * e + 1], sa, h, l);
-        H[e] = h; L[e] = l;
-        split_f16x2(vb[8 * q + 2 * e], vb[8 * q + 2 * e + 1], sbs, h, l);
-        HB[e] = h; LB[e] = l;
+        for (int e = 0; e < 4; ++e) {
+          unsigned h, l;
+          split_f16x2(va[8 * q + 2 * e], va[8 * q + 2 * e + 1], sa, h, l);
+          H[e] = h; L[e] = l;
+          split_f16x2(vb[8 * q + 2 * e], vb[8 * q + 2 * e + 1], sbs, h, l);
+          HB[e] = h; LB[e] = l;
+        }
+      } else {
+        H = (u32x4){wa[4 * q], wa[4 * q + 1], wa[4 * q + 2], wa[4 * q + 3]};
+        HB = (u32x4){wb[4 * q], wb[4 * q + 1], wb[4 * q + 2], wb[4 * q + 3]};
       }
       const int ca = (kha / 8 + q) ^ swz(ra), cb = (khb / 8 + q) ^ swz(rb);
       sA[buf][ra * 4 + ca] = H;
-      sA[buf][kBM * 4 + ra * 4 + ca] = L;
       sB[buf][rb * 4 + cb] = HB;
-      sB[buf][kBN * 4 + rb * 4 + cb] = LB;
+      if constexpr (X3) {
+        sA[buf][kBM * 4 + ra * 4 + ca] = L;
+        sB[buf][kBN * 4 + rb * 4 + cb] = LB;
+      }
     }
   };
 
@@ -189,20 +262,30 @@ __global__ void __launch_bounds__(kThr, 2) gemm_x3_kernel(const GemmArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       const int c = (2 * ks + lh) ^ fsw;
-      u32x4 wf[2][2], af[2][2];
+      u32x4 wf[2][NP], af[2][NP];
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int p = 0; p < 2; ++p) {
+        for (int p = 0; p < NP; ++p) {
           wf[i][p] = sB[buf][(p * kBN + wn * 64 + 32 * i + lr) * 4 + c];
           af[i][p] = sA[buf][(p * kBM + wm * 64 + 32 * i + lr) * 4 + c];
         }
+      if constexpr (X3) {
 #pragma unroll
-      for (int t = 0; t < 3; ++t)   // hi*hi, hi*lo, lo*hi
+        for (int t = 0; t < 3; ++t)   // hi*hi, hi*lo, lo*hi
+#pragma unroll
+          for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_32x32x16_f16(
+                  __builtin_bit_cast(f16x8, af[j][t == 1 ? 1 : 0]), __builtin_bit_cast(f16x8, wf[i][t == 2 ? 1 : 0]),
+                  acc[j][i], 0, 0, 0);
+      } else {
 #pragma unroll
         for (int i = 0; i < 2; ++i)
 #pragma unroll
-          for (int j = 0; j < 2; ++j) acc[j][i] = mfma16(af[j][t == 1 ? 1 : 0], wf[i][t == 2 ? 1 : 0], acc[j][i]);
+          for (int j = 0; j < 2; ++j) acc[j][i] = mfma1<S>(af[j][0], wf[i][0], acc[j][i]);
+      }
     }
   };
 
@@ -224,32 +307,46 @@ __global__ void __launch_bounds__(kThr, 2) gemm_x3_kernel(const GemmArgs a) {
   // r2 is m = 32 j + 4 lh + (r2 & 3) + 8 (r2 >> 2), n = 32 i + lr, so each store
   // instruction writes two 128-B row segments
   const bool direct = a.splits == 1;
-  float* out = direct ? a.C + bz * a.sc : a.slab + ((long long)bz * a.splits + split) * a.M * a.N;
-  const int ld = direct ? a.ldc : a.N;
-  const float* b0 = a.bias0 ? a.bias0 + bz * a.sbias : nullptr;
-  const float* b1 = a.bias1 ? a.bias1 + bz * a.sbias : nullptr;
+  const S* b0 = direct && a.bias0 ? static_cast<const S*>(a.bias0) + bz * a.sbias : nullptr;
+  const S* b1 = direct && a.bias1 ? static_cast<const S*>(a.bias1) + bz * a.sbias : nullptr;
+  S* outc = static_cast<S*>(a.C) + bz * a.sc;
+  float* outs = a.slab + ((long long)bz * a.splits + split) * a.M * a.N;
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int n = n0 + wn * 64 + 32 * i + lr;
     if (n >= a.N) continue;
-    float bias = 0.f;
-    if (direct) {
-      if (b0) bias += b0[n];
-      if (b1) bias += b1[n];
+    float bias_n = 0.f;
+    if (!a.bias_rows) {
+      if (b0) bias_n += (float)b0[n];
+      if (b1) bias_n += (float)b1[n];
     }
 #pragma unroll
     for (int j = 0; j < 2; ++j)
 #pragma unroll
       for (int r2 = 0; r2 < 16; ++r2) {
         const int m = m0 + wm * 64 + 32 * j + 4 * lh + (r2 & 3) + 8 * (r2 >> 2);
-        if (m < a.M) out[(long long)m * ld + n] = __builtin_ldexpf(acc[j][i][r2], ush) + bias;
+        if (m >= a.M) continue;
+        const float v = X3 ? __builtin_ldexpf(acc[j][i][r2], ush) : acc[j][i][r2];
+        if (direct) {
+          float bias = bias_n;
+          if (a.bias_rows) {
+            if (b0) bias += (float)b0[m];
+            if (b1) bias += (float)b1[m];
+          }
+          outc[(long long)m * a.ldc + n] = (S)(v + bias);
+        } else {
+          outs[(long long)m * a.N + n] = v;
+        }
       }
   }
 }
 
 // C[bz](m, n) = sum over splits in order + biases. grid covers nbz * M * N
+template <typename S>
 __global__ void __launch_bounds__(256) gemm_reduce_kernel(const GemmArgs a, long long total) {
   const long long mn = (long long)a.M * a.N;
+  const S* b0 = static_cast<const S*>(a.bias0);
+  const S* b1 = static_cast<const S*>(a.bias1);
   for (long long idx = blockIdx.x * 256LL + threadIdx.x; idx < total; idx += (long long)gridDim.x * 256) {
     const int bz = (int)(idx / mn);
     const long long r = idx - bz * mn;
@@ -257,9 +354,10 @@ __global__ void __launch_bounds__(256) gemm_reduce_kernel(const GemmArgs a, long
     const float* s = a.slab + (long long)bz * a.splits * mn + r;
     float v = 0.f;
     for (int sp = 0; sp < a.splits; ++sp) v += s[sp * mn];
-    if (a.bias0) v += a.bias0[bz * a.sbias + n];
-    if (a.bias1) v += a.bias1[bz * a.sbias + n];
-    a.C[bz * a.sc + (long long)m * a.ldc + n] = v;
+    const int bi = a.bias_rows ? m : n;
+    if (b0) v += (float)b0[bz * a.sbias + bi];
+    if (b1) v += (float)b1[bz * a.sbias + bi];
+    static_cast<S*>(a.C)[bz * a.sc + (long long)m * a.ldc + n] = (S)v;
   }
 }
 
@@ -342,13 +440,16 @@ extern "C" size_t se_gemm_workspace_size(const se_gemm_desc* d) {
   return (size_t)p.nbz * p.splits * d->M * d->N * sizeof(float);
 }
 
-extern "C" int se_gemm(const se_gemm_desc* d, const float* A, const float* B, float* C, const float* bias0,
-                       const float* bias1, const float* amax_a, const float* amax_b, void* ws, size_t ws_bytes,
+extern "C" int se_gemm(const se_gemm_desc* d, const void* A, const void* B, void* C, const void* bias0,
+                       const void* bias1, const float* amax_a, const float* amax_b, void* ws, size_t ws_bytes,
                        void* stream) {
   Plan p;
   const int rc = plan_of(d, p);
   if (rc != SE_OK) return rc;
-  if (!A || !B || !C || !amax_a || !amax_b) return SE_E_ARG;
+  const int dt = d->dtype;
+  if (dt != SE_DTYPE_F32 && dt != SE_DTYPE_BF16 && dt != SE_DTYPE_F16) return SE_E_ARG;
+  if (!A || !B || !C || (dt == SE_DTYPE_F32 && (!amax_a || !amax_b))) return SE_E_ARG;
+  if (dt != SE_DTYPE_F32 && d->kmask_period) return SE_E_UNSUPPORTED;   // the masked form is fp32-only
   const size_t need = se_gemm_workspace_size(d);
   if (need && (!ws || ws_bytes < need)) return SE_E_WORKSPACE;
   GemmArgs a{};
@@ -360,24 +461,34 @@ extern "C" int se_gemm(const se_gemm_desc* d, const float* A, const float* B, fl
   a.nb = d->batches; a.sum_b = d->sum_batches ? 1 : 0;
   a.splits = p.splits; a.kps = p.kps;
   a.kmask_T = d->kmask_period; a.kmask_p = d->kmask_phase;
-  a.vec_a = !d->a_mcontig && ((uintptr_t)A & 15) == 0 && d->lda % 4 == 0 && d->stride_a % 4 == 0;
-  a.vec_b = !d->b_ncontig && ((uintptr_t)B & 15) == 0 && d->ldb % 4 == 0 && d->stride_b % 4 == 0;
+  a.bias_rows = d->bias_rows ? 1 : 0;
+  // 16-B row loads: 4 fp32 / 8 16-bit elements per load, every row start 16-B aligned
+  const int vq = dt == SE_DTYPE_F32 ? 4 : 8;
+  a.vec_a = !d->a_mcontig && ((uintptr_t)A & 15) == 0 && d->lda % vq == 0 && d->stride_a % vq == 0;
+  a.vec_b = !d->b_ncontig && ((uintptr_t)B & 15) == 0 && d->ldb % vq == 0 && d->stride_b % vq == 0;
   hipStream_t st = se::as_stream(stream);
   const dim3 grid(p.MT * p.NT, p.splits, p.nbz);
-  if (d->a_mcontig) {
-    if (d->b_ncontig) hipLaunchKernelGGL((gemm_x3_kernel<true, true>), grid, dim3(kThr), 0, st, a);
-    else hipLaunchKernelGGL((gemm_x3_kernel<true, false>), grid, dim3(kThr), 0, st, a);
-  } else {
-    if (d->b_ncontig) hipLaunchKernelGGL((gemm_x3_kernel<false, true>), grid, dim3(kThr), 0, st, a);
-    else hipLaunchKernelGGL((gemm_x3_kernel<false, false>), grid, dim3(kThr), 0, st, a);
-  }
-  SE_LAUNCH_CHECK();
-  if (p.splits > 1) {
-    const long long total = (long long)p.nbz * d->M * d->N;
-    const long long blocks = std::min<long long>((total + 255) / 256, 4096);
-    hipLaunchKernelGGL(gemm_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, st, a, total);
-    SE_LAUNCH_CHECK();
-  }
+  const long long total = (long long)p.nbz * d->M * d->N;
+  const long long blocks = std::min<long long>((total + 255) / 256, 4096);
+#define SE_GEMM_LAUNCH(S)                                                                                          \
+  do {                                                                                                             \
+    if (d->a_mcontig) {                                                                                            \
+      if (d->b_ncontig) hipLaunchKernelGGL((gemm_x3_kernel<true, true, S>), grid, dim3(kThr), 0, st, a);           \
+      else hipLaunchKernelGGL((gemm_x3_kernel<true, false, S>), grid, dim3(kThr), 0, st, a);                       \
+    } else {                                                                                                       \
+      if (d->b_ncontig) hipLaunchKernelGGL((gemm_x3_kernel<false, true, S>), grid, dim3(kThr), 0, st, a);          \
+      else hipLaunchKernelGGL((gemm_x3_kernel<false, false, S>), grid, dim3(kThr), 0, st, a);                      \
+    }                                                                                                              \
+    SE_LAUNCH_CHECK();                                                                                             \
+    if (p.splits > 1) {                                                                                            \
+      hipLaunchKernelGGL(gemm_reduce_kernel<S>, dim3((unsigned)blocks), dim3(256), 0, st, a, total);               \
+      SE_LAUNCH_CHECK();                                                                                           \
+    }                                                                                                              \
+  } while (0)
+  if (dt == SE_DTYPE_F32) SE_GEMM_LAUNCH(float);
+  else if (dt == SE_DTYPE_BF16) SE_GEMM_LAUNCH(__bf16);
+  else SE_GEMM_LAUNCH(_Float16);
+#undef SE_GEMM_LAUNCH
   return SE_OK;
 }
 

@@ -36,34 +36,38 @@ constexpr int kItemThreads = 1024;   // one workgroup per utterance: the whole C
 // [4] S, [5] N, [6] sum p, [7] sum (e' - p)  (doubles)
 constexpr int kSave = 8;
 
+template <typename T>
+__device__ __forceinline__ float rt(float v) { return (float)(T)v; }
+
+template <typename T>
 __global__ void __launch_bounds__(kItemThreads)
-sisnr_items_kernel(const float* __restrict__ est, int le, long long est_stride, const float* __restrict__ tgt, int lt,
+sisnr_items_kernel(const T* __restrict__ est, int le, long long est_stride, const T* __restrict__ tgt, int lt,
                    int zero_mean, double* __restrict__ save) {
   const int b = blockIdx.x;
-  const float* e = est + (long long)b * est_stride;
-  const float* t = tgt + (long long)b * lt;
+  const T* e = est + (long long)b * est_stride;
+  const T* t = tgt + (long long)b * lt;
   const int ne = min(le, lt);                 // estimate samples inside the target length
   __shared__ double red[kItemThreads / 64];
   float me = 0.f, mt = 0.f;
   if (zero_mean) {
     double se_ = 0, st = 0;
     for (int i = threadIdx.x; i < lt; i += kItemThreads) {
-      se_ += i < ne ? e[i] : 0.f;
-      st += t[i];
+      se_ += i < ne ? (float)e[i] : 0.f;
+      st += (float)t[i];
     }
     me = (float)(block_sum<double, kItemThreads>(se_, red) / lt);
     mt = (float)(block_sum<double, kItemThreads>(st, red) / lt);
   }
   double dot = 0, tt = 0;
   for (int i = threadIdx.x; i < lt; i += kItemThreads) {
-    const float ei = (i < ne ? e[i] : 0.f) - me, ti = t[i] - mt;
+    const float ei = (i < ne ? (float)e[i] : 0.f) - me, ti = (float)t[i] - mt;
     dot += (double)ei * ti;
     tt += (double)ti * ti;
   }
   const float dotf = (float)block_sum<double, kItemThreads>(dot, red), ttf = (float)block_sum<double, kItemThreads>(tt, red);
   double S = 0, Nn = 0, sp = 0, sr = 0;
   for (int i = threadIdx.x; i < lt; i += kItemThreads) {
-    const float ei = (i < ne ? e[i] : 0.f) - me, ti = t[i] - mt;
+    const float ei = (i < ne ? (float)e[i] : 0.f) - me, ti = (float)t[i] - mt;
     const float p = dotf * ti / ttf;          // proj = sum(e*t) * t / t_energy
     const float r = ei - p;
     S += (double)p * p;
@@ -81,8 +85,9 @@ sisnr_items_kernel(const float* __restrict__ est, int le, long long est_stride, 
   }
 }
 
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-sisnr_finalize_kernel(const double* __restrict__ save, int B, float eps, float* __restrict__ loss) {
+sisnr_finalize_kernel(const double* __restrict__ save, int B, float eps, T* __restrict__ loss) {
   __shared__ double red[kThreads / 64];
   double acc = 0;
   for (int b = threadIdx.x; b < B; b += kThreads) {
@@ -91,35 +96,36 @@ sisnr_finalize_kernel(const double* __restrict__ save, int B, float eps, float* 
     acc += (double)(10.f * log10f(sig / noi));
   }
   acc = block_sum(acc, red);
-  if (threadIdx.x == 0) loss[0] = (float)(-acc / B);
+  if (threadIdx.x == 0) loss[0] = (T)(float)(-acc / B);
 }
 
 // grid (ceil(le / kThreads / 4), B): d est[b, i] for i < le (0 past the target length)
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
-sisnr_bwd_kernel(const float* __restrict__ est, int le, long long est_stride, const float* __restrict__ tgt, int lt,
-                 int B, int zero_mean, float eps, const double* __restrict__ save, const float* __restrict__ gloss,
-                 float* __restrict__ gest, long long g_stride) {
+sisnr_bwd_kernel(const T* __restrict__ est, int le, long long est_stride, const T* __restrict__ tgt, int lt,
+                 int B, int zero_mean, float eps, const double* __restrict__ save, const T* __restrict__ gloss,
+                 T* __restrict__ gest, long long g_stride) {
   const int b = blockIdx.y;
   const double* s = save + (long long)b * kSave;
   const float me = (float)s[0], mt = (float)s[1], dotf = (float)s[2], ttf = (float)s[3];
   const float sig = (float)s[4] + eps, noi = (float)s[5] + eps;
   // L_b = 10 log10(sig / noi); loss = -mean_b L_b
-  const float k = -gloss[0] * 10.f / ((float)B * 2.302585093f);
+  const float k = -(float)gloss[0] * 10.f / ((float)B * 2.302585093f);
   const float cs = 2.f * k / sig, cn = -2.f * k / noi;      // dL/dp-part, dL/d(e'-p)-part
   const float gmean = zero_mean ? (float)((cs * s[6] + cn * s[7]) / lt) : 0.f;
-  const float* e = est + (long long)b * est_stride;
-  const float* t = tgt + (long long)b * lt;
+  const T* e = est + (long long)b * est_stride;
+  const T* t = tgt + (long long)b * lt;
   const int ne = min(le, lt);
   for (int u = 0; u < 4; ++u) {
     const int i = (blockIdx.x * 4 + u) * kThreads + threadIdx.x;
     if (i >= le) return;
     float g = 0.f;
     if (i < ne) {
-      const float ei = e[i] - me, ti = t[i] - mt;
+      const float ei = (float)e[i] - me, ti = (float)t[i] - mt;
       const float p = dotf * ti / ttf;
       g = cs * p + cn * (ei - p) - gmean;
     }
-    gest[(long long)b * g_stride + i] = g;
+    gest[(long long)b * g_stride + i] = (T)g;
   }
 }
 
@@ -162,12 +168,13 @@ __device__ __forceinline__ void for_each_elem(const Slot* slots, int nslots, lon
 
 // per-workgroup partial sums into out[1 + blockIdx.x]; sumsq_final_kernel adds
 // them in a fixed order into out[0] (deterministic, unlike fp64 atomics)
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
 sumsq_kernel(const Slot* __restrict__ slots, int nslots, long long total, double* __restrict__ out) {
   __shared__ double red[kThreads / 64];
   double acc = 0;
   for_each_elem(slots, nslots, total, [&](const Slot& s, long long i) {
-    const float g = s.grad[i];
+    const float g = (float)reinterpret_cast<const T*>(s.grad)[i];
     acc += (double)g * g;
   });
   acc = block_sum(acc, red);
@@ -184,14 +191,20 @@ sumsq_final_kernel(double* __restrict__ out, int nparts) {
 }
 
 // torch.nn.utils.clip_grad_norm_: coef = max_norm / (total_norm + 1e-6),
-// clamped to 1, every gradient multiplied by it
+// clamped to 1, every gradient multiplied by it. 16-bit gradients: torch's norms are
+// tensors of the gradients' dtype, so the total norm, its + 1e-6, the coefficient and
+// every product are rounded to it
+template <typename T>
 __global__ void __launch_bounds__(kThreads)
 clip_kernel(const Slot* __restrict__ slots, int nslots, long long total, const double* __restrict__ sumsq,
             float max_norm, float* __restrict__ norm_out) {
-  const float tn = (float)sqrt(*sumsq);
-  const float coef = fminf(max_norm / (tn + 1e-6f), 1.f);
+  const float tn = rt<T>((float)sqrt(*sumsq));
+  const float coef = fminf(rt<T>(max_norm / rt<T>(tn + 1e-6f)), 1.f);
   if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = tn;
-  for_each_elem(slots, nslots, total, [&](const Slot& s, long long i) { s.grad[i] *= coef; });
+  for_each_elem(slots, nslots, total, [&](const Slot& s, long long i) {
+    T* g = reinterpret_cast<T*>(s.grad);
+    g[i] = (T)((float)g[i] * coef);
+  });
 }
 
 // torch.optim.AdamW (foreach form, amsgrad off):
@@ -215,6 +228,33 @@ adamw_kernel(const Slot* __restrict__ slots, int nslots, long long total, float 
   });
 }
 
+// 16-bit parameters and state (a model.to(bfloat16) / .half() run): the same update with
+// every foreach op's result stored in T, as torch's _multi_tensor_adam (decoupled weight
+// decay) does: each _foreach_* call computes in fp32 and writes T
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+adamw16_kernel(const Slot* __restrict__ slots, int nslots, long long total, float decay, float w1, float beta2,
+               float omb2, float bc2_sqrt, float eps, float neg_step) {
+#pragma clang fp contract(off)
+  for_each_elem(slots, nslots, total, [&](const Slot& s, long long i) {
+    T* P = reinterpret_cast<T*>(s.param);
+    T* M = reinterpret_cast<T*>(s.exp_avg);
+    T* V = reinterpret_cast<T*>(s.exp_avg_sq);
+    const float g = (float)reinterpret_cast<const T*>(s.grad)[i];
+    const float p = rt<T>((float)P[i] * decay);                       // _foreach_mul_(params, 1 - lr wd)
+    const float m0 = (float)M[i];
+    const float m = rt<T>(w1 < 0.5f ? m0 + w1 * (g - m0) : g - (g - m0) * (1.f - w1));   // _foreach_lerp_
+    float v = rt<T>((float)V[i] * beta2);                               // _foreach_mul_(v, b2)
+    v = rt<T>(v + omb2 * g * g);                                        // _foreach_addcmul_(v, g, g, 1 - b2)
+    float d = rt<T>(sqrtf(v));                                          // _foreach_sqrt
+    d = rt<T>(d / bc2_sqrt);                                            // _foreach_div_
+    d = rt<T>(d + eps);                                                 // _foreach_add_
+    P[i] = (T)(p + neg_step * (m / d));                                 // _foreach_addcdiv_
+    M[i] = (T)m;
+    V[i] = (T)v;
+  });
+}
+
 constexpr int kMaxSlotGrid = 2048;
 inline unsigned slot_grid(long long total) {
   const long long g = (total + kChunk - 1) / kChunk;
@@ -225,38 +265,55 @@ inline unsigned slot_grid(long long total) {
 
 extern "C" size_t se_sisnr_save_bytes(int B) { return (size_t)(B > 0 ? B : 0) * kSave * sizeof(double); }
 
-extern "C" int se_sisnr_fwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
-                            int zero_mean, float eps, float* loss, void* save, void* stream) {
+#define SE_DT_SWITCH(dtype, BODY)                  \
+  switch (dtype) {                                 \
+    case SE_DTYPE_F32: { using TY = float; BODY; } break;    \
+    case SE_DTYPE_BF16: { using TY = __bf16; BODY; } break;  \
+    case SE_DTYPE_F16: { using TY = _Float16; BODY; } break; \
+    default: return SE_E_ARG;                      \
+  }
+
+extern "C" int se_sisnr_fwd(const void* est, int le, long long est_stride, const void* target, int lt, int B,
+                            int zero_mean, float eps, void* loss, void* save, int dtype, void* stream) {
   if (!est || !target || !loss || !save || B <= 0 || le <= 0 || lt <= 0 || est_stride < le) return SE_E_ARG;
   hipStream_t st = se::as_stream(stream);
-  hipLaunchKernelGGL(sisnr_items_kernel, dim3(B), dim3(kItemThreads), 0, st, est, le, est_stride, target, lt, zero_mean,
-                     (double*)save);
-  SE_LAUNCH_CHECK();
-  hipLaunchKernelGGL(sisnr_finalize_kernel, dim3(1), dim3(kThreads), 0, st, (const double*)save, B, eps, loss);
-  SE_LAUNCH_CHECK();
+  SE_DT_SWITCH(dtype, {
+    hipLaunchKernelGGL(sisnr_items_kernel<TY>, dim3(B), dim3(kItemThreads), 0, st, (const TY*)est, le, est_stride,
+                       (const TY*)target, lt, zero_mean, (double*)save);
+    SE_LAUNCH_CHECK();
+    hipLaunchKernelGGL(sisnr_finalize_kernel<TY>, dim3(1), dim3(kThreads), 0, st, (const double*)save, B, eps,
+                       (TY*)loss);
+    SE_LAUNCH_CHECK();
+  })
   return SE_OK;
 }
 
-extern "C" int se_sisnr_bwd(const float* est, int le, long long est_stride, const float* target, int lt, int B,
-                            int zero_mean, float eps, const void* save, const float* grad_loss, float* grad_est,
-                            long long grad_stride, void* stream) {
+extern "C" int se_sisnr_bwd(const void* est, int le, long long est_stride, const void* target, int lt, int B,
+                            int zero_mean, float eps, const void* save, const void* grad_loss, void* grad_est,
+                            long long grad_stride, int dtype, void* stream) {
   if (!est || !target || !save || !grad_loss || !grad_est || B <= 0 || le <= 0 || lt <= 0 || est_stride < le ||
       grad_stride < le)
     return SE_E_ARG;
-  hipLaunchKernelGGL(sisnr_bwd_kernel, dim3(se::ceil_div(le, 4 * kThreads), B), dim3(kThreads), 0,
-                     se::as_stream(stream), est, le, est_stride, target, lt, B, zero_mean, eps, (const double*)save,
-                     grad_loss, grad_est, grad_stride);
-  SE_LAUNCH_CHECK();
+  SE_DT_SWITCH(dtype, {
+    hipLaunchKernelGGL(sisnr_bwd_kernel<TY>, dim3(se::ceil_div(le, 4 * kThreads), B), dim3(kThreads), 0,
+                       se::as_stream(stream), (const TY*)est, le, est_stride, (const TY*)target, lt, B, zero_mean,
+                       eps, (const double*)save, (const TY*)grad_loss, (TY*)grad_est, grad_stride);
+    SE_LAUNCH_CHECK();
+  })
   return SE_OK;
 }
 
-extern "C" int se_grad_sumsq(const se_tensor_slot* slots, int nslots, long long total, double* sumsq, void* stream) {
+extern "C" int se_grad_sumsq(const se_tensor_slot* slots, int nslots, long long total, double* sumsq, int dtype,
+                             void* stream) {
   if (!slots || !sumsq || nslots <= 0 || total < 0) return SE_E_ARG;
   hipStream_t st = se::as_stream(stream);
   if (total == 0) return hipMemsetAsync(sumsq, 0, sizeof(double), st) == hipSuccess ? SE_OK : SE_E_LAUNCH;
   const unsigned grid = slot_grid(total);
   static_assert(kMaxSlotGrid + 1 == SE_SUMSQ_DOUBLES, "partials fit the caller's buffer");
-  hipLaunchKernelGGL(sumsq_kernel, dim3(grid), dim3(kThreads), 0, st, (const Slot*)slots, nslots, total, sumsq);
+  SE_DT_SWITCH(dtype, {
+    hipLaunchKernelGGL(sumsq_kernel<TY>, dim3(grid), dim3(kThreads), 0, st, (const Slot*)slots, nslots, total,
+                       sumsq);
+  })
   SE_LAUNCH_CHECK();
   hipLaunchKernelGGL(sumsq_final_kernel, dim3(1), dim3(kThreads), 0, st, sumsq, (int)grid);
   SE_LAUNCH_CHECK();
@@ -264,25 +321,43 @@ extern "C" int se_grad_sumsq(const se_tensor_slot* slots, int nslots, long long 
 }
 
 extern "C" int se_clip_grads(const se_tensor_slot* slots, int nslots, long long total, const double* sumsq,
-                             float max_norm, float* total_norm, void* stream) {
+                             float max_norm, float* total_norm, int dtype, void* stream) {
   if (!slots || !sumsq || nslots <= 0 || total < 0) return SE_E_ARG;
   if (total == 0) return SE_OK;
-  hipLaunchKernelGGL(clip_kernel, dim3(slot_grid(total)), dim3(kThreads), 0, se::as_stream(stream),
-                     (const Slot*)slots, nslots, total, sumsq, max_norm, total_norm);
+  SE_DT_SWITCH(dtype, {
+    hipLaunchKernelGGL(clip_kernel<TY>, dim3(slot_grid(total)), dim3(kThreads), 0, se::as_stream(stream),
+                       (const Slot*)slots, nslots, total, sumsq, max_norm, total_norm);
+  })
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
 
 extern "C" int se_adamw_step(const se_tensor_slot* slots, int nslots, long long total, double lr, double beta1,
-                             double beta2, double eps, double weight_decay, long long step, void* stream) {
+                             double beta2, double eps, double weight_decay, long long step, int dtype, void* stream) {
   if (!slots || nslots <= 0 || total < 0 || step < 1) return SE_E_ARG;
   if (total == 0) return SE_OK;
   // host scalars as torch computes them (Python floats, then the kernel's fp32)
   const double bc1 = 1.0 - std::pow(beta1, (double)step);
   const double bc2 = 1.0 - std::pow(beta2, (double)step);
-  hipLaunchKernelGGL(adamw_kernel, dim3(slot_grid(total)), dim3(kThreads), 0, se::as_stream(stream),
-                     (const Slot*)slots, nslots, total, (float)(1.0 - lr * weight_decay), (float)(1.0 - beta1),
-                     (float)beta2, (float)(1.0 - beta2), (float)std::sqrt(bc2), (float)eps, (float)(-(lr / bc1)));
+  const float a0 = (float)(1.0 - lr * weight_decay), a1 = (float)(1.0 - beta1), a2 = (float)beta2,
+              a3 = (float)(1.0 - beta2), a4 = (float)std::sqrt(bc2), a5 = (float)eps, a6 = (float)(-(lr / bc1));
+  hipStream_t st = se::as_stream(stream);
+  const dim3 grid(slot_grid(total));
+  switch (dtype) {
+    case SE_DTYPE_F32:
+      hipLaunchKernelGGL(adamw_kernel, grid, dim3(kThreads), 0, st, (const Slot*)slots, nslots, total, a0, a1, a2,
+                         a3, a4, a5, a6);
+      break;
+    case SE_DTYPE_BF16:
+      hipLaunchKernelGGL(adamw16_kernel<__bf16>, grid, dim3(kThreads), 0, st, (const Slot*)slots, nslots, total, a0,
+                         a1, a2, a3, a4, a5, a6);
+      break;
+    case SE_DTYPE_F16:
+      hipLaunchKernelGGL(adamw16_kernel<_Float16>, grid, dim3(kThreads), 0, st, (const Slot*)slots, nslots, total,
+                         a0, a1, a2, a3, a4, a5, a6);
+      break;
+    default: return SE_E_ARG;
+  }
   SE_LAUNCH_CHECK();
   return SE_OK;
 }
@@ -342,20 +417,19 @@ mask_bwd_kernel(const float* __restrict__ gest, const float* __restrict__ h, con
 // reference's operation order without contraction; the transcendental functions are this
 // toolchain's (torch's build may differ in the last ulp, which the phase terms can amplify).
 // m / n rows: batch stride, row stride (elements), time contiguous. grid (ceil(F T / 256), B)
-template <typename T>
-__device__ __forceinline__ float rt(float v) { return (float)(T)v; }
 template <typename T, int MODE>
 __global__ void __launch_bounds__(kThreads)
 polar_mask_fwd_kernel(const T* __restrict__ mr, const T* __restrict__ mi, long long msb, long long msr,
                       const T* __restrict__ nr, const T* __restrict__ ni, long long nsb, long long nsr, int F, int Tn,
-                      T* __restrict__ out) {
+                      int row0, T* __restrict__ out) {
 #pragma clang fp contract(off)   // one rounding per reference op: no fused multiply-adds
   const int b = blockIdx.y;
   const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
   if (i >= (long long)F * Tn) return;
   const int f = (int)(i / Tn), t = (int)(i - (long long)f * Tn);
-  const long long mo = b * msb + f * msr + t, no = b * nsb + f * nsr + t;
-  const float a = (float)mr[mo], c = (float)mi[mo], x = (float)nr[no], y = (float)ni[no];
+  const long long mo = b * msb + (long long)(f - row0) * msr + t, no = b * nsb + f * nsr + t;
+  const bool mz = f < row0;   // a leading zero row of the mask (not stored)
+  const float a = mz ? 0.f : (float)mr[mo], c = mz ? 0.f : (float)mi[mo], x = (float)nr[no], y = (float)ni[no];
   auto mag = [](float re, float im) __attribute__((always_inline)) {
     return rt<T>(sqrtf(rt<T>(rt<T>(rt<T>(re * re) + rt<T>(im * im)) + 1e-8f)));
   };
@@ -377,8 +451,10 @@ polar_mask_fwd_kernel(const T* __restrict__ mr, const T* __restrict__ mi, long l
 
 extern "C" int se_polar_mask_fwd(const void* mr, const void* mi, long long m_batch_stride, long long m_row_stride,
                                  const void* nr, const void* ni, long long n_batch_stride, long long n_row_stride,
-                                 int B, int F, int T, int mode, int dtype, void* out, void* stream) {
-  if (!mr || !mi || !nr || !ni || !out || B <= 0 || F <= 0 || T <= 0 || (mode != 0 && mode != 1)) return SE_E_ARG;
+                                 int B, int F, int T, int mode, int dtype, int m_row0, void* out, void* stream) {
+  if (!mr || !mi || !nr || !ni || !out || B <= 0 || F <= 0 || T <= 0 || (mode != 0 && mode != 1) || m_row0 < 0 ||
+      m_row0 >= F)
+    return SE_E_ARG;
   const dim3 grid((unsigned)se::ceil_div((long long)F * T, kThreads), B);
   hipStream_t st = se::as_stream(stream);
 #define SE_PM(TY)                                                                                                  \
@@ -386,11 +462,11 @@ extern "C" int se_polar_mask_fwd(const void* mr, const void* mi, long long m_bat
     if (mode == 0)                                                                                                 \
       hipLaunchKernelGGL((polar_mask_fwd_kernel<TY, 0>), grid, dim3(kThreads), 0, st, (const TY*)mr, (const TY*)mi, \
                          m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, n_row_stride, F, \
-                         T, (TY*)out);                                                                            \
+                         T, m_row0, (TY*)out);                                                                          \
     else                                                                                                           \
       hipLaunchKernelGGL((polar_mask_fwd_kernel<TY, 1>), grid, dim3(kThreads), 0, st, (const TY*)mr, (const TY*)mi, \
                          m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, n_row_stride, F, \
-                         T, (TY*)out);                                                                            \
+                         T, m_row0, (TY*)out);                                                                          \
   } while (0)
   switch (dtype) {
     case SE_DTYPE_F32: SE_PM(float); break;
@@ -415,13 +491,19 @@ template <typename T, int MODE>
 __global__ void __launch_bounds__(kThreads)
 polar_mask_bwd_kernel(const T* __restrict__ g, const T* __restrict__ mr, const T* __restrict__ mi, long long msb,
                       long long msr, const T* __restrict__ nr, const T* __restrict__ ni, long long nsb, long long nsr,
-                      int F, int Tn, T* __restrict__ dm) {
+                      int F, int Tn, int row0, int dmT, T* __restrict__ dm) {
 #pragma clang fp contract(off)
   const int b = blockIdx.y;
-  const long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
-  if (i >= (long long)F * Tn) return;
-  const int f = (int)(i / Tn), t = (int)(i - (long long)f * Tn);
-  const long long mo = b * msb + f * msr + t, no = b * nsb + f * nsr + t;
+  const long long Fd = F - row0, i = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (i >= Fd * dmT) return;
+  const int fd = (int)(i / dmT), t = (int)(i - (long long)fd * dmT), f = fd + row0;
+  const long long od = (long long)b * 2 * Fd * dmT + i;
+  if (t >= Tn) {   // a trimmed frame of the stored mask: no gradient
+    dm[od] = (T)0.f;
+    dm[od + Fd * dmT] = (T)0.f;
+    return;
+  }
+  const long long mo = b * msb + (long long)fd * msr + t, no = b * nsb + f * nsr + t;
   const float a = (float)mr[mo], c = (float)mi[mo], x = (float)nr[no], y = (float)ni[no];
   auto mag = [](float re, float im) __attribute__((always_inline)) {
     return rt<T>(sqrtf(rt<T>(rt<T>(rt<T>(re * re) + rt<T>(im * im)) + 1e-8f)));
@@ -440,9 +522,10 @@ polar_mask_bwd_kernel(const T* __restrict__ g, const T* __restrict__ mr, const T
     m_ph = rt<T>(atan2f(v, u));
     ph = rt<T>(n_ph + m_ph);
   }
-  const long long oo = (long long)b * 2 * F * Tn + i, FT = (long long)F * Tn;
+  const long long FT = (long long)F * Tn, oo = (long long)b * 2 * FT + (long long)f * Tn + t;
   const float gre = (float)g[oo], gim = (float)g[oo + FT];
-  const float cp = cosf(ph), sp = sinf(ph);
+  // the forward's T-rounded cos / sin factors (torch's mul backward reads the stored factor)
+  const float cp = rt<T>(cosf(ph)), sp = rt<T>(sinf(ph));
   const float d_gain = gre * cp + gim * sp;
   const float d_ph = gain * (gim * cp - gre * sp);
   float d_mag = d_gain * n_mag * (1.f - th * th);
@@ -462,27 +545,29 @@ polar_mask_bwd_kernel(const T* __restrict__ g, const T* __restrict__ mr, const T
   }
   da += d_mag * (a / m_mag);
   dc += d_mag * (c / m_mag);
-  dm[oo] = (T)da;
-  dm[oo + FT] = (T)dc;
+  dm[od] = (T)da;
+  dm[od + Fd * dmT] = (T)dc;
 }
 
 extern "C" int se_polar_mask_bwd(const void* g, const void* mr, const void* mi, long long m_batch_stride,
                                  long long m_row_stride, const void* nr, const void* ni, long long n_batch_stride,
-                                 long long n_row_stride, int B, int F, int T, int mode, int dtype, void* dm,
-                                 void* stream) {
-  if (!g || !mr || !mi || !nr || !ni || !dm || B <= 0 || F <= 0 || T <= 0 || (mode != 0 && mode != 1)) return SE_E_ARG;
-  const dim3 grid((unsigned)se::ceil_div((long long)F * T, kThreads), B);
+                                 long long n_row_stride, int B, int F, int T, int mode, int dtype, int m_row0,
+                                 int dm_T, void* dm, void* stream) {
+  if (!g || !mr || !mi || !nr || !ni || !dm || B <= 0 || F <= 0 || T <= 0 || (mode != 0 && mode != 1) ||
+      m_row0 < 0 || m_row0 >= F || dm_T < T)
+    return SE_E_ARG;
+  const dim3 grid((unsigned)se::ceil_div((long long)(F - m_row0) * dm_T, kThreads), B);
   hipStream_t st = se::as_stream(stream);
 #define SE_PMB(TY)                                                                                                 \
   do {                                                                                                             \
     if (mode == 0)                                                                                                 \
       hipLaunchKernelGGL((polar_mask_bwd_kernel<TY, 0>), grid, dim3(kThreads), 0, st, (const TY*)g, (const TY*)mr,  \
                          (const TY*)mi, m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, \
-                         n_row_stride, F, T, (TY*)dm);                                                            \
+                         n_row_stride, F, T, m_row0, dm_T, (TY*)dm);                                                          \
     else                                                                                                           \
       hipLaunchKernelGGL((polar_mask_bwd_kernel<TY, 1>), grid, dim3(kThreads), 0, st, (const TY*)g, (const TY*)mr,  \
                          (const TY*)mi, m_batch_stride, m_row_stride, (const TY*)nr, (const TY*)ni, n_batch_stride, \
-                         n_row_stride, F, T, (TY*)dm);                                                            \
+                         n_row_stride, F, T, m_row0, dm_T, (TY*)dm);                                                          \
   } while (0)
   switch (dtype) {
     case SE_DTYPE_F32: SE_PMB(float); break;

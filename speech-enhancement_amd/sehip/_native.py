@@ -51,16 +51,16 @@ class FirstConvDesc(ctypes.Structure):
 
 
 class GemmDesc(ctypes.Structure):
-    """Mirror of se_gemm_desc (include/sehip.h, ABI 6)."""
+    """Mirror of se_gemm_desc (include/sehip.h, ABI 6; dtype / bias_rows ABI 10)."""
 
     _fields_ = [(n, c_int) for n in ("M", "N", "K", "batches", "sum_batches", "a_mcontig", "b_ncontig",
                                      "lda", "ldb", "ldc")] + [
         (n, ctypes.c_longlong) for n in ("stride_a", "stride_b", "stride_c", "stride_bias")] + [
-        (n, c_int) for n in ("kmask_period", "kmask_phase", "splits")]
+        (n, c_int) for n in ("kmask_period", "kmask_phase", "splits", "dtype", "bias_rows")]
 
 
 _P = c_void_p
-ABI_VERSION = 9   # SEHIP_ABI_VERSION (include/sehip.h)
+ABI_VERSION = 10   # SEHIP_ABI_VERSION (include/sehip.h)
 CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
@@ -120,16 +120,17 @@ _SIGNATURES = {
     "se_mask_fwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P]),
     "se_polar_mask_fwd": (c_int, [_P, _P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, ctypes.c_longlong,
                                   ctypes.c_longlong, c_int, c_int,
-                                  c_int, c_int, c_int, _P, _P]),
+                                  c_int, c_int, c_int, c_int, _P, _P]),
     "se_mask_bwd": (c_int, [_P, _P, _P, c_int, c_int, c_int, _P, _P]),
     "se_polar_mask_bwd": (c_int, [_P, _P, _P, ctypes.c_longlong, ctypes.c_longlong, _P, _P, ctypes.c_longlong,
-                                  ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, _P, _P]),
-    "se_sisnr_fwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P]),
+                                  ctypes.c_longlong, c_int, c_int, c_int, c_int, c_int, c_int, c_int, _P, _P]),
+    "se_sisnr_fwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, c_int, _P]),
     "se_sisnr_bwd": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, c_int, c_int, c_float, _P, _P, _P,
-                             ctypes.c_longlong, _P]),
-    "se_grad_sumsq": (c_int, [_P, c_int, ctypes.c_longlong, _P, _P]),
-    "se_clip_grads": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_float, _P, _P]),
-    "se_adamw_step": (c_int, [_P, c_int, ctypes.c_longlong] + [ctypes.c_double] * 5 + [ctypes.c_longlong, _P]),
+                             ctypes.c_longlong, c_int, _P]),
+    "se_grad_sumsq": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_int, _P]),
+    "se_clip_grads": (c_int, [_P, c_int, ctypes.c_longlong, _P, c_float, _P, c_int, _P]),
+    "se_adamw_step": (c_int, [_P, c_int, ctypes.c_longlong] + [ctypes.c_double] * 5 + [ctypes.c_longlong, c_int,
+                                                                                          _P]),
     "se_lstm_wide_supported": (c_int, [c_int]),
     "se_lstm_wide_sync_ints": (c_int, []),
     "se_lstm_wide_fwd": (c_int, [_P, ctypes.c_longlong, c_int, _P, _P, _P, _P] + [c_int] * 4
@@ -145,6 +146,27 @@ _SIGNATURES = {
     "se_ccbam_bwd_dx": (c_int, [_P] * 8 + [c_int] * 3 + [_P]),
     "se_ccbam_mlp_fwd": (c_int, [_P] * 6 + [c_int] * 3 + [_P] * 3),
     "se_ccbam_mlp_bwd": (c_int, [_P] * 9 + [c_int] * 3 + [_P] * 7),
+    # ABI 10: Linear bias gradient, strided copy / cast, ComplexLSTM combine, CARN glue, chunking
+    "se_bias_grad_workspace_size": (c_size_t, [c_int, ctypes.c_longlong, c_int]),
+    "se_bias_grad": (c_int, [_P, c_int, ctypes.c_longlong, c_int] + [ctypes.c_longlong] * 3 + [c_int, _P, _P,
+                                                                                              c_size_t, _P]),
+    "se_copy_strided": (c_int, [_P, c_int, _P, c_int, c_int, _P, _P, _P, _P]),
+    "se_complex_lstm_combine_fwd": (c_int, [_P, ctypes.c_longlong, c_int, c_int, c_int, _P] + [ctypes.c_longlong] * 3
+                                    + [c_int, _P]),
+    "se_complex_lstm_combine_bwd": (c_int, [_P] + [ctypes.c_longlong] * 3 + [c_int, c_int, c_int, c_int, _P,
+                                                                            ctypes.c_longlong, _P]),
+    "se_carn_mask_fwd": (c_int, [_P, ctypes.c_longlong, _P, c_int, c_int, c_int, c_int, _P, _P]),
+    "se_carn_mask_bwd": (c_int, [_P, _P, ctypes.c_longlong, _P, c_int, c_int, c_int, c_int, _P, _P, _P]),
+    "se_add_sigmoid_fwd": (c_int, [_P, _P, _P, ctypes.c_longlong, c_int, _P]),
+    "se_sigmoid_bwd": (c_int, [_P, _P, _P, ctypes.c_longlong, c_int, _P]),
+    "se_gate_cat_fwd": (c_int, [_P, _P, _P, c_int, c_int, ctypes.c_longlong, c_int, _P]),
+    "se_gate_cat_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int, ctypes.c_longlong, c_int, _P]),
+    "se_glu_fwd": (c_int, [_P, _P, _P, ctypes.c_longlong, c_int, _P]),
+    "se_glu_bwd": (c_int, [_P, _P, _P, _P, _P, ctypes.c_longlong, c_int, _P]),
+    "se_clamp_fwd": (c_int, [_P, _P, ctypes.c_longlong, c_float, c_float, c_int, _P]),
+    "se_clamp_bwd": (c_int, [_P, _P, _P, ctypes.c_longlong, c_float, c_float, c_int, _P]),
+    "se_chunk_split": (c_int, [_P, ctypes.c_longlong, c_int, c_int, c_int, c_int, _P, _P]),
+    "se_chunk_overlap_add": (c_int, [_P, c_int, c_int, c_int, c_int, ctypes.c_longlong, c_int, _P, _P]),
     "se_complex_join": (c_int, [_P, c_int, c_int, c_int, _P, c_int, c_int, c_int, _P, c_int, c_int, _P]),
     "se_complex_join_bwd": (c_int, [_P, _P, c_int, c_int, c_int, _P, c_int, c_int, c_int, c_int, c_int, _P]),
 }

@@ -13,6 +13,7 @@ import torch
 import torch.nn as nn
 
 from . import functional as F
+from . import glue
 
 
 # ----------------------------------------------------------- layout helpers
@@ -163,7 +164,14 @@ def real_conv2d(conv: nn.Module, x, input_pad=None):
 
 # ------------------------------------------------------------- linear / LSTM
 class ComplexLinear(nn.Module):
-    """complex_nn.py:93-113 (separate real / imag linears, no cross terms)."""
+    """complex_nn.py:93-113 (separate real / imag linears, no cross terms) on the
+    hand-written GEMM (sehip.linear: se_gemm fwd, input-, weight- and bias-grad).
+    The real_linear / imag_linear nn.Linear modules are the parameter holders.
+    feature_major_out: produce the output as the transposed view of a [B, out, T]
+    storage (the same values and shape), for a consumer that transposes it back
+    (DCCRN's LSTMBlock -> decoder hand-off, dccrn.py:169-171)."""
+
+    feature_major_out = False
 
     def __init__(self, in_channels, out_channels, **kwargs):
         super().__init__()
@@ -173,8 +181,13 @@ class ComplexLinear(nn.Module):
         self.imag_linear = nn.Linear(cin, cout, **kwargs)
 
     def forward(self, x):
+        from .linear import linear, linear_halves
+        rl, il = self.real_linear, self.imag_linear
+        if isinstance(x, torch.Tensor) and not torch.is_complex(x):
+            # both halves of the last axis in place (complex_nn.py:106-113 without chunk / cat)
+            return linear_halves(x, [rl.weight, il.weight], [rl.bias, il.bias], self.feature_major_out)
         re, im = split_complex(x, dim=-1)
-        return merge_real_imag(x, self.real_linear(re), self.imag_linear(im), dim=-1)
+        return merge_real_imag(x, linear(re, rl), linear(im, il), dim=-1)
 
 
 # hidden sizes of the HIP recurrence: se_lstm_* (64, 128), se_lstm_wide_* (256, 512, 1024)
@@ -200,34 +213,39 @@ def _hip_lstm_ok(m: nn.LSTM) -> bool:
             and (m.dropout == 0 or not m.training) and m.mode == "LSTM" and _wide_group_fits(m))
 
 
-def stacked_lstms(x, lstms, batch_first=True, with_state=False):
+def stacked_lstms(x, lstms, batch_first=True, with_state=False, raw=False):
     """Run several nn.LSTMs (same shape) over the same input x on the HIP
     recurrence, all of them in the same launches: per layer one projection
     GEMM, one se_lstm_fwd over every (LSTM, direction), and in backward one
     se_lstm_bwd. Returns one output per LSTM, shaped like nn.LSTM's output[0]
     (with_state: and per LSTM nn.LSTM's (h_n, c_n), [layers * dirs, B, H]).
-    The modules keep their own parameters (state_dict keys unchanged)."""
+    raw=True (unidirectional): the fp32 [len(lstms), B, T, H] output of the last layer
+    as it is, for a consumer that reads it directly (ComplexLSTM's combine).
+    The modules keep their own parameters (state_dict keys unchanged); their bf16 /
+    fp16 weights are stacked in fp32 by one HIP copy per tensor (glue.stack), the
+    recurrence runs in fp32 and the outputs come back in x's dtype (glue.contiguous)."""
     m0 = lstms[0]
     nd = 2 if m0.bidirectional else 1
     H = m0.hidden_size
     dt = x.dtype                                  # bf16 / fp16 models: fp32 recurrence, caller's dtype out
     xb = x if batch_first else x.transpose(0, 1)
-    inp = _f32(xb).contiguous()                   # layer 0: [B, T, I] shared by every LSTM
+    inp = glue.contiguous(xb, torch.float32)      # layer 0: [B, T, I] shared by every LSTM
     rev_mask = sum(1 << (i * nd + 1) for i in range(len(lstms))) if nd == 2 else 0
     out = None
-    h_last, c_last = [], []
+    h_layers, c_layers = [], []
+    f32 = torch.float32
     for k in range(m0.num_layers):
         sfx = [f"_l{k}", f"_l{k}_reverse"][:nd]
-        w_ih = torch.stack([_f32(getattr(m, "weight_ih" + s)) for m in lstms for s in sfx])
-        w_hh = torch.stack([_f32(getattr(m, "weight_hh" + s)) for m in lstms for s in sfx])
+        w_ih = glue.stack([getattr(m, "weight_ih" + s) for m in lstms for s in sfx], f32)
+        w_hh = glue.stack([getattr(m, "weight_hh" + s) for m in lstms for s in sfx], f32)
         b_ih = b_hh = None
         if m0.bias:
-            b_ih = torch.stack([_f32(getattr(m, "bias_ih" + s)) for m in lstms for s in sfx])
-            b_hh = torch.stack([_f32(getattr(m, "bias_hh" + s)) for m in lstms for s in sfx])
+            b_ih = glue.stack([getattr(m, "bias_ih" + s) for m in lstms for s in sfx], f32)
+            b_hh = glue.stack([getattr(m, "bias_hh" + s) for m in lstms for s in sfx], f32)
         h, c = F.lstm_layer(inp, w_ih, w_hh, b_ih, b_hh, rev_mask, with_cell=True)   # [len*nd, B, T, H]
-        if with_state:   # last step in processing order: t = T-1 forward, t = 0 reverse
-            h_last.append(torch.stack([h[i, :, 0 if i % nd else -1] for i in range(h.shape[0])]))
-            c_last.append(torch.stack([c[i, :, 0 if i % nd else -1] for i in range(c.shape[0])]))
+        if with_state:
+            h_layers.append(h)
+            c_layers.append(c)
         Bn, T = h.shape[1], h.shape[2]
         if nd == 2:   # per LSTM: cat(forward, reverse) on features, fed to both directions
             out = h.view(len(lstms), 2, Bn, T, H).permute(0, 2, 3, 1, 4).reshape(len(lstms), Bn, T, 2 * H)
@@ -237,15 +255,19 @@ def stacked_lstms(x, lstms, batch_first=True, with_state=False):
             if m0.dropout > 0 and m0.training:
                 out = torch.nn.functional.dropout(out, m0.dropout, True)
             inp = out.repeat_interleave(nd, dim=0) if nd == 2 else out
-    outs = [o.to(dt) for o in out.unbind(0)]
+    if raw and nd == 1 and not with_state:
+        return out
+    outs = [glue.contiguous(o, dt) for o in out.unbind(0)]
     outs = outs if batch_first else [o.transpose(0, 1) for o in outs]
     if not with_state:
         return outs
-    # per LSTM: [layers * dirs, B, H] in nn.LSTM's (layer, direction) order
-    hs = torch.stack(h_last).view(m0.num_layers, len(lstms), nd, -1, H)
-    cs = torch.stack(c_last).view(m0.num_layers, len(lstms), nd, -1, H)
-    states = [(hs[:, i].reshape(m0.num_layers * nd, -1, H), cs[:, i].reshape(m0.num_layers * nd, -1, H))
-              for i in range(len(lstms))]
+    # per LSTM: [layers * dirs, B, H] in nn.LSTM's (layer, direction) order; the last step in
+    # processing order: t = T-1 forward, t = 0 reverse
+    states = []
+    for i in range(len(lstms)):
+        hn = [hl[i * nd + d, :, -1 if d == 0 else 0] for hl in h_layers for d in range(nd)]
+        cn = [cl[i * nd + d, :, -1 if d == 0 else 0] for cl in c_layers for d in range(nd)]
+        states.append((glue.stack(hn, dt), glue.stack(cn, dt)))
     return outs, states
 
 
@@ -260,10 +282,8 @@ class LSTM(nn.LSTM):
     def forward(self, input, hx=None):
         if (hx is None and _hip_lstm_ok(self) and isinstance(input, torch.Tensor) and input.is_cuda
                 and input.dim() == 3):
-            dt = input.dtype
-            outs, states = stacked_lstms(_f32(input), [self], batch_first=self.batch_first, with_state=True)
-            h_n, c_n = states[0]
-            return outs[0].to(dt), (h_n.to(dt), c_n.to(dt))
+            outs, states = stacked_lstms(input, [self], batch_first=self.batch_first, with_state=True)
+            return outs[0], states[0]
         return super().forward(input, hx)
 
 
@@ -276,6 +296,10 @@ class ComplexLSTM(nn.Module):
     Configurations the HIP recurrence does not cover (hidden size other than
     64 / 128, proj_size) run each nn.LSTM once over the stacked batch."""
 
+    # batch_first: return the output as the transposed view of a [B, 2H, T] storage (same
+    # values and shape) for a caller that transposes it back (FRCRN, frcrn.py:137)
+    feature_major_out = False
+
     def __init__(self, in_channels, hidden_channels, **kwargs):
         super().__init__()
         cin = _check_even(in_channels, "in_channels")
@@ -285,6 +309,14 @@ class ComplexLSTM(nn.Module):
         self._bdim = 0 if kwargs.get("batch_first", False) else 1
 
     def forward(self, x):
+        if (isinstance(x, torch.Tensor) and not torch.is_complex(x) and x.is_cuda and x.dim() == 3
+                and _hip_lstm_ok(self.real_lstm) and not self.real_lstm.bidirectional):
+            # re / im stacked on the batch axis in fp32 (one HIP copy), both LSTMs in the same
+            # launches, the four outputs combined into (re, im) in x's dtype (one HIP pass)
+            xb = x if self._bdim == 0 else x.transpose(0, 1)
+            h = stacked_lstms(glue.stack_re_im(xb), [self.real_lstm, self.imag_lstm], batch_first=True, raw=True)
+            out = glue.complex_lstm_combine(h, x.dtype, self.feature_major_out and self._bdim == 0)
+            return out if self._bdim == 0 else out.transpose(0, 1)
         re, im = split_complex(x, dim=-1)
         both = torch.cat([re, im], dim=self._bdim)
         if _hip_lstm_ok(self.real_lstm):

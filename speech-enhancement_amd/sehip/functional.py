@@ -1055,12 +1055,14 @@ def _polar_planes_ok(ts):
             and mr.stride() == mi.stride() and nr.stride() == ni.stride())
 
 
-def _polar_fwd(mr, mi, nr, ni, mode):
-    B, Fq, T = mr.shape
-    out = torch.empty((B, 2, Fq, T), device=mr.device, dtype=mr.dtype)
+def _polar_fwd(mr, mi, nr, ni, mode, row0=0):
+    """row0: the mask's leading zero rows, not stored (mr / mi hold rows row0 .. F-1)."""
+    B, Fq, T = nr.shape
+    out = torch.empty((B, 2, Fq, T), device=nr.device, dtype=nr.dtype)
     N.check(N.lib().se_polar_mask_fwd(mr.data_ptr(), mi.data_ptr(), mr.stride(0), mr.stride(1), nr.data_ptr(),
                                       ni.data_ptr(), nr.stride(0), nr.stride(1), B, Fq, T, int(mode),
-                                      N.dtype_code(mr), out.data_ptr(), N.stream_of(mr)), "se_polar_mask_fwd")
+                                      N.dtype_code(nr), int(row0), out.data_ptr(), N.stream_of(nr)),
+            "se_polar_mask_fwd")
     POLAR_MASK_CALLS[0] += 1
     return out
 
@@ -1083,9 +1085,51 @@ class _PolarMask(torch.autograd.Function):
         dm = torch.empty((B, 2, Fq, T), device=g.device, dtype=g.dtype)
         N.check(N.lib().se_polar_mask_bwd(g.data_ptr(), mr.data_ptr(), mi.data_ptr(), mr.stride(0), mr.stride(1),
                                           nr.data_ptr(), ni.data_ptr(), nr.stride(0), nr.stride(1), B, Fq, T,
-                                          int(ctx.mode), N.dtype_code(mr), dm.data_ptr(), N.stream_of(g)),
+                                          int(ctx.mode), N.dtype_code(mr), 0, T, dm.data_ptr(), N.stream_of(g)),
                 "se_polar_mask_bwd")
         return dm[:, 0], dm[:, 1], None, None, None
+
+
+class _PolarMaskStored(torch.autograd.Function):
+    """The mask taken from a stored decoder output m [B, 2, F - row0, Tm] (Tm >= T): mask row f
+    is 0 for f < row0 (the reference's F.pad(m, (0, 0, row0, 0)), not materialised) and
+    m[:, :, f - row0, :T] after (the trailing frames trimmed, dccrn.py:172-182). The backward
+    writes m's gradient in m's own layout (0 on the trimmed frames) in the same pass."""
+
+    @staticmethod
+    def forward(ctx, m, nr, ni, mode, row0):
+        ctx.save_for_backward(m, nr, ni)
+        ctx.mode, ctx.row0 = mode, row0
+        return _polar_fwd(m[:, 0], m[:, 1], nr, ni, mode, row0)
+
+    @staticmethod
+    def backward(ctx, g):
+        m, nr, ni = ctx.saved_tensors
+        g = g.contiguous()
+        B, Fq, T = nr.shape
+        dm = torch.empty_like(m)
+        mr, mi = m[:, 0], m[:, 1]
+        N.check(N.lib().se_polar_mask_bwd(g.data_ptr(), mr.data_ptr(), mi.data_ptr(), mr.stride(0), mr.stride(1),
+                                          nr.data_ptr(), ni.data_ptr(), nr.stride(0), nr.stride(1), B, Fq, T,
+                                          int(ctx.mode), N.dtype_code(m), int(ctx.row0), m.shape[3], dm.data_ptr(),
+                                          N.stream_of(g)), "se_polar_mask_bwd")
+        return dm, None, None, None, None
+
+
+def polar_mask_stored(m, nr, ni, mode, row0=0):
+    """polar_mask of the mask planes pad(m, top row0)[:, 0 / 1, :, :T] without the pad or the trim
+    (_PolarMaskStored); None where the layout does not fit (m must be contiguous, of nr's dtype,
+    with F - row0 rows and at least T frames) or the noisy planes need a gradient."""
+    if not (m.is_cuda and m.dim() == 4 and m.shape[1] == 2 and m.is_contiguous() and m.dtype == nr.dtype
+            and nr.dim() == 3 and m.shape[0] == nr.shape[0] and m.shape[2] + row0 == nr.shape[1]
+            and m.shape[3] >= nr.shape[2] and nr.shape == ni.shape and nr.stride() == ni.stride()
+            and nr.stride(2) == 1 and m.dtype in N.DTYPES):
+        return None
+    if torch.is_grad_enabled() and (nr.requires_grad or ni.requires_grad):
+        return None
+    if torch.is_grad_enabled() and m.requires_grad:
+        return _PolarMaskStored.apply(m, nr, ni, int(mode), int(row0))
+    return _polar_fwd(m[:, 0], m[:, 1], nr, ni, mode, row0)
 
 
 def polar_mask(mr, mi, nr, ni, mode):
@@ -1235,22 +1279,26 @@ def lstm_gemm_hip() -> bool:
     return os.environ.get("SEHIP_LSTM_GEMM", "hip") != "torch"
 
 
-def gemm(A, B, C, *, M, N, K, lda, ldb, ldc, amax_a, amax_b, a_mcontig=False, b_ncontig=False, batches=1,
-         sum_batches=False, stride_a=0, stride_b=0, stride_c=0, bias0=None, bias1=None, stride_bias=0,
-         kmask=(0, 0)):
+def gemm(A, B, C, *, M, N, K, lda, ldb, ldc, amax_a=None, amax_b=None, a_mcontig=False, b_ncontig=False,
+         batches=1, sum_batches=False, stride_a=0, stride_b=0, stride_c=0, bias0=None, bias1=None, stride_bias=0,
+         kmask=(0, 0), bias_rows=False, offsets=(0, 0, 0)):
     """C[b](m, n) = sum_k A(b, m, k) B(b, k, n) (+ bias0 + bias1) on se_gemm
-    (include/sehip.h): A, B, C are fp32 device tensors addressed from their
-    data_ptr with the given leading dimensions and batch strides."""
+    (include/sehip.h): A, B, C are device tensors of one storage type addressed from
+    their data_ptr (+ offsets, in elements) with the given leading dimensions and batch
+    strides. fp32: split-fp16 arithmetic scaled by amax_a / amax_b (bounds of max |A|,
+    max |B|); bf16 / fp16: the one-term MFMA of that format (no bounds needed)."""
     nat = _NAT   # (N is the column count here)
+    dt = nat.dtype_code(C)
     d = nat.GemmDesc(M=M, N=N, K=K, batches=batches, sum_batches=int(sum_batches), a_mcontig=int(a_mcontig),
-                   b_ncontig=int(b_ncontig), lda=lda, ldb=ldb, ldc=ldc, stride_a=stride_a, stride_b=stride_b,
-                   stride_c=stride_c, stride_bias=stride_bias, kmask_period=kmask[0], kmask_phase=kmask[1],
-                   splits=0)
+                     b_ncontig=int(b_ncontig), lda=lda, ldb=ldb, ldc=ldc, stride_a=stride_a, stride_b=stride_b,
+                     stride_c=stride_c, stride_bias=stride_bias, kmask_period=kmask[0], kmask_phase=kmask[1],
+                     splits=0, dtype=dt, bias_rows=int(bias_rows))
     lib = nat.lib()
+    es = C.element_size()
     ws = _workspace(lib.se_gemm_workspace_size(nat.ctypes.byref(d)), C.device)
-    nat.check(lib.se_gemm(nat.ctypes.byref(d), A.data_ptr(), B.data_ptr(), C.data_ptr(), nat.ptr(bias0), nat.ptr(bias1),
-                        amax_a.data_ptr(), amax_b.data_ptr(), ws.data_ptr(), ws.numel(), nat.stream_of(C)),
-            "se_gemm")
+    nat.check(lib.se_gemm(nat.ctypes.byref(d), A.data_ptr() + es * offsets[0], B.data_ptr() + es * offsets[1],
+                          C.data_ptr() + es * offsets[2], nat.ptr(bias0), nat.ptr(bias1), nat.ptr(amax_a),
+                          nat.ptr(amax_b), ws.data_ptr(), ws.numel(), nat.stream_of(C)), "se_gemm")
     return C
 
 

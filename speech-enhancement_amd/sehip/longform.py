@@ -8,7 +8,9 @@ chunks run as ONE batch (one launch per op for the whole utterance), and the
 enhanced chunks are overlap-added with a linear cross-fade over each overlap
 (sum of the two fade weights = 1), then trimmed to the input length. The last
 chunk is zero-padded. The same procedure, on the oracle model, is
-oracle/longform.py.
+oracle/longform.py. On the GPU the split and the cross-fade overlap-add are one HIP
+pass each (glue.chunk_split / glue.chunk_overlap_add, csrc/glue.hip); the torch
+forms below are the same arithmetic for host tensors.
 """
 from __future__ import annotations
 
@@ -28,6 +30,9 @@ def split_chunks(wav: torch.Tensor, chunk: int, overlap: int) -> torch.Tensor:
     """[L] or [1, L] -> [n, chunk] (zero-padded at the end)."""
     x = wav.reshape(-1)
     starts = chunk_plan(x.shape[0], chunk, overlap)
+    if x.is_cuda:
+        from . import glue
+        return glue.chunk_split(x, chunk, starts)
     total = starts[-1] + chunk
     xp = torch.nn.functional.pad(x, (0, total - x.shape[0]))
     return xp.unfold(0, chunk, chunk - overlap)[: len(starts)].contiguous()
@@ -37,6 +42,9 @@ def overlap_add(chunks: torch.Tensor, length: int, overlap: int) -> torch.Tensor
     """[n, chunk] -> [length]: linear cross-fade over each overlap."""
     n, chunk = chunks.shape
     hop = chunk - overlap
+    if chunks.is_cuda:
+        from . import glue
+        return glue.chunk_overlap_add(chunks, chunk, overlap, length)
     w = torch.ones(chunk, device=chunks.device, dtype=chunks.dtype)
     if overlap:
         ramp = (torch.arange(overlap, device=chunks.device, dtype=torch.float32) + 0.5) / overlap
@@ -63,8 +71,12 @@ def enhance_chunked(model, wav: torch.Tensor, chunk: int, overlap: int = 0, max_
     step = max_batch or chunks.shape[0]
     for i in range(0, chunks.shape[0], step):
         _, y = model(chunks[i:i + step])
-        y = y.reshape(y.shape[0], -1)
-        if y.shape[1] < chunk:                     # models whose iSTFT shortens (DCCRN)
-            y = torch.nn.functional.pad(y, (0, chunk - y.shape[1]))
-        outs.append(y[:, :chunk])
+        outs.append(y.reshape(y.shape[0], -1))
+    if wav.is_cuda and len(outs) == 1:
+        # the rows read up to their own width (a shorter iSTFT output counts as zero-padded:
+        # DCCRN) in the overlap-add pass itself
+        from . import glue
+        return glue.chunk_overlap_add(outs[0], chunk, overlap, length)[None]
+    outs = [torch.nn.functional.pad(y, (0, chunk - y.shape[1])) if y.shape[1] < chunk else y[:, :chunk]
+            for y in outs]                           # models whose iSTFT shortens (DCCRN)
     return overlap_add(torch.cat(outs), length, overlap)[None]

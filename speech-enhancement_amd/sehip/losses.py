@@ -1,10 +1,11 @@
 """Training losses (drop-in for /root/reference/losses.py).
 
-SI_SNR_loss on CUDA fp32 estimates runs on the HIP kernels (se_sisnr_fwd /
-se_sisnr_bwd, csrc/step.hip: one workgroup per utterance, fp64 sums, one
-elementwise backward); si_snr_loss_aligned also folds utils.py:105-121's mono
-reshape and pad / truncate of the estimate into the kernel's reads. The other
-losses are plain PyTorch device ops."""
+SI_SNR_loss on CUDA estimates (fp32, or the bf16 / fp16 tensors of a
+model.to(bfloat16) / .half() run, read and written in that dtype) runs on the
+HIP kernels (se_sisnr_fwd / se_sisnr_bwd, csrc/step.hip: one workgroup per
+utterance, fp64 sums, one elementwise backward); si_snr_loss_aligned also
+folds utils.py:105-121's mono reshape and pad / truncate of the estimate into
+the kernel's reads. The other losses are plain PyTorch device ops."""
 from __future__ import annotations
 
 import torch
@@ -18,16 +19,17 @@ class _SiSnr(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, est, target, zero_mean, eps):
-        N.require_device(est, target)
+        N.require_device(est, target, dtype=est.dtype)
         if est.stride(1) != 1:
             est = est.contiguous()
         target = target.contiguous()
         B, le = est.shape
         lt = target.shape[1]
-        loss = torch.empty(1, device=est.device, dtype=torch.float32)
+        loss = torch.empty(1, device=est.device, dtype=est.dtype)
         save = torch.empty(int(N.lib().se_sisnr_save_bytes(B)), device=est.device, dtype=torch.uint8)
         N.check(N.lib().se_sisnr_fwd(est.data_ptr(), le, est.stride(0), target.data_ptr(), lt, B, int(zero_mean),
-                                     float(eps), loss.data_ptr(), save.data_ptr(), N.stream_of(est)), "se_sisnr_fwd")
+                                     float(eps), loss.data_ptr(), save.data_ptr(), N.dtype_code(est),
+                                     N.stream_of(est)), "se_sisnr_fwd")
         ctx.save_for_backward(est, target, save)
         ctx.cfg = (int(zero_mean), float(eps))
         return loss.view(())
@@ -37,16 +39,18 @@ class _SiSnr(torch.autograd.Function):
         est, target, save = ctx.saved_tensors
         zero_mean, eps = ctx.cfg
         B, le = est.shape
-        g = torch.empty((B, le), device=est.device, dtype=torch.float32)
-        gl = gl.reshape(1).float().contiguous()
+        g = torch.empty((B, le), device=est.device, dtype=est.dtype)
+        gl = gl.reshape(1)
+        if gl.dtype != est.dtype:
+            gl = gl.to(est.dtype)
         N.check(N.lib().se_sisnr_bwd(est.data_ptr(), le, est.stride(0), target.data_ptr(), target.shape[1], B,
                                      zero_mean, eps, save.data_ptr(), gl.data_ptr(), g.data_ptr(), le,
-                                     N.stream_of(est)), "se_sisnr_bwd")
+                                     N.dtype_code(est), N.stream_of(est)), "se_sisnr_bwd")
         return g, None, None, None
 
 
 def _hip_sisnr_ok(estimate, target) -> bool:
-    return (estimate.is_cuda and estimate.dtype == torch.float32 and target.dtype == torch.float32
+    return (estimate.is_cuda and estimate.dtype in N.DTYPES and target.dtype == estimate.dtype
             and estimate.dim() == 2 and target.dim() == 2 and estimate.shape[0] == target.shape[0]
             and not target.requires_grad)
 

@@ -5,16 +5,20 @@ A real-valued conv U-Net over stacked re/im. The spectral front and back end
 gates, decoder, attention gates) run on the HIP kernels (the real-weight form
 of the conv GEMMs, complex_nn.real_conv2d); BatchNorm2d + PReLU run as one fused
 HIP pass each way (norm.bn_act -> se_bn_*); the LSTM (H = 512) runs on the wide
-HIP recurrence (complex_nn.LSTM -> se_lstm_wide_*).
+HIP recurrence (complex_nn.LSTM -> se_lstm_wide_*); the Linear(512 -> 514) head
+on the hand-written GEMM, reading the decoder output and writing the mask in
+their conv layouts (sehip.linear); the attention gates, the decoder's cat, the
+mask + cat, the clamp and the layout copies as HIP passes (sehip.glue).
 """
 from __future__ import annotations
 
 import torch
 import torch.nn as nn
-import torch.nn.functional as TF
 
-from ..complex_nn import LSTM, mark_data_fed, real_conv2d
+from .. import glue
+from ..complex_nn import LSTM, mark_data_fed, real_conv2d, stacked_lstms, _hip_lstm_ok
 from ..conv_stft import ConvSTFT, ConviSTFT
+from ..linear import linear
 from ..norm import bn_act
 
 
@@ -32,7 +36,7 @@ class ConvGLU(nn.Module):
         self.conv2 = nn.Conv2d(in_channels, out_channels, kernel_size, **kwargs)
 
     def forward(self, x):
-        return _conv(self.conv1, x) * torch.sigmoid(_conv(self.conv2, x))
+        return glue.glu(_conv(self.conv1, x), _conv(self.conv2, x))
 
 
 class DeConvGLU(nn.Module):
@@ -44,7 +48,7 @@ class DeConvGLU(nn.Module):
         self.conv_transpose2 = nn.ConvTranspose2d(in_channels, out_channels, kernel_size, **kwargs)
 
     def forward(self, x):
-        return _conv(self.conv_transpose1, x) * torch.sigmoid(_conv(self.conv_transpose2, x))
+        return glue.glu(_conv(self.conv_transpose1, x), _conv(self.conv_transpose2, x))
 
 
 class ConvBlock(nn.Module):
@@ -84,9 +88,14 @@ class Attention(nn.Module):
         self.conv2 = nn.Conv2d(in_channels, in_channels * 2, kernel_size=3, padding=1, bias=False)
         self.conv3 = nn.Conv2d(in_channels * 2, in_channels, kernel_size=3, padding=1, bias=False)
 
+    def gate_logits(self, x_u, x_c, pad_u=False):
+        """conv3(sigmoid(conv1(x_u) + conv2(x_c))): the pre-sigmoid gate; pad_u = x_u zero-padded by
+        one frequency row at the bottom (the decoder's F.pad, carn.py:108-109), folded into conv1."""
+        a = real_conv2d(self.conv1, x_u, (0, 0, 0, 1) if pad_u else None)
+        return _conv(self.conv3, glue.add_sigmoid(a, _conv(self.conv2, x_c)))
+
     def forward(self, x_u, x_c):
-        gate = torch.sigmoid(_conv(self.conv3, torch.sigmoid(_conv(self.conv1, x_u) + _conv(self.conv2, x_c))))
-        return gate * x_c
+        return glue.glu(x_c, self.gate_logits(x_u, x_c))
 
 
 class Encoder(nn.Module):
@@ -121,9 +130,9 @@ class Decoder(nn.Module):
     def forward(self, x, encoder_outputs):
         for attention, layer in zip(self.attention_layers, self.conv_transpose_layers):
             skip = encoder_outputs.pop()
-            if x.shape[2] < skip.shape[2]:
-                x = TF.pad(x, (0, 0, 0, 1))
-            x = layer(torch.cat([attention(x, skip), skip], dim=1))
+            pad = x.shape[2] < skip.shape[2]      # carn.py:108-109, folded into conv1's padding
+            # cat([sigmoid(gate) * skip, skip]) in one pass (carn.py:74-76, :112-113)
+            x = layer(glue.gate_cat(attention.gate_logits(x, skip, pad), skip))
         return x
 
 
@@ -144,15 +153,21 @@ class CARN(nn.Module):
     def forward(self, x):
         half = self.fft_size // 2 + 1
         spec = self.stft(x)
-        nr, ni = spec[:, :half], spec[:, half:]
-        h, skips = self.encoder(spec.view(spec.shape[0], 2, half, -1)[:, :, 1:].contiguous())
+        h, skips = self.encoder(glue.contiguous(spec.view(spec.shape[0], 2, half, -1)[:, :, 1:]))
         b, c, f, t = h.shape
-        h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2))[0].transpose(1, 2).reshape(b, c, f, t)
+        seq = h.reshape(b, c * f, t).transpose(1, 2)            # [b, t, c f]: a view, read in place
+        if _hip_lstm_ok(self.lstm) and not self.lstm.bidirectional and h.is_cuda:
+            # the LSTM output back to the conv layout and the storage type in one copy
+            raw = stacked_lstms(seq, [self.lstm], batch_first=True, raw=True)[0]   # fp32 [b, t, H]
+            h = glue.contiguous(raw.transpose(1, 2), h.dtype).view(b, c, f, t)
+        else:
+            h = glue.contiguous(self.lstm(seq)[0].transpose(1, 2)).view(b, c, f, t)
         h = self.decoder(h, skips)
-        h = self.linear(h.reshape(b, c * f, t).transpose(1, 2)).transpose(1, 2).reshape(b, 2, half, t)
-        mr, mi = h[:, 0], h[:, 1]
-        est = torch.cat([mr * nr - mi * ni, mr * ni - mi * nr], dim=1)   # carn.py:165-166 (sign as-is)
-        return est, torch.clamp_(self.istft(est), -1, 1)
+        # the Linear head reads the decoder output and writes the mask in their [b, C, t] layouts
+        m = linear(h.reshape(b, c * f, t).transpose(1, 2), self.linear, feature_major_out=True)
+        m = m.transpose(1, 2).reshape(b, 2, half, t)
+        est = glue.carn_mask(m, spec, half)     # carn.py:161-168 (sign as-is) + the cat
+        return est, glue.clamp(self.istft(est), -1, 1)
 
 
 class GCARN(CARN):

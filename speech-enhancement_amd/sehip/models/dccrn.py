@@ -9,7 +9,9 @@ from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspos
                           ComplexLSTM, LSTM, complex_concat, mark_data_fed, norm_act,
                           real_conv2d)
 from .. import functional as F
+from .. import glue
 from ..conv_stft import ConvSTFT, ConviSTFT
+from ..linear import linear
 
 
 class _Block(nn.Module):
@@ -89,8 +91,16 @@ class LSTMBlock(nn.Module):
             self.layers.append(LSTM(in_channels, hidden_channels, num_layers=num_layers, **kwargs))
             self.layers.append(nn.Linear(nd * hidden_channels, linear_channels))
 
+    # the last Linear's output as the transposed view of a [B, out, T] storage: the layout
+    # DCCRN.forward transposes it back to (dccrn.py:169-171), so that transpose is a view
+    feature_major_out = False
+
     def forward(self, x):
-        for layer in self.layers:
+        for i, layer in enumerate(self.layers):
+            last = i == len(self.layers) - 1
+            if isinstance(layer, nn.Linear) and isinstance(x, torch.Tensor) and x.is_cuda:
+                x = linear(x, layer, feature_major_out=last and self.feature_major_out)
+                continue
             x = layer(x)
             if isinstance(x, tuple):
                 x = x[0]
@@ -162,6 +172,9 @@ class DCCRN(nn.Module):
         self.decoder = Decoder(dec, in_channels=256, is_complex=is_complex)
         self.lstm = LSTMBlock(freq_channels, lstm_channels, linear_channels, num_layers=2, batch_first=True,
                               bidirectional=bidirectional, is_complex=is_complex)
+        self.lstm.feature_major_out = True
+        if is_complex:
+            self.lstm.layers[-1].feature_major_out = True
         self.masking, self.fft_size = masking, fft_size
 
     def forward(self, x):
@@ -171,17 +184,24 @@ class DCCRN(nn.Module):
         h, skips = self.encoder(spec.view(spec.shape[0], 2, half, -1)[:, :, 1:].contiguous())
         b, c, f, t = h.shape
         h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2)).transpose(1, 2).reshape(b, c, f, t)
-        h = TF.pad(self.decoder(h, skips), (0, 0, 1, 0))
-        mr, mi = h[:, 0], h[:, 1]
-        if mr.shape[-1] > nr.shape[-1]:
-            mr, mi = mr[..., :-1], mi[..., :-1]
-        est = F.polar_mask(mr, mi, nr, ni, 1) if self.masking == "E" else None
-        if est is not None:   # mask and concat in one pass each way (se_polar_mask_fwd / _bwd)
+        dec = self.decoder(h, skips)
+        est = None
+        if self.masking == "E" and dec.shape[-1] - nr.shape[-1] in (0, 1):
+            # the top zero row (F.pad, dccrn.py:172), the trailing-frame trim (:180-182), the mask
+            # and the concat in one pass each way (se_polar_mask_fwd / _bwd, m_row0 = 1)
+            est = F.polar_mask_stored(dec, nr, ni, 1, row0=1)
+        if est is None:
+            h = TF.pad(dec, (0, 0, 1, 0))
+            mr, mi = h[:, 0], h[:, 1]
+            if mr.shape[-1] > nr.shape[-1]:
+                mr, mi = mr[..., :-1], mi[..., :-1]
+            est = F.polar_mask(mr, mi, nr, ni, 1) if self.masking == "E" else None
+            if est is None:
+                re, im = self._mask_processing(nr, ni, mr, mi)
+                est = torch.cat([re, im], dim=1)
+        if est.dim() == 4:
             est = est.view(est.shape[0], -1, est.shape[-1])
-        else:
-            re, im = self._mask_processing(nr, ni, mr, mi)
-            est = torch.cat([re, im], dim=1)
-        return est, torch.clamp_(self.istft(est), -1, 1)
+        return est, glue.clamp(self.istft(est), -1, 1)
 
     def _mask_processing(self, noisy_real, noisy_imag, mask_real, mask_imag):
         """dccrn.py:187-207."""

@@ -9,6 +9,7 @@ import torch.nn.functional as TF
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLeakyReLU,
                           mark_data_fed, norm_act, real_conv2d)
 from .. import functional as F
+from .. import glue
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 # name -> per-layer ((complex channels, real channels), kernel, stride, padding)
@@ -175,7 +176,7 @@ class DCUNet(nn.Module):
         est = self._mask_processing(h, noisy)
         b, c, f, t = est.shape
         est = est.reshape(b, c * f, t)
-        return est, torch.clamp_(self.istft(est), -1, 1)
+        return est, glue.clamp(self.istft(est), -1, 1)
 
     def _mask_processing(self, x, noisy_spec, method="bounded_tanh"):
         """dcunet.py:158-184."""

@@ -18,6 +18,7 @@ from ..ccbam import CCBAM
 from ..complex_nn import (ComplexBatchNorm2d, ComplexConv2d, ComplexConvTranspose2d, ComplexLSTM,
                           complex_concat, mark_data_fed, norm_act, real_conv2d)
 from .. import functional as F
+from .. import glue
 from ..conv_stft import ConvSTFT, ConviSTFT
 
 
@@ -272,6 +273,7 @@ class FRCRN(nn.Module):
         self.decoder = Decoder(in_channels=128, out_channels=128, is_complex=is_complex,
                                reduction_ratio=reduction_ratio)
         self.lstm = ComplexLSTM(256, lstm_channels, num_layers=2, bidirectional=False, batch_first=True)
+        self.lstm.feature_major_out = True   # forward transposes it back to [b, c f, t] (:137): a view
         self.final_conv = nn.Conv2d(128, 2, kernel_size=(1, 2), bias=False)
         self.fft_size = fft_size
 
@@ -279,7 +281,7 @@ class FRCRN(nn.Module):
         half = self.fft_size // 2 + 1
         spec = self.stft(x)                                            # [B, N+2, T]
         noisy = spec.view(spec.shape[0], 2, half, spec.shape[-1])[:, :, 1:]   # drop DC (:123-127)
-        h, skips = noisy.contiguous(), []
+        h, skips = glue.contiguous(noisy), []
         attended = self.decoder.gate_state(h)
         for layer in self.encoder.layers:                              # Encoder.forward
             h, skip = layer(h, fork=True)
@@ -303,4 +305,4 @@ class FRCRN(nn.Module):
             est = TF.pad(mask * noisy, (0, 0, 1, 0))                   # :145-146 (DC back as 0)
             est = est.reshape(b, 2 * half, est.shape[-1])              # cat(re, im) on dim 1 (:149-152)
         wav = self.istft(est)
-        return est, torch.clamp_(wav, -1, 1)                           # :153-155
+        return est, glue.clamp(wav, -1, 1)                             # :153-155

@@ -7,7 +7,10 @@ Drop-in surface: ``AdamW`` takes torch.optim.AdamW's arguments (amsgrad,
 maximize, capturable, differentiable off) and keeps its state layout
 (state[p] = {'step', 'exp_avg', 'exp_avg_sq'}), so state_dicts load either way;
 ``clip_grad_norm_`` has torch's signature for the 2-norm and returns the
-total norm as a device tensor. Both need fp32 CUDA tensors (no CPU path).
+total norm as a device tensor. Both need contiguous CUDA tensors of one
+storage type per call: fp32, or the bf16 / fp16 of a model.to(bfloat16) /
+.half() run (ABI 10: torch's foreach AdamW rounding reproduced in the kernel).
+There is no CPU path.
 """
 from __future__ import annotations
 
@@ -36,10 +39,16 @@ def _slot_table(rows, device):
 
 
 def _check(ts):
+    """The storage-type code (SE_DTYPE_*) shared by every tensor, or RuntimeError."""
+    dt = None
     for t in ts:
-        if t is not None and (not t.is_cuda or t.dtype != torch.float32 or not t.is_contiguous()):
-            raise RuntimeError("sehip optim: parameters and gradients must be contiguous fp32 CUDA tensors "
-                               "(there is no CPU path)")
+        if t is None:
+            continue
+        if not t.is_cuda or t.dtype not in N.DTYPES or not t.is_contiguous() or (dt is not None and t.dtype != dt):
+            raise RuntimeError("sehip optim: parameters and gradients must be contiguous CUDA tensors of one "
+                               "storage type (fp32, bf16 or fp16; there is no CPU path)")
+        dt = t.dtype
+    return N.DTYPES[dt] if dt is not None else 0
 
 
 def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=False, foreach=None):
@@ -53,18 +62,18 @@ def clip_grad_norm_(parameters, max_norm, norm_type=2.0, error_if_nonfinite=Fals
     grads = [p.grad for p in parameters if p.grad is not None]
     if not grads:
         return torch.tensor(0.0)
-    _check(grads)
+    code = _check(grads)
     dev = grads[0].device
     table, n, total = _slot_table([(None, g, None, None) for g in grads], dev)
     sumsq = torch.empty(SUMSQ_DOUBLES, device=dev, dtype=torch.float64)
     norm = torch.empty(1, device=dev, dtype=torch.float32)
     st = N.stream_of(grads[0])
-    N.check(N.lib().se_grad_sumsq(table.data_ptr(), n, total, sumsq.data_ptr(), st), "se_grad_sumsq")
+    N.check(N.lib().se_grad_sumsq(table.data_ptr(), n, total, sumsq.data_ptr(), code, st), "se_grad_sumsq")
     if error_if_nonfinite and not torch.isfinite(sumsq[0]).item():   # [0] = the total (SE_SUMSQ_DOUBLES)
         raise RuntimeError(f"The total norm of order {float(norm_type)} for gradients from `parameters` "
                            "is non-finite, so it cannot be clipped")
     N.check(N.lib().se_clip_grads(table.data_ptr(), n, total, sumsq.data_ptr(), float(max_norm), norm.data_ptr(),
-                                  st), "se_clip_grads")
+                                  code, st), "se_clip_grads")
     return norm.view(())
 
 
@@ -106,9 +115,13 @@ class AdamW(torch.optim.Optimizer):
                 by_step.setdefault(s, []).append((p, p.grad, st["exp_avg"], st["exp_avg_sq"]))
             b1, b2 = group["betas"]
             for step_val, rows in sorted(by_step.items()):
-                _check([t for r in rows for t in r])
-                table, n, total = _slot_table(rows, rows[0][0].device)
-                N.check(N.lib().se_adamw_step(table.data_ptr(), n, total, float(group["lr"]), float(b1),
-                                              float(b2), float(group["eps"]), float(group["weight_decay"]),
-                                              step_val, N.stream_of(rows[0][0])), "se_adamw_step")
+                by_dtype: dict = {}
+                for r in rows:
+                    by_dtype.setdefault(r[0].dtype, []).append(r)
+                for rs in by_dtype.values():
+                    code = _check([t for r in rs for t in r])
+                    table, n, total = _slot_table(rs, rs[0][0].device)
+                    N.check(N.lib().se_adamw_step(table.data_ptr(), n, total, float(group["lr"]), float(b1),
+                                                  float(b2), float(group["eps"]), float(group["weight_decay"]),
+                                                  step_val, code, N.stream_of(rs[0][0])), "se_adamw_step")
         return loss

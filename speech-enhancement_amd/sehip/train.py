@@ -25,20 +25,22 @@ CLIP_NORM = 0.5                                                           # hype
 
 def make_optimizer(model, **overrides):
     """AdamW with the reference's hyper-parameters: sehip.optim.AdamW (one HIP
-    launch per step) for CUDA fp32 parameters, torch.optim.AdamW otherwise."""
+    launch per step and storage type) for contiguous CUDA parameters (fp32, or a
+    bf16 / fp16 model's), torch.optim.AdamW otherwise (CPU)."""
     kw = dict(ADAMW)
     kw.update(overrides)
     params = list(model.parameters())
-    if params and all(p.is_cuda and p.dtype == torch.float32 and p.is_contiguous() for p in params):
+    if params and all(p.is_cuda and p.dtype in _optim.N.DTYPES and p.is_contiguous() for p in params):
         return _optim.AdamW(params, **kw)
     return torch.optim.AdamW(params, **kw)
 
 
 def _clip(model, clip_norm):
     """clip_grad_norm_(model.parameters(), clip_norm) (trainer.py:216-218): the
-    HIP slot kernels for fp32 CUDA gradients."""
+    HIP slot kernels for CUDA gradients of one storage type (fp32 / bf16 / fp16)."""
     grads = [p.grad for p in model.parameters() if p.grad is not None]
-    if grads and all(g.is_cuda and g.dtype == torch.float32 and g.is_contiguous() for g in grads):
+    if grads and all(g.is_cuda and g.dtype == grads[0].dtype and g.dtype in _optim.N.DTYPES and g.is_contiguous()
+                     for g in grads):
         return _optim.clip_grad_norm_(model.parameters(), clip_norm)
     return torch.nn.utils.clip_grad_norm_(model.parameters(), clip_norm)
 

@@ -124,13 +124,68 @@ def test_models_route_inference_through_the_fused_mask():
     n0 = F.POLAR_MASK_CALLS[0]
     est_f, wav_f = m(x)
     assert F.POLAR_MASK_CALLS[0] == n0 + 1
-    polar = F.polar_mask
+    polar, stored = F.polar_mask, F.polar_mask_stored
     try:
         F.polar_mask = lambda *a, **k: None
+        F.polar_mask_stored = lambda *a, **k: None
         est_r, wav_r = m(x)
     finally:
-        F.polar_mask = polar
+        F.polar_mask, F.polar_mask_stored = polar, stored
     pairs += [(est_f.detach(), est_r.detach()), (wav_f.detach(), wav_r.detach())]
     for a, b in pairs:
         rel = ((a.double() - b.double()).norm() / b.double().norm()).item()
         assert rel <= 1e-5, rel
+
+
+def test_polar_mask_backward_fp16(gpu_device):
+    """The fp16 backward (DCCRN .half() training) against autograd of the reference op
+    sequence, as the fp32 / bf16 cases above (round-5 advice)."""
+    test_polar_mask_backward_matches_autograd(torch.float16, 1)
+    test_polar_mask_backward_matches_autograd(torch.float16, 0)
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float16])
+def test_polar_mask_zero_mask_nan_pattern(gpu_device, dtype):
+    """Mask elements at (0, 0) and near zero: torch's atan2 backward gives non-finite
+    gradients there; the kernel's backward has the same finite / non-finite pattern
+    (DCCRN 'E', the mode that trains)."""
+    g = torch.Generator(device="cuda").manual_seed(17)
+    B, Fq, T = 1, 9, 16
+    mr = torch.randn(B, Fq, T, device="cuda", generator=g).to(dtype)
+    mi = torch.randn(B, Fq, T, device="cuda", generator=g).to(dtype)
+    mr[0, 0, :4] = 0
+    mi[0, 0, :4] = 0
+    mr[0, 1, :4] = torch.tensor([1e-3, -1e-3, 2e-3, 0.0]).to(dtype)   # near zero, representable in both
+    mi[0, 1, :4] = torch.tensor([0.0, 1e-3, -2e-3, 1e-3]).to(dtype)
+    spec = torch.randn(B, 2, Fq, T, device="cuda", generator=g).to(dtype)
+    nr, ni = spec[:, 0], spec[:, 1]
+    gout = torch.randn(B, 2, Fq, T, device="cuda", generator=g).to(dtype)
+    a, c = mr.clone().requires_grad_(True), mi.clone().requires_grad_(True)
+    F.polar_mask(a, c, nr, ni, 1).backward(gout)
+    _, ra, rc = _ref_grads(mr, mi, nr, ni, 1, gout)
+    assert torch.equal(torch.isfinite(a.grad), torch.isfinite(ra))
+    assert torch.equal(torch.isfinite(c.grad), torch.isfinite(rc))
+    assert not torch.isfinite(a.grad[0, 0, :4]).any()
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_polar_mask_stored_equals_pad_trim_form(gpu_device, dtype):
+    """DCCRN's mask from the stored decoder output (ABI 10, m_row0 = 1): the top zero row
+    (F.pad, dccrn.py:172) and the trailing-frame trim (:180-182) folded into the kernels;
+    values and the decoder-output gradient bit-identical to pad + slice + polar_mask."""
+    g = torch.Generator(device="cuda").manual_seed(21)
+    B, Fq, T = 2, 17, 30
+    dec = (0.3 + torch.rand(B, 2, Fq - 1, T + 1, device="cuda", generator=g)).to(dtype)
+    spec = torch.randn(B, 2, Fq, T, device="cuda", generator=g).to(dtype)
+    nr, ni = spec[:, 0], spec[:, 1]
+    gout = torch.randn(B, 2, Fq, T, device="cuda", generator=g).to(dtype)
+    d1 = dec.clone().requires_grad_(True)
+    out1 = F.polar_mask_stored(d1, nr, ni, 1, row0=1)
+    out1.backward(gout)
+    d2 = dec.clone().requires_grad_(True)
+    h = torch.nn.functional.pad(d2, (0, 0, 1, 0))
+    out2 = F.polar_mask(h[:, 0, :, :T], h[:, 1, :, :T], nr, ni, 1)
+    out2.backward(gout)
+    assert torch.equal(out1, out2)
+    assert torch.equal(d1.grad, d2.grad)
+    assert torch.count_nonzero(d1.grad[..., T:]) == 0

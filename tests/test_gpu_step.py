@@ -206,3 +206,71 @@ def test_frcrn_mask_fused_vs_torch(gpu_device):
     est.backward(gest)
     ref.backward(gest)
     assert ((h.grad - h2.grad).norm() / h2.grad.norm()).item() < 1e-6
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_sisnr_16bit_storage(gpu_device, dtype):
+    """ABI 10: a model.to(bfloat16) / .half() run's SI-SNR reads and writes its own dtype
+    (no cast kernels): the loss within one rounding of the fp64 value of the same 16-bit
+    inputs, the gradient within 2 roundings (rel-L2), zero past the target length."""
+    from oracle.train import pad_or_truncate_wav as o_pad, si_snr_loss as o_loss
+    from sehip.losses import si_snr_loss_aligned
+    g = torch.Generator().manual_seed(9)
+    B, le, lt = 4, 16100, 16000
+    tgt = (torch.randn(B, lt, generator=g) * 0.3).to(dtype)
+    est = (torch.randn(B, le, generator=g) * 0.2)
+    est[:, :lt] += 0.8 * tgt.float()
+    est = est.to(dtype)
+    e64 = est.double().requires_grad_(True)
+    ref = o_loss(o_pad(e64, tgt.double()), tgt.double())
+    ref.backward()
+    ed = est.to(gpu_device).requires_grad_(True)
+    loss = si_snr_loss_aligned(ed, tgt.to(gpu_device))
+    assert loss.dtype == dtype
+    eps = torch.finfo(dtype).eps
+    assert abs(loss.item() - ref.item()) <= eps * abs(ref.item()) + 1e-6
+    loss.backward()
+    assert ed.grad.dtype == dtype
+    assert _rel(ed.grad, e64.grad) < 2 * eps
+    assert torch.count_nonzero(ed.grad[:, lt:]) == 0
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float16])
+def test_clip_and_adamw_16bit_match_torch(gpu_device, dtype):
+    """ABI 10: clip_grad_norm_ + AdamW over bf16 / fp16 parameters against torch's own
+    (foreach) implementations on the same tensors: the total norm within 1 rounding, every
+    clipped gradient and every updated parameter / state element within 1 ulp of the format
+    (torch rounds per foreach op; the kernel reproduces that sequence, the one freedom being
+    the fp32 summation order of the norms)."""
+    from sehip.optim import AdamW, clip_grad_norm_
+    a = _params(gpu_device, 4)
+    for p in a:
+        p.data = p.data.to(dtype)
+        p.grad = p.grad.to(dtype)
+    b = [torch.nn.Parameter(p.detach().clone()) for p in a]
+    for p, q in zip(a, b):
+        q.grad = p.grad.clone()
+    ulp = lambda t: torch.finfo(dtype).eps * t.float().abs().clamp_min(torch.finfo(dtype).tiny)
+    ta = torch.nn.utils.clip_grad_norm_(a, 0.5)
+    tb = clip_grad_norm_(b, 0.5)
+    assert abs(ta.float().item() - tb.item()) <= torch.finfo(dtype).eps * ta.float().item()
+    for p, q in zip(a, b):   # the coefficient may differ by one rounding: <= 2 ulp per product
+        assert ((p.grad.float() - q.grad.float()).abs() <= 2 * ulp(p.grad)).all()
+        q.grad.copy_(p.grad)   # the optimizer comparison starts from identical gradients
+    oa = torch.optim.AdamW(a, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2, foreach=True)
+    ob = AdamW(b, lr=1e-3, betas=(0.9, 0.999), eps=1e-8, weight_decay=1e-2)
+    g = torch.Generator().manual_seed(5)
+    for step in range(3):
+        oa.step()
+        ob.step()
+        for p, q in zip(a, b):
+            assert q.dtype == dtype and ob.state[q]["exp_avg"].dtype == dtype
+            bad = (p.float() - q.float()).abs() > ulp(p)
+            assert not bad.any(), (step, p.float()[bad][:4].tolist(), q.float()[bad][:4].tolist(), bad.sum().item())
+            for k in ("exp_avg", "exp_avg_sq"):
+                sa, sb = oa.state[p][k].float(), ob.state[q][k].float()
+                bad = (sa - sb).abs() > ulp(sa) + 1e-30
+                assert not bad.any(), (step, k, sa[bad][:4].tolist(), sb[bad][:4].tolist(), bad.sum().item())
+            ng = (torch.randn(p.shape, generator=g) * 0.05).to(dtype).to(gpu_device)
+            p.grad.copy_(ng)
+            q.grad.copy_(ng)

@@ -1,0 +1,94 @@
+"""Which Python lines still launch ATen / hipBLASLt kernels in a config's step.
+
+Runs one warm step of a BASELINE config under torch.profiler (CPU + GPU
+activity, Python stacks) and prints, per (kernel family, innermost sehip /
+model frame), the launch count: every GPU kernel whose name marks it as
+PyTorch's own (at::native, Cijk_ hipBLASLt, rocclr copies) is attributed to
+the Python line that issued it. Diagnostic only.
+
+  python tools/aten_sources.py --config 3|5|4 [--storage bf16|fp16|fp32]
+"""
+import argparse
+import collections
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "speech-enhancement_amd"))
+import torch
+
+
+def _family(name: str) -> str | None:
+    if "at::native" in name or name.startswith("void at::"):
+        return "aten:" + name.split("<")[0].replace("void ", "")[:60] + ("<" + name.split("<")[1][:70]
+                                                                        if "<" in name else "")
+    if name.startswith("Cijk_"):
+        return "hipblaslt:Cijk"
+    return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", type=int, default=3)
+    ap.add_argument("--storage", default=None)
+    a = ap.parse_args()
+    from sehip import functional as F, models as M, longform as L
+    from sehip.data import synthetic_pairs
+    from sehip.train import make_optimizer, train_step
+    dev = torch.device("cuda")
+    if a.config == 3:
+        st = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.storage or "bf16"]
+        F.set_conv_math("bf16")
+        m = M.DCCRN("dccrn-CL", 400, 100, 512).to(dev).train().to(st)
+        opt = make_optimizer(m)
+        x, c = synthetic_pairs(8, 64000, seed=6, device=dev)
+        x, c = x.to(st), c.to(st)
+        fn = lambda: train_step(m, opt, x, c)
+    elif a.config == 5:
+        st = {"fp16": torch.float16, "fp32": torch.float32}[a.storage or "fp16"]
+        m = M.CARN(320, 160, 512).to(dev).eval().to(st)
+        x, _ = synthetic_pairs(1, 48000 * 30, sr=48000, seed=7, device=dev)
+        x = x.to(st)
+        fn = lambda: L.enhance_chunked(m, x, 4 * 48000, 48000 // 20)
+    elif a.config == 2:
+        st = {"bf16": torch.bfloat16, "fp32": torch.float32}[a.storage or "bf16"]
+        F.set_conv_math("bf16")
+        m = M.DCUNet("dcunet16", 512, 128, 512).to(dev).eval().to(st)
+        x, _ = synthetic_pairs(4, 64000, seed=5, device=dev)
+        x = x.to(st)
+        fn = lambda: m(x)
+    else:
+        m = M.FRCRN().to(dev).train()
+        opt = make_optimizer(m)
+        x, c = synthetic_pairs(4, 64000, seed=6, device=dev)
+        fn = lambda: train_step(m, opt, x, c)
+    ctx = torch.no_grad() if a.config in (2, 5) else torch.enable_grad()
+    with ctx:
+        for _ in range(2):
+            fn()
+        torch.cuda.synchronize()
+        from torch.profiler import ProfilerActivity, profile
+        with profile(activities=[ProfilerActivity.CPU, ProfilerActivity.CUDA], with_stack=True) as prof:
+            fn()
+            torch.cuda.synchronize()
+    counts = collections.Counter()
+    total = collections.Counter()
+    for ev in prof.events():
+        kern = [k for k in getattr(ev, "kernels", [])]
+        if not kern:
+            continue
+        fams = [f for f in (_family(k.name) for k in kern) if f]
+        if not fams:
+            continue
+        frames = [s for s in (ev.stack or []) if "sehip" in s or "tools/" in s]
+        where = frames[0] if frames else (ev.stack[0] if ev.stack else "?")
+        for f in fams:
+            counts[(f, ev.name, where)] += 1
+            total[f] += 1
+    print(f"config {a.config}: {sum(total.values())} non-HIP kernel launches in one step")
+    for (f, op, where), n in counts.most_common():
+        print(f"{n:5d}  {f}\n       op={op}  at {where}")
+
+
+if __name__ == "__main__":
+    main()
