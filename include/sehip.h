@@ -207,6 +207,8 @@ enum { SE_DTYPE_F32 = 0, SE_DTYPE_BF16 = 1, SE_DTYPE_F16 = 2 };
 /* amax[0] = max(amax[0], max_i |x[i]|) over n elements (atomic; zero amax[0]
  * first for a fresh maximum). The scale source of SE_MATH_F16X3. */
 int se_amax(const float* x, long long n, float* amax, void* stream);
+/* ABI 10: amax[0] = max_i |x[i]| (the slot zeroed by the call itself). */
+int se_amax_init(const float* x, long long n, float* amax, void* stream);
 
 /* max(max |wr|, max |wi|) of a conv's weights (wi may be NULL) written to
  * *amax by one single-workgroup launch (no zeroing, no atomics): the

@@ -1817,6 +1817,15 @@ extern "C" int se_amax(const float* x, long long n, float* amax, void* stream) {
   return SE_OK;
 }
 
+extern "C" int se_amax_init(const float* x, long long n, float* amax, void* stream) {
+  if (!x || !amax || n < 0) return SE_E_ARG;
+  hipStream_t st = se::as_stream(stream);
+  if (hipMemsetAsync(amax, 0, sizeof(float), st) != hipSuccess) return SE_E_LAUNCH;
+  launch_amax(x, n, amax, st);
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
 extern "C" int se_conv2d_out_shape(const se_conv2d_desc* d, int* out_h, int* out_w) {
   ConvGeom g;
   const int rc = geom_of(d, g);

@@ -241,15 +241,17 @@ adamw16_kernel(const Slot* __restrict__ slots, int nslots, long long total, floa
     T* M = reinterpret_cast<T*>(s.exp_avg);
     T* V = reinterpret_cast<T*>(s.exp_avg_sq);
     const float g = (float)reinterpret_cast<const T*>(s.grad)[i];
-    const float p = rt<T>((float)P[i] * decay);                       // _foreach_mul_(params, 1 - lr wd)
+    // ATen's device functors contract a + b * c into one fma (the compiler's default); the
+    // same contractions here, explicitly, everything else one rounding per op
+    const float p = rt<T>((float)P[i] * decay);                         // _foreach_mul_(params, 1 - lr wd)
     const float m0 = (float)M[i];
-    const float m = rt<T>(w1 < 0.5f ? m0 + w1 * (g - m0) : g - (g - m0) * (1.f - w1));   // _foreach_lerp_
+    const float m = rt<T>(w1 < 0.5f ? fmaf(w1, g - m0, m0) : fmaf(-(g - m0), 1.f - w1, g));   // _foreach_lerp_
     float v = rt<T>((float)V[i] * beta2);                               // _foreach_mul_(v, b2)
-    v = rt<T>(v + omb2 * g * g);                                        // _foreach_addcmul_(v, g, g, 1 - b2)
+    v = rt<T>(fmaf(omb2 * g, g, v));                                    // _foreach_addcmul_(v, g, g, 1 - b2)
     float d = rt<T>(sqrtf(v));                                          // _foreach_sqrt
     d = rt<T>(d / bc2_sqrt);                                            // _foreach_div_
     d = rt<T>(d + eps);                                                 // _foreach_add_
-    P[i] = (T)(p + neg_step * (m / d));                                 // _foreach_addcdiv_
+    P[i] = (T)fmaf(neg_step, m / d, p);                                 // _foreach_addcdiv_
     M[i] = (T)m;
     V[i] = (T)v;
   });
@@ -483,7 +485,8 @@ extern "C" int se_polar_mask_fwd(const void* mr, const void* mi, long long m_bat
 // noisy spectrum none): from g = dL/d(re, im) [B, 2, F, T],
 //   d_gain = g_re cos ph + g_im sin ph,   d_ph = gain (g_im cos ph - g_re sin ph)
 //   d_mag  = d_gain n_mag (1 - tanh^2 m_mag)  (+ the phase path's m_mag terms)
-// through atan2 (d/dy = x / (x^2 + y^2), d/dx = -y / (x^2 + y^2), as torch's atan2 backward)
+// through atan2 (d/dy = x / (x^2 + y^2), d/dx = -y / (x^2 + y^2), 0 where x^2 + y^2 == 0, as
+// torch's atan2 backward)
 // and m_mag = sqrt(mr^2 + mi^2 + 1e-8) (d/dmr = mr / m_mag). fp32 arithmetic on the storage
 // values, the forward's intermediates recomputed (T-rounded as in the forward), gradients
 // rounded to T once. dm [B, 2, F, T]: (d mr, d mi).
@@ -530,15 +533,16 @@ polar_mask_bwd_kernel(const T* __restrict__ g, const T* __restrict__ mr, const T
   const float d_ph = gain * (gim * cp - gre * sp);
   float d_mag = d_gain * n_mag * (1.f - th * th);
   float da, dc;
+  // torch's atan2 backward is 0 where x^2 + y^2 == 0 (the origin, or squares that underflow)
   if constexpr (MODE == 0) {
     const float d_mph = d_ph / m_mag;                 // ph = n_ph + m_ph / m_mag
     d_mag += d_ph * (-m_ph / (m_mag * m_mag));
     const float r2 = a * a + c * c;
-    da = d_mph * (-c / r2);
-    dc = d_mph * (a / r2);
+    da = r2 == 0.f ? 0.f : d_mph * (-c / r2);
+    dc = r2 == 0.f ? 0.f : d_mph * (a / r2);
   } else {
     const float r2 = u * u + v * v;                   // m_ph = atan2(v, u), u = mr / m_mag, v = mi / m_mag
-    const float du = d_ph * (-v / r2), dv = d_ph * (u / r2);
+    const float du = r2 == 0.f ? 0.f : d_ph * (-v / r2), dv = r2 == 0.f ? 0.f : d_ph * (u / r2);
     d_mag += du * (-a / (m_mag * m_mag)) + dv * (-c / (m_mag * m_mag));
     da = du / m_mag;
     dc = dv / m_mag;

@@ -73,6 +73,7 @@ _SIGNATURES = {
     "se_istft_bwd": (c_int, [_P, _P] + [c_int] * 7 + [_P, _P, c_int, _P]),
     "se_conv2d_out_shape": (c_int, [_P, _P, _P]),
     "se_amax": (c_int, [_P, ctypes.c_longlong, _P, _P]),
+    "se_amax_init": (c_int, [_P, ctypes.c_longlong, _P, _P]),
     "se_amax_weights": (c_int, [_P, ctypes.c_longlong, _P, _P, _P]),
     "se_mix_snr": (c_int, [_P, _P, c_int, c_int, c_int, _P, _P, _P, _P, c_int, _P, _P, _P, _P]),
     "se_crop_pad": (c_int, [_P, _P, _P, _P, c_int, c_int, _P, _P]),

@@ -206,10 +206,21 @@ def amax_of(t: torch.Tensor) -> torch.Tensor:
     """The registered bound of max |t|, else max |t| computed now (and registered)."""
     a = amax_get(t)
     if a is None:
-        a = torch.zeros(1, device=t.device, dtype=torch.float32)
-        N.check(N.lib().se_amax(t.data_ptr(), t.numel(), a.data_ptr(), N.stream_of(t)), "se_amax")
+        a = torch.empty(1, device=t.device, dtype=torch.float32)
+        N.check(N.lib().se_amax_init(t.data_ptr(), t.numel(), a.data_ptr(), N.stream_of(t)), "se_amax_init")
         amax_put(t, a)
     return a
+
+
+def amax_pair(x: torch.Tensor, s: torch.Tensor) -> torch.Tensor:
+    """max(bound of x, bound of s) in a fresh slot: the registered bounds (or one read of each
+    tensor) combined by the amax kernels themselves (se_amax_init + se_amax on the two slots)."""
+    ax, as_ = amax_of(x), amax_of(s)
+    out = new_amax(x.device)
+    lib, st = N.lib(), N.stream_of(x)
+    N.check(lib.se_amax_init(ax.data_ptr(), 1, out.data_ptr(), st), "se_amax_init")
+    N.check(lib.se_amax(as_.data_ptr(), 1, out.data_ptr(), st), "se_amax")
+    return out
 
 
 def new_amax(device) -> torch.Tensor:
@@ -507,7 +518,7 @@ class _ConvJoined(torch.autograd.Function):
         ws = _workspace(nbytes, x.device)
         st = N.stream_of(x)
         # scale source of the joined input: max of the two sources' bounds
-        xa = torch.maximum(amax_of(x), amax_of(s)) if _f16_operands(d)[0] else None
+        xa = amax_pair(x, s) if _f16_operands(d)[0] else None
         d.x_amax = N.ptr(xa)
         wa = _weight_amax(d, wr, wi)
         d.w_amax = N.ptr(wa)
@@ -538,7 +549,7 @@ class _ConvJoined(torch.autograd.Function):
         ga = amax_of(gy) if _f16_operands(d)[1] else None
         xa = ctx.x_amax
         if xa is None and _f16_operands(d)[0]:   # mode changed since forward
-            xa = torch.maximum(amax_of(x), amax_of(s))
+            xa = amax_pair(x, s)
         d.x_amax, d.dy_amax, d.w_amax = N.ptr(xa), N.ptr(ga), N.ptr(ctx.w_amax)
         gx = gs = dwr = dwi = dbr = dbi = None
         if ctx.needs_input_grad[0] or ctx.needs_input_grad[1]:
@@ -1377,7 +1388,10 @@ def _bias_grads(ctx, db):
     if db is None:
         return None, None
     both = ctx.has_b[0] and ctx.has_b[1]
-    return (db if ctx.has_b[0] else None), ((db.clone() if both else db) if ctx.has_b[1] else None)
+    if both:
+        from . import glue
+        db2 = glue.copy_into(db, torch.empty_like(db))
+    return (db if ctx.has_b[0] else None), ((db2 if both else db) if ctx.has_b[1] else None)
 
 
 class _LstmLayer(torch.autograd.Function):

@@ -127,7 +127,9 @@ def clamp(x, lo, hi):
 # --------------------------------------------------------------------------- ComplexLSTM
 class _StackReIm(torch.autograd.Function):
     """x [B, T, 2I] (any dense layout, any storage type) -> fp32 [2B, T, I]: the real
-    half's sequences then the imaginary half's (complex_nn.py:128-131 + the batch stack)."""
+    half's sequences then the imaginary half's (complex_nn.py:128-131 + the batch stack).
+    The input gradient is written in x's own layout (e.g. the transposed view of a conv
+    output), so the producer's backward receives it contiguous."""
 
     @staticmethod
     def forward(ctx, x):
@@ -137,15 +139,18 @@ class _StackReIm(torch.autograd.Function):
         sb, st, sk = x.stride()
         src = torch.as_strided(x, (2, B, T, I), (I * sk, sb, st, sk))
         copy_into(src, out)
+        dense = x.is_contiguous() or x.transpose(1, 2).is_contiguous()
         ctx.shape, ctx.dtype = (B, T, I2), x.dtype
+        ctx.strides = x.stride() if dense else (T * I2, I2, 1)
         return out.view(2 * B, T, I)
 
     @staticmethod
     def backward(ctx, g):
         B, T, I2 = ctx.shape
         I = I2 // 2
-        dx = torch.empty((B, T, I2), device=g.device, dtype=ctx.dtype)
-        dst = torch.as_strided(dx, (2, B, T, I), (I, T * I2, I2, 1))
+        sb, st, sk = ctx.strides
+        dx = torch.empty_strided((B, T, I2), ctx.strides, device=g.device, dtype=ctx.dtype)
+        dst = torch.as_strided(dx, (2, B, T, I), (I * sk, sb, st, sk))
         copy_into(g.reshape(2, B, T, I), dst)
         return dx
 

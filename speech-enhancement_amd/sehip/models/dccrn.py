@@ -181,7 +181,7 @@ class DCCRN(nn.Module):
         half = self.fft_size // 2 + 1
         spec = self.stft(x)
         nr, ni = spec[:, :half], spec[:, half:]
-        h, skips = self.encoder(spec.view(spec.shape[0], 2, half, -1)[:, :, 1:].contiguous())
+        h, skips = self.encoder(glue.contiguous(spec.view(spec.shape[0], 2, half, -1)[:, :, 1:]))
         b, c, f, t = h.shape
         h = self.lstm(h.reshape(b, c * f, t).transpose(1, 2)).transpose(1, 2).reshape(b, c, f, t)
         dec = self.decoder(h, skips)

@@ -57,6 +57,17 @@ def _defer_ok(model) -> bool:
         and os.environ.get("SEHIP_OVERLAP", "1") != "0"
 
 
+_ONES: dict = {}
+
+
+def _ones_like(t):
+    key = (t.device, t.dtype, tuple(t.shape))
+    o = _ONES.get(key)
+    if o is None:
+        o = _ONES[key] = torch.ones_like(t)
+    return o
+
+
 def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
     """One optimisation step; returns the (device) loss, no host sync."""
     from . import functional as F
@@ -64,7 +75,8 @@ def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
     _, wav = model(noisy)
     loss = si_snr_loss_aligned(wav, clean)     # mono reshape + pad / truncate + SI-SNR
     with deferred_weight_grads(_defer_ok(model)):
-        loss.backward()
+        # the backward's seed dL/dL = 1 from a cached tensor (loss.backward() would fill a new one)
+        torch.autograd.backward(loss, _ones_like(loss))
     finish_grads(model)
     if clip_norm:
         _clip(model, clip_norm)

@@ -80,14 +80,45 @@ def main():
         fams = [f for f in (_family(k.name) for k in kern) if f]
         if not fams:
             continue
-        frames = [s for s in (ev.stack or []) if "sehip" in s or "tools/" in s]
-        where = frames[0] if frames else (ev.stack[0] if ev.stack else "?")
+        e, stack = ev, []
+        while e is not None and not stack:   # the nearest ancestor op that recorded Python frames
+            stack = [s for s in (e.stack or [])]
+            e = e.cpu_parent
+        frames = [s for s in stack if "sehip" in s or "tools/" in s or "tests/" in s]
+        where = " <- ".join(frames[:3]) if frames else (stack[0] if stack else "?")
         for f in fams:
             counts[(f, ev.name, where)] += 1
             total[f] += 1
     print(f"config {a.config}: {sum(total.values())} non-HIP kernel launches in one step")
     for (f, op, where), n in counts.most_common():
         print(f"{n:5d}  {f}\n       op={op}  at {where}")
+    # the Python lines of the ATen ops that can launch a kernel (a dispatch mode sees the
+    # backward's ops too: the autograd engine carries the mode to its threads)
+    import traceback
+    from torch.utils._python_dispatch import TorchDispatchMode
+    meta = ("empty", "view", "_unsafe_view", "as_strided", "transpose", "t", "permute", "expand", "slice",
+            "select", "unsqueeze", "squeeze", "detach", "alias", "reshape", "split", "chunk", "unbind",
+            "lift_fresh", "empty_strided", "new_empty", "new_empty_strided", "set_", "is_same_size",
+            "_local_scalar_dense", "record_stream", "empty_like", "_reshape_alias", "split_with_sizes",
+            "unflatten", "flatten", "narrow", "diagonal", "view_as", "expand_as", "sym_size", "sym_stride",
+            "sym_numel", "sym_storage_offset", "is_contiguous", "_has_compatible_shallow_copy_type")
+    seen = collections.Counter()
+
+    class Log(TorchDispatchMode):
+        def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+            name = func.__name__.split(".")[0]
+            dev = [t for t in args if isinstance(t, torch.Tensor)]
+            if name not in meta and any(t.is_cuda for t in dev):
+                fr = [f"{os.path.basename(x.filename)}:{x.lineno}" for x in traceback.extract_stack()
+                      if "sehip" in x.filename or "/tools/" in x.filename]
+                seen[(func.__name__, " <- ".join(fr[-3:][::-1]))] += 1
+            return func(*args, **(kwargs or {}))
+    with ctx, Log():
+        fn()
+        torch.cuda.synchronize()
+    print("ATen ops with a CUDA tensor argument (op, innermost sehip frames):")
+    for (op, where), n in seen.most_common():
+        print(f"{n:5d}  {op}  at {where}")
 
 
 if __name__ == "__main__":
