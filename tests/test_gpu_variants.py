@@ -114,3 +114,51 @@ def test_dcunet_real_raises_like_reference(gpu_device):
     m = M.DCUNet("dcunet16", 512, 128, 512, is_complex=False).cuda()
     with pytest.raises(RuntimeError):
         m(torch.zeros(1, 32000, device="cuda"))
+
+
+def _dcunet16_tanh_grads(dev, dtype, sehip=False, perturb=0.0, seed=1234):
+    """DCUNet-16 with its DEFAULT 'bounded_tanh' mask (_1903_03107_dcunet.py:158-184), the
+    training backward of the whole model, fp64 / fp32 on the CPU (oracle) or the HIP path."""
+    from oracle import models as O, train as OT
+    noisy, clean = paramfill.structured_pair(1, 32000, seed=42)
+    if sehip:
+        from sehip import models as M
+        from sehip.losses import SI_SNR_loss as loss_fn, pad_or_truncate_wav as pad
+        m = M.DCUNet("dcunet16", 512, 128, 512)
+    else:
+        loss_fn, pad = OT.si_snr_loss, OT.pad_or_truncate_wav
+        m = O.DCUNet("dcunet16", 512, 128, 512)
+    m = paramfill.fill_(m, seed=75).to(dev).to(dtype).train()
+    x = torch.from_numpy(noisy).to(dtype)
+    if perturb:
+        gen = torch.Generator().manual_seed(seed)
+        x = x * (1 + perturb * torch.randn(x.shape, generator=gen, dtype=torch.float64)).to(dtype)
+    c = torch.from_numpy(clean).to(dev).to(dtype)
+    _, w = m(x.to(dev))
+    loss_fn(pad(w, c), c).backward()
+    return {n: p.grad.detach().double().cpu() for n, p in m.named_parameters()}
+
+
+def test_dcunet16_bounded_tanh_train_grads_vs_fp64(gpu_device):
+    """The default mask's training gradients through the whole model.
+    At random init this mask's gradient is ill-conditioned (profiles/r6_dcunet_tanh_spread.log,
+    tools/dcunet_tanh_spread.py): a 2^-22 relative input perturbation moves the fp64 gradient by
+    5.7e-2 / 7.3e-2 median per tensor, and the fp32 CPU oracle lands 3.6e-1 off fp64. The gate
+    is therefore anchored on those fp32 evaluations (as DCCRN's and DCUNet-20's): each tensor
+    within 3x the largest fp32-evaluation error of fp64, and the median within 3x the largest
+    median. (The well-conditioned 'bounded_sigmoid' form is gated tightly by
+    test_dcunet20_train_grads_vs_fp64, the op by tests/test_gpu_polar_mask.py.)"""
+    g64 = _dcunet16_tanh_grads("cpu", torch.float64)
+    evals = [_dcunet16_tanh_grads("cpu", torch.float32)] + \
+        [_dcunet16_tanh_grads("cpu", torch.float32, perturb=2.0 ** -22, seed=1234 + i) for i in range(2)]
+    gh = _dcunet16_tanh_grads("cuda", torch.float32, sehip=True)
+    assert sorted(gh) == sorted(g64)
+    assert all(torch.isfinite(g).all() for g in gh.values())
+    rel = lambda g, n: (g[n] - g64[n]).norm().item() / (g64[n].norm().item() + 1e-30)
+    rows = [(rel(gh, n), max(rel(q, n) for q in evals), n) for n in g64]
+    bad = [r for r in rows if r[0] > max(3 * r[1], 1e-4)]
+    med_h = np.median([r[0] for r in rows])
+    med_o = max(np.median([rel(q, n) for n in g64]) for q in evals)
+    print(f"dcunet16 bounded_tanh grads vs fp64: median hip {med_h:.2e}, fp32 evaluations up to {med_o:.2e}")
+    assert not bad, sorted(bad, key=lambda r: -r[0])[:5]
+    assert med_h < 3 * med_o, (med_h, med_o)
