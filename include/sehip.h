@@ -631,8 +631,9 @@ int se_ccbam_channel_pool(const float* x, float* mean, float* mx, int* amax,
                           int B, int C, int HW, void* stream);
 int se_ccbam_spatial_pool(const float* x, const float* ca, float* pooled,
                           short* idx, int B, int C, int HW, void* stream);
+/* ABI 10: out_amax (or NULL) receives max |out| (the slot zeroed by the call). */
 int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out,
-                   int B, int C, int HW, void* stream);
+                   int B, int C, int HW, float* out_amax, void* stream);
 int se_ccbam_bwd_sa(const float* gout, float* dsa, int B, int C, int HW,
                     void* stream);
 /* ABI 6: se_ccbam_bwd_sa with the spatial gate's sigmoid backward fused:
@@ -687,6 +688,8 @@ int se_carn_mask_fwd(const void* m, long long m_batch_stride, const void* spec, 
 int se_carn_mask_bwd(const void* gest, const void* m, long long m_batch_stride, const void* spec, int B, int half,
                      int T, int dtype, void* dm, void* dspec, void* stream);
 int se_add_sigmoid_fwd(const void* a, const void* b, void* y, long long n, int dtype, void* stream);
+/* y = sigmoid(x) = 1 / (1 + exp(-x)) (accurate expf; e.g. CCBAM's spatial gate, ccbam.py:86). */
+int se_sigmoid_fwd(const void* x, void* y, long long n, int dtype, void* stream);
 int se_sigmoid_bwd(const void* g, const void* y, void* dz, long long n, int dtype, void* stream);
 int se_gate_cat_fwd(const void* c, const void* skip, void* out, int B, int C, long long HW, int dtype, void* stream);
 int se_gate_cat_bwd(const void* gout, const void* c, const void* skip, void* dc, void* dskip, int B, int C,

@@ -107,21 +107,33 @@ __global__ __launch_bounds__(kThreads) void spatial_pool_kernel(const float* __r
   }
 }
 
-// out = x*ca + sa[half]
+// out = x*ca + sa[half]; with amax (ABI 10), also max |out| (atomic max of the fp32 bit
+// patterns into the slot the entry point zeroed): the SE_MATH_F16X3 scale source of the
+// GEMMs that read out, exact instead of the bound max |x| + 1
 __global__ __launch_bounds__(kThreads) void apply_kernel(const float* __restrict__ x, const float* __restrict__ ca,
                                                          const float* __restrict__ sa, float* __restrict__ out, int C,
-                                                         int HW) {
+                                                         int HW, unsigned* __restrict__ amax) {
   const int b = blockIdx.y;
   const int hw = blockIdx.x * kThreads + threadIdx.x;
   extern __shared__ float sca[];
   for (int c = threadIdx.x; c < C; c += kThreads) sca[c] = ca[(size_t)b * C + c];
   __syncthreads();
-  if (hw >= HW) return;
-  const int Ch = C / 2;
-  const float s0 = sa[((size_t)b * 2) * HW + hw], s1 = sa[((size_t)b * 2 + 1) * HW + hw];
-  const size_t base = (size_t)b * C * HW + hw;
+  float m = 0.f;
+  if (hw < HW) {
+    const int Ch = C / 2;
+    const float s0 = sa[((size_t)b * 2) * HW + hw], s1 = sa[((size_t)b * 2 + 1) * HW + hw];
+    const size_t base = (size_t)b * C * HW + hw;
 #pragma unroll 8
-  for (int c = 0; c < C; ++c) out[base + (size_t)c * HW] = x[base + (size_t)c * HW] * sca[c] + (c < Ch ? s0 : s1);
+    for (int c = 0; c < C; ++c) {
+      const float v = x[base + (size_t)c * HW] * sca[c] + (c < Ch ? s0 : s1);
+      out[base + (size_t)c * HW] = v;
+      m = fmaxf(m, fabsf(v));
+    }
+  }
+  if (amax) {
+    const unsigned bits = __builtin_bit_cast(unsigned, se::wave_max(m));
+    if ((threadIdx.x & 63) == 0 && bits) atomicMax(amax, bits);
+  }
 }
 
 // ---------------------------------------------------------------- backward
@@ -508,11 +520,12 @@ extern "C" int se_ccbam_spatial_pool(const float* x, const float* ca, float* poo
 }
 
 extern "C" int se_ccbam_apply(const float* x, const float* ca, const float* sa, float* out, int B, int C, int HW,
-                              void* stream) {
+                              float* out_amax, void* stream) {
   if (int rc = check(B, C, HW)) return rc;
   if (!x || !ca || !sa || !out) return SE_E_ARG;
+  if (out_amax && hipMemsetAsync(out_amax, 0, sizeof(float), se::as_stream(stream)) != hipSuccess) return SE_E_LAUNCH;
   hipLaunchKernelGGL(apply_kernel, hw_grid(B, HW), dim3(kThreads), C * sizeof(float), se::as_stream(stream), x, ca,
-                     sa, out, C, HW);
+                     sa, out, C, HW, (unsigned*)out_amax);
   SE_LAUNCH_CHECK();
   return SE_OK;
 }

@@ -204,6 +204,12 @@ __global__ void __launch_bounds__(kThreads) add_sigmoid_kernel(const T* __restri
     y[i] = (T)sigm(rt<T>((float)a[i] + (float)b[i]));
 }
 
+template <typename T>
+__global__ void __launch_bounds__(kThreads) sigmoid_kernel(const T* __restrict__ x, T* __restrict__ y, long long n) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads)
+    y[i] = (T)(1.f / (1.f + expf(-(float)x[i])));
+}
+
 // dz = g (1 - y) y   (torch's sigmoid_backward)
 template <typename T>
 __global__ void __launch_bounds__(kThreads) sigmoid_bwd_kernel(const T* __restrict__ g, const T* __restrict__ y,
@@ -448,6 +454,17 @@ extern "C" int se_add_sigmoid_fwd(const void* a, const void* b, void* y, long lo
   SE_DT_SWITCH(dtype, {
     hipLaunchKernelGGL(add_sigmoid_kernel<TY>, dim3(grid_of(n, 4)), dim3(kThreads), 0, se::as_stream(stream),
                        (const TY*)a, (const TY*)b, (TY*)y, n);
+  })
+  SE_LAUNCH_CHECK();
+  return SE_OK;
+}
+
+extern "C" int se_sigmoid_fwd(const void* x, void* y, long long n, int dtype, void* stream) {
+  if (!x || !y || n < 0) return SE_E_ARG;
+  if (n == 0) return SE_OK;
+  SE_DT_SWITCH(dtype, {
+    hipLaunchKernelGGL(sigmoid_kernel<TY>, dim3(grid_of(n, 4)), dim3(kThreads), 0, se::as_stream(stream),
+                       (const TY*)x, (TY*)y, n);
   })
   SE_LAUNCH_CHECK();
   return SE_OK;

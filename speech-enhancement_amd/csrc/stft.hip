@@ -477,6 +477,10 @@ __global__ void __launch_bounds__(kThreads) stft_fwd_ip_kernel(const StftArgs a)
 #define SE_STFT_WV_PAIRS 8
 #endif
 constexpr int kWvPairs = SE_STFT_WV_PAIRS;
+// the register-radix ConvSTFT for nfft 640 / 512 / 320 (stft_fwd_rg_kernel); 0: the wave-local form
+#ifndef SE_STFT_RG
+#define SE_STFT_RG 1
+#endif
 using se::kWave;
 // Twiddle table per wave-local kernel: staged in LDS (1) or read through L1 (0). The
 // forward and the adjoint read it through L1 (the FFT passes' LDS traffic drops by the
@@ -568,6 +572,9 @@ __device__ __forceinline__ void wv_unpack_store(const float2* A, int t0, int T, 
     }
     im += 0.f;   // -0 -> +0 (atan2 branch cut)
     const int o = k * T + t;
+#if SE_RG_PROBE == 2   // probe: no spectrum stores (kept live by an impossible condition)
+    if (re != 1234.5f) continue;
+#endif
     if (!mag_phase) {
       if constexpr (!LP) {
         float* op = static_cast<float*>(out0) + ub;
@@ -648,6 +655,235 @@ __global__ void __launch_bounds__(kWave * W) stft_fwd_wv_kernel(const StftArgs a
   wfft_pass<N, 0, 1>(Aw, stw, lane);
   __syncthreads();   // every pair of the block transformed
   wv_unpack_store<N, W, LP>(A, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
+}
+
+// ---------------------------------------------------------------------------
+// Register-radix ConvSTFT (nfft = 64 R, R = 10 / 8 / 5: 640, 512, 320). One frame pair per
+// wave, N = 64 x R as a two-level decomposition n = l + 64 q (lane l, register q):
+//   1. the gather leaves each lane its R samples x[l + 64 q] in registers (with win <= N/2
+//      the upper R/2 are the zero padding, compile-time zeros: HALF);
+//   2. an R-point DFT over q in registers, times the twiddle W_N^(l k1)  (no LDS);
+//   3. the R results go to LDS as R rows of 64 (row k1, column l; padded rows), and each
+//      row's 64-point DFT over l runs as two radix-8 passes (wave-local, in place);
+//   4. row k1, column k2 then holds X[k1 + R k2], which the block's unpack reads by that map.
+// One LDS round trip fewer than the three-pass wave-local form (stft_fwd_wv_kernel), and the
+// first radix stage skips the zero half of the padded frame.
+template <int R>
+__device__ __forceinline__ void rdft(const float2 (&v)[kMaxRadix], float2 (&o)[kMaxRadix]) {
+  if constexpr (R == 10) {
+    float2 E[5], O[5];
+    dft5(v[0], v[2], v[4], v[6], v[8], E);
+    dft5(v[1], v[3], v[5], v[7], v[9], O);
+    const float2 W[5] = {make_float2(1.f, 0.f),
+                         make_float2(0.80901699437494742410f, -0.58778525229247312917f),
+                         make_float2(0.30901699437494742410f, -0.95105651629515357212f),
+                         make_float2(-0.30901699437494742410f, -0.95105651629515357212f),
+                         make_float2(-0.80901699437494742410f, -0.58778525229247312917f)};
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const float2 t = k ? cmul(O[k], W[k]) : O[0];
+      o[k] = cadd(E[k], t);
+      o[k + 5] = csub(E[k], t);
+    }
+  } else if constexpr (R == 8) {
+    const float r = 0.70710678118654752440f;
+    const float2 a0 = cadd(v[0], v[4]), a1 = csub(v[0], v[4]);
+    const float2 a2 = cadd(v[2], v[6]), a3 = mul_mi(csub(v[2], v[6]));
+    const float2 a4 = cadd(v[1], v[5]), a5 = csub(v[1], v[5]);
+    const float2 a6 = cadd(v[3], v[7]), a7 = mul_mi(csub(v[3], v[7]));
+    const float2 e0 = cadd(a0, a2), e2 = csub(a0, a2), e1 = cadd(a1, a3), e3 = csub(a1, a3);
+    const float2 o0 = cadd(a4, a6), o2 = csub(a4, a6), o1 = cadd(a5, a7), o3 = csub(a5, a7);
+    const float2 w1 = make_float2(r * (o1.x + o1.y), r * (o1.y - o1.x));
+    const float2 w2 = mul_mi(o2);
+    const float2 w3 = make_float2(r * (o3.y - o3.x), -r * (o3.x + o3.y));
+    o[0] = cadd(e0, o0); o[4] = csub(e0, o0);
+    o[1] = cadd(e1, w1); o[5] = csub(e1, w1);
+    o[2] = cadd(e2, w2); o[6] = csub(e2, w2);
+    o[3] = cadd(e3, w3); o[7] = csub(e3, w3);
+  } else {
+    static_assert(R == 5, "register radix: 10, 8 or 5");
+    float2 x5[5];
+    dft5(v[0], v[1], v[2], v[3], v[4], x5);
+#pragma unroll
+    for (int k = 0; k < 5; ++k) o[k] = x5[k];
+  }
+}
+
+#ifndef SE_RG_ROW
+#define SE_RG_ROW 72
+#endif
+#ifndef SE_RG_NT
+#define SE_RG_NT 0   // non-temporal spectrum stores (variant builds)
+#endif
+#ifndef SE_RG_PROBE
+#define SE_RG_PROBE 0   // timing probes of the register-radix ConvSTFT (variant builds only)
+#endif
+#ifndef SE_RG_W
+#define SE_RG_W 8
+#endif
+#ifndef SE_RG_PPW
+#define SE_RG_PPW 1
+#endif
+constexpr int kRgRow = SE_RG_ROW;   // float2 per LDS row of 64 (+8 pad: the radix-8 reads of 4 rows x
+                                    // 8 columns land on 32 distinct even banks)
+
+// Position of element i (0..63) of a row in LDS: 8 columns of 9 (one pad per 8), so the
+// stride-1 (i = j + 8 q, lanes along j) and the stride-8 (i = 8 j + q, lanes along j)
+// accesses of the radix-8 passes both spread a 32-lane group over 32 distinct banks
+// (row stride kRgRow = 72 = 8 x 9: 4 rows x 8 columns per group)
+__device__ __forceinline__ int rg_pos(int i) { return (i & 7) + 9 * (i >> 3); }
+
+// the 64-point DFTs of the R rows of one wave's image (in place, Stockham order):
+// pass 0 (Ns = 1): reads i = j + 8 q, writes 8 j + q; pass 1 (Ns = 8, twiddles
+// W64^(q j) = W_N^(R q j)): reads and writes j + 8 q
+template <int R, int PS, int ROWS = R>
+__device__ __forceinline__ void rg_row_pass(float2* a, const float2* __restrict__ tw, int lane) {
+  constexpr int NB = 8 * ROWS, ITER = (NB + kWave - 1) / kWave;
+  float2 v[ITER][kMaxRadix];
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int bi = lane + it * kWave;
+    if (NB % kWave == 0 || bi < NB) {
+      const int r = bi >> 3, j = bi & 7;
+      const float2* row = a + r * kRgRow;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) v[it][q] = row[j + 9 * q];   // rg_pos(j + 8 q)
+      if constexpr (PS == 1) {
+#pragma unroll
+        for (int q = 1; q < 8; ++q) v[it][q] = cmul(v[it][q], tw[R * q * j]);
+      }
+    }
+  }
+  wave_lds_sync();
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int bi = lane + it * kWave;
+    if (NB % kWave == 0 || bi < NB) {
+      const int r = bi >> 3, j = bi & 7;
+      float2 o[kMaxRadix];
+      rdft<8>(v[it], o);
+      float2* row = a + r * kRgRow;
+#pragma unroll
+      for (int q = 0; q < 8; ++q) row[PS == 0 ? q + 9 * j : j + 9 * q] = o[q];   // rg_pos(8 j + q) / (j + 8 q)
+    }
+  }
+  wave_lds_sync();
+}
+
+// W pairs per block, TPB threads; lanes along frames: a store covers 2W consecutive frames of
+// a spectrum row (the per-(bin, pair) form with both frames of a pair per item measured slower:
+// its stores interleave at a 2-frame stride)
+template <int N, int R, int W, int TPB, bool LP>
+__device__ __forceinline__ void rg_unpack_store(const float2* A, int t0, int T, int b, void* out0, void* out1,
+                                                int mag_phase, int dt) {
+  constexpr int half = N / 2 + 1, FT = 2 * W, WS = R * kRgRow;
+  const long long ub = (long long)b * (mag_phase ? half : 2 * half) * T;
+  for (int idx = threadIdx.x; idx < half * FT; idx += TPB) {
+    const int k = idx / FT, f = idx - k * FT;
+    const int t = t0 + f;
+    if (t >= T) continue;
+    const int j = f >> 1;
+    const int kc = k ? N - k : 0;
+    const float2 zk = A[j * WS + (k % R) * kRgRow + rg_pos(k / R)];
+    const float2 zc = A[j * WS + (kc % R) * kRgRow + rg_pos(kc / R)];
+    float re, im;
+    if ((f & 1) == 0) {   // (Z[k] + conj Z[N-k]) / 2
+      re = 0.5f * (zk.x + zc.x);
+      im = 0.5f * (zk.y - zc.y);
+    } else {              // (Z[k] - conj Z[N-k]) / (2i)
+      re = 0.5f * (zk.y + zc.y);
+      im = -0.5f * (zk.x - zc.x);
+    }
+    im += 0.f;   // -0 -> +0 (atan2 branch cut)
+    const int o = k * T + t;
+#if SE_RG_PROBE == 2   // probe: no spectrum stores (kept live by an impossible condition)
+    if (re != 1234.5f) continue;
+#endif
+    if (!mag_phase) {
+      if constexpr (!LP) {
+        float* op = static_cast<float*>(out0) + ub;
+#if SE_RG_NT
+        __builtin_nontemporal_store(re, op + o);
+        __builtin_nontemporal_store(im, op + o + half * T);
+#else
+        op[o] = re;
+        op[o + half * T] = im;
+#endif
+      } else {
+        stx<LP>(out0, ub + o, re, dt);
+        stx<LP>(out0, ub + o + half * T, im, dt);
+      }
+    } else {
+      stx<LP>(out0, ub + o, sqrtf(re * re + im * im), dt);
+      stx<LP>(out1, ub + o, atan2f(im, re), dt);
+    }
+  }
+}
+
+// grid (ceil(T / 2 W PPW), B), 64 W threads. HALF: win <= N / 2 (registers q >= R/2 are zeros).
+// PPW frame pairs per wave: their 64-point row passes run together, 8 R PPW butterflies over the
+// wave's 64 lanes (R = 10, PPW = 2: 160 = 2.5 lane rounds per pass instead of 2 x 1.25)
+template <int N, bool HALF, int W = 4, int PPW = 2, bool LP = false>
+__global__ void __launch_bounds__(kWave * W) stft_fwd_rg_kernel(const StftArgs a) {
+  constexpr int R = N / kWave, QN = HALF ? R / 2 : R, FT = 2 * W * PPW;
+  static_assert(R * kWave == N, "nfft = 64 R");
+  __shared__ __attribute__((aligned(16))) float2 A[W * PPW * R * kRgRow];
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int t0 = tb * FT;
+  const long long xo = (long long)b * a.L;
+  const int pl = rg_pos(lane);
+  float2* Aw = A + w * PPW * R * kRgRow;
+#pragma unroll
+  for (int p = 0; p < PPW; ++p) {
+    const int ta = t0 + 2 * (w * PPW + p), tbb = ta + 1;
+    float2 v[kMaxRadix];
+#pragma unroll
+    for (int q = QN; q < kMaxRadix; ++q) v[q] = make_float2(0.f, 0.f);
+    const int sa = ta * a.hop - a.pad;
+#if SE_RG_PROBE == 3   // probe: no signal loads
+    if (true) {
+#pragma unroll
+      for (int q = 0; q < QN; ++q) v[q] = make_float2((float)(lane + q + tb), (float)(lane - q + b));
+    } else
+#endif
+    if (!LP && sa >= 0 && tbb < a.T && sa + a.hop + a.win <= a.L) {
+      const float* xp = static_cast<const float*>(a.x) + xo + sa;
+#pragma unroll
+      for (int q = 0; q < QN; ++q) {
+        const int n = lane + q * kWave;
+        const bool ok = n < a.win;
+        const int nn = ok ? n : 0;
+        const float wv = ok ? a.window[nn] : 0.f;
+        v[q] = make_float2(wv * xp[nn], wv * xp[a.hop + nn]);
+      }
+    } else {
+#pragma unroll
+      for (int q = 0; q < QN; ++q) {
+        const int n = lane + q * kWave;
+        const bool ok = n < a.win;
+        const int nn = ok ? n : 0;
+        const float wv = ok ? a.window[nn] : 0.f;
+        const float xa = ldx<LP>(a.x, xo + reflect_index(min(ta, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+        const float xb = ldx<LP>(a.x, xo + reflect_index(min(tbb, a.T - 1) * a.hop + nn - a.pad, a.L), a.dt);
+        v[q] = make_float2(ta < a.T ? wv * xa : 0.f, tbb < a.T ? wv * xb : 0.f);
+      }
+    }
+    float2 o[kMaxRadix];
+    rdft<R>(v, o);
+    float2* Ap = Aw + p * R * kRgRow;
+    Ap[pl] = o[0];
+#pragma unroll
+    for (int k1 = 1; k1 < R; ++k1) Ap[k1 * kRgRow + pl] = cmul(o[k1], a.tw[lane * k1]);
+  }
+  wave_lds_sync();
+#if SE_RG_PROBE != 1   // probe 1: no 64-point row passes
+  rg_row_pass<R, 0, R * PPW>(Aw, a.tw, lane);
+  rg_row_pass<R, 1, R * PPW>(Aw, a.tw, lane);
+#endif
+  __syncthreads();   // every pair of the block transformed
+  rg_unpack_store<N, R, W * PPW, kWave * W, LP>(A, t0, a.T, b, a.out0, a.out1, a.mag_phase, a.dt);
 }
 
 struct IstftArgs {
@@ -1265,6 +1501,23 @@ extern "C" int se_stft_fwd(const void* x, void* out0, void* out1, int B, int L, 
   a.L = L; a.win = win; a.hop = hop; a.T = T; a.pad = pad; a.mag_phase = mag_phase;
   a.P = pick_pairs(nfft); a.pl = pl;
   const size_t shm = 2 * (size_t)a.P * nfft * sizeof(float2);
+  if (SE_STFT_RG && (nfft == 640 || nfft == 512 || nfft == 320)) {
+    hipStream_t st = se::as_stream(stream);
+    constexpr int W = SE_RG_W, PPW = SE_RG_PPW;
+    const dim3 grid(se::ceil_div(T, 2 * W * PPW), B), blk(se::kWave * W);
+    const bool hf = 2 * win <= nfft;
+#define SE_STFT_RGL(NF, H)                                                                              \
+    do {                                                                                                \
+      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((stft_fwd_rg_kernel<NF, H, W, PPW, true>), grid, blk, 0, st, a); \
+      else hipLaunchKernelGGL((stft_fwd_rg_kernel<NF, H, W, PPW, false>), grid, blk, 0, st, a);         \
+    } while (0)
+    if (nfft == 640) { if (hf) SE_STFT_RGL(640, true); else SE_STFT_RGL(640, false); }
+    else if (nfft == 512) { if (hf) SE_STFT_RGL(512, true); else SE_STFT_RGL(512, false); }
+    else SE_STFT_RGL(320, false);
+#undef SE_STFT_RGL
+    SE_LAUNCH_CHECK();
+    return SE_OK;
+  }
   if (SE_STFT_WV && ip_plan(nfft)) {
     // wave-local FFT, wv_pairs<nfft>() frame pairs per block
     hipStream_t st = se::as_stream(stream);

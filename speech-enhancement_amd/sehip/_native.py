@@ -140,7 +140,7 @@ _SIGNATURES = {
     "se_ccbam_workspace_size": (c_size_t, [c_int] * 3),
     "se_ccbam_channel_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
     "se_ccbam_spatial_pool": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
-    "se_ccbam_apply": (c_int, [_P] * 4 + [c_int] * 3 + [_P]),
+    "se_ccbam_apply": (c_int, [_P] * 4 + [c_int] * 3 + [_P, _P]),
     "se_ccbam_bwd_sa": (c_int, [_P] * 2 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_sa_sigmoid": (c_int, [_P] * 3 + [c_int] * 3 + [_P]),
     "se_ccbam_bwd_dca": (c_int, [_P] * 5 + [c_int] * 3 + [_P, c_size_t, _P]),
@@ -160,6 +160,7 @@ _SIGNATURES = {
     "se_carn_mask_bwd": (c_int, [_P, _P, ctypes.c_longlong, _P, c_int, c_int, c_int, c_int, _P, _P, _P]),
     "se_add_sigmoid_fwd": (c_int, [_P, _P, _P, ctypes.c_longlong, c_int, _P]),
     "se_sigmoid_bwd": (c_int, [_P, _P, _P, ctypes.c_longlong, c_int, _P]),
+    "se_sigmoid_fwd": (c_int, [_P, _P, ctypes.c_longlong, c_int, _P]),
     "se_gate_cat_fwd": (c_int, [_P, _P, _P, c_int, c_int, ctypes.c_longlong, c_int, _P]),
     "se_gate_cat_bwd": (c_int, [_P, _P, _P, _P, _P, c_int, c_int, ctypes.c_longlong, c_int, _P]),
     "se_glu_fwd": (c_int, [_P, _P, _P, ctypes.c_longlong, c_int, _P]),

@@ -120,6 +120,7 @@ class _CCBAMFn(torch.autograd.Function):
     def forward(ctx, x, mod, *params):
         N.require_device(x)
         x = x.contiguous()
+        t0 = F._TIMER.begin() if F._TIMER else None
         B, C, H, W = x.shape
         HW = H * W
         lib, st, dev = N.lib(), N.stream_of(x), x.device
@@ -153,14 +154,16 @@ class _CCBAMFn(torch.autograd.Function):
             z = sab.conv(Pl)                                          # [B, 2, H, W] pre-sigmoid
         # the gate's sigmoid outside autograd: its backward is fused into
         # se_ccbam_bwd_sa_sigmoid
-        sa = torch.sigmoid(z.detach()).contiguous()
+        zc = z.detach().contiguous()
+        sa = torch.empty_like(zc)
+        _call(lib.se_sigmoid_fwd, "se_sigmoid_fwd", zc.data_ptr(), sa.data_ptr(), zc.numel(), 0, st)
         out = torch.empty_like(x)
-        xa = F.amax_get(x)
-        oa = xa + 1.0 if xa is not None else None   # ca, sa in (0, 1): |x ca + sa| <= max |x| + 1
+        oa = F.new_amax(dev)   # max |out|, found by the apply pass: the consumers' F16X3 scale source
         _call(lib.se_ccbam_apply, "se_ccbam_apply", x.data_ptr(), ca.data_ptr(), sa.data_ptr(),
-              out.data_ptr(), B, C, HW, st)
-        if oa is not None:   # F16X3 scale source of the consumers
-            F.amax_put(out, oa)
+              out.data_ptr(), B, C, HW, oa.data_ptr(), st)
+        F.amax_put(out, oa)
+        if t0 is not None:   # algorithmic bytes: x read once, out written once
+            F._TIMER.end("ccbam_fwd", t0, 0.0, 2.0 * x.numel() * x.element_size())
         if need_grad:
             ctx.save_for_backward(x, idx, amax)
             ctx.graphs = (pooled, ca, Pl, z, sa)
@@ -177,6 +180,7 @@ class _CCBAMFn(torch.autograd.Function):
         HW = H * W
         lib, st, dev = N.lib(), N.stream_of(gout), gout.device
         gout = gout.contiguous()
+        t0 = F._TIMER.begin() if F._TIMER else None
         dz = torch.empty(B, 2, H, W, device=dev)   # d loss / d (pre-sigmoid gate)
         _call(lib.se_ccbam_bwd_sa_sigmoid, "se_ccbam_bwd_sa_sigmoid", gout.data_ptr(), sa.data_ptr(),
               dz.data_ptr(), B, C, HW, st)
@@ -205,6 +209,8 @@ class _CCBAMFn(torch.autograd.Function):
         _call(lib.se_ccbam_bwd_dx, "se_ccbam_bwd_dx", gout.data_ptr(), dP.data_ptr(), idx.data_ptr(),
               ca.data_ptr(), dmean.data_ptr(), dmax.data_ptr(), amax.data_ptr(), dx.data_ptr(),
               B, C, HW, st)
+        if t0 is not None:   # algorithmic bytes: gout and x read once, dx written once
+            F._TIMER.end("ccbam_bwd", t0, 0.0, 3.0 * x.numel() * x.element_size())
         grads = {id(p): g for p, g in zip(sp, gs[1:])}
         grads.update({id(p): g for p, g in zip(ch, gc[1:])})
         del ctx.graphs

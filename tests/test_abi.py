@@ -187,7 +187,7 @@ def test_ccbam_and_join_validation_need_no_gpu():
     # (x, mean, max, amax, B, C, HW, stream): odd C -> SE_E_SHAPE, null -> SE_E_ARG
     assert lib.se_ccbam_channel_pool(None, None, None, None, 2, 7, 10, None) == -2
     assert lib.se_ccbam_channel_pool(None, None, None, None, 2, 8, 10, None) == -1
-    assert lib.se_ccbam_apply(None, None, None, None, 2, 8, 10, None) == -1
+    assert lib.se_ccbam_apply(None, None, None, None, 2, 8, 10, None, None) == -1
     ws = lib.se_ccbam_workspace_size(2, 8, 10)
     assert lib.se_ccbam_bwd_dca(None, None, None, None, None, 2, 8, 10, None, ws, None) == -1
     # join: (x, Cx, Fx, Tx, s, Cs, F, T, out, B, stream)

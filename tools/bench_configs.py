@@ -21,15 +21,37 @@ sys.path.insert(0, os.path.join(ROOT, "speech-enhancement_amd"))
 import torch
 
 
+_ROCTX = []
+
+
+def _roctx():
+    """roctxProfilerResume / Pause (librocprofiler-sdk-roctx) when SEHIP_ROCTX_REGIONS=1: under
+    `rocprofv3 --selected-regions` only the timed iterations are traced (no data generation,
+    model construction or warm-up in the kernel statistics)."""
+    if not _ROCTX:
+        lib = None
+        if os.environ.get("SEHIP_ROCTX_REGIONS") == "1":
+            import ctypes
+            lib = ctypes.CDLL("/opt/rocm/lib/librocprofiler-sdk-roctx.so")
+        _ROCTX.append(lib)
+    return _ROCTX[0]
+
+
 def timeit(fn, iters, warm=2):
     for _ in range(warm):
         fn()
     torch.cuda.synchronize()
+    rt = _roctx()
+    if rt is not None:
+        rt.roctxProfilerResume(0)
     t0 = time.perf_counter()
     for _ in range(iters):
         fn()
     torch.cuda.synchronize()
-    return (time.perf_counter() - t0) / iters
+    dt = (time.perf_counter() - t0) / iters
+    if rt is not None:
+        rt.roctxProfilerPause(0)
+    return dt
 
 
 def main():
