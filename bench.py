@@ -318,6 +318,8 @@ def run(args):
     rank, world, local, device = setup_distributed()
     if device.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
+    if os.environ.get("SEHIP_PRIO_MAIN"):   # the step on a stream of that priority (A/B knob)
+        torch.cuda.set_stream(torch.cuda.Stream(device, priority=SF.stream_priority("SEHIP_PRIO_MAIN")))
     if world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} rank(s)")
     dist_backend = torch.distributed.get_backend() if world > 1 else None

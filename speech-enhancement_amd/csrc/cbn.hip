@@ -462,15 +462,17 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
 template <int SRC, typename T, bool V4>
 __global__ void __launch_bounds__(kThreads)
 cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, const T* __restrict__ x,
-                         T* __restrict__ dx, int C, int HW, int act, float slope, const double* part,
-                         const float* ext, int P, double count, const float* save, Ptr5 params, int affine,
-                         MPtr5 dparams, int has_dparams, int training, float* dx_amax) {
+                         T* __restrict__ dx, int C, int HW, int seg_len, int act, float slope,
+                         const double* part, const float* ext, int P, double count, const float* save, Ptr5 params,
+                         int affine, MPtr5 dparams, int has_dparams, int training, float* dx_amax) {
   static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
   __shared__ float k[kCoef];
   const int Cc = C / 2, c = blockIdx.x, b = blockIdx.y;
+  const int hw0 = blockIdx.z * seg_len, hw1 = min(HW, hw0 + seg_len);   // this workgroup's segment
   if (threadIdx.x < 64)
     bwd_finalize_wave<false, T, false>(c, threadIdx.x, part, ext, P, count, Cc, save, params, affine, dparams,
-                                       has_dparams, training, k, dx_amax, nullptr, nullptr, b == 0);
+                                       has_dparams, training, k, dx_amax, nullptr, nullptr,
+                                       b == 0 && blockIdx.z == 0);
   __syncthreads();
   const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
   const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
@@ -487,7 +489,7 @@ cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, co
   };
   if constexpr (V4) {
     constexpr int U = 2;   // float4s per plane and tensor in flight
-    for (int i0 = threadIdx.x * 4; i0 < HW; i0 += kThreads * 4 * U) {
+    for (int i0 = hw0 + threadIdx.x * 4; i0 < hw1; i0 += kThreads * 4 * U) {
       f32x4v xr4[U], xi4[U], gr4[U], gi4[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -504,7 +506,7 @@ cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, co
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + u * kThreads * 4;
-        if (i < HW) {
+        if (i < hw1) {
           f32x4v dr4, di4;
 #pragma unroll
           for (int l = 0; l < 4; ++l) {
@@ -520,7 +522,7 @@ cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, co
     }
   } else {
     constexpr int U = 4;
-    for (int i0 = threadIdx.x; i0 < HW; i0 += kThreads * U) {
+    for (int i0 = hw0 + threadIdx.x; i0 < hw1; i0 += kThreads * U) {
       float fxr[U], fxi[U], fgr[U], fgi[U];
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -533,7 +535,7 @@ cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, co
 #pragma unroll
       for (int u = 0; u < U; ++u) {
         const int i = i0 + u * kThreads;
-        if (i < HW) {
+        if (i < hw1) {
           float dr, di;
           one(fxr[u], fxi[u], fgr[u], fgi[u], dr, di);
           dx[offr + i] = (T)dr;
@@ -1263,9 +1265,16 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
   if (SE_CBN_APPLY_FIN && (src == 0 || src == 1) && !pr && !fc) {
     const bool v4 = HW % 4 == 0;
-#define SE_AF(S, V)                                                                                            \
-  hipLaunchKernelGGL((cbn_bwd_apply_fin_kernel<S, T, V>), dim3(Cc, B), mb, 0, st, gy, gy2, x, dx, C, HW, act, slope, \
-                     part, ext, P, (double)B * HW, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, training, xa)
+    // few channels (CCBAM's one-channel spatial branch: Cc x B = 64 workgroups): each plane
+    // split into segments of whole 2048-element strides, up to ~1024 workgroups
+    constexpr int kStride = kThreads * 8;
+    const int nseg = std::max(1, std::min(se::ceil_div(HW, kStride), 1024 / std::max(1, Cc * B)));
+    const int seg_len = se::ceil_div(se::ceil_div(HW, nseg), kStride) * kStride;
+    const int ns = se::ceil_div(HW, seg_len);
+#define SE_AF(S, V)                                                                                              \
+  hipLaunchKernelGGL((cbn_bwd_apply_fin_kernel<S, T, V>), dim3(Cc, B, ns), mb, 0, st, gy, gy2, x, dx, C, HW, seg_len, \
+                     act, slope, part, ext, P, (double)B * HW, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0,        \
+                     training, xa)
     if (src == 1 && v4) SE_AF(1, true);
     else if (src == 1) SE_AF(1, false);
     else if (v4) SE_AF(0, true);

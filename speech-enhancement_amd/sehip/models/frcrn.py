@@ -28,7 +28,7 @@ _SIDE_STREAMS: dict = {}
 def _side_stream(dev):
     s = _SIDE_STREAMS.get(dev)
     if s is None:
-        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev, priority=F.stream_priority("SEHIP_PRIO_GATES"))
         F.SIDE_STREAMS.append(s)
     return s
 
