@@ -318,8 +318,6 @@ def run(args):
     rank, world, local, device = setup_distributed()
     if device.type != "cuda":
         raise SystemExit("bench.py needs a GPU")
-    if os.environ.get("SEHIP_PRIO_MAIN"):   # the step on a stream of that priority (A/B knob)
-        torch.cuda.set_stream(torch.cuda.Stream(device, priority=SF.stream_priority("SEHIP_PRIO_MAIN")))
     if world != args.gpus:
         raise SystemExit(f"bench.py --gpus {args.gpus} but the process group has {world} rank(s)")
     dist_backend = torch.distributed.get_backend() if world > 1 else None
@@ -331,6 +329,8 @@ def run(args):
     batches = [synthetic_pairs(B, L, seed=2023 + rank * 1_000_003 + i, device=device) for i in range(2)]
     dist = torch.distributed if (world > 1 and torch.distributed.is_initialized()) else None
 
+    trace = os.environ.get("SEHIP_BENCH_TRACE") == "1"
+
     def timed(steps, warmup, timer=None):
         for i in range(warmup):
             noisy, clean = batches[i % 2]
@@ -341,10 +341,20 @@ def run(args):
         torch.cuda.synchronize()
         SF.set_op_timer(timer)
         t0 = time.perf_counter()
+        marks = []
         for i in range(steps):
             noisy, clean = batches[i % 2]
             loss = train_step(model, opt, noisy, clean)
+            if trace:
+                marks.append(time.perf_counter() - t0)
         torch.cuda.synchronize()
+        if trace:   # host enqueue timeline (SEHIP_BENCH_TRACE=1): where the host blocked
+            _note("enqueue ms: " + " ".join(f"{1e3 * m:.0f}" for m in marks)
+                  + f" | sync {1e3 * (time.perf_counter() - t0):.0f}")
+            ms = torch.cuda.memory_stats(device)
+            _note(f"allocator: reserved peak {ms['reserved_bytes.all.peak'] / 2**30:.1f} GiB, allocated peak "
+                  f"{ms['allocated_bytes.all.peak'] / 2**30:.1f} GiB, alloc retries {ms['num_alloc_retries']}, "
+                  f"device mallocs {ms['segment.all.allocated']}")
         if dist:
             dist.barrier()
         elapsed = time.perf_counter() - t0

@@ -59,14 +59,6 @@ def deferred_weight_grads(enabled: bool = True):
             torch.cuda.current_stream(side.device).wait_stream(side)
 
 
-def stream_priority(var):
-    """HIP stream priority of a side stream from the environment (0: torch's default,
-    -1: high; clamped to the device's range)."""
-    p = int(os.environ.get(var, "0"))
-    lo, hi = torch.cuda.Stream.priority_range()
-    return max(min(p, lo), hi)
-
-
 def _wgrad_stream(*inputs):
     """Context for a weight-grad launch: a no-op, or (deferred_weight_grads) the
     device's side stream, after it waited for the current stream; the inputs are
@@ -76,7 +68,7 @@ def _wgrad_stream(*inputs):
     dev = inputs[0].device
     side = _DEFER_STREAMS.get(dev)
     if side is None:
-        side = _DEFER_STREAMS[dev] = torch.cuda.Stream(dev, priority=stream_priority("SEHIP_PRIO_WGRAD"))
+        side = _DEFER_STREAMS[dev] = torch.cuda.Stream(dev)
         SIDE_STREAMS.append(side)
     side.wait_stream(torch.cuda.current_stream(dev))
     for t in inputs:

@@ -3,8 +3,10 @@
 Constructor signature, module tree and state_dict keys (279 entries) match
 the reference. The spectral front/back end (ConvSTFT/ConviSTFT), every
 complex conv / transposed conv, every ComplexBatchNorm2d (+ fused
-LeakyReLU) and the real final_conv run on csrc/*.hip kernels; LSTM, CCBAM
-pooling, pads/concats and the tanh mask are PyTorch device ops.
+LeakyReLU), the real final_conv, the complex LSTM, the CCBAM skip gates, the
+skip joins (folded into the decoder GEMMs), the tanh mask and the SI-SNR loss
+run on csrc/*.hip kernels; a training step launches no ATen kernel
+(profiles/r6_*_kernel_stats.csv, tools/aten_sources.py).
 """
 from __future__ import annotations
 
@@ -28,7 +30,7 @@ _SIDE_STREAMS: dict = {}
 def _side_stream(dev):
     s = _SIDE_STREAMS.get(dev)
     if s is None:
-        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev, priority=F.stream_priority("SEHIP_PRIO_GATES"))
+        s = _SIDE_STREAMS[dev] = torch.cuda.Stream(dev)
         F.SIDE_STREAMS.append(s)
     return s
 

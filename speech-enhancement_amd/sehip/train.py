@@ -68,8 +68,29 @@ def _ones_like(t):
     return o
 
 
+_INFLIGHT: list = []
+
+
+def _throttle(dev):
+    """Host flow control: at most SEHIP_MAX_INFLIGHT (default 2) steps queued on the GPU.
+    A host far ahead of the GPU keeps every queued step's freed temporaries pinned (their
+    uses on the side streams are recorded), the caching allocator grows past the step's
+    working set, and at the HBM limit it frees its cache and allocates again: stalls of
+    seconds when the driver is still clearing the previous process's memory
+    (profiles/r6_host_runahead.log)."""
+    depth = int(os.environ.get("SEHIP_MAX_INFLIGHT", "2"))
+    if depth <= 0 or dev.type != "cuda":
+        return
+    ev = torch.cuda.Event()
+    ev.record(torch.cuda.current_stream(dev))
+    _INFLIGHT.append(ev)
+    while len(_INFLIGHT) > depth:
+        _INFLIGHT.pop(0).synchronize()
+
+
 def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
-    """One optimisation step; returns the (device) loss, no host sync."""
+    """One optimisation step; returns the (device) loss, no host sync (beyond keeping at
+    most SEHIP_MAX_INFLIGHT steps queued, _throttle)."""
     from . import functional as F
     from .functional import deferred_weight_grads
     _, wav = model(noisy)
@@ -83,6 +104,7 @@ def train_step(model, optimizer, noisy, clean, clip_norm=CLIP_NORM):
     optimizer.step()
     optimizer.zero_grad(set_to_none=True)
     F.lstm_wide_poll()      # a wide-LSTM barrier timeout raises here, not as a NaN loss later
+    _throttle(noisy.device)
     return loss.detach()
 
 

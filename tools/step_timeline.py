@@ -17,6 +17,7 @@ from sehip.models import FRCRN  # noqa: E402
 from sehip.train import make_optimizer, train_step  # noqa: E402
 
 secs = float(sys.argv[1]) if len(sys.argv) > 1 else 30.0
+k = int(sys.argv[2]) if len(sys.argv) > 2 else 1
 dev = torch.device("cuda")
 torch.manual_seed(2023)
 model = FRCRN().to(dev).train()
@@ -28,7 +29,8 @@ t0 = time.time()
 i = 0
 while time.time() - t0 < secs:
     s = time.perf_counter()
-    train_step(model, opt, *batches[i % 2])
+    for _ in range(k):
+        train_step(model, opt, *batches[i % 2])
+        i += 1
     torch.cuda.synchronize()
-    print(f"{time.time() - t_start:8.3f} s  step {i:4d}  {1e3 * (time.perf_counter() - s):8.2f} ms", flush=True)
-    i += 1
+    print(f"{time.time() - t_start:8.3f} s  step {i - k:4d}  {1e3 * (time.perf_counter() - s) / k:8.2f} ms", flush=True)
