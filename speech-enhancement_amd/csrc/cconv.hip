@@ -1080,7 +1080,6 @@ __global__ void prep_class_kernel(WeightView w, TapList taps, int Cg, int N, int
 }
 
 #include "cconv_x3.hpp"
-#include "cconv_ws.hpp"
 
 // bias_full[n] for the fused complex conv: re = br - bi, im = bi + br.
 __global__ void prep_bias_kernel(const float* br, const float* bi, int N, int complex_w, float* out, int sd) {
@@ -1439,12 +1438,6 @@ static bool env_flag_off(const char* name) {
   const char* e = std::getenv(name);
   return e && e[0] == '0';
 }
-// SEHIP_X3_WS = 1 + V: the warp-specialised gather GEMM variant V (cconv_ws.hpp), else -1
-static int ws_variant() {
-  const char* e = std::getenv("SEHIP_X3_WS");
-  return (e && e[0] >= '1' && e[0] <= '8') ? e[0] - '1' : -1;
-}
-
 // The weight image of a gather pass: per stride-phase class the GEMM weight
 // tiles Wp (Kp x ldw, in the layout of the kernel the pass runs) and the tap
 // table ktab, laid out 256-byte aligned from base. Built by the pass itself in
@@ -1737,22 +1730,6 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
           else if (wide) SE_X3_SD(2, true, 2);
           else SE_X3_SD(1, true, 2);
 #undef SE_X3_SD
-        } else if (f16 && wide && tu && ws_variant() >= 0 && c.Kp / kBK <= kWsMaxSteps) {   // warp-specialised A/B form
-#define SE_WS(V)                                                                                         \
-  do {                                                                                                   \
-    const dim3 wblk(ws_threads<V>());                                                                    \
-    if (join_in) hipLaunchKernelGGL((gather_ws_kernel<1, V>), grid, wblk, 0, st, a);                      \
-    else if (join_out) hipLaunchKernelGGL((gather_ws_kernel<2, V>), grid, wblk, 0, st, a);                \
-    else hipLaunchKernelGGL((gather_ws_kernel<0, V>), grid, wblk, 0, st, a);                              \
-  } while (0)
-          switch (ws_variant()) {
-            case 0: SE_WS(0); break;
-            case 1: SE_WS(1); break;
-            case 4: SE_WS(4); break;
-            case 6: SE_WS(6); break;
-            default: SE_WS(2); break;
-          }
-#undef SE_WS
         } else if (h1 && wide) SE_X3_LAUNCH(1, 2, true);
         else if (h1) SE_X3_LAUNCH(1, 1, true);
         else if (f16 && wide) SE_X3_LAUNCH(3, 2, true);
