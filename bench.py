@@ -44,7 +44,11 @@ FP32_MFMA_PEAK_TFLOPS = 157.3     # MI355X_MICROARCH.md: f32-in MFMA dense peak
 BF16_MFMA_PEAK_TFLOPS = 2500.0    # MI355X_MICROARCH.md: bf16 / f16 MFMA dense peak (no sparsity)
 HBM_PEAK_GBS = 8000.0             # MI355X_MICROARCH.md: HBM3E spec peak
 SR, SECONDS = 16000, 4
-PROFILE_STATS = os.path.join(ROOT, "profiles", "r5_bench_kernel_stats.csv")
+PROFILE_STATS = os.path.join(ROOT, "profiles", "r6_bench_kernel_stats.csv")
+# the ConvSTFT / iSTFT kernels of the STFT rooflines (se_stft_fwd: the register-radix form
+# for nfft 640)
+STFT_KERNELS = (("stft_fwd", "stft_fwd_rg_kernel"), ("istft_fwd", "istft_fwd_wv_kernel"),
+                ("istft_bwd", "istft_bwd_wv_kernel"))
 
 # OpTimer tag -> (kernel instantiation as rocprof names it, launches per call, description).
 # The decoder's joined passes are one launch of one instantiation per call (the data-grad of
@@ -178,6 +182,25 @@ def cpu_baseline(batch, steps, warmup, budget_s):
                       + (f" (stopped at the {budget_s:.0f} s cap; {steps} planned)" if done < steps else ""),
             "cpu_model": _cpu_model(), "affinity_cpus": affinity, "seconds": round(dt, 2),
             "warmup_seconds": round(t_warm, 2)}
+
+
+_ROCTX: list = []
+
+
+def _roctx():
+    """librocprofiler-sdk-roctx when SEHIP_ROCTX_REGIONS=1: the uninstrumented timed steps run
+    inside a roctx range "timed", which `rocprofv3 --marker-trace` records beside the kernel
+    trace; tools/region_stats.py keeps the kernels inside it (no data generation, model
+    construction or warm-up in the kernel statistics)."""
+    if os.environ.get("SEHIP_ROCTX_REGIONS") != "1":
+        return None
+    if not _ROCTX:
+        import ctypes
+        lib = ctypes.CDLL("/opt/rocm/lib/librocprofiler-sdk-roctx.so")
+        lib.roctxRangePushA.argtypes, lib.roctxRangePushA.restype = [ctypes.c_char_p], ctypes.c_int
+        lib.roctxRangePop.argtypes, lib.roctxRangePop.restype = [], ctypes.c_int
+        _ROCTX.append(lib)
+    return _ROCTX[0]
 
 
 def _rccl_version():
@@ -340,6 +363,9 @@ def run(args):
             dist.barrier()
         torch.cuda.synchronize()
         SF.set_op_timer(timer)
+        rt = _roctx() if timer is None else None
+        if rt is not None:
+            rt.roctxRangePushA(b"timed")
         t0 = time.perf_counter()
         marks = []
         for i in range(steps):
@@ -348,6 +374,8 @@ def run(args):
             if trace:
                 marks.append(time.perf_counter() - t0)
         torch.cuda.synchronize()
+        if rt is not None:
+            rt.roctxRangePop()
         if trace:   # host enqueue timeline (SEHIP_BENCH_TRACE=1): where the host blocked
             _note("enqueue ms: " + " ".join(f"{1e3 * m:.0f}" for m in marks)
                   + f" | sync {1e3 * (time.perf_counter() - t0):.0f}")
@@ -506,8 +534,7 @@ def run(args):
             wg = {k: v for k, v in kern_iso.items() if "wgrad" in k}
             if wg:
                 out["roofline_side_stream_isolated"] = _roofline(wg, args.steps, side_ok=True)
-        for name, kname in (("stft_fwd", "stft_fwd_wv_kernel"), ("istft_fwd", "istft_fwd_wv_kernel"),
-                            ("istft_bwd", "istft_bwd_wv_kernel")):
+        for name, kname in STFT_KERNELS:
             st = kern.get(name)
             if not (st and name in bursts):
                 continue

@@ -25,7 +25,7 @@ def test_roofline_kernels_are_in_the_committed_profiles():
         stats = {b._kernel_key(r["Name"]) for r in csv.DictReader(f)}
     names = [b.KERNEL_OF[t][0] for t in ("conv_data_joined_f16x3", "conv_fwd_joined_f16x3",
                                          "conv_wgrad_joined_f16x3")]
-    names += ["stft_fwd_wv_kernel", "istft_fwd_wv_kernel", "istft_bwd_wv_kernel"]
+    names += [k for _, k in b.STFT_KERNELS]
     for n in names:
         assert n in pmc, n
         assert n in stats or any(s.split("<")[0] == n for s in stats), n

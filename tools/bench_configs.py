@@ -25,14 +25,17 @@ _ROCTX = []
 
 
 def _roctx():
-    """roctxProfilerResume / Pause (librocprofiler-sdk-roctx) when SEHIP_ROCTX_REGIONS=1: under
-    `rocprofv3 --selected-regions` only the timed iterations are traced (no data generation,
-    model construction or warm-up in the kernel statistics)."""
+    """librocprofiler-sdk-roctx when SEHIP_ROCTX_REGIONS=1: the timed iterations run inside a
+    roctx range "timed", which `rocprofv3 --marker-trace` records beside the kernel trace;
+    tools/region_stats.py keeps the kernels inside it (no data generation, model construction
+    or warm-up in the kernel statistics)."""
     if not _ROCTX:
         lib = None
         if os.environ.get("SEHIP_ROCTX_REGIONS") == "1":
             import ctypes
             lib = ctypes.CDLL("/opt/rocm/lib/librocprofiler-sdk-roctx.so")
+            lib.roctxRangePushA.argtypes, lib.roctxRangePushA.restype = [ctypes.c_char_p], ctypes.c_int
+            lib.roctxRangePop.argtypes, lib.roctxRangePop.restype = [], ctypes.c_int
         _ROCTX.append(lib)
     return _ROCTX[0]
 
@@ -43,14 +46,14 @@ def timeit(fn, iters, warm=2):
     torch.cuda.synchronize()
     rt = _roctx()
     if rt is not None:
-        rt.roctxProfilerResume(0)
+        rt.roctxRangePushA(b"timed")
     t0 = time.perf_counter()
     for _ in range(iters):
         fn()
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / iters
     if rt is not None:
-        rt.roctxProfilerPause(0)
+        rt.roctxRangePop()
     return dt
 
 
