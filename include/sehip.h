@@ -28,7 +28,9 @@
 extern "C" {
 #endif
 
-#define SEHIP_ABI_VERSION 10  /* 10: 16-bit storage and row biases in se_gemm (the Linear layers), se_bias_grad,
+#define SEHIP_ABI_VERSION 11  /* 11: se_cbn_bwd_ccbam (the CCBAM gate's input gradient formed inside the
+                                 encoder CBN backward);
+                                 10: 16-bit storage and row biases in se_gemm (the Linear layers), se_bias_grad,
                                  se_copy_strided, the CARN mask / attention-gate / clamp passes, the
                                  ComplexLSTM re/im combine, long-form chunking, 16-bit SI-SNR / clip / AdamW,
                                  the polar masks' leading zero rows;
@@ -330,6 +332,21 @@ int se_cbn_bwd2(const void* gy, const void* gy2, const void* x, void* dx,
                 const float* save, void* const* dparams, int training,
                 int act, float slope, float* dx_amax, const void* prelu_w, void* dprelu_w,
                 int dtype, void* ws, size_t ws_bytes, void* stream);
+
+/* ABI 11. Backward of a forked output whose second consumer is FRCRN's CCBAM skip gate
+ * (frcrn.py:70-75, 93-95; ccbam.py:28-106): dL/dy = gy + the gate's input gradient, formed
+ * on the fly in both passes from the gate's parts instead of being written by a separate
+ * pass (se_ccbam_bwd_dx) and read back. At (b, channel ch = h C/2 + cc, position i):
+ *   gy2 = (g + dP[b, 2h, i] / (C/2) + [idx[b, h, i] == cc] dP[b, 2h + 1, i]) ca[b, ch]
+ *         + dmean[b, ch] / HW + [amax[b, ch] == i] dmax[b, ch]
+ * with g_gate [B, C, HW] the gate's output gradient and dP / idx / ca / dmean / dmax / amax
+ * as se_ccbam_bwd_dx takes them. fp32; LeakyReLU / ReLU / none (no PReLU). Otherwise as
+ * se_cbn_bwd (workspace se_cbn_workspace_size). Replaces se_ccbam_bwd_dx + se_cbn_bwd2. */
+int se_cbn_bwd_ccbam(const float* gy, const float* g_gate, const float* dP, const short* idx,
+                     const float* ca, const float* dmean, const float* dmax, const int* amax,
+                     const float* x, float* dx, int B, int C, int HW, const float* const* params,
+                     const float* save, float* const* dparams, int training, int act, float slope,
+                     float* dx_amax, void* ws, size_t ws_bytes, void* stream);
 
 /* Output head fused into the last ComplexBatchNorm2d (frcrn.py:115, 140-144):
  * FRCRN's final_conv = nn.Conv2d(C, 2, kernel_size=(1, 2), bias=False) applied

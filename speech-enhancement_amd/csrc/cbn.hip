@@ -337,6 +337,32 @@ __device__ __forceinline__ float head_gy(const HeadG& g, const float* wc, int C)
 // coef layout per channel (16 floats): ZTrr ZTri ZTir ZTii gbr gbi Grr Gri Gii Mr Mi Br Bi pad
 constexpr int kCoef = 16;
 
+// SRC 3 (se_cbn_bwd_ccbam): dL/dy = gy + the input gradient of the CCBAM gate that reads
+// the forked output (FRCRN's encoder skip, frcrn.py:70-75 + ccbam.py:95-106), formed on the
+// fly from the gate's parts instead of being written by ccbam.hip's bwd_dx_kernel and read
+// back: at (b, channel ch = h Ch + cc, position i)
+//   gy2 = (g + dP[b, 2h, i] / Ch + [idx[b, h, i] == cc] dP[b, 2h + 1, i]) ca[b, ch]
+//         + dmean[b, ch] / HW + [amax[b, ch] == i] dmax[b, ch]
+// (bwd_dx_kernel's expression, term for term). fp32 only.
+struct CcbamDx {
+  const float* g;       // [B, C, HW] the gate's output gradient
+  const float* dP;      // [B, 4, HW] pooled-map gradient (avg_re, max_re, avg_im, max_im)
+  const short* idx;     // [B, 2, HW] channel argmax per half
+  const float* ca;      // [B, C] channel gate
+  const float* dmean;   // [B, C]
+  const float* dmax;    // [B, C]
+  const int* amax;      // [B, C] HW argmax
+};
+struct CcbRow { float ca, mean, mx; int am; };   // one (b, channel) plane's constants
+__device__ __forceinline__ CcbRow ccb_row(const CcbamDx& cd, long long bc, float invhw) {
+  return CcbRow{cd.ca[bc], cd.dmean[bc] * invhw, cd.dmax[bc], cd.amax[bc]};
+}
+// gy2 of plane h at position i, given the position's pooled-map terms
+__device__ __forceinline__ float ccb_dx(float g, float pa, float pm, int pi, int cc, const CcbRow& r, int i) {
+  const float gx = g + pa + (pi == cc ? pm : 0.f);
+  return gx * r.ca + r.mean + (r.am == i ? r.mx : 0.f);
+}
+
 // One wave per channel, as cbn_finalize_kernel; the bound of max |dx| goes to
 // *dx_amax by atomicMax (zeroed by the backward moments pass).
 // HEAD: part holds the head's 8 weight-grad sums after the 6 moments (stride
@@ -464,8 +490,9 @@ __global__ void __launch_bounds__(kThreads)
 cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, const T* __restrict__ x,
                          T* __restrict__ dx, int C, int HW, int seg_len, int act, float slope,
                          const double* part, const float* ext, int P, double count, const float* save, Ptr5 params,
-                         int affine, MPtr5 dparams, int has_dparams, int training, float* dx_amax) {
-  static_assert(SRC == 0 || SRC == 1, "gy or gy + gy2");
+                         int affine, MPtr5 dparams, int has_dparams, int training, float* dx_amax, CcbamDx cd) {
+  static_assert(SRC == 0 || SRC == 1 || SRC == 3, "gy, gy + gy2, or gy + the CCBAM gate's input gradient");
+  static_assert(SRC != 3 || sizeof(T) == 4, "the CCBAM path is fp32");
   __shared__ float k[kCoef];
   const int Cc = C / 2, c = blockIdx.x, b = blockIdx.y;
   const int hw0 = blockIdx.z * seg_len, hw1 = min(HW, hw0 + seg_len);   // this workgroup's segment
@@ -479,6 +506,20 @@ cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, co
   const float br = k[11], bi = k[12];
   const float neg = act_neg(act, slope);
   const long long offr = ((long long)b * C + c) * HW, offi = ((long long)b * C + Cc + c) * HW;
+  CcbRow rr{}, ri{};
+  const float* dPb = nullptr;
+  const short* ib = nullptr;
+  const float cinv = 1.f / (float)Cc, invhw = 1.f / (float)HW;
+  if constexpr (SRC == 3) {
+    rr = ccb_row(cd, (long long)b * C + c, invhw);
+    ri = ccb_row(cd, (long long)b * C + Cc + c, invhw);
+    dPb = cd.dP + (long long)b * 4 * HW;
+    ib = cd.idx + (long long)b * 2 * HW;
+  }
+  auto gate = [&](long long off, int j, int h) __attribute__((always_inline)) -> float {   // SRC 3's gy2
+    return ccb_dx(cd.g[off + j], dPb[(2 * h) * HW + j] * cinv, dPb[(2 * h + 1) * HW + j], ib[h * HW + j], c,
+                  h ? ri : rr, j);
+  };
   auto one = [&](float fxr, float fxi, float fgr, float fgi, float& dr, float& di) __attribute__((always_inline)) {
     const float xr = fxr - mr, xi = fxi - mi;
     const float zr = a00 * xr + a10 * xi + br, zi = a01 * xr + a11 * xi + bi;   // = forward pre-activation
@@ -501,6 +542,19 @@ cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, co
         if (SRC == 1) {
           gr4[u] += ld4(gy2 + offr + i);
           gi4[u] += ld4(gy2 + offi + i);
+        }
+        if constexpr (SRC == 3) {   // the gate's parts as 16-B / 8-B loads
+          const f32x4v g0 = ld4(cd.g + offr + i), g1 = ld4(cd.g + offi + i);
+          const f32x4v pa0 = ld4(dPb + i), pm0 = ld4(dPb + HW + i);
+          const f32x4v pa1 = ld4(dPb + 2 * HW + i), pm1 = ld4(dPb + 3 * HW + i);
+          typedef short s16x4v __attribute__((ext_vector_type(4)));
+          const s16x4v i0 = *reinterpret_cast<const s16x4v*>(ib + i);
+          const s16x4v i1 = *reinterpret_cast<const s16x4v*>(ib + HW + i);
+#pragma unroll
+          for (int l = 0; l < 4; ++l) {
+            gr4[u][l] += ccb_dx(g0[l], pa0[l] * cinv, pm0[l], i0[l], c, rr, i + l);
+            gi4[u][l] += ccb_dx(g1[l], pa1[l] * cinv, pm1[l], i1[l], c, ri, i + l);
+          }
         }
       }
 #pragma unroll
@@ -531,6 +585,10 @@ cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, co
         fxi[u] = (float)x[offi + j];
         fgr[u] = SRC == 1 ? (float)gy[offr + j] + (float)gy2[offr + j] : (float)gy[offr + j];
         fgi[u] = SRC == 1 ? (float)gy[offi + j] + (float)gy2[offi + j] : (float)gy[offi + j];
+        if constexpr (SRC == 3) {
+          fgr[u] += gate(offr, j, 0);
+          fgi[u] += gate(offi, j, 1);
+        }
       }
 #pragma unroll
       for (int u = 0; u < U; ++u) {
@@ -558,9 +616,9 @@ __global__ void __launch_bounds__(kThreads)
 cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
                        const T* __restrict__ x, int B, int C, int HW, int P,
                        const float* __restrict__ save, int act, float slope, double* part, float* ext,
-                       float* dx_amax, HeadArgs hd, const T* pw) {
+                       float* dx_amax, HeadArgs hd, const T* pw, CcbamDx cd) {
   static_assert(!PR || SRC != 2, "no PReLU on the head path");
-  static_assert(SRC != 2 || sizeof(T) == 4, "the head path is fp32");
+  static_assert((SRC != 2 && SRC != 3) || sizeof(T) == 4, "the head and CCBAM paths are fp32");
   constexpr int NS = SRC == 2 ? 6 + kHeadNS : (PR ? 7 : 6);
   if (PR) slope = (float)pw[0];
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
@@ -629,6 +687,24 @@ cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
       }
     } else {
       const HeadG none{};
+      // SRC 3: the row's gate constants and pooled-map rows
+      CcbRow rr{}, ri{};
+      const float* dPb = nullptr;
+      const short* ib = nullptr;
+      const float inv = 1.f / (float)Cc, invhw = 1.f / (float)HW;
+      if constexpr (SRC == 3) {
+        rr = ccb_row(cd, (long long)b * C + c, invhw);
+        ri = ccb_row(cd, (long long)b * C + Cc + c, invhw);
+        dPb = cd.dP + (long long)b * 4 * HW;
+        ib = cd.idx + (long long)b * 2 * HW;
+      }
+      auto dy = [&](long long off, int j, int h) __attribute__((always_inline)) -> float {
+        if constexpr (SRC == 1) return (float)gy[off + j] + (float)gy2[off + j];
+        if constexpr (SRC == 3)
+          return (float)gy[off + j] + ccb_dx(cd.g[off + j], dPb[(2 * h) * HW + j] * inv, dPb[(2 * h + 1) * HW + j],
+                                             ib[h * HW + j], c, h ? ri : rr, j);
+        return (float)gy[off + j];
+      };
       constexpr int U = 4;   // loads of four positions in flight; the sums keep their order
       for (; i + (U - 1) * kThreads < i1; i += U * kThreads) {
         float fr[U], fm[U], dr[U], dm[U];
@@ -637,17 +713,13 @@ cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
           const int j = i + u * kThreads;
           fr[u] = (float)x[offr + j];
           fm[u] = (float)x[offi + j];
-          dr[u] = SRC == 1 ? (float)gy[offr + j] + (float)gy2[offr + j] : (float)gy[offr + j];
-          dm[u] = SRC == 1 ? (float)gy[offi + j] + (float)gy2[offi + j] : (float)gy[offi + j];
+          dr[u] = dy(offr, j, 0);
+          dm[u] = dy(offi, j, 1);
         }
 #pragma unroll
         for (int u = 0; u < U; ++u) body(fr[u], fm[u], dr[u], dm[u], none);
       }
-      for (; i < i1; i += kThreads) {
-        const float dyr = SRC == 1 ? (float)gy[offr + i] + (float)gy2[offr + i] : (float)gy[offr + i];
-        const float dyi = SRC == 1 ? (float)gy[offi + i] + (float)gy2[offi + i] : (float)gy[offi + i];
-        body((float)x[offr + i], (float)x[offi + i], dyr, dyi, none);
-      }
+      for (; i < i1; i += kThreads) body((float)x[offr + i], (float)x[offi + i], dy(offr, i, 0), dy(offi, i, 1), none);
     }
   }
   block_reduce_store<NS>(v, part + ((long long)c * P + p) * NS);
@@ -1226,8 +1298,8 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
                  int B, int C, int HW, const void* const* params, const float* save, void* const* dparams,
                  int training, int act, float slope, float* dx_amax, float* dwh, void* ws, size_t ws_bytes,
                  void* stream, const FirstConv* fc = nullptr, int fc_w = 0, const T* pw = nullptr,
-                 T* dpw = nullptr) {
-  const int ns = src == 2 ? 6 + kHeadNS : 7;
+                 T* dpw = nullptr, const CcbamDx& cd = CcbamDx{}) {
+  const int ns = src == 2 ? 6 + kHeadNS : 7;   // (src 3: the 6 + 1 layout of src 0 / 1)
   if (ws_bytes < ws_bytes_ns(B, C, HW, ns) || !ws) return SE_E_WORKSPACE;
   if (pw && (src == 2 || fc || !dpw)) return SE_E_ARG;
   hipStream_t st = se::as_stream(stream);
@@ -1247,23 +1319,30 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   if constexpr (sizeof(T) == 4) {
     if (src == 2)
       hipLaunchKernelGGL((cbn_bwd_moments_kernel<2, float>), mg, mb, 0, st, (const float*)gy, (const float*)gy2,
-                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr);
+                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr,
+                         CcbamDx{});
+  }
+  if constexpr (sizeof(T) == 4) {
+    if (src == 3)
+      hipLaunchKernelGGL((cbn_bwd_moments_kernel<3, float>), mg, mb, 0, st, (const float*)gy, (const float*)nullptr,
+                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr, cd);
   }
   if (src == 1 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw);
+                       slope, part, ext, xa, hd, pw, CcbamDx{});
   else if (src == 1)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw);
+                       part, ext, xa, hd, pw, CcbamDx{});
   else if (src == 0 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw);
+                       slope, part, ext, xa, hd, pw, CcbamDx{});
   else if (src == 0)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw);
+                       part, ext, xa, hd, pw, CcbamDx{});
   SE_LAUNCH_CHECK();
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
-  if (SE_CBN_APPLY_FIN && (src == 0 || src == 1) && !pr && !fc) {
+  if (src == 3 && (pr || fc || !SE_CBN_APPLY_FIN)) return SE_E_UNSUPPORTED;
+  if (SE_CBN_APPLY_FIN && (src == 0 || src == 1 || src == 3) && !pr && !fc) {
     const bool v4 = HW % 4 == 0;
     // few channels (CCBAM's one-channel spatial branch: Cc x B = 64 workgroups): each plane
     // split into segments of whole 2048-element strides, up to ~1024 workgroups
@@ -1274,8 +1353,13 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
 #define SE_AF(S, V)                                                                                              \
   hipLaunchKernelGGL((cbn_bwd_apply_fin_kernel<S, T, V>), dim3(Cc, B, ns), mb, 0, st, gy, gy2, x, dx, C, HW, seg_len, \
                      act, slope, part, ext, P, (double)B * HW, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0,        \
-                     training, xa)
-    if (src == 1 && v4) SE_AF(1, true);
+                     training, xa, cd)
+    if constexpr (sizeof(T) == 4) {
+      if (src == 3 && v4) SE_AF(3, true);
+      else if (src == 3) SE_AF(3, false);
+    }
+    if (src == 3) {
+    } else if (src == 1 && v4) SE_AF(1, true);
     else if (src == 1) SE_AF(1, false);
     else if (v4) SE_AF(0, true);
     else SE_AF(0, false);
@@ -1396,6 +1480,23 @@ extern "C" int se_cbn_bwd2(const void* gy, const void* gy2, const void* x, void*
   if (!gy || !gy2 || !bwd_args_ok(x, dx, save, B, C, HW) || !act_ok(act, prelu_w)) return SE_E_ARG;
   return cbn_bwd_dtype(1, gy, gy2, x, dx, B, C, HW, params, save, dparams, training, act, slope, dx_amax,
                        prelu_w, dprelu_w, dtype, ws, ws_bytes, stream);
+}
+
+// Forked output whose second consumer is FRCRN's CCBAM skip gate: gy + the gate's input
+// gradient formed inside both passes from its parts (CcbamDx), so the gate's dx tensor is
+// never written (ccbam.hip bwd_dx_kernel: one read and one write of the skip per layer).
+extern "C" int se_cbn_bwd_ccbam(const float* gy, const float* g_gate, const float* dP, const short* idx,
+                                const float* ca, const float* dmean, const float* dmax, const int* amax,
+                                const float* x, float* dx, int B, int C, int HW, const float* const* params,
+                                const float* save, float* const* dparams, int training, int act, float slope,
+                                float* dx_amax, void* ws, size_t ws_bytes, void* stream) {
+  if (!gy || !g_gate || !dP || !idx || !ca || !dmean || !dmax || !amax) return SE_E_ARG;
+  if (!bwd_args_ok(x, dx, save, B, C, HW) || act < 0 || act > 2) return SE_E_ARG;
+  if (C / 2 > 32767) return SE_E_SHAPE;
+  const CcbamDx cd{g_gate, dP, idx, ca, dmean, dmax, amax};
+  return cbn_bwd_impl<float>(3, gy, nullptr, HeadArgs{}, x, dx, B, C, HW, (const void* const*)params, save,
+                             (void* const*)dparams, training, act, slope, dx_amax, nullptr, ws, ws_bytes, stream,
+                             nullptr, 0, nullptr, nullptr, cd);
 }
 
 extern "C" int se_cbn_head_bwd(const float* gout, const float* x, float* dx, int B, int C, int H, int W,

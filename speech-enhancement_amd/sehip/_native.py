@@ -60,7 +60,7 @@ class GemmDesc(ctypes.Structure):
 
 
 _P = c_void_p
-ABI_VERSION = 10   # SEHIP_ABI_VERSION (include/sehip.h)
+ABI_VERSION = 11   # SEHIP_ABI_VERSION (include/sehip.h)
 CBN_SAVE_FLOATS = 20   # SE_CBN_SAVE_FLOATS (include/sehip.h)
 _PP = ctypes.POINTER(c_void_p)   # host array of device pointers
 _SIGNATURES = {
@@ -96,6 +96,8 @@ _SIGNATURES = {
                            c_int, _P, c_size_t, _P]),
     "se_cbn_bwd2": (c_int, [_P, _P, _P, _P, c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P, _P,
                             c_int, _P, c_size_t, _P]),
+    "se_cbn_bwd_ccbam": (c_int, [_P] * 10 + [c_int, c_int, c_int, _PP, _P, _PP, c_int, c_int, c_float, _P, _P,
+                                               c_size_t, _P]),
     "se_cbn_head_workspace_size": (c_size_t, [c_int, c_int, c_int]),
     "se_cbn_first_conv_workspace_size": (c_size_t, [c_int] * 6),
     "se_cbn_bwd_first_conv": (c_int, [_P, _P, _P] + [c_int] * 4 + [_PP, _P, _PP, c_int, c_int, c_float, _P, _P,

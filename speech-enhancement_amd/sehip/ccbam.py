@@ -125,6 +125,13 @@ class _CCBAMFn(torch.autograd.Function):
         HW = H * W
         lib, st, dev = N.lib(), N.stream_of(x), x.device
         need_grad = any(ctx.needs_input_grad)
+        # SEHIP_CCBAM_DEFER_DX=1 and the input a forked ComplexBatchNorm2d output (FRCRN's
+        # encoder skip): the input gradient is left to that CBN's backward to form
+        # (se_cbn_bwd_ccbam), never written here. Two skip-sized passes fewer per gate, but the
+        # main-stream CBN backward grows by what the side stream saves: the step measured
+        # neutral (-0.3 %, profiles/ab/r6_ccbam_defer_dx_ab.log), so it is off by default.
+        ctx.defer_dx = bool(getattr(x, "_sehip_cbn_fork", False)) and x.dtype == torch.float32 and \
+            os.environ.get("SEHIP_CCBAM_DEFER_DX", "0") == "1"
         cab, sab = mod.channel_attention_branch, mod.spatial_attention_branch
         mean = torch.empty(B, C, device=dev)
         mx = torch.empty(B, C, device=dev)
@@ -205,12 +212,15 @@ class _CCBAMFn(torch.autograd.Function):
         else:
             gc = torch.autograd.grad(ca, [pooled] + ch, dca, allow_unused=True)
             dmean, dmax = (t.contiguous() for t in torch.chunk(gc[0], 2, dim=0))
-        dx = torch.empty_like(x)
-        _call(lib.se_ccbam_bwd_dx, "se_ccbam_bwd_dx", gout.data_ptr(), dP.data_ptr(), idx.data_ptr(),
-              ca.data_ptr(), dmean.data_ptr(), dmax.data_ptr(), amax.data_ptr(), dx.data_ptr(),
-              B, C, HW, st)
-        if t0 is not None:   # algorithmic bytes: gout and x read once, dx written once
-            F._TIMER.end("ccbam_bwd", t0, 0.0, 3.0 * x.numel() * x.element_size())
+        if ctx.defer_dx:   # formed inside the forked CBN's backward (functional.ccbam_dx_defer)
+            dx = F.ccbam_dx_defer(x, (gout, dP, idx, ca, dmean, dmax, amax))
+        else:
+            dx = torch.empty_like(x)
+            _call(lib.se_ccbam_bwd_dx, "se_ccbam_bwd_dx", gout.data_ptr(), dP.data_ptr(), idx.data_ptr(),
+                  ca.data_ptr(), dmean.data_ptr(), dmax.data_ptr(), amax.data_ptr(), dx.data_ptr(),
+                  B, C, HW, st)
+        if t0 is not None:   # algorithmic bytes: gout and x read once (+ dx written once)
+            F._TIMER.end("ccbam_bwd", t0, 0.0, (2.0 if ctx.defer_dx else 3.0) * x.numel() * x.element_size())
         grads = {id(p): g for p, g in zip(sp, gs[1:])}
         grads.update({id(p): g for p, g in zip(ch, gc[1:])})
         del ctx.graphs

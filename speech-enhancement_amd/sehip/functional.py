@@ -716,12 +716,15 @@ class _ComplexBN(torch.autograd.Function):
     def backward(ctx, gy, gy2=None):
         x, save, prelu, *params = ctx.saved_tensors
         training, act, slope, affine = ctx.cfg
+        gate = _ccbam_dx_parts(gy2)   # the CCBAM gate's deferred input gradient (ccbam.py)
+        if gate is not None and (gy is None or prelu is not None or x.dtype != torch.float32):
+            gy2, gate = ccbam_dx_materialize(gate), None   # no fused form: write it as a tensor
         if gy is None:
             gy, gy2 = gy2, None
         if gy is None:
             return (None,) * 16
         gy = gy.contiguous()
-        gy2 = gy2.contiguous() if gy2 is not None else None
+        gy2 = gy2.contiguous() if gy2 is not None and gate is None else None
         dt = N.dtype_code(x)
         b, c = x.shape[:2]
         hw = x[0, 0].numel()
@@ -732,7 +735,18 @@ class _ComplexBN(torch.autograd.Function):
         ws = _workspace(lib.se_cbn_workspace_size(b, c, hw), x.device)
         dxa = new_amax(x.device) if training and dt == 0 else None   # bound of max |dx| (the conv's dy)
         t0 = _TIMER.begin() if _TIMER else None
-        if gy2 is None:
+        if gate is not None:
+            g, dP, idx, ca, dmean, dmax, amax = gate
+            N.check(lib.se_cbn_bwd_ccbam(gy.data_ptr(), g.data_ptr(), dP.data_ptr(), idx.data_ptr(), ca.data_ptr(),
+                                         dmean.data_ptr(), dmax.data_ptr(), amax.data_ptr(), x.data_ptr(),
+                                         dx.data_ptr(), b, c, hw, N.ptr_array(params if affine else None),
+                                         save.data_ptr(), N.ptr_array(dparams), training, act, slope, N.ptr(dxa),
+                                         ws.data_ptr(), ws.numel(), N.stream_of(gy)), "se_cbn_bwd_ccbam")
+            cur = torch.cuda.current_stream(gy.device)
+            for t in gate:   # made on the gate's stream, read here: freed only after this stream's use
+                t.record_stream(cur)
+            CCBAM_DX_FUSED[0] += 1
+        elif gy2 is None:
             N.check(lib.se_cbn_bwd(gy.data_ptr(), None, x.data_ptr(), dx.data_ptr(), b, c, hw,
                                    N.ptr_array(params if affine else None), save.data_ptr(),
                                    N.ptr_array(dparams), training, act, slope, N.ptr(dxa), N.ptr(prelu),
@@ -746,9 +760,48 @@ class _ComplexBN(torch.autograd.Function):
         if dxa is not None:
             amax_put(dx, dxa)
         if t0 is not None:   # (gy [, gy2], x) read twice + dx written
-            _TIMER.end("cbn_bwd", t0, 0.0, x.element_size() * x.numel() * (5 if gy2 is None else 7))
+            _TIMER.end("cbn_bwd", t0, 0.0, x.element_size() * x.numel() * (5 if gy2 is None and gate is None else 7))
         g = dparams or [None] * 5
         return (dx, *g, None, None, None, None, None, None, None, None, dprelu)
+
+
+# The CCBAM gate's input gradient, deferred (ccbam.py): its backward returns a stand-in of
+# the input's shape (one element, expanded) and leaves the parts here, keyed by the stand-in's
+# storage; the forked CBN backward that receives it forms the gradient inside its own passes
+# (se_cbn_bwd_ccbam) instead of reading a written tensor.
+_CCBAM_DX: dict = {}
+CCBAM_DX_FUSED = [0]   # backward passes that took the deferred form (tests)
+
+
+def ccbam_dx_defer(x, parts):
+    """A stand-in gradient for x whose value is the CCBAM input gradient given by parts =
+    (g, dP, idx, ca, dmean, dmax, amax) (se_ccbam_bwd_dx's operands)."""
+    if len(_CCBAM_DX) > 64:   # stand-ins of graphs freed before their backward reached the CBN
+        _CCBAM_DX.clear()
+    tok = torch.empty(1, device=x.device, dtype=x.dtype).expand(x.shape)
+    _CCBAM_DX[tok.data_ptr()] = (tok, parts)
+    return tok
+
+
+def _ccbam_dx_parts(g):
+    if g is None or g.dim() == 0 or any(st != 0 for st in g.stride()):
+        return None
+    ent = _CCBAM_DX.get(g.data_ptr())
+    if ent is None or ent[0].shape != g.shape:
+        return None
+    del _CCBAM_DX[g.data_ptr()]
+    return ent[1]
+
+
+def ccbam_dx_materialize(parts):
+    """The deferred CCBAM input gradient written as a tensor (se_ccbam_bwd_dx)."""
+    g, dP, idx, ca, dmean, dmax, amax = parts
+    B, C = ca.shape
+    dx = torch.empty_like(g)
+    N.check(N.lib().se_ccbam_bwd_dx(g.data_ptr(), dP.data_ptr(), idx.data_ptr(), ca.data_ptr(), dmean.data_ptr(),
+                                    dmax.data_ptr(), amax.data_ptr(), dx.data_ptr(), B, C, g[0, 0].numel(),
+                                    N.stream_of(g)), "se_ccbam_bwd_dx")
+    return dx
 
 
 def complex_batch_norm(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
@@ -758,8 +811,11 @@ def complex_batch_norm(x, wrr, wri, wii, br, bi, running, nbt, training, eps, mo
     prelu: the weight of a one-parameter nn.PReLU applied after the norm (fused).
     fork=True returns (y, alias of y) for two consumers: their two gradients are summed inside
     the backward kernels (se_cbn_bwd2) instead of by autograd's accumulation add."""
-    return _ComplexBN.apply(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
-                            act, slope, fork, prelu)
+    out = _ComplexBN.apply(x, wrr, wri, wii, br, bi, running, nbt, training, eps, momentum,
+                           act, slope, fork, prelu)
+    if fork and isinstance(out, tuple):
+        out[1]._sehip_cbn_fork = True   # a CCBAM gate reading it may defer its input gradient
+    return out
 
 
 class _FirstBlock(torch.autograd.Function):

@@ -190,3 +190,33 @@ def test_spatial_conv_stencil_bit_identical(gpu_device, monkeypatch, shape):
                                      torch.cat([torch.cat([wr, -wi], 1), torch.cat([wi, wr], 1)], 0).double().cpu(),
                                      padding=3)
     assert ((outs[0][0].double().cpu() - ref).norm() / ref.norm()).item() < 1e-6
+
+
+@pytest.mark.parametrize("overlap", ["0", "1"])
+def test_deferred_gate_input_grad_bit_identical(gpu_device, monkeypatch, overlap):
+    """FRCRN's CCBAM gates read forked encoder outputs: their input gradient is formed inside
+    the forked CBN backward (se_cbn_bwd_ccbam, ABI 11) instead of being written by
+    se_ccbam_bwd_dx and read back. Two train steps give bit-identical losses and parameters
+    with the deferral on and off (the kernel forms bwd_dx_kernel's expression term for term),
+    with the gates inline and on the side stream; the five forked-CBN gates (encoder layers
+    1-5; layer 0's output comes from the first-block op) take the deferred form."""
+    import paramfill
+    from sehip import functional as F
+    from sehip import models as M
+    from sehip.train import make_optimizer, train_step
+    monkeypatch.setenv("SEHIP_OVERLAP", overlap)
+    noisy, clean = paramfill.structured_pair(2, 16000, seed=8)
+    x, c = torch.from_numpy(noisy).cuda(), torch.from_numpy(clean).cuda()
+    res = []
+    for defer in ("0", "1"):
+        monkeypatch.setenv("SEHIP_CCBAM_DEFER_DX", defer)
+        m = paramfill.fill_(M.FRCRN(), seed=9).cuda().train()
+        opt = make_optimizer(m)
+        n0 = F.CCBAM_DX_FUSED[0]
+        losses = [train_step(m, opt, x, c) for _ in range(2)]
+        torch.cuda.synchronize()
+        assert F.CCBAM_DX_FUSED[0] - n0 == (10 if defer == "1" else 0)
+        res.append(losses + [p.detach().clone() for p in m.parameters()])
+    assert not F._CCBAM_DX
+    for a, b in zip(*res):
+        assert torch.equal(a, b)
