@@ -1438,6 +1438,10 @@ static bool env_flag_off(const char* name) {
   const char* e = std::getenv(name);
   return e && e[0] == '0';
 }
+static bool env_flag_on(const char* name) {
+  const char* e = std::getenv(name);
+  return e && e[0] == '1';
+}
 // The weight image of a gather pass: per stride-phase class the GEMM weight
 // tiles Wp (Kp x ldw, in the layout of the kernel the pass runs) and the tap
 // table ktab, laid out 256-byte aligned from base. Built by the pass itself in
@@ -1999,6 +2003,13 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
     const dim3 blk(2 * kThreads);
     if (jn) hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, true, true, 2, false, 0, 2>), grid, blk, 0, st, a);
     else hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 2, false, 0, 2>), grid, blk, 0, st, a);
+  } else if (f16 && w.Np == 128 && tu && !jn && w.c.Kp % 256 == 0 && env_flag_on("SEHIP_WGRAD_K256")) {
+    // 256 x 128 tiles, 8 waves of 64 x 64 (the encoder's N = 128): a staged dy row serves two
+    // taps' 256 k rows. PMC 3.16 -> 2.39 GB per encoder launch, but 3.62 -> 3.80 ms alone and
+    // 10.5 -> 12.0 ms per step (one register staging set at one workgroup per CU): opt-in
+    // (profiles/ab/r6_wgrad_256x128_ab.log)
+    const dim3 grid = x3_wgrad_grid(a, w, 1, 2);
+    hipLaunchKernelGGL((wgrad_x3_kernel<true, 3, false, true, 1, false, 0, 2>), grid, dim3(2 * kThreads), 0, st, a);
   } else if (f16 && w.Np % 256 == 0) {   // 128 x 256 tiles, 8 waves
     const dim3 grid = x3_wgrad_grid(a, w, 2);
     const dim3 blk(2 * kThreads);

@@ -541,7 +541,9 @@ __device__ __forceinline__ int wx3_off(int s, int ch) {   // byte offset of chun
 // SD: storage type of X / D (as gather_x3_kernel; 16-bit with the one-term MFMA)
 // KB: 128-row G blocks per workgroup (KB = 2 with NB = 2: 256 k x 256 n tiles, 8 waves of
 // 128 x 64, one register staging set; a staged G row serves 256 columns and a staged D
-// row 256 k rows, a third fewer loads and splits per MFMA than 128 x 256)
+// row 256 k rows, a third fewer loads and splits per MFMA than 128 x 256. KB = 2 with
+// NB = 1 (round 6): 256 k x 128 n, 8 waves of 64 x 64 for N = 128 (the encoder): two taps
+// per workgroup share each staged dy row)
 template <bool TU, int TERMS = 3, bool DJ = false, bool F16 = false, int NB = 1, bool KP = false, int SD = 0,
           int KB = 1>
 __global__ void __launch_bounds__(NB == 2 || KB == 2 ? 2 * kThreads : kThreads, 2)
@@ -551,7 +553,7 @@ wgrad_x3_kernel(const WgradArgs a) {
   static_assert(SD == 0 || F16 == (SD == 2), "16-bit storage: the MFMA format is the storage format");
   constexpr int ES = SD ? 2 : 4;             // bytes per element of X / D
   static_assert(NB == 1 || NB == 2, "one or two 128-row D blocks");
-  static_assert(KB == 1 || (KB == 2 && NB == 2 && !KP), "256 x 256 tiles: full K");
+  static_assert(KB == 1 || (KB == 2 && !KP), "256-row G tiles: full K");
   constexpr int PL = TERMS == 1 ? 1 : 2;     // planes staged / read per operand
   // waves: 4 (128 x 128) or 8 (128 x 256, 256 x 256)
   constexpr int NWV = NB == 2 || KB == 2 ? 8 : 4, THR = 64 * NWV;
@@ -848,10 +850,10 @@ wgrad_x3_kernel(const WgradArgs a) {
     store_step(st0, 0);
   }
   int s = 0;
-  if constexpr (KH > 1 || KB > 1) {
+  if constexpr (KH > 1 || (KB > 1 && NB > 1)) {
     // one register staging set (prefetch distance one round = two 32-position steps,
     // as the two sets of the 32-position form): a round's loads are in flight during
-    // the previous round's 16 MFMAs
+    // the previous round's 16 MFMAs (256 x 128 tiles: two sets, 24 staged rows a thread)
     __syncthreads();
     for (; s + 1 < nsteps; s += 2) {
       load_step(st0, mbeg + (s + 1) * BMS);

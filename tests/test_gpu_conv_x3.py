@@ -259,3 +259,17 @@ def test_many_channel_small_n_stencil(shape, kernel, stride, padding, dtype, gpu
     tol = 1e-6 if dtype == torch.float32 else 6e-3
     assert e_st < tol and d < (1e-6 if dtype == torch.float32 else 8e-3)
 
+
+
+@pytest.mark.parametrize("name,tr,cin,cout,shape,stride", [LAYERS[0], LAYERS[1]])
+def test_encoder_wgrad_256x128_bit_identical(name, tr, cin, cout, shape, stride, gpu_device, monkeypatch):
+    """The encoder weight-grad's opt-in 256 x 128 tiles (SEHIP_WGRAD_K256=1: two taps per
+    workgroup share each staged dy row, round 6) sum every output over the same m-split in the
+    same order as the default 128 x 128 tiles: bit-identical weight gradients."""
+    from sehip import functional as F
+    m, x, gy, _ = _fp64_ref(name, tr, cin, cout, shape, stride)
+    old = _hip(F, m, x, gy, tr, stride, "f16x3")
+    monkeypatch.setenv("SEHIP_WGRAD_K256", "1")
+    new = _hip(F, m, x, gy, tr, stride, "f16x3")
+    for k in ("dwr", "dwi"):
+        assert torch.equal(new[k], old[k]), k
