@@ -485,21 +485,39 @@ cbn_bwd_finalize_kernel(const double* part, const float* ext, int P, double coun
 // the item's two planes. One main-stream launch fewer per CBN backward: beside the
 // side-stream weight-grads the 16-workgroup finalize launch waited 60-310 us for CU slots
 // (profiles/r4_main_stream_kernels.txt). V4: 16-B accesses (HW % 4 == 0). grid (Cc, B)
-template <int SRC, typename T, bool V4>
+// PR: the one-weight nn.PReLU (DCCRN): the slope is read from pw, the channel's writer
+// workgroup stores its PReLU-gradient sum to pw_part[c], and the last of the Cc writers
+// (a device-scope count, zeroed by the moments pass) adds them in channel order into dpw
+// (prelu_grad_finish_kernel's sum): no separate finalize / finish launches.
+template <int SRC, typename T, bool V4, bool PR = false>
 __global__ void __launch_bounds__(kThreads)
 cbn_bwd_apply_fin_kernel(const T* __restrict__ gy, const T* __restrict__ gy2, const T* __restrict__ x,
                          T* __restrict__ dx, int C, int HW, int seg_len, int act, float slope,
                          const double* part, const float* ext, int P, double count, const float* save, Ptr5 params,
-                         int affine, MPtr5 dparams, int has_dparams, int training, float* dx_amax, CcbamDx cd) {
+                         int affine, MPtr5 dparams, int has_dparams, int training, float* dx_amax, CcbamDx cd,
+                         const T* pw, T* dpw, double* pw_part, unsigned* pw_cnt) {
   static_assert(SRC == 0 || SRC == 1 || SRC == 3, "gy, gy + gy2, or gy + the CCBAM gate's input gradient");
   static_assert(SRC != 3 || sizeof(T) == 4, "the CCBAM path is fp32");
+  static_assert(!PR || SRC != 3, "no PReLU on the CCBAM path");
   __shared__ float k[kCoef];
   const int Cc = C / 2, c = blockIdx.x, b = blockIdx.y;
   const int hw0 = blockIdx.z * seg_len, hw1 = min(HW, hw0 + seg_len);   // this workgroup's segment
+  if constexpr (PR) slope = (float)pw[0];
+  const bool writer = b == 0 && blockIdx.z == 0;
   if (threadIdx.x < 64)
-    bwd_finalize_wave<false, T, false>(c, threadIdx.x, part, ext, P, count, Cc, save, params, affine, dparams,
-                                       has_dparams, training, k, dx_amax, nullptr, nullptr,
-                                       b == 0 && blockIdx.z == 0);
+    bwd_finalize_wave<false, T, PR>(c, threadIdx.x, part, ext, P, count, Cc, save, params, affine, dparams,
+                                    has_dparams, training, k, dx_amax, nullptr, pw_part, writer);
+  if constexpr (PR) {
+    if (writer && threadIdx.x == 0) {
+      __threadfence();   // pw_part[c] visible device-wide before the count moves
+      if (atomicAdd(pw_cnt, 1u) == (unsigned)(Cc - 1)) {
+        __threadfence();
+        double sacc = 0.0;
+        for (int q = 0; q < Cc; ++q) sacc += __hip_atomic_load(&pw_part[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        dpw[0] = (T)(float)sacc;
+      }
+    }
+  }
   __syncthreads();
   const float a00 = k[0], a01 = k[1], a10 = k[2], a11 = k[3];
   const float gbr = k[4], gbi = k[5], grr = k[6], gri = k[7], gii = k[8], mr = k[9], mi = k[10];
@@ -616,13 +634,14 @@ __global__ void __launch_bounds__(kThreads)
 cbn_bwd_moments_kernel(const T* __restrict__ gy, const T* __restrict__ gy2,
                        const T* __restrict__ x, int B, int C, int HW, int P,
                        const float* __restrict__ save, int act, float slope, double* part, float* ext,
-                       float* dx_amax, HeadArgs hd, const T* pw, CcbamDx cd) {
+                       float* dx_amax, HeadArgs hd, const T* pw, CcbamDx cd, unsigned* pw_cnt) {
   static_assert(!PR || SRC != 2, "no PReLU on the head path");
   static_assert((SRC != 2 && SRC != 3) || sizeof(T) == 4, "the head and CCBAM paths are fp32");
   constexpr int NS = SRC == 2 ? 6 + kHeadNS : (PR ? 7 : 6);
   if (PR) slope = (float)pw[0];
   const int Cc = C / 2, c = blockIdx.x, p = blockIdx.y;
   if (dx_amax && c == 0 && p == 0 && threadIdx.x == 0) *dx_amax = 0.f;   // the finalize blocks atomicMax into it
+  if (pw_cnt && c == 0 && p == 0 && threadIdx.x == 0) *pw_cnt = 0u;      // cbn_bwd_apply_fin_kernel<PR>'s count
   const int nseg = (HW + kSeg - 1) / kSeg;
   const float* sv = save + c * kSave;
   float gmr = 0.f, gmi = 0.f;   // max |g_r|, max |g_i| (the dx bound)
@@ -1320,29 +1339,31 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
     if (src == 2)
       hipLaunchKernelGGL((cbn_bwd_moments_kernel<2, float>), mg, mb, 0, st, (const float*)gy, (const float*)gy2,
                          (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr,
-                         CcbamDx{});
+                         CcbamDx{}, nullptr);
   }
   if constexpr (sizeof(T) == 4) {
     if (src == 3)
       hipLaunchKernelGGL((cbn_bwd_moments_kernel<3, float>), mg, mb, 0, st, (const float*)gy, (const float*)nullptr,
-                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr, cd);
+                         (const float*)x, B, C, HW, P, save, act, slope, part, ext, xa, hd, (const float*)nullptr, cd,
+                         nullptr);
   }
+  unsigned* pw_cnt = reinterpret_cast<unsigned*>(pwp + Cc);   // (within the workspace's slack)
   if (src == 1 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw, CcbamDx{});
+                       slope, part, ext, xa, hd, pw, CcbamDx{}, pw_cnt);
   else if (src == 1)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<1, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw, CcbamDx{});
+                       part, ext, xa, hd, pw, CcbamDx{}, nullptr);
   else if (src == 0 && pr)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T, true>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act,
-                       slope, part, ext, xa, hd, pw, CcbamDx{});
+                       slope, part, ext, xa, hd, pw, CcbamDx{}, pw_cnt);
   else if (src == 0)
     hipLaunchKernelGGL((cbn_bwd_moments_kernel<0, T>), mg, mb, 0, st, gy, gy2, x, B, C, HW, P, save, act, slope,
-                       part, ext, xa, hd, pw, CcbamDx{});
+                       part, ext, xa, hd, pw, CcbamDx{}, nullptr);
   SE_LAUNCH_CHECK();
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
   if (src == 3 && (pr || fc || !SE_CBN_APPLY_FIN)) return SE_E_UNSUPPORTED;
-  if (SE_CBN_APPLY_FIN && (src == 0 || src == 1 || src == 3) && !pr && !fc) {
+  if (SE_CBN_APPLY_FIN && (src == 0 || src == 1 || src == 3) && !fc) {
     const bool v4 = HW % 4 == 0;
     // few channels (CCBAM's one-channel spatial branch: Cc x B = 64 workgroups): each plane
     // split into segments of whole 2048-element strides, up to ~1024 workgroups
@@ -1350,19 +1371,24 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
     const int nseg = std::max(1, std::min(se::ceil_div(HW, kStride), 1024 / std::max(1, Cc * B)));
     const int seg_len = se::ceil_div(se::ceil_div(HW, nseg), kStride) * kStride;
     const int ns = se::ceil_div(HW, seg_len);
-#define SE_AF(S, V)                                                                                              \
-  hipLaunchKernelGGL((cbn_bwd_apply_fin_kernel<S, T, V>), dim3(Cc, B, ns), mb, 0, st, gy, gy2, x, dx, C, HW, seg_len, \
-                     act, slope, part, ext, P, (double)B * HW, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0,        \
-                     training, xa, cd)
+#define SE_AF(S, V, PRV)                                                                                              \
+  hipLaunchKernelGGL((cbn_bwd_apply_fin_kernel<S, T, V, PRV>), dim3(Cc, B, ns), mb, 0, st, gy, gy2, x, dx, C, HW,      \
+                     seg_len, act, slope, part, ext, P, (double)B * HW, save, pp, params ? 1 : 0, dp, dparams ? 1 : 0, \
+                     training, xa, cd, pw, dpw, pwp, pw_cnt)
     if constexpr (sizeof(T) == 4) {
-      if (src == 3 && v4) SE_AF(3, true);
-      else if (src == 3) SE_AF(3, false);
+      if (src == 3 && v4) SE_AF(3, true, false);
+      else if (src == 3) SE_AF(3, false, false);
     }
     if (src == 3) {
-    } else if (src == 1 && v4) SE_AF(1, true);
-    else if (src == 1) SE_AF(1, false);
-    else if (v4) SE_AF(0, true);
-    else SE_AF(0, false);
+    } else if (pr) {
+      if (src == 1 && v4) SE_AF(1, true, true);
+      else if (src == 1) SE_AF(1, false, true);
+      else if (v4) SE_AF(0, true, true);
+      else SE_AF(0, false, true);
+    } else if (src == 1 && v4) SE_AF(1, true, false);
+    else if (src == 1) SE_AF(1, false, false);
+    else if (v4) SE_AF(0, true, false);
+    else SE_AF(0, false, false);
 #undef SE_AF
     SE_LAUNCH_CHECK();
     return SE_OK;

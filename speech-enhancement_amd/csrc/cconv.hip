@@ -524,9 +524,11 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
   // are written to LDS, so no convert waits on a load in flight
   // (se::uniform_ptr widens the two words as unsigned: a low word >= 2^31 must not
   // sign-extend into the high half of the base)
-  // joined input (a.X2, torch.cat order [x, s], DCUNet's decoder join): X holds s (2 jh
-  // channels per item, grid Hi x Wi), X2 holds x on its grid H2 x W2 (the F.pad zeros outside);
-  // a chunk of kScC channels lies in one source (jh % kScC == 0, checked by the host)
+  // joined input (a.X2): X holds s (2 jh channels per item, grid Hi x Wi), X2 holds x on its
+  // grid H2 x W2 (the F.pad zeros outside, x's extra trailing column never read); torch.cat
+  // order [x, s] (DCUNet's decoder join, a.jcat) or complex_concat's [x_re, s_re, x_im, s_im]
+  // (DCCRN's / FRCRN's, round 6); a chunk of kScC channels lies in one source (jh % kScC == 0,
+  // checked by the host)
   const bool jn = a.X2 != nullptr;
   const int cpb = jn ? 2 * a.jh : a.Cg, H2W2 = a.H2 * a.W2;
   const __amdgpu_buffer_rsrc_t rx = __builtin_amdgcn_make_buffer_rsrc(
@@ -536,9 +538,14 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
   constexpr int PF = (chunk + kThreads - 1) / kThreads;
   typename StageT<SD>::T pf[PF];
   auto fetch = [&](int c0) __attribute__((always_inline)) {
-    const bool from_x = jn && c0 < cpb;                 // chunk-uniform source
-    const int cs = jn ? (from_x ? c0 : c0 - cpb) : c0;  // the chunk's first channel in its source
-    const int sh = from_x ? a.H2 : a.Hi, sw = from_x ? a.W2 : a.Wi, spl = from_x ? H2W2 : HiWi;
+    const int q = jn ? c0 / a.jh : 0;                   // the chunk's join block (chunk-uniform)
+    const bool from_x = jn && (a.jcat ? q < 2 : (q & 1) == 0);
+    // the chunk's first channel in its source
+    const int cs = !jn ? c0 : a.jcat ? (from_x ? c0 : c0 - cpb) : (q >> 1) * a.jh + (c0 - q * a.jh);
+    // x is addressed on its own grid (row pitch W2) but bounded by the joined grid: its columns
+    // past Wi are the frame complex_concat's alignment crops (x[..., :-1]), read as zeros
+    const int sh = from_x ? min(a.H2, a.Hi) : a.Hi, sw = from_x ? min(a.W2, a.Wi) : a.Wi;
+    const int spl = from_x ? H2W2 : HiWi, pitch = from_x ? a.W2 : a.Wi;
 #pragma unroll
     for (int j = 0; j < PF; ++j) {
       const int i = threadIdx.x + j * kThreads;
@@ -546,7 +553,7 @@ gather_stencil_ch_kernel(const GatherArgs a, int h0, int w0, int ntw, int ngrp, 
       const int r = rr / tw, col = rr - r * tw;
       const int hi = qh0 + h0 + r, wi = qw0 + w0 + col;
       const bool ok = (chunk % kThreads == 0 || i < chunk) && c0 + c < cg1 && (unsigned)hi < (unsigned)sh && (unsigned)wi < (unsigned)sw;
-      const int vo = ok ? ((cs + c) * spl + hi * sw + wi) * ES : (int)0x80000000;
+      const int vo = ok ? ((cs + c) * spl + hi * pitch + wi) * ES : (int)0x80000000;
       if (ok) STC_CHECK(0, vo, (long long)(jn ? cpb : a.Cg) * spl * ES);
       if constexpr (SD == 0) pf[j] = bload<0>(from_x ? rx2 : rx, vo, 0);
       else pf[j] = bload_raw16(from_x ? rx2 : rx, vo, 0);
@@ -1582,8 +1589,8 @@ static int launch_gather(const ConvGeom& g, Pass pass, const float* X, const flo
     const long long es = g.sd == SE_DTYPE_F32 ? 4 : 2;
     bool ok = ldw <= 4 && Cg > 4 && c.h.s == 1 && c.w.s == 1 && hdesc && (long long)Cg * Hi * Wi * es < (1ll << 31) &&
               wmax - wmin <= kScPitch - kStW && !env_flag_off("SEHIP_STENCIL");
-    // joined: gather side, torch.cat order, chunk-aligned sources
-    if (jn) ok = ok && join_in && !join_out && jn->cat && jn->jh % kScC == 0;
+    // joined: gather side, chunk-aligned sources (either join order)
+    if (jn) ok = ok && join_in && !join_out && jn->jh % kScC == 0;
     return ok;
   };
   if (jn) {   // the joined forms exist on the split-bf16 / bf16 tap-uniform kernels and the chunked stencil
@@ -2114,12 +2121,15 @@ int wgrad_pass(const ConvGeom& g, const float* x, const float* dy, float* dwr, f
 // [B, Ci, Hi, Wi] = complex_concat([align(x), s]) with s [B, Ci/2, Hi, Wi] and
 // x [B, Ci/2, x_h, x_w], x_h <= Hi (missing rows: F.pad zeros), x_w >= Wi
 // (extra columns: x[..., :-1]); chunks of Ci/4 channels, a multiple of 32.
-int joined_geom(const ConvGeom& g, int x_h, int x_w) {
+// jh_align: the join blocks' channel alignment the pass's kernels need (32: a GEMM tile's
+// 32-row block lies in one chunk; 8: the chunked stencil's channel chunks, the forward of a
+// <= 4-output layer such as DCCRN's last decoder convT, jh = 16)
+int joined_geom(const ConvGeom& g, int x_h, int x_w, int jh_align = 32) {
   if (!g.complex_w) return SE_E_UNSUPPORTED;
   // complex_concat (FRCRN / DCCRN): x's missing rows read 0, its extra columns are cropped;
   // torch.cat (DCUNet): x is zero-padded to the skip's grid in both dimensions
   if (x_h <= 0 || x_w <= 0 || x_h > g.Hi || (g.jcat ? x_w > g.Wi : x_w < g.Wi)) return SE_E_SHAPE;
-  if (g.Ci % 4 || (g.Ci / 4) % 32) return SE_E_UNSUPPORTED;
+  if (g.Ci % 4 || (g.Ci / 4) % jh_align) return SE_E_UNSUPPORTED;
   return SE_OK;
 }
 
@@ -2143,7 +2153,7 @@ extern "C" int se_conv2d_fwd_joined(const se_conv2d_desc* d, const float* x, int
   ConvGeom g;
   int rc = geom_of(d, g);
   if (rc) return rc;
-  if ((rc = joined_geom(g, x_h, x_w))) return rc;
+  if ((rc = joined_geom(g, x_h, x_w, g.Co <= 4 ? 8 : 32))) return rc;
   if (!x || !s || !wr || !wi || !y || !ws || (br && !bi)) return SE_E_ARG;
   JoinIO jn{};
   jn.x2 = x; jn.jh = g.Ci / 4; jn.h2 = x_h; jn.w2 = x_w; jn.cat = g.jcat;

@@ -281,3 +281,28 @@ def test_mask_layer_join_runs_on_the_chunked_stencil(gpu_device, dtype, monkeypa
     ref, got = _joined_pair(gpu_device, (2, 64, 16, 31), (2, 64, 17, 33), (7, 5), (2, 2), (3, 2), True, dtype, 2)
     for name, a, b in zip(("y", "dx", "dskip", "dwr", "dwi"), ref, got):
         assert a.shape == b.shape and torch.equal(a, b), (dtype, name, (a.float() - b.float()).abs().max().item())
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+def test_complex_concat_join_on_the_chunked_stencil(gpu_device, dtype, monkeypatch):
+    """DCCRN's last decoder layer (2 output channels over the complex_concat join,
+    _2008_00264_dccrn.py:106-117; stride (2, 1), kernel (5, 2), x one frame wider than the
+    skip): the forward gathers x and the skip straight into the chunked stencil's LDS tiles in
+    complex_concat's chunk order (round 6; torch.cat order only before), no materialised join;
+    bit-identical to complex_join + the plain conv, gradients included."""
+    from sehip import functional as F
+    calls = []
+    raw = F._join_raw
+    monkeypatch.setattr(F, "_join_raw", lambda *a, **k: calls.append(1) or raw(*a, **k))
+    torch.manual_seed(4)
+    x = torch.randn(2, 32, 9, 24, device=gpu_device).to(dtype)
+    s = torch.randn(2, 32, 9, 23, device=gpu_device).to(dtype)
+    wr = (torch.randn(32, 1, 5, 2, device=gpu_device) * 0.05).to(dtype)
+    wi = (torch.randn(32, 1, 5, 2, device=gpu_device) * 0.05).to(dtype)
+    kw = dict(out_channels=2, kernel=(5, 2), stride=(2, 1), padding=(2, 0), output_padding=(1, 0),
+              transposed=True)
+    with torch.no_grad():
+        y = F.conv2d_joined(x, s, wr, wi, **kw)
+        y_ref = F.conv2d(F.complex_join(x, s), wr, wi, **kw)
+    assert not calls, "the joined forward materialised the join"
+    assert torch.equal(y, y_ref), (y.float() - y_ref.float()).abs().max().item()
