@@ -28,7 +28,13 @@
 namespace {
 
 constexpr int kThreads = 256;
-// SE_CBN_APPLY_FIN: the backward finalize in the apply pass's prologue (cbn_bwd_apply_fin_kernel)
+// SE_CBN_APPLY_FIN: the backward finalize in the apply pass's prologue (cbn_bwd_apply_fin_kernel);
+// SE_CBN_APPLY_FIN_PR: also with the one-weight PReLU (round 6, variant builds: its prologue
+// finalize re-read per apply workgroup cost more than the two launches it saves, DCCRN bf16
+// train 1402 / 1406 vs 1410 / 1410 utt/s, profiles/ab/r6_cbn_prelu_fold_ab.log)
+#ifndef SE_CBN_APPLY_FIN_PR
+#define SE_CBN_APPLY_FIN_PR 0
+#endif
 #ifndef SE_CBN_APPLY_FIN
 #define SE_CBN_APPLY_FIN 1
 #endif
@@ -1363,7 +1369,7 @@ int cbn_bwd_impl(int src, const T* gy, const T* gy2, const HeadArgs& hd, const T
   SE_LAUNCH_CHECK();
   const dim3 fg(se::ceil_div(Cc, kFinWaves)), fb(64 * kFinWaves);
   if (src == 3 && (pr || fc || !SE_CBN_APPLY_FIN)) return SE_E_UNSUPPORTED;
-  if (SE_CBN_APPLY_FIN && (src == 0 || src == 1 || src == 3) && !fc) {
+  if (SE_CBN_APPLY_FIN && (src == 0 || src == 1 || src == 3) && !fc && (SE_CBN_APPLY_FIN_PR || !pr)) {
     const bool v4 = HW % 4 == 0;
     // few channels (CCBAM's one-channel spatial branch: Cc x B = 64 workgroups): each plane
     // split into segments of whole 2048-element strides, up to ~1024 workgroups
