@@ -405,14 +405,18 @@ gather_x3_kernel(const GatherArgs a) {
   };
   // one scheduling region per K-step: the non-MFMA stream (next tiles' loads,
   // fragment reads, LDS writes) interleaved into the MFMA gaps
+#ifndef SE_X3_SCHED
+#define SE_X3_SCHED 0   // variant builds: 1 = two DS / two VALU per MFMA, 2 = the global loads first
+#endif
   auto interleave = [&]() __attribute__((always_inline)) {
     __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);                  // first fragments
+    if constexpr (SE_X3_SCHED == 2) __builtin_amdgcn_sched_group_barrier(0x020, (AJ + 2 * PL) * KH, 0);
 #pragma unroll
     for (int i = 0; i < 2 * TERMS * RN * RM * KH; ++i) {
       __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);                // MFMA
-      __builtin_amdgcn_sched_group_barrier(0x080, 1, 0);                // DS
-      if (i < (AJ + 2 * PL) * KH) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
-      __builtin_amdgcn_sched_group_barrier(0x002, 3, 0);                // VALU
+      __builtin_amdgcn_sched_group_barrier(0x080, SE_X3_SCHED == 1 ? 2 : 1, 0);   // DS
+      if (SE_X3_SCHED != 2 && i < (AJ + 2 * PL) * KH) __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);   // global load
+      __builtin_amdgcn_sched_group_barrier(0x002, SE_X3_SCHED == 1 ? 2 : 3, 0);   // VALU
     }
   };
 
