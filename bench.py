@@ -48,7 +48,7 @@ PROFILE_STATS = os.path.join(ROOT, "profiles", "r6_bench_kernel_stats.csv")
 # the ConvSTFT / iSTFT kernels of the STFT rooflines (se_stft_fwd: the register-radix form
 # for nfft 640)
 STFT_KERNELS = (("stft_fwd", "stft_fwd_rg_kernel"), ("istft_fwd", "istft_fwd_wv_kernel"),
-                ("istft_bwd", "istft_bwd_wv_kernel"))
+                ("istft_bwd", "istft_bwd_rg_kernel"))
 
 # OpTimer tag -> (kernel instantiation as rocprof names it, launches per call, description).
 # The decoder's joined passes are one launch of one instantiation per call (the data-grad of

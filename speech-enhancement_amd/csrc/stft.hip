@@ -721,6 +721,15 @@ __device__ __forceinline__ void rdft(const float2 (&v)[kMaxRadix], float2 (&o)[k
 #ifndef SE_RG_W
 #define SE_RG_W 8
 #endif
+#ifndef SE_ISTFT_BWD_RG
+#define SE_ISTFT_BWD_RG 1   // register-radix iSTFT adjoint (istft_bwd_rg_kernel)
+#endif
+#ifndef SE_ISTFT_FWD_RG
+#define SE_ISTFT_FWD_RG 0   // register-radix FFT in the iSTFT forward (istft_fwd_wv_kernel<.., RG>)
+#endif
+#ifndef SE_IRG_W
+#define SE_IRG_W 4          // its frame pairs per block (8: 38.4 vs 37.2 us, profiles/ab/r6_istft_bwd_rg.log)
+#endif
 #ifndef SE_RG_PPW
 #define SE_RG_PPW 1
 #endif
@@ -1214,9 +1223,14 @@ __global__ void __launch_bounds__(kThreads) istft_bwd_ip_kernel(const IstftArgs 
 // block-wide; each wave transforms its pair, takes its frames' parity sums and
 // writes its two synthesis frames without a block barrier.
 // grid (ceil(out_len / (FT*hop)), B), FT = 2W - 1 - (win-1)/hop, 64 W threads
-template <int CN, int W = wv_pairs<CN>(), bool LP = false>
+// RG: the pair's FFT is the register-radix one of stft_fwd_rg_kernel (nfft = 64 R): lane l
+// takes C[l + 64 q] of its pair into registers, and the frame comes back in the row image
+// (sample n at row n % R, column n / R); pair stride R x kRgRow.
+template <int CN, int W = wv_pairs<CN>(), bool LP = false, bool RG = false>
 __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs a) {
-  constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W, half = N / 2 + 1, P = W;
+  constexpr int N = CN, TPB = kWave * W, half = N / 2 + 1, P = W;
+  constexpr int R = RG ? N / kWave : 1, NP = RG ? R * kRgRow : wv_stride<N>();
+  static_assert(!RG || R * kWave == N, "nfft = 64 R");
   __shared__ __attribute__((aligned(16))) float2 A[W * NP];
 #if SE_STFT_TWL_IFWD
   __shared__ float2 stw[N];
@@ -1271,7 +1285,22 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
   }
   __syncthreads();
   float2* Aw = A + w * NP;
-  wfft_pass<N, 0, 1>(Aw, stw, lane);
+  if constexpr (RG) {
+    float2 v[kMaxRadix], o[kMaxRadix];
+#pragma unroll
+    for (int q = 0; q < kMaxRadix; ++q) v[q] = q < R ? Aw[lane + q * kWave] : make_float2(0.f, 0.f);
+    wave_lds_sync();   // the whole pair read before the row image overwrites it
+    rdft<R>(v, o);
+    const int pl = rg_pos(lane);
+    Aw[pl] = o[0];
+#pragma unroll
+    for (int k1 = 1; k1 < R; ++k1) Aw[k1 * kRgRow + pl] = cmul(o[k1], a.tw[lane * k1]);
+    wave_lds_sync();
+    rg_row_pass<R, 0, R>(Aw, a.tw, lane);
+    rg_row_pass<R, 1, R>(Aw, a.tw, lane);
+  } else {
+    wfft_pass<N, 0, 1>(Aw, stw, lane);
+  }
   // z = conj(Aw): z_a = Aw.x, z_b = -Aw.y. Parity sums over n < win, then the
   // windowed G-corrected frames written over the wave's own buffer as [2][win] floats
   constexpr int IT = (N + kWave - 1) / kWave;
@@ -1280,7 +1309,7 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int n = lane + it * kWave;
-    z[it] = n < a.win ? Aw[n] : make_float2(0.f, 0.f);
+    z[it] = n < a.win ? Aw[RG ? (n % R) * kRgRow + rg_pos(n / R) : n] : make_float2(0.f, 0.f);
     z[it].y = -z[it].y;
     if (n & 1) { soa += z[it].x; sob += z[it].y; } else { sea += z[it].x; seb += z[it].y; }
   }
@@ -1319,29 +1348,19 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
   }
 }
 
-// Adjoint of istft_fwd, wave-local FFT: wave w gathers and normalises frames
-// t0 + 2w, +1 (contiguous gradient samples: coalesced), applies G with its own
-// parity sums, transforms its pair; one barrier before the block-wide spectrum
-// store. grid (ceil(T / 2W), B), 64 W threads
-template <int CN, int W = wv_pairs<CN>(), bool LP = false>
-__global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs a) {
-  constexpr int N = CN, NP = wv_stride<N>(), TPB = kWave * W;
-  __shared__ __attribute__((aligned(16))) float2 A[W * NP];
-#if SE_STFT_TWL_IBWD
-  __shared__ float2 stw[N];
-#else
-  const float2* stw = a.tw;
-#endif
-  __shared__ float swin[N];
-  int tb, b;
-  xcd_frame_block(tb, b);
-  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
-  const int t0 = tb * 2 * W;
+// The adjoint's frame side, shared by istft_bwd_wv_kernel and istft_bwd_rg_kernel: wave w
+// gathers frames t0 + 2w, +1 from the output gradient (contiguous samples: coalesced),
+// divides by the OLA normaliser, windows and applies G with the frames' own parity sums.
+// g[it][h] = sample n = lane + 64 it of frame h (zero for n >= win); iterations it >= QI are
+// not formed (the caller knows them zero: win <= 64 QI). Stages the window in swin (one
+// block barrier, before which the caller may stage more).
+template <int N, int QI, bool LP>
+__device__ __forceinline__ void ibwd_frames(const IstftArgs& a, float* swin, int b, int t0, int w, int lane,
+                                            float (&g)[QI][2]) {
   const long long go = (long long)b * a.out_len;
-  constexpr int IT = (N + kWave - 1) / kWave;
-  float ga[IT][2];
+  float ga[QI][2];
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
+  for (int it = 0; it < QI; ++it) {
     const int n = lane + it * kWave;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -1352,18 +1371,13 @@ __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs
       }
     }
   }
-  for (int i = threadIdx.x; i < N; i += TPB) {
-#if SE_STFT_TWL_IBWD
-    stw[i] = a.tw[i];
-#endif
-    swin[i] = i < a.win ? a.window[i] : 0.f;
-  }
+  for (int i = threadIdx.x; i < N; i += blockDim.x) swin[i] = i < a.win ? a.window[i] : 0.f;
   __syncthreads();
-  float v[IT][2];
+  float v[QI][2];
   float se2[2] = {0.f, 0.f}, so2[2] = {0.f, 0.f};
   const float rh = 1.f / (float)a.hop;
 #pragma unroll
-  for (int it = 0; it < IT; ++it) {
+  for (int it = 0; it < QI; ++it) {
     const int n = lane + it * kWave;
     // frames t + d covering sample u = t hop + n: d in [d0, d1] (n < win), the same
     // for both of the wave's frames up to the clip to [0, T - 1]
@@ -1401,20 +1415,80 @@ __global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs
   for (int h = 0; h < 2; ++h) { se2[h] = se::wave_sum(se2[h]); so2[h] = se::wave_sum(so2[h]); }
   const float ah = 0.5f * N, inv_a = 1.f / ah;
   const float ce = 1.f / (ah + (a.win + 1) / 2), co = 1.f / (ah + a.win / 2);
+#pragma unroll
+  for (int it = 0; it < QI; ++it) {
+    const int n = lane + it * kWave;
+    const bool in = n < a.win;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) g[it][h] = in ? apply_g(v[it][h], n, se2[h], so2[h], inv_a, ce, co) : 0.f;
+  }
+}
+
+// Adjoint of istft_fwd, wave-local FFT: wave w forms its frame pair (ibwd_frames) and
+// transforms it; one barrier before the block-wide spectrum store.
+// grid (ceil(T / 2W), B), 64 W threads
+template <int CN, int W = wv_pairs<CN>(), bool LP = false>
+__global__ void __launch_bounds__(kWave * W) istft_bwd_wv_kernel(const IstftArgs a) {
+  constexpr int N = CN, NP = wv_stride<N>();
+  __shared__ __attribute__((aligned(16))) float2 A[W * NP];
+#if SE_STFT_TWL_IBWD
+  __shared__ float2 stw[N];
+  for (int i = threadIdx.x; i < N; i += kWave * W) stw[i] = a.tw[i];
+#else
+  const float2* stw = a.tw;
+#endif
+  __shared__ float swin[N];
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int t0 = tb * 2 * W;
+  constexpr int IT = (N + kWave - 1) / kWave;
+  float g[IT][2];
+  ibwd_frames<N, IT, LP>(a, swin, b, t0, w, lane, g);
   float2* Aw = A + w * NP;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
     const int n = lane + it * kWave;
-    if (N % kWave == 0 || n < N) {
-      const bool in = n < a.win;
-      Aw[n] = make_float2(in ? apply_g(v[it][0], n, se2[0], so2[0], inv_a, ce, co) : 0.f,
-                          in ? apply_g(v[it][1], n, se2[1], so2[1], inv_a, ce, co) : 0.f);
-    }
+    if (N % kWave == 0 || n < N) Aw[n] = make_float2(g[it][0], g[it][1]);
   }
   wave_lds_sync();
   wfft_pass<N, 0, 1>(Aw, stw, lane);
   __syncthreads();
   wv_unpack_store<N, W, LP>(A, t0, a.T, b, a.out, nullptr, 0, a.dt);
+}
+
+// Adjoint of istft_fwd with the register-radix FFT of stft_fwd_rg_kernel (nfft = 64 R):
+// ibwd_frames leaves lane l samples l + 64 q of its wave's two frames in registers, which is
+// the register-radix input layout, so the R-point DFT runs straight on them (no LDS image
+// before the first stage, and with HALF (win <= N / 2) the upper R / 2 inputs are compile-time
+// zeros); then the two 64-point row passes and the shared unpack store.
+// grid (ceil(T / 2W), B), 64 W threads
+template <int N, bool HALF, int W, bool LP>
+__global__ void __launch_bounds__(kWave * W) istft_bwd_rg_kernel(const IstftArgs a) {
+  constexpr int R = N / kWave, QN = HALF ? R / 2 : R;
+  static_assert(R * kWave == N, "nfft = 64 R");
+  __shared__ __attribute__((aligned(16))) float2 A[W * R * kRgRow];
+  __shared__ float swin[N];
+  int tb, b;
+  xcd_frame_block(tb, b);
+  const int lane = threadIdx.x & (kWave - 1), w = threadIdx.x / kWave;
+  const int t0 = tb * 2 * W;
+  float g[QN][2];
+  ibwd_frames<N, QN, LP>(a, swin, b, t0, w, lane, g);
+  float2 v[kMaxRadix], o[kMaxRadix];
+#pragma unroll
+  for (int q = 0; q < kMaxRadix; ++q) v[q] = q < QN ? make_float2(g[q][0], g[q][1]) : make_float2(0.f, 0.f);
+  rdft<R>(v, o);
+  float2* Aw = A + w * R * kRgRow;
+  const int pl = rg_pos(lane);
+  Aw[pl] = o[0];
+#pragma unroll
+  for (int k1 = 1; k1 < R; ++k1) Aw[k1 * kRgRow + pl] = cmul(o[k1], a.tw[lane * k1]);
+  wave_lds_sync();
+  rg_row_pass<R, 0, R>(Aw, a.tw, lane);
+  rg_row_pass<R, 1, R>(Aw, a.tw, lane);
+  __syncthreads();   // every pair of the block transformed
+  rg_unpack_store<N, R, W, kWave * W, LP>(A, t0, a.T, b, a.out, nullptr, 0, a.dt);
 }
 
 // ---------------------------------------------------------------------------
@@ -1595,17 +1669,17 @@ extern "C" int se_istft_fwd(const void* spec, void* out, int B, int T, int win, 
     if (a.FT >= 1) {
       const dim3 grid(se::ceil_div(out_len, a.FT * hop), B), blk(se::kWave * W);
       hipStream_t st = se::as_stream(stream);
-#define SE_ISTFT_WVL(NF)                                                                                \
+#define SE_ISTFT_WVL(NF, G)                                                                             \
       do {                                                                                              \
-        if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, wv_pairs<NF>(), true>), grid, blk, 0, st, a); \
-        else hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, wv_pairs<NF>(), false>), grid, blk, 0, st, a);  \
+        if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, wv_pairs<NF>(), true, G>), grid, blk, 0, st, a); \
+        else hipLaunchKernelGGL((istft_fwd_wv_kernel<NF, wv_pairs<NF>(), false, G>), grid, blk, 0, st, a); \
       } while (0)
       switch (nfft) {
-        case 640: SE_ISTFT_WVL(640); break;
-        case 512: SE_ISTFT_WVL(512); break;
-        case 400: SE_ISTFT_WVL(400); break;
-        case 320: SE_ISTFT_WVL(320); break;
-        default: SE_ISTFT_WVL(256); break;
+        case 640: SE_ISTFT_WVL(640, SE_ISTFT_FWD_RG); break;
+        case 512: SE_ISTFT_WVL(512, SE_ISTFT_FWD_RG); break;
+        case 400: SE_ISTFT_WVL(400, false); break;
+        case 320: SE_ISTFT_WVL(320, SE_ISTFT_FWD_RG); break;
+        default: SE_ISTFT_WVL(256, false); break;
       }
 #undef SE_ISTFT_WVL
       SE_LAUNCH_CHECK();
@@ -1650,6 +1724,24 @@ extern "C" int se_istft_bwd(const void* gout, void* gspec, int B, int T, int win
   if (rc) return rc;
   if (!gout || !gspec || !window || !twiddle || !dtype_ok(dtype)) return SE_E_ARG;
   a.in = gout; a.out = gspec; a.window = window; a.tw = (const float2*)twiddle; a.dt = dtype;
+  if (SE_ISTFT_BWD_RG && (nfft == 640 || nfft == 512 || nfft == 320)) {
+    // register-radix FFT, SE_IRG_W frame pairs per block
+    hipStream_t st = se::as_stream(stream);
+    constexpr int W = SE_IRG_W;
+    const dim3 grid(se::ceil_div(T, 2 * W), B), blk(se::kWave * W);
+    const bool hf = 2 * win <= nfft;
+#define SE_ISTFT_RGL(NF, H)                                                                             \
+    do {                                                                                                \
+      if (a.dt != SE_DTYPE_F32) hipLaunchKernelGGL((istft_bwd_rg_kernel<NF, H, W, true>), grid, blk, 0, st, a); \
+      else hipLaunchKernelGGL((istft_bwd_rg_kernel<NF, H, W, false>), grid, blk, 0, st, a);             \
+    } while (0)
+    if (nfft == 640) { if (hf) SE_ISTFT_RGL(640, true); else SE_ISTFT_RGL(640, false); }
+    else if (nfft == 512) { if (hf) SE_ISTFT_RGL(512, true); else SE_ISTFT_RGL(512, false); }
+    else SE_ISTFT_RGL(320, false);
+#undef SE_ISTFT_RGL
+    SE_LAUNCH_CHECK();
+    return SE_OK;
+  }
   if (SE_STFT_WV && ip_plan(nfft)) {
     // wave-local FFT, wv_pairs<nfft>() frame pairs per block
     hipStream_t st = se::as_stream(stream);

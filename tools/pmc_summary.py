@@ -62,7 +62,7 @@ def main():
                   "write_bytes_per_launch": wb, "hbm_bytes_per_launch": fb + wb}
     json.dump(res, open(out, "w"), indent=1, sort_keys=True)
     for k in ("gather_x3_kernel<true, 3, 2, 2, true, 0>", "wgrad_x3_kernel<true, 3, true, true, 2, false, 0, 2>",
-              "stft_fwd_wv_kernel", "istft_fwd_wv_kernel", "istft_bwd_wv_kernel", "cbn_apply_kernel"):
+              "stft_fwd_rg_kernel", "istft_fwd_wv_kernel", "istft_bwd_rg_kernel", "cbn_apply_kernel"):
         if k in res:
             print(k, {a: f"{b:.4g}" for a, b in res[k].items()})
 
