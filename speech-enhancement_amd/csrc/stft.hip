@@ -1308,8 +1308,9 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
   float sea = 0.f, soa = 0.f, seb = 0.f, sob = 0.f;
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int n = lane + it * kWave;
-    z[it] = n < a.win ? Aw[RG ? (n % R) * kRgRow + rg_pos(n / R) : n] : make_float2(0.f, 0.f);
+    // RG: lane l takes samples n = R l + it (row it, column l of the image: conflict-free)
+    const int n = RG ? lane * R + it : lane + it * kWave;
+    z[it] = n < a.win ? Aw[RG ? it * kRgRow + rg_pos(lane) : n] : make_float2(0.f, 0.f);
     z[it].y = -z[it].y;
     if (n & 1) { soa += z[it].x; sob += z[it].y; } else { sea += z[it].x; seb += z[it].y; }
   }
@@ -1321,7 +1322,7 @@ __global__ void __launch_bounds__(kWave * W) istft_fwd_wv_kernel(const IstftArgs
   float* fw = reinterpret_cast<float*>(Aw);
 #pragma unroll
   for (int it = 0; it < IT; ++it) {
-    const int n = lane + it * kWave;
+    const int n = RG ? lane * R + it : lane + it * kWave;
     if (n < a.win) {
       const float wn = a.window[n];
       fw[n] = wn * apply_g(z[it].x, n, sea, soa, inv_a, ce, co);
